@@ -1,0 +1,152 @@
+"""ctypes binding of libdreamer_hip.so (include/dreamer_hip.h).
+
+The product path has no CPU fallback: if the library is missing or fails to
+load, every hot-path call raises.  Build with ``python -m dreamer_amd.build``.
+"""
+import ctypes as C
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdreamer_hip.so")
+
+fp = C.c_void_p  # device pointers
+
+
+class dr_linear(C.Structure):
+    _fields_ = [("w", fp), ("b", fp)]
+
+
+class dr_mlp3(C.Structure):
+    _fields_ = [("l0", dr_linear), ("n1", dr_linear), ("l3", dr_linear), ("n4", dr_linear), ("l6", dr_linear)]
+
+
+class dr_dims(C.Structure):
+    _fields_ = [(n, C.c_int) for n in (
+        "hidden", "rows", "cols", "action", "img_h", "img_w", "enc_f1", "enc_f2", "enc_hidden",
+        "prior_h1", "prior_h2", "rew_h1", "rew_h2", "cont_h1", "cont_h2",
+        "actor_h1", "actor_h2", "critic_h1", "critic_h2", "buckets")]
+
+
+class dr_world_model(C.Structure):
+    _fields_ = [("conv", dr_linear * 4), ("map0", dr_linear), ("map1", dr_linear), ("map3", dr_linear),
+                ("w_ih", fp), ("w_hh", fp), ("b_ih", fp), ("b_hh", fp),
+                ("prior", dr_mlp3), ("reward", dr_mlp3), ("cont", dr_mlp3), ("buckets_rew", fp)]
+
+
+class dr_actor(C.Structure):
+    _fields_ = [("l0", dr_linear), ("n1", dr_linear), ("l3", dr_linear), ("n4", dr_linear),
+                ("mu", dr_linear), ("ls", dr_linear)]
+
+
+class dr_critic(C.Structure):
+    _fields_ = [("net", dr_mlp3), ("buckets", fp)]
+
+
+class dr_noise(C.Structure):
+    _fields_ = [("q", fp), ("eps", fp), ("rng", fp), ("row0", C.c_int), ("stream", C.c_int)]
+
+
+class dr_frames(C.Structure):
+    _fields_ = [("ring", fp), ("ring_cap", C.c_longlong), ("starts", fp), ("obs", fp),
+                ("stride_b", C.c_longlong), ("stride_t", C.c_longlong), ("raw255", C.c_int)]
+
+
+_P = C.POINTER
+_sz = C.c_size_t
+_i = C.c_int
+_ll = C.c_longlong
+_f = C.c_float
+
+_SIGS = {
+    "dr_last_error": (C.c_char_p, []),
+    "dr_version": (_i, []),
+    "dr_encoder_workspace_bytes": (_sz, [_P(dr_dims), _i]),
+    "dr_encoder_features": (_i, [_P(dr_dims), _P(dr_world_model), _P(dr_frames), _i, _i, fp, fp, _sz, fp]),
+    "dr_observe_workspace_bytes": (_sz, [_P(dr_dims), _i]),
+    "dr_observe_scan": (_i, [_P(dr_dims), _P(dr_world_model), _i, _i, fp, fp, _ll, _ll, fp, fp, dr_noise,
+                             fp, fp, fp, fp, _sz, fp]),
+    "dr_imagine_tape_bytes": (_sz, [_P(dr_dims), _i, _i]),
+    "dr_imagine_workspace_bytes": (_sz, [_P(dr_dims), _i, _i]),
+    "dr_imagine_fwd": (_i, [_P(dr_dims), _P(dr_world_model), _P(dr_actor), _i, _i, fp, fp, dr_noise, _i,
+                            fp, fp, fp, fp, fp, fp, fp, fp, fp, _sz, fp]),
+    "dr_imagine_bwd": (_i, [_P(dr_dims), _P(dr_world_model), _P(dr_actor), _i, _i, fp, fp, fp, fp, fp,
+                            fp, fp, fp, fp, _P(dr_actor), fp, _sz, fp]),
+    "dr_step_workspace_bytes": (_sz, [_P(dr_dims), _i]),
+    "dr_imagine_step": (_i, [_P(dr_dims), _P(dr_world_model), _i, fp, fp, fp, dr_noise, fp, fp, fp, fp,
+                             fp, _sz, fp]),
+    "dr_actor_act": (_i, [_P(dr_dims), _P(dr_actor), _i, fp, fp, dr_noise, _i, fp, fp, fp, fp, _sz, fp]),
+    "dr_gru_cell": (_i, [_P(dr_dims), _P(dr_world_model), _i, fp, fp, fp, fp, fp, _sz, fp]),
+    "dr_categorical_sample": (_i, [_i, _i, _i, fp, dr_noise, fp, fp, fp, fp]),
+    "dr_mlp3_fwd": (_i, [_P(dr_mlp3), _i, _i, fp, _ll, _i, fp, _ll, _i, _i, _i, fp, _ll, fp, _sz, fp]),
+    "dr_bucket_value": (_i, [_i, _i, fp, fp, fp, fp]),
+    "dr_critic_tape_bytes": (_sz, [_P(dr_dims), _i]),
+    "dr_critic_workspace_bytes": (_sz, [_P(dr_dims), _i, _i]),
+    "dr_critic_fwd": (_i, [_P(dr_dims), _P(dr_critic), _i, fp, _ll, fp, _ll, fp, fp, fp, fp, _sz, fp]),
+    "dr_lambda_returns": (_i, [_i, _i, fp, fp, fp, _f, _f, fp, fp]),
+    "dr_update_S": (_i, [_i, fp, fp, fp, fp, _sz, fp]),
+    "dr_actor_loss_grad": (_i, [_i, _i, _i, fp, fp, fp, fp, fp, fp, _f, _f, fp, fp, fp, fp]),
+    "dr_critic_loss_bwd": (_i, [_P(dr_dims), _P(dr_critic), _i, _i, fp, fp, fp, fp, _f, fp, _P(dr_critic),
+                                fp, _sz, fp]),
+    "dr_sqnorm": (_i, [_ll, fp, fp, fp]),
+    "dr_adamw": (_i, [_ll, fp, fp, fp, fp, fp, _f, _f, _f, _f, _f, _f, fp, fp, fp, fp]),
+    "dr_ema": (_i, [_ll, fp, fp, _f, _f, fp, fp]),
+    "dr_nonfinite": (_i, [_ll, fp, fp, fp]),
+    "dr_replay_gather": (_i, [_ll, _i, _i, _i, _i, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp]),
+    "dr_rng_advance": (_i, [fp, C.c_ulonglong, fp]),
+}
+
+EXPORTED = sorted(_SIGS)
+
+_lib = None
+_load_error = None
+
+
+def load():
+    """Load the HIP library (no GPU needed to load it)."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        _load_error = f"{LIB_PATH} not built (run: python -m dreamer_amd.build)"
+        raise RuntimeError("dreamer_amd: HIP library missing: " + _load_error)
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Call an int-returning entry point; raise on a non-zero code."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.dr_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+
+
+def query(name, *args):
+    return getattr(load(), name)(*args)
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("dreamer_amd: tensors must live on the GPU (this framework is MI355X-only)")
+    return t.data_ptr()
+
+
+def stream_ptr(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_gpu(t):
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        raise RuntimeError("dreamer_amd: hot-path ops run only on the GPU (MI355X); "
+                           "move the model and tensors to 'cuda'")

@@ -1,0 +1,747 @@
+// Composite entry points of libdreamer_hip: encoder, posterior scan (warm
+// start), imagination unroll forward/backward, critic forward/backward.
+// Each is a fixed sequence of kernel launches on one stream (no host sync,
+// no allocation) so a whole train_Agent epoch can be captured in a hipGraph.
+#include <string.h>
+
+#include "gemm.h"
+#include "ops.h"
+
+int op_critic_ce(int B, int H, int nb, const float* logits, const float* R, const float* buckets, float scale,
+                 float* row_loss, float* g_logits, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// workspace carving (the same sequence runs in "dry" mode for size queries)
+// ---------------------------------------------------------------------------
+struct Carve {
+  char* base;
+  size_t off;
+  explicit Carve(void* b) : base((char*)b), off(0) {}
+  float* f(long long n) { return (float*)raw(n * sizeof(float)); }
+  int* i(long long n) { return (int*)raw(n * sizeof(int)); }
+  void* raw(size_t bytes) {
+    const size_t o = (off + 255) & ~(size_t)255;
+    off = o + bytes;
+    return base ? (void*)(base + o) : nullptr;
+  }
+};
+
+#define WS_CHECK(c, bytes)                                                                 \
+  do {                                                                                     \
+    if ((c).off > (bytes)) {                                                               \
+      dr_set_error("%s: workspace too small (%zu < %zu)", __func__, (size_t)(bytes), (c).off); \
+      return DR_E_WORKSPACE;                                                               \
+    }                                                                                      \
+  } while (0)
+
+static int copy2d(float* dst, long long dpitch, const float* src, long long spitch, long long width, long long rows,
+                  hipStream_t s) {
+  if (rows == 0 || width == 0) return DR_OK;
+  hipError_t e = hipMemcpy2DAsync(dst, dpitch * sizeof(float), src, spitch * sizeof(float), width * sizeof(float),
+                                  rows, hipMemcpyDeviceToDevice, s);
+  if (e != hipSuccess) {
+    dr_set_error("copy2d: %s", hipGetErrorString(e));
+    return DR_E_HIP;
+  }
+  return DR_OK;
+}
+
+static int zero(float* p, long long n, hipStream_t s) {
+  if (n == 0) return DR_OK;
+  hipError_t e = hipMemsetAsync(p, 0, n * sizeof(float), s);
+  if (e != hipSuccess) {
+    dr_set_error("memset: %s", hipGetErrorString(e));
+    return DR_E_HIP;
+  }
+  return DR_OK;
+}
+
+static int latent(const dr_dims* d) { return d->rows * d->cols; }
+
+// Y[M][N] = A[M][K] W^T + b  (torch Linear), A row stride lda
+static GemmArgs lin(int M, int N, int K, const float* A, long long lda, const float* W, long long ldw,
+                    const float* bias, float* Y, long long ldy) {
+  GemmArgs g = gemm_args();
+  g.M = M; g.N = N; g.K = K;
+  g.A = A; g.lda = lda;
+  g.W = W; g.ldb = ldw;
+  g.bias = bias;
+  g.Y = Y; g.ldy = ldy;
+  return g;
+}
+// Linear over the concatenation [A (Ka cols) | A2 (K2 cols)]
+static GemmArgs lin2(int M, int N, const float* A, long long lda, int Ka, const float* A2, long long lda2, int K2,
+                     const float* W, const float* bias, float* Y, long long ldy) {
+  GemmArgs g = lin(M, N, Ka + K2, A, lda, W, Ka + K2, bias, Y, ldy);
+  g.A2 = A2; g.lda2 = lda2; g.ksplitA = Ka;
+  return g;
+}
+// Linear applied to SiLU(LayerNorm(pre)) (the LN+SiLU of the previous layer fused on load)
+static GemmArgs lin_ln(int M, int N, int K, const float* pre, long long ldp, const dr_linear& ln, const float* W,
+                       const float* bias, float* Y, long long ldy) {
+  GemmArgs g = lin(M, N, K, pre, ldp, W, K, bias, Y, ldy);
+  g.ln_g = ln.w; g.ln_b = ln.b;
+  return g;
+}
+// input gradient: Y[M][N] (+)= G[M][K] W[K][N]  (W = torch weight [out=K][in=N])
+static GemmArgs bwd_in(int M, int N, int K, const float* G, long long ldg, const float* W, long long ldw, float* Y,
+                       long long ldy, int accumulate) {
+  GemmArgs g = gemm_args();
+  g.M = M; g.N = N; g.K = K;
+  g.A = G; g.lda = ldg;
+  g.W = W; g.ldb = ldw;
+  g.Y = Y; g.ldy = ldy;
+  g.accumulate = accumulate;
+  return g;
+}
+// weight gradient: dW[M=out][N=in] = sum_r G[r][m] X[r][n]  (rows r < R)
+static GemmArgs bwd_w(int out, int in, int R, const float* G, long long ldg, const float* X, long long ldx, float* dW) {
+  GemmArgs g = gemm_args();
+  g.M = out; g.N = in; g.K = R;
+  g.A = G; g.lda = ldg;
+  g.W = X; g.ldb = ldx;
+  g.Y = dW; g.ldy = in;
+  return g;
+}
+
+static int run(GemmLayout lay, int amode, const GemmArgs& a, hipStream_t s) { return gemm_launch(lay, amode, &a, 1, s); }
+
+// ===========================================================================
+// a3  encoder features
+// ===========================================================================
+struct EncWs {
+  float *a1, *a2, *a3, *a4, *wr2, *wr3, *wr4;
+};
+
+static void enc_carve(Carve& c, const dr_dims* d, int n, EncWs& w) {
+  const int c1 = d->enc_f1, c2 = d->enc_f2, c3 = 2 * d->enc_f2, c4 = 4 * d->enc_f2;
+  const long long p1 = (long long)(d->img_h / 2) * (d->img_w / 2), p2 = p1 / 4, p3 = p2 / 4, p4 = p3 / 4;
+  w.a1 = c.f((long long)n * p1 * c1);
+  w.a2 = c.f((long long)n * p2 * c2);
+  w.a3 = c.f((long long)n * p3 * c3);
+  w.a4 = c.f((long long)n * p4 * c4);
+  w.wr2 = c.f((long long)c2 * c1 * 16);
+  w.wr3 = c.f((long long)c3 * c2 * 16);
+  w.wr4 = c.f((long long)c4 * c3 * 16);
+}
+
+extern "C" size_t dr_encoder_workspace_bytes(const dr_dims* d, int n_frames) {
+  Carve c(nullptr);
+  EncWs w;
+  enc_carve(c, d, n_frames, w);
+  return c.off;
+}
+
+static GemmArgs conv_args(int n, int cin, int ih, int iw, int cout, const float* act_in, const float* w,
+                          const float* b, float* out) {
+  GemmArgs g = gemm_args();
+  g.cin = cin; g.ih = ih; g.iw = iw; g.oh = ih / 2; g.ow = iw / 2;
+  g.M = n * g.oh * g.ow; g.N = cout; g.K = cin * 16;
+  g.A = act_in;
+  g.W = w; g.ldb = cin * 16;
+  g.bias = b;
+  g.Y = out; g.ldy = cout;
+  g.act = 1;
+  return g;
+}
+
+extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, const dr_frames* src, int B, int T,
+                                   float* feat, void* ws, size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(d && wm && src && feat && B > 0 && T > 0, "null argument or empty batch");
+  DR_REQUIRE(d->img_h % 16 == 0 && d->img_w % 16 == 0, "image size must be a multiple of 16");
+  const int n = B * T;
+  Carve c(ws);
+  EncWs w;
+  enc_carve(c, d, n, w);
+  WS_CHECK(c, ws_bytes);
+  const int c1 = d->enc_f1, c2 = d->enc_f2, c3 = 2 * d->enc_f2, c4 = 4 * d->enc_f2;
+  const int h0 = d->img_h, w0 = d->img_w;
+  DR_TRY(op_conv_repack(c2, c1, wm->conv[1].w, w.wr2, s));
+  DR_TRY(op_conv_repack(c3, c2, wm->conv[2].w, w.wr3, s));
+  DR_TRY(op_conv_repack(c4, c3, wm->conv[3].w, w.wr4, s));
+  // conv1 straight from the frames (u8 ring or f32), NCHW source, torch K order
+  GemmArgs g1 = conv_args(n, 3, h0, w0, c1, nullptr, wm->conv[0].w, wm->conv[0].b, w.a1);
+  g1.src = *src;
+  g1.nb = B;
+  DR_TRY(run(G_NT, AM_CONV_SRC, g1, s));
+  DR_TRY(run(G_NT, AM_CONV, conv_args(n, c1, h0 / 2, w0 / 2, c2, w.a1, w.wr2, wm->conv[1].b, w.a2), s));
+  DR_TRY(run(G_NT, AM_CONV, conv_args(n, c2, h0 / 4, w0 / 4, c3, w.a2, w.wr3, wm->conv[2].b, w.a3), s));
+  GemmArgs g4 = conv_args(n, c3, h0 / 8, w0 / 8, c4, w.a3, w.wr4, wm->conv[3].b, w.a4);
+  g4.out_conv = 1;  // NCHW == nn.Flatten order of Encoder.forward (VAE.py:72)
+  DR_TRY(run(G_NT, AM_CONV, g4, s));
+  const int F = c4 * (h0 / 16) * (w0 / 16);
+  return run(G_NT, AM_PLAIN, lin(n, d->enc_hidden, F, w.a4, F, wm->map0.w, F + d->hidden, wm->map0.b, feat, d->enc_hidden), s);
+}
+
+// ===========================================================================
+// a2/a5  posterior scan
+// ===========================================================================
+struct ObsWs {
+  float *gi, *gh, *pre1, *logits;
+};
+static void obs_carve(Carve& c, const dr_dims* d, int B, ObsWs& w) {
+  w.gi = c.f((long long)B * 3 * d->hidden);
+  w.gh = c.f((long long)B * 3 * d->hidden);
+  w.pre1 = c.f((long long)B * d->enc_hidden);
+  w.logits = c.f((long long)B * latent(d));
+}
+
+extern "C" size_t dr_observe_workspace_bytes(const dr_dims* d, int B) {
+  Carve c(nullptr);
+  ObsWs w;
+  obs_carve(c, d, B, w);
+  return c.off;
+}
+
+// h' = GRU(z, a, h) with gi/gh from one grouped GEMM launch
+static int gru_step(const dr_dims* d, const dr_world_model* wm, int B, const float* z, long long ldz,
+                    const float* a, long long lda, const float* h, long long ldh, float* hout, long long ldo,
+                    float* gi, float* gh, float* sr, float* su, float* sn, float* sghn, hipStream_t s) {
+  const int L = latent(d), Hd = d->hidden, A = d->action;
+  GemmArgs p[2];
+  p[0] = lin2(B, 3 * Hd, z, ldz, L, a, lda, A, wm->w_ih, wm->b_ih, gi, 3 * Hd);
+  p[1] = lin(B, 3 * Hd, h ? Hd : 0, h, ldh, wm->w_hh, Hd, wm->b_hh, gh, 3 * Hd);
+  DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, 2, s));
+  return op_gru_fwd(B, Hd, gi, gh, h, ldh, hout, ldo, sr, su, sn, sghn, s);
+}
+
+extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B, int T, const float* feat,
+                               const float* actions, long long act_sb, long long act_st, const float* h_init,
+                               const float* z_init, dr_noise noise, float* z_out, float* h_out, float* logits_out,
+                               void* ws, size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(d && wm && feat && z_out && h_out && B > 0 && T > 0, "null argument or empty batch");
+  DR_REQUIRE(T == 1 || (z_init == nullptr ? T > 1 : true), "bad T");
+  DR_REQUIRE(actions || (z_init == nullptr && T == 1), "actions required");
+  Carve c(ws);
+  ObsWs w;
+  obs_carve(c, d, B, w);
+  WS_CHECK(c, ws_bytes);
+  const int L = latent(d), Hd = d->hidden, eh = d->enc_hidden;
+  const int F = 4 * d->enc_f2 * (d->img_h / 16) * (d->img_w / 16);
+  bool h_valid = h_init != nullptr;
+  if (h_init && h_init != h_out) DR_TRY(copy2d(h_out, Hd, h_init, Hd, Hd, B, s));
+  if (!h_init) DR_TRY(zero(h_out, (long long)B * Hd, s));
+  if (z_init && z_init != z_out) DR_TRY(copy2d(z_out, L, z_init, L, L, B, s));
+  for (int t = 0; t < T; ++t) {
+    const bool do_gru = (z_init != nullptr) || t > 0;
+    if (do_gru) {
+      const int ai = t - (z_init == nullptr ? 1 : 0);
+      DR_TRY(gru_step(d, wm, B, z_out, L, actions + ai * act_st, act_sb, h_valid ? h_out : nullptr, Hd, h_out, Hd,
+                      w.gi, w.gh, nullptr, nullptr, nullptr, nullptr, s));
+      h_valid = true;
+    }
+    // latent_mapper.0 on cat(features, h): feature part precomputed in feat[t]
+    GemmArgs g = lin(B, eh, h_valid ? Hd : 0, h_out, Hd, wm->map0.w + F, F + Hd, nullptr, w.pre1, eh);
+    g.addend = feat + (long long)t * B * eh;
+    g.ld_add = eh;
+    DR_TRY(run(G_NT, AM_PLAIN, g, s));
+    float* lg = (t == T - 1 && logits_out) ? logits_out : w.logits;
+    DR_TRY(run(G_NT, AM_LNSILU, lin_ln(B, L, eh, w.pre1, eh, wm->map1, wm->map3.w, wm->map3.b, lg, L), s));
+    DR_TRY(op_sample(B, d->rows, d->cols, lg, L, &noise, t, z_out, L, nullptr, nullptr, 0, s));
+  }
+  return DR_OK;
+}
+
+// ===========================================================================
+// a7  imagination unroll
+// ===========================================================================
+struct Tape {
+  float *eps, *ls_raw;                // [H][B][A], [B][H][A]
+  float *pre1a, *x1a, *pre2a, *x2a;   // [B][H][ah*]
+  float *r, *u, *n, *ghn;             // [H][B][hidden]
+  float *pre1p, *pre2p, *soft;        // [H][B][*]
+};
+static void tape_carve(Carve& c, const dr_dims* d, int B, int H, Tape& t) {
+  const long long BH = (long long)B * H;
+  t.eps = c.f(BH * d->action);
+  t.ls_raw = c.f(BH * d->action);
+  t.pre1a = c.f(BH * d->actor_h1);
+  t.x1a = c.f(BH * d->actor_h1);
+  t.pre2a = c.f(BH * d->actor_h2);
+  t.x2a = c.f(BH * d->actor_h2);
+  t.r = c.f(BH * d->hidden);
+  t.u = c.f(BH * d->hidden);
+  t.n = c.f(BH * d->hidden);
+  t.ghn = c.f(BH * d->hidden);
+  t.pre1p = c.f(BH * d->prior_h1);
+  t.pre2p = c.f(BH * d->prior_h2);
+  t.soft = c.f(BH * latent(d));
+}
+
+extern "C" size_t dr_imagine_tape_bytes(const dr_dims* d, int B, int H) {
+  Carve c(nullptr);
+  Tape t;
+  tape_carve(c, d, B, H, t);
+  return c.off;
+}
+
+struct ImWs {
+  float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog;  // forward scratch
+  // backward
+  float *gH, *gZ, *gA, *glog, *gx2, *gp2, *gx1, *gp1, *ggi, *ggh, *gheads, *gx2a, *gpre2a, *gy2a, *xh2a, *gx1a,
+      *gpre1a, *gy1a, *xh1a, *hcat, *zcat;
+};
+static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
+  const long long Bl = B, BH = (long long)B * H, B1 = (long long)B * (H + 1);
+  const int L = latent(d), Hd = d->hidden, A = d->action;
+  w.gi = c.f(Bl * 3 * Hd);
+  w.gh = c.f(Bl * 3 * Hd);
+  w.plog = c.f(Bl * L);
+  w.p1r = c.f(Bl * d->rew_h1);
+  w.p1c = c.f(Bl * d->cont_h1);
+  w.p2r = c.f(Bl * d->rew_h2);
+  w.p2c = c.f(Bl * d->cont_h2);
+  w.rlog = c.f(Bl * d->buckets);
+  w.clog = c.f(Bl);
+  w.gH = c.f(B1 * Hd);
+  w.gZ = c.f(B1 * L);
+  w.gA = c.f(BH * A);
+  w.glog = c.f(Bl * L);
+  w.gx2 = c.f(Bl * d->prior_h2);
+  w.gp2 = c.f(Bl * d->prior_h2);
+  w.gx1 = c.f(Bl * d->prior_h1);
+  w.gp1 = c.f(Bl * d->prior_h1);
+  w.ggi = c.f(Bl * 3 * Hd);
+  w.ggh = c.f(Bl * 3 * Hd);
+  w.gheads = c.f(BH * 2 * A);
+  w.gx2a = c.f(Bl * d->actor_h2);
+  w.gpre2a = c.f(BH * d->actor_h2);
+  w.gy2a = c.f(BH * d->actor_h2);
+  w.xh2a = c.f(BH * d->actor_h2);
+  w.gx1a = c.f(Bl * d->actor_h1);
+  w.gpre1a = c.f(BH * d->actor_h1);
+  w.gy1a = c.f(BH * d->actor_h1);
+  w.xh1a = c.f(BH * d->actor_h1);
+  w.hcat = c.f(BH * Hd);
+  w.zcat = c.f(BH * L);
+}
+
+extern "C" size_t dr_imagine_workspace_bytes(const dr_dims* d, int B, int H) {
+  Carve c(nullptr);
+  ImWs w;
+  imws_carve(c, d, B, H, w);
+  return c.off;
+}
+
+extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, int B, int H,
+                              const float* z0, const float* h0, dr_noise noise, int deterministic, float* latents,
+                              float* hiddens, float* actions, float* rewards, float* continues, float* mus,
+                              float* sigmas, void* tape, void* ws, size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(d && wm && ac && z0 && h0 && latents && hiddens && actions && rewards && continues && mus && sigmas &&
+                 tape && B > 0 && H > 0,
+             "null argument or empty batch");
+  Carve c(ws);
+  ImWs w;
+  imws_carve(c, d, B, H, w);
+  WS_CHECK(c, ws_bytes);
+  Carve ct(tape);
+  Tape tp;
+  tape_carve(ct, d, B, H, tp);
+  const int L = latent(d), Hd = d->hidden, A = d->action, a1 = d->actor_h1, a2 = d->actor_h2;
+  const long long ldH = (long long)(H + 1) * Hd, ldL = (long long)(H + 1) * L, ldA = (long long)H * A;
+  const long long lda1 = (long long)H * a1, lda2 = (long long)H * a2;
+  DR_TRY(copy2d(latents, ldL, z0, L, L, B, s));
+  DR_TRY(copy2d(hiddens, ldH, h0, Hd, Hd, B, s));
+  dr_noise nq = noise;  // Categorical draws: a Philox stream apart from the actor's
+  nq.stream += 65536;
+
+  // actor at step 0 (Agent.py:191-210)
+  DR_TRY(run(G_NT, AM_PLAIN, lin2(B, a1, hiddens, ldH, Hd, latents, ldL, L, ac->l0.w, ac->l0.b, tp.pre1a, lda1), s));
+  {
+    GemmArgs g = lin_ln(B, a2, a1, tp.pre1a, lda1, ac->n1, ac->l3.w, ac->l3.b, tp.pre2a, lda2);
+    g.a_out = tp.x1a; g.ld_aout = lda1;
+    DR_TRY(run(G_NT, AM_LNSILU, g, s));
+    GemmArgs p[2];
+    p[0] = lin_ln(B, A, a2, tp.pre2a, lda2, ac->n4, ac->mu.w, ac->mu.b, mus, ldA);
+    p[0].a_out = tp.x2a; p[0].ld_aout = lda2;
+    p[1] = lin_ln(B, A, a2, tp.pre2a, lda2, ac->n4, ac->ls.w, ac->ls.b, tp.ls_raw, ldA);
+    DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, 2, s));
+    DR_TRY(op_actor_head(B, A, mus, ldA, tp.ls_raw, ldA, &noise, 0, deterministic, actions, ldA, nullptr, 0, sigmas,
+                         ldA, tp.eps, s));
+  }
+  for (int t = 0; t < H; ++t) {
+    const long long hb = (long long)Hd * B * t;
+    float* h_t = hiddens + (long long)t * Hd;
+    float* h_n = hiddens + (long long)(t + 1) * Hd;
+    float* z_t = latents + (long long)t * L;
+    float* z_n = latents + (long long)(t + 1) * L;
+    // WorldModel.imagine_step (WorldModel.py:72-77)
+    DR_TRY(gru_step(d, wm, B, z_t, ldL, actions + (long long)t * A, ldA, h_t, ldH, h_n, ldH, w.gi, w.gh, tp.r + hb,
+                    tp.u + hb, tp.n + hb, tp.ghn + hb, s));
+    float* p1 = tp.pre1p + (long long)t * B * d->prior_h1;
+    float* p2 = tp.pre2p + (long long)t * B * d->prior_h2;
+    DR_TRY(run(G_NT, AM_PLAIN, lin(B, d->prior_h1, Hd, h_n, ldH, wm->prior.l0.w, Hd, wm->prior.l0.b, p1, d->prior_h1), s));
+    DR_TRY(run(G_NT, AM_LNSILU, lin_ln(B, d->prior_h2, d->prior_h1, p1, d->prior_h1, wm->prior.n1, wm->prior.l3.w,
+                                       wm->prior.l3.b, p2, d->prior_h2), s));
+    DR_TRY(run(G_NT, AM_LNSILU, lin_ln(B, L, d->prior_h2, p2, d->prior_h2, wm->prior.n4, wm->prior.l6.w,
+                                       wm->prior.l6.b, w.plog, L), s));
+    DR_TRY(op_sample(B, d->rows, d->cols, w.plog, L, &nq, t, z_n, ldL, nullptr, tp.soft + (long long)t * B * L, L,
+                     s));
+    // reward / continue heads on (h', z') and the actor for step t+1, grouped
+    const bool nxt = (t + 1 < H);
+    {
+      GemmArgs p[3];
+      p[0] = lin2(B, d->rew_h1, h_n, ldH, Hd, z_n, ldL, L, wm->reward.l0.w, wm->reward.l0.b, w.p1r, d->rew_h1);
+      p[1] = lin2(B, d->cont_h1, h_n, ldH, Hd, z_n, ldL, L, wm->cont.l0.w, wm->cont.l0.b, w.p1c, d->cont_h1);
+      if (nxt)
+        p[2] = lin2(B, a1, h_n, ldH, Hd, z_n, ldL, L, ac->l0.w, ac->l0.b, tp.pre1a + (long long)(t + 1) * a1, lda1);
+      DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, nxt ? 3 : 2, s));
+    }
+    {
+      GemmArgs p[3];
+      p[0] = lin_ln(B, d->rew_h2, d->rew_h1, w.p1r, d->rew_h1, wm->reward.n1, wm->reward.l3.w, wm->reward.l3.b, w.p2r,
+                    d->rew_h2);
+      p[1] = lin_ln(B, d->cont_h2, d->cont_h1, w.p1c, d->cont_h1, wm->cont.n1, wm->cont.l3.w, wm->cont.l3.b, w.p2c,
+                    d->cont_h2);
+      if (nxt) {
+        p[2] = lin_ln(B, a2, a1, tp.pre1a + (long long)(t + 1) * a1, lda1, ac->n1, ac->l3.w, ac->l3.b,
+                      tp.pre2a + (long long)(t + 1) * a2, lda2);
+        p[2].a_out = tp.x1a + (long long)(t + 1) * a1;
+        p[2].ld_aout = lda1;
+      }
+      DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, nxt ? 3 : 2, s));
+    }
+    {
+      GemmArgs p[4];
+      p[0] = lin_ln(B, d->buckets, d->rew_h2, w.p2r, d->rew_h2, wm->reward.n4, wm->reward.l6.w, wm->reward.l6.b,
+                    w.rlog, d->buckets);
+      p[1] = lin_ln(B, 1, d->cont_h2, w.p2c, d->cont_h2, wm->cont.n4, wm->cont.l6.w, wm->cont.l6.b, w.clog, 1);
+      if (nxt) {
+        float* pre2 = tp.pre2a + (long long)(t + 1) * a2;
+        p[2] = lin_ln(B, A, a2, pre2, lda2, ac->n4, ac->mu.w, ac->mu.b, mus + (long long)(t + 1) * A, ldA);
+        p[2].a_out = tp.x2a + (long long)(t + 1) * a2;
+        p[2].ld_aout = lda2;
+        p[3] = lin_ln(B, A, a2, pre2, lda2, ac->n4, ac->ls.w, ac->ls.b, tp.ls_raw + (long long)(t + 1) * A, ldA);
+      }
+      DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, nxt ? 4 : 2, s));
+    }
+    DR_TRY(op_bucket_value(B, d->buckets, w.rlog, d->buckets, wm->buckets_rew, rewards + t, H, s));
+    DR_TRY(op_sigmoid(B, w.clog, 1, continues + t, H, s));
+    if (nxt) {
+      const long long o = (long long)(t + 1) * A;
+      DR_TRY(op_actor_head(B, A, mus + o, ldA, tp.ls_raw + o, ldA, &noise, t + 1, deterministic, actions + o, ldA,
+                           nullptr, 0, sigmas + o, ldA, tp.eps + (long long)(t + 1) * B * A, s));
+    }
+  }
+  return DR_OK;
+}
+
+extern "C" int dr_imagine_bwd(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, int B, int H,
+                              const float* latents, const float* hiddens, const float* actions,
+                              const float* g_mus, const float* g_sigmas,
+                              const float* g_actions, const float* g_latents, const float* g_hiddens,
+                              const void* tape, const dr_actor* gr, void* ws, size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(d && wm && ac && latents && hiddens && actions && tape && gr && B > 0 && H > 0,
+             "null argument or empty batch");
+  Carve c(ws);
+  ImWs w;
+  imws_carve(c, d, B, H, w);
+  WS_CHECK(c, ws_bytes);
+  Carve ct((void*)tape);
+  Tape tp;
+  tape_carve(ct, d, B, H, tp);
+  const int L = latent(d), Hd = d->hidden, A = d->action, a1 = d->actor_h1, a2 = d->actor_h2;
+  const long long ldH = (long long)(H + 1) * Hd, ldL = (long long)(H + 1) * L, ldA = (long long)H * A;
+  const long long lda1 = (long long)H * a1, lda2 = (long long)H * a2;
+  const int BH = B * H;
+  // upstream gradients
+  if (g_hiddens) DR_TRY(copy2d(w.gH, Hd, g_hiddens, Hd, Hd, (long long)B * (H + 1), s));
+  else DR_TRY(zero(w.gH, (long long)B * (H + 1) * Hd, s));
+  if (g_latents) DR_TRY(copy2d(w.gZ, L, g_latents, L, L, (long long)B * (H + 1), s));
+  else DR_TRY(zero(w.gZ, (long long)B * (H + 1) * L, s));
+  if (g_actions) DR_TRY(copy2d(w.gA, A, g_actions, A, A, (long long)BH, s));
+  else DR_TRY(zero(w.gA, (long long)BH * A, s));
+  const bool upstream_state = g_latents || g_hiddens;
+
+  for (int t = H - 1; t >= 0; --t) {
+    const long long hb = (long long)Hd * B * t;
+    float* gH_t = w.gH + (long long)t * Hd;
+    float* gH_n = w.gH + (long long)(t + 1) * Hd;
+    float* gZ_t = w.gZ + (long long)t * L;
+    float* gZ_n = w.gZ + (long long)(t + 1) * L;
+    const bool state_grad = upstream_state || t < H - 1;
+    if (state_grad) {
+      // z_{t+1} = STE(prior(h_{t+1}))   (DynamicsPredictors.py:31-40)
+      DR_TRY(op_softmax_ste_bwd(B, d->rows, d->cols, gZ_n, ldL, tp.soft + (long long)t * B * L, L, w.glog, s));
+      DR_TRY(run(G_NN, AM_PLAIN, bwd_in(B, d->prior_h2, L, w.glog, L, wm->prior.l6.w, d->prior_h2, w.gx2, d->prior_h2, 0), s));
+      DR_TRY(op_ln_silu_bwd(B, d->prior_h2, w.gx2, d->prior_h2, tp.pre2p + (long long)t * B * d->prior_h2, d->prior_h2,
+                            wm->prior.n4.w, wm->prior.n4.b, w.gp2, d->prior_h2, nullptr, nullptr, s));
+      DR_TRY(run(G_NN, AM_PLAIN, bwd_in(B, d->prior_h1, d->prior_h2, w.gp2, d->prior_h2, wm->prior.l3.w, d->prior_h1,
+                                        w.gx1, d->prior_h1, 0), s));
+      DR_TRY(op_ln_silu_bwd(B, d->prior_h1, w.gx1, d->prior_h1, tp.pre1p + (long long)t * B * d->prior_h1, d->prior_h1,
+                            wm->prior.n1.w, wm->prior.n1.b, w.gp1, d->prior_h1, nullptr, nullptr, s));
+      DR_TRY(run(G_NN, AM_PLAIN, bwd_in(B, Hd, d->prior_h1, w.gp1, d->prior_h1, wm->prior.l0.w, Hd, gH_n, ldH, 1), s));
+      // h_{t+1} = GRU(z_t, a_t, h_t)   (SequenceModel.py:19-24)
+      DR_TRY(op_gru_bwd(B, Hd, gH_n, ldH, hiddens + (long long)t * Hd, ldH, tp.r + hb, tp.u + hb, tp.n + hb,
+                        tp.ghn + hb, w.ggi, w.ggh, gH_t, ldH, 1, s));
+      if (t > 0) {
+        GemmArgs p[2];
+        p[0] = bwd_in(B, L + A, 3 * Hd, w.ggi, 3 * Hd, wm->w_ih, L + A, gZ_t, ldL, 1);
+        p[0].Y2 = w.gA + (long long)t * A; p[0].ldy2 = ldA; p[0].nsplitY = L;
+        p[1] = bwd_in(B, Hd, 3 * Hd, w.ggh, 3 * Hd, wm->w_hh, Hd, gH_t, ldH, 1);
+        DR_TRY(gemm_launch(G_NN, AM_PLAIN, p, 2, s));
+      } else {
+        // only the action gradient is consumed at t = 0
+        DR_TRY(run(G_NN, AM_PLAIN, bwd_in(B, A, 3 * Hd, w.ggi, 3 * Hd, wm->w_ih + L, L + A, w.gA, ldA, 1), s));
+      }
+    }
+    // actor at step t: heads, then base_net (Agent.py:191-210)
+    const long long ot = (long long)t * A;
+    float* gh_t = w.gheads + (long long)t * 2 * A;
+    DR_TRY(op_actor_head_bwd(B, A, w.gA + ot, ldA, g_mus ? g_mus + ot : nullptr, g_sigmas ? g_sigmas + ot : nullptr,
+                             ldA, actions + ot, ldA, nullptr, 0, tp.ls_raw + ot, ldA, tp.eps + (long long)t * B * A,
+                             gh_t, (long long)H * 2 * A, s));
+    {
+      GemmArgs g = bwd_in(B, a2, 2 * A, gh_t, (long long)H * 2 * A, ac->mu.w, a2, w.gx2a, a2, 0);
+      g.W2 = ac->ls.w; g.ldb2 = a2; g.ksplitB = A;
+      DR_TRY(run(G_NN, AM_PLAIN, g, s));
+    }
+    const long long o2 = (long long)t * a2, o1 = (long long)t * a1;
+    DR_TRY(op_ln_silu_bwd(B, a2, w.gx2a, a2, tp.pre2a + o2, lda2, ac->n4.w, ac->n4.b, w.gpre2a + o2, lda2,
+                          w.gy2a + o2, w.xh2a + o2, s));
+    DR_TRY(run(G_NN, AM_PLAIN, bwd_in(B, a1, a2, w.gpre2a + o2, lda2, ac->l3.w, a1, w.gx1a, a1, 0), s));
+    DR_TRY(op_ln_silu_bwd(B, a1, w.gx1a, a1, tp.pre1a + o1, lda1, ac->n1.w, ac->n1.b, w.gpre1a + o1, lda1,
+                          w.gy1a + o1, w.xh1a + o1, s));
+    if (t > 0) {
+      GemmArgs g = bwd_in(B, Hd + L, a1, w.gpre1a + o1, lda1, ac->l0.w, Hd + L, gH_t, ldH, 1);
+      g.Y2 = gZ_t; g.ldy2 = ldL; g.nsplitY = Hd;
+      DR_TRY(run(G_NN, AM_PLAIN, g, s));
+    }
+  }
+  // ---- actor weight gradients over all B*H rows (rows r = b*H + t) ----
+  DR_TRY(copy2d(w.hcat, (long long)H * Hd, hiddens, ldH, (long long)H * Hd, B, s));
+  DR_TRY(copy2d(w.zcat, (long long)H * L, latents, ldL, (long long)H * L, B, s));
+  {
+    GemmArgs p[4];
+    p[0] = bwd_w(a1, Hd + L, BH, w.gpre1a, a1, w.hcat, Hd, gr->l0.w);
+    p[0].W2 = w.zcat; p[0].ldb2 = L; p[0].nsplitB = Hd;
+    p[1] = bwd_w(a2, a1, BH, w.gpre2a, a2, tp.x1a, a1, gr->l3.w);
+    p[2] = bwd_w(A, a2, BH, w.gheads, 2 * A, tp.x2a, a2, gr->mu.w);
+    p[3] = bwd_w(A, a2, BH, w.gheads + A, 2 * A, tp.x2a, a2, gr->ls.w);
+    DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 4, s));
+  }
+  DR_TRY(op_colsum(BH, a1, w.gpre1a, a1, nullptr, 0, gr->l0.b, 0, s));
+  DR_TRY(op_colsum(BH, a1, w.gy1a, a1, w.xh1a, a1, gr->n1.w, 0, s));
+  DR_TRY(op_colsum(BH, a1, w.gy1a, a1, nullptr, 0, gr->n1.b, 0, s));
+  DR_TRY(op_colsum(BH, a2, w.gpre2a, a2, nullptr, 0, gr->l3.b, 0, s));
+  DR_TRY(op_colsum(BH, a2, w.gy2a, a2, w.xh2a, a2, gr->n4.w, 0, s));
+  DR_TRY(op_colsum(BH, a2, w.gy2a, a2, nullptr, 0, gr->n4.b, 0, s));
+  DR_TRY(op_colsum(BH, A, w.gheads, 2 * A, nullptr, 0, gr->mu.b, 0, s));
+  DR_TRY(op_colsum(BH, A, w.gheads + A, 2 * A, nullptr, 0, gr->ls.b, 0, s));
+  return DR_OK;
+}
+
+// ===========================================================================
+// a13  critic forward / a16 critic loss + backward
+// ===========================================================================
+struct CTape {
+  float *pre1, *x1, *pre2, *x2, *logits;
+};
+static void ctape_carve(Carve& c, const dr_dims* d, int M, CTape& t) {
+  t.pre1 = c.f((long long)M * d->critic_h1);
+  t.x1 = c.f((long long)M * d->critic_h1);
+  t.pre2 = c.f((long long)M * d->critic_h2);
+  t.x2 = c.f((long long)M * d->critic_h2);
+  t.logits = c.f((long long)M * d->buckets);
+}
+
+extern "C" size_t dr_critic_tape_bytes(const dr_dims* d, int M) {
+  Carve c(nullptr);
+  CTape t;
+  ctape_carve(c, d, M, t);
+  return c.off;
+}
+
+static size_t critic_ws_bytes(const dr_dims* d, int M) {
+  Carve c(nullptr);
+  CTape t;
+  ctape_carve(c, d, M, t);
+  return c.off;
+}
+
+extern "C" int dr_critic_fwd(const dr_dims* d, const dr_critic* cr, int M, const float* h, long long ldh,
+                             const float* z, long long ldz, float* logits, float* values, void* tape, void* ws,
+                             size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(d && cr && h && z && M > 0, "null argument or empty batch");
+  CTape t;
+  if (tape) {
+    Carve c(tape);
+    ctape_carve(c, d, M, t);
+  } else {
+    Carve c(ws);
+    ctape_carve(c, d, M, t);
+    WS_CHECK(c, ws_bytes);
+  }
+  const int L = latent(d), Hd = d->hidden, c1 = d->critic_h1, c2 = d->critic_h2, nb = d->buckets;
+  DR_TRY(run(G_NT, AM_PLAIN, lin2(M, c1, h, ldh, Hd, z, ldz, L, cr->net.l0.w, cr->net.l0.b, t.pre1, c1), s));
+  GemmArgs g2 = lin_ln(M, c2, c1, t.pre1, c1, cr->net.n1, cr->net.l3.w, cr->net.l3.b, t.pre2, c2);
+  g2.a_out = t.x1; g2.ld_aout = c1;
+  DR_TRY(run(G_NT, AM_LNSILU, g2, s));
+  float* lg = logits ? logits : t.logits;
+  GemmArgs g3 = lin_ln(M, nb, c2, t.pre2, c2, cr->net.n4, cr->net.l6.w, cr->net.l6.b, lg, nb);
+  g3.a_out = t.x2; g3.ld_aout = c2;
+  DR_TRY(run(G_NT, AM_LNSILU, g3, s));
+  if (tape && logits && logits != t.logits) DR_TRY(copy2d(t.logits, nb, logits, nb, nb, M, s));
+  if (values) DR_TRY(op_bucket_value(M, nb, lg, nb, cr->buckets, values, 1, s));
+  return DR_OK;
+}
+
+struct CBws {
+  float *row_loss, *glog, *gx2, *gp2, *gy2, *xh2, *gx1, *gp1, *gy1, *xh1;
+};
+static void cbws_carve(Carve& c, const dr_dims* d, int B, int H, CBws& w) {
+  const long long M = (long long)B * (H + 1);
+  w.row_loss = c.f((long long)B * H);
+  w.glog = c.f(M * d->buckets);
+  w.gx2 = c.f(M * d->critic_h2);
+  w.gp2 = c.f(M * d->critic_h2);
+  w.gy2 = c.f(M * d->critic_h2);
+  w.xh2 = c.f(M * d->critic_h2);
+  w.gx1 = c.f(M * d->critic_h1);
+  w.gp1 = c.f(M * d->critic_h1);
+  w.gy1 = c.f(M * d->critic_h1);
+  w.xh1 = c.f(M * d->critic_h1);
+}
+
+extern "C" size_t dr_critic_workspace_bytes(const dr_dims* d, int B, int H) {
+  Carve c(nullptr);
+  CBws w;
+  cbws_carve(c, d, B, H, w);
+  const size_t a = c.off, b = critic_ws_bytes(d, B * (H + 1));
+  return a > b ? a : b;
+}
+
+extern "C" int dr_critic_loss_bwd(const dr_dims* d, const dr_critic* cr, int B, int H, const float* hiddens,
+                                  const float* latents, const float* R, const void* tape, float scale,
+                                  float* loss_out, const dr_critic* gr, void* ws, size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(d && cr && hiddens && latents && R && tape && loss_out && gr && B > 0 && H > 0, "null argument");
+  Carve c(ws);
+  CBws w;
+  cbws_carve(c, d, B, H, w);
+  WS_CHECK(c, ws_bytes);
+  const int M = B * (H + 1);
+  Carve ct((void*)tape);
+  CTape t;
+  ctape_carve(ct, d, M, t);
+  const int L = latent(d), Hd = d->hidden, c1 = d->critic_h1, c2 = d->critic_h2, nb = d->buckets;
+  DR_TRY(op_critic_ce(B, H, nb, t.logits, R, cr->buckets, scale, w.row_loss, w.glog, s));
+  DR_TRY(op_mean(B * H, w.row_loss, loss_out, s));
+  // value_net.6
+  DR_TRY(run(G_NN, AM_PLAIN, bwd_in(M, c2, nb, w.glog, nb, cr->net.l6.w, c2, w.gx2, c2, 0), s));
+  DR_TRY(op_ln_silu_bwd(M, c2, w.gx2, c2, t.pre2, c2, cr->net.n4.w, cr->net.n4.b, w.gp2, c2, w.gy2, w.xh2, s));
+  DR_TRY(run(G_NN, AM_PLAIN, bwd_in(M, c1, c2, w.gp2, c2, cr->net.l3.w, c1, w.gx1, c1, 0), s));
+  DR_TRY(op_ln_silu_bwd(M, c1, w.gx1, c1, t.pre1, c1, cr->net.n1.w, cr->net.n1.b, w.gp1, c1, w.gy1, w.xh1, s));
+  {
+    GemmArgs p[3];
+    p[0] = bwd_w(nb, c2, M, w.glog, nb, t.x2, c2, gr->net.l6.w);
+    p[1] = bwd_w(c2, c1, M, w.gp2, c2, t.x1, c1, gr->net.l3.w);
+    p[2] = bwd_w(c1, Hd + L, M, w.gp1, c1, hiddens, Hd, gr->net.l0.w);
+    p[2].W2 = latents; p[2].ldb2 = L; p[2].nsplitB = Hd;
+    DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 3, s));
+  }
+  DR_TRY(op_colsum(M, nb, w.glog, nb, nullptr, 0, gr->net.l6.b, 0, s));
+  DR_TRY(op_colsum(M, c2, w.gp2, c2, nullptr, 0, gr->net.l3.b, 0, s));
+  DR_TRY(op_colsum(M, c2, w.gy2, c2, w.xh2, c2, gr->net.n4.w, 0, s));
+  DR_TRY(op_colsum(M, c2, w.gy2, c2, nullptr, 0, gr->net.n4.b, 0, s));
+  DR_TRY(op_colsum(M, c1, w.gp1, c1, nullptr, 0, gr->net.l0.b, 0, s));
+  DR_TRY(op_colsum(M, c1, w.gy1, c1, w.xh1, c1, gr->net.n1.w, 0, s));
+  DR_TRY(op_colsum(M, c1, w.gy1, c1, nullptr, 0, gr->net.n1.b, 0, s));
+  return DR_OK;
+}
+
+// ===========================================================================
+// single steps
+// ===========================================================================
+static size_t step_ws(const dr_dims* d, int B) {
+  Carve c(nullptr);
+  c.f((long long)B * 3 * d->hidden);
+  c.f((long long)B * 3 * d->hidden);
+  c.f((long long)B * latent(d));
+  const int mx = d->prior_h1 > d->rew_h1 ? d->prior_h1 : d->rew_h1;
+  c.f((long long)B * (mx > d->actor_h1 ? mx : d->actor_h1) * 2);
+  c.f((long long)B * (d->buckets + 8) * 2);
+  return c.off;
+}
+
+extern "C" size_t dr_step_workspace_bytes(const dr_dims* d, int B) { return step_ws(d, B) + 4096; }
+
+// generic 3-layer MLP forward on [h | z] (z may be NULL / in_z = 0)
+static int mlp3(const dr_mlp3& m, int M, int in_h, const float* h, long long ldh, int in_z, const float* z,
+                long long ldz, int h1, int h2, int n_out, float* out, long long ldo, float* p1, float* p2,
+                hipStream_t s) {
+  GemmArgs g = in_z ? lin2(M, h1, h, ldh, in_h, z, ldz, in_z, m.l0.w, m.l0.b, p1, h1)
+                    : lin(M, h1, in_h, h, ldh, m.l0.w, in_h, m.l0.b, p1, h1);
+  DR_TRY(run(G_NT, AM_PLAIN, g, s));
+  DR_TRY(run(G_NT, AM_LNSILU, lin_ln(M, h2, h1, p1, h1, m.n1, m.l3.w, m.l3.b, p2, h2), s));
+  return run(G_NT, AM_LNSILU, lin_ln(M, n_out, h2, p2, h2, m.n4, m.l6.w, m.l6.b, out, ldo), s);
+}
+
+extern "C" int dr_mlp3_fwd(const dr_mlp3* m, int M, int in_h, const float* h, long long ldh, int in_z,
+                           const float* z, long long ldz, int h1, int h2, int n_out, float* out, long long ldo,
+                           void* ws, size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(m && h && out && M > 0 && h1 > 0 && h2 > 0 && n_out > 0, "null argument or bad widths");
+  Carve c(ws);
+  float* p1 = c.f((long long)M * h1);
+  float* p2 = c.f((long long)M * h2);
+  WS_CHECK(c, ws_bytes);
+  return mlp3(*m, M, in_h, h, ldh, in_z, z, ldz, h1, h2, n_out, out, ldo, p1, p2, s);
+}
+
+extern "C" int dr_gru_cell(const dr_dims* d, const dr_world_model* wm, int B, const float* z, const float* h,
+                           const float* a, float* h_out, void* ws, size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(d && wm && z && a && h_out && B > 0, "null argument");
+  Carve c(ws);
+  float* gi = c.f((long long)B * 3 * d->hidden);
+  float* gh = c.f((long long)B * 3 * d->hidden);
+  WS_CHECK(c, ws_bytes);
+  return gru_step(d, wm, B, z, latent(d), a, d->action, h, d->hidden, h_out, d->hidden, gi, gh, nullptr, nullptr,
+                  nullptr, nullptr, s);
+}
+
+extern "C" int dr_imagine_step(const dr_dims* d, const dr_world_model* wm, int B, const float* h, const float* z,
+                               const float* a, dr_noise noise, float* h_out, float* z_out, float* r_out,
+                               float* c_out, void* ws, size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(d && wm && z && a && h_out && z_out && B > 0, "null argument");
+  const int L = latent(d), Hd = d->hidden;
+  Carve c(ws);
+  float* gi = c.f((long long)B * 3 * Hd);
+  float* gh = c.f((long long)B * 3 * Hd);
+  float* lg = c.f((long long)B * L);
+  const int mx = d->prior_h1 > d->rew_h1 ? d->prior_h1 : d->rew_h1;
+  const int w1 = mx > d->cont_h1 ? mx : d->cont_h1;
+  float* p1 = c.f((long long)B * w1 * 2);
+  float* p2 = c.f((long long)B * (d->buckets + 8) * 2);
+  WS_CHECK(c, ws_bytes);
+  DR_TRY(gru_step(d, wm, B, z, L, a, d->action, h, Hd, h_out, Hd, gi, gh, nullptr, nullptr, nullptr, nullptr, s));
+  DR_TRY(mlp3(wm->prior, B, Hd, h_out, Hd, 0, nullptr, 0, d->prior_h1, d->prior_h2, L, lg, L, p1, p2, s));
+  DR_TRY(op_sample(B, d->rows, d->cols, lg, L, &noise, 0, z_out, L, nullptr, nullptr, 0, s));
+  if (r_out) {
+    DR_TRY(mlp3(wm->reward, B, Hd, h_out, Hd, L, z_out, L, d->rew_h1, d->rew_h2, d->buckets, lg, d->buckets, p1, p2, s));
+    DR_TRY(op_bucket_value(B, d->buckets, lg, d->buckets, wm->buckets_rew, r_out, 1, s));
+  }
+  if (c_out) {
+    DR_TRY(mlp3(wm->cont, B, Hd, h_out, Hd, L, z_out, L, d->cont_h1, d->cont_h2, 1, lg, 1, p1, p2, s));
+    DR_TRY(op_sigmoid(B, lg, 1, c_out, 1, s));
+  }
+  return DR_OK;
+}
+
+extern "C" int dr_actor_act(const dr_dims* d, const dr_actor* ac, int B, const float* h, const float* z,
+                            dr_noise noise, int deterministic, float* a_out, float* mu_out, float* sigma_out,
+                            void* ws, size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(d && ac && h && z && a_out && mu_out && sigma_out && B > 0, "null argument");
+  const int L = latent(d), Hd = d->hidden, A = d->action, a1 = d->actor_h1, a2 = d->actor_h2;
+  Carve c(ws);
+  float* p1 = c.f((long long)B * a1);
+  float* p2 = c.f((long long)B * a2);
+  float* ls = c.f((long long)B * A);
+  WS_CHECK(c, ws_bytes);
+  DR_TRY(run(G_NT, AM_PLAIN, lin2(B, a1, h, Hd, Hd, z, L, L, ac->l0.w, ac->l0.b, p1, a1), s));
+  DR_TRY(run(G_NT, AM_LNSILU, lin_ln(B, a2, a1, p1, a1, ac->n1, ac->l3.w, ac->l3.b, p2, a2), s));
+  GemmArgs p[2];
+  p[0] = lin_ln(B, A, a2, p2, a2, ac->n4, ac->mu.w, ac->mu.b, mu_out, A);
+  p[1] = lin_ln(B, A, a2, p2, a2, ac->n4, ac->ls.w, ac->ls.b, ls, A);
+  DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, 2, s));
+  return op_actor_head(B, A, mu_out, A, ls, A, &noise, 0, deterministic, a_out, A, nullptr, 0, sigma_out, A, nullptr,
+                       s);
+}

@@ -1,0 +1,38 @@
+// Generic fused f32 GEMM on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32).
+//   Y[m][n] (+)= act( alpha * sum_k opA(m,k) * opB(k,n) + bias[n] + addend[m][n] )
+// A operand: row-major [M][K] ("MK", optional 2nd K-segment, optional
+// LayerNorm+SiLU applied on load, or conv im2col) or [K][M] ("KM").
+// B operand: [N][K] ("NK": Y = A W^T, forward Linear) or [K][N] ("KN":
+// Y = A W, backward input-grad / weight-grad), optional 2nd segment.
+#pragma once
+#include "common.h"
+
+enum { AM_PLAIN = 0, AM_LNSILU = 1, AM_CONV = 2, AM_CONV_SRC = 3 };
+
+struct GemmArgs {
+  int M, N, K;
+  // A
+  const float* A; long long lda;
+  const float* A2; long long lda2; int ksplitA;  // MK: k >= ksplitA reads A2[m][k-ksplitA]
+  const float* ln_g; const float* ln_b;          // AM_LNSILU (LN width == K)
+  float* a_out; long long ld_aout;               // optional copy of the transformed A (n-tile 0 writes)
+  // conv im2col (k4 s2 p1), A = NCHW activations [frame][cin][ih][iw]
+  int cin, ih, iw, oh, ow;
+  dr_frames src;                                 // AM_CONV_SRC: frames, f = t*nb + b
+  int nb;
+  // B
+  const float* W; long long ldb;
+  const float* W2; long long ldb2; int ksplitB; int nsplitB;  // KN: k>=ksplitB | n>=nsplitB -> W2
+  // epilogue
+  const float* bias; const float* addend; long long ld_add;
+  float* Y; long long ldy;
+  float* Y2; long long ldy2; int nsplitY;        // n >= nsplitY -> Y2[m][n-nsplitY]
+  int accumulate, act, out_conv;                 // act 1 = SiLU; out_conv: Y NCHW [frame][N][oh*ow]
+  float alpha;
+};
+
+enum GemmLayout { G_NT = 0, G_NN = 1, G_TN = 2 };
+
+GemmArgs gemm_args();  // zero-initialised with neutral defaults
+// Launch up to 4 problems sharing layout/A-mode in one dispatch.
+int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hipStream_t s);

@@ -1,0 +1,812 @@
+// Row / elementwise kernels of libdreamer_hip: GRU gates, categorical
+// sampler, heads, LayerNorm-SiLU backward, losses, returns, quantile,
+// optimiser.  Built with -ffp-contract=off: each expression rounds like the
+// corresponding PyTorch CPU op sequence of the reference (cited per kernel).
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "ops.h"
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+static thread_local char g_err[512] = "";
+
+void dr_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int dr_check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    dr_set_error("%s: %s", what, hipGetErrorString(e));
+    return DR_E_HIP;
+  }
+  return DR_OK;
+}
+
+extern "C" const char* dr_last_error(void) { return g_err; }
+extern "C" int dr_version(void) { return 1; }
+
+static inline int blocks_for(long long n, int t) { return (int)((n + t - 1) / t); }
+
+// ---------------------------------------------------------------------------
+// GRU gates (SequenceModel.py:13-23 -> torch gru_cell)
+// ---------------------------------------------------------------------------
+__global__ void k_gru_fwd(int B, int Hd, const float* __restrict__ gi, const float* __restrict__ gh,
+                          const float* __restrict__ h, long long ldh, float* __restrict__ hout, long long ldo,
+                          float* sr, float* su, float* sn, float* sghn) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * Hd) return;
+  const int b = (int)(i / Hd), j = (int)(i - (long long)b * Hd);
+  const float* gib = gi + (long long)b * 3 * Hd;
+  const float* ghb = gh + (long long)b * 3 * Hd;
+  const float r = 1.0f / (1.0f + expf(-(ghb[j] + gib[j])));
+  const float u = 1.0f / (1.0f + expf(-(ghb[Hd + j] + gib[Hd + j])));
+  const float hn = ghb[2 * Hd + j];
+  const float n = tanhf(gib[2 * Hd + j] + hn * r);
+  const float hv = h ? h[(long long)b * ldh + j] : 0.0f;
+  hout[(long long)b * ldo + j] = (hv - n) * u + n;
+  if (sr) {
+    sr[i] = r;
+    su[i] = u;
+    sn[i] = n;
+    sghn[i] = hn;
+  }
+}
+
+int op_gru_fwd(int B, int Hd, const float* gi, const float* gh, const float* h, long long ldh, float* hout,
+               long long ldo, float* sr, float* su, float* sn, float* sghn, hipStream_t s) {
+  const long long n = (long long)B * Hd;
+  if (n == 0) return DR_OK;
+  hipLaunchKernelGGL(k_gru_fwd, dim3(blocks_for(n, 256)), dim3(256), 0, s, B, Hd, gi, gh, h, ldh, hout, ldo, sr,
+                     su, sn, sghn);
+  return dr_check_launch("gru_fwd");
+}
+
+__global__ void k_gru_bwd(int B, int Hd, const float* __restrict__ g_hp, long long ldg, const float* __restrict__ h,
+                          long long ldh, const float* sr, const float* su, const float* sn, const float* sghn,
+                          float* g_gi, float* g_gh, float* gh_out, long long ldo, int accumulate) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * Hd) return;
+  const int b = (int)(i / Hd), j = (int)(i - (long long)b * Hd);
+  const float g = g_hp[(long long)b * ldg + j];
+  const float r = sr[i], u = su[i], n = sn[i], hn = sghn[i];
+  const float hv = h ? h[(long long)b * ldh + j] : 0.0f;
+  // h' = (h - n)*u + n
+  const float g_hmn = g * u;
+  const float g_u = g * (hv - n);
+  const float g_n = g + (-g_hmn);
+  // n = tanh(in + hn*r)
+  const float g_pn = g_n * (1.0f - n * n);
+  const float g_r = g_pn * hn;
+  const float g_hn = g_pn * r;
+  const float g_pr = g_r * (1.0f - r) * r;
+  const float g_pu = g_u * (1.0f - u) * u;
+  float* gib = g_gi + (long long)b * 3 * Hd;
+  float* ghb = g_gh + (long long)b * 3 * Hd;
+  gib[j] = g_pr;
+  gib[Hd + j] = g_pu;
+  gib[2 * Hd + j] = g_pn;
+  ghb[j] = g_pr;
+  ghb[Hd + j] = g_pu;
+  ghb[2 * Hd + j] = g_hn;
+  float* o = gh_out + (long long)b * ldo + j;
+  if (accumulate) *o = *o + g_hmn;
+  else *o = g_hmn;
+}
+
+int op_gru_bwd(int B, int Hd, const float* g_hp, long long ldg, const float* h, long long ldh, const float* sr,
+               const float* su, const float* sn, const float* sghn, float* g_gi, float* g_gh, float* gh_out,
+               long long ldo, int accumulate, hipStream_t s) {
+  const long long n = (long long)B * Hd;
+  if (n == 0) return DR_OK;
+  hipLaunchKernelGGL(k_gru_bwd, dim3(blocks_for(n, 256)), dim3(256), 0, s, B, Hd, g_hp, ldg, h, ldh, sr, su, sn,
+                     sghn, g_gi, g_gh, gh_out, ldo, accumulate);
+  return dr_check_launch("gru_bwd");
+}
+
+// ---------------------------------------------------------------------------
+// Categorical sample with 1% unimix and straight-through value
+// (VAE.py:88-98, DynamicsPredictors.py:33-39; torch Categorical normalises
+// p by its sum, multinomial(n=1) == argmax(p_hat / Exp(1))).
+// One aligned group of W = pow2 >= C lanes per (row, latent group).
+// ---------------------------------------------------------------------------
+__global__ void k_sample(int M, int R, int C, int W, const float* __restrict__ logits, long long ldl, dr_noise nz,
+                         int step, float unimix_add, float* __restrict__ z, long long ldz, int* idx, float* soft,
+                         long long lds) {
+  const int gtid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int grp = gtid / W, c = gtid - grp * W;
+  const bool valid = grp < M * R;
+  const int m = valid ? grp / R : 0, r = valid ? grp - m * R : 0;
+  const bool act = valid && c < C;
+  const float x = act ? logits[(long long)m * ldl + r * C + c] : -INFINITY;
+  const float mx = group_max(x, W);
+  const float e = act ? expf(x - mx) : 0.0f;
+  const float se = group_sum(e, W);
+  const float p = e / se;
+  const float pu = act ? (0.99f * p + unimix_add) : 0.0f;
+  const float sp = group_sum(pu, W);
+  const float ph = pu / sp;
+  float q = 1.0f;
+  if (act) {
+    if (nz.q) q = nz.q[((long long)step * M * R + grp) * C + c];
+    else q = dr_exp1(nz.rng, (uint32_t)(nz.stream + step), (uint32_t)(nz.row0 + m), (uint32_t)(r * C + c));
+  }
+  float best = act ? ph / q : -INFINITY;
+  int bi = act ? c : 0x7fffffff;
+  for (int o = W >> 1; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ob > best || (ob == best && oi < bi)) {
+      best = ob;
+      bi = oi;
+    }
+  }
+  if (act) {
+    z[(long long)m * ldz + r * C + c] = (c == bi) ? ((1.0f + pu) - pu) : 0.0f;
+    if (soft) soft[(long long)m * lds + r * C + c] = p;
+    if (idx && c == 0) idx[grp] = bi;
+  }
+}
+
+static int pow2_at_least(int c) {
+  int w = 1;
+  while (w < c) w <<= 1;
+  return w;
+}
+
+int op_sample(int M, int R, int C, const float* logits, long long ldl, const dr_noise* nz, int step, float* z,
+              long long ldz, int* idx, float* soft, long long lds, hipStream_t s) {
+  if (C < 1 || C > 64) {
+    dr_set_error("sample: latent classes must be in [1,64], got %d", C);
+    return DR_E_INVALID;
+  }
+  const int W = pow2_at_least(C);
+  const long long threads = (long long)M * R * W;
+  if (threads == 0) return DR_OK;
+  const float unimix = (float)(0.01 * (1.0 / C));
+  hipLaunchKernelGGL(k_sample, dim3(blocks_for(threads, 256)), dim3(256), 0, s, M, R, C, W, logits, ldl, *nz, step,
+                     unimix, z, ldz, idx, soft, lds);
+  return dr_check_launch("sample");
+}
+
+extern "C" int dr_categorical_sample(int M, int R, int C, const float* logits, dr_noise noise, float* z_out,
+                                     int* idx_out, float* soft_out, hipStream_t stream) {
+  return op_sample(M, R, C, logits, (long long)R * C, &noise, 0, z_out, (long long)R * C, idx_out, soft_out,
+                   (long long)R * C, stream);
+}
+
+// softmax backward through the STE value: g_logit = s*(g_s - sum(g_s*s)), g_s = 0.99*g_z
+__global__ void k_softmax_ste_bwd(int M, int R, int C, int W, const float* __restrict__ gz, long long ldg,
+                                  const float* __restrict__ soft, long long lds, float* __restrict__ gl) {
+  const int gtid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int grp = gtid / W, c = gtid - grp * W;
+  const bool valid = grp < M * R;
+  const int m = valid ? grp / R : 0, r = valid ? grp - m * R : 0;
+  const bool act = valid && c < C;
+  const float gs = act ? gz[(long long)m * ldg + r * C + c] * 0.99f : 0.0f;
+  const float sv = act ? soft[(long long)m * lds + r * C + c] : 0.0f;
+  const float dot = group_sum(gs * sv, W);
+  if (act) gl[(long long)m * R * C + r * C + c] = sv * (gs - dot);
+}
+
+int op_softmax_ste_bwd(int M, int R, int C, const float* gz, long long ldg, const float* soft, long long lds,
+                       float* g_logits, hipStream_t s) {
+  const int W = pow2_at_least(C);
+  const long long threads = (long long)M * R * W;
+  if (threads == 0) return DR_OK;
+  hipLaunchKernelGGL(k_softmax_ste_bwd, dim3(blocks_for(threads, 256)), dim3(256), 0, s, M, R, C, W, gz, ldg, soft,
+                     lds, g_logits);
+  return dr_check_launch("softmax_ste_bwd");
+}
+
+// ---------------------------------------------------------------------------
+// LayerNorm(eps=1e-5) + SiLU backward, one wave per row
+// ---------------------------------------------------------------------------
+__global__ void k_ln_silu_bwd(int M, int K, const float* __restrict__ gx, long long ldgx,
+                              const float* __restrict__ pre, long long ldp, const float* __restrict__ gamma,
+                              const float* __restrict__ beta, float* __restrict__ g_pre, long long ldgp, float* gy_out,
+                              float* xhat_out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* p = pre + (long long)row * ldp;
+  const float* g = gx + (long long)row * ldgx;
+  float s = 0.f;
+  for (int k = lane; k < K; k += 64) s += p[k];
+  const float mean = wave_sum(s) / (float)K;
+  float v = 0.f;
+  for (int k = lane; k < K; k += 64) {
+    const float d = p[k] - mean;
+    v += d * d;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(v) / (float)K + 1e-5f);
+  float c1 = 0.f, c2 = 0.f;
+  for (int k = lane; k < K; k += 64) {
+    const float xh = (p[k] - mean) * rstd;
+    const float y = xh * gamma[k] + beta[k];
+    const float sg = 1.0f / (1.0f + expf(-y));
+    const float gyv = g[k] * (sg * (1.0f + y * (1.0f - sg)));
+    const float gxh = gyv * gamma[k];
+    c1 += gxh;
+    c2 += gxh * xh;
+    if (gy_out) {
+      gy_out[(long long)row * ldgp + k] = gyv;
+      xhat_out[(long long)row * ldgp + k] = xh;
+    }
+  }
+  c1 = wave_sum(c1) / (float)K;
+  c2 = wave_sum(c2) / (float)K;
+  for (int k = lane; k < K; k += 64) {
+    const float xh = (p[k] - mean) * rstd;
+    const float y = xh * gamma[k] + beta[k];
+    const float sg = 1.0f / (1.0f + expf(-y));
+    const float gxh = g[k] * (sg * (1.0f + y * (1.0f - sg))) * gamma[k];
+    g_pre[(long long)row * ldgp + k] = rstd * (gxh - c1 - xh * c2);
+  }
+}
+
+int op_ln_silu_bwd(int M, int K, const float* gx, long long ldgx, const float* pre, long long ldp,
+                   const float* gamma, const float* beta, float* g_pre, long long ldgp, float* gy, float* xhat,
+                   hipStream_t s) {
+  if (M == 0) return DR_OK;
+  hipLaunchKernelGGL(k_ln_silu_bwd, dim3(dr_cdiv(M, 4)), dim3(256), 0, s, M, K, gx, ldgx, pre, ldp, gamma, beta,
+                     g_pre, ldgp, gy, xhat);
+  return dr_check_launch("ln_silu_bwd");
+}
+
+// ---------------------------------------------------------------------------
+// column sums (bias / LayerNorm parameter gradients), deterministic order
+// ---------------------------------------------------------------------------
+__global__ void k_colsum(int M, int N, const float* __restrict__ X, long long ldx, const float* __restrict__ Y,
+                         long long ldy, float* out, int accumulate) {
+  __shared__ float part[4][64];
+  const int n = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  float acc = 0.f;
+  if (n < N) {
+    for (int m = rg; m < M; m += 4) {
+      float v = X[(long long)m * ldx + n];
+      if (Y) v = v * Y[(long long)m * ldy + n];
+      acc += v;
+    }
+  }
+  part[rg][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (rg == 0 && n < N) {
+    const float t = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
+    out[n] = accumulate ? out[n] + t : t;
+  }
+}
+
+int op_colsum(int M, int N, const float* X, long long ldx, const float* Y, long long ldy, float* out, int accumulate,
+              hipStream_t s) {
+  if (N == 0) return DR_OK;
+  hipLaunchKernelGGL(k_colsum, dim3(dr_cdiv(N, 64)), dim3(256), 0, s, M, N, X, ldx, Y, ldy, out, accumulate);
+  return dr_check_launch("colsum");
+}
+
+// ---------------------------------------------------------------------------
+// heads
+// ---------------------------------------------------------------------------
+// RewardPredictor.predict / Critic.value: symexp(sum(softmax(l) * buckets))
+// (DynamicsPredictors.py:70-74, Agent.py:237-241); one wave per row
+__global__ void k_bucket_value(int M, int nb, const float* __restrict__ logits, long long ldl,
+                               const float* __restrict__ buckets, float* out, long long ostride) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* l = logits + (long long)row * ldl;
+  float mx = -INFINITY;
+  for (int k = lane; k < nb; k += 64) mx = fmaxf(mx, l[k]);
+  mx = wave_max(mx);
+  float se = 0.f;
+  for (int k = lane; k < nb; k += 64) se += expf(l[k] - mx);
+  se = wave_sum(se);
+  float acc = 0.f;
+  for (int k = lane; k < nb; k += 64) acc += (expf(l[k] - mx) / se) * buckets[k];
+  acc = wave_sum(acc);
+  if (lane == 0) out[(long long)row * ostride] = dr_symexp(acc);
+}
+
+int op_bucket_value(int M, int nb, const float* logits, long long ldl, const float* buckets, float* out,
+                    long long ostride, hipStream_t s) {
+  if (M == 0) return DR_OK;
+  hipLaunchKernelGGL(k_bucket_value, dim3(dr_cdiv(M, 4)), dim3(256), 0, s, M, nb, logits, ldl, buckets, out,
+                     ostride);
+  return dr_check_launch("bucket_value");
+}
+
+extern "C" int dr_bucket_value(int M, int nb, const float* logits, const float* buckets, float* out,
+                               hipStream_t stream) {
+  return op_bucket_value(M, nb, logits, nb, buckets, out, 1, stream);
+}
+
+// ContinuePredictor.predict: sigmoid(logit) (DynamicsPredictors.py:95-105)
+__global__ void k_sigmoid(int M, const float* x, long long ldx, float* out, long long ostride) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  out[(long long)i * ostride] = 1.0f / (1.0f + expf(-x[(long long)i * ldx]));
+}
+
+int op_sigmoid(int M, const float* x, long long ldx, float* out, long long ostride, hipStream_t s) {
+  if (M == 0) return DR_OK;
+  hipLaunchKernelGGL(k_sigmoid, dim3(dr_cdiv(M, 256)), dim3(256), 0, s, M, x, ldx, out, ostride);
+  return dr_check_launch("sigmoid");
+}
+
+// Actor.forward tail + act (Agent.py:196-210)
+__global__ void k_actor_head(int M, int A, const float* __restrict__ mu_raw, long long ldm,
+                             const float* __restrict__ ls_raw, long long ldl, dr_noise nz, int step, int det,
+                             float* a, long long lda, float* mu, long long ldmu, float* sigma, long long lds,
+                             float* eps_save) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * A) return;
+  const int m = i / A, k = i - m * A;
+  const float muv = mu_raw[(long long)m * ldm + k];
+  const float ls = fminf(fmaxf(ls_raw[(long long)m * ldl + k], -5.0f), 2.0f);
+  const float sg = dr_softplus(ls) + 1e-3f;
+  float av;
+  if (det) {
+    av = tanhf(muv);
+  } else {
+    float e;
+    if (nz.eps) e = nz.eps[((long long)step * M + m) * A + k];
+    else e = dr_normal(nz.rng, (uint32_t)(nz.stream + step), (uint32_t)(nz.row0 + m), (uint32_t)k);
+    if (eps_save) eps_save[i] = e;
+    av = tanhf(muv + e * sg);
+  }
+  if (a) a[(long long)m * lda + k] = av;
+  if (mu) mu[(long long)m * ldmu + k] = muv;
+  if (sigma) sigma[(long long)m * lds + k] = sg;
+}
+
+int op_actor_head(int M, int A, const float* mu_raw, long long ldm, const float* ls_raw, long long ldl,
+                  const dr_noise* nz, int step, int deterministic, float* a, long long lda, float* mu,
+                  long long ldmu, float* sigma, long long lds, float* eps_save, hipStream_t s) {
+  if (M * A == 0) return DR_OK;
+  hipLaunchKernelGGL(k_actor_head, dim3(dr_cdiv(M * A, 256)), dim3(256), 0, s, M, A, mu_raw, ldm, ls_raw, ldl, *nz,
+                     step, deterministic, a, lda, mu, ldmu, sigma, lds, eps_save);
+  return dr_check_launch("actor_head");
+}
+
+// backward of a = tanh(mu + eps*sigma), sigma = softplus(clamp(ls)) + 1e-3,
+// plus the loss gradients on mu/sigma; g_heads [M][2A] = [g_mu | g_ls]
+__global__ void k_actor_head_bwd(int M, int A, const float* g_a, long long ldga, const float* g_mu_l,
+                                 const float* g_sig_l, long long ldgl, const float* a, long long lda,
+                                 const float* sigma, long long lds, const float* ls_raw, long long ldl,
+                                 const float* eps, float* g_heads, long long ldh) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * A) return;
+  const int m = i / A, k = i - m * A;
+  float gmu = g_mu_l ? g_mu_l[(long long)m * ldgl + k] : 0.0f;
+  float gsg = g_sig_l ? g_sig_l[(long long)m * ldgl + k] : 0.0f;
+  if (g_a) {
+    const float av = a[(long long)m * lda + k];
+    const float gp = g_a[(long long)m * ldga + k] * (1.0f - av * av);
+    gmu = gmu + gp;
+    gsg = gsg + gp * eps[i];
+  }
+  const float lr = ls_raw[(long long)m * ldl + k];
+  const float lc = fminf(fmaxf(lr, -5.0f), 2.0f);
+  float gls = 0.0f;
+  if (lr >= -5.0f && lr <= 2.0f) {
+    const float ez = expf(lc);
+    gls = (lc > 20.0f) ? gsg : gsg * ez / (ez + 1.0f);
+  }
+  g_heads[(long long)m * ldh + k] = gmu;
+  g_heads[(long long)m * ldh + A + k] = gls;
+}
+
+int op_actor_head_bwd(int M, int A, const float* g_a, long long ldga, const float* g_mu_l, const float* g_sig_l,
+                      long long ldgl, const float* a, long long lda, const float* sigma, long long lds,
+                      const float* ls_raw, long long ldl, const float* eps, float* g_heads, long long ldh,
+                      hipStream_t s) {
+  if (M * A == 0) return DR_OK;
+  hipLaunchKernelGGL(k_actor_head_bwd, dim3(dr_cdiv(M * A, 256)), dim3(256), 0, s, M, A, g_a, ldga, g_mu_l, g_sig_l,
+                     ldgl, a, lda, sigma, lds, ls_raw, ldl, eps, g_heads, ldh);
+  return dr_check_launch("actor_head_bwd");
+}
+
+// ---------------------------------------------------------------------------
+// lambda returns (Agent.py:156-172), one thread per batch row
+// ---------------------------------------------------------------------------
+__global__ void k_lambda_returns(int B, int H, const float* r, const float* c, const float* V, float gamma,
+                                 float lam, float lam_c, float* R) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float* rb = r + (long long)b * H;
+  const float* cb = c + (long long)b * H;
+  const float* vb = V + (long long)b * (H + 1);
+  float* Rb = R + (long long)b * H;
+  float nxt = rb[H - 1] + (gamma * cb[H - 1]) * vb[H];
+  Rb[H - 1] = nxt;
+  for (int t = H - 2; t >= 0; --t) {
+    const float v = rb[t] + (gamma * cb[t]) * ((lam_c * vb[t + 1]) + (lam * nxt));
+    Rb[t] = v;
+    nxt = v;
+  }
+}
+
+extern "C" int dr_lambda_returns(int B, int H, const float* r, const float* c, const float* V, float gamma,
+                                 float lam, float* R, hipStream_t stream) {
+  if (B <= 0 || H <= 0) {
+    dr_set_error("lambda_returns: bad dims B=%d H=%d", B, H);
+    return DR_E_INVALID;
+  }
+  const float lam_c = (float)(1.0 - (double)lam);
+  hipLaunchKernelGGL(k_lambda_returns, dim3(dr_cdiv(B, 64)), dim3(64), 0, stream, B, H, r, c, V, gamma, lam, lam_c,
+                     R);
+  return dr_check_launch("lambda_returns");
+}
+
+// ---------------------------------------------------------------------------
+// update_S (Agent.py:78-88): quantiles 0.95/0.05 (torch linear interpolation)
+// over all returns by a bitonic sort in LDS, EMA of the range, norm=max(S,1)
+// ---------------------------------------------------------------------------
+#define DR_SORT_MAX 16384
+
+__device__ float torch_lerp(float a, float b, float w) {
+  return (w < 0.5f) ? a + w * (b - a) : b - (b - a) * (1.0f - w);
+}
+
+__device__ float quantile_sorted(const float* v, int n, float q) {
+  const float rank = q * (float)(n - 1);
+  const int lo = (int)rank;
+  const int hi = (int)ceilf(rank);
+  const float w = rank - (float)lo;
+  return torch_lerp(v[lo], v[hi], w);
+}
+
+__global__ __launch_bounds__(1024) void k_update_S(int n, int n2, const float* R, float* S, float* norm_out) {
+  extern __shared__ __attribute__((aligned(16))) float sv[];
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n2; i += blockDim.x) {
+    float x = INFINITY;
+    if (i < n) {
+      x = R[i];
+      if (!isfinite(x)) bad = 1;
+    }
+    sv[i] = x;
+  }
+  __syncthreads();
+  if (!bad) {
+    for (int k = 2; k <= n2; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = threadIdx.x; i < n2; i += blockDim.x) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const float a = sv[i], b = sv[ixj];
+            const bool up = ((i & k) == 0);
+            if ((a > b) == up) {
+              sv[i] = b;
+              sv[ixj] = a;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  if (threadIdx.x == 0) {
+    float s = *S;
+    if (!bad) {
+      const float q95 = quantile_sorted(sv, n, 0.95f);
+      const float q05 = quantile_sorted(sv, n, 0.05f);
+      const float range = fmaxf(q95 - q05, 1.0f);
+      s = 0.99f * s + 0.01f * range;
+      *S = s;
+    }
+    if (norm_out) *norm_out = fmaxf(s, 1.0f);
+  }
+}
+
+extern "C" int dr_update_S(int n, const float* R, float* S, float* norm_out, void* ws, size_t ws_bytes,
+                           hipStream_t stream) {
+  (void)ws;
+  (void)ws_bytes;
+  if (n <= 0 || n > DR_SORT_MAX) {
+    dr_set_error("update_S: n=%d outside [1,%d]", n, DR_SORT_MAX);
+    return DR_E_INVALID;
+  }
+  int n2 = 1;
+  while (n2 < n) n2 <<= 1;
+  hipLaunchKernelGGL(k_update_S, dim3(1), dim3(1024), n2 * sizeof(float), stream, n, n2, R, S, norm_out);
+  return dr_check_launch("update_S");
+}
+
+// ---------------------------------------------------------------------------
+// actor loss (Agent.py:105-125) and dL/dmu, dL/dsigma
+// ---------------------------------------------------------------------------
+__global__ void k_actor_loss_grad(int B, int H, int A, const float* mus, const float* sigmas, const float* actions,
+                                  const float* R, const float* V, const float* norm, float nu, float scale,
+                                  float* row_loss, float* g_mus, float* g_sigmas) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (b,t)
+  if (i >= B * H) return;
+  const int b = i / H, t = i - b * H;
+  const float adv = R[i] - V[(long long)b * (H + 1) + t];
+  const float sadv = adv / (*norm);
+  const float HALF_LOG_2PI = 0.91893853320467274178f;  // math.log(math.sqrt(2*math.pi))
+  const float LOG2 = 0.69314718055994530942f;
+  float logp = 0.f;
+  for (int k = 0; k < A; ++k) {
+    const long long o = (long long)i * A + k;
+    float y = fminf(fmaxf(actions[o], -1.0f + 1e-6f), 1.0f - 1e-6f);
+    const float x = atanhf(y);
+    const float mu = mus[o], sg = sigmas[o];
+    const float d = x - mu;
+    const float var = sg * sg;
+    const float lp = -(d * d) / (2.0f * var) - logf(sg) - HALF_LOG_2PI;
+    const float ladj = 2.0f * (LOG2 - x - dr_softplus(-2.0f * x));
+    logp += -ladj + lp;
+  }
+  const float gl = scale * (nu - sadv);
+  for (int k = 0; k < A; ++k) {
+    const long long o = (long long)i * A + k;
+    float y = fminf(fmaxf(actions[o], -1.0f + 1e-6f), 1.0f - 1e-6f);
+    const float x = atanhf(y);
+    const float mu = mus[o], sg = sigmas[o];
+    const float d = x - mu;
+    g_mus[o] = gl * (d / (sg * sg));
+    g_sigmas[o] = gl * ((d * d) / (sg * sg * sg) - 1.0f / sg);
+  }
+  row_loss[i] = -(logp * sadv) - (nu * (-logp));
+}
+
+__global__ __launch_bounds__(1024) void k_mean(int n, const float* x, float* out) {
+  __shared__ float part[1024];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < n; i += 1024) acc += x[i];
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 512; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) part[threadIdx.x] += part[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = part[0] / (float)n;
+}
+
+int op_mean(int n, const float* x, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_mean, dim3(1), dim3(1024), 0, s, n, x, out);
+  return dr_check_launch("mean");
+}
+
+extern "C" int dr_actor_loss_grad(int B, int H, int A, const float* mus, const float* sigmas, const float* actions,
+                                  const float* R, const float* V, const float* norm, float nu, float scale,
+                                  float* loss_out, float* g_mus, float* g_sigmas, hipStream_t stream) {
+  // row losses are staged in g_sigmas' tail? no: use a small scratch in loss_out[1..]
+  if (B <= 0 || H <= 0 || A <= 0) {
+    dr_set_error("actor_loss_grad: bad dims");
+    return DR_E_INVALID;
+  }
+  float* row_loss = loss_out + 1;  // caller provides 1 + B*H floats
+  hipLaunchKernelGGL(k_actor_loss_grad, dim3(dr_cdiv(B * H, 128)), dim3(128), 0, stream, B, H, A, mus, sigmas,
+                     actions, R, V, norm, nu, scale, row_loss, g_mus, g_sigmas);
+  DR_TRY(dr_check_launch("actor_loss_grad"));
+  return op_mean(B * H, row_loss, loss_out, stream);
+}
+
+// ---------------------------------------------------------------------------
+// critic two-hot CE (Agent.py:127-135, DreamerUtils.py:39-50): one wave per
+// row (b,t<H) of logits [B][H+1][nb]; rows t==H get zero gradient.
+// ---------------------------------------------------------------------------
+__global__ void k_critic_ce(int B, int H, int nb, const float* __restrict__ logits, const float* __restrict__ R,
+                            const float* __restrict__ buckets, float scale, float* row_loss, float* g_logits) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B * (H + 1)) return;
+  const int b = row / (H + 1), t = row - b * (H + 1);
+  const float* l = logits + (long long)row * nb;
+  float* g = g_logits + (long long)row * nb;
+  if (t == H) {
+    for (int k = lane; k < nb; k += 64) g[k] = 0.0f;
+    return;
+  }
+  // target two-hot of symlog(R)
+  const float bmin = buckets[0], bmax = buckets[nb - 1];
+  float v = dr_symlog(R[(long long)b * H + t]);
+  v = fminf(fmaxf(v, bmin), bmax);
+  int cnt = 0;
+  for (int k = lane; k < nb; k += 64) cnt += (buckets[k] <= v) ? 1 : 0;
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+  int lo = cnt - 1;
+  if (lo > nb - 2) lo = nb - 2;
+  const float blo = buckets[lo], bhi = buckets[lo + 1];
+  const float w = (v - blo) / (bhi - blo + 1e-8f);
+  const float wlo = 1.0f - w;
+  const float sum_th = wlo + w;
+  // log_softmax
+  float mx = -INFINITY;
+  for (int k = lane; k < nb; k += 64) mx = fmaxf(mx, l[k]);
+  mx = wave_max(mx);
+  float se = 0.f;
+  for (int k = lane; k < nb; k += 64) se += expf(l[k] - mx);
+  se = wave_sum(se);
+  const float lse = logf(se);
+  for (int k = lane; k < nb; k += 64) {
+    const float sm = expf(l[k] - mx) / se;
+    const float th = (k == lo) ? wlo : ((k == lo + 1) ? w : 0.0f);
+    g[k] = scale * (sm * sum_th - th);
+  }
+  if (lane == 0) {
+    const float ls_lo = (l[lo] - mx) - lse, ls_hi = (l[lo + 1] - mx) - lse;
+    row_loss[(long long)b * H + t] = -(wlo * ls_lo + w * ls_hi);
+  }
+}
+
+int op_critic_ce(int B, int H, int nb, const float* logits, const float* R, const float* buckets, float scale,
+                 float* row_loss, float* g_logits, hipStream_t s) {
+  const int rows = B * (H + 1);
+  hipLaunchKernelGGL(k_critic_ce, dim3(dr_cdiv(rows, 4)), dim3(256), 0, s, B, H, nb, logits, R, buckets, scale,
+                     row_loss, g_logits);
+  return dr_check_launch("critic_ce");
+}
+
+// ---------------------------------------------------------------------------
+// optimiser: clip_grad_norm_(100) + AdamW (torch single-tensor op order) + EMA
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_sqnorm(long long n, const float* g, float* acc) {
+  __shared__ float part[1024];
+  float s = 0.f;
+  for (long long i = threadIdx.x; i < n; i += 1024) s += g[i] * g[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 512; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) part[threadIdx.x] += part[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *acc = *acc + part[0];
+}
+
+extern "C" int dr_sqnorm(long long n, const float* g, float* acc, hipStream_t stream) {
+  hipLaunchKernelGGL(k_sqnorm, dim3(1), dim3(1024), 0, stream, n, g, acc);
+  return dr_check_launch("sqnorm");
+}
+
+// prelude: step += 1 (unless skipped), bias corrections in double like
+// torch's python scalars (adam.py: bias_correction1 = 1 - beta1**step ...)
+__global__ void k_adamw_prelude(int* step, float* hyper, float lr, float b1, float b2, const int* skip) {
+  if (skip && *skip) return;
+  const int st = *step + 1;
+  *step = st;
+  const double bc1 = 1.0 - pow((double)b1, (double)st);
+  const double bc2 = 1.0 - pow((double)b2, (double)st);
+  hyper[0] = (float)((double)lr / bc1);  // step_size
+  hyper[1] = (float)sqrt(bc2);           // bias_correction2_sqrt
+}
+
+__global__ void k_adamw(long long n, float* p, float* g, float* m, float* v, const float* sqnorm,
+                        float max_norm, float keep, float omb1, float b2, float omb2, const float* hyper, float eps,
+                        const int* skip) {
+  if (skip && *skip) return;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float clip = 1.0f;
+  if (sqnorm) clip = fminf(max_norm / (sqrtf(*sqnorm) + 1e-6f), 1.0f);
+  float gv = g[i];
+  if (clip != 1.0f) {  // clip_grad_norm_ scales p.grad in place (Agent.py:147-148)
+    gv = gv * clip;
+    g[i] = gv;
+  }
+  const float pv = p[i] * keep;
+  const float mv = m[i];
+  const float mn = (omb1 < 0.5f) ? mv + omb1 * (gv - mv) : gv - (gv - mv) * (1.0f - omb1);
+  const float vn = v[i] * b2 + (omb2 * gv) * gv;
+  const float den = sqrtf(vn) / hyper[1] + eps;
+  p[i] = pv + ((-hyper[0]) * mn) / den;
+  m[i] = mn;
+  v[i] = vn;
+}
+
+extern "C" int dr_adamw(long long n, float* p, float* g, float* m, float* v, const float* sqnorm,
+                        float max_norm, float lr, float b1, float b2, float eps, float wd, int* step, float* hyper,
+                        const int* skip, hipStream_t stream) {
+  if (n <= 0) return DR_OK;
+  hipLaunchKernelGGL(k_adamw_prelude, dim3(1), dim3(1), 0, stream, step, hyper, lr, b1, b2, skip);
+  DR_TRY(dr_check_launch("adamw_prelude"));
+  const float keep = (float)(1.0 - (double)lr * (double)wd);
+  const float omb1 = (float)(1.0 - (double)b1), omb2 = (float)(1.0 - (double)b2);
+  hipLaunchKernelGGL(k_adamw, dim3(blocks_for(n, 256)), dim3(256), 0, stream, n, p, g, m, v, sqnorm, max_norm, keep,
+                     omb1, b2, omb2, hyper, eps, skip);
+  return dr_check_launch("adamw");
+}
+
+__global__ void k_ema(long long n, float* t, const float* s, float keep, float tau, const int* skip) {
+  if (skip && *skip) return;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float a = t[i] * keep;
+  t[i] = a + tau * s[i];
+}
+
+extern "C" int dr_ema(long long n, float* target, const float* src, float keep, float tau, const int* skip,
+                      hipStream_t stream) {
+  if (n <= 0) return DR_OK;
+  hipLaunchKernelGGL(k_ema, dim3(blocks_for(n, 256)), dim3(256), 0, stream, n, target, src, keep, tau, skip);
+  return dr_check_launch("ema");
+}
+
+__global__ void k_nonfinite(long long n, const float* x, int* flag) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  bool bad = (i < n) && !isfinite(x[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+extern "C" int dr_nonfinite(long long n, const float* x, int* flag, hipStream_t stream) {
+  if (n <= 0) return DR_OK;
+  hipLaunchKernelGGL(k_nonfinite, dim3(blocks_for(n, 256)), dim3(256), 0, stream, n, x, flag);
+  return dr_check_launch("nonfinite");
+}
+
+// ---------------------------------------------------------------------------
+// misc
+// ---------------------------------------------------------------------------
+__global__ void k_fill(long long n, float* x, float v) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = v;
+}
+
+int op_fill(long long n, float* x, float v, hipStream_t s) {
+  if (n <= 0) return DR_OK;
+  hipLaunchKernelGGL(k_fill, dim3(blocks_for(n, 256)), dim3(256), 0, s, n, x, v);
+  return dr_check_launch("fill");
+}
+
+// Conv2d weight [co][ci][4][4] -> [co][tap][ci] for NHWC implicit GEMM
+__global__ void k_conv_repack(int cout, int cin, const float* w, float* wr) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cout * cin * 16) return;
+  const int co = i / (cin * 16), rem = i - co * cin * 16;
+  const int ci = rem / 16, tap = rem - ci * 16;
+  wr[(long long)co * cin * 16 + tap * cin + ci] = w[i];
+}
+
+int op_conv_repack(int cout, int cin, const float* w, float* wr, hipStream_t s) {
+  hipLaunchKernelGGL(k_conv_repack, dim3(dr_cdiv(cout * cin * 16, 256)), dim3(256), 0, s, cout, cin, w, wr);
+  return dr_check_launch("conv_repack");
+}
+
+// Buffer.sample_sequences gather (Buffer.py:49-61): u8 frames -> f32 0..255
+__global__ void k_replay_gather(long long cap, int B, int S, int fe, int A, const unsigned char* frames,
+                                const float* actions, const float* rewards, const float* continues,
+                                const long long* starts, float* obs, float* act, float* rew, float* cont) {
+  const long long bs = blockIdx.y;  // (b, s)
+  const int b = (int)(bs / S), s = (int)(bs - (long long)b * S);
+  const long long slot = (starts[b] + s) % cap;
+  if (fe > 0) {
+    const unsigned char* src = frames + slot * fe;
+    float* dst = obs + bs * fe;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < fe; e += gridDim.x * blockDim.x) dst[e] = (float)src[e];
+  }
+  if (blockIdx.x == 0) {
+    if ((int)threadIdx.x < A) act[bs * A + threadIdx.x] = actions[slot * A + threadIdx.x];
+    if (threadIdx.x == 0) {
+      if (rew) rew[bs] = rewards[slot];
+      if (cont) cont[bs] = continues[slot];
+    }
+  }
+}
+
+extern "C" int dr_replay_gather(long long cap, int B, int S, int frame_elems, int A, const unsigned char* frames,
+                                const float* actions, const float* rewards, const float* continues,
+                                const long long* starts, float* obs_out, float* act_out, float* rew_out,
+                                float* cont_out, hipStream_t stream) {
+  if (B <= 0 || S <= 0 || A > 256) {
+    dr_set_error("replay_gather: bad dims");
+    return DR_E_INVALID;
+  }
+  const int gx = frame_elems > 0 ? dr_cdiv(frame_elems, 1024) : 1;
+  hipLaunchKernelGGL(k_replay_gather, dim3(gx, B * S), dim3(256), 0, stream, cap, B, S,
+                     frame_elems, A, frames, actions, rewards, continues, starts, obs_out, act_out, rew_out,
+                     cont_out);
+  return dr_check_launch("replay_gather");
+}
+
+__global__ void k_rng_advance(unsigned long long* rng, unsigned long long d) { rng[1] += d; }
+
+extern "C" int dr_rng_advance(unsigned long long* rng, unsigned long long delta, hipStream_t stream) {
+  hipLaunchKernelGGL(k_rng_advance, dim3(1), dim3(1), 0, stream, rng, delta);
+  return dr_check_launch("rng_advance");
+}

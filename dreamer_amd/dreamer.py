@@ -1,0 +1,303 @@
+"""Dreamer: the reference's top-level agent (Dreamer.py) on the MI355X engine.
+
+Same constructor (config dict + device), attributes, methods and state_dict
+layout, so train_car_racer.py runs unchanged.  train_Agent -- the metric's
+unit of work -- runs as one fused device-resident epoch (engine.py); the
+world-model step stays PyTorch-ROCm this round."""
+import os
+
+import numpy as np
+import torch
+import torch.nn as nn
+from tqdm import tqdm
+
+from . import _lib as L
+from . import hip
+from .agent import Agent
+from .buffer import Buffer
+from .utils import _sanitize_for_save
+from .world_model import WorldModel
+
+
+class _DreamFn(torch.autograd.Function):
+    """dream_episodes as one autograd node: forward = dr_imagine_fwd, backward
+    = dr_imagine_bwd (BPTT through the unroll into the actor's parameters).
+    The world model receives no gradient (the reference's WM grads from this
+    path are discarded, WorldModel.py:195)."""
+
+    @staticmethod
+    def forward(ctx, dreamer, z0, h0, *actor_params):
+        ctx.set_materialize_grads(False)
+        out, tape = dreamer._imagine_raw(z0, h0)
+        ctx.dreamer, ctx.tape = dreamer, tape
+        ctx.save_for_backward(out[0], out[1], out[2])
+        return out
+
+    @staticmethod
+    def backward(ctx, g_lat, g_hid, g_act, g_rew, g_cont, g_mu, g_sig):
+        for g, n in ((g_rew, "rewards"), (g_cont, "continues")):
+            if g is not None and bool(torch.any(g != 0)):
+                raise NotImplementedError(f"gradient through imagined {n} is not part of the reference's loss")
+        lat, hid, act = ctx.saved_tensors
+        dr = ctx.dreamer
+        ag = dr.agent
+        grad_flat = torch.zeros_like(ag.fa.flat)
+        f = ag.fa
+        gptr = lambda n: grad_flat.data_ptr() + 4 * f.offsets[n]
+        gs = L.dr_actor(*(L.dr_linear(gptr(w), gptr(b)) for w, b in (
+            ("base_net.0.weight", "base_net.0.bias"), ("base_net.1.weight", "base_net.1.bias"),
+            ("base_net.3.weight", "base_net.3.bias"), ("base_net.4.weight", "base_net.4.bias"),
+            ("mu_head.weight", "mu_head.bias"), ("log_sig_head.weight", "log_sig_head.bias"))))
+        B, H1 = hid.shape[:2]
+        d = dr.world_model.dims(ag)
+        c = lambda t: None if t is None else t.float().contiguous()
+        g_mu, g_sig, g_act, g_lat, g_hid = (c(t) for t in (g_mu, g_sig, g_act, g_lat, g_hid))
+        ws = hip.workspace(hid.device).get("im_bwd", L.query("dr_imagine_workspace_bytes", d, B, H1 - 1))
+        L.call("dr_imagine_bwd", d, dr.world_model.packed(), ag.actor_struct(), B, H1 - 1, L.ptr(lat), L.ptr(hid),
+               L.ptr(act), L.ptr(g_mu), L.ptr(g_sig), L.ptr(g_act), L.ptr(g_lat), L.ptr(g_hid), L.ptr(ctx.tape), gs,
+               L.ptr(ws), ws.numel(), hip.stream())
+        grads = [grad_flat[f.offsets[n]:f.offsets[n] + p.numel()].view_as(p) for n, p in zip(f.names, f.params)]
+        return (None, None, None, *grads)
+
+
+class Dreamer(nn.Module):
+    def __init__(self, config, device):
+        super().__init__()
+        c = config
+        self.hidden_state_dims = c["hidden_state_dims"]
+        self.action_dims = c["action_dims"]
+        self.observation_dims = tuple(c["observation_dims"])
+        self.latent_state_dims = tuple(c["latent_state_dims"])
+        device = torch.device(device)
+        self.world_model = WorldModel(
+            c["hidden_state_dims"], tuple(c["latent_state_dims"]), tuple(c["observation_dims"]), c["action_dims"],
+            c["horizon"], c["batch_size"], c["world_model_lr"], tuple(c["world_model_betas"]), c["world_model_eps"],
+            c["beta_prediction"], c["beta_dynamics"], c["beta_representation"], c["encoder_filter_num_1"],
+            c["encoder_filter_num_2"], c["encoder_hidden_layer_nodes"], c["decoder_filter_num_1"],
+            c["decoder_filter_num_2"], c["decoder_hidden_layer_nodes"], c["dyn_pred_hidden_num_nodes_1"],
+            c["dyn_pred_hidden_num_nodes_2"], c["rew_pred_hidden_num_nodes_1"], c["rew_pred_hidden_num_nodes_2"],
+            c["critic_reward_buckets"], c["cont_pred_hidden_num_nodes_1"], c["cont_pred_hidden_num_nodes_2"],
+            device=device)
+        self.agent = Agent(
+            c["action_dims"], tuple(c["latent_state_dims"]), c["hidden_state_dims"], c["hidden_layer_actor_1_size"],
+            c["hidden_layer_actor_2_size"], c["hidden_layer_critic_1_size"], c["hidden_layer_critic_2_size"],
+            c["critic_reward_buckets"], c["actor_lr"], tuple(c["actor_betas"]), c["actor_eps"], c["critic_lr"],
+            tuple(c["critic_betas"]), c["critic_eps"], c["nu"], c["lambda_"], c["gamma"], device=device)
+        self.buffer = Buffer(c["buffer_size"], c["sequence_length"], c["action_dims"], tuple(c["observation_dims"]),
+                             device=device)
+        self.horizon = c["horizon"]
+        self.batch_size = c["batch_size"]
+        self.sequence_length = c["sequence_length"]
+        self.training_iterations = c["training_iterations"]
+        self.random_iterations = c["random_iterations"]
+        self.WM_epochs = c["WM_epochs"]
+        self.AC_epochs = c["AC_epochs"]
+        self.seed = c["seed"]
+        self.device = device
+        self.agent_obs = None
+        self.agent_hidden = None
+        self.agent_latent = None
+        self._engine = None
+        self.world = None  # (rank, size, group) for data-parallel train_Agent
+
+    # ------------------------------------------------------------- imagination
+    def _imagine_raw(self, z0, h0, eps=None, q=None):
+        L.require_gpu(h0)
+        B = h0.shape[0]
+        H = self.horizon
+        R, C = self.latent_state_dims
+        A = self.action_dims
+        dev = h0.device
+        d = self.world_model.dims(self.agent)
+        lat = torch.empty(B, H + 1, R, C, device=dev)
+        hid = torch.empty(B, H + 1, self.hidden_state_dims, device=dev)
+        act, mu, sg = (torch.empty(B, H, A, device=dev) for _ in range(3))
+        rew, cont = torch.empty(B, H, 1, device=dev), torch.empty(B, H, 1, device=dev)
+        tape = torch.empty(L.query("dr_imagine_tape_bytes", d, B, H), dtype=torch.uint8, device=dev)
+        ws = hip.workspace(dev).get("im", L.query("dr_imagine_workspace_bytes", d, B, H))
+        if eps is None and q is None:
+            nz = hip.rng(dev).noise()
+        else:
+            nz = hip.explicit_noise(q=q, eps=eps, device=dev)
+        z = z0.reshape(B, -1).float().contiguous()
+        h = h0.reshape(B, -1).float().contiguous()
+        L.call("dr_imagine_fwd", d, self.world_model.packed(), self.agent.actor_struct(), B, H, L.ptr(z), L.ptr(h),
+               nz, 0, L.ptr(lat), L.ptr(hid), L.ptr(act), L.ptr(rew), L.ptr(cont), L.ptr(mu), L.ptr(sg), L.ptr(tape),
+               L.ptr(ws), ws.numel(), hip.stream())
+        return (lat, hid, act, rew, cont, mu, sg), tape
+
+    def dream_episodes(self, starting_latent_state_batch, starting_hidden_state_batch):
+        """Dreamer.dream_episodes (Dreamer.py:143-175) as one HIP unroll."""
+        self.agent._ensure_flat()
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.agent.actor.parameters()):
+            return _DreamFn.apply(self, starting_latent_state_batch.detach(), starting_hidden_state_batch.detach(),
+                                  *self.agent.fa.params)
+        return self._imagine_raw(starting_latent_state_batch, starting_hidden_state_batch)[0]
+
+    def warm_start_generator(self, observation_seq_batch, action_seq_batch, sequence_length):
+        """Dreamer.warm_start_generator (Dreamer.py:244-262): time-batched conv
+        encoder over the S/2 warm-up frames, then the posterior scan."""
+        obs = observation_seq_batch.float().contiguous()
+        L.require_gpu(obs)
+        B, S = obs.shape[:2]
+        T = sequence_length // 2
+        d = self.world_model.dims(self.agent)
+        wm = self.world_model.packed()
+        dev = obs.device
+        fe = int(np.prod(obs.shape[2:]))
+        fr = L.dr_frames(None, 0, None, L.ptr(obs), S * fe, fe, 1)
+        feat = torch.empty(T * B, d.enc_hidden, device=dev)
+        st = hip.stream()
+        ws = hip.workspace(dev).get("enc", L.query("dr_encoder_workspace_bytes", d, T * B))
+        L.call("dr_encoder_features", d, wm, fr, B, T, L.ptr(feat), L.ptr(ws), ws.numel(), st)
+        act = action_seq_batch.float().contiguous()
+        A = act.shape[-1]
+        R, C = self.latent_state_dims
+        z = torch.empty(B, 1, R, C, device=dev)
+        h = torch.empty(B, 1, self.hidden_state_dims, device=dev)
+        ws2 = hip.workspace(dev).get("obs", L.query("dr_observe_workspace_bytes", d, B))
+        L.call("dr_observe_scan", d, wm, B, T, L.ptr(feat), L.ptr(act), act.shape[1] * A, A, None, None,
+               hip.rng(dev).noise(), L.ptr(z), L.ptr(h), None, L.ptr(ws2), ws2.numel(), st)
+        return z, h
+
+    # --------------------------------------------------------------- training
+    @property
+    def engine(self):
+        if self._engine is None:
+            from .engine import ImaginationEngine
+            self._engine = ImaginationEngine(self, world=self.world)
+        return self._engine
+
+    def train_Agent(self):
+        """Dreamer.train_Agent (Dreamer.py:264-287): AC_epochs fused epochs."""
+        la, lc = [], []
+        for _ in tqdm(range(self.AC_epochs), desc="Training Agent in Dreams", leave=False):
+            starts = self.buffer.sample_start_indices(self.batch_size if self.world is None else self.engine.B)
+            a, c = self.engine.run(starts)
+            la.append(a.clone())
+            lc.append(c.clone())
+        return torch.cat(la).mean(dim=0), torch.cat(lc).mean(dim=0)
+
+    def train_world_model(self):  # Dreamer.py:228-242
+        out = []
+        for _ in tqdm(range(self.WM_epochs), desc="Training World Model On Buffer Data", leave=False):
+            obs, act, rew, cont, _ = self.buffer.sample_sequences(batch_size=self.batch_size)
+            out.append(self.world_model.training_step(obs, act, rew, cont))
+        return out
+
+    def load_pretrained_dreamer(self, path):
+        self.load_state_dict(torch.load(path, weights_only=True))
+
+    def save_trained_Dreamer(self, save_path):
+        torch.save(self.state_dict(), save_path)
+
+    # ------------------------------------------------- acting (batch-1, HIP)
+    def _obs_tensor(self, observation):
+        obs = observation.transpose(2, 0, 1).astype(np.uint8)
+        norm = (obs.astype(np.float32) / 255.0) - 0.5
+        return norm, torch.tensor(norm, dtype=torch.float32, device=self.device).unsqueeze(0).unsqueeze(0)
+
+    def rollout_policy(self, env, random_policy=False):  # Dreamer.py:177-226
+        with torch.no_grad():
+            if self.agent_obs is None:
+                observation, _ = env.reset(seed=self.seed)
+                self.agent_obs, ot = self._obs_tensor(observation)
+                self.agent_hidden = torch.zeros(1, 1, self.hidden_state_dims, device=self.device)
+                self.agent_latent, _ = self.world_model.encoder.encode(self.agent_hidden, ot)
+            for _ in range(self.sequence_length):
+                if random_policy:
+                    action_np = env.action_space.sample()
+                    action = torch.tensor(action_np, dtype=torch.float32, device=self.device).view(1, 1, -1)
+                else:
+                    action, _, _ = self.agent.actor.act(self.agent_hidden, self.agent_latent, deterministic=False)
+                    action_np = action.detach().cpu().numpy().reshape(-1)
+                observation_, reward, terminated, truncated, _ = env.step(action_np)
+                norm_, ot_ = self._obs_tensor(observation_)
+                done = terminated or truncated
+                current_u8 = ((self.agent_obs + 0.5) * 255.0).astype(np.uint8)
+                self.buffer.add_to_buffer(current_u8, action_np, reward, 1 - done)
+                if done:
+                    self.seed += 1
+                    observation, _ = env.reset(seed=self.seed)
+                    self.agent_obs, ot = self._obs_tensor(observation)
+                    self.agent_hidden = torch.zeros(1, 1, self.hidden_state_dims, device=self.device)
+                    self.agent_latent, _ = self.world_model.encoder.encode(self.agent_hidden, ot)
+                else:
+                    self.agent_obs = norm_
+                    self.agent_latent, self.agent_hidden, _ = self.world_model.observe_step(
+                        self.agent_latent, self.agent_hidden, action, ot_)
+
+    def evaluate_agent(self, env, eval_episodes):  # Dreamer.py:295-322
+        rewards = []
+        with torch.no_grad():
+            for _ in tqdm(range(eval_episodes), desc="Evaluating Agent", leave=False):
+                self.seed += 1
+                total = 0
+                observation, _ = env.reset(seed=self.seed)
+                _, ot = self._obs_tensor(observation)
+                hidden = torch.zeros(1, 1, self.hidden_state_dims, device=self.device)
+                latent, _ = self.world_model.encoder.encode(hidden, ot)
+                done = False
+                while not done:
+                    action, _, _ = self.agent.actor.act(hidden, latent, deterministic=True)
+                    observation_, reward, terminated, truncated, _ = env.step(
+                        action.detach().cpu().numpy().squeeze(0).squeeze(0))
+                    _, ot = self._obs_tensor(observation_)
+                    total += reward
+                    done = terminated or truncated
+                    latent, hidden, _ = self.world_model.observe_step(latent, hidden, action, ot)
+                rewards.append(total)
+        return torch.tensor(rewards, dtype=torch.float32, device=self.device).mean()
+
+    def train_dreamer(self, env, eval_env):  # Dreamer.py:324-372
+        WM_loss_list, actor_loss_list, critic_loss_list, evaluation_list = [], [], [], []
+        print("Starting Training...")
+        print("Starting Random Kickstart.")
+        for _ in tqdm(range(self.random_iterations), desc="Kickstarting Dreamer Agent.", leave=True):
+            self.rollout_policy(env, random_policy=True)
+            WM_loss_list.append([x.detach().cpu().item() for x in self.train_world_model()])
+        print("Starting Training Loop...")
+        evaluation_list.append(self.evaluate_agent(eval_env, eval_episodes=3).detach().cpu().item())
+        for it in tqdm(range(self.training_iterations), desc="Training Dreamer Agent.", leave=True):
+            self.rollout_policy(env, random_policy=False)
+            wm_loss = self.train_world_model()
+            actor_loss, critic_loss = self.train_Agent()
+            WM_loss_list.append([x.detach().cpu().item() for x in wm_loss])
+            actor_loss_list.append(actor_loss.detach().cpu().item())
+            critic_loss_list.append(critic_loss.detach().cpu().item())
+            if it % 1000 == 0:
+                os.makedirs("./models", exist_ok=True)
+                self.save_trained_Dreamer(os.path.join("./models", f"agent_checkpoint_{it}.pth"))
+                self.save_trained_Dreamer(os.path.join("./models", "agent_latest.pth"))
+                np.savez(os.path.join("./models", "training_logs.npz"),
+                         world_model_loss=_sanitize_for_save(WM_loss_list),
+                         actor_loss=_sanitize_for_save(actor_loss_list),
+                         critic_loss=_sanitize_for_save(critic_loss_list),
+                         rewards=_sanitize_for_save(evaluation_list))
+            if it % 500 == 0:
+                evaluation_list.append(self.evaluate_agent(eval_env, eval_episodes=3).detach().cpu().item())
+        print("Training Complete.")
+        evaluation_list.append(self.evaluate_agent(eval_env, eval_episodes=10).detach().cpu().item())
+        return WM_loss_list, actor_loss_list, critic_loss_list, evaluation_list
+
+    def Run(self, env, env_seed, render=True):  # Dreamer.py:374-401
+        total = 0
+        observation, _ = env.reset(seed=env_seed)
+        _, ot = self._obs_tensor(observation)
+        hidden = torch.zeros(1, 1, self.hidden_state_dims, device=self.device)
+        with torch.no_grad():
+            latent, _ = self.world_model.encoder.encode(hidden, ot)
+        done = False
+        while not done:
+            if render:
+                env.render()
+            with torch.no_grad():
+                action, _, _ = self.agent.actor.act(hidden, latent, deterministic=True)
+            observation_, reward, terminated, truncated, _ = env.step(
+                action.detach().cpu().numpy().squeeze(0).squeeze(0))
+            _, ot = self._obs_tensor(observation_)
+            total += reward
+            done = terminated or truncated
+            with torch.no_grad():
+                latent, hidden, _ = self.world_model.observe_step(latent, hidden, action, ot)
+        return total

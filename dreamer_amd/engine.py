@@ -1,0 +1,209 @@
+"""ImaginationEngine: the fused, device-resident train_Agent epoch.
+
+One epoch (Dreamer.train_Agent's unit of work, Dreamer.py:264-287) is a fixed
+sequence of libdreamer_hip calls on one stream:
+
+  a1  window starts (host numpy RNG, Buffer.py:36-48) -> device
+  a3  encoder conv stack over the S/2 warm-start frames of all B windows,
+      read straight from the u8 replay ring in HBM (time-batched)
+  a2  posterior scan (GRU + latent_mapper + sampler), S/2 steps
+  a7  H-step imagination unroll (actor, GRU, prior, reward, continue)
+  a13-a16 target/critic forward, lambda returns, update_S, actor loss and
+      BPTT through the unroll, critic two-hot CE backward, clip + AdamW,
+      soft target update
+
+With world_size > 1 (one process per GPU, RCCL over xGMI) each rank runs its
+slice of the batch; the exchange is one all-gather of the lambda returns
+(global quantile of update_S) and one all-reduce of a flat
+[actor grads | critic grads | losses] buffer.  Everything else is local.
+On one GPU the whole epoch is captured once into a HIP graph and replayed.
+"""
+import numpy as np
+import torch
+
+from . import _lib as L
+from . import hip
+
+WARM_STREAM = 1 << 24
+DREAM_STREAM = 2 << 24
+
+
+class ImaginationEngine:
+    def __init__(self, dreamer, B=None, world=None, use_graph=True):
+        self.dr = dreamer
+        self.dev = dreamer.device
+        self.B = int(B or dreamer.batch_size)
+        self.S = int(dreamer.sequence_length)
+        self.H = int(dreamer.horizon)
+        self.T = self.S // 2
+        self.world = world  # (rank, size, group) or None
+        self.rank = world[0] if world else 0
+        self.wsize = world[1] if world else 1
+        self.use_graph = use_graph and self.wsize == 1
+        self.graph = None
+        self.graph_key = None
+        self._alloc()
+
+    # ------------------------------------------------------------------ setup
+    def dims(self):
+        return self.dr.world_model.dims(self.dr.agent)
+
+    def _alloc(self):
+        d = self.dims()
+        self.d = d
+        B, H, T = self.B, self.H, self.T
+        L_ = d.rows * d.cols
+        dev = self.dev
+        f = lambda *s: torch.zeros(*s, device=dev)
+        self.starts = torch.zeros(B, dtype=torch.int64, device=dev)
+        # two pinned staging buffers; an event guards reuse (a graph replay
+        # returns at once, so the next epoch's host write must not race the
+        # previous epoch's pending H2D copy)
+        self.starts_host = [torch.zeros(B, dtype=torch.int64).pin_memory() for _ in range(2)]
+        self.copy_ev = [None, None]
+        self.epochs = 0
+        self.act_win = f(B, self.S, d.action)
+        self.feat = f(T * B, d.enc_hidden)
+        self.z0, self.h0 = f(B, L_), f(B, d.hidden)
+        self.latents, self.hiddens = f(B, H + 1, L_), f(B, H + 1, d.hidden)
+        self.actions, self.mus, self.sigmas = f(B, H, d.action), f(B, H, d.action), f(B, H, d.action)
+        self.rewards, self.continues = f(B, H), f(B, H)
+        self.V_t, self.V_c = f(B, H + 1), f(B, H + 1)
+        self.R = f(B, H)
+        self.R_all = f(self.wsize * B, H) if self.wsize > 1 else self.R
+        self.norm = f(1)
+        self.loss_a = f(1 + B * H)
+        self.g_mu, self.g_sig = f(B, H, d.action), f(B, H, d.action)
+        self.sq = f(2)
+        self.skip = torch.zeros(1, dtype=torch.int32, device=dev)
+        M = B * (H + 1)
+        self.ws_enc = hip.workspace(dev).get("e_enc", L.query("dr_encoder_workspace_bytes", d, T * B))
+        self.ws_obs = hip.workspace(dev).get("e_obs", L.query("dr_observe_workspace_bytes", d, B))
+        self.tape = torch.zeros(L.query("dr_imagine_tape_bytes", d, B, H), dtype=torch.uint8, device=dev)
+        self.ws_im = hip.workspace(dev).get("e_im", L.query("dr_imagine_workspace_bytes", d, B, H))
+        self.ctape = torch.zeros(L.query("dr_critic_tape_bytes", d, M), dtype=torch.uint8, device=dev)
+        self.ws_cr = hip.workspace(dev).get("e_cr", L.query("dr_critic_workspace_bytes", d, B, H))
+        self.rng = hip.rng(dev)
+
+    # ------------------------------------------------------------- the phases
+    def encode_and_warm(self, frames, noise_q=None):
+        """a3 + a2: frames is a dr_frames over (B, T) windows; actions come from
+        self.act_win [B][S][A].  Writes self.z0, self.h0."""
+        d, st = self.d, hip.stream()
+        wm = self.dr.world_model.packed()
+        L.call("dr_encoder_features", d, wm, frames, self.B, self.T, L.ptr(self.feat), L.ptr(self.ws_enc),
+               self.ws_enc.numel(), st)
+        if noise_q is not None:
+            nz = hip.explicit_noise(q=noise_q, device=self.dev)
+        else:
+            nz = L.dr_noise(None, None, self.rng.state.data_ptr(), self.rank * self.B, WARM_STREAM)
+        A = d.action
+        L.call("dr_observe_scan", d, wm, self.B, self.T, L.ptr(self.feat), L.ptr(self.act_win), self.S * A, A, None,
+               None, nz, L.ptr(self.z0), L.ptr(self.h0), None, L.ptr(self.ws_obs), self.ws_obs.numel(), st)
+
+    def imagine(self, eps=None, q=None, deterministic=False):
+        """a7: unroll H steps from (self.z0, self.h0)."""
+        d = self.d
+        if eps is not None or q is not None:
+            nz = hip.explicit_noise(q=q, eps=eps, device=self.dev)
+        else:
+            nz = L.dr_noise(None, None, self.rng.state.data_ptr(), self.rank * self.B, DREAM_STREAM)
+        L.call("dr_imagine_fwd", d, self.dr.world_model.packed(), self.dr.agent.actor_struct(), self.B, self.H,
+               L.ptr(self.z0), L.ptr(self.h0), nz, int(deterministic), L.ptr(self.latents), L.ptr(self.hiddens),
+               L.ptr(self.actions), L.ptr(self.rewards), L.ptr(self.continues), L.ptr(self.mus),
+               L.ptr(self.sigmas), L.ptr(self.tape), L.ptr(self.ws_im), self.ws_im.numel(), hip.stream())
+
+    def returns(self):
+        """target-critic values and lambda returns (Agent.py:156-172)."""
+        ag, d, st = self.dr.agent, self.d, hip.stream()
+        M = self.B * (self.H + 1)
+        L_ = d.rows * d.cols
+        L.call("dr_critic_fwd", d, ag.critic_struct(target=True), M, L.ptr(self.hiddens), d.hidden,
+               L.ptr(self.latents), L_, None, L.ptr(self.V_t), None, L.ptr(self.ws_cr), self.ws_cr.numel(), st)
+        L.call("dr_lambda_returns", self.B, self.H, L.ptr(self.rewards), L.ptr(self.continues), L.ptr(self.V_t),
+               ag.gamma, ag.lambda_, L.ptr(self.R), st)
+
+    def losses_and_grads(self):
+        """update_S, actor loss + BPTT, critic CE backward (Agent.py:96-145)."""
+        ag, d, st = self.dr.agent, self.d, hip.stream()
+        B, H = self.B, self.H
+        M = B * (H + 1)
+        L_ = d.rows * d.cols
+        scale = 1.0 / float(B * self.wsize * H)
+        L.call("dr_critic_fwd", d, ag.critic_struct(), M, L.ptr(self.hiddens), d.hidden, L.ptr(self.latents), L_,
+               None, L.ptr(self.V_c), L.ptr(self.ctape), None, 0, st)
+        L.call("dr_update_S", self.R_all.numel(), L.ptr(self.R_all), L.ptr(ag.S_dev), L.ptr(self.norm), None, 0, st)
+        L.call("dr_actor_loss_grad", B, H, d.action, L.ptr(self.mus), L.ptr(self.sigmas), L.ptr(self.actions),
+               L.ptr(self.R), L.ptr(self.V_c), L.ptr(self.norm), ag.nu, scale, L.ptr(self.loss_a), L.ptr(self.g_mu),
+               L.ptr(self.g_sig), st)
+        L.call("dr_critic_loss_bwd", d, ag.critic_struct(), B, H, L.ptr(self.hiddens), L.ptr(self.latents),
+               L.ptr(self.R), L.ptr(self.ctape), scale, L.ptr(ag.loss_slot(1)), ag.critic_struct(grad=True),
+               L.ptr(self.ws_cr), self.ws_cr.numel(), st)
+        L.call("dr_imagine_bwd", d, self.dr.world_model.packed(), ag.actor_struct(), B, H, L.ptr(self.latents),
+               L.ptr(self.hiddens), L.ptr(self.actions), L.ptr(self.g_mu), L.ptr(self.g_sig), None, None, None,
+               L.ptr(self.tape), ag.actor_struct(grad=True), L.ptr(self.ws_im), self.ws_im.numel(), st)
+        ag.loss_slot(0).copy_(self.loss_a[0:1])
+
+    def optimise(self):
+        """non-finite skip, clip_grad_norm_(100) x2, AdamW x2, soft target (Agent.py:137-153)."""
+        self.dr.agent.fused_optimiser_step(self.sq, self.skip)
+
+    def epoch_body(self):
+        frames = self.dr.buffer.frames_struct(self.starts)
+        self.dr.buffer.gather_actions(self.starts, self.act_win)
+        self.encode_and_warm(frames)
+        self.imagine()
+        self.returns()
+        if self.wsize > 1:
+            self._allgather_R()
+        self.losses_and_grads()
+        if self.wsize > 1:
+            self._allreduce_grads()
+        self.optimise()
+        L.call("dr_rng_advance", self.rng.state.data_ptr(), 1, hip.stream())
+
+    # ------------------------------------------------------------------ DP
+    def _allgather_R(self):
+        import torch.distributed as dist
+        parts = list(self.R_all.view(self.wsize, self.B, self.H).unbind(0))
+        dist.all_gather(parts, self.R, group=self.world[2])
+
+    def _allreduce_grads(self):
+        import torch.distributed as dist
+        ag = self.dr.agent
+        dist.all_reduce(ag.grad_buffer, op=dist.ReduceOp.SUM, group=self.world[2])
+        ag.loss_buffer.div_(self.wsize)
+
+    # ----------------------------------------------------------------- driver
+    def run(self, starts_np):
+        """One train_Agent epoch from host window starts; returns the device
+        loss slots (actor, critic)."""
+        i = self.epochs & 1
+        if self.copy_ev[i] is not None:
+            self.copy_ev[i].synchronize()
+        self.starts_host[i].copy_(torch.from_numpy(np.asarray(starts_np, dtype=np.int64)))
+        self.starts.copy_(self.starts_host[i], non_blocking=True)
+        self.copy_ev[i] = torch.cuda.Event()
+        self.copy_ev[i].record()
+        self.epochs += 1
+        ag = self.dr.agent
+        key = (ag.params_key(), self.dr.world_model.params_key(), self.dr.buffer.device_key())
+        if self.use_graph:
+            if self.graph is None or self.graph_key != key:
+                self._capture(key)
+            self.graph.replay()
+        else:
+            self.epoch_body()
+        return ag.loss_slot(0), ag.loss_slot(1)
+
+    def _capture(self, key):
+        # record one epoch into a graph (capture does not execute it; the
+        # caller replays it right after)
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                self.epoch_body()
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        self.graph, self.graph_key = g, key

@@ -1,0 +1,99 @@
+"""Glue between the reference-shaped nn.Modules and libdreamer_hip: packs
+parameters (in PyTorch's own layout, no copies) into the C structs, owns
+per-device workspaces and the Philox RNG state."""
+import threading
+
+import torch
+
+from . import _lib as L
+
+_tls = threading.local()
+
+
+def linear(mod):
+    """dr_linear for an nn.Linear / nn.LayerNorm (None -> NULL)."""
+    if mod is None:
+        return L.dr_linear(None, None)
+    return L.dr_linear(L.ptr(mod.weight), L.ptr(mod.bias))
+
+
+def mlp3(seq):
+    """dr_mlp3 for Sequential(Linear, LN, SiLU, Linear, LN, SiLU, Linear)."""
+    return L.dr_mlp3(linear(seq[0]), linear(seq[1]), linear(seq[3]), linear(seq[4]), linear(seq[6]))
+
+
+def flat_linear(flat, offsets, key_w, key_b):
+    base = flat.data_ptr()
+    return L.dr_linear(base + 4 * offsets[key_w], base + 4 * offsets[key_b])
+
+
+class Workspace:
+    """Grow-only scratch buffers on one device, keyed by name."""
+
+    def __init__(self, device):
+        self.device = device
+        self.bufs = {}
+
+    def get(self, name, nbytes):
+        nbytes = max(int(nbytes), 256)
+        b = self.bufs.get(name)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self.bufs[name] = b
+        return b
+
+
+_ws = {}
+
+
+def workspace(device):
+    key = torch.device(device).index or 0
+    if key not in _ws:
+        _ws[key] = Workspace(torch.device("cuda", key))
+    return _ws[key]
+
+
+class Rng:
+    """Device Philox state {seed, offset} (uint64 x2).  The seed is drawn from
+    torch's CPU generator so torch.manual_seed controls it; each call site
+    gets a fresh 32-bit stream id."""
+
+    def __init__(self, device):
+        seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+        self.state = torch.tensor([seed, 0], dtype=torch.int64, device=device)
+        self.counter = 1
+
+    def reseed(self, seed):
+        self.state.copy_(torch.tensor([seed, 0], dtype=torch.int64))
+
+    def noise(self, row0=0):
+        self.counter = (self.counter + 1) & 0x3FFFFFFF
+        return L.dr_noise(None, None, self.state.data_ptr(), row0, self.counter << 1)
+
+
+_rngs = {}
+
+
+def rng(device):
+    key = torch.device(device).index or 0
+    if key not in _rngs:
+        _rngs[key] = Rng(torch.device("cuda", key))
+    return _rngs[key]
+
+
+def explicit_noise(q=None, eps=None, device=None):
+    """dr_noise reading caller-supplied variates (parity mode)."""
+    st = rng(device).state.data_ptr() if device is not None else None
+    return L.dr_noise(L.ptr(q) if q is not None else None, L.ptr(eps) if eps is not None else None, st, 0, 0)
+
+
+def stream():
+    return L.stream_ptr()
+
+
+def needs_torch_grad(*mods):
+    """True when autograd through these modules' parameters is requested
+    (the world-model training step, which stays PyTorch-ROCm this round)."""
+    if not torch.is_grad_enabled():
+        return False
+    return any(p.requires_grad for m in mods for p in m.parameters())

@@ -1,0 +1,222 @@
+/*
+ * libdreamer_hip -- C ABI of the MI355X (gfx950) Dreamer imagination engine.
+ *
+ * The reference (youngers2006/Dreamer) has no FFI: its hot path is a
+ * composition of PyTorch ops inside Python classes.  Each entry point below
+ * replaces one of those compositions and cites the reference code it
+ * restates (file:line in /root/reference).  The Python package
+ * ``dreamer_amd`` binds them with ctypes behind the reference's own class API
+ * (Dreamer / WorldModel / Agent / Buffer ...).
+ *
+ * Conventions
+ *  - every function returns 0 (DR_OK) or an error code; dr_last_error() gives
+ *    a thread-local message.  Nothing throws across the ABI.
+ *  - all pointers are device pointers owned by the caller (the PyTorch caching
+ *    allocator); the library never allocates, frees, or keeps a pointer after
+ *    returning.  Scratch comes from the caller's workspace (sizes from the
+ *    *_bytes queries).
+ *  - calls are asynchronous on the given hipStream_t; no implicit sync, so the
+ *    whole train_Agent epoch can be captured into one hipGraph.
+ *  - parameters are read in PyTorch's own layouts (Linear weight [out][in],
+ *    GRUCell weight_ih [3H][in] gate order r,z,n, Conv2d [out][in][4][4]).
+ *  - arithmetic is fp32 (parity mode): GEMMs use the exact-f32 MFMA
+ *    (v_mfma_f32_16x16x4_f32), elementwise code is built -ffp-contract=off.
+ */
+#ifndef DREAMER_HIP_H
+#define DREAMER_HIP_H
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DR_OK 0
+#define DR_E_INVALID 1001   /* bad dims / pointers */
+#define DR_E_HIP 1002       /* a HIP launch failed */
+#define DR_E_WORKSPACE 1003 /* workspace too small */
+
+/* Linear (or LayerNorm) parameters: w [out][in] (LN: gamma [n]), b [out]. */
+typedef struct { float* w; float* b; } dr_linear;
+
+/* nn.Sequential(Linear, LayerNorm, SiLU, Linear, LayerNorm, SiLU, Linear)
+ * indices 0,1,3,4,6 (DynamicsPredictors.py:15-23,52-60,85-93; Agent.py:219-227). */
+typedef struct { dr_linear l0, n1, l3, n4, l6; } dr_mlp3;
+
+/* Model widths (Dreamer.py:20-64 config keys). */
+typedef struct {
+  int hidden;          /* hidden_state_dims (600) */
+  int rows, cols;      /* latent_state_dims (32, 32) */
+  int action;          /* action_dims (3) */
+  int img_h, img_w;    /* observation_dims (64, 64) */
+  int enc_f1, enc_f2;  /* encoder_filter_num_1/2 (32, 64): conv channels f1, f2, 2*f2, 4*f2 */
+  int enc_hidden;      /* encoder_hidden_layer_nodes (200) */
+  int prior_h1, prior_h2, rew_h1, rew_h2, cont_h1, cont_h2;
+  int actor_h1, actor_h2, critic_h1, critic_h2;
+  int buckets;         /* critic_reward_buckets (255) */
+} dr_dims;
+
+/* WorldModel parameters (WorldModel.py:55-60). */
+typedef struct {
+  dr_linear conv[4];              /* encoder.feature_extractor.{0,2,4,6} */
+  dr_linear map0, map1, map3;     /* encoder.latent_mapper.{0, 1 (LN), 3} */
+  float *w_ih, *w_hh, *b_ih, *b_hh; /* sequence_model.GRU */
+  dr_mlp3 prior;                  /* dynamics_predictor.logit_net */
+  dr_mlp3 reward;                 /* reward_predictor.logit_net */
+  dr_mlp3 cont;                   /* continue_predictor.logit_generator */
+  float* buckets_rew;             /* reward_predictor.buckets_rew */
+} dr_world_model;
+
+/* Actor (Agent.py:174-200): base_net.{0,1,3,4}, mu_head, log_sig_head. */
+typedef struct { dr_linear l0, n1, l3, n4, mu, ls; } dr_actor;
+
+/* Critic (Agent.py:212-241): value_net, buckets_crit. */
+typedef struct { dr_mlp3 net; float* buckets; } dr_critic;
+
+/* Randomness.  Explicit-noise mode reproduces the reference's draws
+ * (parity); Philox mode generates them in-kernel keyed by
+ * (seed, offset, stream, global row, element) so a data-parallel shard draws
+ * exactly what the single-GPU run draws for the same global rows. */
+typedef struct {
+  const float* q;   /* Exp(1) variates [steps][rows*R][C] (Categorical sample), or NULL */
+  const float* eps; /* N(0,1) variates [steps][rows][A] (actor rsample), or NULL */
+  const unsigned long long* rng; /* device {seed, offset}; used where q/eps are NULL */
+  int row0;         /* global index of local row 0 */
+  int stream;       /* Philox stream id (distinct per call site) */
+} dr_noise;
+
+/* Source of observation frames for the encoder.  Frame f = t*B + b. */
+typedef struct {
+  const unsigned char* ring; /* u8 replay ring [cap][3][H][W] (Buffer.py:7), or NULL */
+  long long ring_cap;
+  const long long* starts;   /* device [B] window starts (Buffer.py:36-50) */
+  const float* obs;          /* f32 frames (when ring == NULL) */
+  long long stride_b, stride_t; /* f32: element offset of frame (b,t) = b*stride_b + t*stride_t */
+  int raw255;                /* 1: values are 0..255 -> x/255-0.5 (Dreamer.py:251); 0: already normalised */
+} dr_frames;
+
+const char* dr_last_error(void);
+int dr_version(void);
+
+/* ---- a3  Encoder conv stack + latent_mapper.0 feature columns ---------------
+ * feat[f][enc_hidden] = flatten(SiLU(conv4(...SiLU(conv1(frame f)))))
+ *                       . map0.w[:, :F]^T + map0.b            (VAE.py:57-75)
+ * for the n = B*T frames of `src` (time-major: f = t*B + b). */
+size_t dr_encoder_workspace_bytes(const dr_dims* d, int n_frames);
+int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, const dr_frames* src, int B, int T,
+                        float* feat, void* ws, size_t ws_bytes, hipStream_t stream);
+
+/* ---- a2/a5  posterior scan (warm_start_generator, Dreamer.py:244-262;
+ *      observe_step, WorldModel.py:79-82; Encoder.encode, VAE.py:77-99) -----
+ * If z_init == NULL, frame 0 is an encode from h_init (zeros if NULL) and
+ * frame t>=1 runs GRU(z, actions[t-1], h) first.  If z_init != NULL every
+ * frame t runs GRU(z, actions[t], h) first.  actions element (b,t,i) is at
+ * actions[b*act_sb + t*act_st + i].  Writes the last frame's z, h (and
+ * logits if non-NULL). */
+size_t dr_observe_workspace_bytes(const dr_dims* d, int B);
+int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B, int T, const float* feat,
+                    const float* actions, long long act_sb, long long act_st, const float* h_init,
+                    const float* z_init, dr_noise noise, float* z_out, float* h_out, float* logits_out,
+                    void* ws, size_t ws_bytes, hipStream_t stream);
+
+/* ---- a7  imagination unroll (dream_episodes, Dreamer.py:143-175) -----------
+ * Outputs use the reference's layouts: latents [B][H+1][R*C], hiddens
+ * [B][H+1][hidden], actions/mus/sigmas [B][H][A], rewards/continues [B][H].
+ * `tape` (dr_imagine_tape_bytes) keeps what dr_imagine_bwd needs. */
+size_t dr_imagine_tape_bytes(const dr_dims* d, int B, int H);
+size_t dr_imagine_workspace_bytes(const dr_dims* d, int B, int H);
+int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const dr_actor* actor, int B, int H,
+                   const float* z0, const float* h0, dr_noise noise, int deterministic, float* latents,
+                   float* hiddens, float* actions, float* rewards, float* continues, float* mus,
+                   float* sigmas, void* tape, void* ws, size_t ws_bytes, hipStream_t stream);
+
+/* Backprop through the unroll for the actor (Agent.py:141-145 backward):
+ * given dL/dmus, dL/dsigmas (and optionally dL/dactions, dL/dlatents,
+ * dL/dhiddens; NULL = 0), writes dL/d(actor params) into `grad` (overwrite).
+ * World-model weights receive no gradient (the reference's WM grads from this
+ * path are discarded by WorldModel.training_step's zero_grad, WorldModel.py:195). */
+int dr_imagine_bwd(const dr_dims* d, const dr_world_model* wm, const dr_actor* actor, int B, int H,
+                   const float* latents, const float* hiddens, const float* actions, const float* g_mus,
+                   const float* g_sigmas,
+                   const float* g_actions, const float* g_latents, const float* g_hiddens,
+                   const void* tape, const dr_actor* grad, void* ws, size_t ws_bytes, hipStream_t stream);
+
+/* ---- single steps (batch-1 acting path and per-block API) ------------------ */
+/* imagine_step (WorldModel.py:72-77): h' = GRU(z,h,a); z' ~ prior(h'); r; c */
+int dr_imagine_step(const dr_dims* d, const dr_world_model* wm, int B, const float* h, const float* z,
+                    const float* a, dr_noise noise, float* h_out, float* z_out, float* r_out, float* c_out,
+                    void* ws, size_t ws_bytes, hipStream_t stream);
+/* Actor.act (Agent.py:202-210) */
+int dr_actor_act(const dr_dims* d, const dr_actor* actor, int B, const float* h, const float* z,
+                 dr_noise noise, int deterministic, float* a_out, float* mu_out, float* sigma_out, void* ws,
+                 size_t ws_bytes, hipStream_t stream);
+/* GRU cell (SequenceModel.py:19-24) */
+int dr_gru_cell(const dr_dims* d, const dr_world_model* wm, int B, const float* z, const float* h,
+                const float* a, float* h_out, void* ws, size_t ws_bytes, hipStream_t stream);
+/* Categorical sampler with unimix + straight-through value (VAE.py:88-98,
+ * DynamicsPredictors.py:33-39): z = onehot(argmax(p_hat/q)) + p - p (value). */
+int dr_categorical_sample(int M, int R, int C, const float* logits, dr_noise noise, float* z_out,
+                          int* idx_out, float* soft_out, hipStream_t stream);
+/* heads: prior logits, reward value (symexp E[bucket]), continue prob */
+int dr_mlp3_fwd(const dr_mlp3* m, int M, int in_h, const float* h, long long ldh, int in_z, const float* z,
+                long long ldz, int h1, int h2, int n_out, float* out, long long ldo, void* ws, size_t ws_bytes,
+                hipStream_t stream);
+size_t dr_step_workspace_bytes(const dr_dims* d, int B);
+int dr_bucket_value(int M, int nb, const float* logits, const float* buckets, float* out, hipStream_t stream);
+
+/* ---- a13-a16  actor-critic update pieces (Agent.py:78-172) ----------------- */
+size_t dr_critic_tape_bytes(const dr_dims* d, int M);
+size_t dr_critic_workspace_bytes(const dr_dims* d, int B, int H);
+/* logits [M][nb] (optional), values [M] (optional); tape (optional) for bwd */
+int dr_critic_fwd(const dr_dims* d, const dr_critic* c, int M, const float* h, long long ldh, const float* z,
+                  long long ldz, float* logits, float* values, void* tape, void* ws, size_t ws_bytes,
+                  hipStream_t stream);
+/* lambda returns (Agent.py:156-172): V [B][H+1] target values */
+int dr_lambda_returns(int B, int H, const float* r, const float* c, const float* V, float gamma, float lam,
+                      float* R, hipStream_t stream);
+/* update_S (Agent.py:78-88) over n returns; S is a device scalar updated in
+ * place unless R holds NaN/Inf; norm_out = max(S, 1) (Agent.py:120). */
+int dr_update_S(int n, const float* R, float* S, float* norm_out, void* ws, size_t ws_bytes,
+                hipStream_t stream);
+/* actor loss (Agent.py:105-125) and its gradient wrt mus/sigmas; loss_out
+ * holds 1 + B*H floats: [0] = mean loss over the B*H local rows, the rest is
+ * per-row scratch.  scale = dL/d(row loss) (1/(B*H) on one device). */
+int dr_actor_loss_grad(int B, int H, int A, const float* mus, const float* sigmas, const float* actions,
+                       const float* R, const float* V, const float* norm, float nu, float scale,
+                       float* loss_out, float* g_mus, float* g_sigmas, hipStream_t stream);
+/* critic two-hot cross-entropy (Agent.py:127-135) + backward into `grad`
+ * (overwrite); rows are (b,t) with t<=H of hiddens/latents; row t=H is unused. */
+int dr_critic_loss_bwd(const dr_dims* d, const dr_critic* c, int B, int H, const float* hiddens,
+                       const float* latents, const float* R, const void* tape, float scale, float* loss_out,
+                       const dr_critic* grad, void* ws, size_t ws_bytes, hipStream_t stream);
+
+/* ---- optimiser (torch.optim.AdamW + clip_grad_norm_ + soft target) -------- */
+int dr_sqnorm(long long n, const float* g, float* acc, hipStream_t stream);
+/* p <- AdamW(p, g*clip) (torch.optim.AdamW single-tensor op order) where
+ * clip = min(1, max_norm/(sqrt(*sqnorm)+1e-6)) (sqnorm NULL: no clip).  The
+ * step counter lives on the device: a prelude increments *step and writes
+ * hyper[0] = lr/(1-b1^step), hyper[1] = sqrt(1-b2^step) (double math, like
+ * torch's python scalars).  g is scaled in place by clip (as clip_grad_norm_
+ * does).  Everything is skipped when *skip != 0. */
+int dr_adamw(long long n, float* p, float* g, float* m, float* v, const float* sqnorm, float max_norm,
+             float lr, float b1, float b2, float eps, float wd, int* step, float* hyper, const int* skip,
+             hipStream_t stream);
+int dr_ema(long long n, float* target, const float* src, float keep, float tau, const int* skip,
+           hipStream_t stream);
+/* non-finite flag: *flag = any(!isfinite(x[0..n))) (OR-accumulate) */
+int dr_nonfinite(long long n, const float* x, int* flag, hipStream_t stream);
+
+/* ---- a1  replay gather (Buffer.sample_sequences, Buffer.py:49-61) --------- */
+int dr_replay_gather(long long cap, int B, int S, int frame_elems, int A, const unsigned char* frames,
+                     const float* actions, const float* rewards, const float* continues,
+                     const long long* starts, float* obs_out, float* act_out, float* rew_out,
+                     float* cont_out, hipStream_t stream);
+
+/* Philox offset bump (keeps graph replays drawing fresh noise) */
+int dr_rng_advance(unsigned long long* rng, unsigned long long delta, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

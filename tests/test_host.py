@@ -1,0 +1,123 @@
+"""Host-side checks that need no GPU: the C ABI library loads and exports
+every entry point include/dreamer_hip.h declares, the modules reproduce the
+reference's state_dict layout, the Buffer reproduces the reference's sampling
+RNG consumption, and the reference module names import."""
+import os
+import re
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO, load_fixture, state_layout
+from formula import FULL, SMALL
+from oracle import dreamer_oracle as O
+
+
+def _header_symbols():
+    src = open(os.path.join(REPO, "include", "dreamer_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dr_[A-Za-z0-9_]+)\s*\(", src)))
+
+
+def test_abi_exports_every_declared_symbol():
+    from dreamer_amd import _lib
+    lib = _lib.load()
+    declared = _header_symbols()
+    assert len(declared) > 20
+    missing = [s for s in declared if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(declared) == set(_lib.EXPORTED), set(declared) ^ set(_lib.EXPORTED)
+    assert lib.dr_version() == 1
+
+
+def test_workspace_queries_need_no_gpu():
+    from dreamer_amd import _lib as L
+    from dreamer_amd import Dreamer
+    d = Dreamer(dict(FULL), torch.device("cpu"))
+    dims = d.world_model.dims(d.agent)
+    assert dims.hidden == 600 and dims.rows == 32 and dims.enc_hidden == 200 and dims.critic_h2 == 200
+    assert L.query("dr_imagine_tape_bytes", dims, 64, 15) > 64 * 15 * 600 * 4 * 4
+    assert L.query("dr_encoder_workspace_bytes", dims, 2048) > 2048 * 32 * 32 * 32 * 4
+
+
+@pytest.mark.parametrize("which,cfg", [("small", SMALL), ("full", FULL)])
+def test_state_dict_layout_matches_reference(which, cfg):
+    from dreamer_amd import Dreamer
+    d = Dreamer(dict(cfg), torch.device("cpu"))
+    assert [(k, tuple(v.shape)) for k, v in d.state_dict().items()] == state_layout(which)
+
+
+def test_reference_checkpoint_round_trip(tmp_path):
+    """A reference-format state_dict loads (weights_only) and flat views survive."""
+    from dreamer_amd import Dreamer
+    fx = load_fixture("small_epoch")
+    d = Dreamer(dict(SMALL), torch.device("cpu"))
+    sd = {k: torch.from_numpy(fx["param_" + k].copy()) for k, _ in state_layout("small")}
+    torch.save(sd, tmp_path / "ref.pth")
+    d.load_pretrained_dreamer(str(tmp_path / "ref.pth"))
+    for k, v in d.state_dict().items():
+        assert torch.equal(v, sd[k]), k
+    assert d.agent.fa.intact() and d.agent.fc.intact() and d.agent.ft.intact()
+    d.save_trained_Dreamer(str(tmp_path / "mine.pth"))
+    back = torch.load(str(tmp_path / "mine.pth"), weights_only=True)
+    assert all(torch.equal(back[k], sd[k]) for k in sd)
+
+
+def test_buffer_sampling_semantics():
+    """Buffer.sample_start_indices == reference Buffer.sample_sequences' starts
+    (fixture recorded from the reference, including the straddle redraw)."""
+    from dreamer_amd import Buffer
+    for name in ("small_epoch", "full_epoch"):
+        fx = load_fixture(name)
+        cap = int(fx["buf_capacity"])
+        b = Buffer(cap, int(fx["cfg_S"]), int(fx["cfg_A"]), fx["buf_frames"].shape[2:])
+        b.load_arrays(fx["buf_frames"], fx["buf_actions"], fx["buf_rewards"], fx["buf_continues"])
+        b.size, b.next_idx = int(fx["buf_size"]), int(fx["buf_next_idx"])
+        np.random.seed(int(fx["np_seed"]))
+        assert np.array_equal(b.sample_start_indices(int(fx["cfg_B"])), fx["starts"])
+        # host sample_sequences on CPU returns the reference's windows
+        np.random.seed(int(fx["np_seed"]))
+        obs, act, rew, cont, S = b.sample_sequences(int(fx["cfg_B"]))
+        idx = (fx["starts"][:, None] + np.arange(S)[None, :]) % cap
+        assert torch.equal(obs, torch.tensor(fx["buf_frames"][idx], dtype=torch.float32))
+
+
+def test_add_to_buffer_symlog_and_wrap():
+    from dreamer_amd import Buffer
+    b = Buffer(4, 2, 3, (16, 16))
+    for i in range(6):
+        b.add_to_buffer(np.full((3, 16, 16), i, np.uint8), np.ones(3) * i, float(i) - 2.5, 1 - (i == 3))
+    assert b.size == 4 and b.next_idx == 2
+    assert b.observation_buffer[0, 0, 0, 0] == 4 and b.observation_buffer[3, 0, 0, 0] == 3
+    np.testing.assert_allclose(b.reward_buffer[1, 0], O.symlog(torch.tensor(5 - 2.5)).item(), rtol=1e-6)
+    assert b.continue_buffer[3, 0] == 0.0
+
+
+def test_reference_module_names_import():
+    sys.path.insert(0, os.path.join(REPO, "dreamer_amd", "refapi"))
+    try:
+        import Adaptors, Agent, Buffer, Dreamer, DreamerUtils, DynamicsPredictors  # noqa: F401
+        import SequenceModel, VariationalAutoEncoder, WorldModel  # noqa: F401
+        assert Dreamer.Dreamer.__module__ == "dreamer_amd.dreamer"
+        assert hasattr(DreamerUtils, "_sanitize_for_save")
+        arr = DreamerUtils._sanitize_for_save([torch.tensor(1.5), torch.tensor(2.0), 4.0])
+        assert arr.tolist() == [1.5, 2.0, 4.0]
+        arr = DreamerUtils._sanitize_for_save([[torch.tensor(1.0), 2.0], [torch.tensor(3.0), 4.0]])
+        assert arr.shape == (2, 2)
+    finally:
+        sys.path.remove(os.path.join(REPO, "dreamer_amd", "refapi"))
+
+
+def test_hot_path_refuses_cpu_tensors():
+    """No CPU fallback: hot-path calls on CPU tensors raise."""
+    from dreamer_amd import Dreamer
+    d = Dreamer(dict(SMALL), torch.device("cpu"))
+    h = torch.zeros(2, 1, SMALL["hidden_state_dims"])
+    z = torch.zeros(2, 1, 8, 8)
+    a = torch.zeros(2, 1, 3)
+    with torch.no_grad(), pytest.raises(RuntimeError, match="GPU"):
+        d.world_model.imagine_step(h, z, a)
+    with pytest.raises(RuntimeError, match="GPU"):
+        d.dream_episodes(z, h)
