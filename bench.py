@@ -1,0 +1,242 @@
+"""Benchmark: imagined latent-steps/sec (B x H) of Dreamer.train_Agent epochs
+on MI355X (BASELINE.json metric), 64x64x3 CarRacing-shaped synthetic replay.
+
+  python bench.py [--gpus N --steps K --warmup W --batch B --seq S --horizon H]
+
+Multi-GPU: launched by torch.distributed.run, one process per GPU; weak
+scaling (B rows per GPU), RCCL all-gather of lambda returns + one all-reduce
+of the flat [actor|critic|loss] gradient buffer per epoch.  Rank 0 prints ONE
+JSON line.  The CPU baseline (rank 0, N=1 only) times the oracle's
+reference-faithful CPU restatement on a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "imagined latent-steps/sec (B×H) at 64×64 CarRacing, 1/2/4/8 MI355X"
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 = f32 vector peak
+HBM_PEAK_GBS = 8000.0
+
+CAR_RACER = dict(
+    hidden_state_dims=600, latent_state_dims=[32, 32], action_dims=3, observation_dims=[64, 64],
+    encoder_filter_num_1=32, encoder_filter_num_2=64, encoder_hidden_layer_nodes=200,
+    decoder_filter_num_1=32, decoder_filter_num_2=64, decoder_hidden_layer_nodes=200,
+    dyn_pred_hidden_num_nodes_1=200, dyn_pred_hidden_num_nodes_2=200,
+    rew_pred_hidden_num_nodes_1=200, rew_pred_hidden_num_nodes_2=200,
+    cont_pred_hidden_num_nodes_1=200, cont_pred_hidden_num_nodes_2=200,
+    hidden_layer_actor_1_size=200, hidden_layer_actor_2_size=200,
+    hidden_layer_critic_1_size=200, hidden_layer_critic_2_size=200, device="cuda",
+    horizon=15, batch_size=64, nu=0.0003, lambda_=0.95, gamma=0.99, buffer_size=200000,
+    sequence_length=64, seed=42, training_iterations=10000, random_iterations=500,
+    actor_lr=0.00008, actor_betas=[0.9, 0.999], actor_eps=0.00001, critic_lr=0.0001,
+    critic_betas=[0.9, 0.999], critic_eps=0.00001, AC_epochs=1, world_model_lr=0.0001,
+    world_model_betas=[0.9, 0.999], world_model_eps=0.00001, WM_epochs=1,
+    beta_prediction=1.0, beta_dynamics=0.5, beta_representation=0.1, critic_reward_buckets=255,
+    env_id="CarRacing-v3",
+)
+
+
+def synthetic_replay(n, hw, A, seed=0):
+    """u8 frames, U(-1,1) actions, N(0,1) rewards (symlog'ed as
+    add_to_buffer does), continues 1 except every 1000th."""
+    rng = np.random.default_rng(seed)
+    frames = rng.integers(0, 256, size=(n, 3, hw[0], hw[1]), dtype=np.uint8)
+    acts = rng.uniform(-1, 1, size=(n, A)).astype(np.float32)
+    r = rng.standard_normal(size=(n,)).astype(np.float32)
+    rews = (np.sign(r) * np.log(1.0 + np.abs(r))).astype(np.float32)
+    conts = np.ones((n,), dtype=np.float32)
+    conts[::1000] = 0.0
+    return frames, acts, rews, conts
+
+
+def encoder_flops_per_frame(c):
+    """Algorithmic FLOPs of the conv stack + latent_mapper.0 feature columns
+    for one 64x64 frame (dense conv FLOPs; SURVEY §8d counting)."""
+    ch = [3, c["encoder_filter_num_1"], c["encoder_filter_num_2"], 2 * c["encoder_filter_num_2"],
+          4 * c["encoder_filter_num_2"]]
+    h, w = c["observation_dims"]
+    fl = 0
+    for i in range(4):
+        h, w = h // 2, w // 2
+        fl += 2 * h * w * ch[i + 1] * ch[i] * 16
+    F = ch[4] * h * w
+    return fl + 2 * F * c["encoder_hidden_layer_nodes"]
+
+
+def cpu_baseline(cfg, B, S, H, budget_s=15.0, threads=None):
+    """Reference-faithful CPU epoch (oracle restatement of Dreamer.train_Agent:
+    warm start with the un-detached graph, dream, train_step with backward into
+    everything, AdamW, EMA) timed on the host cores."""
+    from oracle import dreamer_oracle as O
+    from dreamer_amd import Dreamer
+    threads = threads or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    c = dict(cfg)
+    c.update(device="cpu", batch_size=B, sequence_length=S, horizon=H)
+    torch.manual_seed(0)
+    d = Dreamer(c, torch.device("cpu"))
+    P = {k: v.detach().clone().requires_grad_(v.dtype == torch.float32 and "buckets" not in k)
+         for k, v in d.state_dict().items()}
+    R, C = c["latent_state_dims"]
+    A = c["action_dims"]
+    frames, acts, rews, conts = synthetic_replay(max(4096, 8 * S), c["observation_dims"], A, seed=0)
+    rng = np.random.default_rng(1)
+    actor = [P["agent." + k] for k in O.ACTOR_KEYS]
+    critic = [P["agent." + k] for k in O.CRITIC_KEYS]
+    m = {id(p): (torch.zeros_like(p), torch.zeros_like(p)) for p in actor + critic}
+    S_val = 1.0
+
+    def epoch(step):
+        nonlocal S_val
+        st = rng.integers(0, len(frames) - S, size=B)
+        idx = st[:, None] + np.arange(S)[None, :]
+        obs = torch.tensor(frames[idx], dtype=torch.float32)
+        act = torch.tensor(acts[idx])
+        qw = torch.empty(S // 2, B * R, C).exponential_()
+        z0, h0 = O.warm_start(obs, act, S, P, qw, R, C)
+        eps = torch.randn(H, B, 1, A)
+        q = torch.empty(H, B * R, C).exponential_()
+        z, h, a, r, cc, mu, sg = O.dream(z0, h0, P, eps, q, H, R, C)
+        la, lc, Rl, S_val = O.ac_losses(z, h, r, cc, a, mu, sg, P, S_val)
+        for p in actor + critic:
+            p.grad = None
+        lc.backward()
+        la.backward()  # traverses the dream AND the warm-start graph, as the reference does
+        for ps, lr in ((critic, 1e-4), (actor, 8e-5)):
+            gs, _ = O.clip_grad_norm([p.grad for p in ps])
+            with torch.no_grad():
+                for p, g in zip(ps, gs):
+                    mm, vv = m[id(p)]
+                    pn, mn, vn = O.adamw_step(p, g, mm, vv, step, lr)
+                    p.copy_(pn); mm.copy_(mn); vv.copy_(vn)
+        with torch.no_grad():
+            for k in O.CRITIC_KEYS:
+                t = P["agent.target_" + k]
+                t.mul_(0.98).add_(0.02 * P["agent." + k])
+
+    epoch(1)  # warm-up (not timed)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        epoch(2 + n)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 50:
+            break
+    return dict(value=B * H * n / el, unit="imagined latent-steps/s", cores=threads, kind="port",
+                sample=f"{n} reference-faithful train_Agent epochs (oracle CPU restatement, fp32, warm-start "
+                       f"backward included) at B={B} S={S} H={H} 64x64x3, {el:.1f} s on {threads} threads")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="imagination rows per GPU (configs[1]: 64)")
+    ap.add_argument("--seq", type=int, default=64)
+    ap.add_argument("--horizon", type=int, default=15)
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--phases", action="store_true", help="print per-phase ms to stderr")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+        group = dist.group.WORLD
+
+    from dreamer_amd import Dreamer
+    from dreamer_amd.engine import ImaginationEngine
+    B, S, H = args.batch, args.seq, args.horizon
+    cfg = dict(CAR_RACER)
+    cfg.update(batch_size=B, sequence_length=S, horizon=H)
+    torch.manual_seed(0)
+    d = Dreamer(cfg, dev)
+    n_rep = max(4096, 8 * S)
+    fr, ac, rw, ct = synthetic_replay(n_rep, cfg["observation_dims"], cfg["action_dims"], seed=0)
+    d.buffer.load_arrays(fr, ac, rw, ct)
+    d.buffer._mirror()
+    eng = ImaginationEngine(d, B=B, world=(rank, world, group) if world > 1 else None)
+    d._engine = eng
+    np.random.seed(1000 + rank)
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        eng.run(d.buffer.sample_start_indices(B))
+    barrier()
+    t0 = time.perf_counter()
+    enc_ms, phase_tot = [], {}
+    for _ in range(args.steps):
+        eng.run(d.buffer.sample_start_indices(B), timing=True)
+        torch.cuda.current_stream().synchronize() if args.phases else None
+        if args.phases:
+            ph = eng.phase_ms()
+            for k, v in ph.items():
+                phase_tot[k] = phase_tot.get(k, 0.0) + v
+    barrier()
+    el = time.perf_counter() - t0
+    # live HIP-event time of the dominant phase (conv encoder) over the timed region
+    # is recomputed from the recorded events of the last epoch when --phases is off
+    if not args.phases:
+        ph = eng.phase_ms()
+        phase_tot = {k: v * args.steps for k, v in ph.items()}
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    la, lc = float(d.agent.loss_buffer[0]), float(d.agent.loss_buffer[1])
+    if rank != 0:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
+    value = world * B * H * args.steps / el
+    frames = B * (S // 2)
+    enc_flops = encoder_flops_per_frame(cfg) * frames
+    enc_s = phase_tot["encode"] / args.steps / 1e3
+    achieved = enc_flops / enc_s / 1e12
+    if args.phases:
+        print(json.dumps({k: round(v / args.steps, 4) for k, v in phase_tot.items()}), file=sys.stderr)
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "imagined latent-steps/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"Dreamer.train_Agent epoch (replay sample + warm start S/2 + H-step imagination + "
+                               f"actor-critic update), B={B}/GPU S={S} H={H} 64x64x3 (BASELINE configs[1])",
+                   "global_batch": B * world, "seq_len": S, "horizon": H, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "mfma", "kernel": "encoder conv stack + feature projection (5 launches, phase 'encode')",
+                     "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "algorithmic_flops_per_launch": enc_flops, "phase_ms": round(enc_s * 1e3, 4)},
+        "losses": {"actor": la, "critic": lc},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(CAR_RACER, B, S, H, budget_s=args.cpu_budget)
+    print(json.dumps(out))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -26,17 +26,19 @@ class _Flat:
         named = list(self.module.named_parameters())
         self.names = [n for n, _ in named]
         self.params = [p for _, p in named]
-        n = sum(p.numel() for p in self.params)
-        dev = self.params[0].device
-        self.flat = torch.empty(n, device=dev, dtype=torch.float32)
-        self.offsets = {}
-        off = 0
+        # every parameter starts on a 256-byte boundary (float4 weight rows for
+        # the skinny GEMM); the pad elements stay 0 (zero grad -> AdamW no-op)
+        self.offsets, off = {}, 0
         for name, p in named:
-            k = p.numel()
-            self.flat[off:off + k].copy_(p.data.reshape(-1))
-            p.data = self.flat[off:off + k].view_as(p)
             self.offsets[name] = off
-            off += k
+            off += -(-p.numel() // 64) * 64
+        n = off
+        dev = self.params[0].device
+        self.flat = torch.zeros(n, device=dev, dtype=torch.float32)
+        for name, p in named:
+            o, k = self.offsets[name], p.numel()
+            self.flat[o:o + k].copy_(p.data.reshape(-1))
+            p.data = self.flat[o:o + k].view_as(p)
         self.numel = n
         self.grad = grad_storage if grad_storage is not None else torch.zeros(n, device=dev)
         self.bind_grads()
@@ -228,8 +230,8 @@ class Agent(nn.Module):
 
     # ---- flat buffers --------------------------------------------------------
     def _bind(self):
-        na = sum(p.numel() for p in self.actor.parameters())
-        nc = sum(p.numel() for p in self.critic.parameters())
+        pad = lambda m: sum(-(-p.numel() // 64) * 64 for p in m.parameters())
+        na, nc = pad(self.actor), pad(self.critic)
         self.grad_buffer = torch.zeros(na + nc + 2, device=self.device)
         self.loss_buffer = self.grad_buffer[na + nc:]
         self.fa = _Flat(self.actor, self.grad_buffer[:na])

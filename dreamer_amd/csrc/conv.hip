@@ -1,0 +1,220 @@
+// Encoder convolutions (VariationalAutoEncoder.py:33-42: 4x Conv2d(k4, s2, p1)
+// + SiLU) as NHWC implicit GEMMs on the exact-f32 MFMA.
+//
+//   out[pix][co] = SiLU(bias[co] + sum_{tap, ci} in[f][2oy-1+ky][2ox-1+kx][ci] * Wr[co][tap][ci])
+//
+// Tile BM pixels x BN output channels, K chunk = 32 (a run of channels of one
+// or more taps; CIN % 4 == 0 so every float4 stays inside one tap).  Each
+// thread keeps the (frame, oy, ox) of its pixels in registers for the whole K
+// loop; A/B chunks are double-buffered in LDS with one barrier per chunk.  MFMA
+// fragments are read with ds_read_b128: lane (r, q) takes 4 consecutive k of
+// its row, and the same k permutation is used for A and B, so MFMA step c of
+// a 16-k slice sums k = {c, 4+c, 8+c, 12+c} -- every product is still an
+// exact f32 fma.
+#include "conv.h"
+
+#define CBK 32
+#define CLDS (CBK + 4)  // 144-byte rows: 16-byte aligned float4 slots
+
+template <int BM, int BN, int CIN, bool OUT_NCHW>
+__global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw, int cout,
+                                                   const float* __restrict__ in, const float* __restrict__ wr,
+                                                   const float* __restrict__ bias, float* __restrict__ out) {
+  constexpr int K = CIN * 16;
+  constexpr int APT = BM / 32;  // pixel rows loaded per thread (8 float4 per 32-k row)
+  constexpr int BPT = BN >= 32 ? BN / 32 : 1;
+  constexpr int WN = BN >= 32 ? 2 : 1, WM = 4 / WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
+  static_assert(FM >= 1 && FN >= 1, "conv tile too small");
+  __shared__ __attribute__((aligned(16))) float As[2][BM][CLDS];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN][CLDS];
+
+  const int oh = ih / 2, ow = iw / 2, hw = oh * ow;
+  const long long M = (long long)n_frames * hw;
+  const long long m0 = (long long)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int quad = tid & 7, prow = tid >> 3;  // 8 float4 per 32-k row
+
+  // per-thread pixel coordinates (fixed over the K loop)
+  long long pbase[APT];
+  int piy[APT], pix[APT];
+  bool pvalid[APT];
+#pragma unroll
+  for (int i = 0; i < APT; ++i) {
+    const long long m = m0 + prow + 32 * i;
+    pvalid[i] = m < M;
+    const long long mm = pvalid[i] ? m : 0;
+    const long long f = mm / hw;
+    const int p = (int)(mm - f * hw);
+    const int oy = p / ow, ox = p - oy * ow;
+    pbase[i] = f * ih * iw * CIN;
+    piy[i] = 2 * oy - 1;
+    pix[i] = 2 * ox - 1;
+  }
+
+  float4 ra[APT], rb[BPT];
+  auto load = [&](int k0) {
+    const int k = k0 + 4 * quad;
+    const int tap = k / CIN, ci = k - tap * CIN;
+    const int ky = tap >> 2, kx = tap & 3;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const int y = piy[i] + ky, x = pix[i] + kx;
+      if (pvalid[i] && y >= 0 && y < ih && x >= 0 && x < iw)
+        ra[i] = *reinterpret_cast<const float4*>(in + pbase[i] + ((long long)y * iw + x) * CIN + ci);
+      else
+        ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int co = n0 + prow + 32 * i;
+      rb[i] = (co < cout && prow + 32 * i < BN) ? *reinterpret_cast<const float4*>(wr + (long long)co * K + k)
+                                                : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < APT; ++i) *reinterpret_cast<float4*>(&As[buf][prow + 32 * i][4 * quad]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BPT; ++i)
+      if (prow + 32 * i < BN) *reinterpret_cast<float4*>(&Bs[buf][prow + 32 * i][4 * quad]) = rb[i];
+  };
+
+  const int wm0 = (wave / WN) * WTM, wn0 = (wave % WN) * WTN;
+  const int r = lane & 15, q = lane >> 4;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  store(0);
+  __syncthreads();
+  constexpr int NCH = K / CBK;
+  for (int c = 0; c < NCH; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < NCH) load((c + 1) * CBK);
+#pragma unroll
+    for (int s = 0; s < CBK; s += 16) {
+      float4 a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const float4*>(&As[buf][wm0 + 16 * i + r][s + 4 * q]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const float4*>(&Bs[buf][wn0 + 16 * j + r][s + 4 * q]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+        }
+    }
+    if (c + 1 < NCH) store(buf ^ 1);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long long m = m0 + wm0 + 16 * i + 4 * q + e;
+        const int co = n0 + wn0 + 16 * j + r;
+        if (m >= M || co >= cout) continue;
+        float v = acc[i][j][e] + bias[co];
+        v = v / (1.0f + expf(-v));
+        if (OUT_NCHW) {
+          const long long f = m / hw;
+          out[(f * cout + co) * hw + (m - f * hw)] = v;
+        } else {
+          out[m * cout + co] = v;
+        }
+      }
+}
+
+template <int BM, int BN, int CIN, bool OUT_NCHW>
+static int launch_conv(int n, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
+                       float* out, hipStream_t s) {
+  const long long M = (long long)n * (ih / 2) * (iw / 2);
+  dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((cout + BN - 1) / BN));
+  hipLaunchKernelGGL((k_conv_nhwc<BM, BN, CIN, OUT_NCHW>), grid, dim3(256), 0, s, n, ih, iw, cout, in, wr, bias,
+                     out);
+  return dr_check_launch("conv");
+}
+
+int op_conv_nhwc(int n, int cin, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
+                 float* out, int out_nchw, hipStream_t s) {
+#define DR_CONV_CASE(C)                                                                               \
+  if (cin == C) {                                                                                     \
+    if (cout <= 16) {                                                                                 \
+      if (out_nchw) return launch_conv<128, 16, C, true>(n, ih, iw, cout, in, wr, bias, out, s);      \
+      return launch_conv<128, 16, C, false>(n, ih, iw, cout, in, wr, bias, out, s);                   \
+    }                                                                                                 \
+    if (out_nchw) return launch_conv<128, 64, C, true>(n, ih, iw, cout, in, wr, bias, out, s);        \
+    if (cout % 64 == 0) return launch_conv<128, 64, C, false>(n, ih, iw, cout, in, wr, bias, out, s); \
+    return launch_conv<128, 32, C, false>(n, ih, iw, cout, in, wr, bias, out, s);                     \
+  }
+  DR_CONV_CASE(4)
+  DR_CONV_CASE(8)
+  DR_CONV_CASE(16)
+  DR_CONV_CASE(32)
+  DR_CONV_CASE(64)
+  DR_CONV_CASE(128)
+  DR_CONV_CASE(256)
+#undef DR_CONV_CASE
+  dr_set_error("conv: unsupported input channels %d", cin);
+  return DR_E_INVALID;
+}
+
+// frames (u8 replay ring or f32 tensor, NCHW 3 channels) -> normalised f32
+// NHWC with 4 channels (channel 3 = 0), frame f = t*nb + b.  x/255 - 0.5 is
+// evaluated exactly as the reference does (IEEE div, then sub; Dreamer.py:251).
+__global__ void k_frames_nhwc4(int n, int nb, int h, int w, dr_frames src, float* out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // (f, y, x)
+  const long long hw = (long long)h * w;
+  if (i >= (long long)n * hw) return;
+  const long long f = i / hw;
+  const long long p = i - f * hw;
+  const int b = (int)(f % nb), t = (int)(f / nb);
+  float v[3];
+  if (src.ring) {
+    const unsigned char* fr = src.ring + ((src.starts[b] + t) % src.ring_cap) * 3 * hw;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c] = (float)fr[c * hw + p];
+  } else {
+    const float* fr = src.obs + (long long)b * src.stride_b + (long long)t * src.stride_t;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c] = fr[c * hw + p];
+  }
+  if (src.raw255) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c] = v[c] / 255.0f - 0.5f;
+  }
+  reinterpret_cast<float4*>(out)[i] = make_float4(v[0], v[1], v[2], 0.0f);
+}
+
+int op_frames_nhwc4(int n, int nb, int h, int w, const dr_frames* src, float* out, hipStream_t s) {
+  const long long total = (long long)n * h * w;
+  hipLaunchKernelGGL(k_frames_nhwc4, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, n, nb, h, w, *src, out);
+  return dr_check_launch("frames_nhwc4");
+}
+
+// Conv2d weight [co][ci][4][4] -> [co][tap][cin_pad] (zero-padded channels)
+__global__ void k_conv_repack_pad(int cout, int cin, int cin_pad, const float* w, float* wr) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cout * 16 * cin_pad) return;
+  const int co = i / (16 * cin_pad), rem = i - co * 16 * cin_pad;
+  const int tap = rem / cin_pad, ci = rem - tap * cin_pad;
+  wr[i] = (ci < cin) ? w[((long long)co * cin + ci) * 16 + tap] : 0.0f;
+}
+
+int op_conv_repack_pad(int cout, int cin, int cin_pad, const float* w, float* wr, hipStream_t s) {
+  const int total = cout * 16 * cin_pad;
+  hipLaunchKernelGGL(k_conv_repack_pad, dim3((total + 255) / 256), dim3(256), 0, s, cout, cin, cin_pad, w, wr);
+  return dr_check_launch("conv_repack_pad");
+}

@@ -4,6 +4,7 @@
 // no allocation) so a whole train_Agent epoch can be captured in a hipGraph.
 #include <string.h>
 
+#include "conv.h"
 #include "gemm.h"
 #include "ops.h"
 
@@ -110,16 +111,18 @@ static int run(GemmLayout lay, int amode, const GemmArgs& a, hipStream_t s) { re
 // a3  encoder features
 // ===========================================================================
 struct EncWs {
-  float *a1, *a2, *a3, *a4, *wr2, *wr3, *wr4;
+  float *x0, *a1, *a2, *a3, *a4, *wr1, *wr2, *wr3, *wr4;
 };
 
 static void enc_carve(Carve& c, const dr_dims* d, int n, EncWs& w) {
   const int c1 = d->enc_f1, c2 = d->enc_f2, c3 = 2 * d->enc_f2, c4 = 4 * d->enc_f2;
-  const long long p1 = (long long)(d->img_h / 2) * (d->img_w / 2), p2 = p1 / 4, p3 = p2 / 4, p4 = p3 / 4;
+  const long long p0 = (long long)d->img_h * d->img_w, p1 = p0 / 4, p2 = p1 / 4, p3 = p2 / 4, p4 = p3 / 4;
+  w.x0 = c.f((long long)n * p0 * 4);
   w.a1 = c.f((long long)n * p1 * c1);
   w.a2 = c.f((long long)n * p2 * c2);
   w.a3 = c.f((long long)n * p3 * c3);
   w.a4 = c.f((long long)n * p4 * c4);
+  w.wr1 = c.f((long long)c1 * 4 * 16);
   w.wr2 = c.f((long long)c2 * c1 * 16);
   w.wr3 = c.f((long long)c3 * c2 * 16);
   w.wr4 = c.f((long long)c4 * c3 * 16);
@@ -132,23 +135,11 @@ extern "C" size_t dr_encoder_workspace_bytes(const dr_dims* d, int n_frames) {
   return c.off;
 }
 
-static GemmArgs conv_args(int n, int cin, int ih, int iw, int cout, const float* act_in, const float* w,
-                          const float* b, float* out) {
-  GemmArgs g = gemm_args();
-  g.cin = cin; g.ih = ih; g.iw = iw; g.oh = ih / 2; g.ow = iw / 2;
-  g.M = n * g.oh * g.ow; g.N = cout; g.K = cin * 16;
-  g.A = act_in;
-  g.W = w; g.ldb = cin * 16;
-  g.bias = b;
-  g.Y = out; g.ldy = cout;
-  g.act = 1;
-  return g;
-}
-
 extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, const dr_frames* src, int B, int T,
                                    float* feat, void* ws, size_t ws_bytes, hipStream_t s) {
   DR_REQUIRE(d && wm && src && feat && B > 0 && T > 0, "null argument or empty batch");
   DR_REQUIRE(d->img_h % 16 == 0 && d->img_w % 16 == 0, "image size must be a multiple of 16");
+  DR_REQUIRE(d->enc_f1 % 4 == 0 && d->enc_f2 % 4 == 0, "encoder filter counts must be multiples of 4");
   const int n = B * T;
   Carve c(ws);
   EncWs w;
@@ -156,19 +147,17 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
   WS_CHECK(c, ws_bytes);
   const int c1 = d->enc_f1, c2 = d->enc_f2, c3 = 2 * d->enc_f2, c4 = 4 * d->enc_f2;
   const int h0 = d->img_h, w0 = d->img_w;
-  DR_TRY(op_conv_repack(c2, c1, wm->conv[1].w, w.wr2, s));
-  DR_TRY(op_conv_repack(c3, c2, wm->conv[2].w, w.wr3, s));
-  DR_TRY(op_conv_repack(c4, c3, wm->conv[3].w, w.wr4, s));
-  // conv1 straight from the frames (u8 ring or f32), NCHW source, torch K order
-  GemmArgs g1 = conv_args(n, 3, h0, w0, c1, nullptr, wm->conv[0].w, wm->conv[0].b, w.a1);
-  g1.src = *src;
-  g1.nb = B;
-  DR_TRY(run(G_NT, AM_CONV_SRC, g1, s));
-  DR_TRY(run(G_NT, AM_CONV, conv_args(n, c1, h0 / 2, w0 / 2, c2, w.a1, w.wr2, wm->conv[1].b, w.a2), s));
-  DR_TRY(run(G_NT, AM_CONV, conv_args(n, c2, h0 / 4, w0 / 4, c3, w.a2, w.wr3, wm->conv[2].b, w.a3), s));
-  GemmArgs g4 = conv_args(n, c3, h0 / 8, w0 / 8, c4, w.a3, w.wr4, wm->conv[3].b, w.a4);
-  g4.out_conv = 1;  // NCHW == nn.Flatten order of Encoder.forward (VAE.py:72)
-  DR_TRY(run(G_NT, AM_CONV, g4, s));
+  DR_TRY(op_conv_repack_pad(c1, 3, 4, wm->conv[0].w, w.wr1, s));
+  DR_TRY(op_conv_repack_pad(c2, c1, c1, wm->conv[1].w, w.wr2, s));
+  DR_TRY(op_conv_repack_pad(c3, c2, c2, wm->conv[2].w, w.wr3, s));
+  DR_TRY(op_conv_repack_pad(c4, c3, c3, wm->conv[3].w, w.wr4, s));
+  // frames (u8 ring or f32) -> normalised NHWC4, then four NHWC implicit GEMMs
+  DR_TRY(op_frames_nhwc4(n, B, h0, w0, src, w.x0, s));
+  DR_TRY(op_conv_nhwc(n, 4, h0, w0, c1, w.x0, w.wr1, wm->conv[0].b, w.a1, 0, s));
+  DR_TRY(op_conv_nhwc(n, c1, h0 / 2, w0 / 2, c2, w.a1, w.wr2, wm->conv[1].b, w.a2, 0, s));
+  DR_TRY(op_conv_nhwc(n, c2, h0 / 4, w0 / 4, c3, w.a2, w.wr3, wm->conv[2].b, w.a3, 0, s));
+  // last layer in NCHW == nn.Flatten order of Encoder.forward (VAE.py:72)
+  DR_TRY(op_conv_nhwc(n, c3, h0 / 8, w0 / 8, c4, w.a3, w.wr4, wm->conv[3].b, w.a4, 1, s));
   const int F = c4 * (h0 / 16) * (w0 / 16);
   return run(G_NT, AM_PLAIN, lin(n, d->enc_hidden, F, w.a4, F, wm->map0.w, F + d->hidden, wm->map0.b, feat, d->enc_hidden), s);
 }

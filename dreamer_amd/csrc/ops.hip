@@ -261,22 +261,26 @@ int op_ln_silu_bwd(int M, int K, const float* gx, long long ldgx, const float* p
 // ---------------------------------------------------------------------------
 // column sums (bias / LayerNorm parameter gradients), deterministic order
 // ---------------------------------------------------------------------------
-__global__ void k_colsum(int M, int N, const float* __restrict__ X, long long ldx, const float* __restrict__ Y,
-                         long long ldy, float* out, int accumulate) {
-  __shared__ float part[4][64];
-  const int n = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+__global__ __launch_bounds__(1024) void k_colsum(int M, int N, const float* __restrict__ X, long long ldx,
+                                                 const float* __restrict__ Y, long long ldy, float* out,
+                                                 int accumulate) {
+  __shared__ float part[16][64];
+  const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c;
   float acc = 0.f;
   if (n < N) {
-    for (int m = rg; m < M; m += 4) {
+    for (int m = rg; m < M; m += 16) {
       float v = X[(long long)m * ldx + n];
       if (Y) v = v * Y[(long long)m * ldy + n];
       acc += v;
     }
   }
-  part[rg][threadIdx.x & 63] = acc;
+  part[rg][c] = acc;
   __syncthreads();
   if (rg == 0 && n < N) {
-    const float t = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += part[k][c];
     out[n] = accumulate ? out[n] + t : t;
   }
 }
@@ -284,7 +288,7 @@ __global__ void k_colsum(int M, int N, const float* __restrict__ X, long long ld
 int op_colsum(int M, int N, const float* X, long long ldx, const float* Y, long long ldy, float* out, int accumulate,
               hipStream_t s) {
   if (N == 0) return DR_OK;
-  hipLaunchKernelGGL(k_colsum, dim3(dr_cdiv(N, 64)), dim3(256), 0, s, M, N, X, ldx, Y, ldy, out, accumulate);
+  hipLaunchKernelGGL(k_colsum, dim3(dr_cdiv(N, 64)), dim3(1024), 0, s, M, N, X, ldx, Y, ldy, out, accumulate);
   return dr_check_launch("colsum");
 }
 
@@ -649,9 +653,18 @@ int op_critic_ce(int B, int H, int nb, const float* logits, const float* R, cons
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_sqnorm(long long n, const float* g, float* acc) {
   __shared__ float part[1024];
-  float s = 0.f;
-  for (long long i = threadIdx.x; i < n; i += 1024) s += g[i] * g[i];
-  part[threadIdx.x] = s;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  const long long n4 = ((uintptr_t)g & 15) == 0 ? n / 4 : 0;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (long long i = threadIdx.x; i < n4; i += 1024) {
+    const float4 v = g4[i];
+    s0 += v.x * v.x;
+    s1 += v.y * v.y;
+    s2 += v.z * v.z;
+    s3 += v.w * v.w;
+  }
+  for (long long i = 4 * n4 + threadIdx.x; i < n; i += 1024) s0 += g[i] * g[i];
+  part[threadIdx.x] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   for (int k = 512; k > 0; k >>= 1) {
     if ((int)threadIdx.x < k) part[threadIdx.x] += part[threadIdx.x + k];

@@ -16,7 +16,8 @@ With world_size > 1 (one process per GPU, RCCL over xGMI) each rank runs its
 slice of the batch; the exchange is one all-gather of the lambda returns
 (global quantile of update_S) and one all-reduce of a flat
 [actor grads | critic grads | losses] buffer.  Everything else is local.
-On one GPU the whole epoch is captured once into a HIP graph and replayed.
+Each phase is captured once into a HIP graph and replayed; collectives run
+between the phase graphs.
 """
 import numpy as np
 import torch
@@ -39,7 +40,7 @@ class ImaginationEngine:
         self.world = world  # (rank, size, group) or None
         self.rank = world[0] if world else 0
         self.wsize = world[1] if world else 1
-        self.use_graph = use_graph and self.wsize == 1
+        self.use_graph = use_graph
         self.graph = None
         self.graph_key = None
         self._alloc()
@@ -148,19 +149,41 @@ class ImaginationEngine:
         """non-finite skip, clip_grad_norm_(100) x2, AdamW x2, soft target (Agent.py:137-153)."""
         self.dr.agent.fused_optimiser_step(self.sq, self.skip)
 
-    def epoch_body(self):
-        frames = self.dr.buffer.frames_struct(self.starts)
+    # phases of one epoch; collectives (world > 1) run between phases
+    def _ph_encode(self):
         self.dr.buffer.gather_actions(self.starts, self.act_win)
-        self.encode_and_warm(frames)
-        self.imagine()
-        self.returns()
-        if self.wsize > 1:
-            self._allgather_R()
+        self.encode_and_warm_frames = self.dr.buffer.frames_struct(self.starts)
+        d, st = self.d, hip.stream()
+        L.call("dr_encoder_features", d, self.dr.world_model.packed(), self.encode_and_warm_frames, self.B, self.T,
+               L.ptr(self.feat), L.ptr(self.ws_enc), self.ws_enc.numel(), st)
+
+    def _ph_warm(self):
+        d, A = self.d, self.d.action
+        nz = L.dr_noise(None, None, self.rng.state.data_ptr(), self.rank * self.B, WARM_STREAM)
+        L.call("dr_observe_scan", d, self.dr.world_model.packed(), self.B, self.T, L.ptr(self.feat),
+               L.ptr(self.act_win), self.S * A, A, None, None, nz, L.ptr(self.z0), L.ptr(self.h0), None,
+               L.ptr(self.ws_obs), self.ws_obs.numel(), hip.stream())
+
+    def _ph_update(self):
         self.losses_and_grads()
-        if self.wsize > 1:
-            self._allreduce_grads()
+
+    def _ph_optim(self):
         self.optimise()
         L.call("dr_rng_advance", self.rng.state.data_ptr(), 1, hip.stream())
+
+    def phases(self):
+        """(name, body, collective-after) in execution order."""
+        ph = [("encode", self._ph_encode, None), ("warm", self._ph_warm, None), ("imagine", self.imagine, None),
+              ("returns", self.returns, self._allgather_R if self.wsize > 1 else None),
+              ("update", self._ph_update, self._allreduce_grads if self.wsize > 1 else None),
+              ("optim", self._ph_optim, None)]
+        return ph
+
+    def epoch_body(self):
+        for _, body, coll in self.phases():
+            body()
+            if coll is not None:
+                coll()
 
     # ------------------------------------------------------------------ DP
     def _allgather_R(self):
@@ -175,9 +198,10 @@ class ImaginationEngine:
         ag.loss_buffer.div_(self.wsize)
 
     # ----------------------------------------------------------------- driver
-    def run(self, starts_np):
+    def run(self, starts_np, timing=False):
         """One train_Agent epoch from host window starts; returns the device
-        loss slots (actor, critic)."""
+        loss slots (actor, critic).  With timing=True, HIP events bracket every
+        phase (self.last_events)."""
         i = self.epochs & 1
         if self.copy_ev[i] is not None:
             self.copy_ev[i].synchronize()
@@ -188,22 +212,42 @@ class ImaginationEngine:
         self.epochs += 1
         ag = self.dr.agent
         key = (ag.params_key(), self.dr.world_model.params_key(), self.dr.buffer.device_key())
-        if self.use_graph:
-            if self.graph is None or self.graph_key != key:
-                self._capture(key)
-            self.graph.replay()
-        else:
-            self.epoch_body()
+        if self.use_graph and (self.graph is None or self.graph_key != key):
+            self._capture(key)
+        evs = [torch.cuda.Event(enable_timing=True)] if timing else None
+        if evs:
+            evs[0].record()
+        for k, (name, body, coll) in enumerate(self.phases()):
+            if self.use_graph:
+                self.graph[k].replay()
+            else:
+                body()
+            if coll is not None:
+                coll()
+            if evs:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record()
+                evs.append(e)
+        self.last_events = evs
         return ag.loss_slot(0), ag.loss_slot(1)
 
+    def phase_ms(self):
+        """Per-phase milliseconds of the last timed run (after a sync)."""
+        names = [p[0] for p in self.phases()]
+        ev = self.last_events
+        return {n: ev[k].elapsed_time(ev[k + 1]) for k, n in enumerate(names)}
+
     def _capture(self, key):
-        # record one epoch into a graph (capture does not execute it; the
-        # caller replays it right after)
+        """Record each phase into its own HIP graph (capture does not execute;
+        run() replays right after).  Collectives stay outside the graphs."""
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
-        g = torch.cuda.CUDAGraph()
+        graphs = []
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
-                self.epoch_body()
+            for _, body, _ in self.phases():
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    body()
+                graphs.append(g)
         torch.cuda.current_stream(self.dev).wait_stream(s)
-        self.graph, self.graph_key = g, key
+        self.graph, self.graph_key = graphs, key
