@@ -6,6 +6,7 @@
 
 #include "conv.h"
 #include "gemm.h"
+#include "gru.h"
 #include "ops.h"
 
 int op_critic_ce(int B, int H, int nb, const float* logits, const float* R, const float* buckets, float scale,
@@ -166,13 +167,30 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
 // a2/a5  posterior scan
 // ===========================================================================
 struct ObsWs {
-  float *gi, *gh, *pre1, *logits;
+  float *gi, *gh, *pre1, *logits, *wt, *hb[2];
+  int* idx;
 };
 static void obs_carve(Carve& c, const dr_dims* d, int B, ObsWs& w) {
   w.gi = c.f((long long)B * 3 * d->hidden);
   w.gh = c.f((long long)B * 3 * d->hidden);
   w.pre1 = c.f((long long)B * d->enc_hidden);
   w.logits = c.f((long long)B * latent(d));
+  w.wt = c.f((long long)(latent(d) + d->action) * 3 * d->hidden);
+  w.hb[0] = c.f((long long)B * d->hidden);
+  w.hb[1] = c.f((long long)B * d->hidden);
+  w.idx = c.i((long long)B * d->rows);
+}
+
+// GRU step on a sampled one-hot latent (idx) via the fused kernel
+static int gru_onehot(const dr_dims* d, const dr_world_model* wm, int B, const int* idx, const float* z,
+                      long long ldz, const float* a, long long lda, const float* h, long long ldh, float* hout,
+                      long long ldo, const float* wt, float* sr, float* su, float* sn, float* sghn, hipStream_t s) {
+  GruArgs g;
+  g.B = B; g.Hd = d->hidden; g.R = d->rows; g.C = d->cols; g.A = d->action;
+  g.idx = idx; g.z = z; g.ldz = ldz; g.a = a; g.lda = lda; g.h = h; g.ldh = ldh;
+  g.wt = wt; g.b_ih = wm->b_ih; g.w_hh = wm->w_hh; g.b_hh = wm->b_hh;
+  g.hout = hout; g.ldo = ldo; g.sr = sr; g.su = su; g.sn = sn; g.sghn = sghn;
+  return op_gru_fused(g, s);
 }
 
 extern "C" size_t dr_observe_workspace_bytes(const dr_dims* d, int B) {
@@ -207,27 +225,41 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
   WS_CHECK(c, ws_bytes);
   const int L = latent(d), Hd = d->hidden, eh = d->enc_hidden;
   const int F = 4 * d->enc_f2 * (d->img_h / 16) * (d->img_w / 16);
-  bool h_valid = h_init != nullptr;
-  if (h_init && h_init != h_out) DR_TRY(copy2d(h_out, Hd, h_init, Hd, Hd, B, s));
-  if (!h_init) DR_TRY(zero(h_out, (long long)B * Hd, s));
-  if (z_init && z_init != z_out) DR_TRY(copy2d(z_out, L, z_init, L, L, B, s));
+  // W_ih^T for the one-hot gather of the fused GRU (weights are fixed for the
+  // call); only needed when a GRU step runs (an encode-only call passes a
+  // world model without GRU weights)
+  const bool any_gru = (z_init != nullptr) || T > 1;
+  if (any_gru) {
+    DR_REQUIRE(wm->w_ih && wm->w_hh && wm->b_ih && wm->b_hh, "GRU weights required");
+    DR_TRY(op_transpose(3 * Hd, L + d->action, wm->w_ih, w.wt, s));
+  }
+  const float* h = h_init;  // current hidden (NULL = zeros)
+  int hb = 0;
+  if (z_init) {
+    if (z_init != z_out) DR_TRY(copy2d(z_out, L, z_init, L, L, B, s));
+    DR_TRY(op_onehot_index(B, d->rows, d->cols, z_out, L, w.idx, s));
+  }
   for (int t = 0; t < T; ++t) {
     const bool do_gru = (z_init != nullptr) || t > 0;
     if (do_gru) {
       const int ai = t - (z_init == nullptr ? 1 : 0);
-      DR_TRY(gru_step(d, wm, B, z_out, L, actions + ai * act_st, act_sb, h_valid ? h_out : nullptr, Hd, h_out, Hd,
-                      w.gi, w.gh, nullptr, nullptr, nullptr, nullptr, s));
-      h_valid = true;
+      float* hn = w.hb[hb];
+      hb ^= 1;
+      DR_TRY(gru_onehot(d, wm, B, w.idx, z_out, L, actions + ai * act_st, act_sb, h, Hd, hn, Hd, w.wt, nullptr,
+                        nullptr, nullptr, nullptr, s));
+      h = hn;
     }
     // latent_mapper.0 on cat(features, h): feature part precomputed in feat[t]
-    GemmArgs g = lin(B, eh, h_valid ? Hd : 0, h_out, Hd, wm->map0.w + F, F + Hd, nullptr, w.pre1, eh);
+    GemmArgs g = lin(B, eh, h ? Hd : 0, h, Hd, wm->map0.w + F, F + Hd, nullptr, w.pre1, eh);
     g.addend = feat + (long long)t * B * eh;
     g.ld_add = eh;
     DR_TRY(run(G_NT, AM_PLAIN, g, s));
     float* lg = (t == T - 1 && logits_out) ? logits_out : w.logits;
     DR_TRY(run(G_NT, AM_LNSILU, lin_ln(B, L, eh, w.pre1, eh, wm->map1, wm->map3.w, wm->map3.b, lg, L), s));
-    DR_TRY(op_sample(B, d->rows, d->cols, lg, L, &noise, t, z_out, L, nullptr, nullptr, 0, s));
+    DR_TRY(op_sample(B, d->rows, d->cols, lg, L, &noise, t, z_out, L, w.idx, nullptr, 0, s));
   }
+  if (h) DR_TRY(copy2d(h_out, Hd, h, Hd, Hd, B, s));
+  else DR_TRY(zero(h_out, (long long)B * Hd, s));
   return DR_OK;
 }
 
@@ -265,7 +297,8 @@ extern "C" size_t dr_imagine_tape_bytes(const dr_dims* d, int B, int H) {
 }
 
 struct ImWs {
-  float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog;  // forward scratch
+  float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog, *wt;  // forward scratch
+  int* idx[2];
   // backward
   float *gH, *gZ, *gA, *glog, *gx2, *gp2, *gx1, *gp1, *ggi, *ggh, *gheads, *gx2a, *gpre2a, *gy2a, *xh2a, *gx1a,
       *gpre1a, *gy1a, *xh1a, *hcat, *zcat;
@@ -282,6 +315,9 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.p2c = c.f(Bl * d->cont_h2);
   w.rlog = c.f(Bl * d->buckets);
   w.clog = c.f(Bl);
+  w.wt = c.f((long long)(L + A) * 3 * Hd);
+  w.idx[0] = c.i(Bl * d->rows);
+  w.idx[1] = c.i(Bl * d->rows);
   w.gH = c.f(B1 * Hd);
   w.gZ = c.f(B1 * L);
   w.gA = c.f(BH * A);
@@ -333,6 +369,8 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
   DR_TRY(copy2d(hiddens, ldH, h0, Hd, Hd, B, s));
   dr_noise nq = noise;  // Categorical draws: a Philox stream apart from the actor's
   nq.stream += 65536;
+  DR_TRY(op_transpose(3 * Hd, L + A, wm->w_ih, w.wt, s));
+  DR_TRY(op_onehot_index(B, d->rows, d->cols, latents, ldL, w.idx[0], s));
 
   // actor at step 0 (Agent.py:191-210)
   DR_TRY(run(G_NT, AM_PLAIN, lin2(B, a1, hiddens, ldH, Hd, latents, ldL, L, ac->l0.w, ac->l0.b, tp.pre1a, lda1), s));
@@ -355,8 +393,8 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
     float* z_t = latents + (long long)t * L;
     float* z_n = latents + (long long)(t + 1) * L;
     // WorldModel.imagine_step (WorldModel.py:72-77)
-    DR_TRY(gru_step(d, wm, B, z_t, ldL, actions + (long long)t * A, ldA, h_t, ldH, h_n, ldH, w.gi, w.gh, tp.r + hb,
-                    tp.u + hb, tp.n + hb, tp.ghn + hb, s));
+    DR_TRY(gru_onehot(d, wm, B, w.idx[t & 1], z_t, ldL, actions + (long long)t * A, ldA, h_t, ldH, h_n, ldH, w.wt,
+                      tp.r + hb, tp.u + hb, tp.n + hb, tp.ghn + hb, s));
     float* p1 = tp.pre1p + (long long)t * B * d->prior_h1;
     float* p2 = tp.pre2p + (long long)t * B * d->prior_h2;
     DR_TRY(run(G_NT, AM_PLAIN, lin(B, d->prior_h1, Hd, h_n, ldH, wm->prior.l0.w, Hd, wm->prior.l0.b, p1, d->prior_h1), s));
@@ -364,8 +402,8 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
                                        wm->prior.l3.b, p2, d->prior_h2), s));
     DR_TRY(run(G_NT, AM_LNSILU, lin_ln(B, L, d->prior_h2, p2, d->prior_h2, wm->prior.n4, wm->prior.l6.w,
                                        wm->prior.l6.b, w.plog, L), s));
-    DR_TRY(op_sample(B, d->rows, d->cols, w.plog, L, &nq, t, z_n, ldL, nullptr, tp.soft + (long long)t * B * L, L,
-                     s));
+    DR_TRY(op_sample(B, d->rows, d->cols, w.plog, L, &nq, t, z_n, ldL, w.idx[(t + 1) & 1],
+                     tp.soft + (long long)t * B * L, L, s));
     // reward / continue heads on (h', z') and the actor for step t+1, grouped
     const bool nxt = (t + 1 < H);
     {

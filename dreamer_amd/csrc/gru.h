@@ -1,0 +1,25 @@
+// Fused GRU step with a one-hot latent input (gru.hip).
+#pragma once
+#include "common.h"
+
+struct GruArgs {
+  int B, Hd, R, C, A;
+  const int* idx;       // [B][R] sampled class per latent group
+  const float* z;       // straight-through latents (value at idx), row stride ldz
+  long long ldz;
+  const float* a;       // actions [B][A], row stride lda
+  long long lda;
+  const float* h;       // previous hidden (NULL = zeros), row stride ldh
+  long long ldh;
+  const float* wt;      // W_ih^T [R*C + A][3*Hd]
+  const float* b_ih;
+  const float* w_hh;    // [3*Hd][Hd]
+  const float* b_hh;
+  float* hout;          // row stride ldo; must NOT alias h (other workgroups still read h)
+  long long ldo;
+  float *sr, *su, *sn, *sghn;  // optional saves [B][Hd] for the backward
+};
+
+int op_gru_fused(const GruArgs& g, hipStream_t s);
+int op_transpose(int rows, int cols, const float* in, float* out, hipStream_t s);
+int op_onehot_index(int M, int R, int C, const float* z, long long ldz, int* idx, hipStream_t s);

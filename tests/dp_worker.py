@@ -1,0 +1,54 @@
+"""Worker for the data-parallel tests (spawned; one process per rank)."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.dirname(HERE), HERE, os.path.join(HERE, "golden")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def make_dreamer(dev, B, S=8, H=5):
+    from formula import SMALL, replay_data
+    from dreamer_amd import Dreamer
+    cfg = dict(SMALL)
+    cfg.update(batch_size=B, sequence_length=S, horizon=H, buffer_size=64)
+    torch.manual_seed(0)
+    d = Dreamer(cfg, dev)
+    fr, ac, rw, ct = replay_data(64, (32, 32), 3, seed=3)
+    rw = (np.sign(rw) * np.log1p(np.abs(rw))).astype(np.float32)
+    d.buffer.load_arrays(fr, ac, rw, ct)
+    return d
+
+
+def run_epochs(d, eng, starts_list, seed=4321):
+    eng.rng.reseed(seed)
+    out = []
+    for st in starts_list:
+        la, lc = eng.run(st)
+        torch.cuda.synchronize()
+        out.append((float(la), float(lc)))
+    ag = d.agent
+    return out, ag.fa.flat.cpu(), ag.fc.flat.cpu(), ag.ft.flat.cpu(), float(ag.S_dev)
+
+
+def worker(rank, world, port, B_global, starts_list, out_path, backend):
+    import torch.distributed as dist
+    from dreamer_amd.engine import ImaginationEngine
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    b = B_global // world
+    d = make_dreamer(dev, b)
+    eng = ImaginationEngine(d, B=b, world=(rank, world, dist.group.WORLD))
+    mine = [st[rank * b:(rank + 1) * b] for st in starts_list]
+    res = run_epochs(d, eng, mine)
+    if rank == 0:
+        torch.save(res, out_path)
+    dist.barrier()
+    dist.destroy_process_group()

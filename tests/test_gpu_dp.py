@@ -1,0 +1,43 @@
+"""Data-parallel train_Agent on the real HIP path: 2 ranks (gloo, both on
+cuda:0 of the one-GPU box) vs one process on the concatenated batch.
+Philox noise is keyed by the global row, so both runs draw identical noise;
+the all-gathered returns give the same global quantile, and the all-reduced
+flat gradient differs from the single-device sum only in summation order."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import dp_worker
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_rank_matches_single(gpu, tmp_path):
+    from dreamer_amd.engine import ImaginationEngine
+    B = 8
+    rng = np.random.RandomState(11)
+    starts = [rng.randint(0, 64 - 8 + 1, size=B) for _ in range(3)]
+    out = str(tmp_path / "dp.pt")
+    mp.spawn(dp_worker.worker, args=(2, _port(), B, starts, out, "gloo"), nprocs=2, join=True)
+    dp = torch.load(out, weights_only=False)
+    d = dp_worker.make_dreamer(gpu, B)
+    eng = ImaginationEngine(d, B=B)
+    single = dp_worker.run_epochs(d, eng, starts)
+    for (la1, lc1), (la2, lc2) in zip(single[0], dp[0]):
+        assert abs(la1 - la2) <= 1e-4 * max(1.0, abs(la1)), (la1, la2)
+        assert abs(lc1 - lc2) <= 1e-4 * max(1.0, abs(lc1)), (lc1, lc2)
+    for a, b, name in zip(single[1:4], dp[1:4], ("actor", "critic", "target")):
+        assert torch.allclose(a, b, rtol=0, atol=5e-6), (name, float((a - b).abs().max()))
+    assert abs(single[4] - dp[4]) < 1e-6
