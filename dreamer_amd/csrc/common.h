@@ -50,24 +50,123 @@ __device__ __forceinline__ float dr_symlog(float x) {  // DreamerUtils.py:29-30
   return s * logf(1.0f + fabsf(x));
 }
 
-// wave64 reductions
+// Phase timestamps for the kernel microbenchmark (tools/kbench): compiled in
+// only with -DDR_PHASE_TIMING; wave 0 of each workgroup records the 100 MHz
+// constant clock at phase boundaries.
+#define DR_TS_SLOTS 8
+#ifdef DR_PHASE_TIMING
+#define DR_TS(buf, i)                                                        \
+  do {                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 1024 && blockIdx.y == 0 && blockIdx.z == 0) \
+      buf[blockIdx.x * DR_TS_SLOTS + (i)] = (long long)wall_clock64();      \
+  } while (0)
+#else
+#define DR_TS(buf, i) \
+  do {                \
+  } while (0)
+#endif
+
+// Kernel-argument staging.  A kernel that reads a large argument block field by
+// field issues one dependent scalar load per field, and on a graph replay the
+// argument lines are cold (each miss ~0.5 us), so the fields arrive one after
+// another.  Copying the block into LDS with one parallel vector load per
+// 16 bytes turns that chain into a single round trip.
+template <typename T>
+__device__ __forceinline__ void dr_stage_args(const T& src, T& dst, int tid) {
+  static_assert(sizeof(T) % 16 == 0, "argument block must be a multiple of 16 bytes");
+  constexpr int N16 = sizeof(T) / 16;
+  if (tid < N16) reinterpret_cast<int4*>(&dst)[tid] = reinterpret_cast<const int4*>(&src)[tid];
+  __syncthreads();
+}
+
+// Wave-uniform values.  Arguments read back from LDS are VGPRs as far as the
+// compiler knows; readfirstlane turns them into SGPRs, so address math runs
+// on the scalar unit and loads use the saddr + 32-bit voffset form.
+__device__ __forceinline__ int dr_uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ float dr_uni(float x) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+template <typename T>
+__device__ __forceinline__ T* dr_uni(T* p) {
+  const unsigned long long v = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (T*)(((unsigned long long)hi << 32) | lo);
+}
+// loads at a 32-bit element offset from a uniform base (callers guarantee
+// offsets < 2^30 elements)
+__device__ __forceinline__ float4 dr_ld4(const float* base, unsigned e) {
+  return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + (e << 2));
+}
+__device__ __forceinline__ float dr_ld1(const float* base, unsigned e) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (e << 2));
+}
+// SiLU on the hardware exp2 / reciprocal (~2 ulp, 6 VALU instead of ~25 for
+// the IEEE expf + division); used where the input is transformed once per
+// consuming tile, inside the GEMM prologue
+__device__ __forceinline__ float dr_silu_fast(float x) {
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
+
+// XCD-aware tile order.  Workgroups are dealt to the 8 XCDs round-robin
+// (block b runs on XCD b % 8, each XCD has its own L2).  Mapping block b to
+// logical tile (b % 8) * per + b / 8 gives every XCD a contiguous run of
+// logical tiles, so tiles that share operands (ordered next to each other by
+// the caller) share one L2.  Launch 8 * per blocks, per = ceil(tiles / 8);
+// returns -1 for the padding blocks.
+#define DR_XCDS 8
+__host__ __device__ __forceinline__ int dr_xcd_grid(int tiles) { return DR_XCDS * ((tiles + DR_XCDS - 1) / DR_XCDS); }
+__device__ __forceinline__ int dr_xcd_tile(int b, int tiles) {
+  const int per = (tiles + DR_XCDS - 1) / DR_XCDS;
+  const int k = b / DR_XCDS;
+  if (k >= per) return -1;  // a grid sized for a larger problem of the batch
+  const int t = (b % DR_XCDS) * per + k;
+  return t < tiles ? t : -1;
+}
+
+// wave64 reductions (call with the whole wave active).  In-row butterfly on
+// DPP (quad xor 1, quad xor 2, half-row mirror, row mirror: every lane of a
+// 16-lane row ends with the row total, bitwise identical by commutativity),
+// then the four row totals read as scalars -- no LDS crossbar round trips.
+template <int CTRL>
+__device__ __forceinline__ float dr_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dr_lane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dr_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dr_dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dr_dpp<0x141>(v);  // row_half_mirror
+  v += dr_dpp<0x140>(v);  // row_mirror
+  return ((dr_lane(v, 0) + dr_lane(v, 16)) + dr_lane(v, 32)) + dr_lane(v, 48);
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, dr_dpp<0xB1>(v));
+  v = fmaxf(v, dr_dpp<0x4E>(v));
+  v = fmaxf(v, dr_dpp<0x141>(v));
+  v = fmaxf(v, dr_dpp<0x140>(v));
+  return fmaxf(fmaxf(dr_lane(v, 0), dr_lane(v, 16)), fmaxf(dr_lane(v, 32), dr_lane(v, 48)));
 }
-// reductions inside aligned sub-groups of `width` lanes (power of two <= 64)
+// reductions inside aligned sub-groups of `width` lanes (power of two <= 64,
+// wave-uniform): DPP inside 16-lane rows, lane shuffles across rows
 __device__ __forceinline__ float group_sum(float v, int width) {
-  for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (width >= 2) v += dr_dpp<0xB1>(v);
+  if (width >= 4) v += dr_dpp<0x4E>(v);
+  if (width >= 8) v += dr_dpp<0x141>(v);
+  if (width >= 16) v += dr_dpp<0x140>(v);
+  if (width >= 32) v += __shfl_xor(v, 16, 64);
+  if (width >= 64) v += __shfl_xor(v, 32, 64);
   return v;
 }
 __device__ __forceinline__ float group_max(float v, int width) {
-  for (int o = width >> 1; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  if (width >= 2) v = fmaxf(v, dr_dpp<0xB1>(v));
+  if (width >= 4) v = fmaxf(v, dr_dpp<0x4E>(v));
+  if (width >= 8) v = fmaxf(v, dr_dpp<0x141>(v));
+  if (width >= 16) v = fmaxf(v, dr_dpp<0x140>(v));
+  if (width >= 32) v = fmaxf(v, __shfl_xor(v, 16, 64));
+  if (width >= 64) v = fmaxf(v, __shfl_xor(v, 32, 64));
   return v;
 }
 

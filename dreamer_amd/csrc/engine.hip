@@ -108,6 +108,47 @@ static GemmArgs bwd_w(int out, int in, int R, const float* G, long long ldg, con
 
 static int run(GemmLayout lay, int amode, const GemmArgs& a, hipStream_t s) { return gemm_launch(lay, amode, &a, 1, s); }
 
+// one-hot index buffers hold [B][R] class indices followed by the [B][R]
+// straight-through values at those indices (what the fused GRU gathers)
+static float* onehot_vals(int* idx, long long B, int R) { return reinterpret_cast<float*>(idx + B * R); }
+
+// fused categorical-sampler epilogue on a logits GEMM (VAE.py:88-98,
+// DynamicsPredictors.py:33-39): z (STE value), idx, softmax for the backward
+static void with_sampler(GemmArgs& g, const dr_dims* d, const dr_noise& nz, int step, float* z, long long ldz,
+                         int* idx, float* soft, long long ld_soft) {
+  g.epi = EPI_SAMPLE;
+  g.noise = nz;
+  g.step = step;
+  g.R = d->rows;
+  g.C = d->cols;
+  g.unimix = (float)(0.01 * (1.0 / d->cols));
+  g.z_out = z; g.ldz = ldz; g.idx_out = idx; g.soft_out = soft; g.ld_soft = ld_soft;
+  g.zval_out = idx ? onehot_vals(idx, g.M, d->rows) : nullptr;
+}
+
+// fused actor-head epilogue on the stacked [mu_head; log_sig_head] GEMM
+static void with_actor_head(GemmArgs& g, int A, const dr_noise& nz, int step, int det, float* act, long long ld_act,
+                            float* mu, long long ld_mu, float* sig, long long ld_sig, float* eps_save, float* ls_save,
+                            long long ld_ls) {
+  g.epi = EPI_ACTOR;
+  g.noise = nz;
+  g.step = step;
+  g.na = A;
+  g.det = det;
+  g.act_out = act; g.ld_act = ld_act; g.mu_out = mu; g.ld_mu = ld_mu; g.sig_out = sig; g.ld_sig = ld_sig;
+  g.eps_save = eps_save; g.ls_save = ls_save; g.ld_ls = ld_ls;
+  g.Y = nullptr;
+}
+
+// [mu_head; log_sig_head] stacked into one [2A][in] weight (+ bias) so one
+// workgroup sees both halves of a row
+static int stack_heads(const dr_actor* ac, int A, int in, float* w, float* b, hipStream_t s) {
+  DR_TRY(copy2d(w, in, ac->mu.w, in, in, A, s));
+  DR_TRY(copy2d(w + (long long)A * in, in, ac->ls.w, in, in, A, s));
+  DR_TRY(copy2d(b, A, ac->mu.b, A, A, 1, s));
+  return copy2d(b + A, A, ac->ls.b, A, A, 1, s);
+}
+
 // ===========================================================================
 // a3  encoder features
 // ===========================================================================
@@ -178,16 +219,15 @@ static void obs_carve(Carve& c, const dr_dims* d, int B, ObsWs& w) {
   w.wt = c.f((long long)(latent(d) + d->action) * 3 * d->hidden);
   w.hb[0] = c.f((long long)B * d->hidden);
   w.hb[1] = c.f((long long)B * d->hidden);
-  w.idx = c.i((long long)B * d->rows);
+  w.idx = c.i(2LL * B * d->rows);
 }
 
 // GRU step on a sampled one-hot latent (idx) via the fused kernel
-static int gru_onehot(const dr_dims* d, const dr_world_model* wm, int B, const int* idx, const float* z,
-                      long long ldz, const float* a, long long lda, const float* h, long long ldh, float* hout,
+static int gru_onehot(const dr_dims* d, const dr_world_model* wm, int B, int* idx, const float* a, long long lda, const float* h, long long ldh, float* hout,
                       long long ldo, const float* wt, float* sr, float* su, float* sn, float* sghn, hipStream_t s) {
   GruArgs g;
   g.B = B; g.Hd = d->hidden; g.R = d->rows; g.C = d->cols; g.A = d->action;
-  g.idx = idx; g.z = z; g.ldz = ldz; g.a = a; g.lda = lda; g.h = h; g.ldh = ldh;
+  g.idx = idx; g.zval = onehot_vals(idx, B, d->rows); g.a = a; g.lda = lda; g.h = h; g.ldh = ldh;
   g.wt = wt; g.b_ih = wm->b_ih; g.w_hh = wm->w_hh; g.b_hh = wm->b_hh;
   g.hout = hout; g.ldo = ldo; g.sr = sr; g.su = su; g.sn = sn; g.sghn = sghn;
   return op_gru_fused(g, s);
@@ -237,7 +277,7 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
   int hb = 0;
   if (z_init) {
     if (z_init != z_out) DR_TRY(copy2d(z_out, L, z_init, L, L, B, s));
-    DR_TRY(op_onehot_index(B, d->rows, d->cols, z_out, L, w.idx, s));
+    DR_TRY(op_onehot_index(B, d->rows, d->cols, z_out, L, w.idx, onehot_vals(w.idx, B, d->rows), s));
   }
   for (int t = 0; t < T; ++t) {
     const bool do_gru = (z_init != nullptr) || t > 0;
@@ -245,7 +285,7 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
       const int ai = t - (z_init == nullptr ? 1 : 0);
       float* hn = w.hb[hb];
       hb ^= 1;
-      DR_TRY(gru_onehot(d, wm, B, w.idx, z_out, L, actions + ai * act_st, act_sb, h, Hd, hn, Hd, w.wt, nullptr,
+      DR_TRY(gru_onehot(d, wm, B, w.idx, actions + ai * act_st, act_sb, h, Hd, hn, Hd, w.wt, nullptr,
                         nullptr, nullptr, nullptr, s));
       h = hn;
     }
@@ -254,9 +294,10 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
     g.addend = feat + (long long)t * B * eh;
     g.ld_add = eh;
     DR_TRY(run(G_NT, AM_PLAIN, g, s));
-    float* lg = (t == T - 1 && logits_out) ? logits_out : w.logits;
-    DR_TRY(run(G_NT, AM_LNSILU, lin_ln(B, L, eh, w.pre1, eh, wm->map1, wm->map3.w, wm->map3.b, lg, L), s));
-    DR_TRY(op_sample(B, d->rows, d->cols, lg, L, &noise, t, z_out, L, w.idx, nullptr, 0, s));
+    float* lg = (t == T - 1 && logits_out) ? logits_out : nullptr;
+    GemmArgs gp = lin_ln(B, L, eh, w.pre1, eh, wm->map1, wm->map3.w, wm->map3.b, lg, L);
+    with_sampler(gp, d, noise, t, z_out, L, w.idx, nullptr, 0);
+    DR_TRY(run(G_NT, AM_LNSILU, gp, s));
   }
   if (h) DR_TRY(copy2d(h_out, Hd, h, Hd, Hd, B, s));
   else DR_TRY(zero(h_out, (long long)B * Hd, s));
@@ -297,7 +338,7 @@ extern "C" size_t dr_imagine_tape_bytes(const dr_dims* d, int B, int H) {
 }
 
 struct ImWs {
-  float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog, *wt;  // forward scratch
+  float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog, *wt, *wst, *bst;  // forward scratch
   int* idx[2];
   // backward
   float *gH, *gZ, *gA, *glog, *gx2, *gp2, *gx1, *gp1, *ggi, *ggh, *gheads, *gx2a, *gpre2a, *gy2a, *xh2a, *gx1a,
@@ -313,11 +354,13 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.p1c = c.f(Bl * d->cont_h1);
   w.p2r = c.f(Bl * d->rew_h2);
   w.p2c = c.f(Bl * d->cont_h2);
-  w.rlog = c.f(Bl * d->buckets);
+  w.rlog = c.f((long long)B * H * d->buckets);
   w.clog = c.f(Bl);
   w.wt = c.f((long long)(L + A) * 3 * Hd);
-  w.idx[0] = c.i(Bl * d->rows);
-  w.idx[1] = c.i(Bl * d->rows);
+  w.wst = c.f((long long)2 * A * d->actor_h2);
+  w.bst = c.f((long long)2 * A);
+  w.idx[0] = c.i(2 * Bl * d->rows);
+  w.idx[1] = c.i(2 * Bl * d->rows);
   w.gH = c.f(B1 * Hd);
   w.gZ = c.f(B1 * L);
   w.gA = c.f(BH * A);
@@ -370,7 +413,7 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
   dr_noise nq = noise;  // Categorical draws: a Philox stream apart from the actor's
   nq.stream += 65536;
   DR_TRY(op_transpose(3 * Hd, L + A, wm->w_ih, w.wt, s));
-  DR_TRY(op_onehot_index(B, d->rows, d->cols, latents, ldL, w.idx[0], s));
+  DR_TRY(op_onehot_index(B, d->rows, d->cols, latents, ldL, w.idx[0], onehot_vals(w.idx[0], B, d->rows), s));
 
   // actor at step 0 (Agent.py:191-210)
   DR_TRY(run(G_NT, AM_PLAIN, lin2(B, a1, hiddens, ldH, Hd, latents, ldL, L, ac->l0.w, ac->l0.b, tp.pre1a, lda1), s));
@@ -378,13 +421,11 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
     GemmArgs g = lin_ln(B, a2, a1, tp.pre1a, lda1, ac->n1, ac->l3.w, ac->l3.b, tp.pre2a, lda2);
     g.a_out = tp.x1a; g.ld_aout = lda1;
     DR_TRY(run(G_NT, AM_LNSILU, g, s));
-    GemmArgs p[2];
-    p[0] = lin_ln(B, A, a2, tp.pre2a, lda2, ac->n4, ac->mu.w, ac->mu.b, mus, ldA);
-    p[0].a_out = tp.x2a; p[0].ld_aout = lda2;
-    p[1] = lin_ln(B, A, a2, tp.pre2a, lda2, ac->n4, ac->ls.w, ac->ls.b, tp.ls_raw, ldA);
-    DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, 2, s));
-    DR_TRY(op_actor_head(B, A, mus, ldA, tp.ls_raw, ldA, &noise, 0, deterministic, actions, ldA, nullptr, 0, sigmas,
-                         ldA, tp.eps, s));
+    DR_TRY(stack_heads(ac, A, a2, w.wst, w.bst, s));
+    GemmArgs h = lin_ln(B, 2 * A, a2, tp.pre2a, lda2, ac->n4, w.wst, w.bst, nullptr, 0);
+    h.a_out = tp.x2a; h.ld_aout = lda2;
+    with_actor_head(h, A, noise, 0, deterministic, actions, ldA, mus, ldA, sigmas, ldA, tp.eps, tp.ls_raw, ldA);
+    DR_TRY(run(G_NT, AM_LNSILU, h, s));
   }
   for (int t = 0; t < H; ++t) {
     const long long hb = (long long)Hd * B * t;
@@ -393,17 +434,18 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
     float* z_t = latents + (long long)t * L;
     float* z_n = latents + (long long)(t + 1) * L;
     // WorldModel.imagine_step (WorldModel.py:72-77)
-    DR_TRY(gru_onehot(d, wm, B, w.idx[t & 1], z_t, ldL, actions + (long long)t * A, ldA, h_t, ldH, h_n, ldH, w.wt,
+    DR_TRY(gru_onehot(d, wm, B, w.idx[t & 1], actions + (long long)t * A, ldA, h_t, ldH, h_n, ldH, w.wt,
                       tp.r + hb, tp.u + hb, tp.n + hb, tp.ghn + hb, s));
     float* p1 = tp.pre1p + (long long)t * B * d->prior_h1;
     float* p2 = tp.pre2p + (long long)t * B * d->prior_h2;
     DR_TRY(run(G_NT, AM_PLAIN, lin(B, d->prior_h1, Hd, h_n, ldH, wm->prior.l0.w, Hd, wm->prior.l0.b, p1, d->prior_h1), s));
     DR_TRY(run(G_NT, AM_LNSILU, lin_ln(B, d->prior_h2, d->prior_h1, p1, d->prior_h1, wm->prior.n1, wm->prior.l3.w,
                                        wm->prior.l3.b, p2, d->prior_h2), s));
-    DR_TRY(run(G_NT, AM_LNSILU, lin_ln(B, L, d->prior_h2, p2, d->prior_h2, wm->prior.n4, wm->prior.l6.w,
-                                       wm->prior.l6.b, w.plog, L), s));
-    DR_TRY(op_sample(B, d->rows, d->cols, w.plog, L, &nq, t, z_n, ldL, w.idx[(t + 1) & 1],
-                     tp.soft + (long long)t * B * L, L, s));
+    {
+      GemmArgs g = lin_ln(B, L, d->prior_h2, p2, d->prior_h2, wm->prior.n4, wm->prior.l6.w, wm->prior.l6.b, nullptr, 0);
+      with_sampler(g, d, nq, t, z_n, ldL, w.idx[(t + 1) & 1], tp.soft + (long long)t * B * L, L);
+      DR_TRY(run(G_NT, AM_LNSILU, g, s));
+    }
     // reward / continue heads on (h', z') and the actor for step t+1, grouped
     const bool nxt = (t + 1 < H);
     {
@@ -429,27 +471,26 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
       DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, nxt ? 3 : 2, s));
     }
     {
-      GemmArgs p[4];
+      // reward logits kept for one deferred bucket-value pass; continue
+      // probability via the sigmoid epilogue; actor head (next step) fused
+      GemmArgs p[3];
       p[0] = lin_ln(B, d->buckets, d->rew_h2, w.p2r, d->rew_h2, wm->reward.n4, wm->reward.l6.w, wm->reward.l6.b,
-                    w.rlog, d->buckets);
-      p[1] = lin_ln(B, 1, d->cont_h2, w.p2c, d->cont_h2, wm->cont.n4, wm->cont.l6.w, wm->cont.l6.b, w.clog, 1);
+                    w.rlog + (long long)t * d->buckets, (long long)H * d->buckets);
+      p[1] = lin_ln(B, 1, d->cont_h2, w.p2c, d->cont_h2, wm->cont.n4, wm->cont.l6.w, wm->cont.l6.b, continues + t, H);
+      p[1].act = 2;
       if (nxt) {
-        float* pre2 = tp.pre2a + (long long)(t + 1) * a2;
-        p[2] = lin_ln(B, A, a2, pre2, lda2, ac->n4, ac->mu.w, ac->mu.b, mus + (long long)(t + 1) * A, ldA);
+        const long long o = (long long)(t + 1) * A;
+        p[2] = lin_ln(B, 2 * A, a2, tp.pre2a + (long long)(t + 1) * a2, lda2, ac->n4, w.wst, w.bst, nullptr, 0);
         p[2].a_out = tp.x2a + (long long)(t + 1) * a2;
         p[2].ld_aout = lda2;
-        p[3] = lin_ln(B, A, a2, pre2, lda2, ac->n4, ac->ls.w, ac->ls.b, tp.ls_raw + (long long)(t + 1) * A, ldA);
+        with_actor_head(p[2], A, noise, t + 1, deterministic, actions + o, ldA, mus + o, ldA, sigmas + o, ldA,
+                        tp.eps + (long long)(t + 1) * B * A, tp.ls_raw + o, ldA);
       }
-      DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, nxt ? 4 : 2, s));
-    }
-    DR_TRY(op_bucket_value(B, d->buckets, w.rlog, d->buckets, wm->buckets_rew, rewards + t, H, s));
-    DR_TRY(op_sigmoid(B, w.clog, 1, continues + t, H, s));
-    if (nxt) {
-      const long long o = (long long)(t + 1) * A;
-      DR_TRY(op_actor_head(B, A, mus + o, ldA, tp.ls_raw + o, ldA, &noise, t + 1, deterministic, actions + o, ldA,
-                           nullptr, 0, sigmas + o, ldA, tp.eps + (long long)(t + 1) * B * A, s));
+      DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, nxt ? 3 : 2, s));
     }
   }
+  // RewardPredictor.predict for every imagined step at once (rows b*H + t)
+  DR_TRY(op_bucket_value(B * H, d->buckets, w.rlog, d->buckets, wm->buckets_rew, rewards, 1, s));
   return DR_OK;
 }
 

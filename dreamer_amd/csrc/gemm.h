@@ -9,7 +9,7 @@
 
 enum { AM_PLAIN = 0, AM_LNSILU = 1, AM_CONV = 2, AM_CONV_SRC = 3 };
 
-struct GemmArgs {
+struct alignas(16) GemmArgs {
   int M, N, K;
   // A
   const float* A; long long lda;
@@ -27,9 +27,22 @@ struct GemmArgs {
   const float* bias; const float* addend; long long ld_add;
   float* Y; long long ldy;
   float* Y2; long long ldy2; int nsplitY;        // n >= nsplitY -> Y2[m][n-nsplitY]
-  int accumulate, act, out_conv;                 // act 1 = SiLU; out_conv: Y NCHW [frame][N][oh*ow]
+  int accumulate, act, out_conv;                 // act 1 = SiLU, 2 = sigmoid; out_conv: Y NCHW [frame][N][oh*ow]
   float alpha;
+  // fused epilogues of the skinny kernel (epi != EPI_NONE; Y may be NULL)
+  int epi;
+  dr_noise noise; int step;
+  // EPI_SAMPLE: rows of R groups x C classes -> straight-through one-hot
+  int R, C; float unimix;
+  float* z_out; long long ldz; int* idx_out; float* soft_out; long long ld_soft;
+  float* zval_out;  // optional compact [M][R] straight-through value at idx
+  // EPI_ACTOR: columns [mu (A) | log_sig (A)] -> clamp, softplus, tanh(mu + eps*sigma)
+  int na, det;
+  float* act_out; long long ld_act; float* mu_out; long long ld_mu; float* sig_out; long long ld_sig;
+  float* eps_save; float* ls_save; long long ld_ls;
 };
+
+enum { EPI_NONE = 0, EPI_SAMPLE = 1, EPI_ACTOR = 2 };
 
 enum GemmLayout { G_NT = 0, G_NN = 1, G_TN = 2 };
 

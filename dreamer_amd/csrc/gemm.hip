@@ -82,7 +82,9 @@ __device__ __forceinline__ float load_b(const GemmArgs& g, bool kn, int n, int k
 
 template <int BM, int BN, int AMODE, bool A_KM, bool B_KN>
 __global__ __launch_bounds__(256) void k_gemm(GemmBatch gb) {
-  const GemmArgs& g = gb.p[blockIdx.z];
+  __shared__ GemmArgs s_args;
+  dr_stage_args(gb.p[blockIdx.z], s_args, threadIdx.x);
+  const GemmArgs& g = s_args;
   const int tiles_n = (g.N + BN - 1) / BN;
   const int tiles_m = (g.M + BM - 1) / BM;
   if ((int)blockIdx.x >= tiles_m * tiles_n) return;
@@ -244,80 +246,108 @@ __global__ __launch_bounds__(256) void k_gemm(GemmBatch gb) {
 }
 
 // ---------------------------------------------------------------------------
-// Skinny GEMM for per-step activations (M <= 64..256 rows): a workgroup owns
-// MT rows x 16 columns and splits K over its 8 waves.  Operands go straight
-// from global memory into MFMA fragments -- each lane loads 4 consecutive k
-// (one float4) of its row / weight row, and the 16-k chunk's k order is
-// permuted identically for A and B, so MFMA step c of a chunk sums over
-// k = k0 + c + {0,4,8,12}.  No LDS staging and no barriers in the K loop; the
-// 8 partial accumulators are reduced through LDS in fixed order
-// (deterministic), then the shared epilogue runs.
+// Skinny GEMM for per-step activations (M up to a few thousand rows, N
+// moderate): a workgroup owns MT rows x NT columns and splits K over its 8
+// waves.  Operands go straight from global memory into MFMA fragments -- each
+// lane loads 4 consecutive k (one float4) of its row / weight row, and the
+// 16-k chunk's k order is permuted identically for A and B, so MFMA step c of
+// a chunk sums k = k0 + c + {0,4,8,12}.  No LDS staging of the weights and no
+// barriers in the K loop; the weight chunk is prefetched one step ahead.
+// With LayerNorm+SiLU on load, the MT input rows are staged once in LDS (one
+// global pass) and the row statistics come from there.  The 8 partial
+// accumulators are reduced through LDS in fixed order (deterministic), then
+// either the element epilogue or a fused row epilogue runs:
+//   EPI_SAMPLE  softmax / 1% unimix / argmax(p_hat / Exp(1)) / one-hot STE per
+//               latent group (VAE.py:88-98, DynamicsPredictors.py:33-39)
+//   EPI_ACTOR   mu, clamp(log_sig), softplus + 1e-3, tanh(mu + eps*sigma)
+//               (Agent.py:196-210)
 // ---------------------------------------------------------------------------
-template <int AMODE, bool VEC>
-__device__ __forceinline__ void skinny_load_a(const GemmArgs& g, int m, int kq, float mean, float rstd, float (&a)[4]) {
-  const int M = g.M, K = g.K;
-  if (m >= M) {
-    a[0] = a[1] = a[2] = a[3] = 0.f;
-    return;
-  }
-  if (VEC) {
-    if (kq >= K) {
-      a[0] = a[1] = a[2] = a[3] = 0.f;
-      return;
-    }
-    const float* src = (kq < g.ksplitA) ? g.A + (long long)m * g.lda + kq
-                                        : g.A2 + (long long)m * g.lda2 + (kq - g.ksplitA);
-    const float4 v = *reinterpret_cast<const float4*>(src);
-    a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
-  } else {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int k = kq + c;
-      if (k >= K) { a[c] = 0.f; continue; }
-      a[c] = (k < g.ksplitA) ? g.A[(long long)m * g.lda + k] : g.A2[(long long)m * g.lda2 + (k - g.ksplitA)];
-    }
-  }
-  if (AMODE == AM_LNSILU) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int k = kq + c;
-      if (k < K) {
-        float x = (a[c] - mean) * rstd;
-        x = x * g.ln_g[k] + g.ln_b[k];
-        a[c] = x / (1.0f + expf(-x));
-      }
-    }
-  }
+#ifdef DR_PHASE_TIMING
+__device__ long long dr_tbuf_gemm[1024 * DR_TS_SLOTS];
+extern "C" int dr_debug_tbuf_gemm(long long* out, int n) {  // read, then clear
+  const int rc = (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(dr_tbuf_gemm), (size_t)n * sizeof(long long));
+  static long long zeros[1024 * DR_TS_SLOTS];
+  return rc | (int)hipMemcpyToSymbol(HIP_SYMBOL(dr_tbuf_gemm), zeros, sizeof(zeros));
 }
+#endif
+#define SK_LN_MAXF 33280  // floats of staged LayerNorm rows (MT * (K + 4)); 130 KB of the 160 KB LDS
+#define SK_LN_MAXK 2048   // LayerNorm width staged with its gamma / beta
+#define SK_STAGE 8        // float4 staging loads in flight per thread
+
+// hot operands of a skinny problem as wave-uniform scalars (see dr_uni)
+struct SkOps {
+  const float *A, *A2, *W, *W2;
+  int lda, lda2, ksA, ldb, ldb2, ksB, nsB, M, N, K;
+};
 
 template <bool B_KN, bool VEC>
-__device__ __forceinline__ void skinny_load_b(const GemmArgs& g, int n, int kq, float (&b)[4]) {
-  const int N = g.N, K = g.K;
-  if (n >= N) {
-    b[0] = b[1] = b[2] = b[3] = 0.f;
-    return;
-  }
+__device__ __forceinline__ void skinny_load_b(const SkOps& o, int n, int kq, float (&b)[4]) {
   if (!B_KN && VEC) {
-    if (kq >= K) {
-      b[0] = b[1] = b[2] = b[3] = 0.f;
-      return;
-    }
-    const float4 v = *reinterpret_cast<const float4*>(g.W + (long long)n * g.ldb + kq);
+    const bool ok = (n < o.N) && (kq < o.K);
+    float4 v = dr_ld4(o.W, ok ? (unsigned)(n * o.ldb + kq) : 0u);
+    if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
     b[0] = v.x; b[1] = v.y; b[2] = v.z; b[3] = v.w;
     return;
   }
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int k = kq + c;
-    b[c] = (k < K) ? load_b(g, B_KN, n, k) : 0.f;
+    const bool ok = (n < o.N) && (k < o.K);
+    float v;
+    if (!B_KN) {
+      v = dr_ld1(o.W, ok ? (unsigned)(n * o.ldb + k) : 0u);
+    } else if (k >= o.ksB) {  // KN second segment: rows past ksplitB or columns past nsplitB
+      v = dr_ld1(o.W2, ok ? (unsigned)((k - o.ksB) * o.ldb2 + n) : 0u);
+    } else if (n >= o.nsB) {
+      v = dr_ld1(o.W2, ok ? (unsigned)(k * o.ldb2 + n - o.nsB) : 0u);
+    } else {
+      v = dr_ld1(o.W, ok ? (unsigned)(k * o.ldb + n) : 0u);
+    }
+    b[c] = ok ? v : 0.f;
   }
 }
 
-__device__ __forceinline__ void epilogue_store(const GemmArgs& g, int m, int n, float acc) {
+// A rows: the 16-k chunk starting at k16 lies in one segment (A below ksA, A2
+// above) unless ksA is not a multiple of 16, in which case lanes pick theirs
+template <bool VEC>
+__device__ __forceinline__ void skinny_load_a(const SkOps& o, int m, int k16, int kq, float (&a)[4]) {
+  if (VEC) {
+    const bool ok = (m < o.M) && (kq < o.K);
+    float4 v;
+    if (k16 + 16 <= o.ksA) {
+      v = dr_ld4(o.A, ok ? (unsigned)(m * o.lda + kq) : 0u);
+    } else if (k16 >= o.ksA) {
+      v = dr_ld4(o.A2, ok ? (unsigned)(m * o.lda2 + kq - o.ksA) : 0u);
+    } else {
+      const float* src = (kq < o.ksA) ? o.A + (long long)m * o.lda + kq : o.A2 + (long long)m * o.lda2 + (kq - o.ksA);
+      v = *reinterpret_cast<const float4*>(ok ? src : o.A);
+    }
+    if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+    a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int k = kq + c;
+      const bool ok = (m < o.M) && (k < o.K);
+      float v;
+      if (k < o.ksA) v = dr_ld1(o.A, ok ? (unsigned)(m * o.lda + k) : 0u);
+      else v = dr_ld1(o.A2, ok ? (unsigned)(m * o.lda2 + k - o.ksA) : 0u);
+      a[c] = ok ? v : 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ float epi_act(const GemmArgs& g, float v) {
+  if (g.act == 1) return v / (1.0f + expf(-v));
+  if (g.act == 2) return 1.0f / (1.0f + expf(-v));
+  return v;
+}
+
+__device__ __forceinline__ void epilogue_store_b(const GemmArgs& g, int m, int n, float acc, float bias) {
   float v = (g.alpha == 1.0f) ? acc : g.alpha * acc;
-  if (g.bias) v = v + g.bias[n];
+  if (g.bias) v = v + bias;
   if (g.addend) v = v + g.addend[(long long)m * g.ld_add + n];
-  if (g.act == 1) v = v / (1.0f + expf(-v));
+  v = epi_act(g, v);
   float* dst;
   if (n < g.nsplitY) dst = g.Y + (long long)m * g.ldy + n;
   else dst = g.Y2 + (long long)m * g.ldy2 + (n - g.nsplitY);
@@ -325,89 +355,353 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, int m, int n, 
   else *dst = v;
 }
 
-template <int MT, int AMODE, bool B_KN, bool VEC>
+template <int MT, int NT, int AMODE, bool B_KN, bool VEC, int EPI>
 __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
-  constexpr int NWAVE = 8, FT = MT / 16;
-  const GemmArgs& g = gb.p[blockIdx.z];
-  const int M = g.M, N = g.N, K = g.K;
-  const int tiles_n = (N + 15) / 16;
+  constexpr int NWAVE = 8, FT = MT / 16, FN = NT / 16;
+  __shared__ GemmArgs s_args;
+  dr_stage_args(gb.p[blockIdx.z], s_args, threadIdx.x);
+  const GemmArgs& g = s_args;
+  SkOps o;
+  o.M = dr_uni(g.M); o.N = dr_uni(g.N); o.K = dr_uni(g.K);
+  o.A = dr_uni(g.A); o.A2 = dr_uni(g.A2); o.W = dr_uni(g.W);
+  o.lda = dr_uni((int)g.lda); o.lda2 = dr_uni((int)g.lda2); o.ksA = dr_uni(g.ksplitA); o.ldb = dr_uni((int)g.ldb);
+  o.W2 = dr_uni(g.W2); o.ldb2 = dr_uni((int)g.ldb2); o.ksB = dr_uni(g.ksplitB); o.nsB = dr_uni(g.nsplitB);
+  const int M = o.M, N = o.N, K = o.K;
+  const int tiles_n = (N + NT - 1) / NT;
   const int tiles_m = (M + MT - 1) / MT;
-  if ((int)blockIdx.x >= tiles_m * tiles_n) return;
-  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x - tm * tiles_n;
-  const int m0 = tm * MT, n0 = tn * 16;
+  // logical tiles column-major: the row tiles reading one weight slice are
+  // adjacent and share an XCD's L2
+  const int lt = dr_xcd_tile(blockIdx.x, tiles_m * tiles_n);
+  if (lt < 0) return;
+  const int tn = lt / tiles_m, tm = lt - tn * tiles_m;
+  const int m0 = tm * MT, n0 = tn * NT;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r = lane & 15, q = lane >> 4;
+  DR_TS(dr_tbuf_gemm, 0);
 
+  constexpr int RED = NWAVE * FT * FN * 4 * 64;
+  constexpr int LNF = (AMODE == AM_LNSILU) ? SK_LN_MAXF : 0;
+  constexpr int SMEM = (RED > LNF ? RED : LNF);
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
   __shared__ float s_mean[MT], s_rstd[MT];
-  __shared__ float red[NWAVE][FT][4][64];
+  __shared__ float s_out[MT][NT + 1];
+  constexpr int LNK = (AMODE == AM_LNSILU) ? SK_LN_MAXK : 1;
+  __shared__ float s_lng[LNK], s_lnb[LNK];
+  // bias of the output columns this thread finalises, issued now and waited
+  // for only in the epilogue
+  constexpr int NEPI = (FT * FN * 256 + 511) / 512;
+  float ebias[NEPI];
+  {
+    const float* bias = dr_uni(g.bias);
+#pragma unroll
+    for (int i = 0; i < NEPI; ++i) {
+      const int x = tid + 512 * i;
+      const int n = n0 + ((x >> 8) % FN) * 16 + (x & 15);
+      const bool ok = bias && x < FT * FN * 256 && n < N;
+      const float v = dr_ld1(ok ? bias : o.W, ok ? (unsigned)n : 0u);
+      ebias[i] = ok ? v : 0.f;
+    }
+  }
 
+  const int kw = ((K + NWAVE * 16 - 1) / (NWAVE * 16)) * 16;
+  const int kb = wave * kw;
+  const int ke = min(K, kb + kw);
+
+  // K loop in batches of PRE 16-k chunks: every load of a batch is issued
+  // before its first MFMA, so a wave pays one memory round trip per batch
+  // (one in total for K <= PRE*16*8 = 1024).  The first batch of weights (and
+  // of plain A rows) is issued before the LayerNorm staging.
+  constexpr int PRE = (FT >= 4) ? 4 : 8;
+  float bb[PRE][FN][4];
+  float aa[PRE][FT][4];
+  auto load_batch = [&](int kc) {
+#pragma unroll
+    for (int p = 0; p < PRE; ++p) {
+      const int k16 = kc + 16 * p;
+      const int kq = k16 + 4 * q;
+      const bool live = k16 < ke;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        if (live) {
+          skinny_load_b<B_KN, VEC>(o, n0 + j * 16 + r, kq, bb[p][j]);
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) bb[p][j][c] = 0.f;
+        }
+      }
+      if (AMODE != AM_LNSILU) {
+#pragma unroll
+        for (int t = 0; t < FT; ++t) {
+          if (live) {
+            skinny_load_a<VEC>(o, m0 + t * 16 + r, k16, kq, aa[p][t]);
+          } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) aa[p][t][c] = 0.f;
+          }
+        }
+      }
+    }
+  };
+  if (kb < ke) load_batch(kb);
+
+  // LayerNorm rows staged in LDS with a padded stride (K + 4 floats: the 16
+  // rows an MFMA fragment reads fall in distinct banks)
+  const int KP = K + 4;
+  const bool ln_lds = (AMODE == AM_LNSILU) && (MT * KP <= SK_LN_MAXF) && VEC && (K <= LNK);
+  DR_TS(dr_tbuf_gemm, 1);
   if (AMODE == AM_LNSILU) {
-    for (int rr = wave; rr < MT; rr += NWAVE) {
-      const int m = m0 + rr;
-      float mean = 0.f, rstd = 0.f;
-      if (m < M) {
-        const float* row = g.A + (long long)m * g.lda;
-        float s = 0.f;
+    if (ln_lds) {
+      // one global pass: every float4 of the MT rows is issued before the
+      // first LDS write (SK_STAGE per thread), statistics come from LDS
+      const int K4 = K >> 2;
+      const int total = MT * K4;
+      for (int e0 = 0; e0 < total; e0 += 512 * SK_STAGE) {
+        float4 v[SK_STAGE];
+#pragma unroll
+        for (int i = 0; i < SK_STAGE; ++i) {
+          const int e = e0 + tid + 512 * i;
+          const int rr = e / K4, k4 = e - rr * K4, m = m0 + rr;
+          const bool ok = e < total && m < M;
+          v[i] = dr_ld4(o.A, ok ? (unsigned)(m * o.lda + 4 * k4) : 0u);
+          if (!ok) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < SK_STAGE; ++i) {
+          const int e = e0 + tid + 512 * i;
+          const int rr = e / K4, k4 = e - rr * K4;
+          if (e < total) *reinterpret_cast<float4*>(&smem[rr * KP + 4 * k4]) = v[i];
+        }
+      }
+      const float* lg = dr_uni(g.ln_g);
+      const float* lb = dr_uni(g.ln_b);
+      for (int k = tid; k < K; k += 512) {
+        s_lng[k] = dr_ld1(lg, (unsigned)k);
+        s_lnb[k] = dr_ld1(lb, (unsigned)k);
+      }
+      __syncthreads();
+      DR_TS(dr_tbuf_gemm, 2);
+      for (int rr = wave; rr < MT; rr += NWAVE) {
+        const float* row = &smem[rr * KP];
+        float s = 0.f, v = 0.f;
         for (int k = lane; k < K; k += 64) s += row[k];
-        mean = wave_sum(s) / (float)K;
-        float v = 0.f;
+        const float mean = wave_sum(s) / (float)K;
         for (int k = lane; k < K; k += 64) {
           const float d = row[k] - mean;
           v += d * d;
         }
-        rstd = 1.0f / sqrtf(wave_sum(v) / (float)K + 1e-5f);
+        const float rstd = 1.0f / sqrtf(wave_sum(v) / (float)K + 1e-5f);
+        if (lane == 0) {
+          s_mean[rr] = mean;
+          s_rstd[rr] = rstd;
+        }
       }
-      if (lane == 0) {
-        s_mean[rr] = mean;
-        s_rstd[rr] = rstd;
+    } else {
+      for (int rr = wave; rr < MT; rr += NWAVE) {
+        const int m = m0 + rr;
+        float mean = 0.f, rstd = 0.f;
+        if (m < M) {
+          const float* row = o.A + (long long)m * o.lda;
+          float s = 0.f, v = 0.f;
+          for (int k = lane; k < K; k += 64) s += row[k];
+          mean = wave_sum(s) / (float)K;
+          for (int k = lane; k < K; k += 64) {
+            const float d = row[k] - mean;
+            v += d * d;
+          }
+          rstd = 1.0f / sqrtf(wave_sum(v) / (float)K + 1e-5f);
+        }
+        if (lane == 0) {
+          s_mean[rr] = mean;
+          s_rstd[rr] = rstd;
+        }
       }
     }
     __syncthreads();
+    DR_TS(dr_tbuf_gemm, 3);
   }
 
-  f32x4 acc[FT];
-#pragma unroll
-  for (int t = 0; t < FT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const int kw = ((K + NWAVE * 16 - 1) / (NWAVE * 16)) * 16;
-  const int kb = wave * kw;
-  const int ke = min(K, kb + kw);
-  const bool store_a = (g.a_out != nullptr) && (tn == 0);
-#pragma unroll 2
-  for (int k0 = kb; k0 < ke; k0 += 16) {
-    const int kq = k0 + 4 * q;
-    float b[4];
-    float a[FT][4];
-    skinny_load_b<B_KN, VEC>(g, n0 + r, kq, b);
-#pragma unroll
-    for (int t = 0; t < FT; ++t) {
-      const int ml = t * 16 + r;
-      skinny_load_a<AMODE, VEC>(g, m0 + ml, kq, (AMODE == AM_LNSILU) ? s_mean[ml] : 0.f,
-                                (AMODE == AM_LNSILU) ? s_rstd[ml] : 0.f, a[t]);
-      if (store_a && m0 + ml < M) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (kq + c < K) g.a_out[(long long)(m0 + ml) * g.ld_aout + kq + c] = a[t][c];
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int t = 0; t < FT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][c], b[c], acc[t], 0, 0, 0);
-  }
+  f32x4 acc[FT][FN];
 #pragma unroll
   for (int t = 0; t < FT; ++t)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) red[wave][t][j][lane] = acc[t][j];
+    for (int j = 0; j < FN; ++j) acc[t][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float* a_out = dr_uni(g.a_out);
+  const int ld_aout = dr_uni((int)g.ld_aout);
+  const bool store_a = (a_out != nullptr) && (tn == 0);
+  const float* lg = dr_uni(g.ln_g);
+  const float* lb = dr_uni(g.ln_b);
+  for (int kc = kb; kc < ke; kc += PRE * 16) {
+    if (kc != kb) load_batch(kc);
+    if (AMODE == AM_LNSILU) {
+#pragma unroll
+      for (int p = 0; p < PRE; ++p) {
+        const int k16 = kc + 16 * p;
+        const int kq = k16 + 4 * q;
+        const bool live = k16 < ke;
+#pragma unroll
+        for (int t = 0; t < FT; ++t) {
+          const int ml = t * 16 + r, m = m0 + ml;
+          if (!live) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) aa[p][t][c] = 0.f;
+          } else if (ln_lds) {
+            if (m < M && kq < K) {
+              const float4 v = *reinterpret_cast<const float4*>(&smem[ml * KP + kq]);
+              aa[p][t][0] = v.x; aa[p][t][1] = v.y; aa[p][t][2] = v.z; aa[p][t][3] = v.w;
+            } else {
+              aa[p][t][0] = aa[p][t][1] = aa[p][t][2] = aa[p][t][3] = 0.f;
+            }
+          } else {
+            skinny_load_a<VEC>(o, m, k16, kq, aa[p][t]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < PRE; ++p) {
+      if (kc + 16 * p >= ke) break;
+      const int kq = kc + 16 * p + 4 * q;
+#pragma unroll
+      for (int t = 0; t < FT; ++t) {
+        const int ml = t * 16 + r, m = m0 + ml;
+        if (AMODE == AM_LNSILU) {
+          const float mean = s_mean[ml], rstd = s_rstd[ml];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int k = kq + c;
+            if (m < M && k < K) {
+              float x = (aa[p][t][c] - mean) * rstd;
+              if (ln_lds) x = x * s_lng[k] + s_lnb[k];
+              else x = x * dr_ld1(lg, (unsigned)k) + dr_ld1(lb, (unsigned)k);
+              aa[p][t][c] = dr_silu_fast(x);
+            }
+          }
+        }
+        if (store_a && m < M) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (kq + c < K) a_out[(unsigned)(m * ld_aout + kq + c)] = aa[p][t][c];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int t = 0; t < FT; ++t)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[p][t][c], bb[p][j][c], acc[t][j], 0, 0, 0);
+    }
+  }
+  DR_TS(dr_tbuf_gemm, 4);
+  if (AMODE == AM_LNSILU) __syncthreads();  // smem held the staged rows
+#pragma unroll
+  for (int t = 0; t < FT; ++t)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) smem[(((wave * FT + t) * FN + j) * 4 + e) * 64 + lane] = acc[t][j][e];
   __syncthreads();
-  // output element e = (t, j, l): D[row 4*(l>>4)+j][col l&15] of m-tile t
-  for (int e = tid; e < FT * 256; e += 512) {
-    const int t = e >> 8, j = (e >> 6) & 3, l = e & 63;
+  DR_TS(dr_tbuf_gemm, 5);
+  // element (t, j, e, l): D[row 4*(l>>4)+e][col l&15] of tile (t, j)
+#pragma unroll
+  for (int i = 0; i < NEPI; ++i) {
+    const int x = tid + 512 * i;
+    if (x >= FT * FN * 256) break;
+    const int l = x & 63, e = (x >> 6) & 3, tj = x >> 8;
     float v = 0.f;
 #pragma unroll
-    for (int w = 0; w < NWAVE; ++w) v += red[w][t][j][l];
-    const int m = m0 + t * 16 + 4 * (l >> 4) + j, n = n0 + (l & 15);
-    if (m < M && n < N) epilogue_store(g, m, n, v);
+    for (int w = 0; w < NWAVE; ++w) v += smem[((w * FT * FN + tj) * 4 + e) * 64 + l];
+    const int t = tj / FN, j = tj - t * FN;
+    const int ml = t * 16 + 4 * (l >> 4) + e, nl = j * 16 + (l & 15);
+    const int m = m0 + ml, n = n0 + nl;
+    if (EPI == EPI_NONE || g.epi == EPI_NONE) {
+      if (m < M && n < N) epilogue_store_b(g, m, n, v, ebias[i]);
+    } else {
+      if (m < M && n < N) {
+        float y = v + ebias[i];
+        if (g.Y) g.Y[(long long)m * g.ldy + n] = y;
+        s_out[ml][nl] = y;
+      }
+    }
   }
+  if (EPI == EPI_SAMPLE) {
+    // groups of C classes inside this NT-column tile; W lanes per group
+    __syncthreads();
+    const int C = g.C;
+    int W = 1;
+    while (W < C) W <<= 1;
+    const int gpr = NT / C;                // groups per row in this tile
+    const int npairs = MT * gpr;           // (row, group) pairs
+    const int per_wave = 64 / W;
+    for (int pbase = wave * per_wave; pbase < npairs; pbase += NWAVE * per_wave) {
+      const int pidx = pbase + lane / W, c = lane % W;
+      const bool valid = pidx < npairs;
+      const int ml = valid ? pidx / gpr : 0, gl = valid ? pidx - ml * gpr : 0;
+      const int m = m0 + ml, grp = (n0 / C) + gl;
+      const bool act = valid && c < C && m < M && (n0 + gl * C + c) < N;
+      const float x = act ? s_out[ml][gl * C + c] : -INFINITY;
+      const float mx = group_max(x, W);
+      const float ex = act ? expf(x - mx) : 0.0f;
+      const float se = group_sum(ex, W);
+      const float p = ex / se;
+      const float pu = act ? (0.99f * p + g.unimix) : 0.0f;
+      const float sp = group_sum(pu, W);
+      const float ph = pu / sp;
+      float qv = 1.0f;
+      const int Rg = g.R;
+      if (act) {
+        if (g.noise.q) qv = g.noise.q[((long long)g.step * M * Rg + (long long)m * Rg + grp) * C + c];
+        else qv = dr_exp1(g.noise.rng, (uint32_t)(g.noise.stream + g.step), (uint32_t)(g.noise.row0 + m),
+                          (uint32_t)(grp * C + c));
+      }
+      float best = act ? ph / qv : -INFINITY;
+      int bi = act ? c : 0x7fffffff;
+      for (int o = W >> 1; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ob > best || (ob == best && oi < bi)) {
+          best = ob;
+          bi = oi;
+        }
+      }
+      if (act) {
+        g.z_out[(long long)m * g.ldz + grp * C + c] = (c == bi) ? ((1.0f + pu) - pu) : 0.0f;
+        if (g.soft_out) g.soft_out[(long long)m * g.ld_soft + grp * C + c] = p;
+        if (g.idx_out && c == 0) g.idx_out[m * Rg + grp] = bi;
+        if (g.zval_out && c == bi) g.zval_out[m * Rg + grp] = (1.0f + pu) - pu;
+      }
+    }
+  } else if (EPI == EPI_ACTOR && g.epi == EPI_ACTOR) {
+    __syncthreads();
+    const int A = g.na;
+    for (int x = tid; x < MT * A; x += 512) {
+      const int ml = x / A, i = x - ml * A, m = m0 + ml;
+      if (m >= M) continue;
+      const float muv = s_out[ml][i];
+      const float lr = s_out[ml][A + i];
+      const float ls = fminf(fmaxf(lr, -5.0f), 2.0f);
+      const float sg = dr_softplus(ls) + 1e-3f;
+      float av;
+      if (g.det) {
+        av = tanhf(muv);
+      } else {
+        float e;
+        if (g.noise.eps) e = g.noise.eps[((long long)g.step * M + m) * A + i];
+        else e = dr_normal(g.noise.rng, (uint32_t)(g.noise.stream + g.step), (uint32_t)(g.noise.row0 + m),
+                           (uint32_t)i);
+        if (g.eps_save) g.eps_save[(long long)m * A + i] = e;
+        av = tanhf(muv + e * sg);
+      }
+      if (g.act_out) g.act_out[(long long)m * g.ld_act + i] = av;
+      if (g.mu_out) g.mu_out[(long long)m * g.ld_mu + i] = muv;
+      if (g.sig_out) g.sig_out[(long long)m * g.ld_sig + i] = sg;
+      if (g.ls_save) g.ls_save[(long long)m * g.ld_ls + i] = lr;
+    }
+  }
+}
+
+__device__ __forceinline__ void epilogue_store(const GemmArgs& g, int m, int n, float acc) {
+  epilogue_store_b(g, m, n, acc, g.bias ? g.bias[n] : 0.f);
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -419,31 +713,62 @@ static bool skinny_vec_ok(const GemmArgs& g, bool b_kn) {
   return true;
 }
 
-template <int MT, int AMODE, bool B_KN>
+// the skinny kernel addresses A, A2, W and a_out with 32-bit element offsets
+static bool skinny_offsets_ok(const GemmArgs& g, bool b_kn) {
+  const long long lim = 1LL << 30;
+  if ((long long)g.M * g.lda >= lim || (long long)g.M * g.lda2 >= lim) return false;
+  if ((b_kn ? (long long)g.K * g.ldb : (long long)g.N * g.ldb) >= lim) return false;
+  if (g.W2 && (long long)(g.K + g.N) * g.ldb2 >= lim) return false;
+  if (g.a_out && (long long)g.M * g.ld_aout >= lim) return false;
+  return true;
+}
+
+template <int MT, int NT, int AMODE, bool B_KN, int EPI>
 static void launch_skinny(const GemmBatch& gb, int count, bool vec, hipStream_t s) {
   int maxt = 0;
   for (int i = 0; i < count; ++i) {
-    const int t = dr_cdiv(gb.p[i].M, MT) * dr_cdiv(gb.p[i].N, 16);
+    const int t = dr_cdiv(gb.p[i].M, MT) * dr_cdiv(gb.p[i].N, NT);
     maxt = t > maxt ? t : maxt;
   }
   if (maxt == 0) return;
-  if (vec) hipLaunchKernelGGL((k_gemm_skinny<MT, AMODE, B_KN, true>), dim3(maxt, 1, count), dim3(512), 0, s, gb);
-  else hipLaunchKernelGGL((k_gemm_skinny<MT, AMODE, B_KN, false>), dim3(maxt, 1, count), dim3(512), 0, s, gb);
+  if (vec)
+    hipLaunchKernelGGL((k_gemm_skinny<MT, NT, AMODE, B_KN, true, EPI>), dim3(dr_xcd_grid(maxt), 1, count), dim3(512),
+                       0, s, gb);
+  else
+    hipLaunchKernelGGL((k_gemm_skinny<MT, NT, AMODE, B_KN, false, EPI>), dim3(dr_xcd_grid(maxt), 1, count), dim3(512),
+                       0, s, gb);
 }
+
+// tile-shape override for the kernel microbenchmark (0 = heuristic)
+static int g_force_nt = 0;
+extern "C" void dr_debug_gemm_tile(int nt) { g_force_nt = nt; }
 
 template <int AMODE, bool B_KN>
 static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
-  int maxM = 0;
+  int maxM = 0, epi = EPI_NONE;
   bool vec = true;
   for (int i = 0; i < count; ++i) {
     const GemmArgs& g = gb.p[i];
     if (g.out_conv) return false;
+    if ((g.epi == EPI_SAMPLE) != (gb.p[0].epi == EPI_SAMPLE)) return false;  // 32-column tiles for all or none
+    if (g.epi != EPI_NONE) epi = g.epi;
     maxM = g.M > maxM ? g.M : maxM;
+    if (!skinny_offsets_ok(g, B_KN)) return false;
     vec = vec && skinny_vec_ok(g, B_KN);
   }
-  if (maxM > 256) return false;
-  if (maxM > 64) launch_skinny<64, AMODE, B_KN>(gb, count, vec, s);
-  else launch_skinny<16, AMODE, B_KN>(gb, count, vec, s);
+  if (maxM > 4096) return false;
+  if (epi == EPI_SAMPLE) {
+    if (maxM > 64) launch_skinny<64, 32, AMODE, B_KN, EPI_SAMPLE>(gb, count, vec, s);
+    else launch_skinny<16, 32, AMODE, B_KN, EPI_SAMPLE>(gb, count, vec, s);
+  } else if (epi == EPI_ACTOR) {
+    if (maxM > 64) launch_skinny<64, 16, AMODE, B_KN, EPI_ACTOR>(gb, count, vec, s);
+    else launch_skinny<16, 16, AMODE, B_KN, EPI_ACTOR>(gb, count, vec, s);
+  } else {
+    if (maxM > 64) launch_skinny<64, 16, AMODE, B_KN, EPI_NONE>(gb, count, vec, s);
+    else if (g_force_nt == 32) launch_skinny<16, 32, AMODE, B_KN, EPI_NONE>(gb, count, vec, s);
+    else if (g_force_nt == 64) launch_skinny<16, 64, AMODE, B_KN, EPI_NONE>(gb, count, vec, s);
+    else launch_skinny<16, 16, AMODE, B_KN, EPI_NONE>(gb, count, vec, s);
+  }
   return true;
 }
 
@@ -475,6 +800,22 @@ int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hip
   if (count < 1 || count > 4) {
     dr_set_error("gemm_launch: bad problem count %d", count);
     return DR_E_INVALID;
+  }
+  for (int i = 0; i < count; ++i) {
+    const GemmArgs& g = probs[i];
+    if (g.epi == EPI_SAMPLE && (g.C < 1 || g.C > 32 || 32 % g.C != 0 || g.N != g.R * g.C)) {
+      dr_set_error("gemm_launch: sampler epilogue needs C | 32 and N == R*C (C=%d R=%d N=%d)", g.C, g.R, g.N);
+      return DR_E_INVALID;
+    }
+    if (g.epi == EPI_ACTOR && (g.N != 2 * g.na || g.na > 8)) {
+      dr_set_error("gemm_launch: actor epilogue needs N == 2A <= 16");
+      return DR_E_INVALID;
+    }
+    if (g.epi != EPI_NONE && (lay != G_NT || (amode != AM_PLAIN && amode != AM_LNSILU) || g.M > 4096 ||
+                              !skinny_offsets_ok(g, false))) {
+      dr_set_error("gemm_launch: fused epilogues need the NT skinny path");
+      return DR_E_INVALID;
+    }
   }
   GemmBatch gb;
   for (int i = 0; i < count; ++i) {

@@ -2,11 +2,10 @@
 #pragma once
 #include "common.h"
 
-struct GruArgs {
+struct alignas(16) GruArgs {
   int B, Hd, R, C, A;
   const int* idx;       // [B][R] sampled class per latent group
-  const float* z;       // straight-through latents (value at idx), row stride ldz
-  long long ldz;
+  const float* zval;    // [B][R] straight-through latent value at idx
   const float* a;       // actions [B][A], row stride lda
   long long lda;
   const float* h;       // previous hidden (NULL = zeros), row stride ldh
@@ -22,4 +21,4 @@ struct GruArgs {
 
 int op_gru_fused(const GruArgs& g, hipStream_t s);
 int op_transpose(int rows, int cols, const float* in, float* out, hipStream_t s);
-int op_onehot_index(int M, int R, int C, const float* z, long long ldz, int* idx, hipStream_t s);
+int op_onehot_index(int M, int R, int C, const float* z, long long ldz, int* idx, float* zval, hipStream_t s);

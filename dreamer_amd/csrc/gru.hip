@@ -32,142 +32,210 @@ int op_transpose(int rows, int cols, const float* in, float* out, hipStream_t s)
 }
 
 // index of the non-zero entry of each one-hot group (z values are exactly 0
-// off the sample); groups with no non-zero entry get index 0 and value 0
-__global__ void k_onehot_index(int M, int R, int C, const float* z, long long ldz, int* idx) {
+// off the sample) and its value; groups with no non-zero entry get (0, 0)
+__global__ void k_onehot_index(int M, int R, int C, const float* z, long long ldz, int* idx, float* zval) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M * R) return;
   const int m = i / R, g = i - m * R;
   const float* zz = z + (long long)m * ldz + g * C;
   int k = 0;
+  float v = 0.f;
   for (int c = 0; c < C; ++c)
-    if (zz[c] != 0.0f) { k = c; break; }
+    if (zz[c] != 0.0f) {
+      k = c;
+      v = zz[c];
+      break;
+    }
   idx[i] = k;
+  zval[i] = v;
 }
 
-int op_onehot_index(int M, int R, int C, const float* z, long long ldz, int* idx, hipStream_t s) {
+int op_onehot_index(int M, int R, int C, const float* z, long long ldz, int* idx, float* zval, hipStream_t s) {
   if (M * R == 0) return DR_OK;
-  hipLaunchKernelGGL(k_onehot_index, dim3((M * R + 255) / 256), dim3(256), 0, s, M, R, C, z, ldz, idx);
+  hipLaunchKernelGGL(k_onehot_index, dim3((M * R + 255) / 256), dim3(256), 0, s, M, R, C, z, ldz, idx, zval);
   return dr_check_launch("onehot_index");
 }
 
-template <bool VEC>
-__global__ __launch_bounds__(512) void k_gru_fused(GruArgs g) {
-  constexpr int NW = 8;
-  const int Hd = g.Hd, B = g.B;
-  const int tiles_j = (Hd + 15) / 16;
-  const int tm = blockIdx.x / tiles_j, tj = blockIdx.x - tm * tiles_j;
+// Work split inside the 512-thread workgroup (16 batch rows x 16 hidden units,
+// all three gates):
+//   waves 0-3  gh = h W_hh^T on the exact-f32 MFMA, K split four ways, every
+//              operand of a wave issued before its first MFMA;
+//   waves 4-7  gi by gather: one thread per (row, gate, 4 units) reads the
+//              sampled W_ih^T row of every latent group as one float4
+//              (coalesced along the hidden units) and accumulates
+//              z_value * w in group order, then actions and bias.
+// The two halves run concurrently (one MFMA wave and one gather wave per SIMD)
+// and meet at a single barrier before the gate math.
+#define GRU_MW 4       // MFMA waves
+#define GRU_PRE 8      // 16-k chunks per MFMA wave held in registers
+#define GRU_MAXR 32    // latent groups
+#define GRU_MAXA 8     // actions
+
+#ifdef DR_PHASE_TIMING
+__device__ long long dr_tbuf_gru[1024 * DR_TS_SLOTS];
+extern "C" int dr_debug_tbuf_gru(long long* out, int n) {  // read, then clear
+  const int rc = (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(dr_tbuf_gru), (size_t)n * sizeof(long long));
+  static long long zeros[1024 * DR_TS_SLOTS];
+  return rc | (int)hipMemcpyToSymbol(HIP_SYMBOL(dr_tbuf_gru), zeros, sizeof(zeros));
+}
+#endif
+
+__global__ __launch_bounds__(512) void k_gru_fused(GruArgs ga) {
+  __shared__ GruArgs g;
+  dr_stage_args(ga, g, threadIdx.x);
+  const int Hd = dr_uni(g.Hd), B = dr_uni(g.B);
+  const int R = dr_uni(g.R), C = dr_uni(g.C), A = dr_uni(g.A), L = R * C;
+  // logical tiles unit-major: the row tiles of one unit slice (same W_hh rows,
+  // same W_ih^T columns) are adjacent and land on one XCD
+  const int tiles_j = (Hd + 15) / 16, tiles_m = (B + 15) / 16;
+  const int lt = dr_xcd_tile(blockIdx.x, tiles_j * tiles_m);
+  if (lt < 0) return;
+  const int tj = lt / tiles_m, tm = lt - tj * tiles_m;
   const int m0 = tm * 16, j0 = tj * 16;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int r = lane & 15, q = lane >> 4;
+  DR_TS(dr_tbuf_gru, 0);
 
-  __shared__ float red[NW][3][4][64];
-  __shared__ float gh_s[16][3][16];
+  __shared__ float red[GRU_MW][3][4][64];
   __shared__ float gi_s[16][3][16];
-  __shared__ int idx_s[16][64];
-  __shared__ float zv_s[16][64];
+  __shared__ float gh_s[16][3][16];
 
-  // stage the one-hot indices / straight-through values of the 16 rows
-  const int R = g.R, C = g.C;
-  for (int e = tid; e < 16 * R; e += 512) {
-    const int ml = e / R, grp = e - ml * R, m = m0 + ml;
-    int k = 0;
-    float v = 0.f;
-    if (m < B) {
-      k = g.idx[m * R + grp];
-      v = g.z[(long long)m * g.ldz + grp * C + k];
-    }
-    idx_s[ml][grp] = k;
-    zv_s[ml][grp] = v;
-  }
-
-  // gh = h W_hh^T (3 gate tiles), K = Hd split over the 8 waves
-  f32x4 acc[3];
-#pragma unroll
-  for (int t = 0; t < 3; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  if (g.h) {
+  const float* h = dr_uni(g.h);
+  if (wave < GRU_MW) {
+    // ---- gh: 16 rows x (3 gates x 16 units), K = Hd over GRU_MW waves ----
+    const float* whh = dr_uni(g.w_hh);
+    const int ldh = dr_uni((int)g.ldh);
+    const int r = lane & 15, q = lane >> 4;
     const int K = Hd;
-    const int kw = ((K + NW * 16 - 1) / (NW * 16)) * 16;
+    const int kw = ((K + GRU_MW * 16 - 1) / (GRU_MW * 16)) * 16;
     const int kb = wave * kw, ke = min(K, kb + kw);
-    const int m = m0 + r;
-    for (int k0 = kb; k0 < ke; k0 += 16) {
-      const int kq = k0 + 4 * q;
-      float a[4], b[3][4];
-      if (VEC) {
-        // select a valid global address (the array base) instead of a value:
-        // a ternary on the dereference makes hipcc spill a zero vector and
-        // emit flat loads
-        const bool oka = (m < B && kq < K);
-        float4 va = *reinterpret_cast<const float4*>(oka ? g.h + (long long)m * g.ldh + kq : g.h);
-        if (!oka) va = make_float4(0.f, 0.f, 0.f, 0.f);
-        a[0] = va.x; a[1] = va.y; a[2] = va.z; a[3] = va.w;
-        const int j = j0 + r;
-        const bool okb = (j < Hd && kq < K);
+    const int mrow = m0 + r, jrow = j0 + r;
+    const bool mok = mrow < B, jok = jrow < Hd;
+    f32x4 acc[3];
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {
-          float4 vb = *reinterpret_cast<const float4*>(okb ? g.w_hh + (long long)(t * Hd + j) * K + kq : g.w_hh);
-          if (!okb) vb = make_float4(0.f, 0.f, 0.f, 0.f);
-          b[t][0] = vb.x; b[t][1] = vb.y; b[t][2] = vb.z; b[t][3] = vb.w;
-        }
-      } else {
+    for (int t = 0; t < 3; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (h) {
+      for (int kc = kb; kc < ke; kc += GRU_PRE * 16) {
+        float4 ha[GRU_PRE], wb[GRU_PRE][3];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int k = kq + c;
-          a[c] = (m < B && k < K) ? g.h[(long long)m * g.ldh + k] : 0.f;
+        for (int p = 0; p < GRU_PRE; ++p) {
+          const int kq = kc + 16 * p + 4 * q;
+          const bool live = kc + 16 * p < ke && kq < K;
+          const bool oka = live && mok, okb = live && jok;
+          ha[p] = dr_ld4(h, oka ? (unsigned)(mrow * ldh + kq) : 0u);
+          if (!oka) ha[p] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
           for (int t = 0; t < 3; ++t) {
-            const int j = j0 + r;
-            b[t][c] = (j < Hd && k < K) ? g.w_hh[(long long)(t * Hd + j) * K + k] : 0.f;
+            wb[p][t] = dr_ld4(whh, okb ? (unsigned)((t * Hd + jrow) * K + kq) : 0u);
+            if (!okb) wb[p][t] = make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+#pragma unroll
+        for (int p = 0; p < GRU_PRE; ++p) {
+          if (kc + 16 * p >= ke) break;
+#pragma unroll
+          for (int t = 0; t < 3; ++t) {
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[p].x, wb[p][t].x, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[p].y, wb[p][t].y, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[p].z, wb[p][t].z, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[p].w, wb[p][t].w, acc[t], 0, 0, 0);
           }
         }
       }
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int t = 0; t < 3; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c], b[t][c], acc[t], 0, 0, 0);
     }
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[wave][t][e][lane] = acc[t][e];
+    DR_TS(dr_tbuf_gru, 1);
+  } else {
+    // ---- gi: thread (row ml, gate t, units 4*j4..4*j4+3) ----
+    const int x = tid - GRU_MW * 64;  // 0..255, 192 live
+    if (x < 192) {
+      const int j4 = x & 3, t = (x >> 2) % 3, ml = x / 12;
+      const int m = m0 + ml, jj = j0 + 4 * j4;
+      const bool live = m < B && jj < Hd;
+      const int* idx = dr_uni(g.idx);
+      const float* zval = dr_uni(g.zval);
+      const float* wt = dr_uni(g.wt);
+      const float* act = dr_uni(g.a);
+      const int lda = dr_uni((int)g.lda);
+      const unsigned ldw = 3u * Hd;
+      const unsigned col = (unsigned)(t * Hd + jj);
+      // indices + straight-through values of this row (one round trip)
+      int iv[GRU_MAXR];
+      float zv[GRU_MAXR];
+#pragma unroll
+      for (int u4 = 0; u4 < GRU_MAXR / 4; ++u4) {
+        const bool ok = live && 4 * u4 < R;
+        const unsigned e = ok ? (unsigned)(m * R + 4 * u4) : 0u;
+        const int4 i4 = *reinterpret_cast<const int4*>(reinterpret_cast<const char*>(idx) + (e << 2));
+        const float4 z4 = dr_ld4(zval, e);
+        iv[4 * u4] = i4.x; iv[4 * u4 + 1] = i4.y; iv[4 * u4 + 2] = i4.z; iv[4 * u4 + 3] = i4.w;
+        zv[4 * u4] = z4.x; zv[4 * u4 + 1] = z4.y; zv[4 * u4 + 2] = z4.z; zv[4 * u4 + 3] = z4.w;
+      }
+      float av[GRU_MAXA];
+#pragma unroll
+      for (int i = 0; i < GRU_MAXA; ++i) {
+        const bool ok = live && i < A;
+        const float v = dr_ld1(act, ok ? (unsigned)(m * lda + i) : 0u);
+        av[i] = ok ? v : 0.f;
+      }
+      // sampled rows of W_ih^T (one round trip: every gather issued first)
+      float4 w[GRU_MAXR];
+#pragma unroll
+      for (int u = 0; u < GRU_MAXR; ++u) {
+        const bool ok = live && u < R;
+        w[u] = dr_ld4(wt, ok ? (unsigned)(u * C + iv[u]) * ldw + col : 0u);
+      }
+      float4 wa[GRU_MAXA];
+#pragma unroll
+      for (int i = 0; i < GRU_MAXA; ++i) {
+        const bool ok = live && i < A;
+        wa[i] = dr_ld4(wt, ok ? (unsigned)(L + i) * ldw + col : 0u);
+      }
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < GRU_MAXR; ++u) {
+        if (u < R) {
+          v.x = fmaf(w[u].x, zv[u], v.x);
+          v.y = fmaf(w[u].y, zv[u], v.y);
+          v.z = fmaf(w[u].z, zv[u], v.z);
+          v.w = fmaf(w[u].w, zv[u], v.w);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < GRU_MAXA; ++i) {
+        if (i < A) {
+          v.x = fmaf(wa[i].x, av[i], v.x);
+          v.y = fmaf(wa[i].y, av[i], v.y);
+          v.z = fmaf(wa[i].z, av[i], v.z);
+          v.w = fmaf(wa[i].w, av[i], v.w);
+        }
+      }
+      const float* bih = dr_uni(g.b_ih);
+      const float4 bb = dr_ld4(bih, live ? col : 0u);
+      gi_s[ml][t][4 * j4 + 0] = v.x + bb.x;
+      gi_s[ml][t][4 * j4 + 1] = v.y + bb.y;
+      gi_s[ml][t][4 * j4 + 2] = v.z + bb.z;
+      gi_s[ml][t][4 * j4 + 3] = v.w + bb.w;
+    }
+    DR_TS(dr_tbuf_gru, 2);
   }
-#pragma unroll
-  for (int t = 0; t < 3; ++t)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) red[wave][t][e][lane] = acc[t][e];
   __syncthreads();
-  // reduce the 8 partials: element (t, e, l) -> row 4*(l>>4)+e, unit l&15
+  DR_TS(dr_tbuf_gru, 3);
+  // reduce the MFMA partials: element (t, e, l) -> row 4*(l>>4)+e, unit l&15
+  const float* bhh = dr_uni(g.b_hh);
   for (int x = tid; x < 3 * 256; x += 512) {
     const int t = x >> 8, e = (x >> 6) & 3, l = x & 63;
     float v = 0.f;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) v += red[w][t][e][l];
+    for (int w = 0; w < GRU_MW; ++w) v += red[w][t][e][l];
     const int ml = 4 * (l >> 4) + e, jl = l & 15, j = j0 + jl;
-    gh_s[ml][t][jl] = v + ((j < Hd) ? g.b_hh[t * Hd + j] : 0.f);
-  }
-  // gi by gather: one thread per (row, gate, unit); consecutive threads ->
-  // consecutive hidden units -> coalesced reads of the W_ih^T rows
-  const int L = R * C, A = g.A;
-  for (int x = tid; x < 16 * 3 * 16; x += 512) {
-    const int jl = x & 15, t = (x >> 4) % 3, ml = x / 48;
-    const int m = m0 + ml, j = j0 + jl;
-    float v = 0.f;
-    if (m < B && j < Hd) {
-      const int col = t * Hd + j;
-      const long long ld = 3LL * Hd;
-      // issue 16 independent gathers, then accumulate them in group order
-      for (int g0 = 0; g0 < R; g0 += 16) {
-        float w16[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int grp = g0 + u;
-          w16[u] = (grp < R) ? g.wt[(long long)(grp * C + idx_s[ml][grp]) * ld + col] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < 16; ++u)
-          if (g0 + u < R) v += w16[u] * zv_s[ml][g0 + u];
-      }
-      for (int i = 0; i < A; ++i) v += g.wt[(long long)(L + i) * ld + col] * g.a[(long long)m * g.lda + i];
-      v = v + g.b_ih[col];
-    }
-    gi_s[ml][t][jl] = v;
+    const float bv = dr_ld1(bhh, (j < Hd) ? (unsigned)(t * Hd + j) : 0u);
+    gh_s[ml][t][jl] = v + ((j < Hd) ? bv : 0.f);
   }
   __syncthreads();
+  DR_TS(dr_tbuf_gru, 4);
   // gates (torch gru_cell op order)
   if (tid < 256) {
     const int ml = tid >> 4, jl = tid & 15, m = m0 + ml, j = j0 + jl;
@@ -176,7 +244,7 @@ __global__ __launch_bounds__(512) void k_gru_fused(GruArgs g) {
       const float uu = 1.0f / (1.0f + expf(-(gh_s[ml][1][jl] + gi_s[ml][1][jl])));
       const float hn = gh_s[ml][2][jl];
       const float nn = tanhf(gi_s[ml][2][jl] + hn * rr);
-      const float hv = g.h ? g.h[(long long)m * g.ldh + j] : 0.0f;
+      const float hv = h ? h[(long long)m * g.ldh + j] : 0.0f;
       g.hout[(long long)m * g.ldo + j] = (hv - nn) * uu + nn;
       if (g.sr) {
         const long long o = (long long)m * Hd + j;
@@ -187,17 +255,24 @@ __global__ __launch_bounds__(512) void k_gru_fused(GruArgs g) {
       }
     }
   }
+  DR_TS(dr_tbuf_gru, 5);
 }
 
 int op_gru_fused(const GruArgs& g, hipStream_t s) {
-  if (g.R > 64 || g.C > 64 || g.B <= 0) {
-    dr_set_error("gru_fused: bad dims B=%d R=%d C=%d", g.B, g.R, g.C);
+  if (g.R > GRU_MAXR || g.A > GRU_MAXA || g.B <= 0 || g.Hd <= 0 || g.Hd % 4 != 0 || g.ldh % 4 != 0 ||
+      (((uintptr_t)g.h | (uintptr_t)g.w_hh | (uintptr_t)g.wt | (uintptr_t)g.b_ih | (uintptr_t)g.zval |
+        (uintptr_t)g.idx) & 15) != 0 || (g.R % 4) != 0) {
+    dr_set_error("gru_fused: unsupported dims/alignment B=%d Hd=%d R=%d A=%d (R %% 4 == 0, R <= %d, A <= %d, "
+                 "Hd %% 4 == 0, 16-byte aligned operands)", g.B, g.Hd, g.R, g.A, GRU_MAXR, GRU_MAXA);
+    return DR_E_INVALID;
+  }
+  const long long lim = 1LL << 30;
+  if ((long long)(g.R * g.C + g.A) * 3 * g.Hd >= lim || (long long)g.B * g.ldh >= lim ||
+      3LL * g.Hd * g.Hd >= lim) {
+    dr_set_error("gru_fused: operands exceed 32-bit offsets");
     return DR_E_INVALID;
   }
   const int tiles = ((g.Hd + 15) / 16) * ((g.B + 15) / 16);
-  const bool vec = (g.Hd % 4 == 0) && (g.ldh % 4 == 0) && (((uintptr_t)g.h & 15) == 0) &&
-                   (((uintptr_t)g.w_hh & 15) == 0);
-  if (vec) hipLaunchKernelGGL(k_gru_fused<true>, dim3(tiles), dim3(512), 0, s, g);
-  else hipLaunchKernelGGL(k_gru_fused<false>, dim3(tiles), dim3(512), 0, s, g);
+  hipLaunchKernelGGL(k_gru_fused, dim3(dr_xcd_grid(tiles)), dim3(512), 0, s, g);
   return dr_check_launch("gru_fused");
 }

@@ -207,6 +207,11 @@ int op_softmax_ste_bwd(int M, int R, int C, const float* gz, long long ldg, cons
 // ---------------------------------------------------------------------------
 // LayerNorm(eps=1e-5) + SiLU backward, one wave per row
 // ---------------------------------------------------------------------------
+// one wave per row; the row (pre, upstream grad, gamma, beta) is loaded into
+// registers once (K <= 64 * LNB_NPL), so the kernel makes one memory round
+// trip; the reductions keep the k = lane, lane + 64, ... order
+#define LNB_NPL 16
+template <bool REG>
 __global__ void k_ln_silu_bwd(int M, int K, const float* __restrict__ gx, long long ldgx,
                               const float* __restrict__ pre, long long ldp, const float* __restrict__ gamma,
                               const float* __restrict__ beta, float* __restrict__ g_pre, long long ldgp, float* gy_out,
@@ -215,6 +220,56 @@ __global__ void k_ln_silu_bwd(int M, int K, const float* __restrict__ gx, long l
   if (row >= M) return;
   const float* p = pre + (long long)row * ldp;
   const float* g = gx + (long long)row * ldgx;
+  if (REG) {
+    float pv[LNB_NPL], gv[LNB_NPL], gm[LNB_NPL], bt[LNB_NPL];
+#pragma unroll
+    for (int i = 0; i < LNB_NPL; ++i) {
+      const int k = lane + 64 * i;
+      const bool ok = k < K;
+      const int kk = ok ? k : 0;
+      pv[i] = p[kk]; gv[i] = g[kk]; gm[i] = gamma[kk]; bt[i] = beta[kk];
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < LNB_NPL; ++i)
+      if (lane + 64 * i < K) s += pv[i];
+    const float mean = wave_sum(s) / (float)K;
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < LNB_NPL; ++i)
+      if (lane + 64 * i < K) {
+        const float d = pv[i] - mean;
+        v += d * d;
+      }
+    const float rstd = 1.0f / sqrtf(wave_sum(v) / (float)K + 1e-5f);
+    float c1 = 0.f, c2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < LNB_NPL; ++i) {
+      const int k = lane + 64 * i;
+      if (k >= K) continue;
+      const float xh = (pv[i] - mean) * rstd;
+      const float y = xh * gm[i] + bt[i];
+      const float sg = 1.0f / (1.0f + expf(-y));
+      const float gyv = gv[i] * (sg * (1.0f + y * (1.0f - sg)));
+      const float gxh = gyv * gm[i];
+      c1 += gxh;
+      c2 += gxh * xh;
+      if (gy_out) {
+        gy_out[(long long)row * ldgp + k] = gyv;
+        xhat_out[(long long)row * ldgp + k] = xh;
+      }
+      pv[i] = xh;   // keep x_hat and d/dx_hat for the last pass
+      gv[i] = gxh;
+    }
+    c1 = wave_sum(c1) / (float)K;
+    c2 = wave_sum(c2) / (float)K;
+#pragma unroll
+    for (int i = 0; i < LNB_NPL; ++i) {
+      const int k = lane + 64 * i;
+      if (k < K) g_pre[(long long)row * ldgp + k] = rstd * (gv[i] - c1 - pv[i] * c2);
+    }
+    return;
+  }
   float s = 0.f;
   for (int k = lane; k < K; k += 64) s += p[k];
   const float mean = wave_sum(s) / (float)K;
@@ -253,8 +308,12 @@ int op_ln_silu_bwd(int M, int K, const float* gx, long long ldgx, const float* p
                    const float* gamma, const float* beta, float* g_pre, long long ldgp, float* gy, float* xhat,
                    hipStream_t s) {
   if (M == 0) return DR_OK;
-  hipLaunchKernelGGL(k_ln_silu_bwd, dim3(dr_cdiv(M, 4)), dim3(256), 0, s, M, K, gx, ldgx, pre, ldp, gamma, beta,
-                     g_pre, ldgp, gy, xhat);
+  if (K <= 64 * LNB_NPL)
+    hipLaunchKernelGGL(k_ln_silu_bwd<true>, dim3(dr_cdiv(M, 4)), dim3(256), 0, s, M, K, gx, ldgx, pre, ldp, gamma,
+                       beta, g_pre, ldgp, gy, xhat);
+  else
+    hipLaunchKernelGGL(k_ln_silu_bwd<false>, dim3(dr_cdiv(M, 4)), dim3(256), 0, s, M, K, gx, ldgx, pre, ldp, gamma,
+                       beta, g_pre, ldgp, gy, xhat);
   return dr_check_launch("ln_silu_bwd");
 }
 
@@ -269,7 +328,23 @@ __global__ __launch_bounds__(1024) void k_colsum(int M, int N, const float* __re
   const int n = blockIdx.x * 64 + c;
   float acc = 0.f;
   if (n < N) {
-    for (int m = rg; m < M; m += 16) {
+    // 8 rows of loads in flight per thread; summed in row order
+    int m = rg;
+    for (; m + 16 * 7 < M; m += 16 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = X[(long long)(m + 16 * u) * ldx + n];
+      if (Y) {
+        float w[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) w[u] = Y[(long long)(m + 16 * u) * ldy + n];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = v[u] * w[u];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; m < M; m += 16) {
       float v = X[(long long)m * ldx + n];
       if (Y) v = v * Y[(long long)m * ldy + n];
       acc += v;

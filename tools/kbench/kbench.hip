@@ -1,0 +1,253 @@
+// Kernel latency microbenchmark: links the engine's objects and times single
+// kernels launched back to back on one stream (HIP events around REPS
+// launches).  Build: python tools/kbench/build.py ; run on the GPU box.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+#include <functional>
+#include "../../dreamer_amd/csrc/gemm.h"
+#include "../../dreamer_amd/csrc/gru.h"
+#include "../../dreamer_amd/csrc/ops.h"
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+static const char* g_filter = nullptr;
+static int g_reps = 200;
+extern "C" int dr_debug_tbuf_gru(long long* out, int n);
+extern "C" int dr_debug_tbuf_gemm(long long* out, int n);
+extern "C" void dr_debug_gemm_tile(int nt);
+
+// one more launch, then the per-phase times of wave 0 of each workgroup
+// (relative to its own start) averaged over the workgroups that wrote them
+static void phases(const char* name, std::function<void(hipStream_t)> f, int (*rd)(long long*, int), hipStream_t s) {
+  if (g_filter && !strstr(name, g_filter)) return;
+  const int n = 1024 * DR_TS_SLOTS;
+  std::vector<long long> z(n, 0), t(n);
+  hipStreamSynchronize(s);
+  rd(t.data(), n);  // clears stale stamps
+  f(s);
+  hipStreamSynchronize(s);
+  rd(t.data(), n);
+  double sum[DR_TS_SLOTS] = {0};
+  int cnt[DR_TS_SLOTS] = {0};
+  long long smin = -1, smax = 0, emax = 0;
+  for (int b = 0; b < 1024; ++b) {
+    const long long* r = &t[b * DR_TS_SLOTS];
+    if (r[0] == 0) continue;
+    if (smin < 0 || r[0] < smin) smin = r[0];
+    if (r[0] > smax) smax = r[0];
+    for (int i = 1; i < DR_TS_SLOTS; ++i)
+      if (r[i] >= r[0] && r[i] - r[0] < 1000000) {
+        sum[i] += r[i] - r[0];
+        cnt[i]++;
+        if (r[i] > emax) emax = r[i];
+      }
+  }
+  printf("   phases %-38s start spread %.2f us, last stamp %.2f us after first start |", name, (smax - smin) * 0.01,
+         (emax - smin) * 0.01);
+  for (int i = 1; i < DR_TS_SLOTS; ++i)
+    if (cnt[i]) printf(" p%d %.2f", i, sum[i] / cnt[i] * 0.01);
+  printf("\n");
+}
+
+// I-cache probe: the same 4096 independent FMAs as straight-line code or as a loop
+__global__ __launch_bounds__(512) void k_code_unrolled(float* out, float x) {
+  float a[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = x + i;
+#pragma unroll
+  for (int it = 0; it < 512; ++it)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = a[i] * 0.999f + 0.001f * (float)(it + i);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s += a[i];
+  if (s == 12345.f) out[threadIdx.x] = s;
+}
+__global__ __launch_bounds__(512) void k_code_rolled(float* out, float x) {
+  float a[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = x + i;
+#pragma unroll 1
+  for (int it = 0; it < 512; ++it)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = a[i] * 0.999f + 0.001f * (float)(it + i);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s += a[i];
+  if (s == 12345.f) out[threadIdx.x] = s;
+}
+
+// dependent-load chain: per-round-trip latency with the whole grid loading
+__global__ __launch_bounds__(512) void k_chase(const unsigned* __restrict__ nxt, int rounds, unsigned* out) {
+  unsigned i = (blockIdx.x * 512 + threadIdx.x) * 97u & ((1u << 18) - 1);
+  for (int r = 0; r < rounds; ++r) i = nxt[i];
+  if (i == 0xffffffffu) out[0] = i;
+}
+
+struct Big { long long f[200]; };
+__global__ void k_empty_small(int* p) { if (p && threadIdx.x == 9999) *p = 1; }
+__global__ void k_empty_big(Big b) { if (threadIdx.x == 9999) ((int*)b.f[3])[0] = (int)b.f[150]; }
+
+static float* frand(size_t n, float scale = 0.1f) {
+  std::vector<float> h(n);
+  for (size_t i = 0; i < n; ++i) h[i] = scale * ((rand() / (float)RAND_MAX) - 0.5f);
+  float* d;
+  CK(hipMalloc(&d, n * sizeof(float)));
+  CK(hipMemcpy(d, h.data(), n * sizeof(float), hipMemcpyHostToDevice));
+  return d;
+}
+
+static void timeit(const char* name, std::function<void(hipStream_t)> f, hipStream_t s, int reps = 0) {
+  if (g_filter && !strstr(name, g_filter)) return;
+  if (reps == 0) reps = g_reps;
+  for (int i = 0; i < 10; ++i) f(s);
+  CK(hipStreamSynchronize(s));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  // graph-captured chain (what the engine replays)
+  hipGraph_t g;
+  hipGraphExec_t ge;
+  CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+  for (int i = 0; i < reps; ++i) f(s);
+  CK(hipStreamEndCapture(s, &g));
+  CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  CK(hipGraphLaunch(ge, s));
+  CK(hipStreamSynchronize(s));
+  CK(hipEventRecord(a, s));
+  CK(hipGraphLaunch(ge, s));
+  CK(hipEventRecord(b, s));
+  CK(hipEventSynchronize(b));
+  float ms;
+  CK(hipEventElapsedTime(&ms, a, b));
+  printf("%-48s %8.2f us/launch (graph chain of %d)\n", name, 1000.f * ms / reps, reps);
+  CK(hipGraphExecDestroy(ge));
+  CK(hipGraphDestroy(g));
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1) g_filter = argv[1];
+  if (getenv("KB_REPS")) g_reps = atoi(getenv("KB_REPS"));
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  const int B = 64, Hd = 600, R = 32, C = 32, A = 3, L = R * C;
+  timeit("empty kernel (1 WG, small args)", [&](hipStream_t st) { hipLaunchKernelGGL(k_empty_small, dim3(1), dim3(64), 0, st, nullptr); }, s);
+  timeit("empty kernel (128 WG x 512, small args)", [&](hipStream_t st) { hipLaunchKernelGGL(k_empty_small, dim3(128), dim3(512), 0, st, nullptr); }, s);
+  Big big;
+  memset(&big, 0, sizeof(big));
+  timeit("empty kernel (128 WG x 512, 1.6 KB args)", [&](hipStream_t st) { hipLaunchKernelGGL(k_empty_big, dim3(128), dim3(512), 0, st, big); }, s);
+
+  float* dummy;
+  CK(hipMalloc(&dummy, 4096));
+  timeit("4096 FMA straight-line (128 WG x 512)", [&](hipStream_t st) { hipLaunchKernelGGL(k_code_unrolled, dim3(128), dim3(512), 0, st, dummy, 1.0f); }, s);
+  timeit("4096 FMA rolled loop   (128 WG x 512)", [&](hipStream_t st) { hipLaunchKernelGGL(k_code_rolled, dim3(128), dim3(512), 0, st, dummy, 1.0f); }, s);
+  timeit("4096 FMA straight-line (1 WG x 64)", [&](hipStream_t st) { hipLaunchKernelGGL(k_code_unrolled, dim3(1), dim3(64), 0, st, dummy, 1.0f); }, s);
+  timeit("4096 FMA rolled loop   (1 WG x 64)", [&](hipStream_t st) { hipLaunchKernelGGL(k_code_rolled, dim3(1), dim3(64), 0, st, dummy, 1.0f); }, s);
+
+  {
+    const int n = 1 << 18;  // 1 MB of indices
+    std::vector<unsigned> h(n);
+    for (int i = 0; i < n; ++i) h[i] = (unsigned)((i * 2654435761u + 12345u) & (n - 1));
+    unsigned* d;
+    CK(hipMalloc(&d, n * 4));
+    CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+    for (int rounds : {1, 4, 16}) {
+      char nm[96];
+      snprintf(nm, sizeof nm, "pointer chase %2d rounds (128 WG x 512)", rounds);
+      timeit(nm, [&](hipStream_t st) { hipLaunchKernelGGL(k_chase, dim3(128), dim3(512), 0, st, d, rounds, (unsigned*)dummy); }, s);
+      snprintf(nm, sizeof nm, "pointer chase %2d rounds (1 WG x 64)", rounds);
+      timeit(nm, [&](hipStream_t st) { hipLaunchKernelGGL(k_chase, dim3(1), dim3(64), 0, st, d, rounds, (unsigned*)dummy); }, s);
+    }
+  }
+
+  // GRU
+  float* wih = frand((size_t)3 * Hd * (L + A));
+  float* wt = frand((size_t)3 * Hd * (L + A));
+  float* whh = frand((size_t)3 * Hd * Hd);
+  float* bih = frand(3 * Hd);
+  float* bhh = frand(3 * Hd);
+  float* h = frand((size_t)B * Hd);
+  float* hout = frand((size_t)B * Hd);
+  float* act = frand((size_t)B * A);
+  float* save = frand((size_t)4 * B * Hd);
+  std::vector<int> hidx(2 * B * R);
+  for (int i = 0; i < B * R; ++i) hidx[i] = rand() % C;
+  float one = 1.0f;
+  for (int i = 0; i < B * R; ++i) memcpy(&hidx[B * R + i], &one, 4);
+  int* idx;
+  CK(hipMalloc(&idx, hidx.size() * 4));
+  CK(hipMemcpy(idx, hidx.data(), hidx.size() * 4, hipMemcpyHostToDevice));
+  if (op_transpose(3 * Hd, L + A, wih, wt, s)) { printf("transpose failed\n"); return 1; }
+  GruArgs ga;
+  memset(&ga, 0, sizeof(ga));
+  ga.B = B; ga.Hd = Hd; ga.R = R; ga.C = C; ga.A = A;
+  ga.idx = idx; ga.zval = reinterpret_cast<float*>(idx + B * R); ga.a = act; ga.lda = A; ga.h = h; ga.ldh = Hd;
+  ga.wt = wt; ga.b_ih = bih; ga.w_hh = whh; ga.b_hh = bhh; ga.hout = hout; ga.ldo = Hd;
+  timeit("gru_fused B64 H600 R32 (no saves)", [&](hipStream_t st) { op_gru_fused(ga, st); }, s);
+  phases("gru_fused", [&](hipStream_t st) { op_gru_fused(ga, st); }, dr_debug_tbuf_gru, s);
+  GruArgs gs = ga;
+  gs.sr = save; gs.su = save + B * Hd; gs.sn = save + 2 * B * Hd; gs.sghn = save + 3 * B * Hd;
+  timeit("gru_fused B64 H600 R32 (saves)", [&](hipStream_t st) { op_gru_fused(gs, st); }, s);
+  GruArgs gn = ga;
+  gn.h = nullptr;
+  timeit("gru_fused h=NULL (gather only)", [&](hipStream_t st) { op_gru_fused(gn, st); }, s);
+  GruArgs g0 = ga;
+  g0.R = 0;
+  g0.A = 0;
+  timeit("gru_fused R=0 A=0 (MFMA only)", [&](hipStream_t st) { op_gru_fused(g0, st); }, s);
+
+  // skinny GEMMs
+  float* X = frand((size_t)1024 * 2048);
+  float* W = frand((size_t)2048 * 2048);
+  float* bias = frand(2048);
+  float* Y = frand((size_t)1024 * 2048);
+  float* lng = frand(2048, 1.0f);
+  float* lnb = frand(2048);
+  auto nt_ = [&](int M, int N, int K) {
+    GemmArgs g = gemm_args();
+    g.M = M; g.N = N; g.K = K; g.A = X; g.lda = K; g.ksplitA = K; g.W = W; g.ldb = K; g.bias = bias; g.Y = Y; g.ldy = N;
+    return g;
+  };
+  char buf[128];
+  int shapes[][3] = {{64, 200, 600}, {64, 200, 200}, {64, 1024, 200}, {64, 200, 1624}, {64, 255, 200}, {960, 200, 200}};
+  for (auto& sh : shapes) {
+    GemmArgs g = nt_(sh[0], sh[1], sh[2]);
+    snprintf(buf, sizeof buf, "NT plain M%d N%d K%d", sh[0], sh[1], sh[2]);
+    timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, &g, 1, st); }, s);
+    phases(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, &g, 1, st); }, dr_debug_tbuf_gemm, s);
+    GemmArgs gl = g;
+    gl.ln_g = lng; gl.ln_b = lnb;
+    snprintf(buf, sizeof buf, "NT lnsilu M%d N%d K%d", sh[0], sh[1], sh[2]);
+    timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_LNSILU, &gl, 1, st); }, s);
+    phases(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_LNSILU, &gl, 1, st); }, dr_debug_tbuf_gemm, s);
+    GemmArgs gk = g;
+    gk.ldb = sh[1];
+    snprintf(buf, sizeof buf, "NN plain M%d N%d K%d", sh[0], sh[1], sh[2]);
+    timeit(buf, [&](hipStream_t st) { gemm_launch(G_NN, AM_PLAIN, &gk, 1, st); }, s);
+  }
+  for (int nt : {32, 64}) {
+    dr_debug_gemm_tile(nt);
+    for (auto& sh : shapes) {
+      if (sh[0] > 64) continue;
+      GemmArgs g = nt_(sh[0], sh[1], sh[2]);
+      snprintf(buf, sizeof buf, "NT%d plain M%d N%d K%d", nt, sh[0], sh[1], sh[2]);
+      timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, &g, 1, st); }, s);
+      GemmArgs gl = g;
+      gl.ln_g = lng; gl.ln_b = lnb;
+      snprintf(buf, sizeof buf, "NT%d lnsilu M%d N%d K%d", nt, sh[0], sh[1], sh[2]);
+      timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_LNSILU, &gl, 1, st); }, s);
+    }
+  }
+  dr_debug_gemm_tile(0);
+  // ln_silu_bwd / colsum
+  timeit("ln_silu_bwd M64 K512", [&](hipStream_t st) { op_ln_silu_bwd(64, 512, X, 512, Y, 512, lng, lnb, W, 512, nullptr, nullptr, st); }, s);
+  timeit("ln_silu_bwd M64 K512 +saves", [&](hipStream_t st) { op_ln_silu_bwd(64, 512, X, 512, Y, 512, lng, lnb, W, 512, W + 65536, W + 2 * 65536, st); }, s);
+  timeit("colsum M960 N512", [&](hipStream_t st) { op_colsum(960, 512, X, 512, nullptr, 0, bias, 0, st); }, s);
+  timeit("colsum M64 N512", [&](hipStream_t st) { op_colsum(64, 512, X, 512, nullptr, 0, bias, 0, st); }, s);
+  CK(hipDeviceSynchronize());
+  printf("ok\n");
+  return 0;
+}
