@@ -24,6 +24,9 @@ sys.path.insert(0, REPO)
 METRIC = "imagined latent-steps/sec (B×H) at 64×64 CarRacing, 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 = f32 vector peak
 HBM_PEAK_GBS = 8000.0
+# SURVEY.md §8d figure of record: necessary dense FLOPs per imagined step at
+# 64x64, S=64, H=15 (warm start 131.07 + dream 8.88 + update 11.17 MFLOP)
+PATH_MFLOP_PER_STEP = {(64, 15): 151.12, (50, 15): 122.36}
 
 CAR_RACER = dict(
     hidden_state_dims=600, latent_state_dims=[32, 32], action_dims=3, observation_dims=[64, 64],
@@ -230,6 +233,13 @@ def main():
                      "algorithmic_flops_per_launch": enc_flops, "phase_ms": round(enc_s * 1e3, 4)},
         "losses": {"actor": la, "critic": lc},
     }
+    mf = PATH_MFLOP_PER_STEP.get((S, H))
+    if mf is not None:
+        tf = value * mf * 1e6 / 1e12
+        out["path_roofline"] = {"bound": "mfma", "achieved": round(tf, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                                "unit": "TFLOP/s", "frac": round(tf / FP32_MFMA_PEAK_TFLOPS, 4),
+                                "mflop_per_imagined_step": mf,
+                                "note": "whole train_Agent epoch, SURVEY §8d necessary FLOPs x imagined steps/s"}
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(CAR_RACER, B, S, H, budget_s=args.cpu_budget)
     print(json.dumps(out))
