@@ -50,7 +50,7 @@ class dr_noise(C.Structure):
 
 class dr_frames(C.Structure):
     _fields_ = [("ring", fp), ("ring_cap", C.c_longlong), ("starts", fp), ("obs", fp),
-                ("stride_b", C.c_longlong), ("stride_t", C.c_longlong), ("raw255", C.c_int)]
+                ("stride_b", C.c_longlong), ("stride_t", C.c_longlong), ("raw255", C.c_int), ("t0", C.c_int)]
 
 
 _P = C.POINTER

@@ -180,7 +180,7 @@ __global__ void k_frames_nhwc4(int n, int nb, int h, int w, dr_frames src, float
   if (i >= (long long)n * hw) return;
   const long long f = i / hw;
   const long long p = i - f * hw;
-  const int b = (int)(f % nb), t = (int)(f / nb);
+  const int b = (int)(f % nb), t = (int)(f / nb) + src.t0;
   float v[3];
   if (src.ring) {
     const unsigned char* fr = src.ring + ((src.starts[b] + t) % src.ring_cap) * 3 * hw;

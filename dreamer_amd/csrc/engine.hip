@@ -96,6 +96,17 @@ static GemmArgs bwd_in(int M, int N, int K, const float* G, long long ldg, const
   g.accumulate = accumulate;
   return g;
 }
+// input gradient against a transposed weight WT [N=in][K=out] (NT, float4 loads)
+static GemmArgs bwd_nt(int M, int N, int K, const float* G, long long ldg, const float* WT, float* Y, long long ldy,
+                       int accumulate) {
+  GemmArgs g = gemm_args();
+  g.M = M; g.N = N; g.K = K;
+  g.A = G; g.lda = ldg;
+  g.W = WT; g.ldb = K;
+  g.Y = Y; g.ldy = ldy;
+  g.accumulate = accumulate;
+  return g;
+}
 // weight gradient: dW[M=out][N=in] = sum_r G[r][m] X[r][n]  (rows r < R)
 static GemmArgs bwd_w(int out, int in, int R, const float* G, long long ldg, const float* X, long long ldx, float* dW) {
   GemmArgs g = gemm_args();
@@ -343,6 +354,8 @@ struct ImWs {
   // backward
   float *gH, *gZ, *gA, *glog, *gx2, *gp2, *gx1, *gp1, *ggi, *ggh, *gheads, *gx2a, *gpre2a, *gy2a, *xh2a, *gx1a,
       *gpre1a, *gy1a, *xh1a, *hcat, *zcat;
+  // transposed weights for the input-gradient GEMMs (NT with float4 loads)
+  float *tl6p, *tl3p, *tl0p, *twhh, *thead, *tl3a, *tl0a;
 };
 static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   const long long Bl = B, BH = (long long)B * H, B1 = (long long)B * (H + 1);
@@ -361,6 +374,13 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.bst = c.f((long long)2 * A);
   w.idx[0] = c.i(2 * Bl * d->rows);
   w.idx[1] = c.i(2 * Bl * d->rows);
+  w.tl6p = c.f((long long)L * d->prior_h2);
+  w.tl3p = c.f((long long)d->prior_h2 * d->prior_h1);
+  w.tl0p = c.f((long long)d->prior_h1 * Hd);
+  w.twhh = c.f((long long)3 * Hd * Hd);
+  w.thead = c.f((long long)2 * A * d->actor_h2);
+  w.tl3a = c.f((long long)d->actor_h2 * d->actor_h1);
+  w.tl0a = c.f((long long)d->actor_h1 * (Hd + L));
   w.gH = c.f(B1 * Hd);
   w.gZ = c.f(B1 * L);
   w.gA = c.f(BH * A);
@@ -520,6 +540,23 @@ extern "C" int dr_imagine_bwd(const dr_dims* d, const dr_world_model* wm, const 
   if (g_actions) DR_TRY(copy2d(w.gA, A, g_actions, A, A, (long long)BH, s));
   else DR_TRY(zero(w.gA, (long long)BH * A, s));
   const bool upstream_state = g_latents || g_hiddens;
+  {
+    // weights are constant over the backward: transpose them once (one launch)
+    // so every input-gradient GEMM below runs NT with 16-byte weight loads
+    const int h1 = d->prior_h1, h2 = d->prior_h2;
+    TransposeJob tj[9] = {
+        {L, h2, L, wm->prior.l6.w, w.tl6p},
+        {h2, h1, h2, wm->prior.l3.w, w.tl3p},
+        {h1, Hd, h1, wm->prior.l0.w, w.tl0p},
+        {3 * Hd, L + A, 3 * Hd, wm->w_ih, w.wt},
+        {3 * Hd, Hd, 3 * Hd, wm->w_hh, w.twhh},
+        {A, a2, 2 * A, ac->mu.w, w.thead},
+        {A, a2, 2 * A, ac->ls.w, w.thead + A},
+        {a2, a1, a2, ac->l3.w, w.tl3a},
+        {a1, Hd + L, a1, ac->l0.w, w.tl0a},
+    };
+    DR_TRY(op_transpose_multi(tj, 9, s));
+  }
 
   for (int t = H - 1; t >= 0; --t) {
     const long long hb = (long long)Hd * B * t;
@@ -531,26 +568,26 @@ extern "C" int dr_imagine_bwd(const dr_dims* d, const dr_world_model* wm, const 
     if (state_grad) {
       // z_{t+1} = STE(prior(h_{t+1}))   (DynamicsPredictors.py:31-40)
       DR_TRY(op_softmax_ste_bwd(B, d->rows, d->cols, gZ_n, ldL, tp.soft + (long long)t * B * L, L, w.glog, s));
-      DR_TRY(run(G_NN, AM_PLAIN, bwd_in(B, d->prior_h2, L, w.glog, L, wm->prior.l6.w, d->prior_h2, w.gx2, d->prior_h2, 0), s));
+      DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, d->prior_h2, L, w.glog, L, w.tl6p, w.gx2, d->prior_h2, 0), s));
       DR_TRY(op_ln_silu_bwd(B, d->prior_h2, w.gx2, d->prior_h2, tp.pre2p + (long long)t * B * d->prior_h2, d->prior_h2,
                             wm->prior.n4.w, wm->prior.n4.b, w.gp2, d->prior_h2, nullptr, nullptr, s));
-      DR_TRY(run(G_NN, AM_PLAIN, bwd_in(B, d->prior_h1, d->prior_h2, w.gp2, d->prior_h2, wm->prior.l3.w, d->prior_h1,
-                                        w.gx1, d->prior_h1, 0), s));
+      DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, d->prior_h1, d->prior_h2, w.gp2, d->prior_h2, w.tl3p, w.gx1, d->prior_h1, 0),
+                 s));
       DR_TRY(op_ln_silu_bwd(B, d->prior_h1, w.gx1, d->prior_h1, tp.pre1p + (long long)t * B * d->prior_h1, d->prior_h1,
                             wm->prior.n1.w, wm->prior.n1.b, w.gp1, d->prior_h1, nullptr, nullptr, s));
-      DR_TRY(run(G_NN, AM_PLAIN, bwd_in(B, Hd, d->prior_h1, w.gp1, d->prior_h1, wm->prior.l0.w, Hd, gH_n, ldH, 1), s));
+      DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, Hd, d->prior_h1, w.gp1, d->prior_h1, w.tl0p, gH_n, ldH, 1), s));
       // h_{t+1} = GRU(z_t, a_t, h_t)   (SequenceModel.py:19-24)
       DR_TRY(op_gru_bwd(B, Hd, gH_n, ldH, hiddens + (long long)t * Hd, ldH, tp.r + hb, tp.u + hb, tp.n + hb,
                         tp.ghn + hb, w.ggi, w.ggh, gH_t, ldH, 1, s));
       if (t > 0) {
         GemmArgs p[2];
-        p[0] = bwd_in(B, L + A, 3 * Hd, w.ggi, 3 * Hd, wm->w_ih, L + A, gZ_t, ldL, 1);
+        p[0] = bwd_nt(B, L + A, 3 * Hd, w.ggi, 3 * Hd, w.wt, gZ_t, ldL, 1);
         p[0].Y2 = w.gA + (long long)t * A; p[0].ldy2 = ldA; p[0].nsplitY = L;
-        p[1] = bwd_in(B, Hd, 3 * Hd, w.ggh, 3 * Hd, wm->w_hh, Hd, gH_t, ldH, 1);
-        DR_TRY(gemm_launch(G_NN, AM_PLAIN, p, 2, s));
+        p[1] = bwd_nt(B, Hd, 3 * Hd, w.ggh, 3 * Hd, w.twhh, gH_t, ldH, 1);
+        DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, 2, s));
       } else {
         // only the action gradient is consumed at t = 0
-        DR_TRY(run(G_NN, AM_PLAIN, bwd_in(B, A, 3 * Hd, w.ggi, 3 * Hd, wm->w_ih + L, L + A, w.gA, ldA, 1), s));
+        DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, A, 3 * Hd, w.ggi, 3 * Hd, w.wt + (long long)L * 3 * Hd, w.gA, ldA, 1), s));
       }
     }
     // actor at step t: heads, then base_net (Agent.py:191-210)
@@ -560,20 +597,18 @@ extern "C" int dr_imagine_bwd(const dr_dims* d, const dr_world_model* wm, const 
                              ldA, actions + ot, ldA, nullptr, 0, tp.ls_raw + ot, ldA, tp.eps + (long long)t * B * A,
                              gh_t, (long long)H * 2 * A, s));
     {
-      GemmArgs g = bwd_in(B, a2, 2 * A, gh_t, (long long)H * 2 * A, ac->mu.w, a2, w.gx2a, a2, 0);
-      g.W2 = ac->ls.w; g.ldb2 = a2; g.ksplitB = A;
-      DR_TRY(run(G_NN, AM_PLAIN, g, s));
+      DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, a2, 2 * A, gh_t, (long long)H * 2 * A, w.thead, w.gx2a, a2, 0), s));
     }
     const long long o2 = (long long)t * a2, o1 = (long long)t * a1;
     DR_TRY(op_ln_silu_bwd(B, a2, w.gx2a, a2, tp.pre2a + o2, lda2, ac->n4.w, ac->n4.b, w.gpre2a + o2, lda2,
                           w.gy2a + o2, w.xh2a + o2, s));
-    DR_TRY(run(G_NN, AM_PLAIN, bwd_in(B, a1, a2, w.gpre2a + o2, lda2, ac->l3.w, a1, w.gx1a, a1, 0), s));
+    DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, a1, a2, w.gpre2a + o2, lda2, w.tl3a, w.gx1a, a1, 0), s));
     DR_TRY(op_ln_silu_bwd(B, a1, w.gx1a, a1, tp.pre1a + o1, lda1, ac->n1.w, ac->n1.b, w.gpre1a + o1, lda1,
                           w.gy1a + o1, w.xh1a + o1, s));
     if (t > 0) {
-      GemmArgs g = bwd_in(B, Hd + L, a1, w.gpre1a + o1, lda1, ac->l0.w, Hd + L, gH_t, ldH, 1);
+      GemmArgs g = bwd_nt(B, Hd + L, a1, w.gpre1a + o1, lda1, w.tl0a, gH_t, ldH, 1);
       g.Y2 = gZ_t; g.ldy2 = ldL; g.nsplitY = Hd;
-      DR_TRY(run(G_NN, AM_PLAIN, g, s));
+      DR_TRY(run(G_NT, AM_PLAIN, g, s));
     }
   }
   // ---- actor weight gradients over all B*H rows (rows r = b*H + t) ----
@@ -588,14 +623,15 @@ extern "C" int dr_imagine_bwd(const dr_dims* d, const dr_world_model* wm, const 
     p[3] = bwd_w(A, a2, BH, w.gheads + A, 2 * A, tp.x2a, a2, gr->ls.w);
     DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 4, s));
   }
-  DR_TRY(op_colsum(BH, a1, w.gpre1a, a1, nullptr, 0, gr->l0.b, 0, s));
-  DR_TRY(op_colsum(BH, a1, w.gy1a, a1, w.xh1a, a1, gr->n1.w, 0, s));
-  DR_TRY(op_colsum(BH, a1, w.gy1a, a1, nullptr, 0, gr->n1.b, 0, s));
-  DR_TRY(op_colsum(BH, a2, w.gpre2a, a2, nullptr, 0, gr->l3.b, 0, s));
-  DR_TRY(op_colsum(BH, a2, w.gy2a, a2, w.xh2a, a2, gr->n4.w, 0, s));
-  DR_TRY(op_colsum(BH, a2, w.gy2a, a2, nullptr, 0, gr->n4.b, 0, s));
-  DR_TRY(op_colsum(BH, A, w.gheads, 2 * A, nullptr, 0, gr->mu.b, 0, s));
-  DR_TRY(op_colsum(BH, A, w.gheads + A, 2 * A, nullptr, 0, gr->ls.b, 0, s));
+  {
+    ColsumJob cj[8] = {
+        {a1, w.gpre1a, a1, nullptr, 0, gr->l0.b}, {a1, w.gy1a, a1, w.xh1a, a1, gr->n1.w},
+        {a1, w.gy1a, a1, nullptr, 0, gr->n1.b},   {a2, w.gpre2a, a2, nullptr, 0, gr->l3.b},
+        {a2, w.gy2a, a2, w.xh2a, a2, gr->n4.w},   {a2, w.gy2a, a2, nullptr, 0, gr->n4.b},
+        {A, w.gheads, 2 * A, nullptr, 0, gr->mu.b}, {A, w.gheads + A, 2 * A, nullptr, 0, gr->ls.b},
+    };
+    DR_TRY(op_colsum_multi(BH, cj, 8, s));
+  }
   return DR_OK;
 }
 
@@ -656,10 +692,13 @@ extern "C" int dr_critic_fwd(const dr_dims* d, const dr_critic* cr, int M, const
 
 struct CBws {
   float *row_loss, *glog, *gx2, *gp2, *gy2, *xh2, *gx1, *gp1, *gy1, *xh1;
+  float *tl6, *tl3;  // transposed value_net.6 / .3 weights
 };
 static void cbws_carve(Carve& c, const dr_dims* d, int B, int H, CBws& w) {
   const long long M = (long long)B * (H + 1);
   w.row_loss = c.f((long long)B * H);
+  w.tl6 = c.f((long long)d->buckets * d->critic_h2);
+  w.tl3 = c.f((long long)d->critic_h2 * d->critic_h1);
   w.glog = c.f(M * d->buckets);
   w.gx2 = c.f(M * d->critic_h2);
   w.gp2 = c.f(M * d->critic_h2);
@@ -695,9 +734,13 @@ extern "C" int dr_critic_loss_bwd(const dr_dims* d, const dr_critic* cr, int B, 
   DR_TRY(op_critic_ce(B, H, nb, t.logits, R, cr->buckets, scale, w.row_loss, w.glog, s));
   DR_TRY(op_mean(B * H, w.row_loss, loss_out, s));
   // value_net.6
-  DR_TRY(run(G_NN, AM_PLAIN, bwd_in(M, c2, nb, w.glog, nb, cr->net.l6.w, c2, w.gx2, c2, 0), s));
+  {
+    TransposeJob tj[2] = {{nb, c2, nb, cr->net.l6.w, w.tl6}, {c2, c1, c2, cr->net.l3.w, w.tl3}};
+    DR_TRY(op_transpose_multi(tj, 2, s));
+  }
+  DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M, c2, nb, w.glog, nb, w.tl6, w.gx2, c2, 0), s));
   DR_TRY(op_ln_silu_bwd(M, c2, w.gx2, c2, t.pre2, c2, cr->net.n4.w, cr->net.n4.b, w.gp2, c2, w.gy2, w.xh2, s));
-  DR_TRY(run(G_NN, AM_PLAIN, bwd_in(M, c1, c2, w.gp2, c2, cr->net.l3.w, c1, w.gx1, c1, 0), s));
+  DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M, c1, c2, w.gp2, c2, w.tl3, w.gx1, c1, 0), s));
   DR_TRY(op_ln_silu_bwd(M, c1, w.gx1, c1, t.pre1, c1, cr->net.n1.w, cr->net.n1.b, w.gp1, c1, w.gy1, w.xh1, s));
   {
     GemmArgs p[3];
@@ -707,13 +750,15 @@ extern "C" int dr_critic_loss_bwd(const dr_dims* d, const dr_critic* cr, int B, 
     p[2].W2 = latents; p[2].ldb2 = L; p[2].nsplitB = Hd;
     DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 3, s));
   }
-  DR_TRY(op_colsum(M, nb, w.glog, nb, nullptr, 0, gr->net.l6.b, 0, s));
-  DR_TRY(op_colsum(M, c2, w.gp2, c2, nullptr, 0, gr->net.l3.b, 0, s));
-  DR_TRY(op_colsum(M, c2, w.gy2, c2, w.xh2, c2, gr->net.n4.w, 0, s));
-  DR_TRY(op_colsum(M, c2, w.gy2, c2, nullptr, 0, gr->net.n4.b, 0, s));
-  DR_TRY(op_colsum(M, c1, w.gp1, c1, nullptr, 0, gr->net.l0.b, 0, s));
-  DR_TRY(op_colsum(M, c1, w.gy1, c1, w.xh1, c1, gr->net.n1.w, 0, s));
-  DR_TRY(op_colsum(M, c1, w.gy1, c1, nullptr, 0, gr->net.n1.b, 0, s));
+  {
+    ColsumJob cj[7] = {
+        {nb, w.glog, nb, nullptr, 0, gr->net.l6.b}, {c2, w.gp2, c2, nullptr, 0, gr->net.l3.b},
+        {c2, w.gy2, c2, w.xh2, c2, gr->net.n4.w},   {c2, w.gy2, c2, nullptr, 0, gr->net.n4.b},
+        {c1, w.gp1, c1, nullptr, 0, gr->net.l0.b},  {c1, w.gy1, c1, w.xh1, c1, gr->net.n1.w},
+        {c1, w.gy1, c1, nullptr, 0, gr->net.n1.b},
+    };
+    DR_TRY(op_colsum_multi(M, cj, 7, s));
+  }
   return DR_OK;
 }
 

@@ -8,10 +8,13 @@
 // exact f32 fma (v_mfma_f32_16x16x4_f32), so results differ from the CPU
 // oracle only by summation order.
 #include <limits.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
 
 #include "gemm.h"
+
+#include <algorithm>
 
 #define BK 32
 #define LDS_K (BK + 2)
@@ -60,7 +63,7 @@ __device__ __forceinline__ float load_a_mk(const GemmArgs& g, int m, int k, floa
     const int ci = k >> 4, iy = 2 * oy - 1 + ((k >> 2) & 3), ix = 2 * ox - 1 + (k & 3);
     if (iy < 0 || iy >= g.ih || ix < 0 || ix >= g.iw) return 0.0f;
     const long long off = ((long long)ci * g.ih + iy) * g.iw + ix;
-    const int b = f % g.nb, t = f / g.nb;
+    const int b = f % g.nb, t = f / g.nb + g.src.t0;
     float v;
     if (g.src.ring) {
       const long long slot = (g.src.starts[b] + t) % g.src.ring_cap;
@@ -379,14 +382,13 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
   const int r = lane & 15, q = lane >> 4;
   DR_TS(dr_tbuf_gemm, 0);
 
+  // dynamic LDS, sized by the host for this launch (skinny_lds_floats):
+  // [ max(reduction slab, staged LN rows) | LN gamma (K) | LN beta (K) ]
   constexpr int RED = NWAVE * FT * FN * 4 * 64;
-  constexpr int LNF = (AMODE == AM_LNSILU) ? SK_LN_MAXF : 0;
-  constexpr int SMEM = (RED > LNF ? RED : LNF);
-  __shared__ __attribute__((aligned(16))) float smem[SMEM];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ float s_mean[MT], s_rstd[MT];
   __shared__ float s_out[MT][NT + 1];
   constexpr int LNK = (AMODE == AM_LNSILU) ? SK_LN_MAXK : 1;
-  __shared__ float s_lng[LNK], s_lnb[LNK];
   // bias of the output columns this thread finalises, issued now and waited
   // for only in the epilogue
   constexpr int NEPI = (FT * FN * 256 + 511) / 512;
@@ -448,6 +450,8 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
   // rows an MFMA fragment reads fall in distinct banks)
   const int KP = K + 4;
   const bool ln_lds = (AMODE == AM_LNSILU) && (MT * KP <= SK_LN_MAXF) && VEC && (K <= LNK);
+  float* s_lng = smem + (MT * KP > RED ? MT * KP : RED);
+  float* s_lnb = s_lng + K;
   DR_TS(dr_tbuf_gemm, 1);
   if (AMODE == AM_LNSILU) {
     if (ln_lds) {
@@ -723,6 +727,32 @@ static bool skinny_offsets_ok(const GemmArgs& g, bool b_kn) {
   return true;
 }
 
+// minimum dynamic LDS per skinny workgroup (bytes); a large value keeps one
+// workgroup per CU.  Set by dr_debug_gemm_min_lds / DREAMER_MIN_LDS.
+static size_t g_min_lds = (size_t)-1;
+extern "C" void dr_debug_gemm_min_lds(long long bytes) { g_min_lds = (size_t)bytes; }
+static size_t min_lds() {
+  if (g_min_lds == (size_t)-1) {
+    const char* e = getenv("DREAMER_MIN_LDS");
+    g_min_lds = e ? (size_t)atoll(e) : 0;
+  }
+  return g_min_lds;
+}
+
+// floats of dynamic LDS a skinny launch needs (mirrors the kernel's layout)
+template <int MT, int NT, int AMODE>
+static size_t skinny_lds_floats(const GemmBatch& gb, int count, bool vec) {
+  const size_t red = (size_t)8 * (MT / 16) * (NT / 16) * 4 * 64;
+  size_t need = red;
+  if (AMODE == AM_LNSILU && vec) {
+    for (int i = 0; i < count; ++i) {
+      const size_t K = gb.p[i].K, rows = (size_t)MT * (K + 4);
+      if (rows <= SK_LN_MAXF && K <= SK_LN_MAXK) need = std::max(need, std::max(rows, red) + 2 * K);
+    }
+  }
+  return need;
+}
+
 template <int MT, int NT, int AMODE, bool B_KN, int EPI>
 static void launch_skinny(const GemmBatch& gb, int count, bool vec, hipStream_t s) {
   int maxt = 0;
@@ -731,12 +761,23 @@ static void launch_skinny(const GemmBatch& gb, int count, bool vec, hipStream_t 
     maxt = t > maxt ? t : maxt;
   }
   if (maxt == 0) return;
+  const size_t lds = std::max(skinny_lds_floats<MT, NT, AMODE>(gb, count, vec) * sizeof(float), min_lds());
+  if (lds > 64 * 1024) {  // opt in to more than the default dynamic LDS (once per instantiation)
+    static const bool raised = [] {
+      (void)hipFuncSetAttribute((const void*)k_gemm_skinny<MT, NT, AMODE, B_KN, true, EPI>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_gemm_skinny<MT, NT, AMODE, B_KN, false, EPI>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+      return true;
+    }();
+    (void)raised;
+  }
   if (vec)
     hipLaunchKernelGGL((k_gemm_skinny<MT, NT, AMODE, B_KN, true, EPI>), dim3(dr_xcd_grid(maxt), 1, count), dim3(512),
-                       0, s, gb);
+                       lds, s, gb);
   else
     hipLaunchKernelGGL((k_gemm_skinny<MT, NT, AMODE, B_KN, false, EPI>), dim3(dr_xcd_grid(maxt), 1, count), dim3(512),
-                       0, s, gb);
+                       lds, s, gb);
 }
 
 // tile-shape override for the kernel microbenchmark (0 = heuristic)

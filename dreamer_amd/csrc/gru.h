@@ -21,4 +21,12 @@ struct alignas(16) GruArgs {
 
 int op_gru_fused(const GruArgs& g, hipStream_t s);
 int op_transpose(int rows, int cols, const float* in, float* out, hipStream_t s);
+// batched transposes in one launch: out[c * ldo + r] = in[r * cols + c]
+struct TransposeJob {
+  int rows, cols, ldo;
+  const float* in;
+  float* out;
+};
+#define DR_MAX_TJOBS 10
+int op_transpose_multi(const TransposeJob* jobs, int n, hipStream_t s);
 int op_onehot_index(int M, int R, int C, const float* z, long long ldz, int* idx, float* zval, hipStream_t s);

@@ -10,6 +10,8 @@
 // units (3 gate column tiles of W_hh) and splits K over 8 waves.
 #include "gru.h"
 
+#include <algorithm>
+
 __global__ void k_transpose(int rows, int cols, const float* __restrict__ in, float* __restrict__ out) {
   __shared__ float tile[32][33];
   const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
@@ -29,6 +31,43 @@ int op_transpose(int rows, int cols, const float* in, float* out, hipStream_t s)
   dim3 grid((cols + 31) / 32, (rows + 31) / 32);
   hipLaunchKernelGGL(k_transpose, grid, dim3(256), 0, s, rows, cols, in, out);
   return dr_check_launch("transpose");
+}
+
+struct TransposeBatch {
+  TransposeJob j[DR_MAX_TJOBS];
+};
+__global__ void k_transpose_multi(TransposeBatch tb) {
+  __shared__ float tile[32][33];
+  const TransposeJob& J = tb.j[blockIdx.z];
+  const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
+  if (bx >= J.cols || by >= J.rows) return;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int k = ty; k < 32; k += 8) {
+    const int r = by + k, c = bx + tx;
+    tile[k][tx] = (r < J.rows && c < J.cols) ? J.in[(long long)r * J.cols + c] : 0.f;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int c = bx + k, r = by + tx;
+    if (c < J.cols && r < J.rows) J.out[(long long)c * J.ldo + r] = tile[tx][k];
+  }
+}
+
+int op_transpose_multi(const TransposeJob* jobs, int n, hipStream_t s) {
+  if (n <= 0) return DR_OK;
+  if (n > DR_MAX_TJOBS) {
+    dr_set_error("transpose_multi: at most %d jobs", DR_MAX_TJOBS);
+    return DR_E_INVALID;
+  }
+  TransposeBatch tb;
+  int gx = 1, gy = 1;
+  for (int i = 0; i < n; ++i) {
+    tb.j[i] = jobs[i];
+    gx = std::max(gx, (jobs[i].cols + 31) / 32);
+    gy = std::max(gy, (jobs[i].rows + 31) / 32);
+  }
+  hipLaunchKernelGGL(k_transpose_multi, dim3(gx, gy, n), dim3(256), 0, s, tb);
+  return dr_check_launch("transpose_multi");
 }
 
 // index of the non-zero entry of each one-hot group (z values are exactly 0

@@ -22,6 +22,15 @@ int op_ln_silu_bwd(int M, int K, const float* gx, long long ldgx, const float* p
                    const float* gamma, const float* beta, float* g_pre, long long ldgp, float* gy, float* xhat,
                    hipStream_t s);
 // out[n] (+)= sum_m X[m][n] * (Y ? Y[m][n] : 1)
+// several column sums in one launch (bias / LayerNorm parameter gradients)
+struct ColsumJob {
+  int N;
+  const float* X; long long ldx;
+  const float* Y; long long ldy;  // optional elementwise factor
+  float* out;
+};
+#define DR_MAX_CSJOBS 8
+int op_colsum_multi(int M, const ColsumJob* jobs, int n, hipStream_t s);
 int op_colsum(int M, int N, const float* X, long long ldx, const float* Y, long long ldy, float* out, int accumulate,
               hipStream_t s);
 // symexp(sum softmax(logits) * buckets) per row -> out[m*ostride]

@@ -320,15 +320,15 @@ int op_ln_silu_bwd(int M, int K, const float* gx, long long ldgx, const float* p
 // ---------------------------------------------------------------------------
 // column sums (bias / LayerNorm parameter gradients), deterministic order
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_colsum(int M, int N, const float* __restrict__ X, long long ldx,
-                                                 const float* __restrict__ Y, long long ldy, float* out,
-                                                 int accumulate) {
-  __shared__ float part[16][64];
+// one 64-column slab per workgroup, 16 row groups; rows summed in a fixed
+// order (deterministic), 8 rows of loads in flight per thread
+__device__ __forceinline__ void colsum_slab(int M, int N, const float* __restrict__ X, long long ldx,
+                                            const float* __restrict__ Y, long long ldy, float* out, int accumulate,
+                                            int slab, float (&part)[16][64]) {
   const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int n = blockIdx.x * 64 + c;
+  const int n = slab * 64 + c;
   float acc = 0.f;
   if (n < N) {
-    // 8 rows of loads in flight per thread; summed in row order
     int m = rg;
     for (; m + 16 * 7 < M; m += 16 * 8) {
       float v[8];
@@ -358,6 +358,46 @@ __global__ __launch_bounds__(1024) void k_colsum(int M, int N, const float* __re
     for (int k = 0; k < 16; ++k) t += part[k][c];
     out[n] = accumulate ? out[n] + t : t;
   }
+}
+
+__global__ __launch_bounds__(1024) void k_colsum(int M, int N, const float* __restrict__ X, long long ldx,
+                                                 const float* __restrict__ Y, long long ldy, float* out,
+                                                 int accumulate) {
+  __shared__ float part[16][64];
+  colsum_slab(M, N, X, ldx, Y, ldy, out, accumulate, blockIdx.x, part);
+}
+
+struct ColsumBatch {
+  ColsumJob j[DR_MAX_CSJOBS];
+  int first_slab[DR_MAX_CSJOBS + 1];
+  int n;
+};
+__global__ __launch_bounds__(1024) void k_colsum_multi(int M, ColsumBatch cb) {
+  __shared__ float part[16][64];
+  int j = 0;
+  while (j + 1 < cb.n && (int)blockIdx.x >= cb.first_slab[j + 1]) ++j;
+  const ColsumJob& J = cb.j[j];
+  colsum_slab(M, J.N, J.X, J.ldx, J.Y, J.ldy, J.out, 0, blockIdx.x - cb.first_slab[j], part);
+}
+
+int op_colsum_multi(int M, const ColsumJob* jobs, int n, hipStream_t s) {
+  if (n <= 0) return DR_OK;
+  if (n > DR_MAX_CSJOBS) {
+    dr_set_error("colsum_multi: at most %d jobs", DR_MAX_CSJOBS);
+    return DR_E_INVALID;
+  }
+  ColsumBatch cb;
+  cb.n = n;
+  int slabs = 0;
+  for (int i = 0; i < n; ++i) {
+    cb.j[i] = jobs[i];
+    cb.first_slab[i] = slabs;
+    slabs += dr_cdiv(jobs[i].N, 64);
+  }
+  cb.first_slab[n] = slabs;
+  if (slabs == 0) return DR_OK;
+  hipLaunchKernelGGL(k_colsum_multi, dim3(slabs), dim3(1024), 0, s, M, cb);
+  return dr_check_launch("colsum_multi");
 }
 
 int op_colsum(int M, int N, const float* X, long long ldx, const float* Y, long long ldy, float* out, int accumulate,

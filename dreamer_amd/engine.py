@@ -43,9 +43,27 @@ class ImaginationEngine:
         self.use_graph = use_graph
         self.graph = None
         self.graph_key = None
+        # Optional second stream for branches that could overlap inside an
+        # epoch graph: the time-chunked conv encoder under the posterior scan
+        # and the critic backward beside the actor BPTT.  Measured on MI355X
+        # (profiles/r01_ab_overlap.txt) neither pays: the conv kernels fill
+        # every CU slot, so the scan's small kernels only queue behind them,
+        # and a forked branch slowed every later graph replay by ~6 %.  Both
+        # stay available behind DREAMER_WARM_CHUNK / DREAMER_FORK for
+        # re-measurement; the defaults run one stream, one encoder chunk.
+        self.side = torch.cuda.Stream(self.dev)
+        import os
+        self.chunks = self.warm_chunks(self.T, int(os.environ.get("DREAMER_WARM_CHUNK", str(self.T))))
+        self.fork = os.environ.get("DREAMER_FORK", "0") == "1"
         self._alloc()
 
     # ------------------------------------------------------------------ setup
+    @staticmethod
+    def warm_chunks(T, size=8):
+        """Time chunks [t0, t1) of the warm-start window: conv chunk c+1 runs
+        while the posterior scan consumes chunk c."""
+        return [(t0, min(T, t0 + size)) for t0 in range(0, T, size)]
+
     def dims(self):
         return self.dr.world_model.dims(self.dr.agent)
 
@@ -124,48 +142,102 @@ class ImaginationEngine:
         L.call("dr_lambda_returns", self.B, self.H, L.ptr(self.rewards), L.ptr(self.continues), L.ptr(self.V_t),
                ag.gamma, ag.lambda_, L.ptr(self.R), st)
 
-    def losses_and_grads(self):
-        """update_S, actor loss + BPTT, critic CE backward (Agent.py:96-145)."""
-        ag, d, st = self.dr.agent, self.d, hip.stream()
+    def losses_and_grads(self, fork=True):
+        """update_S, actor loss + BPTT, critic CE backward (Agent.py:96-145).
+        With fork=True the critic backward runs on the side stream beside the
+        actor's BPTT (they share only read-only inputs)."""
+        ag, d = self.dr.agent, self.d
+        main = torch.cuda.current_stream(self.dev)
+        st = main.cuda_stream
         B, H = self.B, self.H
         M = B * (H + 1)
         L_ = d.rows * d.cols
         scale = 1.0 / float(B * self.wsize * H)
         L.call("dr_critic_fwd", d, ag.critic_struct(), M, L.ptr(self.hiddens), d.hidden, L.ptr(self.latents), L_,
                None, L.ptr(self.V_c), L.ptr(self.ctape), None, 0, st)
+        critic_args = (d, ag.critic_struct(), B, H, L.ptr(self.hiddens), L.ptr(self.latents), L.ptr(self.R),
+                       L.ptr(self.ctape), scale, L.ptr(ag.loss_slot(1)), ag.critic_struct(grad=True),
+                       L.ptr(self.ws_cr), self.ws_cr.numel())
+        if fork:
+            self.side.wait_stream(main)
+            L.call("dr_critic_loss_bwd", *critic_args, self.side.cuda_stream)
         L.call("dr_update_S", self.R_all.numel(), L.ptr(self.R_all), L.ptr(ag.S_dev), L.ptr(self.norm), None, 0, st)
         L.call("dr_actor_loss_grad", B, H, d.action, L.ptr(self.mus), L.ptr(self.sigmas), L.ptr(self.actions),
                L.ptr(self.R), L.ptr(self.V_c), L.ptr(self.norm), ag.nu, scale, L.ptr(self.loss_a), L.ptr(self.g_mu),
                L.ptr(self.g_sig), st)
-        L.call("dr_critic_loss_bwd", d, ag.critic_struct(), B, H, L.ptr(self.hiddens), L.ptr(self.latents),
-               L.ptr(self.R), L.ptr(self.ctape), scale, L.ptr(ag.loss_slot(1)), ag.critic_struct(grad=True),
-               L.ptr(self.ws_cr), self.ws_cr.numel(), st)
+        if not fork:
+            L.call("dr_critic_loss_bwd", *critic_args, st)
         L.call("dr_imagine_bwd", d, self.dr.world_model.packed(), ag.actor_struct(), B, H, L.ptr(self.latents),
                L.ptr(self.hiddens), L.ptr(self.actions), L.ptr(self.g_mu), L.ptr(self.g_sig), None, None, None,
                L.ptr(self.tape), ag.actor_struct(grad=True), L.ptr(self.ws_im), self.ws_im.numel(), st)
         ag.loss_slot(0).copy_(self.loss_a[0:1])
+        if fork:
+            main.wait_stream(self.side)
 
     def optimise(self):
         """non-finite skip, clip_grad_norm_(100) x2, AdamW x2, soft target (Agent.py:137-153)."""
         self.dr.agent.fused_optimiser_step(self.sq, self.skip)
 
     # phases of one epoch; collectives (world > 1) run between phases
-    def _ph_encode(self):
-        self.dr.buffer.gather_actions(self.starts, self.act_win)
-        self.encode_and_warm_frames = self.dr.buffer.frames_struct(self.starts)
-        d, st = self.d, hip.stream()
-        L.call("dr_encoder_features", d, self.dr.world_model.packed(), self.encode_and_warm_frames, self.B, self.T,
-               L.ptr(self.feat), L.ptr(self.ws_enc), self.ws_enc.numel(), st)
+    def _encode_chunk(self, t0, t1, stream_ptr):
+        d = self.d
+        fr = self.dr.buffer.frames_struct(self.starts)
+        fr.t0 = t0
+        off = t0 * self.B * d.enc_hidden * 4
+        L.call("dr_encoder_features", d, self.dr.world_model.packed(), fr, self.B, t1 - t0,
+               L.ptr(self.feat) + off, L.ptr(self.ws_enc), self.ws_enc.numel(), stream_ptr)
 
-    def _ph_warm(self):
+    def _scan_chunk(self, t0, t1, stream_ptr):
+        """Posterior scan over window steps [t0, t1) (Dreamer.py:244-262).  A
+        chunk after the first continues from (self.z0, self.h0): its first
+        step runs GRU(z_{t0-1}, a_{t0-1}, h) and the sampler's Philox stream
+        is offset by t0, so the draws equal the unchunked scan's."""
         d, A = self.d, self.d.action
-        nz = L.dr_noise(None, None, self.rng.state.data_ptr(), self.rank * self.B, WARM_STREAM)
-        L.call("dr_observe_scan", d, self.dr.world_model.packed(), self.B, self.T, L.ptr(self.feat),
-               L.ptr(self.act_win), self.S * A, A, None, None, nz, L.ptr(self.z0), L.ptr(self.h0), None,
-               L.ptr(self.ws_obs), self.ws_obs.numel(), hip.stream())
+        nz = L.dr_noise(None, None, self.rng.state.data_ptr(), self.rank * self.B, WARM_STREAM + t0)
+        feat = L.ptr(self.feat) + t0 * self.B * d.enc_hidden * 4
+        if t0 == 0:
+            acts, zi, hi = L.ptr(self.act_win), None, None
+        else:
+            acts, zi, hi = L.ptr(self.act_win) + (t0 - 1) * A * 4, L.ptr(self.z0), L.ptr(self.h0)
+        L.call("dr_observe_scan", d, self.dr.world_model.packed(), self.B, t1 - t0, feat, acts, self.S * A, A,
+               hi, zi, nz, L.ptr(self.z0), L.ptr(self.h0), None, L.ptr(self.ws_obs), self.ws_obs.numel(),
+               stream_ptr)
+
+    def _ph_encwarm(self):
+        """a3 + a2, pipelined: the conv encoder runs chunk by chunk on the side
+        stream; the scan of chunk c waits only for chunk c's features."""
+        main = torch.cuda.current_stream(self.dev)
+        self.dr.buffer.gather_actions(self.starts, self.act_win)
+        self.side.wait_stream(main)
+        done = []
+        with torch.cuda.stream(self.side):
+            for t0, t1 in self.chunks:
+                self._encode_chunk(t0, t1, self.side.cuda_stream)
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+                done.append(ev)
+        for (t0, t1), ev in zip(self.chunks, done):
+            main.wait_event(ev)
+            self._scan_chunk(t0, t1, main.cuda_stream)
+
+    def time_encoder(self, reps=5):
+        """Average ms of the conv encoder (all chunks, back to back on one
+        stream, no overlap): the dominant kernel group's live duration for the
+        bench's roofline line."""
+        st = torch.cuda.current_stream(self.dev)
+        for t0, t1 in self.chunks:
+            self._encode_chunk(t0, t1, st.cuda_stream)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        for _ in range(reps):
+            for t0, t1 in self.chunks:
+                self._encode_chunk(t0, t1, st.cuda_stream)
+        b.record(st)
+        b.synchronize()
+        return a.elapsed_time(b) / reps
 
     def _ph_update(self):
-        self.losses_and_grads()
+        self.losses_and_grads(fork=self.fork)
 
     def _ph_optim(self):
         self.optimise()
@@ -173,7 +245,7 @@ class ImaginationEngine:
 
     def phases(self):
         """(name, body, collective-after) in execution order."""
-        ph = [("encode", self._ph_encode, None), ("warm", self._ph_warm, None), ("imagine", self.imagine, None),
+        ph = [("encwarm", self._ph_encwarm, None), ("imagine", self.imagine, None),
               ("returns", self.returns, self._allgather_R if self.wsize > 1 else None),
               ("update", self._ph_update, self._allreduce_grads if self.wsize > 1 else None),
               ("optim", self._ph_optim, None)]

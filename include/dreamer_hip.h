@@ -94,6 +94,7 @@ typedef struct {
   const float* obs;          /* f32 frames (when ring == NULL) */
   long long stride_b, stride_t; /* f32: element offset of frame (b,t) = b*stride_b + t*stride_t */
   int raw255;                /* 1: values are 0..255 -> x/255-0.5 (Dreamer.py:251); 0: already normalised */
+  int t0;                    /* time offset: frame (b, t) is window step t0 + t (chunked encoding) */
 } dr_frames;
 
 const char* dr_last_error(void);

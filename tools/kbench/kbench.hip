@@ -87,6 +87,63 @@ __global__ __launch_bounds__(512) void k_chase(const unsigned* __restrict__ nxt,
   if (i == 0xffffffffu) out[0] = i;
 }
 
+// busy kernel: each workgroup spins for `iters` dependent FMAs
+__global__ __launch_bounds__(256) void k_spin(float* out, int iters) {
+  float a = threadIdx.x;
+  for (int i = 0; i < iters; ++i) a = a * 0.9999f + 0.5f;
+  if (a == 12345.f) out[0] = a;
+}
+
+// two independent chains captured on two streams (fork/join) vs one stream
+static void concurrency_probe(float* dummy) {
+  hipStream_t s1, s2;
+  CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+  CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+  hipEvent_t fork, join, a, b;
+  CK(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+  CK(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  auto big = [&](hipStream_t st) { hipLaunchKernelGGL(k_spin, dim3(512), dim3(256), 0, st, dummy, 20000); };
+  auto chain = [&](hipStream_t st) {
+    for (int i = 0; i < 40; ++i) hipLaunchKernelGGL(k_spin, dim3(64), dim3(256), 0, st, dummy, 1000);
+  };
+  for (int mode = 0; mode < 4; ++mode) {
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(s1, hipStreamCaptureModeGlobal));
+    if (mode == 0) {
+      big(s1);
+    } else if (mode == 1) {
+      chain(s1);
+    } else if (mode == 2) {
+      big(s1);
+      chain(s1);
+    } else {
+      CK(hipEventRecord(fork, s1));
+      CK(hipStreamWaitEvent(s2, fork, 0));
+      big(s2);
+      chain(s1);
+      CK(hipEventRecord(join, s2));
+      CK(hipStreamWaitEvent(s1, join, 0));
+    }
+    CK(hipStreamEndCapture(s1, &g));
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    CK(hipGraphLaunch(ge, s1));
+    CK(hipStreamSynchronize(s1));
+    CK(hipEventRecord(a, s1));
+    for (int r = 0; r < 5; ++r) CK(hipGraphLaunch(ge, s1));
+    CK(hipEventRecord(b, s1));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    const char* nm[] = {"big alone", "chain of 40 alone", "big then chain (1 stream)", "big || chain (fork/join)"};
+    printf("graph concurrency: %-28s %8.1f us\n", nm[mode], 1000.f * ms / 5);
+    CK(hipGraphExecDestroy(ge));
+    CK(hipGraphDestroy(g));
+  }
+}
+
 struct Big { long long f[200]; };
 __global__ void k_empty_small(int* p) { if (p && threadIdx.x == 9999) *p = 1; }
 __global__ void k_empty_big(Big b) { if (threadIdx.x == 9999) ((int*)b.f[3])[0] = (int)b.f[150]; }
@@ -162,6 +219,8 @@ int main(int argc, char** argv) {
       timeit(nm, [&](hipStream_t st) { hipLaunchKernelGGL(k_chase, dim3(1), dim3(64), 0, st, d, rounds, (unsigned*)dummy); }, s);
     }
   }
+
+  if (!g_filter || strstr("concurrency", g_filter)) concurrency_probe(dummy);
 
   // GRU
   float* wih = frand((size_t)3 * Hd * (L + A));
