@@ -388,7 +388,6 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ float s_mean[MT], s_rstd[MT];
   __shared__ float s_out[MT][NT + 1];
-  constexpr int LNK = (AMODE == AM_LNSILU) ? SK_LN_MAXK : 1;
   // bias of the output columns this thread finalises, issued now and waited
   // for only in the epilogue
   constexpr int NEPI = (FT * FN * 256 + 511) / 512;
@@ -409,195 +408,336 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
   const int kb = wave * kw;
   const int ke = min(K, kb + kw);
 
-  // K loop in batches of PRE 16-k chunks: every load of a batch is issued
-  // before its first MFMA, so a wave pays one memory round trip per batch
-  // (one in total for K <= PRE*16*8 = 1024).  The first batch of weights (and
-  // of plain A rows) is issued before the LayerNorm staging.
-  constexpr int PRE = (FT >= 4) ? 4 : 8;
-  float bb[PRE][FN][4];
-  float aa[PRE][FT][4];
-  auto load_batch = [&](int kc) {
-#pragma unroll
-    for (int p = 0; p < PRE; ++p) {
-      const int k16 = kc + 16 * p;
-      const int kq = k16 + 4 * q;
-      const bool live = k16 < ke;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        if (live) {
-          skinny_load_b<B_KN, VEC>(o, n0 + j * 16 + r, kq, bb[p][j]);
-        } else {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) bb[p][j][c] = 0.f;
-        }
-      }
-      if (AMODE != AM_LNSILU) {
-#pragma unroll
-        for (int t = 0; t < FT; ++t) {
-          if (live) {
-            skinny_load_a<VEC>(o, m0 + t * 16 + r, k16, kq, aa[p][t]);
-          } else {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) aa[p][t][c] = 0.f;
-          }
-        }
-      }
-    }
-  };
-  if (kb < ke) load_batch(kb);
-
-  // LayerNorm rows staged in LDS with a padded stride (K + 4 floats: the 16
-  // rows an MFMA fragment reads fall in distinct banks)
+  // ---- operand path ---------------------------------------------------
+  // Staged (LayerNorm-SiLU A, NT, 16-byte aligned, K <= 1024): every row of the A tile and of
+  // the weight tile is read by one wave with coalesced 1 KB row pieces
+  // (lane -> float4 column), all loads issued before the first wait; the
+  // LayerNorm-SiLU prologue (rows in registers: DPP statistics, one
+  // normalise + activate per element) runs on the way; both tiles land in LDS
+  // with a padded stride (K + 4 floats: the 16 rows an MFMA fragment reads
+  // fall in distinct banks); the K loop then reads fragments from LDS.
+  // Direct (otherwise): each lane loads its MFMA fragments from global memory.
   const int KP = K + 4;
-  const bool ln_lds = (AMODE == AM_LNSILU) && (MT * KP <= SK_LN_MAXF) && VEC && (K <= LNK);
-  float* s_lng = smem + (MT * KP > RED ? MT * KP : RED);
-  float* s_lnb = s_lng + K;
-  DR_TS(dr_tbuf_gemm, 1);
-  if (AMODE == AM_LNSILU) {
-    if (ln_lds) {
-      // one global pass: every float4 of the MT rows is issued before the
-      // first LDS write (SK_STAGE per thread), statistics come from LDS
-      const int K4 = K >> 2;
-      const int total = MT * K4;
-      for (int e0 = 0; e0 < total; e0 += 512 * SK_STAGE) {
-        float4 v[SK_STAGE];
-#pragma unroll
-        for (int i = 0; i < SK_STAGE; ++i) {
-          const int e = e0 + tid + 512 * i;
-          const int rr = e / K4, k4 = e - rr * K4, m = m0 + rr;
-          const bool ok = e < total && m < M;
-          v[i] = dr_ld4(o.A, ok ? (unsigned)(m * o.lda + 4 * k4) : 0u);
-          if (!ok) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int i = 0; i < SK_STAGE; ++i) {
-          const int e = e0 + tid + 512 * i;
-          const int rr = e / K4, k4 = e - rr * K4;
-          if (e < total) *reinterpret_cast<float4*>(&smem[rr * KP + 4 * k4]) = v[i];
-        }
-      }
-      const float* lg = dr_uni(g.ln_g);
-      const float* lb = dr_uni(g.ln_b);
-      for (int k = tid; k < K; k += 512) {
-        s_lng[k] = dr_ld1(lg, (unsigned)k);
-        s_lnb[k] = dr_ld1(lb, (unsigned)k);
-      }
-      __syncthreads();
-      DR_TS(dr_tbuf_gemm, 2);
-      for (int rr = wave; rr < MT; rr += NWAVE) {
-        const float* row = &smem[rr * KP];
-        float s = 0.f, v = 0.f;
-        for (int k = lane; k < K; k += 64) s += row[k];
-        const float mean = wave_sum(s) / (float)K;
-        for (int k = lane; k < K; k += 64) {
-          const float d = row[k] - mean;
-          v += d * d;
-        }
-        const float rstd = 1.0f / sqrtf(wave_sum(v) / (float)K + 1e-5f);
-        if (lane == 0) {
-          s_mean[rr] = mean;
-          s_rstd[rr] = rstd;
-        }
-      }
-    } else {
-      for (int rr = wave; rr < MT; rr += NWAVE) {
-        const int m = m0 + rr;
-        float mean = 0.f, rstd = 0.f;
-        if (m < M) {
-          const float* row = o.A + (long long)m * o.lda;
-          float s = 0.f, v = 0.f;
-          for (int k = lane; k < K; k += 64) s += row[k];
-          mean = wave_sum(s) / (float)K;
-          for (int k = lane; k < K; k += 64) {
-            const float d = row[k] - mean;
-            v += d * d;
-          }
-          rstd = 1.0f / sqrtf(wave_sum(v) / (float)K + 1e-5f);
-        }
-        if (lane == 0) {
-          s_mean[rr] = mean;
-          s_rstd[rr] = rstd;
-        }
-      }
-    }
-    __syncthreads();
-    DR_TS(dr_tbuf_gemm, 3);
-  }
-
+  const int K4 = K >> 2;
+  constexpr int RPW = MT / NWAVE;                    // A rows per wave
+  constexpr int BPW = (NT + NWAVE - 1) / NWAVE;      // weight rows per wave
+  constexpr int SV = 4;                              // float4 per lane per staged row (K <= 1024)
+  float* a_out = dr_uni(g.a_out);
+  const int ld_aout = dr_uni((int)g.ld_aout);
+  const bool store_a = (a_out != nullptr) && (tn == 0);
+  // (measured: staging pays only where the LayerNorm needs the barrier anyway;
+  // a plain GEMM is faster with direct fragment loads, profiles/r01_v5_kbench.txt)
+  const bool staged = (AMODE == AM_LNSILU) && VEC && !B_KN && (K4 <= 64 * SV) && ((MT + NT) * KP <= SK_LN_MAXF);
   f32x4 acc[FT][FN];
 #pragma unroll
   for (int t = 0; t < FT; ++t)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[t][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float* a_out = dr_uni(g.a_out);
-  const int ld_aout = dr_uni((int)g.ld_aout);
-  const bool store_a = (a_out != nullptr) && (tn == 0);
-  const float* lg = dr_uni(g.ln_g);
-  const float* lb = dr_uni(g.ln_b);
-  for (int kc = kb; kc < ke; kc += PRE * 16) {
-    if (kc != kb) load_batch(kc);
-    if (AMODE == AM_LNSILU) {
+  DR_TS(dr_tbuf_gemm, 1);
+  if (staged) {
+    float* sA = smem;
+    float* sB = smem + MT * KP;
+    float4 xa[RPW][SV], xb[BPW][SV], gv[SV], bv[SV];
+    const float* lg = dr_uni(g.ln_g);
+    const float* lb = dr_uni(g.ln_b);
 #pragma unroll
+    for (int i = 0; i < SV; ++i) {
+      if (64 * i >= K4) break;  // wave-uniform: no dummy loads past the row
+      const int k4 = lane + 64 * i, k = 4 * k4;
+      const bool okk = k4 < K4;
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr) {
+        const int m = m0 + wave + NWAVE * rr;
+        const bool ok = okk && m < M;
+        const bool seg1 = k < o.ksA;
+        const float* base = seg1 ? o.A : o.A2;
+        const unsigned e = ok ? (unsigned)(seg1 ? m * o.lda + k : m * o.lda2 + k - o.ksA) : 0u;
+        xa[rr][i] = dr_ld4(ok ? base : o.W, e);
+        if (!ok) xa[rr][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int jj = 0; jj < BPW; ++jj) {
+        const int nl = wave + NWAVE * jj, n = n0 + nl;
+        const bool ok = okk && nl < NT && n < N;
+        xb[jj][i] = dr_ld4(o.W, ok ? (unsigned)(n * o.ldb + k) : 0u);
+        if (!ok) xb[jj][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      if (AMODE == AM_LNSILU) {
+        gv[i] = dr_ld4(lg, okk ? (unsigned)k : 0u);
+        bv[i] = dr_ld4(lb, okk ? (unsigned)k : 0u);
+      }
+    }
+    DR_TS(dr_tbuf_gemm, 2);
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) {
+      const int ml = wave + NWAVE * rr, m = m0 + ml;
+      if (AMODE == AM_LNSILU) {
+        float sm = 0.f;
+#pragma unroll
+        for (int i = 0; i < SV; ++i) {
+          if (64 * i >= K4) break;
+          sm += (xa[rr][i].x + xa[rr][i].y) + (xa[rr][i].z + xa[rr][i].w);
+        }
+        const float mean = wave_sum(sm) / (float)K;
+        float sq = 0.f;
+#pragma unroll
+        for (int i = 0; i < SV; ++i) {
+          if (64 * i >= K4) break;
+          if (lane + 64 * i < K4) {
+            const float dx = xa[rr][i].x - mean, dy = xa[rr][i].y - mean;
+            const float dz = xa[rr][i].z - mean, dw = xa[rr][i].w - mean;
+            sq += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+          }
+        }
+        const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)K + 1e-5f);
+#pragma unroll
+        for (int i = 0; i < SV; ++i) {
+          if (64 * i >= K4) break;
+          float4& x = xa[rr][i];
+          x.x = dr_silu_fast((x.x - mean) * rstd * gv[i].x + bv[i].x);
+          x.y = dr_silu_fast((x.y - mean) * rstd * gv[i].y + bv[i].y);
+          x.z = dr_silu_fast((x.z - mean) * rstd * gv[i].z + bv[i].z);
+          x.w = dr_silu_fast((x.w - mean) * rstd * gv[i].w + bv[i].w);
+          if (m >= M) x = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < SV; ++i) {
+        if (64 * i >= K4) break;
+        const int k4 = lane + 64 * i;
+        if (k4 < K4) {
+          *reinterpret_cast<float4*>(&sA[ml * KP + 4 * k4]) = xa[rr][i];
+          if (store_a && m < M) *reinterpret_cast<float4*>(&a_out[(unsigned)(m * ld_aout + 4 * k4)]) = xa[rr][i];
+        }
+      }
+    }
+#pragma unroll
+    for (int jj = 0; jj < BPW; ++jj) {
+      const int nl = wave + NWAVE * jj;
+      if (nl >= NT) break;
+#pragma unroll
+      for (int i = 0; i < SV; ++i) {
+        if (64 * i >= K4) break;
+        const int k4 = lane + 64 * i;
+        if (k4 < K4) *reinterpret_cast<float4*>(&sB[nl * KP + 4 * k4]) = xb[jj][i];
+      }
+    }
+    DR_TS(dr_tbuf_gemm, 6);
+    __syncthreads();
+    DR_TS(dr_tbuf_gemm, 3);
+    for (int k16 = kb; k16 < ke; k16 += 16) {
+      const int kq = k16 + 4 * q;
+      const bool okq = kq < K;
+      float4 fa[FT], fb[FN];
+#pragma unroll
+      for (int t = 0; t < FT; ++t) {
+        fa[t] = *reinterpret_cast<const float4*>(&sA[(t * 16 + r) * KP + (okq ? kq : 0)]);
+        if (!okq) fa[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        fb[j] = *reinterpret_cast<const float4*>(&sB[(j * 16 + r) * KP + (okq ? kq : 0)]);
+        if (!okq) fb[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int t = 0; t < FT; ++t)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[t].x, fb[j].x, acc[t][j], 0, 0, 0);
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[t].y, fb[j].y, acc[t][j], 0, 0, 0);
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[t].z, fb[j].z, acc[t][j], 0, 0, 0);
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[t].w, fb[j].w, acc[t][j], 0, 0, 0);
+        }
+    }
+  } else {
+    // K loop in batches of PRE 16-k chunks: every load of a batch is issued
+    // before its first MFMA, so a wave pays one memory round trip per batch
+    // (one in total for K <= PRE*16*8 = 1024).  The first batch of weights (and
+    // of plain A rows) is issued before the LayerNorm staging.
+    constexpr int PRE = (FT >= 4) ? 4 : 8;
+    float bb[PRE][FN][4];
+    float aa[PRE][FT][4];
+    auto load_batch = [&](int kc) {
+  #pragma unroll
       for (int p = 0; p < PRE; ++p) {
         const int k16 = kc + 16 * p;
         const int kq = k16 + 4 * q;
         const bool live = k16 < ke;
-#pragma unroll
+  #pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          if (live) {
+            skinny_load_b<B_KN, VEC>(o, n0 + j * 16 + r, kq, bb[p][j]);
+          } else {
+  #pragma unroll
+            for (int c = 0; c < 4; ++c) bb[p][j][c] = 0.f;
+          }
+        }
+        if (AMODE != AM_LNSILU) {
+  #pragma unroll
+          for (int t = 0; t < FT; ++t) {
+            if (live) {
+              skinny_load_a<VEC>(o, m0 + t * 16 + r, k16, kq, aa[p][t]);
+            } else {
+  #pragma unroll
+              for (int c = 0; c < 4; ++c) aa[p][t][c] = 0.f;
+            }
+          }
+        }
+      }
+    };
+    if (kb < ke) load_batch(kb);
+
+    // direct path: LayerNorm (when K > 1024) from global memory; large-K rows
+    // staged (K <= 256 * LNV) like the staged path's A tile
+    constexpr int LNV = (MT == 16) ? 8 : 2;
+    const bool ln_lds = (AMODE == AM_LNSILU) && VEC && (MT * KP <= SK_LN_MAXF) && (K4 <= 64 * LNV);
+    if (AMODE == AM_LNSILU) {
+      if (ln_lds) {
+        const float* lg = dr_uni(g.ln_g);
+        const float* lb = dr_uni(g.ln_b);
+        float4 xv[RPW][LNV], gv[LNV], bv[LNV];
+  #pragma unroll
+        for (int i = 0; i < LNV; ++i) {
+          if (64 * i >= K4) break;  // wave-uniform: no dummy loads past the row
+          const int k4 = lane + 64 * i;
+          const bool okk = k4 < K4;
+          gv[i] = dr_ld4(lg, okk ? (unsigned)(4 * k4) : 0u);
+          bv[i] = dr_ld4(lb, okk ? (unsigned)(4 * k4) : 0u);
+  #pragma unroll
+          for (int rr = 0; rr < RPW; ++rr) {
+            const int m = m0 + wave + NWAVE * rr;
+            const bool ok = okk && m < M;
+            xv[rr][i] = dr_ld4(o.A, ok ? (unsigned)(m * o.lda + 4 * k4) : 0u);
+            if (!ok) xv[rr][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+  #pragma unroll
+        for (int rr = 0; rr < RPW; ++rr) {
+          const int ml = wave + NWAVE * rr, m = m0 + ml;
+          float sm = 0.f;
+  #pragma unroll
+          for (int i = 0; i < LNV; ++i) {
+            if (64 * i >= K4) break;
+            sm += (xv[rr][i].x + xv[rr][i].y) + (xv[rr][i].z + xv[rr][i].w);
+          }
+          const float mean = wave_sum(sm) / (float)K;
+          float sq = 0.f;
+  #pragma unroll
+          for (int i = 0; i < LNV; ++i) {
+            if (64 * i >= K4) break;
+            if (lane + 64 * i < K4) {
+              const float dx = xv[rr][i].x - mean, dy = xv[rr][i].y - mean;
+              const float dz = xv[rr][i].z - mean, dw = xv[rr][i].w - mean;
+              sq += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+            }
+          }
+          const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)K + 1e-5f);
+  #pragma unroll
+          for (int i = 0; i < LNV; ++i) {
+            if (64 * i >= K4) break;
+            const int k4 = lane + 64 * i;
+            if (k4 < K4) {
+              float4 y;
+              y.x = dr_silu_fast((xv[rr][i].x - mean) * rstd * gv[i].x + bv[i].x);
+              y.y = dr_silu_fast((xv[rr][i].y - mean) * rstd * gv[i].y + bv[i].y);
+              y.z = dr_silu_fast((xv[rr][i].z - mean) * rstd * gv[i].z + bv[i].z);
+              y.w = dr_silu_fast((xv[rr][i].w - mean) * rstd * gv[i].w + bv[i].w);
+              if (m >= M) y = make_float4(0.f, 0.f, 0.f, 0.f);
+              *reinterpret_cast<float4*>(&smem[ml * KP + 4 * k4]) = y;
+              if (store_a && m < M) *reinterpret_cast<float4*>(&a_out[(unsigned)(m * ld_aout + 4 * k4)]) = y;
+            }
+          }
+        }
+      } else {
+        for (int rr = wave; rr < MT; rr += NWAVE) {
+          const int m = m0 + rr;
+          float mean = 0.f, rstd = 0.f;
+          if (m < M) {
+            const float* row = o.A + (long long)m * o.lda;
+            float s = 0.f, v = 0.f;
+            for (int k = lane; k < K; k += 64) s += row[k];
+            mean = wave_sum(s) / (float)K;
+            for (int k = lane; k < K; k += 64) {
+              const float d = row[k] - mean;
+              v += d * d;
+            }
+            rstd = 1.0f / sqrtf(wave_sum(v) / (float)K + 1e-5f);
+          }
+          if (lane == 0) {
+            s_mean[rr] = mean;
+            s_rstd[rr] = rstd;
+          }
+        }
+      }
+      __syncthreads();
+    }
+
+    const float* lg = dr_uni(g.ln_g);
+    const float* lb = dr_uni(g.ln_b);
+    for (int kc = kb; kc < ke; kc += PRE * 16) {
+      if (kc != kb) load_batch(kc);
+      if (AMODE == AM_LNSILU) {
+  #pragma unroll
+        for (int p = 0; p < PRE; ++p) {
+          const int k16 = kc + 16 * p;
+          const int kq = k16 + 4 * q;
+          const bool live = k16 < ke;
+  #pragma unroll
+          for (int t = 0; t < FT; ++t) {
+            const int ml = t * 16 + r, m = m0 + ml;
+            if (!live) {
+  #pragma unroll
+              for (int c = 0; c < 4; ++c) aa[p][t][c] = 0.f;
+            } else if (ln_lds) {
+              if (m < M && kq < K) {
+                const float4 v = *reinterpret_cast<const float4*>(&smem[ml * KP + kq]);
+                aa[p][t][0] = v.x; aa[p][t][1] = v.y; aa[p][t][2] = v.z; aa[p][t][3] = v.w;
+              } else {
+                aa[p][t][0] = aa[p][t][1] = aa[p][t][2] = aa[p][t][3] = 0.f;
+              }
+            } else {
+              skinny_load_a<VEC>(o, m, k16, kq, aa[p][t]);
+            }
+          }
+        }
+      }
+  #pragma unroll
+      for (int p = 0; p < PRE; ++p) {
+        if (kc + 16 * p >= ke) break;
+        const int kq = kc + 16 * p + 4 * q;
+  #pragma unroll
         for (int t = 0; t < FT; ++t) {
           const int ml = t * 16 + r, m = m0 + ml;
-          if (!live) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) aa[p][t][c] = 0.f;
-          } else if (ln_lds) {
-            if (m < M && kq < K) {
-              const float4 v = *reinterpret_cast<const float4*>(&smem[ml * KP + kq]);
-              aa[p][t][0] = v.x; aa[p][t][1] = v.y; aa[p][t][2] = v.z; aa[p][t][3] = v.w;
-            } else {
-              aa[p][t][0] = aa[p][t][1] = aa[p][t][2] = aa[p][t][3] = 0.f;
-            }
-          } else {
-            skinny_load_a<VEC>(o, m, k16, kq, aa[p][t]);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int p = 0; p < PRE; ++p) {
-      if (kc + 16 * p >= ke) break;
-      const int kq = kc + 16 * p + 4 * q;
-#pragma unroll
-      for (int t = 0; t < FT; ++t) {
-        const int ml = t * 16 + r, m = m0 + ml;
-        if (AMODE == AM_LNSILU) {
-          const float mean = s_mean[ml], rstd = s_rstd[ml];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int k = kq + c;
-            if (m < M && k < K) {
-              float x = (aa[p][t][c] - mean) * rstd;
-              if (ln_lds) x = x * s_lng[k] + s_lnb[k];
-              else x = x * dr_ld1(lg, (unsigned)k) + dr_ld1(lb, (unsigned)k);
-              aa[p][t][c] = dr_silu_fast(x);
+          if (AMODE == AM_LNSILU && !ln_lds) {  // global fallback: transform on the fly
+            const float mean = s_mean[ml], rstd = s_rstd[ml];
+  #pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const int k = kq + c;
+              if (m < M && k < K) {
+                float x = (aa[p][t][c] - mean) * rstd;
+                x = x * dr_ld1(lg, (unsigned)k) + dr_ld1(lb, (unsigned)k);
+                aa[p][t][c] = dr_silu_fast(x);
+              }
             }
           }
+          if (store_a && m < M && !(AMODE == AM_LNSILU && ln_lds)) {
+  #pragma unroll
+            for (int c = 0; c < 4; ++c)
+              if (kq + c < K) a_out[(unsigned)(m * ld_aout + kq + c)] = aa[p][t][c];
+          }
         }
-        if (store_a && m < M) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-            if (kq + c < K) a_out[(unsigned)(m * ld_aout + kq + c)] = aa[p][t][c];
-        }
+  #pragma unroll
+        for (int c = 0; c < 4; ++c)
+  #pragma unroll
+          for (int t = 0; t < FT; ++t)
+  #pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[p][t][c], bb[p][j][c], acc[t][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int t = 0; t < FT; ++t)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[p][t][c], bb[p][j][c], acc[t][j], 0, 0, 0);
     }
   }
   DR_TS(dr_tbuf_gemm, 4);
-  if (AMODE == AM_LNSILU) __syncthreads();  // smem held the staged rows
+  if (staged || AMODE == AM_LNSILU) __syncthreads();  // smem held the staged rows
 #pragma unroll
   for (int t = 0; t < FT; ++t)
 #pragma unroll
@@ -740,15 +880,18 @@ static size_t min_lds() {
 }
 
 // floats of dynamic LDS a skinny launch needs (mirrors the kernel's layout)
-template <int MT, int NT, int AMODE>
+template <int MT, int NT, int AMODE, bool B_KN>
 static size_t skinny_lds_floats(const GemmBatch& gb, int count, bool vec) {
   const size_t red = (size_t)8 * (MT / 16) * (NT / 16) * 4 * 64;
   size_t need = red;
-  if (AMODE == AM_LNSILU && vec) {
-    for (int i = 0; i < count; ++i) {
-      const size_t K = gb.p[i].K, rows = (size_t)MT * (K + 4);
-      if (rows <= SK_LN_MAXF && K <= SK_LN_MAXK) need = std::max(need, std::max(rows, red) + 2 * K);
-    }
+  if (!vec) return need;
+  for (int i = 0; i < count; ++i) {
+    const size_t K = gb.p[i].K;
+    const size_t staged = (size_t)(MT + NT) * (K + 4), rows = (size_t)MT * (K + 4);
+    if (AMODE == AM_LNSILU && !B_KN && K / 4 <= 64 * 4 && staged <= SK_LN_MAXF)
+      need = std::max(need, staged);  // kernel's `staged`
+    else if (AMODE == AM_LNSILU && rows <= SK_LN_MAXF && K / 4 <= 64 * (MT == 16 ? 8 : 2))
+      need = std::max(need, rows);  // direct path, LN rows in LDS
   }
   return need;
 }
@@ -761,7 +904,7 @@ static void launch_skinny(const GemmBatch& gb, int count, bool vec, hipStream_t 
     maxt = t > maxt ? t : maxt;
   }
   if (maxt == 0) return;
-  const size_t lds = std::max(skinny_lds_floats<MT, NT, AMODE>(gb, count, vec) * sizeof(float), min_lds());
+  const size_t lds = std::max(skinny_lds_floats<MT, NT, AMODE, B_KN>(gb, count, vec) * sizeof(float), min_lds());
   if (lds > 64 * 1024) {  // opt in to more than the default dynamic LDS (once per instantiation)
     static const bool raised = [] {
       (void)hipFuncSetAttribute((const void*)k_gemm_skinny<MT, NT, AMODE, B_KN, true, EPI>,
@@ -780,9 +923,6 @@ static void launch_skinny(const GemmBatch& gb, int count, bool vec, hipStream_t 
                        lds, s, gb);
 }
 
-// tile-shape override for the kernel microbenchmark (0 = heuristic)
-static int g_force_nt = 0;
-extern "C" void dr_debug_gemm_tile(int nt) { g_force_nt = nt; }
 
 template <int AMODE, bool B_KN>
 static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
@@ -806,8 +946,6 @@ static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
     else launch_skinny<16, 16, AMODE, B_KN, EPI_ACTOR>(gb, count, vec, s);
   } else {
     if (maxM > 64) launch_skinny<64, 16, AMODE, B_KN, EPI_NONE>(gb, count, vec, s);
-    else if (g_force_nt == 32) launch_skinny<16, 32, AMODE, B_KN, EPI_NONE>(gb, count, vec, s);
-    else if (g_force_nt == 64) launch_skinny<16, 64, AMODE, B_KN, EPI_NONE>(gb, count, vec, s);
     else launch_skinny<16, 16, AMODE, B_KN, EPI_NONE>(gb, count, vec, s);
   }
   return true;

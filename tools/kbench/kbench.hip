@@ -17,7 +17,6 @@ static const char* g_filter = nullptr;
 static int g_reps = 200;
 extern "C" int dr_debug_tbuf_gru(long long* out, int n);
 extern "C" int dr_debug_tbuf_gemm(long long* out, int n);
-extern "C" void dr_debug_gemm_tile(int nt);
 
 // one more launch, then the per-phase times of wave 0 of each workgroup
 // (relative to its own start) averaged over the workgroups that wrote them
@@ -144,6 +143,31 @@ static void concurrency_probe(float* dummy) {
   }
 }
 
+// N float4 loads per lane issued back to back, then one reduction + store.
+// STRIDED: lanes r = 0..15 read 16 different rows (2400-byte stride), the
+// four q-lanes of a row read consecutive 16-byte pieces (the skinny GEMM's
+// weight-fragment pattern); otherwise fully coalesced 1 KB per wave load.
+template <int N, bool STRIDED>
+__global__ __launch_bounds__(512) void k_loads(const float* __restrict__ buf, float* out) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float4 v[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    unsigned e;
+    if (STRIDED) {
+      const int r = lane & 15, q = lane >> 4;
+      e = (unsigned)(((blockIdx.x * 16 + r) * 600 + (wave * N + i) * 16 + 4 * q) & ((1 << 22) - 1));
+    } else {
+      e = (unsigned)(((blockIdx.x * 512 + tid) * 4 + i * 262144) & ((1 << 22) - 1));
+    }
+    v[i] = dr_ld4(buf, e);
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < N; ++i) acc += v[i].x + v[i].y + v[i].z + v[i].w;
+  if (acc == 1234.5f) out[0] = acc;
+}
+
 struct Big { long long f[200]; };
 __global__ void k_empty_small(int* p) { if (p && threadIdx.x == 9999) *p = 1; }
 __global__ void k_empty_big(Big b) { if (threadIdx.x == 9999) ((int*)b.f[3])[0] = (int)b.f[150]; }
@@ -221,6 +245,19 @@ int main(int argc, char** argv) {
   }
 
   if (!g_filter || strstr("concurrency", g_filter)) concurrency_probe(dummy);
+  {
+    float* buf = frand((size_t)1 << 22);
+#define KB_LOADS(NN)                                                                                        \
+    timeit("loads " #NN " float4/lane coalesced (128 WG x 512)",                                         \
+           [&](hipStream_t st) { hipLaunchKernelGGL((k_loads<NN, false>), dim3(128), dim3(512), 0, st, buf, dummy); }, s); \
+    timeit("loads " #NN " float4/lane strided   (128 WG x 512)",                                         \
+           [&](hipStream_t st) { hipLaunchKernelGGL((k_loads<NN, true>), dim3(128), dim3(512), 0, st, buf, dummy); }, s);
+    KB_LOADS(1)
+    KB_LOADS(4)
+    KB_LOADS(8)
+    KB_LOADS(16)
+    KB_LOADS(32)
+  }
 
   // GRU
   float* wih = frand((size_t)3 * Hd * (L + A));
@@ -287,20 +324,6 @@ int main(int argc, char** argv) {
     snprintf(buf, sizeof buf, "NN plain M%d N%d K%d", sh[0], sh[1], sh[2]);
     timeit(buf, [&](hipStream_t st) { gemm_launch(G_NN, AM_PLAIN, &gk, 1, st); }, s);
   }
-  for (int nt : {32, 64}) {
-    dr_debug_gemm_tile(nt);
-    for (auto& sh : shapes) {
-      if (sh[0] > 64) continue;
-      GemmArgs g = nt_(sh[0], sh[1], sh[2]);
-      snprintf(buf, sizeof buf, "NT%d plain M%d N%d K%d", nt, sh[0], sh[1], sh[2]);
-      timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, &g, 1, st); }, s);
-      GemmArgs gl = g;
-      gl.ln_g = lng; gl.ln_b = lnb;
-      snprintf(buf, sizeof buf, "NT%d lnsilu M%d N%d K%d", nt, sh[0], sh[1], sh[2]);
-      timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_LNSILU, &gl, 1, st); }, s);
-    }
-  }
-  dr_debug_gemm_tile(0);
   // ln_silu_bwd / colsum
   timeit("ln_silu_bwd M64 K512", [&](hipStream_t st) { op_ln_silu_bwd(64, 512, X, 512, Y, 512, lng, lnb, W, 512, nullptr, nullptr, st); }, s);
   timeit("ln_silu_bwd M64 K512 +saves", [&](hipStream_t st) { op_ln_silu_bwd(64, 512, X, 512, Y, 512, lng, lnb, W, 512, W + 65536, W + 2 * 65536, st); }, s);
