@@ -66,6 +66,16 @@ __device__ __forceinline__ float dr_symlog(float x) {  // DreamerUtils.py:29-30
   } while (0)
 #endif
 
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup
+// release/acquire fence on all memory, so it waits for every outstanding
+// global load (s_waitcnt vmcnt(0)) -- including loads a pipelined loop issued
+// for later iterations.  The LDS-scoped fences wait only on lgkmcnt.
+__device__ __forceinline__ void dr_lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Kernel-argument staging.  A kernel that reads a large argument block field by
 // field issues one dependent scalar load per field, and on a graph replay the
 // argument lines are cold (each miss ~0.5 us), so the fields arrive one after
@@ -93,14 +103,30 @@ __device__ __forceinline__ T* dr_uni(T* p) {
   const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
   return (T*)(((unsigned long long)hi << 32) | lo);
 }
+// Global-memory access through pointers the compiler cannot trace to a
+// kernel argument (e.g. fields of an argument block staged in LDS): without
+// the explicit address space they become flat accesses, which count on both
+// vmcnt and lgkmcnt -- every LDS wait would then drain all global loads.
+#define DR_GLOBAL __attribute__((address_space(1)))
+typedef float dr_f4 __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ __forceinline__ DR_GLOBAL T* dr_g(T* p) {
+  return (DR_GLOBAL T*)p;
+}
 // loads at a 32-bit element offset from a uniform base (callers guarantee
-// offsets < 2^30 elements)
+// offsets < 2^30 elements): global_load with saddr + voffset
 __device__ __forceinline__ float4 dr_ld4(const float* base, unsigned e) {
-  return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + (e << 2));
+  const dr_f4 t = *(const DR_GLOBAL dr_f4*)((const DR_GLOBAL char*)base + (e << 2));
+  return make_float4(t.x, t.y, t.z, t.w);
 }
 __device__ __forceinline__ float dr_ld1(const float* base, unsigned e) {
-  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (e << 2));
+  return *(const DR_GLOBAL float*)((const DR_GLOBAL char*)base + (e << 2));
 }
+__device__ __forceinline__ void dr_st4(float* base, unsigned e, float4 v) {
+  dr_f4 t = {v.x, v.y, v.z, v.w};
+  *(DR_GLOBAL dr_f4*)((DR_GLOBAL char*)base + (e << 2)) = t;
+}
+
 // SiLU on the hardware exp2 / reciprocal (~2 ulp, 6 VALU instead of ~25 for
 // the IEEE expf + division); used where the input is transformed once per
 // consuming tile, inside the GEMM prologue

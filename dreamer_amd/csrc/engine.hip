@@ -6,6 +6,7 @@
 
 #include "conv.h"
 #include "gemm.h"
+#include <limits.h>
 #include "gru.h"
 #include "ops.h"
 
@@ -107,6 +108,44 @@ static GemmArgs bwd_nt(int M, int N, int K, const float* G, long long ldg, const
   g.accumulate = accumulate;
   return g;
 }
+static int run(GemmLayout lay, int amode, const GemmArgs& a, hipStream_t s) { return gemm_launch(lay, amode, &a, 1, s); }
+
+// split-K scratch for the tile GEMM: hand problem g up to 4 partial planes
+// from a carved region (grouped problems take disjoint slices)
+#define DR_SPLITK_MAX 4
+static void give_splitk(GemmArgs& g, float*& cur, long long& left) {
+  const long long need = (long long)DR_SPLITK_MAX * g.M * g.N;
+  if (!cur || left < need) return;
+  g.splitk_ws = cur;
+  g.splitk_floats = need;
+  cur += need;
+  left -= need;
+}
+static long long splitk_floats(long long M, long long N) { return DR_SPLITK_MAX * M * N; }
+
+// input gradient through SiLU(LayerNorm(pre)) and a transposed weight, fused:
+// the GEMM's staged prologue computes g_pre from (gx, pre) (gemm.h AM_LNBWD);
+// g_pre and the LN-parameter saves are written when requested.  Falls back to
+// k_ln_silu_bwd + NT GEMM where the fused path does not apply.
+static int lnbwd_nt(int M, int N, int K, const float* gx, long long ldgx, const float* pre, long long ld_pre,
+                    const dr_linear& ln, const float* WT, float* Y, long long ldy, int accumulate, float* gpre,
+                    long long ld_gpre, float* gy, float* xh, float* Y2, long long ldy2, int nsplitY, hipStream_t s) {
+  GemmArgs g = bwd_nt(M, N, K, gx, ldgx, WT, Y, ldy, accumulate);
+  g.Y2 = Y2; g.ldy2 = ldy2; g.nsplitY = nsplitY;
+  const bool ok = K % 4 == 0 && K <= (M <= 64 ? 1024 : 256) && M <= 4096 && ldgx % 4 == 0 && ld_pre % 4 == 0 &&
+                  ((((uintptr_t)gx | (uintptr_t)pre | (uintptr_t)WT | (uintptr_t)ln.w | (uintptr_t)ln.b) & 15) == 0);
+  if (ok) {
+    g.pre = pre; g.ld_pre = ld_pre; g.ln_g = ln.w; g.ln_b = ln.b;
+    g.a_out = gpre; g.ld_aout = ld_gpre;
+    g.sv_gy = gy; g.sv_xh = xh; g.ld_sv = ld_gpre;
+    return run(G_NT, AM_LNBWD, g, s);
+  }
+  DR_REQUIRE(gpre != nullptr, "LN-backward fallback needs a g_pre buffer");
+  DR_TRY(op_ln_silu_bwd(M, K, gx, ldgx, pre, ld_pre, ln.w, ln.b, gpre, ld_gpre, gy, xh, s));
+  g.A = gpre; g.lda = ld_gpre;
+  return run(G_NT, AM_PLAIN, g, s);
+}
+
 // weight gradient: dW[M=out][N=in] = sum_r G[r][m] X[r][n]  (rows r < R)
 static GemmArgs bwd_w(int out, int in, int R, const float* G, long long ldg, const float* X, long long ldx, float* dW) {
   GemmArgs g = gemm_args();
@@ -117,7 +156,6 @@ static GemmArgs bwd_w(int out, int in, int R, const float* G, long long ldg, con
   return g;
 }
 
-static int run(GemmLayout lay, int amode, const GemmArgs& a, hipStream_t s) { return gemm_launch(lay, amode, &a, 1, s); }
 
 // one-hot index buffers hold [B][R] class indices followed by the [B][R]
 // straight-through values at those indices (what the fused GRU gathers)
@@ -164,12 +202,15 @@ static int stack_heads(const dr_actor* ac, int A, int in, float* w, float* b, hi
 // a3  encoder features
 // ===========================================================================
 struct EncWs {
-  float *x0, *a1, *a2, *a3, *a4, *wr1, *wr2, *wr3, *wr4;
+  float *x0, *a1, *a2, *a3, *a4, *wr1, *wr2, *wr3, *wr4, *sk;
+  long long sk_n;
 };
 
 static void enc_carve(Carve& c, const dr_dims* d, int n, EncWs& w) {
   const int c1 = d->enc_f1, c2 = d->enc_f2, c3 = 2 * d->enc_f2, c4 = 4 * d->enc_f2;
   const long long p0 = (long long)d->img_h * d->img_w, p1 = p0 / 4, p2 = p1 / 4, p3 = p2 / 4, p4 = p3 / 4;
+  w.sk_n = splitk_floats(n, d->enc_hidden);
+  w.sk = c.f(w.sk_n);
   w.x0 = c.f((long long)n * p0 * 4);
   w.a1 = c.f((long long)n * p1 * c1);
   w.a2 = c.f((long long)n * p2 * c2);
@@ -212,7 +253,11 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
   // last layer in NCHW == nn.Flatten order of Encoder.forward (VAE.py:72)
   DR_TRY(op_conv_nhwc(n, c3, h0 / 8, w0 / 8, c4, w.a3, w.wr4, wm->conv[3].b, w.a4, 1, s));
   const int F = c4 * (h0 / 16) * (w0 / 16);
-  return run(G_NT, AM_PLAIN, lin(n, d->enc_hidden, F, w.a4, F, wm->map0.w, F + d->hidden, wm->map0.b, feat, d->enc_hidden), s);
+  GemmArgs gp = lin(n, d->enc_hidden, F, w.a4, F, wm->map0.w, F + d->hidden, wm->map0.b, feat, d->enc_hidden);
+  float* sk = w.sk;
+  long long skn = w.sk_n;
+  give_splitk(gp, sk, skn);
+  return run(G_NT, AM_PLAIN, gp, s);
 }
 
 // ===========================================================================
@@ -353,7 +398,8 @@ struct ImWs {
   int* idx[2];
   // backward
   float *gH, *gZ, *gA, *glog, *gx2, *gp2, *gx1, *gp1, *ggi, *ggh, *gheads, *gx2a, *gpre2a, *gy2a, *xh2a, *gx1a,
-      *gpre1a, *gy1a, *xh1a, *hcat, *zcat;
+      *gpre1a, *gy1a, *xh1a, *hcat, *zcat, *sk;
+  long long sk_n;
   // transposed weights for the input-gradient GEMMs (NT with float4 loads)
   float *tl6p, *tl3p, *tl0p, *twhh, *thead, *tl3a, *tl0a;
 };
@@ -402,6 +448,9 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.xh1a = c.f(BH * d->actor_h1);
   w.hcat = c.f(BH * Hd);
   w.zcat = c.f(BH * L);
+  w.sk_n = splitk_floats(d->actor_h1, Hd + L) + splitk_floats(d->actor_h2, d->actor_h1) +
+           2 * splitk_floats(A, d->actor_h2);
+  w.sk = c.f(w.sk_n);
 }
 
 extern "C" size_t dr_imagine_workspace_bytes(const dr_dims* d, int B, int H) {
@@ -568,14 +617,13 @@ extern "C" int dr_imagine_bwd(const dr_dims* d, const dr_world_model* wm, const 
     if (state_grad) {
       // z_{t+1} = STE(prior(h_{t+1}))   (DynamicsPredictors.py:31-40)
       DR_TRY(op_softmax_ste_bwd(B, d->rows, d->cols, gZ_n, ldL, tp.soft + (long long)t * B * L, L, w.glog, s));
-      DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, d->prior_h2, L, w.glog, L, w.tl6p, w.gx2, d->prior_h2, 0), s));
-      DR_TRY(op_ln_silu_bwd(B, d->prior_h2, w.gx2, d->prior_h2, tp.pre2p + (long long)t * B * d->prior_h2, d->prior_h2,
-                            wm->prior.n4.w, wm->prior.n4.b, w.gp2, d->prior_h2, nullptr, nullptr, s));
-      DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, d->prior_h1, d->prior_h2, w.gp2, d->prior_h2, w.tl3p, w.gx1, d->prior_h1, 0),
-                 s));
-      DR_TRY(op_ln_silu_bwd(B, d->prior_h1, w.gx1, d->prior_h1, tp.pre1p + (long long)t * B * d->prior_h1, d->prior_h1,
-                            wm->prior.n1.w, wm->prior.n1.b, w.gp1, d->prior_h1, nullptr, nullptr, s));
-      DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, Hd, d->prior_h1, w.gp1, d->prior_h1, w.tl0p, gH_n, ldH, 1), s));
+      const int h1 = d->prior_h1, h2 = d->prior_h2;
+      DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, h2, L, w.glog, L, w.tl6p, w.gx2, h2, 0), s));
+      // dynamic_predictor.4/.3 and .1/.0: LN-SiLU backward fused into the next input-gradient GEMM
+      DR_TRY(lnbwd_nt(B, h1, h2, w.gx2, h2, tp.pre2p + (long long)t * B * h2, h2, wm->prior.n4, w.tl3p, w.gx1, h1, 0,
+                      w.gp2, h2, nullptr, nullptr, nullptr, 0, INT_MAX, s));
+      DR_TRY(lnbwd_nt(B, Hd, h1, w.gx1, h1, tp.pre1p + (long long)t * B * h1, h1, wm->prior.n1, w.tl0p, gH_n, ldH, 1,
+                      w.gp1, h1, nullptr, nullptr, nullptr, 0, INT_MAX, s));
       // h_{t+1} = GRU(z_t, a_t, h_t)   (SequenceModel.py:19-24)
       DR_TRY(op_gru_bwd(B, Hd, gH_n, ldH, hiddens + (long long)t * Hd, ldH, tp.r + hb, tp.u + hb, tp.n + hb,
                         tp.ghn + hb, w.ggi, w.ggh, gH_t, ldH, 1, s));
@@ -600,15 +648,17 @@ extern "C" int dr_imagine_bwd(const dr_dims* d, const dr_world_model* wm, const 
       DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, a2, 2 * A, gh_t, (long long)H * 2 * A, w.thead, w.gx2a, a2, 0), s));
     }
     const long long o2 = (long long)t * a2, o1 = (long long)t * a1;
-    DR_TRY(op_ln_silu_bwd(B, a2, w.gx2a, a2, tp.pre2a + o2, lda2, ac->n4.w, ac->n4.b, w.gpre2a + o2, lda2,
-                          w.gy2a + o2, w.xh2a + o2, s));
-    DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, a1, a2, w.gpre2a + o2, lda2, w.tl3a, w.gx1a, a1, 0), s));
-    DR_TRY(op_ln_silu_bwd(B, a1, w.gx1a, a1, tp.pre1a + o1, lda1, ac->n1.w, ac->n1.b, w.gpre1a + o1, lda1,
-                          w.gy1a + o1, w.xh1a + o1, s));
+    // base_net.4/.3: LN-SiLU backward fused into the .3 input-gradient GEMM; the
+    // prologue also writes g_pre and the LN-parameter saves for the weight grads
+    DR_TRY(lnbwd_nt(B, a1, a2, w.gx2a, a2, tp.pre2a + o2, lda2, ac->n4, w.tl3a, w.gx1a, a1, 0, w.gpre2a + o2, lda2,
+                    w.gy2a + o2, w.xh2a + o2, nullptr, 0, INT_MAX, s));
     if (t > 0) {
-      GemmArgs g = bwd_nt(B, Hd + L, a1, w.gpre1a + o1, lda1, w.tl0a, gH_t, ldH, 1);
-      g.Y2 = gZ_t; g.ldy2 = ldL; g.nsplitY = Hd;
-      DR_TRY(run(G_NT, AM_PLAIN, g, s));
+      DR_TRY(lnbwd_nt(B, Hd + L, a1, w.gx1a, a1, tp.pre1a + o1, lda1, ac->n1, w.tl0a, gH_t, ldH, 1, w.gpre1a + o1,
+                      lda1, w.gy1a + o1, w.xh1a + o1, gZ_t, ldL, Hd, s));
+    } else {
+      // step 0 feeds no state gradient: only the saves for the weight grads
+      DR_TRY(op_ln_silu_bwd(B, a1, w.gx1a, a1, tp.pre1a + o1, lda1, ac->n1.w, ac->n1.b, w.gpre1a + o1, lda1,
+                            w.gy1a + o1, w.xh1a + o1, s));
     }
   }
   // ---- actor weight gradients over all B*H rows (rows r = b*H + t) ----
@@ -621,6 +671,9 @@ extern "C" int dr_imagine_bwd(const dr_dims* d, const dr_world_model* wm, const 
     p[1] = bwd_w(a2, a1, BH, w.gpre2a, a2, tp.x1a, a1, gr->l3.w);
     p[2] = bwd_w(A, a2, BH, w.gheads, 2 * A, tp.x2a, a2, gr->mu.w);
     p[3] = bwd_w(A, a2, BH, w.gheads + A, 2 * A, tp.x2a, a2, gr->ls.w);
+    float* sk = w.sk;
+    long long skn = w.sk_n;
+    for (int i = 0; i < 4; ++i) give_splitk(p[i], sk, skn);
     DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 4, s));
   }
   {
@@ -660,6 +713,7 @@ static size_t critic_ws_bytes(const dr_dims* d, int M) {
   Carve c(nullptr);
   CTape t;
   ctape_carve(c, d, M, t);
+  c.f(splitk_floats(M, d->critic_h1));
   return c.off;
 }
 
@@ -668,16 +722,33 @@ extern "C" int dr_critic_fwd(const dr_dims* d, const dr_critic* cr, int M, const
                              size_t ws_bytes, hipStream_t s) {
   DR_REQUIRE(d && cr && h && z && M > 0, "null argument or empty batch");
   CTape t;
+  float* sk = nullptr;
+  long long skn = 0;
   if (tape) {
     Carve c(tape);
     ctape_carve(c, d, M, t);
-  } else {
-    Carve c(ws);
-    ctape_carve(c, d, M, t);
-    WS_CHECK(c, ws_bytes);
   }
+  if (ws) {  // scratch: the tape (when none is given), then split-K partials if they fit
+    Carve c(ws);
+    CTape tw;
+    ctape_carve(c, d, M, tw);
+    if (!tape) {
+      t = tw;
+      WS_CHECK(c, ws_bytes);
+    }
+    const long long want = splitk_floats(M, d->critic_h1);
+    if (c.off + (size_t)want * sizeof(float) + 256 <= ws_bytes) {
+      skn = want;
+      sk = c.f(skn);
+    }
+  }
+  DR_REQUIRE(tape || ws, "dr_critic_fwd needs a tape or a workspace");
   const int L = latent(d), Hd = d->hidden, c1 = d->critic_h1, c2 = d->critic_h2, nb = d->buckets;
-  DR_TRY(run(G_NT, AM_PLAIN, lin2(M, c1, h, ldh, Hd, z, ldz, L, cr->net.l0.w, cr->net.l0.b, t.pre1, c1), s));
+  {
+    GemmArgs g1 = lin2(M, c1, h, ldh, Hd, z, ldz, L, cr->net.l0.w, cr->net.l0.b, t.pre1, c1);
+    give_splitk(g1, sk, skn);
+    DR_TRY(run(G_NT, AM_PLAIN, g1, s));
+  }
   GemmArgs g2 = lin_ln(M, c2, c1, t.pre1, c1, cr->net.n1, cr->net.l3.w, cr->net.l3.b, t.pre2, c2);
   g2.a_out = t.x1; g2.ld_aout = c1;
   DR_TRY(run(G_NT, AM_LNSILU, g2, s));
@@ -693,10 +764,15 @@ extern "C" int dr_critic_fwd(const dr_dims* d, const dr_critic* cr, int M, const
 struct CBws {
   float *row_loss, *glog, *gx2, *gp2, *gy2, *xh2, *gx1, *gp1, *gy1, *xh1;
   float *tl6, *tl3;  // transposed value_net.6 / .3 weights
+  float* sk;         // split-K partials of the weight-gradient GEMMs
+  long long sk_n;
 };
 static void cbws_carve(Carve& c, const dr_dims* d, int B, int H, CBws& w) {
   const long long M = (long long)B * (H + 1);
   w.row_loss = c.f((long long)B * H);
+  w.sk_n = splitk_floats(d->buckets, d->critic_h2) + splitk_floats(d->critic_h2, d->critic_h1) +
+           splitk_floats(d->critic_h1, d->hidden + latent(d));
+  w.sk = c.f(w.sk_n);
   w.tl6 = c.f((long long)d->buckets * d->critic_h2);
   w.tl3 = c.f((long long)d->critic_h2 * d->critic_h1);
   w.glog = c.f(M * d->buckets);
@@ -739,8 +815,8 @@ extern "C" int dr_critic_loss_bwd(const dr_dims* d, const dr_critic* cr, int B, 
     DR_TRY(op_transpose_multi(tj, 2, s));
   }
   DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M, c2, nb, w.glog, nb, w.tl6, w.gx2, c2, 0), s));
-  DR_TRY(op_ln_silu_bwd(M, c2, w.gx2, c2, t.pre2, c2, cr->net.n4.w, cr->net.n4.b, w.gp2, c2, w.gy2, w.xh2, s));
-  DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M, c1, c2, w.gp2, c2, w.tl3, w.gx1, c1, 0), s));
+  DR_TRY(lnbwd_nt(M, c1, c2, w.gx2, c2, t.pre2, c2, cr->net.n4, w.tl3, w.gx1, c1, 0, w.gp2, c2, w.gy2, w.xh2, nullptr,
+                  0, INT_MAX, s));
   DR_TRY(op_ln_silu_bwd(M, c1, w.gx1, c1, t.pre1, c1, cr->net.n1.w, cr->net.n1.b, w.gp1, c1, w.gy1, w.xh1, s));
   {
     GemmArgs p[3];
@@ -748,6 +824,9 @@ extern "C" int dr_critic_loss_bwd(const dr_dims* d, const dr_critic* cr, int B, 
     p[1] = bwd_w(c2, c1, M, w.gp2, c2, t.x1, c1, gr->net.l3.w);
     p[2] = bwd_w(c1, Hd + L, M, w.gp1, c1, hiddens, Hd, gr->net.l0.w);
     p[2].W2 = latents; p[2].ldb2 = L; p[2].nsplitB = Hd;
+    float* sk = w.sk;
+    long long skn = w.sk_n;
+    for (int i = 0; i < 3; ++i) give_splitk(p[i], sk, skn);
     DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 3, s));
   }
   {

@@ -7,7 +7,11 @@
 #pragma once
 #include "common.h"
 
-enum { AM_PLAIN = 0, AM_LNSILU = 1, AM_CONV = 2, AM_CONV_SRC = 3 };
+enum { AM_PLAIN = 0, AM_LNSILU = 1, AM_CONV = 2, AM_CONV_SRC = 3, AM_LNBWD = 4 };
+// AM_LNBWD (NT skinny only): A = d/d(pre) of SiLU(LayerNorm(pre)) given the
+// upstream gradient gx = A-argument rows; the LN input `pre` and gamma/beta
+// (ln_g/ln_b) come from the fields below.  a_out receives g_pre, sv_gy /
+// sv_xh the SiLU-input gradient and x_hat (for the LayerNorm parameter grads).
 
 struct alignas(16) GemmArgs {
   int M, N, K;
@@ -16,6 +20,9 @@ struct alignas(16) GemmArgs {
   const float* A2; long long lda2; int ksplitA;  // MK: k >= ksplitA reads A2[m][k-ksplitA]
   const float* ln_g; const float* ln_b;          // AM_LNSILU (LN width == K)
   float* a_out; long long ld_aout;               // optional copy of the transformed A (n-tile 0 writes)
+  const float* pre; long long ld_pre;            // AM_LNBWD: LayerNorm input rows
+  float* splitk_ws; long long splitk_floats;     // optional scratch for split-K partials (tile GEMM)
+  float* sv_gy; float* sv_xh; long long ld_sv;   // AM_LNBWD: optional saves (n-tile 0 writes)
   // conv im2col (k4 s2 p1), A = NCHW activations [frame][cin][ih][iw]
   int cin, ih, iw, oh, ow;
   dr_frames src;                                 // AM_CONV_SRC: frames, f = t*nb + b

@@ -77,17 +77,15 @@ __device__ __forceinline__ float load_a_mk(const GemmArgs& g, int m, int k, floa
 }
 
 __device__ __forceinline__ float load_b(const GemmArgs& g, bool kn, int n, int k) {
-  if (!kn) return g.W[(long long)n * g.ldb + k];
-  if (k >= g.ksplitB) return g.W2[(long long)(k - g.ksplitB) * g.ldb2 + n];
-  if (n >= g.nsplitB) return g.W2[(long long)k * g.ldb2 + (n - g.nsplitB)];
-  return g.W[(long long)k * g.ldb + n];
+  if (!kn) return dr_g(g.W)[(long long)n * g.ldb + k];
+  if (k >= g.ksplitB) return dr_g(g.W2)[(long long)(k - g.ksplitB) * g.ldb2 + n];
+  if (n >= g.nsplitB) return dr_g(g.W2)[(long long)k * g.ldb2 + (n - g.nsplitB)];
+  return dr_g(g.W)[(long long)k * g.ldb + n];
 }
 
 template <int BM, int BN, int AMODE, bool A_KM, bool B_KN>
 __global__ __launch_bounds__(256) void k_gemm(GemmBatch gb) {
-  __shared__ GemmArgs s_args;
-  dr_stage_args(gb.p[blockIdx.z], s_args, threadIdx.x);
-  const GemmArgs& g = s_args;
+  const GemmArgs& g = gb.p[blockIdx.z];  // kernarg pointers: the compiler keeps them global
   const int tiles_n = (g.N + BN - 1) / BN;
   const int tiles_m = (g.M + BM - 1) / BM;
   if ((int)blockIdx.x >= tiles_m * tiles_n) return;
@@ -323,7 +321,7 @@ __device__ __forceinline__ void skinny_load_a(const SkOps& o, int m, int k16, in
       v = dr_ld4(o.A2, ok ? (unsigned)(m * o.lda2 + kq - o.ksA) : 0u);
     } else {
       const float* src = (kq < o.ksA) ? o.A + (long long)m * o.lda + kq : o.A2 + (long long)m * o.lda2 + (kq - o.ksA);
-      v = *reinterpret_cast<const float4*>(ok ? src : o.A);
+      v = dr_ld4(ok ? src : o.A, 0u);
     }
     if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
     a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
@@ -349,11 +347,11 @@ __device__ __forceinline__ float epi_act(const GemmArgs& g, float v) {
 __device__ __forceinline__ void epilogue_store_b(const GemmArgs& g, int m, int n, float acc, float bias) {
   float v = (g.alpha == 1.0f) ? acc : g.alpha * acc;
   if (g.bias) v = v + bias;
-  if (g.addend) v = v + g.addend[(long long)m * g.ld_add + n];
+  if (g.addend) v = v + dr_g(g.addend)[(long long)m * g.ld_add + n];
   v = epi_act(g, v);
-  float* dst;
-  if (n < g.nsplitY) dst = g.Y + (long long)m * g.ldy + n;
-  else dst = g.Y2 + (long long)m * g.ldy2 + (n - g.nsplitY);
+  DR_GLOBAL float* dst;
+  if (n < g.nsplitY) dst = dr_g(g.Y) + (long long)m * g.ldy + n;
+  else dst = dr_g(g.Y2) + (long long)m * g.ldy2 + (n - g.nsplitY);
   if (g.accumulate) *dst = *dst + v;
   else *dst = v;
 }
@@ -417,29 +415,36 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
   // with a padded stride (K + 4 floats: the 16 rows an MFMA fragment reads
   // fall in distinct banks); the K loop then reads fragments from LDS.
   // Direct (otherwise): each lane loads its MFMA fragments from global memory.
-  const int KP = K + 4;
+  const int KP = K + ((8 - (K & 15)) & 15);  // row stride = 8 mod 16 dwords: ds_read_b128 fragments conflict-free
   const int K4 = K >> 2;
   constexpr int RPW = MT / NWAVE;                    // A rows per wave
   constexpr int BPW = (NT + NWAVE - 1) / NWAVE;      // weight rows per wave
-  constexpr int SV = 4;                              // float4 per lane per staged row (K <= 1024)
+  constexpr int SV = (MT == 16) ? 4 : 1;             // float4 per lane per staged row (K <= 256 * SV)
   float* a_out = dr_uni(g.a_out);
   const int ld_aout = dr_uni((int)g.ld_aout);
   const bool store_a = (a_out != nullptr) && (tn == 0);
   // (measured: staging pays only where the LayerNorm needs the barrier anyway;
   // a plain GEMM is faster with direct fragment loads, profiles/r01_v5_kbench.txt)
-  const bool staged = (AMODE == AM_LNSILU) && VEC && !B_KN && (K4 <= 64 * SV) && ((MT + NT) * KP <= SK_LN_MAXF);
-  f32x4 acc[FT][FN];
+  const bool staged = (AMODE == AM_LNSILU || AMODE == AM_LNBWD) && VEC && !B_KN && (K4 <= 64 * SV) &&
+                     ((MT + NT) * KP <= SK_LN_MAXF);
+  // with few accumulator tiles, alternate 16-k chunks between two accumulator
+  // sets so consecutive MFMAs are independent (40-cycle result latency)
+  constexpr bool DUAL = FT * FN < 4;
+  f32x4 acc[FT][FN], acc2[FT][FN];
 #pragma unroll
   for (int t = 0; t < FT; ++t)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[t][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[t][j] = acc2[t][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   DR_TS(dr_tbuf_gemm, 1);
   if (staged) {
     float* sA = smem;
     float* sB = smem + MT * KP;
-    float4 xa[RPW][SV], xb[BPW][SV], gv[SV], bv[SV];
+    constexpr int PRW = (AMODE == AM_LNBWD) ? RPW : 1;
+    float4 xa[RPW][SV], xb[BPW][SV], gv[SV], bv[SV], xp[PRW][SV];
     const float* lg = dr_uni(g.ln_g);
     const float* lb = dr_uni(g.ln_b);
+    const float* pre = dr_uni(g.pre);
+    const int ld_pre = dr_uni((int)g.ld_pre);
 #pragma unroll
     for (int i = 0; i < SV; ++i) {
       if (64 * i >= K4) break;  // wave-uniform: no dummy loads past the row
@@ -454,6 +459,10 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
         const unsigned e = ok ? (unsigned)(seg1 ? m * o.lda + k : m * o.lda2 + k - o.ksA) : 0u;
         xa[rr][i] = dr_ld4(ok ? base : o.W, e);
         if (!ok) xa[rr][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (AMODE == AM_LNBWD) {
+          xp[rr][i] = dr_ld4(pre, ok ? (unsigned)(m * ld_pre + k) : 0u);
+          if (!ok) xp[rr][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
       }
 #pragma unroll
       for (int jj = 0; jj < BPW; ++jj) {
@@ -462,7 +471,7 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
         xb[jj][i] = dr_ld4(o.W, ok ? (unsigned)(n * o.ldb + k) : 0u);
         if (!ok) xb[jj][i] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      if (AMODE == AM_LNSILU) {
+      if (AMODE == AM_LNSILU || AMODE == AM_LNBWD) {
         gv[i] = dr_ld4(lg, okk ? (unsigned)k : 0u);
         bv[i] = dr_ld4(lb, okk ? (unsigned)k : 0u);
       }
@@ -501,13 +510,88 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
           if (m >= M) x = make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
+      if (AMODE == AM_LNBWD) {
+        // SiLU(LayerNorm(pre)) backward (ops.hip k_ln_silu_bwd, restated on
+        // registers): x_hat, y, s = sigmoid(y), dy = gx * s(1 + y(1 - s)),
+        // dx_hat = dy*gamma, g_pre = rstd (dx_hat - mean(dx_hat) - x_hat mean(dx_hat x_hat))
+        const int PR = (AMODE == AM_LNBWD) ? rr : 0;
+        float sm = 0.f;
+#pragma unroll
+        for (int i = 0; i < SV; ++i) {
+          if (64 * i >= K4) break;
+          sm += (xp[PR][i].x + xp[PR][i].y) + (xp[PR][i].z + xp[PR][i].w);
+        }
+        const float mean = wave_sum(sm) / (float)K;
+        float sq = 0.f;
+#pragma unroll
+        for (int i = 0; i < SV; ++i) {
+          if (64 * i >= K4) break;
+          if (lane + 64 * i < K4) {
+            const float dx = xp[PR][i].x - mean, dy = xp[PR][i].y - mean;
+            const float dz = xp[PR][i].z - mean, dw = xp[PR][i].w - mean;
+            sq += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+          }
+        }
+        const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)K + 1e-5f);
+        float c1 = 0.f, c2 = 0.f;
+        float* sgy = dr_uni(g.sv_gy);
+        float* sxh = dr_uni(g.sv_xh);
+        const int ld_sv = dr_uni((int)g.ld_sv);
+        const bool save = sgy && tn == 0 && m < M;
+#pragma unroll
+        for (int i = 0; i < SV; ++i) {
+          if (64 * i >= K4) break;
+          const int k4 = lane + 64 * i;
+          const bool okk = k4 < K4;
+          float4 xh, gy;
+          float* xhp = &xh.x;
+          float* gyp = &gy.x;
+          const float* pp = &xp[PR][i].x;
+          const float* gxp = &xa[rr][i].x;
+          const float* gg = &gv[i].x;
+          const float* bb4 = &bv[i].x;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float x_h = (pp[c] - mean) * rstd;
+            const float y = x_h * gg[c] + bb4[c];
+            const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(y * -1.4426950408889634f));
+            const float gyv = gxp[c] * (sg * (1.0f + y * (1.0f - sg)));
+            const float gxh = gyv * gg[c];
+            xhp[c] = x_h;
+            gyp[c] = gxh;  // keep dx_hat for the last pass
+            if (okk) {
+              c1 += gxh;
+              c2 += gxh * x_h;
+            }
+            if (save && okk) {
+              dr_g(sgy)[(unsigned)(m * ld_sv + 4 * k4 + c)] = gyv;
+              dr_g(sxh)[(unsigned)(m * ld_sv + 4 * k4 + c)] = x_h;
+            }
+          }
+          xa[rr][i] = gy;   // dx_hat
+          xp[PR][i] = xh;   // x_hat
+        }
+        c1 = wave_sum(c1) / (float)K;
+        c2 = wave_sum(c2) / (float)K;
+#pragma unroll
+        for (int i = 0; i < SV; ++i) {
+          if (64 * i >= K4) break;
+          float4& x = xa[rr][i];
+          const float4& h = xp[PR][i];
+          x.x = rstd * (x.x - c1 - h.x * c2);
+          x.y = rstd * (x.y - c1 - h.y * c2);
+          x.z = rstd * (x.z - c1 - h.z * c2);
+          x.w = rstd * (x.w - c1 - h.w * c2);
+          if (m >= M) x = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < SV; ++i) {
         if (64 * i >= K4) break;
         const int k4 = lane + 64 * i;
         if (k4 < K4) {
           *reinterpret_cast<float4*>(&sA[ml * KP + 4 * k4]) = xa[rr][i];
-          if (store_a && m < M) *reinterpret_cast<float4*>(&a_out[(unsigned)(m * ld_aout + 4 * k4)]) = xa[rr][i];
+          if (store_a && m < M) dr_st4(a_out, (unsigned)(m * ld_aout + 4 * k4), xa[rr][i]);
         }
       }
     }
@@ -528,6 +612,7 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
     for (int k16 = kb; k16 < ke; k16 += 16) {
       const int kq = k16 + 4 * q;
       const bool okq = kq < K;
+      f32x4 (&ac)[FT][FN] = (DUAL && (((k16 - kb) >> 4) & 1)) ? acc2 : acc;
       float4 fa[FT], fb[FN];
 #pragma unroll
       for (int t = 0; t < FT; ++t) {
@@ -542,12 +627,19 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
 #pragma unroll
       for (int t = 0; t < FT; ++t)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[t].x, fb[j].x, acc[t][j], 0, 0, 0);
-          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[t].y, fb[j].y, acc[t][j], 0, 0, 0);
-          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[t].z, fb[j].z, acc[t][j], 0, 0, 0);
-          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[t].w, fb[j].w, acc[t][j], 0, 0, 0);
-        }
+        for (int j = 0; j < FN; ++j) ac[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[t].x, fb[j].x, ac[t][j], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < FT; ++t)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) ac[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[t].y, fb[j].y, ac[t][j], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < FT; ++t)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) ac[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[t].z, fb[j].z, ac[t][j], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < FT; ++t)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) ac[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[t].w, fb[j].w, ac[t][j], 0, 0, 0);
     }
   } else {
     // K loop in batches of PRE 16-k chunks: every load of a batch is issued
@@ -644,7 +736,7 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
               y.w = dr_silu_fast((xv[rr][i].w - mean) * rstd * gv[i].w + bv[i].w);
               if (m >= M) y = make_float4(0.f, 0.f, 0.f, 0.f);
               *reinterpret_cast<float4*>(&smem[ml * KP + 4 * k4]) = y;
-              if (store_a && m < M) *reinterpret_cast<float4*>(&a_out[(unsigned)(m * ld_aout + 4 * k4)]) = y;
+              if (store_a && m < M) dr_st4(a_out, (unsigned)(m * ld_aout + 4 * k4), y);
             }
           }
         }
@@ -653,7 +745,7 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
           const int m = m0 + rr;
           float mean = 0.f, rstd = 0.f;
           if (m < M) {
-            const float* row = o.A + (long long)m * o.lda;
+            const DR_GLOBAL float* row = dr_g(o.A) + (long long)m * o.lda;
             float s = 0.f, v = 0.f;
             for (int k = lane; k < K; k += 64) s += row[k];
             mean = wave_sum(s) / (float)K;
@@ -723,18 +815,25 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
           if (store_a && m < M && !(AMODE == AM_LNSILU && ln_lds)) {
   #pragma unroll
             for (int c = 0; c < 4; ++c)
-              if (kq + c < K) a_out[(unsigned)(m * ld_aout + kq + c)] = aa[p][t][c];
+              if (kq + c < K) dr_g(a_out)[(unsigned)(m * ld_aout + kq + c)] = aa[p][t][c];
           }
         }
+        f32x4 (&ac)[FT][FN] = (DUAL && (p & 1)) ? acc2 : acc;
   #pragma unroll
         for (int c = 0; c < 4; ++c)
   #pragma unroll
           for (int t = 0; t < FT; ++t)
   #pragma unroll
             for (int j = 0; j < FN; ++j)
-              acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[p][t][c], bb[p][j][c], acc[t][j], 0, 0, 0);
+              ac[t][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa[p][t][c], bb[p][j][c], ac[t][j], 0, 0, 0);
       }
     }
+  }
+  if (DUAL) {
+#pragma unroll
+    for (int t = 0; t < FT; ++t)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[t][j] += acc2[t][j];
   }
   DR_TS(dr_tbuf_gemm, 4);
   if (staged || AMODE == AM_LNSILU) __syncthreads();  // smem held the staged rows
@@ -763,7 +862,7 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
     } else {
       if (m < M && n < N) {
         float y = v + ebias[i];
-        if (g.Y) g.Y[(long long)m * g.ldy + n] = y;
+        if (g.Y) dr_g(g.Y)[(long long)m * g.ldy + n] = y;
         s_out[ml][nl] = y;
       }
     }
@@ -794,7 +893,7 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
       float qv = 1.0f;
       const int Rg = g.R;
       if (act) {
-        if (g.noise.q) qv = g.noise.q[((long long)g.step * M * Rg + (long long)m * Rg + grp) * C + c];
+        if (g.noise.q) qv = dr_g(g.noise.q)[((long long)g.step * M * Rg + (long long)m * Rg + grp) * C + c];
         else qv = dr_exp1(g.noise.rng, (uint32_t)(g.noise.stream + g.step), (uint32_t)(g.noise.row0 + m),
                           (uint32_t)(grp * C + c));
       }
@@ -809,10 +908,10 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
         }
       }
       if (act) {
-        g.z_out[(long long)m * g.ldz + grp * C + c] = (c == bi) ? ((1.0f + pu) - pu) : 0.0f;
-        if (g.soft_out) g.soft_out[(long long)m * g.ld_soft + grp * C + c] = p;
-        if (g.idx_out && c == 0) g.idx_out[m * Rg + grp] = bi;
-        if (g.zval_out && c == bi) g.zval_out[m * Rg + grp] = (1.0f + pu) - pu;
+        dr_g(g.z_out)[(long long)m * g.ldz + grp * C + c] = (c == bi) ? ((1.0f + pu) - pu) : 0.0f;
+        if (g.soft_out) dr_g(g.soft_out)[(long long)m * g.ld_soft + grp * C + c] = p;
+        if (g.idx_out && c == 0) dr_g(g.idx_out)[m * Rg + grp] = bi;
+        if (g.zval_out && c == bi) dr_g(g.zval_out)[m * Rg + grp] = (1.0f + pu) - pu;
       }
     }
   } else if (EPI == EPI_ACTOR && g.epi == EPI_ACTOR) {
@@ -830,22 +929,235 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
         av = tanhf(muv);
       } else {
         float e;
-        if (g.noise.eps) e = g.noise.eps[((long long)g.step * M + m) * A + i];
+        if (g.noise.eps) e = dr_g(g.noise.eps)[((long long)g.step * M + m) * A + i];
         else e = dr_normal(g.noise.rng, (uint32_t)(g.noise.stream + g.step), (uint32_t)(g.noise.row0 + m),
                            (uint32_t)i);
-        if (g.eps_save) g.eps_save[(long long)m * A + i] = e;
+        if (g.eps_save) dr_g(g.eps_save)[(long long)m * A + i] = e;
         av = tanhf(muv + e * sg);
       }
-      if (g.act_out) g.act_out[(long long)m * g.ld_act + i] = av;
-      if (g.mu_out) g.mu_out[(long long)m * g.ld_mu + i] = muv;
-      if (g.sig_out) g.sig_out[(long long)m * g.ld_sig + i] = sg;
-      if (g.ls_save) g.ls_save[(long long)m * g.ld_ls + i] = lr;
+      if (g.act_out) dr_g(g.act_out)[(long long)m * g.ld_act + i] = av;
+      if (g.mu_out) dr_g(g.mu_out)[(long long)m * g.ld_mu + i] = muv;
+      if (g.sig_out) dr_g(g.sig_out)[(long long)m * g.ld_sig + i] = sg;
+      if (g.ls_save) dr_g(g.ls_save)[(long long)m * g.ld_ls + i] = lr;
     }
   }
 }
 
 __device__ __forceinline__ void epilogue_store(const GemmArgs& g, int m, int n, float acc) {
-  epilogue_store_b(g, m, n, acc, g.bias ? g.bias[n] : 0.f);
+  epilogue_store_b(g, m, n, acc, g.bias ? dr_g(g.bias)[n] : 0.f);
+}
+
+// ---------------------------------------------------------------------------
+// Tile GEMM for the mid-size problems (M >= 256 rows or TN weight gradients):
+// BM x BN output tile, 4 waves (2 x 2), K in chunks of 32 double-buffered
+// through LDS (rows padded to 36 floats, fragments read as float4 along k).
+// Operand layouts: A [M][K] (MK) or [K][M] (KM), B [N][K] (NK) or [K][N]
+// (KN); MK/NK rows load as float4 (VEC), KM/KN as coalesced scalars
+// transposed into LDS.  Optional deterministic split-K: each split writes a
+// partial tile to splitk_ws and k_splitk_finish sums the splits in order and
+// applies the epilogue.
+// ---------------------------------------------------------------------------
+#define TBK 32  // k-chunk granularity of the split-K ranges (kernel chunks are a multiple)
+
+__device__ __forceinline__ float tile_b_kn(const GemmArgs& g, const float* W, int ldb, int n, int k) {
+  if (k >= g.ksplitB) return dr_g(g.W2)[(long long)(k - g.ksplitB) * g.ldb2 + n];
+  if (n >= g.nsplitB) return dr_g(g.W2)[(long long)k * g.ldb2 + (n - g.nsplitB)];
+  return dr_ld1(W, (unsigned)(k * ldb + n));
+}
+
+template <int BM, int BN, int KC, bool A_KM, bool B_KN, bool VEC>
+__global__ __launch_bounds__(256) void k_gemm_tile(GemmBatch gb, int splits) {
+  constexpr int TLDS = KC + 8;  // = 8 mod 16 dwords: conflict-free ds_read_b128 fragments
+  constexpr int KQ = KC / 4;  // float4 per row piece
+  __shared__ GemmArgs s_args;
+  dr_stage_args(gb.p[blockIdx.z], s_args, threadIdx.x);
+  const GemmArgs& g = s_args;
+  const int M = dr_uni(g.M), N = dr_uni(g.N), K = dr_uni(g.K);
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const int lt = dr_xcd_tile(blockIdx.x, tiles_m * tiles_n);
+  if (lt < 0) return;
+  const int tn = lt / tiles_m, tm = lt - tn * tiles_m;  // m-tiles sharing a weight slice are adjacent
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nch = (K + KC - 1) / KC;
+  const int per = (nch + splits - 1) / splits;
+  const int c0 = blockIdx.y * per, c1 = min(nch, c0 + per);
+  const float* A = dr_uni(g.A);
+  const float* W = dr_uni(g.W);
+  const int lda = dr_uni((int)g.lda), ldb = dr_uni((int)g.ldb);
+  const int ksA = dr_uni(g.ksplitA);
+  const float* A2 = dr_uni(g.A2);
+  const int lda2 = dr_uni((int)g.lda2);
+
+  __shared__ __attribute__((aligned(16))) float As[2][BM][TLDS];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN][TLDS];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+
+  // row-major loader (MK / NK): thread -> (row prow + RS i, float4 quad)
+  constexpr int RS = 256 / KQ;
+  constexpr int APT = BM * KQ / 256, BPT = BN * KQ / 256;
+  // transposed loader (KM / KN): thread -> (k row kk0 + KS i, 4 consecutive m)
+  constexpr int AR4 = BM / 4, AKS = 256 / AR4, BR4 = BN / 4, BKS = 256 / BR4;
+  constexpr int APTT = KC * AR4 / 256, BPTT = KC * BR4 / 256;
+  static_assert(APT >= 1 && BPT >= 1 && AKS >= 1 && BKS >= 1, "tile");
+  static_assert(A_KM ? APTT == APT : true, "loader");
+  static_assert(B_KN ? BPTT == BPT : true, "loader");
+  // register ring: chunk loads are issued PIPE chunks ahead of their use
+  constexpr int PIPE = 3;
+  float4 ra[PIPE][APT], rb[PIPE][BPT];
+  const int quad = tid % KQ, prow = tid / KQ;
+  auto load = [&](int c, int sl) {
+    const int k0 = c * KC;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      if (!A_KM) {
+        const int m = m0 + prow + RS * i, k = k0 + 4 * quad;
+        if (VEC) {
+          const bool ok = m < M && k < K;
+          const bool s1 = k < ksA;
+          const float* base = s1 ? A : A2;
+          const unsigned e = ok ? (unsigned)(s1 ? m * lda + k : m * lda2 + k - ksA) : 0u;
+          ra[sl][i] = dr_ld4(ok ? base : W, e);
+          if (!ok) ra[sl][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          float* v = &ra[sl][i].x;
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) {
+            const int kk = k + cc;
+            v[cc] = (m < M && kk < K) ? ((kk < ksA) ? dr_ld1(A, (unsigned)(m * lda + kk))
+                                                    : dr_ld1(A2, (unsigned)(m * lda2 + kk - ksA)))
+                                      : 0.f;
+          }
+        }
+      } else {
+        const int kk = tid / AR4 + AKS * i, k = k0 + kk, m = m0 + 4 * (tid % AR4);
+        float* v = &ra[sl][i].x;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) v[cc] = (k < K && m + cc < M) ? dr_ld1(A, (unsigned)(k * lda + m + cc)) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      if (!B_KN) {
+        const int n = n0 + prow + RS * i, k = k0 + 4 * quad;
+        if (VEC) {
+          const bool ok = n < N && k < K;
+          rb[sl][i] = dr_ld4(W, ok ? (unsigned)(n * ldb + k) : 0u);
+          if (!ok) rb[sl][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          float* v = &rb[sl][i].x;
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) v[cc] = (n < N && k + cc < K) ? dr_ld1(W, (unsigned)(n * ldb + k + cc)) : 0.f;
+        }
+      } else {
+        const int kk = tid / BR4 + BKS * i, k = k0 + kk, n = n0 + 4 * (tid % BR4);
+        float* v = &rb[sl][i].x;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) v[cc] = (k < K && n + cc < N) ? tile_b_kn(g, W, ldb, n + cc, k) : 0.f;
+      }
+    }
+  };
+  auto store = [&](int sl, int buf) {
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      if (!A_KM) {
+        *reinterpret_cast<float4*>(&As[buf][prow + RS * i][4 * quad]) = ra[sl][i];
+      } else {
+        const int kk = tid / AR4 + AKS * i, ml = 4 * (tid % AR4);
+        if (kk < KC) {
+          As[buf][ml + 0][kk] = ra[sl][i].x;
+          As[buf][ml + 1][kk] = ra[sl][i].y;
+          As[buf][ml + 2][kk] = ra[sl][i].z;
+          As[buf][ml + 3][kk] = ra[sl][i].w;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      if (!B_KN) {
+        *reinterpret_cast<float4*>(&Bs[buf][prow + RS * i][4 * quad]) = rb[sl][i];
+      } else {
+        const int kk = tid / BR4 + BKS * i, nl = 4 * (tid % BR4);
+        if (kk < KC) {
+          Bs[buf][nl + 0][kk] = rb[sl][i].x;
+          Bs[buf][nl + 1][kk] = rb[sl][i].y;
+          Bs[buf][nl + 2][kk] = rb[sl][i].z;
+          Bs[buf][nl + 3][kk] = rb[sl][i].w;
+        }
+      }
+    }
+  };
+
+  constexpr int WTM = BM / 2, WTN = BN / 2, FM = WTM / 16, FN = WTN / 16;
+  const int wm0 = (wave >> 1) * WTM, wn0 = (wave & 1) * WTN;
+  const int r = lane & 15, q = lane >> 4;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < PIPE; ++u)
+    if (c0 + u < c1) load(c0 + u, u);
+  if (c0 < c1) store(0, 0);
+  __syncthreads();
+  for (int cb = c0; cb < c1; cb += PIPE) {
+#pragma unroll
+    for (int u = 0; u < PIPE; ++u) {
+      const int c = cb + u;
+      if (c >= c1) break;
+      const int buf = (c - c0) & 1;
+      if (c + PIPE < c1) load(c + PIPE, u);  // slot u was stored to LDS last iteration
+#pragma unroll
+      for (int s = 0; s < KC; s += 16) {
+        float4 a[FM], b[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const float4*>(&As[buf][wm0 + 16 * i + r][s + 4 * q]);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const float4*>(&Bs[buf][wn0 + 16 * j + r][s + 4 * q]);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+      }
+      if (c + 1 < c1) store((u + 1) % PIPE, buf ^ 1);
+      dr_lds_barrier();  // keeps the PIPE-ahead loads in flight
+    }
+  }
+  float* part = g.splitk_ws;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm0 + 16 * i + 4 * q + e, n = n0 + wn0 + 16 * j + r;
+        if (m >= M || n >= N) continue;
+        if (splits == 1) epilogue_store(g, m, n, acc[i][j][e]);
+        else dr_g(part)[((long long)blockIdx.y * M + m) * N + n] = acc[i][j][e];
+      }
+}
+
+__global__ __launch_bounds__(256) void k_splitk_finish(GemmBatch gb, int splits) {
+  const GemmArgs& g = gb.p[blockIdx.z];
+  const long long MN = (long long)g.M * g.N;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= MN) return;
+  float v = 0.f;
+  for (int sp = 0; sp < splits; ++sp) v += dr_g(g.splitk_ws)[sp * MN + i];
+  const int m = (int)(i / g.N), n = (int)(i - (long long)m * g.N);
+  epilogue_store(g, m, n, v);
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -886,9 +1198,10 @@ static size_t skinny_lds_floats(const GemmBatch& gb, int count, bool vec) {
   size_t need = red;
   if (!vec) return need;
   for (int i = 0; i < count; ++i) {
-    const size_t K = gb.p[i].K;
-    const size_t staged = (size_t)(MT + NT) * (K + 4), rows = (size_t)MT * (K + 4);
-    if (AMODE == AM_LNSILU && !B_KN && K / 4 <= 64 * 4 && staged <= SK_LN_MAXF)
+    const size_t K = gb.p[i].K, KP = K + ((8 - (K & 15)) & 15);
+    const size_t staged = (size_t)(MT + NT) * KP, rows = (size_t)MT * KP;
+    if ((AMODE == AM_LNSILU || AMODE == AM_LNBWD) && !B_KN && K / 4 <= 64 * (MT == 16 ? 4 : 1) &&
+        staged <= SK_LN_MAXF)
       need = std::max(need, staged);  // kernel's `staged`
     else if (AMODE == AM_LNSILU && rows <= SK_LN_MAXF && K / 4 <= 64 * (MT == 16 ? 8 : 2))
       need = std::max(need, rows);  // direct path, LN rows in LDS
@@ -962,8 +1275,80 @@ static void launch_tile(const GemmBatch& gb, int count, hipStream_t s) {
   hipLaunchKernelGGL((k_gemm<BM, BN, AMODE, A_KM, B_KN>), dim3(maxt, 1, count), dim3(256), 0, s, gb);
 }
 
+// mid-size GEMMs: LDS double-buffered tile kernel, split-K when the tile grid
+// is too small to fill the chip and every problem brought scratch for it
+template <int BM, int BN, int KC, bool A_KM, bool B_KN>
+static void launch_tile2(GemmBatch& gb, int count, hipStream_t s) {
+  int maxt = 0, nch = 1 << 30;
+  long long maxMN = 0;
+  bool vec = true, ws = true;
+  for (int i = 0; i < count; ++i) {
+    const GemmArgs& g = gb.p[i];
+    maxt = std::max(maxt, dr_cdiv(g.M, BM) * dr_cdiv(g.N, BN));
+    nch = std::min(nch, dr_cdiv(g.K, KC));
+    maxMN = std::max(maxMN, (long long)g.M * g.N);
+    if (!A_KM) {
+      vec = vec && g.K % 4 == 0 && g.lda % 4 == 0 && aligned16(g.A);
+      if (g.ksplitA < g.K) vec = vec && g.lda2 % 4 == 0 && g.ksplitA % 4 == 0 && aligned16(g.A2);
+    }
+    if (!B_KN) vec = vec && g.ldb % 4 == 0 && aligned16(g.W);
+    ws = ws && g.splitk_ws != nullptr;
+  }
+  if (maxt == 0) return;
+  int splits = 1;
+  if (ws) {
+    splits = std::max(1, std::min(8, dr_cdiv(256, maxt * count)));
+    splits = std::min(splits, std::max(1, nch / 2));  // at least 2 chunks per split
+    for (int i = 0; i < count; ++i)
+      while (splits > 1 && (long long)splits * gb.p[i].M * gb.p[i].N > gb.p[i].splitk_floats) --splits;
+  }
+  dim3 grid(dr_xcd_grid(maxt), splits, count);
+  if (vec) hipLaunchKernelGGL((k_gemm_tile<BM, BN, KC, A_KM, B_KN, true>), grid, dim3(256), 0, s, gb, splits);
+  else hipLaunchKernelGGL((k_gemm_tile<BM, BN, KC, A_KM, B_KN, false>), grid, dim3(256), 0, s, gb, splits);
+  if (splits > 1)
+    hipLaunchKernelGGL(k_splitk_finish, dim3((unsigned)((maxMN + 255) / 256), 1, count), dim3(256), 0, s, gb, splits);
+}
+
+// tile-GEMM shape variant (microbenchmark knob)
+static int g_tile_variant = 0;
+extern "C" void dr_debug_tile_variant(int v) { g_tile_variant = v; }
+
+static bool tile_offsets_ok(const GemmBatch& gb, int count) {
+  const long long lim = 1LL << 30;
+  for (int i = 0; i < count; ++i) {
+    const GemmArgs& g = gb.p[i];
+    const long long arows = std::max((long long)g.M, (long long)g.K), brows = std::max((long long)g.N, (long long)g.K);
+    if (arows * g.lda >= lim || arows * g.lda2 >= lim || brows * g.ldb >= lim) return false;
+    if (g.epi != EPI_NONE || g.out_conv) return false;
+  }
+  return true;
+}
+
 template <int AMODE, bool A_KM, bool B_KN>
 static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
+  if (AMODE == AM_PLAIN && tile_offsets_ok(gb, count)) {
+    int maxM = 0, minK = 1 << 30;
+    for (int i = 0; i < count; ++i) {
+      maxM = std::max(maxM, gb.p[i].M);
+      minK = std::min(minK, gb.p[i].K);
+    }
+    // weight gradients (TN) and tall, deep products go to the tile kernel
+    if (A_KM || (maxM >= 256 && minK >= 512)) {
+      GemmBatch gt = gb;
+      switch (g_tile_variant) {
+        case 1: launch_tile2<64, 64, 64, A_KM, B_KN>(gt, count, s); break;
+        case 2: launch_tile2<128, 64, 32, A_KM, B_KN>(gt, count, s); break;
+        case 3: launch_tile2<128, 64, 64, A_KM, B_KN>(gt, count, s); break;
+        default: launch_tile2<64, 64, 32, A_KM, B_KN>(gt, count, s); break;
+      }
+      return;
+    }
+  }
+  if (AMODE == AM_LNBWD) {
+    if (!A_KM && !B_KN && try_skinny<AM_LNBWD, false>(gb, count, s)) return;
+    dr_set_error("gemm: LayerNorm-backward prologue needs the staged NT skinny path");
+    return;
+  }
   if (!A_KM && (AMODE == AM_PLAIN || AMODE == AM_LNSILU)) {
     if (try_skinny<(AMODE == AM_LNSILU ? AM_LNSILU : AM_PLAIN), B_KN>(gb, count, s)) return;
   }
@@ -1011,6 +1396,19 @@ int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hip
         case AM_LNSILU: launch_pick<AM_LNSILU, false, false>(gb, count, s); break;
         case AM_CONV: launch_pick<AM_CONV, false, false>(gb, count, s); break;
         case AM_CONV_SRC: launch_pick<AM_CONV_SRC, false, false>(gb, count, s); break;
+        case AM_LNBWD: {
+          for (int i = 0; i < count; ++i) {
+            const GemmArgs& g = probs[i];
+            const int lim = (g.M <= 64) ? 1024 : 256;  // staged rows per lane: SV = 4 (MT 16) / 1 (MT 64)
+            if (g.K % 4 || g.K > lim || g.lda % 4 || g.ld_pre % 4 || g.ldb % 4 ||
+                ((uintptr_t)g.A | (uintptr_t)g.pre | (uintptr_t)g.W | (uintptr_t)g.ln_g | (uintptr_t)g.ln_b) & 15) {
+              dr_set_error("gemm_launch: AM_LNBWD needs K %% 4 == 0, K <= %d, 16-byte aligned rows (K=%d)", lim, g.K);
+              return DR_E_INVALID;
+            }
+          }
+          launch_pick<AM_LNBWD, false, false>(gb, count, s);
+          break;
+        }
         default: dr_set_error("gemm_launch: bad amode"); return DR_E_INVALID;
       }
       break;

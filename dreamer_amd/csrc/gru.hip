@@ -172,12 +172,13 @@ __global__ __launch_bounds__(512) void k_gru_fused(GruArgs ga) {
         for (int p = 0; p < GRU_PRE; ++p) {
           if (kc + 16 * p >= ke) break;
 #pragma unroll
-          for (int t = 0; t < 3; ++t) {
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[p].x, wb[p][t].x, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[p].y, wb[p][t].y, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[p].z, wb[p][t].z, acc[t], 0, 0, 0);
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[p].w, wb[p][t].w, acc[t], 0, 0, 0);
-          }
+          for (int t = 0; t < 3; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[p].x, wb[p][t].x, acc[t], 0, 0, 0);
+#pragma unroll
+          for (int t = 0; t < 3; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[p].y, wb[p][t].y, acc[t], 0, 0, 0);
+#pragma unroll
+          for (int t = 0; t < 3; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[p].z, wb[p][t].z, acc[t], 0, 0, 0);
+#pragma unroll
+          for (int t = 0; t < 3; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[p].w, wb[p][t].w, acc[t], 0, 0, 0);
         }
       }
     }
@@ -207,7 +208,9 @@ __global__ __launch_bounds__(512) void k_gru_fused(GruArgs ga) {
       for (int u4 = 0; u4 < GRU_MAXR / 4; ++u4) {
         const bool ok = live && 4 * u4 < R;
         const unsigned e = ok ? (unsigned)(m * R + 4 * u4) : 0u;
-        const int4 i4 = *reinterpret_cast<const int4*>(reinterpret_cast<const char*>(idx) + (e << 2));
+        const dr_f4 i4f = *(const DR_GLOBAL dr_f4*)((const DR_GLOBAL char*)idx + (e << 2));
+        const int4 i4 = make_int4(__float_as_int(i4f.x), __float_as_int(i4f.y), __float_as_int(i4f.z),
+                                  __float_as_int(i4f.w));
         const float4 z4 = dr_ld4(zval, e);
         iv[4 * u4] = i4.x; iv[4 * u4 + 1] = i4.y; iv[4 * u4 + 2] = i4.z; iv[4 * u4 + 3] = i4.w;
         zv[4 * u4] = z4.x; zv[4 * u4 + 1] = z4.y; zv[4 * u4 + 2] = z4.z; zv[4 * u4 + 3] = z4.w;
@@ -283,14 +286,14 @@ __global__ __launch_bounds__(512) void k_gru_fused(GruArgs ga) {
       const float uu = 1.0f / (1.0f + expf(-(gh_s[ml][1][jl] + gi_s[ml][1][jl])));
       const float hn = gh_s[ml][2][jl];
       const float nn = tanhf(gi_s[ml][2][jl] + hn * rr);
-      const float hv = h ? h[(long long)m * g.ldh + j] : 0.0f;
-      g.hout[(long long)m * g.ldo + j] = (hv - nn) * uu + nn;
+      const float hv = h ? dr_g(h)[(long long)m * g.ldh + j] : 0.0f;
+      dr_g(g.hout)[(long long)m * g.ldo + j] = (hv - nn) * uu + nn;
       if (g.sr) {
         const long long o = (long long)m * Hd + j;
-        g.sr[o] = rr;
-        g.su[o] = uu;
-        g.sn[o] = nn;
-        g.sghn[o] = hn;
+        dr_g(g.sr)[o] = rr;
+        dr_g(g.su)[o] = uu;
+        dr_g(g.sn)[o] = nn;
+        dr_g(g.sghn)[o] = hn;
       }
     }
   }

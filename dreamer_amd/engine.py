@@ -154,7 +154,7 @@ class ImaginationEngine:
         L_ = d.rows * d.cols
         scale = 1.0 / float(B * self.wsize * H)
         L.call("dr_critic_fwd", d, ag.critic_struct(), M, L.ptr(self.hiddens), d.hidden, L.ptr(self.latents), L_,
-               None, L.ptr(self.V_c), L.ptr(self.ctape), None, 0, st)
+               None, L.ptr(self.V_c), L.ptr(self.ctape), L.ptr(self.ws_cr), self.ws_cr.numel(), st)
         critic_args = (d, ag.critic_struct(), B, H, L.ptr(self.hiddens), L.ptr(self.latents), L.ptr(self.R),
                        L.ptr(self.ctape), scale, L.ptr(ag.loss_slot(1)), ag.critic_struct(grad=True),
                        L.ptr(self.ws_cr), self.ws_cr.numel())

@@ -2,6 +2,7 @@
 // kernels launched back to back on one stream (HIP events around REPS
 // launches).  Build: python tools/kbench/build.py ; run on the GPU box.
 #include <hip/hip_runtime.h>
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -17,6 +18,7 @@ static const char* g_filter = nullptr;
 static int g_reps = 200;
 extern "C" int dr_debug_tbuf_gru(long long* out, int n);
 extern "C" int dr_debug_tbuf_gemm(long long* out, int n);
+extern "C" void dr_debug_tile_variant(int v);
 
 // one more launch, then the per-phase times of wave 0 of each workgroup
 // (relative to its own start) averaged over the workgroups that wrote them
@@ -168,6 +170,30 @@ __global__ __launch_bounds__(512) void k_loads(const float* __restrict__ buf, fl
   if (acc == 1234.5f) out[0] = acc;
 }
 
+// MFMA issue rate: each wave runs `iters` x 8 independent f32 16x16x4 MFMAs
+// (register operands only); 256 workgroups x 256 threads = one wave per SIMD
+__global__ __launch_bounds__(256) void k_mfma_rate(float* out, int iters) {
+  f32x4 acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float a = threadIdx.x * 1e-3f, b = 1.0f;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i], 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+  if (s == 12345.f) out[threadIdx.x] = s;
+}
+__global__ void k_clock(long long* out, int spin) {
+  const long long t0 = wall_clock64(), c0 = clock64();
+  float a = 1.f;
+  for (int i = 0; i < spin; ++i) a = a * 0.9999f + 0.5f;
+  const long long t1 = wall_clock64(), c1 = clock64();
+  if (threadIdx.x == 0) { out[0] = t1 - t0; out[1] = c1 - c0; out[2] = (long long)a; }
+}
+
 struct Big { long long f[200]; };
 __global__ void k_empty_small(int* p) { if (p && threadIdx.x == 9999) *p = 1; }
 __global__ void k_empty_big(Big b) { if (threadIdx.x == 9999) ((int*)b.f[3])[0] = (int)b.f[150]; }
@@ -245,6 +271,20 @@ int main(int argc, char** argv) {
   }
 
   if (!g_filter || strstr("concurrency", g_filter)) concurrency_probe(dummy);
+  if (!g_filter || strstr("mfma rate", g_filter)) {
+    for (int iters : {1000, 4000}) {
+      char nm[96];
+      snprintf(nm, sizeof nm, "mfma rate: 8 x %d f32 16x16x4 per wave, 256 WG x 4 waves", iters);
+      timeit(nm, [&](hipStream_t st) { hipLaunchKernelGGL(k_mfma_rate, dim3(256), dim3(256), 0, st, dummy, iters); }, s, 20);
+    }
+    long long* ck;
+    CK(hipMalloc(&ck, 64));
+    hipLaunchKernelGGL(k_clock, dim3(1), dim3(64), 0, s, ck, 2000000);
+    long long h[3];
+    CK(hipMemcpy(h, ck, 24, hipMemcpyDeviceToHost));
+    printf("clock probe: %lld shader cycles in %lld x 10 ns -> %.0f MHz (idle chip, 1 wave)\n", h[1], h[0],
+           (double)h[1] / (h[0] * 10e-9) / 1e6);
+  }
   {
     float* buf = frand((size_t)1 << 22);
 #define KB_LOADS(NN)                                                                                        \
@@ -323,6 +363,30 @@ int main(int argc, char** argv) {
     gk.ldb = sh[1];
     snprintf(buf, sizeof buf, "NN plain M%d N%d K%d", sh[0], sh[1], sh[2]);
     timeit(buf, [&](hipStream_t st) { gemm_launch(G_NN, AM_PLAIN, &gk, 1, st); }, s);
+  }
+  // mid-size shapes (tile GEMM, split-K scratch when given)
+  {
+    float* skw = frand((size_t)8 << 20);
+    float* Xm = frand((size_t)2048 * 4096);  // largest A of the cases below
+    float* Wm = frand((size_t)1624 * 1024);  // largest B
+    float* Ym = frand((size_t)2048 * 1624);
+    struct Mid { int M, N, K; bool tn; bool sk; } mids[] = {
+        {1024, 200, 1624, false, false}, {1024, 200, 1624, false, true}, {2048, 200, 4096, false, true},
+        {200, 1624, 960, true, false},   {200, 1624, 960, true, true},   {200, 200, 1024, true, true}};
+    for (int var = 0; var < 4; ++var)
+    for (auto& c : mids) {
+      dr_debug_tile_variant(var);
+      GemmArgs g = gemm_args();
+      g.M = c.M; g.N = c.N; g.K = c.K;
+      if (!c.tn) { g.A = Xm; g.lda = c.K; g.W = Wm; g.ldb = c.K; }
+      else { g.A = Xm; g.lda = c.M; g.W = Wm; g.ldb = c.N; }
+      g.ksplitA = INT_MAX;
+      g.Y = Ym; g.ldy = c.N;
+      if (c.sk) { g.splitk_ws = skw; g.splitk_floats = (long long)8 << 20; }
+      snprintf(buf, sizeof buf, "v%d %s M%d N%d K%d%s", var, c.tn ? "TN" : "NT", c.M, c.N, c.K, c.sk ? " splitK" : "");
+      timeit(buf, [&](hipStream_t st) { gemm_launch(c.tn ? G_TN : G_NT, AM_PLAIN, &g, 1, st); }, s, 50);
+    }
+    dr_debug_tile_variant(0);
   }
   // ln_silu_bwd / colsum
   timeit("ln_silu_bwd M64 K512", [&](hipStream_t st) { op_ln_silu_bwd(64, 512, X, 512, Y, 512, lng, lnb, W, 512, nullptr, nullptr, st); }, s);
