@@ -24,6 +24,9 @@ sys.path.insert(0, REPO)
 METRIC = "imagined latent-steps/sec (B×H) at 64×64 CarRacing, 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 = f32 vector peak
 HBM_PEAK_GBS = 8000.0
+# HBM-side bytes of the encoder group per epoch, measured by tools/pmc_traffic.sh
+# (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, gfx950 correction)
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_traffic.json")
 # SURVEY.md §8d figure of record: necessary dense FLOPs per imagined step at
 # 64x64, S=64, H=15 (warm start 131.07 + dream 8.88 + update 11.17 MFLOP)
 PATH_MFLOP_PER_STEP = {(64, 15): 151.12, (50, 15): 122.36}
@@ -223,6 +226,10 @@ def main():
     achieved = enc_flops / enc_s / 1e12
     if args.phases:
         print(json.dumps({k: round(v / args.steps, 4) for k, v in phase_tot.items()}), file=sys.stderr)
+    traffic, traffic_src = None, None
+    if os.path.exists(TRAFFIC_FILE):
+        t = json.load(open(TRAFFIC_FILE))
+        traffic, traffic_src = t.get("encoder_bytes_per_epoch"), os.path.relpath(TRAFFIC_FILE, REPO)
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "imagined latent-steps/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
@@ -232,7 +239,8 @@ def main():
                    "global_batch": B * world, "seq_len": S, "horizon": H, "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": f"encoder conv stack + feature projection ({len(eng.chunks)} time chunks x 5 launches)",
                      "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                     "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                     "traffic_unit": "bytes per epoch (HBM side)", "traffic_source": traffic_src,
                      "algorithmic_flops_per_launch": enc_flops, "encoder_ms": round(enc_s * 1e3, 4)},
         "losses": {"actor": la, "critic": lc},
     }

@@ -31,8 +31,15 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
 
   const int oh = ih / 2, ow = iw / 2, hw = oh * ow;
   const long long M = (long long)n_frames * hw;
-  const long long m0 = (long long)blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  // XCD-aware 1-D tile order, channel tiles fastest: the channel tiles of one
+  // pixel tile and the neighbouring pixel tiles (which share input halo rows)
+  // run on one XCD and re-read activations from its L2, not from the fabric
+  const int tiles_n = (cout + BN - 1) / BN;
+  const long long tiles = ((M + BM - 1) / BM) * tiles_n;
+  const int lt = dr_xcd_tile(blockIdx.x, (int)tiles);
+  if (lt < 0) return;
+  const long long m0 = (long long)(lt / tiles_n) * BM;
+  const int n0 = (lt % tiles_n) * BN;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int quad = tid & 7, prow = tid >> 3;  // 8 float4 per 32-k row
 
@@ -150,7 +157,12 @@ template <int BM, int BN, int CIN, bool OUT_NCHW>
 static int launch_conv(int n, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
                        float* out, hipStream_t s) {
   const long long M = (long long)n * (ih / 2) * (iw / 2);
-  dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((cout + BN - 1) / BN));
+  const long long tiles = ((M + BM - 1) / BM) * ((cout + BN - 1) / BN);
+  if (tiles >= (1LL << 30)) {
+    dr_set_error("conv: too many tiles");
+    return DR_E_INVALID;
+  }
+  dim3 grid((unsigned)dr_xcd_grid((int)tiles));
   hipLaunchKernelGGL((k_conv_nhwc<BM, BN, CIN, OUT_NCHW>), grid, dim3(256), 0, s, n, ih, iw, cout, in, wr, bias,
                      out);
   return dr_check_launch("conv");
