@@ -358,3 +358,102 @@ def replay_starts(size, capacity, next_idx, seq_len, batch, rng=None):
                 out.append(s)
         starts = np.array(out)
     return starts
+
+
+# ----------------------------------------------------------------------------
+# world-model training step (WorldModel.py:84-202, VariationalAutoEncoder.py:139-161)
+# ----------------------------------------------------------------------------
+def decoder_forward(h, z, P, img_hw):
+    """Decoder.forward (VariationalAutoEncoder.py:139-161): cat(h, flatten z) ->
+    Linear-LN-SiLU-Linear-SiLU -> view (C0, H/16, W/16) -> 4x ConvTranspose2d
+    (k4 s2 p1) with SiLU between and Tanh at the end."""
+    B, S, Hd = h.shape
+    x = torch.cat((h.reshape(B * S, Hd), z.reshape(B * S, -1)), dim=-1)
+    D = WM + "decoder."
+    x = F.silu(_ln(_lin(x, P, D + "upscaler.0"), P, D + "upscaler.1"))
+    x = F.silu(_lin(x, P, D + "upscaler.3"))
+    c0 = P[D + "image_builder.0.weight"].shape[0]
+    x = x.view(-1, c0, img_hw[0] // 16, img_hw[1] // 16)
+    for j, i in enumerate((0, 2, 4, 6)):
+        x = F.conv_transpose2d(x, P[D + f"image_builder.{i}.weight"], P[D + f"image_builder.{i}.bias"],
+                               stride=2, padding=1)
+        x = torch.tanh(x) if j == 3 else F.silu(x)
+    _, C, Hh, Ww = x.shape
+    return x.view(B, S, C, Hh, Ww)
+
+
+def wm_unroll(obs, act, rew, cont, P, q, rows, cols, horizon):
+    """WorldModel.unroll_model (WorldModel.py:84-146); obs normalised.
+    q: (horizon, B*rows, cols) Exp(1) draws of the posterior samples."""
+    B = cont.shape[0]
+    Hd = P[WM + "sequence_model.GRU.weight_hh"].shape[1]
+    A = act.shape[-1]
+    h = torch.zeros(B, 1, Hd, dtype=torch.float32)
+    z = torch.zeros(B, 1, rows, cols, dtype=torch.float32)
+    zs, hs, lgs = [], [], []
+    for t in range(horizon):
+        a = act[:, t - 1:t] if t > 0 else torch.zeros(B, 1, A)
+        z, h, lg = observe_step(z, h, a, obs[:, t:t + 1], P, q[t], rows, cols)
+        zs.append(z); hs.append(h); lgs.append(lg)
+    post_logits, hid, lat = torch.cat(lgs, 1), torch.cat(hs, 1), torch.cat(zs, 1)
+    prior = prior_logits(hid, P, rows, cols)
+    dec_mu = decoder_forward(hid, lat, P, tuple(obs.shape[-2:]))
+    rin = torch.cat([hid[:, 1:], lat[:, 1:].flatten(2)], -1)
+    rew_logits = mlp3(rin, P, WM + "reward_predictor.logit_net")
+    cont_logits = mlp3(rin, P, WM + "continue_predictor.logit_generator")
+    obs_t, rew_t, cont_t = obs[:, :horizon], rew[:, :horizon - 1], cont[:, :horizon - 1]
+    th = twohot(rew_t, P[WM + "reward_predictor.buckets_rew"])
+    obs_ll = -(dec_mu.float() - obs_t.float()).pow(2).sum(dim=[-3, -2, -1])
+    cont_ll = F.binary_cross_entropy_with_logits(cont_logits, cont_t, reduction="none")
+    rew_ll = torch.sum(th * F.log_softmax(rew_logits, dim=-1), dim=-1, keepdim=True)
+    return dict(prior=prior[:, 1:], post=post_logits[:, 1:], obs_ll=obs_ll[:, 1:], rew_ll=rew_ll,
+                cont_ll=cont_ll, hiddens=hid, latents=lat, post_logits=post_logits, dec_mu=dec_mu)
+
+
+def _cat_kl(p_logits, q_logits):
+    """kl_divergence(Categorical(logits=p), Categorical(logits=q)) over the last
+    dim (torch.distributions.kl._kl_categorical_categorical)."""
+    lp = p_logits - p_logits.logsumexp(-1, keepdim=True)
+    lq = q_logits - q_logits.logsumexp(-1, keepdim=True)
+    t = lp.exp() * (lp - lq)
+    return t.sum(-1)
+
+
+def wm_losses(obs_u8, act, rew, cont, P, q, rows, cols, horizon, betas=(1.0, 0.5, 0.1)):
+    """WorldModel.training_step loss construction (WorldModel.py:148-189) with
+    autocast disabled (fp32).  Returns a dict of losses (0-d tensors) and the
+    unroll outputs."""
+    obs = normalise_obs(obs_u8)
+    H = horizon
+    u = wm_unroll(obs[:, :H], act[:, :H], rew[:, :H], cont[:, :H], P, q, rows, cols, H)
+    mask = cont[:, :H - 1]
+    obs_ll = u["obs_ll"] * mask.squeeze(-1)
+    rew_ll = u["rew_ll"] * mask
+    cont_ll = u["cont_ll"] * mask
+    prior, post = u["prior"].float(), u["post"].float()
+    kl_dyn = _cat_kl(post.detach(), prior).sum(dim=-1)
+    kl_rep = _cat_kl(post, prior.detach()).sum(dim=-1)
+    kl_dyn = torch.mean(kl_dyn * mask.squeeze(-1))
+    kl_rep = torch.mean(kl_rep * mask.squeeze(-1))
+    denom = mask.sum() + 1e-5
+    loss_pred = (-obs_ll.sum() - rew_ll.sum() + cont_ll.sum()) / denom
+    one = torch.tensor(1.0)
+    loss_dyn, loss_rep = torch.max(one, kl_dyn), torch.max(one, kl_rep)
+    total = betas[0] * loss_pred + betas[1] * loss_dyn + betas[2] * loss_rep
+    return dict(total=total, loss_pred=loss_pred, kl_dyn=kl_dyn, kl_rep=kl_rep, loss_dyn=loss_dyn,
+                loss_rep=loss_rep, **u)
+
+
+def wm_train_step(obs_u8, act, rew, cont, P, q, rows, cols, horizon, wm_keys, betas=(1.0, 0.5, 0.1)):
+    """Loss + gradients of WorldModel.training_step (WorldModel.py:148-198),
+    pre-optimiser.  ``wm_keys`` are the world-model parameter names in
+    ``WorldModel.parameters()`` order; P must hold leaf tensors for them with
+    requires_grad.  Returns losses, raw and clipped grads (clip 100, as
+    clip_grad_norm_ at WorldModel.py:198) and the total norm."""
+    out = wm_losses(obs_u8, act, rew, cont, P, q, rows, cols, horizon, betas)
+    params = [P[k] for k in wm_keys]
+    g = torch.autograd.grad(out["total"], params, allow_unused=True)
+    g = [torch.zeros_like(p) if gi is None else gi for gi, p in zip(g, params)]
+    gc, norm = clip_grad_norm(g)
+    out.update(grads=[x.detach() for x in g], grads_clipped=[x.detach() for x in gc], norm=norm.detach())
+    return out
