@@ -26,13 +26,26 @@ class dr_dims(C.Structure):
     _fields_ = [(n, C.c_int) for n in (
         "hidden", "rows", "cols", "action", "img_h", "img_w", "enc_f1", "enc_f2", "enc_hidden",
         "prior_h1", "prior_h2", "rew_h1", "rew_h2", "cont_h1", "cont_h2",
-        "actor_h1", "actor_h2", "critic_h1", "critic_h2", "buckets")]
+        "actor_h1", "actor_h2", "critic_h1", "critic_h2", "buckets", "dec_f1", "dec_f2", "dec_hidden")]
 
 
 class dr_world_model(C.Structure):
     _fields_ = [("conv", dr_linear * 4), ("map0", dr_linear), ("map1", dr_linear), ("map3", dr_linear),
                 ("w_ih", fp), ("w_hh", fp), ("b_ih", fp), ("b_hh", fp),
                 ("prior", dr_mlp3), ("reward", dr_mlp3), ("cont", dr_mlp3), ("buckets_rew", fp)]
+
+
+class dr_decoder(C.Structure):
+    _fields_ = [("up0", dr_linear), ("up1", dr_linear), ("up3", dr_linear), ("convt", dr_linear * 4)]
+
+
+class dr_wm_batch(C.Structure):
+    _fields_ = [("actions", fp), ("act_sb", C.c_longlong), ("act_st", C.c_longlong), ("rewards", fp),
+                ("continues", fp), ("rc_sb", C.c_longlong), ("rc_st", C.c_longlong)]
+
+
+class dr_wm_loss_cfg(C.Structure):
+    _fields_ = [("beta_pred", C.c_float), ("beta_dyn", C.c_float), ("beta_rep", C.c_float)]
 
 
 class dr_actor(C.Structure):
@@ -95,6 +108,10 @@ _SIGS = {
     "dr_nonfinite": (_i, [_ll, fp, fp, fp]),
     "dr_replay_gather": (_i, [_ll, _i, _i, _i, _i, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp]),
     "dr_rng_advance": (_i, [fp, C.c_ulonglong, fp]),
+    "dr_wm_train_workspace_bytes": (_sz, [_P(dr_dims), _i, _i]),
+    "dr_wm_train_grads": (_i, [_P(dr_dims), _P(dr_world_model), _P(dr_decoder), _i, _i, _P(dr_frames),
+                               _P(dr_wm_batch), dr_noise, dr_wm_loss_cfg, fp, fp, _P(dr_world_model),
+                               _P(dr_decoder), fp, fp, fp, fp, _sz, fp]),
 }
 
 EXPORTED = sorted(_SIGS)

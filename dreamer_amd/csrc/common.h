@@ -37,6 +37,11 @@ int dr_check_launch(const char* what);
 __device__ __forceinline__ float dr_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float dr_sigmoid_precise(float x) { return 1.0f / (1.0f + expf(-x)); }
 __device__ __forceinline__ float dr_silu(float x) { return x / (1.0f + expf(-x)); }
+// d SiLU(x) / dx as torch's silu_backward: s * (1 + x * (1 - s))
+__device__ __forceinline__ float dr_dsilu(float x) {
+  const float s = 1.0f / (1.0f + expf(-x));
+  return s * (1.0f + x * (1.0f - s));
+}
 __device__ __forceinline__ float dr_softplus(float x) {  // torch softplus(beta=1, threshold=20)
   return x > 20.0f ? x : log1pf(expf(x));
 }

@@ -1,4 +1,6 @@
-// NHWC implicit-GEMM encoder convolutions (conv.hip).
+// NHWC implicit-GEMM convolutions: the encoder's Conv2d stack (conv.hip) and
+// the world-model training step's transposed convolutions, conv data
+// gradients and weight gradients (wmconv.hip).
 #pragma once
 #include "common.h"
 
@@ -7,5 +9,52 @@
 // out_nchw, [n][cout][ih/2][iw/2] (the encoder's flatten order).
 int op_conv_nhwc(int n, int cin, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
                  float* out, int out_nchw, hipStream_t s);
+enum { CONV_EPI_FWD = 0, CONV_EPI_DSILU = 1 };
+// as op_conv_nhwc, plus: pre (optional with CONV_EPI_FWD) receives acc + bias
+// in NHWC; CONV_EPI_DSILU writes acc * SiLU'(pre) (no bias, NHWC out).
+int op_conv_nhwc_ex(int n, int cin, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
+                    float* out, int out_nchw, float* pre, int epi, hipStream_t s);
 int op_frames_nhwc4(int n, int nb, int h, int w, const dr_frames* src, float* out, hipStream_t s);
 int op_conv_repack_pad(int cout, int cin, int cin_pad, const float* w, float* wr, hipStream_t s);
+
+// ---- wmconv.hip -------------------------------------------------------------
+// Upsampling k4 s2 p1 (ConvTranspose2d, or the data gradient of a Conv2d):
+//   out[f][Y][X][co] = sum_{ci, (y,ky): Y = 2y-1+ky, (x,kx): X = 2x-1+kx} in[f][y][x][ci] * wt[ci][co][ky][kx]
+// in NHWC [n][h][w][cin]; wt in ConvTranspose2d layout [cin][cout][4][4] (a
+// Conv2d weight [co][ci][4][4] read as [cin=co][cout=ci] gives the Conv2d
+// input gradient).  wq = op_convT_repack(wt) scratch [4 parity classes][cout][4 taps][cin].
+enum { CT_EPI_BIAS = 0, CT_EPI_DSILU = 1, CT_EPI_TANH_MSE = 2 };
+struct ConvTArgs {
+  int n, cin, h, w, cout;
+  const float* in;
+  int silu_in;          // apply SiLU to `in` on load (in holds pre-activations)
+  const float* wq;
+  const float* bias;    // CT_EPI_BIAS / CT_EPI_TANH_MSE
+  float* out;           // NHWC [n][2h][2w][ldc]
+  int ldc;              // channel stride of out (>= cout; extra channels written as 0)
+  const float* pre;     // CT_EPI_DSILU: out = acc * SiLU'(pre) (pre NHWC, stride cout)
+  // CT_EPI_TANH_MSE: mu = tanh(acc + bias); err = mu - target; out = coef[f] * err * (1 - mu^2)
+  // (the gradient wrt the pre-tanh value); part[f * nparts + j] = sum err^2 over tile j of frame f
+  const float* target;  // NHWC [n][2h][2w][tstride]
+  int tstride;
+  const float* coef;    // [n]
+  float* part;          // [n][parts_per_frame()]
+};
+int op_convT_repack(int cin, int cout, const float* wt, float* wq, hipStream_t s);
+int op_convT_nhwc(int epi, const ConvTArgs& a, hipStream_t s);
+int op_convT_mse_parts(int h, int w);  // partial sums per frame written by CT_EPI_TANH_MSE
+
+// Weight gradient of a k4 s2 p1 (transposed) convolution:
+//   dW[a][b][ky][kx] (+)= scale * sum_{f,y,x} lo[f][y][x][a] * hi[f][2y-1+ky][2x-1+kx][b]
+// lo NHWC [n][h][w][ca] (stride lda), hi NHWC [n][2h][2w][cb] (stride ldb).
+// Conv2d: lo = output gradient, hi = input -> dW [cout][cin][4][4];
+// ConvTranspose2d: lo = input, hi = output gradient -> dW [cin][cout][4][4].
+// lo_silu: lo holds pre-activations, SiLU is applied on load.
+size_t op_conv_wgrad_ws_floats(int n, int h, int w, int ca, int cb);
+// dW has cbo <= cb channels per row (cbo < cb when hi carries zero padding channels).
+int op_conv_wgrad(int n, int h, int w, int ca, int cb, const float* lo, int lda, int lo_silu, const float* hi, int ldb,
+                  float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s);
+// out[c] (+)= sum_r X[r][c] for c < C (row stride ldx); two deterministic passes
+size_t op_chan_sum_ws_floats(long long rows, int C);
+int op_chan_sum(long long rows, int C, const float* X, int ldx, float* out, int accumulate, float* ws, size_t ws_floats,
+                hipStream_t s);

@@ -16,10 +16,14 @@
 #define CBK 32
 #define CLDS (CBK + 8)  // 160-byte rows (= 8 mod 16 dwords): conflict-free ds_read_b128 fragments
 
-template <int BM, int BN, int CIN, bool OUT_NCHW>
+// CONV_EPI_FWD: out = SiLU(acc + bias), optionally pre[m][co] = acc + bias
+// (NHWC, kept for the backward).  CONV_EPI_DSILU (world-model backward, a
+// transposed conv's input gradient): out[m][co] = acc * SiLU'(pre[m][co]).
+template <int BM, int BN, int CIN, bool OUT_NCHW, int EPI>
 __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw, int cout,
                                                    const float* __restrict__ in, const float* __restrict__ wr,
-                                                   const float* __restrict__ bias, float* __restrict__ out) {
+                                                   const float* __restrict__ bias, float* __restrict__ out,
+                                                   float* __restrict__ pre) {
   constexpr int K = CIN * 16;
   constexpr int APT = BM / 32;  // pixel rows loaded per thread (8 float4 per 32-k row)
   constexpr int BPT = BN >= 32 ? BN / 32 : 1;
@@ -142,8 +146,14 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
         const long long m = m0 + wm0 + 16 * i + 4 * q + e;
         const int co = n0 + wn0 + 16 * j + r;
         if (m >= M || co >= cout) continue;
-        float v = acc[i][j][e] + bias[co];
-        v = v / (1.0f + expf(-v));
+        float v;
+        if (EPI == CONV_EPI_DSILU) {
+          v = acc[i][j][e] * dr_dsilu(pre[m * cout + co]);
+        } else {
+          v = acc[i][j][e] + bias[co];
+          if (pre) pre[m * cout + co] = v;
+          v = v / (1.0f + expf(-v));
+        }
         if (OUT_NCHW) {
           const long long f = m / hw;
           out[(f * cout + co) * hw + (m - f * hw)] = v;
@@ -153,9 +163,9 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
       }
 }
 
-template <int BM, int BN, int CIN, bool OUT_NCHW>
+template <int BM, int BN, int CIN, bool OUT_NCHW, int EPI>
 static int launch_conv(int n, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
-                       float* out, hipStream_t s) {
+                       float* out, float* pre, hipStream_t s) {
   const long long M = (long long)n * (ih / 2) * (iw / 2);
   const long long tiles = ((M + BM - 1) / BM) * ((cout + BN - 1) / BN);
   if (tiles >= (1LL << 30)) {
@@ -163,22 +173,30 @@ static int launch_conv(int n, int ih, int iw, int cout, const float* in, const f
     return DR_E_INVALID;
   }
   dim3 grid((unsigned)dr_xcd_grid((int)tiles));
-  hipLaunchKernelGGL((k_conv_nhwc<BM, BN, CIN, OUT_NCHW>), grid, dim3(256), 0, s, n, ih, iw, cout, in, wr, bias,
-                     out);
+  hipLaunchKernelGGL((k_conv_nhwc<BM, BN, CIN, OUT_NCHW, EPI>), grid, dim3(256), 0, s, n, ih, iw, cout, in, wr,
+                     bias, out, pre);
   return dr_check_launch("conv");
 }
 
-int op_conv_nhwc(int n, int cin, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
-                 float* out, int out_nchw, hipStream_t s) {
-#define DR_CONV_CASE(C)                                                                               \
-  if (cin == C) {                                                                                     \
-    if (cout <= 16) {                                                                                 \
-      if (out_nchw) return launch_conv<128, 16, C, true>(n, ih, iw, cout, in, wr, bias, out, s);      \
-      return launch_conv<128, 16, C, false>(n, ih, iw, cout, in, wr, bias, out, s);                   \
-    }                                                                                                 \
-    if (out_nchw) return launch_conv<128, 64, C, true>(n, ih, iw, cout, in, wr, bias, out, s);        \
-    if (cout % 64 == 0) return launch_conv<128, 64, C, false>(n, ih, iw, cout, in, wr, bias, out, s); \
-    return launch_conv<128, 32, C, false>(n, ih, iw, cout, in, wr, bias, out, s);                     \
+int op_conv_nhwc_ex(int n, int cin, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
+                    float* out, int out_nchw, float* pre, int epi, hipStream_t s) {
+  if (epi == CONV_EPI_DSILU && (out_nchw || !pre)) {
+    dr_set_error("conv: the SiLU-backward epilogue needs NHWC output and a pre-activation tensor");
+    return DR_E_INVALID;
+  }
+#define DR_CONV_L(BM, BN, C, NCHW)                                                                \
+  (epi == CONV_EPI_DSILU                                                                          \
+       ? launch_conv<BM, BN, C, NCHW, CONV_EPI_DSILU>(n, ih, iw, cout, in, wr, bias, out, pre, s) \
+       : launch_conv<BM, BN, C, NCHW, CONV_EPI_FWD>(n, ih, iw, cout, in, wr, bias, out, pre, s))
+#define DR_CONV_CASE(C)                                                                                     \
+  if (cin == C) {                                                                                           \
+    if (cout <= 16) {                                                                                       \
+      if (out_nchw) return launch_conv<128, 16, C, true, CONV_EPI_FWD>(n, ih, iw, cout, in, wr, bias, out, pre, s); \
+      return DR_CONV_L(128, 16, C, false);                                                                  \
+    }                                                                                                       \
+    if (out_nchw) return launch_conv<128, 64, C, true, CONV_EPI_FWD>(n, ih, iw, cout, in, wr, bias, out, pre, s); \
+    if (cout % 64 == 0) return DR_CONV_L(128, 64, C, false);                                                \
+    return DR_CONV_L(128, 32, C, false);                                                                    \
   }
   DR_CONV_CASE(4)
   DR_CONV_CASE(8)
@@ -188,8 +206,14 @@ int op_conv_nhwc(int n, int cin, int ih, int iw, int cout, const float* in, cons
   DR_CONV_CASE(128)
   DR_CONV_CASE(256)
 #undef DR_CONV_CASE
+#undef DR_CONV_L
   dr_set_error("conv: unsupported input channels %d", cin);
   return DR_E_INVALID;
+}
+
+int op_conv_nhwc(int n, int cin, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
+                 float* out, int out_nchw, hipStream_t s) {
+  return op_conv_nhwc_ex(n, cin, ih, iw, cout, in, wr, bias, out, out_nchw, nullptr, CONV_EPI_FWD, s);
 }
 
 // frames (u8 replay ring or f32 tensor, NCHW 3 channels) -> normalised f32

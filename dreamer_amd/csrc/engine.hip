@@ -2,201 +2,7 @@
 // start), imagination unroll forward/backward, critic forward/backward.
 // Each is a fixed sequence of kernel launches on one stream (no host sync,
 // no allocation) so a whole train_Agent epoch can be captured in a hipGraph.
-#include <string.h>
-
-#include "conv.h"
-#include "gemm.h"
-#include <limits.h>
-#include "gru.h"
-#include "ops.h"
-
-int op_critic_ce(int B, int H, int nb, const float* logits, const float* R, const float* buckets, float scale,
-                 float* row_loss, float* g_logits, hipStream_t s);
-
-// ---------------------------------------------------------------------------
-// workspace carving (the same sequence runs in "dry" mode for size queries)
-// ---------------------------------------------------------------------------
-struct Carve {
-  char* base;
-  size_t off;
-  explicit Carve(void* b) : base((char*)b), off(0) {}
-  float* f(long long n) { return (float*)raw(n * sizeof(float)); }
-  int* i(long long n) { return (int*)raw(n * sizeof(int)); }
-  void* raw(size_t bytes) {
-    const size_t o = (off + 255) & ~(size_t)255;
-    off = o + bytes;
-    return base ? (void*)(base + o) : nullptr;
-  }
-};
-
-#define WS_CHECK(c, bytes)                                                                 \
-  do {                                                                                     \
-    if ((c).off > (bytes)) {                                                               \
-      dr_set_error("%s: workspace too small (%zu < %zu)", __func__, (size_t)(bytes), (c).off); \
-      return DR_E_WORKSPACE;                                                               \
-    }                                                                                      \
-  } while (0)
-
-static int copy2d(float* dst, long long dpitch, const float* src, long long spitch, long long width, long long rows,
-                  hipStream_t s) {
-  if (rows == 0 || width == 0) return DR_OK;
-  hipError_t e = hipMemcpy2DAsync(dst, dpitch * sizeof(float), src, spitch * sizeof(float), width * sizeof(float),
-                                  rows, hipMemcpyDeviceToDevice, s);
-  if (e != hipSuccess) {
-    dr_set_error("copy2d: %s", hipGetErrorString(e));
-    return DR_E_HIP;
-  }
-  return DR_OK;
-}
-
-static int zero(float* p, long long n, hipStream_t s) {
-  if (n == 0) return DR_OK;
-  hipError_t e = hipMemsetAsync(p, 0, n * sizeof(float), s);
-  if (e != hipSuccess) {
-    dr_set_error("memset: %s", hipGetErrorString(e));
-    return DR_E_HIP;
-  }
-  return DR_OK;
-}
-
-static int latent(const dr_dims* d) { return d->rows * d->cols; }
-
-// Y[M][N] = A[M][K] W^T + b  (torch Linear), A row stride lda
-static GemmArgs lin(int M, int N, int K, const float* A, long long lda, const float* W, long long ldw,
-                    const float* bias, float* Y, long long ldy) {
-  GemmArgs g = gemm_args();
-  g.M = M; g.N = N; g.K = K;
-  g.A = A; g.lda = lda;
-  g.W = W; g.ldb = ldw;
-  g.bias = bias;
-  g.Y = Y; g.ldy = ldy;
-  return g;
-}
-// Linear over the concatenation [A (Ka cols) | A2 (K2 cols)]
-static GemmArgs lin2(int M, int N, const float* A, long long lda, int Ka, const float* A2, long long lda2, int K2,
-                     const float* W, const float* bias, float* Y, long long ldy) {
-  GemmArgs g = lin(M, N, Ka + K2, A, lda, W, Ka + K2, bias, Y, ldy);
-  g.A2 = A2; g.lda2 = lda2; g.ksplitA = Ka;
-  return g;
-}
-// Linear applied to SiLU(LayerNorm(pre)) (the LN+SiLU of the previous layer fused on load)
-static GemmArgs lin_ln(int M, int N, int K, const float* pre, long long ldp, const dr_linear& ln, const float* W,
-                       const float* bias, float* Y, long long ldy) {
-  GemmArgs g = lin(M, N, K, pre, ldp, W, K, bias, Y, ldy);
-  g.ln_g = ln.w; g.ln_b = ln.b;
-  return g;
-}
-// input gradient: Y[M][N] (+)= G[M][K] W[K][N]  (W = torch weight [out=K][in=N])
-static GemmArgs bwd_in(int M, int N, int K, const float* G, long long ldg, const float* W, long long ldw, float* Y,
-                       long long ldy, int accumulate) {
-  GemmArgs g = gemm_args();
-  g.M = M; g.N = N; g.K = K;
-  g.A = G; g.lda = ldg;
-  g.W = W; g.ldb = ldw;
-  g.Y = Y; g.ldy = ldy;
-  g.accumulate = accumulate;
-  return g;
-}
-// input gradient against a transposed weight WT [N=in][K=out] (NT, float4 loads)
-static GemmArgs bwd_nt(int M, int N, int K, const float* G, long long ldg, const float* WT, float* Y, long long ldy,
-                       int accumulate) {
-  GemmArgs g = gemm_args();
-  g.M = M; g.N = N; g.K = K;
-  g.A = G; g.lda = ldg;
-  g.W = WT; g.ldb = K;
-  g.Y = Y; g.ldy = ldy;
-  g.accumulate = accumulate;
-  return g;
-}
-static int run(GemmLayout lay, int amode, const GemmArgs& a, hipStream_t s) { return gemm_launch(lay, amode, &a, 1, s); }
-
-// split-K scratch for the tile GEMM: hand problem g up to 4 partial planes
-// from a carved region (grouped problems take disjoint slices)
-#define DR_SPLITK_MAX 4
-static void give_splitk(GemmArgs& g, float*& cur, long long& left) {
-  const long long need = (long long)DR_SPLITK_MAX * g.M * g.N;
-  if (!cur || left < need) return;
-  g.splitk_ws = cur;
-  g.splitk_floats = need;
-  cur += need;
-  left -= need;
-}
-static long long splitk_floats(long long M, long long N) { return DR_SPLITK_MAX * M * N; }
-
-// input gradient through SiLU(LayerNorm(pre)) and a transposed weight, fused:
-// the GEMM's staged prologue computes g_pre from (gx, pre) (gemm.h AM_LNBWD);
-// g_pre and the LN-parameter saves are written when requested.  Falls back to
-// k_ln_silu_bwd + NT GEMM where the fused path does not apply.
-static int lnbwd_nt(int M, int N, int K, const float* gx, long long ldgx, const float* pre, long long ld_pre,
-                    const dr_linear& ln, const float* WT, float* Y, long long ldy, int accumulate, float* gpre,
-                    long long ld_gpre, float* gy, float* xh, float* Y2, long long ldy2, int nsplitY, hipStream_t s) {
-  GemmArgs g = bwd_nt(M, N, K, gx, ldgx, WT, Y, ldy, accumulate);
-  g.Y2 = Y2; g.ldy2 = ldy2; g.nsplitY = nsplitY;
-  const bool ok = K % 4 == 0 && K <= (M <= 64 ? 1024 : 256) && M <= 4096 && ldgx % 4 == 0 && ld_pre % 4 == 0 &&
-                  ((((uintptr_t)gx | (uintptr_t)pre | (uintptr_t)WT | (uintptr_t)ln.w | (uintptr_t)ln.b) & 15) == 0);
-  if (ok) {
-    g.pre = pre; g.ld_pre = ld_pre; g.ln_g = ln.w; g.ln_b = ln.b;
-    g.a_out = gpre; g.ld_aout = ld_gpre;
-    g.sv_gy = gy; g.sv_xh = xh; g.ld_sv = ld_gpre;
-    return run(G_NT, AM_LNBWD, g, s);
-  }
-  DR_REQUIRE(gpre != nullptr, "LN-backward fallback needs a g_pre buffer");
-  DR_TRY(op_ln_silu_bwd(M, K, gx, ldgx, pre, ld_pre, ln.w, ln.b, gpre, ld_gpre, gy, xh, s));
-  g.A = gpre; g.lda = ld_gpre;
-  return run(G_NT, AM_PLAIN, g, s);
-}
-
-// weight gradient: dW[M=out][N=in] = sum_r G[r][m] X[r][n]  (rows r < R)
-static GemmArgs bwd_w(int out, int in, int R, const float* G, long long ldg, const float* X, long long ldx, float* dW) {
-  GemmArgs g = gemm_args();
-  g.M = out; g.N = in; g.K = R;
-  g.A = G; g.lda = ldg;
-  g.W = X; g.ldb = ldx;
-  g.Y = dW; g.ldy = in;
-  return g;
-}
-
-
-// one-hot index buffers hold [B][R] class indices followed by the [B][R]
-// straight-through values at those indices (what the fused GRU gathers)
-static float* onehot_vals(int* idx, long long B, int R) { return reinterpret_cast<float*>(idx + B * R); }
-
-// fused categorical-sampler epilogue on a logits GEMM (VAE.py:88-98,
-// DynamicsPredictors.py:33-39): z (STE value), idx, softmax for the backward
-static void with_sampler(GemmArgs& g, const dr_dims* d, const dr_noise& nz, int step, float* z, long long ldz,
-                         int* idx, float* soft, long long ld_soft) {
-  g.epi = EPI_SAMPLE;
-  g.noise = nz;
-  g.step = step;
-  g.R = d->rows;
-  g.C = d->cols;
-  g.unimix = (float)(0.01 * (1.0 / d->cols));
-  g.z_out = z; g.ldz = ldz; g.idx_out = idx; g.soft_out = soft; g.ld_soft = ld_soft;
-  g.zval_out = idx ? onehot_vals(idx, g.M, d->rows) : nullptr;
-}
-
-// fused actor-head epilogue on the stacked [mu_head; log_sig_head] GEMM
-static void with_actor_head(GemmArgs& g, int A, const dr_noise& nz, int step, int det, float* act, long long ld_act,
-                            float* mu, long long ld_mu, float* sig, long long ld_sig, float* eps_save, float* ls_save,
-                            long long ld_ls) {
-  g.epi = EPI_ACTOR;
-  g.noise = nz;
-  g.step = step;
-  g.na = A;
-  g.det = det;
-  g.act_out = act; g.ld_act = ld_act; g.mu_out = mu; g.ld_mu = ld_mu; g.sig_out = sig; g.ld_sig = ld_sig;
-  g.eps_save = eps_save; g.ls_save = ls_save; g.ld_ls = ld_ls;
-  g.Y = nullptr;
-}
-
-// [mu_head; log_sig_head] stacked into one [2A][in] weight (+ bias) so one
-// workgroup sees both halves of a row
-static int stack_heads(const dr_actor* ac, int A, int in, float* w, float* b, hipStream_t s) {
-  DR_TRY(copy2d(w, in, ac->mu.w, in, in, A, s));
-  DR_TRY(copy2d(w + (long long)A * in, in, ac->ls.w, in, in, A, s));
-  DR_TRY(copy2d(b, A, ac->mu.b, A, A, 1, s));
-  return copy2d(b + A, A, ac->ls.b, A, A, 1, s);
-}
+#include "engine_util.h"
 
 // ===========================================================================
 // a3  encoder features
@@ -278,34 +84,11 @@ static void obs_carve(Carve& c, const dr_dims* d, int B, ObsWs& w) {
   w.idx = c.i(2LL * B * d->rows);
 }
 
-// GRU step on a sampled one-hot latent (idx) via the fused kernel
-static int gru_onehot(const dr_dims* d, const dr_world_model* wm, int B, int* idx, const float* a, long long lda, const float* h, long long ldh, float* hout,
-                      long long ldo, const float* wt, float* sr, float* su, float* sn, float* sghn, hipStream_t s) {
-  GruArgs g;
-  g.B = B; g.Hd = d->hidden; g.R = d->rows; g.C = d->cols; g.A = d->action;
-  g.idx = idx; g.zval = onehot_vals(idx, B, d->rows); g.a = a; g.lda = lda; g.h = h; g.ldh = ldh;
-  g.wt = wt; g.b_ih = wm->b_ih; g.w_hh = wm->w_hh; g.b_hh = wm->b_hh;
-  g.hout = hout; g.ldo = ldo; g.sr = sr; g.su = su; g.sn = sn; g.sghn = sghn;
-  return op_gru_fused(g, s);
-}
-
 extern "C" size_t dr_observe_workspace_bytes(const dr_dims* d, int B) {
   Carve c(nullptr);
   ObsWs w;
   obs_carve(c, d, B, w);
   return c.off;
-}
-
-// h' = GRU(z, a, h) with gi/gh from one grouped GEMM launch
-static int gru_step(const dr_dims* d, const dr_world_model* wm, int B, const float* z, long long ldz,
-                    const float* a, long long lda, const float* h, long long ldh, float* hout, long long ldo,
-                    float* gi, float* gh, float* sr, float* su, float* sn, float* sghn, hipStream_t s) {
-  const int L = latent(d), Hd = d->hidden, A = d->action;
-  GemmArgs p[2];
-  p[0] = lin2(B, 3 * Hd, z, ldz, L, a, lda, A, wm->w_ih, wm->b_ih, gi, 3 * Hd);
-  p[1] = lin(B, 3 * Hd, h ? Hd : 0, h, ldh, wm->w_hh, Hd, wm->b_hh, gh, 3 * Hd);
-  DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, 2, s));
-  return op_gru_fwd(B, Hd, gi, gh, h, ldh, hout, ldo, sr, su, sn, sghn, s);
 }
 
 extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B, int T, const float* feat,

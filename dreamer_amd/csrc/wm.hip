@@ -1,0 +1,695 @@
+// a19/a20: the world-model training step (WorldModel.training_step,
+// WorldModel.py:148-198; unroll_model 84-146; Decoder.forward
+// VariationalAutoEncoder.py:139-161) as one fixed launch sequence.
+//
+// Rows are time-major (m = t*B + b).  The posterior scan runs per step (B
+// rows); every head that does not feed the recurrence (prior, decoder, reward,
+// continue) runs once over the M1 = (T-1)*B rows t >= 1 -- the only rows the
+// losses read (WorldModel.py:141-145), so row t = 0 of the decoder / prior is
+// never computed.  The backward mirrors it: batched head backward into dL/dh,
+// dL/dz, then the reverse scan (straight-through sampler, latent_mapper, GRU),
+// then the encoder convolutions over all M frames.
+#include "engine_util.h"
+
+// ---------------------------------------------------------------------------
+// small kernels of the loss
+// ---------------------------------------------------------------------------
+// window actions / rewards / continues -> time-major [T][B](*A)
+__global__ void k_wm_gather(int B, int T, int A, dr_wm_batch bt, float* act_tm, float* rew_tm, float* cont_tm) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * T) return;
+  const int t = i / B, b = i - t * B;
+  for (int a = 0; a < A; ++a) act_tm[(long long)i * A + a] = bt.actions[b * bt.act_sb + t * bt.act_st + a];
+  rew_tm[i] = bt.rewards[b * bt.rc_sb + t * bt.rc_st];
+  cont_tm[i] = bt.continues[b * bt.rc_sb + t * bt.rc_st];
+}
+
+// block-wide sum in a fixed order (deterministic)
+__device__ float block_sum256(float v, float* red) {
+  const int tid = threadIdx.x;
+  red[tid] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  const float r = red[0];
+  __syncthreads();
+  return r;
+}
+
+// mask = continues[:, :T-1] (WorldModel.py:170); row i < M1 of every head /
+// decoder frame is (t = i/B + 1, b) and its mask is cont_tm[i].
+// scal[0] = mask.sum() + 1e-5 (185); coef_row = beta_pred * mask / denom (the
+// factor of every prediction-loss gradient); coef_obs = 2 * coef_row.
+__global__ __launch_bounds__(256) void k_wm_prep(int M1, const float* cont_tm, float beta_pred, float* scal,
+                                                 float* coef_row, float* coef_obs) {
+  __shared__ float red[256];
+  float s = 0.0f;
+  for (int i = threadIdx.x; i < M1; i += 256) s += cont_tm[i];
+  const float denom = block_sum256(s, red) + 1e-5f;
+  if (threadIdx.x == 0) scal[0] = denom;
+  for (int i = threadIdx.x; i < M1; i += 256) {
+    const float c = beta_pred * cont_tm[i] / denom;
+    coef_row[i] = c;
+    coef_obs[i] = 2.0f * c;
+  }
+}
+
+// KL(post || prior) per (row, latent group) (WorldModel.py:175-183;
+// torch.distributions.kl._kl_categorical_categorical on normalised logits).
+// MODE 0: kl_grp[row][g].  MODE 1: gradients -- dyn: d/d prior = cd*(q - p);
+// rep: d/d post = cr * p * (lp - lq - KL_g), cd/cr = scal[1]/scal[2] * mask.
+template <int MODE>
+__global__ void k_wm_kl(int M1, int R, int C, int W, const float* __restrict__ prior, const float* __restrict__ post,
+                        const float* __restrict__ cont_tm, const float* __restrict__ scal, float* kl_grp,
+                        float* g_prior, float* g_post) {
+  const int gtid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int grp = gtid / W, c = gtid - grp * W;
+  const bool valid = grp < M1 * R;
+  const int row = valid ? grp / R : 0, g = valid ? grp - row * R : 0;
+  const bool act = valid && c < C;
+  const long long o = (long long)row * R * C + (long long)g * C + c;
+  const float xp = act ? post[o] : -INFINITY;
+  const float xq = act ? prior[o] : -INFINITY;
+  const float mp = group_max(xp, W), mq = group_max(xq, W);
+  const float ep = act ? expf(xp - mp) : 0.0f, eq = act ? expf(xq - mq) : 0.0f;
+  const float sp = group_sum(ep, W), sq = group_sum(eq, W);
+  const float lp = xp - (mp + logf(sp)), lq = xq - (mq + logf(sq));
+  const float p = ep / sp;
+  const float term = act ? p * (lp - lq) : 0.0f;
+  const float klg = group_sum(term, W);
+  if (MODE == 0) {
+    if (act && c == 0) kl_grp[(long long)row * R + g] = klg;
+  } else if (act) {
+    const float m = cont_tm[row];
+    const float cd = scal[1] * m, cr = scal[2] * m;
+    g_prior[o] = cd * (eq / sq - p);
+    g_post[o] = cr * (p * (lp - lq - klg));
+  }
+}
+
+// reward two-hot log-likelihood and continue BCE per row (WorldModel.py:125-138)
+// and their gradients scaled by coef_row; one wave per row
+__global__ __launch_bounds__(256) void k_wm_heads(int M1, int nb, const float* __restrict__ rlog,
+                                                  const float* __restrict__ clog, const float* __restrict__ rew_tm,
+                                                  const float* __restrict__ cont_tm,
+                                                  const float* __restrict__ buckets,
+                                                  const float* __restrict__ coef_row, float* rew_row, float* cont_row,
+                                                  float* g_rew, float* g_cont) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M1) return;
+  const float* x = rlog + (long long)row * nb;
+  float mx = -INFINITY;
+  for (int j = lane; j < nb; j += 64) mx = fmaxf(mx, x[j]);
+  mx = wave_max(mx);
+  float se = 0.0f;
+  for (int j = lane; j < nb; j += 64) se += expf(x[j] - mx);
+  se = wave_sum(se);
+  const float lse = mx + logf(se);
+  // to_twohot (DreamerUtils.py:39-50): clamp, searchsorted(right=True) - 1, clamp <= nb-2
+  const float rv = rew_tm[row];  // torch.clamp keeps NaN (-> non-finite loss -> skipped step)
+  const float v = isnan(rv) ? rv : fminf(fmaxf(rv, buckets[0]), buckets[nb - 1]);
+  float cnt = 0.0f;
+  for (int j = lane; j < nb; j += 64) cnt += (buckets[j] <= v) ? 1.0f : 0.0f;
+  int lo = (int)wave_sum(cnt) - 1;
+  lo = lo > nb - 2 ? nb - 2 : (lo < 0 ? 0 : lo);
+  const float blo = buckets[lo], bhi = buckets[lo + 1];
+  const float w = (v - blo) / (bhi - blo + 1e-8f);
+  const float coef = coef_row[row];
+  for (int j = lane; j < nb; j += 64) {
+    const float th = (j == lo) ? 1.0f - w : ((j == lo + 1) ? w : 0.0f);
+    g_rew[(long long)row * nb + j] = coef * (expf(x[j] - mx) / se - th);
+  }
+  if (lane == 0) {
+    rew_row[row] = (1.0f - w) * (x[lo] - lse) + w * (x[lo + 1] - lse);
+    const float xc = clog[row], y = cont_tm[row];
+    // binary_cross_entropy_with_logits: (1 - y) x + max(-x, 0) + log(exp(-max) + exp(-x - max))
+    const float mv = fmaxf(-xc, 0.0f);
+    cont_row[row] = (1.0f - y) * xc + mv + logf(expf(-mv) + expf(-xc - mv));
+    g_cont[row] = coef * (1.0f / (1.0f + expf(-xc)) - y);
+  }
+}
+
+// losses (WorldModel.py:170-189) and the KL-gradient factors of the free-bit
+// clamp max(1, KL): d max(1, k)/dk = 1 (k > 1), 1/2 (k == 1), 0 (k < 1)
+__global__ __launch_bounds__(256) void k_wm_final(int M1, int R, int nparts, const float* __restrict__ obs_part,
+                                                  const float* __restrict__ rew_row,
+                                                  const float* __restrict__ cont_row,
+                                                  const float* __restrict__ kl_grp, const float* __restrict__ cont_tm,
+                                                  dr_wm_loss_cfg cfg, float* scal, float* losses, int* skip) {
+  __shared__ float red[256];
+  float so = 0.f, sr = 0.f, sc = 0.f, sk = 0.f;
+  for (int i = threadIdx.x; i < M1; i += 256) {
+    const float m = cont_tm[i];
+    float o = 0.f;
+    for (int j = 0; j < nparts; ++j) o += obs_part[(long long)i * nparts + j];
+    float k = 0.f;
+    for (int g = 0; g < R; ++g) k += kl_grp[(long long)i * R + g];
+    so += o * m;
+    sr += rew_row[i] * m;
+    sc += cont_row[i] * m;
+    sk += k * m;
+  }
+  so = block_sum256(so, red);
+  sr = block_sum256(sr, red);
+  sc = block_sum256(sc, red);
+  sk = block_sum256(sk, red);
+  if (threadIdx.x == 0) {
+    const float denom = scal[0];
+    const float pred = (so - sr + sc) / denom;
+    const float kl = sk / (float)M1;
+    const float total = cfg.beta_pred * pred + cfg.beta_dyn * fmaxf(1.0f, kl) + cfg.beta_rep * fmaxf(1.0f, kl);
+    const float wk = kl > 1.0f ? 1.0f : (kl == 1.0f ? 0.5f : 0.0f);
+    scal[1] = cfg.beta_dyn * wk / (float)M1;
+    scal[2] = cfg.beta_rep * wk / (float)M1;
+    losses[0] = total;
+    losses[1] = pred;
+    losses[2] = kl;
+    losses[3] = kl;
+    if (skip) *skip = isfinite(total) ? 0 : 1;
+  }
+}
+
+// gl = 0.99 * softmax-backward(gz) (+ extra): the straight-through sampler's
+// gradient (VAE.py:92-98) plus the KL-rep gradient of the same logits
+__global__ void k_ste_bwd_add(int M, int R, int C, int W, const float* __restrict__ gz, long long ldg,
+                              const float* __restrict__ soft, long long lds, const float* __restrict__ extra,
+                              long long lde, float* __restrict__ gl, long long ldl) {
+  const int gtid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int grp = gtid / W, c = gtid - grp * W;
+  const bool valid = grp < M * R;
+  const int m = valid ? grp / R : 0, r = valid ? grp - m * R : 0;
+  const bool act = valid && c < C;
+  const float gs = act ? gz[(long long)m * ldg + r * C + c] * 0.99f : 0.0f;
+  const float sv = act ? soft[(long long)m * lds + r * C + c] : 0.0f;
+  const float dot = group_sum(gs * sv, W);
+  if (act) {
+    float v = sv * (gs - dot);
+    if (extra) v += extra[(long long)m * lde + r * C + c];
+    gl[(long long)m * ldl + r * C + c] = v;
+  }
+}
+
+__global__ void k_mul_dsilu(long long n, float* __restrict__ g, const float* __restrict__ pre) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) g[i] = g[i] * dr_dsilu(pre[i]);
+}
+
+// rows of a [C*P][K] matrix between the NCHW flatten order (c*P + p) and NHWC
+// (p*C + c): to_nhwc: out[p*C + c] = in[c*P + p], else the inverse
+__global__ void k_perm_rows(int C, int P, int K, const float* __restrict__ in, float* __restrict__ out, int to_nhwc) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)C * P * K) return;
+  const long long row = i / K;
+  const int k = (int)(i - row * K);
+  const int c = (int)(row / P), p = (int)(row - (long long)c * P);  // row in NCHW order
+  const long long nh = ((long long)p * C + c) * K + k;
+  if (to_nhwc) out[nh] = in[i];
+  else out[i] = in[nh];
+}
+
+static int blocks(long long n, int t) { return (int)((n + t - 1) / t); }
+
+static int perm_rows(int C, int P, int K, const float* in, float* out, int to_nhwc, hipStream_t s) {
+  const long long n = (long long)C * P * K;
+  hipLaunchKernelGGL(k_perm_rows, dim3(blocks(n, 256)), dim3(256), 0, s, C, P, K, in, out, to_nhwc);
+  return dr_check_launch("perm_rows");
+}
+
+static int pow2_ge(int c) {
+  int w = 1;
+  while (w < c) w <<= 1;
+  return w;
+}
+
+// ---------------------------------------------------------------------------
+// workspace
+// ---------------------------------------------------------------------------
+struct MlpBwd {  // backward scratch of one 3-layer head (and its LayerNorm saves)
+  float *gx2, *gp2, *gy2, *xh2, *gx1, *gp1, *gy1, *xh1;
+};
+struct WmWs {
+  // encoder (all M frames)
+  float *x0, *pre1, *a1, *pre2, *a2, *pre3, *a3, *pre4, *a4, *feat;
+  float *wr1, *wr2, *wr3, *wr4, *wqe2, *wqe3, *wqe4;
+  // window data, scan tape
+  float *act_tm, *rew_tm, *cont_tm, *zeros, *h_all, *z_all, *soft, *plog, *pre_m, *x_m, *sr, *su, *sn, *sghn, *gi, *gh,
+      *wt;
+  int* idx;
+  // heads (M1 rows)
+  float *pp1, *px1, *pp2, *px2, *prior_lg, *rp1, *rx1, *rp2, *rx2, *rew_lg, *cp1, *cx1, *cp2, *cx2, *cont_lg;
+  float *du1, *dx1, *du2, *dq1, *dq2, *dq3, *dg4, *w3p, *b3p, *wqd[4], *wrd[4];
+  // loss
+  float *coef_row, *coef_obs, *obs_part, *kl_grp, *rew_row, *cont_row, *scal;
+  // backward
+  float *gH, *gZ, *glog, *gpost, *g_prior, *g_rew, *g_cont;
+  MlpBwd bp, br, bc;
+  float *gxu, *gpu, *gyu, *xhu, *dgq3, *dgq2, *dgq1, *dgu2, *dw3p, *db3p;
+  float *ggi, *ggh, *gpre_m, *gy_m, *xh_m, *gx_s, *gh_dummy;
+  float *ga4, *gp3, *gp2, *gp1;
+  // transposed / permuted weights
+  float *t_pl6, *t_pl3, *t_pl0, *t_rl6, *t_rl3, *t_rl0, *t_cl6, *t_cl3, *t_cl0, *t_up3, *t_up0, *t_map3, *t_map0, *t_whh,
+      *w0tp;
+  float *cws;  // conv weight-gradient / channel-sum scratch
+  long long cws_n;
+};
+
+struct WmDims {
+  int B, T, M, M1, L, Hd, A, eh, nb, IH, IW, c1, c2, c3, c4, P16, F, d1, d2, C0, dh, Fd, ph1, ph2, rh1, rh2, ch1, ch2;
+  long long p0, p1, p2, p3;
+};
+static WmDims wm_dims(const dr_dims* d, int B, int T) {
+  WmDims w;
+  w.B = B; w.T = T; w.M = B * T; w.M1 = B * (T - 1);
+  w.L = latent(d); w.Hd = d->hidden; w.A = d->action; w.eh = d->enc_hidden; w.nb = d->buckets;
+  w.IH = d->img_h; w.IW = d->img_w;
+  w.c1 = d->enc_f1; w.c2 = d->enc_f2; w.c3 = 2 * d->enc_f2; w.c4 = 4 * d->enc_f2;
+  w.P16 = (w.IH / 16) * (w.IW / 16);
+  w.F = w.c4 * w.P16;
+  w.d1 = d->dec_f1; w.d2 = d->dec_f2; w.C0 = 4 * d->dec_f2; w.dh = d->dec_hidden; w.Fd = w.C0 * w.P16;
+  w.ph1 = d->prior_h1; w.ph2 = d->prior_h2; w.rh1 = d->rew_h1; w.rh2 = d->rew_h2; w.ch1 = d->cont_h1; w.ch2 = d->cont_h2;
+  w.p0 = (long long)w.IH * w.IW; w.p1 = w.p0 / 4; w.p2 = w.p0 / 16; w.p3 = w.p0 / 64;
+  return w;
+}
+
+static void mlp_bwd_carve(Carve& c, long long M1, int w1, int w2, MlpBwd& b) {
+  b.gx2 = c.f(M1 * w2); b.gp2 = c.f(M1 * w2); b.gy2 = c.f(M1 * w2); b.xh2 = c.f(M1 * w2);
+  b.gx1 = c.f(M1 * w1); b.gp1 = c.f(M1 * w1); b.gy1 = c.f(M1 * w1); b.xh1 = c.f(M1 * w1);
+}
+
+static long long wm_conv_scratch(const WmDims& D) {
+  const int n = D.M, n1 = D.M1;
+  long long m = 0;
+  auto mx = [&](long long v) { if (v > m) m = v; };
+  // encoder weight grads: lo = output grad (h, w), hi = input
+  mx(op_conv_wgrad_ws_floats(n, D.IH / 2, D.IW / 2, D.c1, 4));
+  mx(op_conv_wgrad_ws_floats(n, D.IH / 4, D.IW / 4, D.c2, D.c1));
+  mx(op_conv_wgrad_ws_floats(n, D.IH / 8, D.IW / 8, D.c3, D.c2));
+  mx(op_conv_wgrad_ws_floats(n, D.IH / 16, D.IW / 16, D.c4, D.c3));
+  // decoder weight grads: lo = convT input, hi = output grad
+  mx(op_conv_wgrad_ws_floats(n1, D.IH / 16, D.IW / 16, D.C0, 2 * D.d2));
+  mx(op_conv_wgrad_ws_floats(n1, D.IH / 8, D.IW / 8, 2 * D.d2, D.d2));
+  mx(op_conv_wgrad_ws_floats(n1, D.IH / 4, D.IW / 4, D.d2, D.d1));
+  mx(op_conv_wgrad_ws_floats(n1, D.IH / 2, D.IW / 2, D.d1, 4));
+  mx(op_chan_sum_ws_floats((long long)n * D.p1, D.c1));
+  mx(op_chan_sum_ws_floats((long long)n1 * D.p0, 3));
+  mx(op_chan_sum_ws_floats((long long)n1 * D.p1, D.d1));
+  return m;
+}
+
+static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
+  const long long M = D.M, M1 = D.M1, B = D.B;
+  const int L = D.L, Hd = D.Hd, A = D.A, eh = D.eh;
+  w.x0 = c.f(M * D.p0 * 4);
+  w.pre1 = c.f(M * D.p1 * D.c1); w.a1 = c.f(M * D.p1 * D.c1);
+  w.pre2 = c.f(M * D.p2 * D.c2); w.a2 = c.f(M * D.p2 * D.c2);
+  w.pre3 = c.f(M * D.p3 * D.c3); w.a3 = c.f(M * D.p3 * D.c3);
+  w.pre4 = c.f(M * D.F); w.a4 = c.f(M * D.F);
+  w.feat = c.f(M * eh);
+  w.wr1 = c.f((long long)D.c1 * 16 * 4); w.wr2 = c.f((long long)D.c2 * 16 * D.c1);
+  w.wr3 = c.f((long long)D.c3 * 16 * D.c2); w.wr4 = c.f((long long)D.c4 * 16 * D.c3);
+  w.wqe2 = c.f((long long)16 * D.c2 * D.c1); w.wqe3 = c.f((long long)16 * D.c3 * D.c2);
+  w.wqe4 = c.f((long long)16 * D.c4 * D.c3);
+  w.act_tm = c.f(M * A); w.rew_tm = c.f(M); w.cont_tm = c.f(M);
+  w.zeros = c.f(B * (L + A + Hd));
+  w.h_all = c.f(M * Hd); w.z_all = c.f(M * L); w.soft = c.f(M * L); w.plog = c.f(M * L);
+  w.pre_m = c.f(M * eh); w.x_m = c.f(M * eh);
+  w.sr = c.f(M * Hd); w.su = c.f(M * Hd); w.sn = c.f(M * Hd); w.sghn = c.f(M * Hd);
+  w.gi = c.f(B * 3 * Hd); w.gh = c.f(B * 3 * Hd);
+  w.wt = c.f((long long)(L + A) * 3 * Hd);
+  w.idx = c.i((long long)D.T * 2 * B * d->rows);
+  w.pp1 = c.f(M1 * D.ph1); w.px1 = c.f(M1 * D.ph1); w.pp2 = c.f(M1 * D.ph2); w.px2 = c.f(M1 * D.ph2);
+  w.prior_lg = c.f(M1 * L);
+  w.rp1 = c.f(M1 * D.rh1); w.rx1 = c.f(M1 * D.rh1); w.rp2 = c.f(M1 * D.rh2); w.rx2 = c.f(M1 * D.rh2);
+  w.rew_lg = c.f(M1 * D.nb);
+  w.cp1 = c.f(M1 * D.ch1); w.cx1 = c.f(M1 * D.ch1); w.cp2 = c.f(M1 * D.ch2); w.cx2 = c.f(M1 * D.ch2);
+  w.cont_lg = c.f(M1);
+  w.du1 = c.f(M1 * D.dh); w.dx1 = c.f(M1 * D.dh); w.du2 = c.f(M1 * D.Fd);
+  w.dq1 = c.f(M1 * D.p3 * 2 * D.d2); w.dq2 = c.f(M1 * D.p2 * D.d2); w.dq3 = c.f(M1 * D.p1 * D.d1);
+  w.dg4 = c.f(M1 * D.p0 * 4);
+  w.w3p = c.f((long long)D.Fd * D.dh); w.b3p = c.f(D.Fd);
+  const int cin_t[4] = {D.C0, 2 * D.d2, D.d2, D.d1}, cout_t[4] = {2 * D.d2, D.d2, D.d1, 3};
+  for (int k = 0; k < 4; ++k) {
+    w.wqd[k] = c.f((long long)16 * cin_t[k] * cout_t[k]);
+    w.wrd[k] = c.f((long long)16 * cin_t[k] * (k == 3 ? 4 : cout_t[k]));
+  }
+  w.coef_row = c.f(M1); w.coef_obs = c.f(M1);
+  w.obs_part = c.f(M1 * op_convT_mse_parts(D.IH / 2, D.IW / 2));
+  w.kl_grp = c.f(M1 * d->rows); w.rew_row = c.f(M1); w.cont_row = c.f(M1); w.scal = c.f(8);
+  w.gH = c.f(M * Hd); w.gZ = c.f(M * L); w.glog = c.f(M * L); w.gpost = c.f(M1 * L);
+  w.g_prior = c.f(M1 * L); w.g_rew = c.f(M1 * D.nb); w.g_cont = c.f(M1);
+  mlp_bwd_carve(c, M1, D.ph1, D.ph2, w.bp);
+  mlp_bwd_carve(c, M1, D.rh1, D.rh2, w.br);
+  mlp_bwd_carve(c, M1, D.ch1, D.ch2, w.bc);
+  w.gxu = c.f(M1 * D.dh); w.gpu = c.f(M1 * D.dh); w.gyu = c.f(M1 * D.dh); w.xhu = c.f(M1 * D.dh);
+  w.dgq3 = c.f(M1 * D.p1 * D.d1); w.dgq2 = c.f(M1 * D.p2 * D.d2); w.dgq1 = c.f(M1 * D.p3 * 2 * D.d2);
+  w.dgu2 = c.f(M1 * D.Fd);
+  w.dw3p = c.f((long long)D.Fd * D.dh); w.db3p = c.f(D.Fd);
+  w.ggi = c.f(M * 3 * Hd); w.ggh = c.f(M * 3 * Hd);
+  w.gpre_m = c.f(M * eh); w.gy_m = c.f(M * eh); w.xh_m = c.f(M * eh);
+  w.gx_s = c.f(B * eh); w.gh_dummy = c.f(B * Hd);
+  w.ga4 = c.f(M * D.F); w.gp3 = c.f(M * D.p3 * D.c3); w.gp2 = c.f(M * D.p2 * D.c2); w.gp1 = c.f(M * D.p1 * D.c1);
+  w.t_pl6 = c.f((long long)L * D.ph2); w.t_pl3 = c.f((long long)D.ph2 * D.ph1); w.t_pl0 = c.f((long long)D.ph1 * Hd);
+  w.t_rl6 = c.f((long long)D.nb * D.rh2); w.t_rl3 = c.f((long long)D.rh2 * D.rh1);
+  w.t_rl0 = c.f((long long)D.rh1 * (Hd + L));
+  w.t_cl6 = c.f(D.ch2); w.t_cl3 = c.f((long long)D.ch2 * D.ch1); w.t_cl0 = c.f((long long)D.ch1 * (Hd + L));
+  w.t_up3 = c.f((long long)D.Fd * D.dh); w.t_up0 = c.f((long long)D.dh * (Hd + L));
+  w.t_map3 = c.f((long long)L * eh); w.t_map0 = c.f((long long)eh * (D.F + Hd));
+  w.t_whh = c.f((long long)3 * Hd * Hd); w.w0tp = c.f((long long)D.F * eh);
+  w.cws_n = wm_conv_scratch(D);
+  w.cws = c.f(w.cws_n);
+}
+
+extern "C" size_t dr_wm_train_workspace_bytes(const dr_dims* d, int B, int T) {
+  if (!d || B <= 0 || T < 2) return 0;
+  Carve c(nullptr);
+  WmWs w;
+  wm_carve(c, d, wm_dims(d, B, T), w);
+  return c.off;
+}
+
+// input-gradient + weight-gradient pass of one head MLP (Linear-LN-SiLU x2 +
+// Linear) over M1 rows whose input is [h | z] (in_z = 0: h only).  Adds the
+// input gradient into gH/gZ rows t >= 1.
+static int head_bwd(const WmDims& D, const dr_mlp3& m, const dr_mlp3& g, int w1, int w2, int nout, const float* glog,
+                    const float* t6, const float* t3, const float* t0, const float* x1, const float* x2,
+                    const float* pre1, const float* pre2, int in_z, const float* hB, const float* zB, float* gHB,
+                    float* gZB, MlpBwd& b, hipStream_t s) {
+  const int M1 = D.M1, Hd = D.Hd, L = D.L;
+  DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M1, w2, nout, glog, nout, t6, b.gx2, w2, 0), s));
+  DR_TRY(lnbwd_nt(M1, w1, w2, b.gx2, w2, pre2, w2, m.n4, t3, b.gx1, w1, 0, b.gp2, w2, b.gy2, b.xh2, nullptr, 0,
+                  INT_MAX, s));
+  DR_TRY(lnbwd_nt(M1, in_z ? Hd + L : Hd, w1, b.gx1, w1, pre1, w1, m.n1, t0, gHB, Hd, 1, b.gp1, w1, b.gy1, b.xh1,
+                  in_z ? gZB : nullptr, L, in_z ? Hd : INT_MAX, s));
+  GemmArgs p[3];
+  p[0] = bwd_w(nout, w2, M1, glog, nout, x2, w2, g.l6.w);
+  p[1] = bwd_w(w2, w1, M1, b.gp2, w2, x1, w1, g.l3.w);
+  p[2] = bwd_w(w1, in_z ? Hd + L : Hd, M1, b.gp1, w1, hB, Hd, g.l0.w);
+  if (in_z) {
+    p[2].W2 = zB; p[2].ldb2 = L; p[2].nsplitB = Hd;
+  }
+  DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 3, s));
+  ColsumJob cj[7] = {
+      {nout, glog, nout, nullptr, 0, g.l6.b}, {w2, b.gp2, w2, nullptr, 0, g.l3.b},
+      {w2, b.gy2, w2, b.xh2, w2, g.n4.w},     {w2, b.gy2, w2, nullptr, 0, g.n4.b},
+      {w1, b.gp1, w1, nullptr, 0, g.l0.b},    {w1, b.gy1, w1, b.xh1, w1, g.n1.w},
+      {w1, b.gy1, w1, nullptr, 0, g.n1.b},
+  };
+  return op_colsum_multi(M1, cj, 7, s);
+}
+
+extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, const dr_decoder* dec, int B, int T,
+                                 const dr_frames* src, const dr_wm_batch* bt, dr_noise noise, dr_wm_loss_cfg cfg,
+                                 float* losses, int* skip, const dr_world_model* gw, const dr_decoder* gd,
+                                 float* hiddens_out, float* latents_out, float* post_logits_out, void* ws,
+                                 size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(d && wm && dec && src && bt && losses && gw && gd && B > 0 && T >= 2, "null argument or T < 2");
+  DR_REQUIRE(bt->actions && bt->rewards && bt->continues, "window actions / rewards / continues required");
+  DR_REQUIRE(d->img_h % 32 == 0 && d->img_w % 32 == 0 && (d->img_h / 2) * (d->img_w / 2) % 128 == 0,
+             "image size must be a multiple of 32 with (H/2)*(W/2) % 128 == 0");
+  DR_REQUIRE(d->enc_f1 % 8 == 0 && d->enc_f2 % 8 == 0 && d->dec_f1 % 8 == 0 && d->dec_f2 % 8 == 0,
+             "encoder / decoder filter counts must be multiples of 8");
+  DR_REQUIRE(d->cols <= 64, "latent classes must be <= 64");
+  const WmDims D = wm_dims(d, B, T);
+  Carve c(ws);
+  WmWs w;
+  wm_carve(c, d, D, w);
+  WS_CHECK(c, ws_bytes);
+  const int M = D.M, M1 = D.M1, L = D.L, Hd = D.Hd, A = D.A, eh = D.eh, nb = D.nb, F = D.F, R = d->rows;
+  const int IH = D.IH, IW = D.IW;
+  const float* hB = w.h_all + (long long)B * Hd;
+  const float* zB = w.z_all + (long long)B * L;
+  float* gHB = w.gH + (long long)B * Hd;
+  float* gZB = w.gZ + (long long)B * L;
+
+  // ---- weights: repacks, transposes, permutations (fixed for the call) ----
+  DR_TRY(op_conv_repack_pad(D.c1, 3, 4, wm->conv[0].w, w.wr1, s));
+  DR_TRY(op_conv_repack_pad(D.c2, D.c1, D.c1, wm->conv[1].w, w.wr2, s));
+  DR_TRY(op_conv_repack_pad(D.c3, D.c2, D.c2, wm->conv[2].w, w.wr3, s));
+  DR_TRY(op_conv_repack_pad(D.c4, D.c3, D.c3, wm->conv[3].w, w.wr4, s));
+  // Conv2d data gradient = upsampling conv with the weight read as [cin=co][cout=ci]
+  DR_TRY(op_convT_repack(D.c2, D.c1, wm->conv[1].w, w.wqe2, s));
+  DR_TRY(op_convT_repack(D.c3, D.c2, wm->conv[2].w, w.wqe3, s));
+  DR_TRY(op_convT_repack(D.c4, D.c3, wm->conv[3].w, w.wqe4, s));
+  const int cin_t[4] = {D.C0, 2 * D.d2, D.d2, D.d1}, cout_t[4] = {2 * D.d2, D.d2, D.d1, 3};
+  for (int k = 0; k < 4; ++k) {
+    DR_TRY(op_convT_repack(cin_t[k], cout_t[k], dec->convt[k].w, w.wqd[k], s));
+    // ConvTranspose2d data gradient = strided Conv2d with the weight read as [out=ci][in=co]
+    DR_TRY(op_conv_repack_pad(cin_t[k], cout_t[k], k == 3 ? 4 : cout_t[k], dec->convt[k].w, w.wrd[k], s));
+  }
+  // decoder.upscaler.3 rows to NHWC order, so its output is the first convT's NHWC input
+  DR_TRY(perm_rows(D.C0, D.P16, D.dh, dec->up3.w, w.w3p, 1, s));
+  DR_TRY(perm_rows(D.C0, D.P16, 1, dec->up3.b, w.b3p, 1, s));
+  {
+    TransposeJob tj[10] = {
+        {L, D.ph2, L, wm->prior.l6.w, w.t_pl6},          {D.ph2, D.ph1, D.ph2, wm->prior.l3.w, w.t_pl3},
+        {D.ph1, Hd, D.ph1, wm->prior.l0.w, w.t_pl0},     {nb, D.rh2, nb, wm->reward.l6.w, w.t_rl6},
+        {D.rh2, D.rh1, D.rh2, wm->reward.l3.w, w.t_rl3}, {D.rh1, Hd + L, D.rh1, wm->reward.l0.w, w.t_rl0},
+        {1, D.ch2, 1, wm->cont.l6.w, w.t_cl6},           {D.ch2, D.ch1, D.ch2, wm->cont.l3.w, w.t_cl3},
+        {D.ch1, Hd + L, D.ch1, wm->cont.l0.w, w.t_cl0},  {3 * Hd, L + A, 3 * Hd, wm->w_ih, w.wt},
+    };
+    DR_TRY(op_transpose_multi(tj, 10, s));
+    TransposeJob tj2[5] = {
+        {D.Fd, D.dh, D.Fd, w.w3p, w.t_up3},          {D.dh, Hd + L, D.dh, dec->up0.w, w.t_up0},
+        {L, eh, L, wm->map3.w, w.t_map3},            {eh, F + Hd, eh, wm->map0.w, w.t_map0},
+        {3 * Hd, Hd, 3 * Hd, wm->w_hh, w.t_whh},
+    };
+    DR_TRY(op_transpose_multi(tj2, 5, s));
+  }
+  // latent_mapper.0 feature rows (of its transpose) to NHWC: dL/d conv4-out comes out NHWC
+  DR_TRY(perm_rows(D.c4, D.P16, eh, w.t_map0, w.w0tp, 1, s));
+
+  // ---- window data ----
+  hipLaunchKernelGGL(k_wm_gather, dim3(blocks(M, 256)), dim3(256), 0, s, B, T, A, *bt, w.act_tm, w.rew_tm, w.cont_tm);
+  DR_TRY(dr_check_launch("wm_gather"));
+  DR_TRY(zero(w.zeros, (long long)B * (L + A + Hd), s));
+  hipLaunchKernelGGL(k_wm_prep, dim3(1), dim3(256), 0, s, M1, w.cont_tm, cfg.beta_pred, w.scal, w.coef_row,
+                     w.coef_obs);
+  DR_TRY(dr_check_launch("wm_prep"));
+
+  // ---- encoder over all M frames (VAE.py:57-75), activations kept ----
+  DR_TRY(op_frames_nhwc4(M, B, IH, IW, src, w.x0, s));
+  DR_TRY(op_conv_nhwc_ex(M, 4, IH, IW, D.c1, w.x0, w.wr1, wm->conv[0].b, w.a1, 0, w.pre1, CONV_EPI_FWD, s));
+  DR_TRY(op_conv_nhwc_ex(M, D.c1, IH / 2, IW / 2, D.c2, w.a1, w.wr2, wm->conv[1].b, w.a2, 0, w.pre2, CONV_EPI_FWD, s));
+  DR_TRY(op_conv_nhwc_ex(M, D.c2, IH / 4, IW / 4, D.c3, w.a2, w.wr3, wm->conv[2].b, w.a3, 0, w.pre3, CONV_EPI_FWD, s));
+  DR_TRY(op_conv_nhwc_ex(M, D.c3, IH / 8, IW / 8, D.c4, w.a3, w.wr4, wm->conv[3].b, w.a4, 1, w.pre4, CONV_EPI_FWD, s));
+  DR_TRY(run(G_NT, AM_PLAIN, lin(M, eh, F, w.a4, F, wm->map0.w, F + Hd, wm->map0.b, w.feat, eh), s));
+
+  // ---- posterior scan (unroll_model, WorldModel.py:97-107) ----
+  const long long idx_stride = 2LL * B * R;
+  for (int t = 0; t < T; ++t) {
+    const long long rb = (long long)t * B;
+    float* h_t = w.h_all + rb * Hd;
+    float* z_t = w.z_all + rb * L;
+    if (t == 0) {  // GRU from z = 0, a = 0, h = 0
+      DR_TRY(gru_step(d, wm, B, w.zeros, L, w.zeros + (long long)B * L, A, w.zeros + (long long)B * (L + A), Hd, h_t,
+                      Hd, w.gi, w.gh, w.sr, w.su, w.sn, w.sghn, s));
+    } else {
+      DR_TRY(gru_onehot(d, wm, B, w.idx + (t - 1) * idx_stride, w.act_tm + (rb - B) * A, A, h_t - (long long)B * Hd,
+                        Hd, h_t, Hd, w.wt, w.sr + rb * Hd, w.su + rb * Hd, w.sn + rb * Hd, w.sghn + rb * Hd, s));
+    }
+    GemmArgs g = lin(B, eh, Hd, h_t, Hd, wm->map0.w + F, F + Hd, nullptr, w.pre_m + rb * eh, eh);
+    g.addend = w.feat + rb * eh;
+    g.ld_add = eh;
+    DR_TRY(run(G_NT, AM_PLAIN, g, s));
+    GemmArgs gp = lin_ln(B, L, eh, w.pre_m + rb * eh, eh, wm->map1, wm->map3.w, wm->map3.b, w.plog + rb * L, L);
+    gp.a_out = w.x_m + rb * eh;
+    gp.ld_aout = eh;
+    with_sampler(gp, d, noise, t, z_t, L, w.idx + t * idx_stride, w.soft + rb * L, L);
+    DR_TRY(run(G_NT, AM_LNSILU, gp, s));
+  }
+
+  // ---- heads on rows t >= 1 (WorldModel.py:116-119) ----
+  {
+    GemmArgs p[4];
+    p[0] = lin(M1, D.ph1, Hd, hB, Hd, wm->prior.l0.w, Hd, wm->prior.l0.b, w.pp1, D.ph1);
+    p[1] = lin2(M1, D.rh1, hB, Hd, Hd, zB, L, L, wm->reward.l0.w, wm->reward.l0.b, w.rp1, D.rh1);
+    p[2] = lin2(M1, D.ch1, hB, Hd, Hd, zB, L, L, wm->cont.l0.w, wm->cont.l0.b, w.cp1, D.ch1);
+    p[3] = lin2(M1, D.dh, hB, Hd, Hd, zB, L, L, dec->up0.w, dec->up0.b, w.du1, D.dh);
+    DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, 4, s));
+  }
+  {
+    GemmArgs p[3];
+    p[0] = lin_ln(M1, D.ph2, D.ph1, w.pp1, D.ph1, wm->prior.n1, wm->prior.l3.w, wm->prior.l3.b, w.pp2, D.ph2);
+    p[0].a_out = w.px1; p[0].ld_aout = D.ph1;
+    p[1] = lin_ln(M1, D.rh2, D.rh1, w.rp1, D.rh1, wm->reward.n1, wm->reward.l3.w, wm->reward.l3.b, w.rp2, D.rh2);
+    p[1].a_out = w.rx1; p[1].ld_aout = D.rh1;
+    p[2] = lin_ln(M1, D.ch2, D.ch1, w.cp1, D.ch1, wm->cont.n1, wm->cont.l3.w, wm->cont.l3.b, w.cp2, D.ch2);
+    p[2].a_out = w.cx1; p[2].ld_aout = D.ch1;
+    DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, 3, s));
+  }
+  {
+    GemmArgs p[3];
+    p[0] = lin_ln(M1, L, D.ph2, w.pp2, D.ph2, wm->prior.n4, wm->prior.l6.w, wm->prior.l6.b, w.prior_lg, L);
+    p[0].a_out = w.px2; p[0].ld_aout = D.ph2;
+    p[1] = lin_ln(M1, nb, D.rh2, w.rp2, D.rh2, wm->reward.n4, wm->reward.l6.w, wm->reward.l6.b, w.rew_lg, nb);
+    p[1].a_out = w.rx2; p[1].ld_aout = D.rh2;
+    p[2] = lin_ln(M1, 1, D.ch2, w.cp2, D.ch2, wm->cont.n4, wm->cont.l6.w, wm->cont.l6.b, w.cont_lg, 1);
+    p[2].a_out = w.cx2; p[2].ld_aout = D.ch2;
+    DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, 3, s));
+  }
+  // decoder (VAE.py:139-161): upscaler.3 pre-activation in NHWC, SiLU applied by the consumers
+  {
+    GemmArgs g = lin_ln(M1, D.Fd, D.dh, w.du1, D.dh, dec->up1, w.w3p, w.b3p, w.du2, D.Fd);
+    g.a_out = w.dx1; g.ld_aout = D.dh;
+    DR_TRY(run(G_NT, AM_LNSILU, g, s));
+  }
+  {
+    const float* ins[4] = {w.du2, w.dq1, w.dq2, w.dq3};
+    float* outs[3] = {w.dq1, w.dq2, w.dq3};
+    for (int k = 0; k < 4; ++k) {
+      ConvTArgs a = {};
+      a.n = M1; a.cin = cin_t[k]; a.h = IH >> (4 - k); a.w = IW >> (4 - k); a.cout = cout_t[k];
+      a.in = ins[k]; a.silu_in = 1; a.wq = w.wqd[k]; a.bias = dec->convt[k].b;
+      if (k < 3) {
+        a.out = outs[k]; a.ldc = cout_t[k];
+        DR_TRY(op_convT_nhwc(CT_EPI_BIAS, a, s));
+      } else {
+        // Tanh + squared error against frames t >= 1 (WorldModel.py:129); writes dL/d(pre-tanh)
+        a.out = w.dg4; a.ldc = 4;
+        a.target = w.x0 + (long long)B * D.p0 * 4; a.tstride = 4;
+        a.coef = w.coef_obs; a.part = w.obs_part;
+        DR_TRY(op_convT_nhwc(CT_EPI_TANH_MSE, a, s));
+      }
+    }
+  }
+
+  // ---- losses ----
+  {
+    const int W = pow2_ge(d->cols);
+    const long long th = (long long)M1 * R * W;
+    const float* post1 = w.plog + (long long)B * L;
+    hipLaunchKernelGGL(k_wm_kl<0>, dim3(blocks(th, 256)), dim3(256), 0, s, M1, R, d->cols, W, w.prior_lg, post1,
+                       w.cont_tm, w.scal, w.kl_grp, nullptr, nullptr);
+    DR_TRY(dr_check_launch("wm_kl"));
+    hipLaunchKernelGGL(k_wm_heads, dim3(blocks(M1, 4)), dim3(256), 0, s, M1, nb, w.rew_lg, w.cont_lg, w.rew_tm,
+                       w.cont_tm, wm->buckets_rew, w.coef_row, w.rew_row, w.cont_row, w.g_rew, w.g_cont);
+    DR_TRY(dr_check_launch("wm_heads"));
+    hipLaunchKernelGGL(k_wm_final, dim3(1), dim3(256), 0, s, M1, R, op_convT_mse_parts(IH / 2, IW / 2), w.obs_part,
+                       w.rew_row, w.cont_row, w.kl_grp, w.cont_tm, cfg, w.scal, losses, skip);
+    DR_TRY(dr_check_launch("wm_final"));
+    hipLaunchKernelGGL(k_wm_kl<1>, dim3(blocks(th, 256)), dim3(256), 0, s, M1, R, d->cols, W, w.prior_lg, post1,
+                       w.cont_tm, w.scal, nullptr, w.g_prior, w.gpost);
+    DR_TRY(dr_check_launch("wm_kl_bwd"));
+  }
+
+  // ---- backward: heads (rows t >= 1) into dL/dh, dL/dz ----
+  DR_TRY(zero(w.gH, (long long)M * Hd, s));
+  DR_TRY(zero(w.gZ, (long long)M * L, s));
+  DR_TRY(head_bwd(D, wm->prior, gw->prior, D.ph1, D.ph2, L, w.g_prior, w.t_pl6, w.t_pl3, w.t_pl0, w.px1, w.px2, w.pp1,
+                  w.pp2, 0, hB, zB, gHB, gZB, w.bp, s));
+  DR_TRY(head_bwd(D, wm->reward, gw->reward, D.rh1, D.rh2, nb, w.g_rew, w.t_rl6, w.t_rl3, w.t_rl0, w.rx1, w.rx2, w.rp1,
+                  w.rp2, 1, hB, zB, gHB, gZB, w.br, s));
+  DR_TRY(head_bwd(D, wm->cont, gw->cont, D.ch1, D.ch2, 1, w.g_cont, w.t_cl6, w.t_cl3, w.t_cl0, w.cx1, w.cx2, w.cp1,
+                  w.cp2, 1, hB, zB, gHB, gZB, w.bc, s));
+  // decoder: image_builder.6 .. .0 (data grads as strided convs, weight grads, bias sums)
+  {
+    float* gins[4] = {w.dgu2, w.dgq1, w.dgq2, w.dgq3};   // dL/d(pre-activation) of each convT input
+    const float* pres[4] = {w.du2, w.dq1, w.dq2, w.dq3};
+    const float* gouts[4] = {w.dgq1, w.dgq2, w.dgq3, w.dg4};
+    for (int k = 3; k >= 0; --k) {
+      const int ih = IH >> (3 - k), iw = IW >> (3 - k);  // output (high-res) size of convT k
+      const int co = cout_t[k], co_st = (k == 3) ? 4 : co;
+      DR_TRY(op_conv_nhwc_ex(M1, co_st, ih, iw, cin_t[k], gouts[k], w.wrd[k], nullptr, gins[k], 0,
+                             const_cast<float*>(pres[k]), CONV_EPI_DSILU, s));
+      DR_TRY(op_conv_wgrad(M1, ih / 2, iw / 2, cin_t[k], co_st, pres[k], cin_t[k], 1, gouts[k], co_st, gd->convt[k].w,
+                           co, 1.0f, 0, w.cws, w.cws_n, s));
+      DR_TRY(op_chan_sum((long long)M1 * ih * iw, co, gouts[k], co_st, gd->convt[k].b, 0, w.cws, w.cws_n, s));
+    }
+  }
+  // decoder.upscaler: .3 (permuted rows) then LN-SiLU(.1) and .0 into dL/d[h | z]
+  DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M1, D.dh, D.Fd, w.dgu2, D.Fd, w.t_up3, w.gxu, D.dh, 0), s));
+  DR_TRY(lnbwd_nt(M1, Hd + L, D.dh, w.gxu, D.dh, w.du1, D.dh, dec->up1, w.t_up0, gHB, Hd, 1, w.gpu, D.dh, w.gyu, w.xhu,
+                  gZB, L, Hd, s));
+  {
+    GemmArgs p[2];
+    p[0] = bwd_w(D.Fd, D.dh, M1, w.dgu2, D.Fd, w.dx1, D.dh, w.dw3p);
+    p[1] = bwd_w(D.dh, Hd + L, M1, w.gpu, D.dh, hB, Hd, gd->up0.w);
+    p[1].W2 = zB; p[1].ldb2 = L; p[1].nsplitB = Hd;
+    DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 2, s));
+    ColsumJob cj[4] = {
+        {D.Fd, w.dgu2, D.Fd, nullptr, 0, w.db3p},
+        {D.dh, w.gpu, D.dh, nullptr, 0, gd->up0.b},
+        {D.dh, w.gyu, D.dh, w.xhu, D.dh, gd->up1.w},
+        {D.dh, w.gyu, D.dh, nullptr, 0, gd->up1.b},
+    };
+    DR_TRY(op_colsum_multi(M1, cj, 4, s));
+    DR_TRY(perm_rows(D.C0, D.P16, D.dh, w.dw3p, gd->up3.w, 0, s));
+    DR_TRY(perm_rows(D.C0, D.P16, 1, w.db3p, gd->up3.b, 0, s));
+  }
+
+  // ---- backward through the posterior scan, t = T-1 .. 0 ----
+  const int Wc = pow2_ge(d->cols);
+  for (int t = T - 1; t >= 0; --t) {
+    const long long rb = (long long)t * B;
+    float* gH_t = w.gH + rb * Hd;
+    // straight-through sampler (+ KL-rep on rows t >= 1) -> dL/d logits
+    hipLaunchKernelGGL(k_ste_bwd_add, dim3(blocks((long long)B * R * Wc, 256)), dim3(256), 0, s, B, R, d->cols, Wc,
+                       w.gZ + rb * L, (long long)L, w.soft + rb * L, (long long)L,
+                       t > 0 ? w.gpost + (rb - B) * L : nullptr, (long long)L, w.glog + rb * L, (long long)L);
+    DR_TRY(dr_check_launch("ste_bwd_add"));
+    // latent_mapper.3, then LN-SiLU(.1) fused into latent_mapper.0's h-columns input gradient
+    DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, eh, L, w.glog + rb * L, L, w.t_map3, w.gx_s, eh, 0), s));
+    DR_TRY(lnbwd_nt(B, Hd, eh, w.gx_s, eh, w.pre_m + rb * eh, eh, wm->map1, w.t_map0 + (long long)F * eh, gH_t, Hd, 1,
+                    w.gpre_m + rb * eh, eh, w.gy_m + rb * eh, w.xh_m + rb * eh, nullptr, 0, INT_MAX, s));
+    // GRU (SequenceModel.py:19-24): h_t = GRU([z_{t-1}, a_{t-1}], h_{t-1})
+    const float* hprev = t > 0 ? w.h_all + (rb - B) * Hd : w.zeros + (long long)B * (L + A);
+    DR_TRY(op_gru_bwd(B, Hd, gH_t, Hd, hprev, Hd, w.sr + rb * Hd, w.su + rb * Hd, w.sn + rb * Hd, w.sghn + rb * Hd,
+                      w.ggi + rb * 3 * Hd, w.ggh + rb * 3 * Hd, t > 0 ? gH_t - (long long)B * Hd : w.gh_dummy, Hd,
+                      t > 0 ? 1 : 0, s));
+    if (t > 0) {
+      GemmArgs p[2];
+      p[0] = bwd_nt(B, L, 3 * Hd, w.ggi + rb * 3 * Hd, 3 * Hd, w.wt, w.gZ + (rb - B) * L, L, 1);
+      p[1] = bwd_nt(B, Hd, 3 * Hd, w.ggh + rb * 3 * Hd, 3 * Hd, w.t_whh, gH_t - (long long)B * Hd, Hd, 1);
+      DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, 2, s));
+    }
+  }
+  // scan weight gradients over all rows
+  {
+    GemmArgs p[4];
+    p[0] = bwd_w(L, eh, M, w.glog, L, w.x_m, eh, gw->map3.w);
+    p[1] = bwd_w(eh, F + Hd, M, w.gpre_m, eh, w.a4, F, gw->map0.w);
+    p[1].W2 = w.h_all; p[1].ldb2 = Hd; p[1].nsplitB = F;
+    p[2] = bwd_w(3 * Hd, L + A, M1, w.ggi + (long long)B * 3 * Hd, 3 * Hd, w.z_all, L, gw->w_ih);
+    p[2].W2 = w.act_tm; p[2].ldb2 = A; p[2].nsplitB = L;
+    p[3] = bwd_w(3 * Hd, Hd, M1, w.ggh + (long long)B * 3 * Hd, 3 * Hd, w.h_all, Hd, gw->w_hh);
+    DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 4, s));
+    ColsumJob cj[6] = {
+        {L, w.glog, L, nullptr, 0, gw->map3.b},       {eh, w.gpre_m, eh, nullptr, 0, gw->map0.b},
+        {eh, w.gy_m, eh, w.xh_m, eh, gw->map1.w},     {eh, w.gy_m, eh, nullptr, 0, gw->map1.b},
+        {3 * Hd, w.ggi, 3 * Hd, nullptr, 0, gw->b_ih}, {3 * Hd, w.ggh, 3 * Hd, nullptr, 0, gw->b_hh},
+    };
+    DR_TRY(op_colsum_multi(M, cj, 6, s));
+  }
+
+  // ---- backward through the encoder convolutions (all M frames) ----
+  DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M, F, eh, w.gpre_m, eh, w.w0tp, w.ga4, F, 0), s));
+  hipLaunchKernelGGL(k_mul_dsilu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, w.ga4,
+                     w.pre4);
+  DR_TRY(dr_check_launch("mul_dsilu"));
+  {
+    float* go[4] = {w.gp1, w.gp2, w.gp3, w.ga4};           // dL/d pre-activation of conv k's output
+    const float* pr[3] = {w.pre1, w.pre2, w.pre3};
+    const float* hi[4] = {w.x0, w.a1, w.a2, w.a3};         // conv k's input
+    const float* wq[4] = {nullptr, w.wqe2, w.wqe3, w.wqe4};
+    const int cin[4] = {4, D.c1, D.c2, D.c3}, cout[4] = {D.c1, D.c2, D.c3, D.c4};
+    for (int k = 3; k >= 0; --k) {
+      const int oh = IH >> (k + 1), ow = IW >> (k + 1);
+      DR_TRY(op_conv_wgrad(M, oh, ow, cout[k], cin[k], go[k], cout[k], 0, hi[k], cin[k], gw->conv[k].w,
+                           k == 0 ? 3 : cin[k], 1.0f, 0, w.cws, w.cws_n, s));
+      DR_TRY(op_chan_sum((long long)M * oh * ow, cout[k], go[k], cout[k], gw->conv[k].b, 0, w.cws, w.cws_n, s));
+      if (k > 0) {
+        ConvTArgs a = {};
+        a.n = M; a.cin = cout[k]; a.h = oh; a.w = ow; a.cout = cin[k];
+        a.in = go[k]; a.wq = wq[k]; a.out = go[k - 1]; a.ldc = cin[k]; a.pre = pr[k - 1];
+        DR_TRY(op_convT_nhwc(CT_EPI_DSILU, a, s));
+      }
+    }
+  }
+
+  if (hiddens_out) DR_TRY(copy2d(hiddens_out, Hd, w.h_all, Hd, Hd, M, s));
+  if (latents_out) DR_TRY(copy2d(latents_out, L, w.z_all, L, L, M, s));
+  if (post_logits_out) DR_TRY(copy2d(post_logits_out, L, w.plog, L, L, M, s));
+  return DR_OK;
+}

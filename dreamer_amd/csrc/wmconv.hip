@@ -1,0 +1,509 @@
+// Convolutions of the world-model training step (WorldModel.training_step,
+// WorldModel.py:148-202): the decoder's ConvTranspose2d stack
+// (VariationalAutoEncoder.py:128-137), the encoder's Conv2d data gradients and
+// the weight gradients of both.  NHWC implicit GEMMs on the exact-f32 MFMA
+// (v_mfma_f32_16x16x4_f32), like the forward encoder convs in conv.hip.
+//
+// Upsampling (k4 s2 p1): output row Y = 2y - 1 + ky, so each output parity
+// class (Y % 2, X % 2) sees exactly 2 x 2 of the 16 taps -- a dense implicit
+// GEMM with K = 4 * cin per class (no zero-inserted input, no wasted MFMA).
+//   py = 0: (y, ky = 1), (y - 1, ky = 3);   py = 1: (y + 1, ky = 0), (y, ky = 2)
+// i.e. tap dy in {0, 1}: iy = y + py - dy, ky = 1 - py + 2 dy.
+#include "conv.h"
+
+#define TBK 32
+#define TLDS (TBK + 8)  // 160-byte rows: conflict-free ds_read_b128 fragments (as conv.hip)
+
+// wq[cls][co][tap][ci] = wt[ci][co][ky][kx], cls = py*2+px, tap = dy*2+dx
+__global__ void k_convT_repack(int cin, int cout, const float* __restrict__ wt, float* __restrict__ wq) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int total = 4 * cout * 4 * cin;
+  if (i >= total) return;
+  const int ci = i % cin;
+  const int tap = (i / cin) & 3;
+  const int co = (i / (4 * cin)) % cout;
+  const int cls = i / (4 * cin * cout);
+  const int py = cls >> 1, px = cls & 1, dy = tap >> 1, dx = tap & 1;
+  const int ky = 1 - py + 2 * dy, kx = 1 - px + 2 * dx;
+  wq[i] = wt[(((long long)ci * cout + co) * 4 + ky) * 4 + kx];
+}
+
+int op_convT_repack(int cin, int cout, const float* wt, float* wq, hipStream_t s) {
+  const int total = 16 * cout * cin;
+  hipLaunchKernelGGL(k_convT_repack, dim3((total + 255) / 256), dim3(256), 0, s, cin, cout, wt, wq);
+  return dr_check_launch("convT_repack");
+}
+
+template <int BM, int BN, int CIN, int EPI, bool SILU_IN>
+__global__ __launch_bounds__(256) void k_convT_nhwc(ConvTArgs a) {
+  constexpr int K = CIN * 4;
+  constexpr int APT = BM / 32;
+  constexpr int BPT = BN >= 32 ? BN / 32 : 1;
+  constexpr int WN = BN >= 32 ? 2 : 1, WM = 4 / WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
+  static_assert(FM >= 1 && FN >= 1, "convT tile too small");
+  static_assert(K % TBK == 0, "cin must be a multiple of 8");
+  __shared__ __attribute__((aligned(16))) float As[2][BM][TLDS];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN][TLDS];
+  __shared__ float red[4];
+
+  const int h = a.h, w = a.w, hw = h * w, cout = a.cout;
+  const long long M = (long long)a.n * hw;
+  const int tiles_n = (cout + BN - 1) / BN;
+  const long long tiles_m = (M + BM - 1) / BM;
+  const int lt = dr_xcd_tile(blockIdx.x, (int)(4 * tiles_m * tiles_n));
+  if (lt < 0) return;
+  const int cls = (int)(lt / (tiles_m * tiles_n));
+  const long long rem = lt - (long long)cls * tiles_m * tiles_n;
+  const long long m0 = (rem / tiles_n) * BM;
+  const int n0 = (int)(rem % tiles_n) * BN;
+  const int py = cls >> 1, px = cls & 1;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int quad = tid & 7, prow = tid >> 3;
+  const float* __restrict__ in = a.in;
+  const float* __restrict__ wq = a.wq + (long long)cls * cout * K;
+
+  long long pbase[APT];
+  int piy[APT], pix[APT];
+  bool pvalid[APT];
+#pragma unroll
+  for (int i = 0; i < APT; ++i) {
+    const long long m = m0 + prow + 32 * i;
+    pvalid[i] = m < M;
+    const long long mm = pvalid[i] ? m : 0;
+    const long long f = mm / hw;
+    const int p = (int)(mm - f * hw);
+    const int y = p / w, x = p - y * w;
+    pbase[i] = f * hw * CIN;
+    piy[i] = y + py;
+    pix[i] = x + px;
+  }
+
+  float4 ra[APT], rb[BPT];
+  auto load = [&](int k0) {
+    const int k = k0 + 4 * quad;
+    const int tap = k / CIN, ci = k - tap * CIN;
+    const int dy = tap >> 1, dx = tap & 1;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const int y = piy[i] - dy, x = pix[i] - dx;
+      if (pvalid[i] && y >= 0 && y < h && x >= 0 && x < w) {
+        float4 v = *reinterpret_cast<const float4*>(in + pbase[i] + ((long long)y * w + x) * CIN + ci);
+        if (SILU_IN) v = make_float4(dr_silu(v.x), dr_silu(v.y), dr_silu(v.z), dr_silu(v.w));
+        ra[i] = v;
+      } else {
+        ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int co = n0 + prow + 32 * i;
+      rb[i] = (co < cout && prow + 32 * i < BN) ? *reinterpret_cast<const float4*>(wq + (long long)co * K + k)
+                                                : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < APT; ++i) *reinterpret_cast<float4*>(&As[buf][prow + 32 * i][4 * quad]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BPT; ++i)
+      if (prow + 32 * i < BN) *reinterpret_cast<float4*>(&Bs[buf][prow + 32 * i][4 * quad]) = rb[i];
+  };
+
+  const int wm0 = (wave / WN) * WTM, wn0 = (wave % WN) * WTN;
+  const int r = lane & 15, q = lane >> 4;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  store(0);
+  __syncthreads();
+  constexpr int NCH = K / TBK;
+  for (int c = 0; c < NCH; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < NCH) load((c + 1) * TBK);
+#pragma unroll
+    for (int s = 0; s < TBK; s += 16) {
+      float4 av[FM], bv[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) av[i] = *reinterpret_cast<const float4*>(&As[buf][wm0 + 16 * i + r][s + 4 * q]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bv[j] = *reinterpret_cast<const float4*>(&Bs[buf][wn0 + 16 * j + r][s + 4 * q]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].x, bv[j].x, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].y, bv[j].y, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].z, bv[j].z, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].w, bv[j].w, acc[i][j], 0, 0, 0);
+    }
+    if (c + 1 < NCH) store(buf ^ 1);
+    dr_lds_barrier();
+  }
+
+  const int OW = 2 * w, OH = 2 * h, ldc = a.ldc;
+  float sq = 0.0f;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long long m = m0 + wm0 + 16 * i + 4 * q + e;
+      if (m >= M) continue;
+      const long long f = m / hw;
+      const int p = (int)(m - f * hw);
+      const int y = p / w, x = p - y * w;
+      const long long opix = (f * OH + 2 * y + py) * OW + 2 * x + px;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int co = n0 + wn0 + 16 * j + r;
+        if (co >= ldc) continue;
+        if (co >= cout) {  // padding channels of a wider output row
+          a.out[opix * ldc + co] = 0.0f;
+          continue;
+        }
+        const float v = acc[i][j][e];
+        if (EPI == CT_EPI_BIAS) {
+          a.out[opix * ldc + co] = v + a.bias[co];
+        } else if (EPI == CT_EPI_DSILU) {
+          a.out[opix * ldc + co] = v * dr_dsilu(a.pre[opix * cout + co]);
+        } else {  // CT_EPI_TANH_MSE (VAE.py:136 Tanh; WorldModel.py:129 squared error)
+          const float mu = tanhf(v + a.bias[co]);
+          const float err = mu - a.target[opix * a.tstride + co];
+          sq += err * err;
+          a.out[opix * ldc + co] = a.coef[f] * err * (1.0f - mu * mu);
+        }
+      }
+    }
+  if (EPI == CT_EPI_TANH_MSE) {
+    // per-tile partial sums of err^2; a tile never straddles two frames
+    // (the launcher checks hw % BM == 0) and there is one channel tile
+    sq = wave_sum(sq);
+    if (lane == 0) red[wave] = sq;
+    __syncthreads();
+    if (tid == 0) {
+      const int per_cls = hw / BM;
+      const long long f = m0 / hw;
+      const int j = (int)((m0 - f * hw) / BM);
+      a.part[f * 4 * per_cls + cls * per_cls + j] = ((red[0] + red[1]) + red[2]) + red[3];
+    }
+  }
+}
+
+int op_convT_mse_parts(int h, int w) { return 4 * (h * w / 128); }
+
+template <int BM, int BN, int CIN, int EPI>
+static int launch_convT(const ConvTArgs& a, hipStream_t s) {
+  const long long M = (long long)a.n * a.h * a.w;
+  const long long tiles = 4 * ((M + BM - 1) / BM) * ((a.cout + BN - 1) / BN);
+  if (tiles >= (1LL << 30)) {
+    dr_set_error("convT: too many tiles");
+    return DR_E_INVALID;
+  }
+  dim3 grid((unsigned)dr_xcd_grid((int)tiles));
+  if (a.silu_in)
+    hipLaunchKernelGGL((k_convT_nhwc<BM, BN, CIN, EPI, true>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_convT_nhwc<BM, BN, CIN, EPI, false>), grid, dim3(256), 0, s, a);
+  return dr_check_launch("convT");
+}
+
+template <int CIN>
+static int convT_cin(int epi, const ConvTArgs& a, hipStream_t s) {
+  if (epi == CT_EPI_TANH_MSE) {
+    if (a.cout > 16 || (a.h * a.w) % 128 != 0 || !a.target || !a.coef || !a.part || !a.bias) {
+      dr_set_error("convT: the tanh/MSE epilogue needs cout <= 16, h*w %% 128 == 0 and target/coef/part/bias");
+      return DR_E_INVALID;
+    }
+    return launch_convT<128, 16, CIN, CT_EPI_TANH_MSE>(a, s);
+  }
+  if (epi == CT_EPI_DSILU) {
+    if (!a.pre || a.ldc != a.cout) {
+      dr_set_error("convT: the SiLU-backward epilogue needs pre and ldc == cout");
+      return DR_E_INVALID;
+    }
+    if (a.cout <= 16) return launch_convT<128, 16, CIN, CT_EPI_DSILU>(a, s);
+    if (a.cout % 64 == 0) return launch_convT<128, 64, CIN, CT_EPI_DSILU>(a, s);
+    return launch_convT<128, 32, CIN, CT_EPI_DSILU>(a, s);
+  }
+  if (!a.bias) {
+    dr_set_error("convT: bias required");
+    return DR_E_INVALID;
+  }
+  if (a.cout <= 16) return launch_convT<128, 16, CIN, CT_EPI_BIAS>(a, s);
+  if (a.cout % 64 == 0) return launch_convT<128, 64, CIN, CT_EPI_BIAS>(a, s);
+  return launch_convT<128, 32, CIN, CT_EPI_BIAS>(a, s);
+}
+
+int op_convT_nhwc(int epi, const ConvTArgs& a, hipStream_t s) {
+  if (a.n <= 0 || !a.in || !a.wq || !a.out || a.ldc < a.cout) {
+    dr_set_error("convT: bad arguments");
+    return DR_E_INVALID;
+  }
+  switch (a.cin) {
+    case 8: return convT_cin<8>(epi, a, s);
+    case 16: return convT_cin<16>(epi, a, s);
+    case 32: return convT_cin<32>(epi, a, s);
+    case 64: return convT_cin<64>(epi, a, s);
+    case 128: return convT_cin<128>(epi, a, s);
+    case 256: return convT_cin<256>(epi, a, s);
+    default: break;
+  }
+  dr_set_error("convT: unsupported input channels %d", a.cin);
+  return DR_E_INVALID;
+}
+
+// ---------------------------------------------------------------------------
+// weight gradient: GEMM [ca] x [16*cb] over K = n*h*w low-res pixels, split-K
+// into deterministic partial planes (no atomics) and one ordered reduction.
+// Column n = tap * cb + b, so a float4 of the hi operand is 4 channels of one
+// tap.  LDS holds both operands pixel-major ([k][m], [k][n]); MFMA step c of a
+// 16-pixel slice takes pixel s + 4q + c on lane group q for A and B alike.
+// ---------------------------------------------------------------------------
+#define WBK 32
+template <int BM>
+__global__ __launch_bounds__(256) void k_conv_wgrad(int n, int h, int w, int ca, int cb, const float* __restrict__ lo,
+                                                    int lda, int lo_silu, const float* __restrict__ hi, int ldb,
+                                                    int nsplit, int chunk, float* __restrict__ part) {
+  constexpr int BN = 64;
+  constexpr int AP = BM + 4, BP = BN + 4;  // row pitch = 4 mod 16 dwords: lane groups q hit distinct banks
+  constexpr int WTM = BM / 2, WTN = BN / 2, FM = WTM / 16, FN = WTN / 16;
+  constexpr int ACOL = BM / 4, AROWS = 256 / ACOL, APT = WBK / AROWS;
+  constexpr int BROWS = 16, BPT = WBK / BROWS;
+  __shared__ __attribute__((aligned(16))) float As[2][WBK][AP];
+  __shared__ __attribute__((aligned(16))) float Bs[2][WBK][BP];
+
+  const int N = 16 * cb;
+  const int tiles_m = (ca + BM - 1) / BM, tiles_n = N / BN;
+  const int tiles = tiles_m * tiles_n;
+  const int split = blockIdx.x / tiles;
+  const int lt = blockIdx.x - split * tiles;
+  const int m0 = (lt / tiles_n) * BM, n0 = (lt % tiles_n) * BN;
+  const long long K = (long long)n * h * w;
+  const long long k_begin = (long long)split * chunk;
+  const long long k_end = k_begin + chunk < K ? k_begin + chunk : K;
+  const int hw = h * w, H2 = 2 * h, W2 = 2 * w;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int acol = tid % ACOL, arow = tid / ACOL;
+  const int bcol = tid % 16, brow = tid / 16;
+  // the 4 hi channels this thread loads: fixed over the K loop
+  const int bn = n0 + 4 * bcol;
+  const int btap = bn / cb, bch = bn - btap * cb;
+  const int bky = btap >> 2, bkx = btap & 3;
+  const int am = m0 + 4 * acol;
+
+  float4 ra[APT], rb[BPT];
+  auto load = [&](long long k0) {
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const long long k = k0 + arow + AROWS * i;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k < k_end && am < ca) {
+        v = *reinterpret_cast<const float4*>(lo + k * lda + am);
+        if (lo_silu) v = make_float4(dr_silu(v.x), dr_silu(v.y), dr_silu(v.z), dr_silu(v.w));
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const long long k = k0 + brow + BROWS * i;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k < k_end) {
+        const long long f = k / hw;
+        const int p = (int)(k - f * hw);
+        const int y = p / w, x = p - y * w;
+        const int Y = 2 * y - 1 + bky, X = 2 * x - 1 + bkx;
+        if (Y >= 0 && Y < H2 && X >= 0 && X < W2)
+          v = *reinterpret_cast<const float4*>(hi + ((f * H2 + Y) * W2 + X) * ldb + bch);
+      }
+      rb[i] = v;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < APT; ++i) *reinterpret_cast<float4*>(&As[buf][arow + AROWS * i][4 * acol]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) *reinterpret_cast<float4*>(&Bs[buf][brow + BROWS * i][4 * bcol]) = rb[i];
+  };
+
+  const int wm0 = (wave >> 1) * WTM, wn0 = (wave & 1) * WTN;
+  const int r = lane & 15, q = lane >> 4;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  if (k_begin < k_end) {
+    load(k_begin);
+    store(0);
+    __syncthreads();
+    const int nch = (int)((k_end - k_begin + WBK - 1) / WBK);
+    for (int c = 0; c < nch; ++c) {
+      const int buf = c & 1;
+      if (c + 1 < nch) load(k_begin + (long long)(c + 1) * WBK);
+#pragma unroll
+      for (int s = 0; s < WBK; s += 16) {
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+          float av[FM], bv[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i) av[i] = As[buf][s + 4 * q + cc][wm0 + 16 * i + r];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) bv[j] = Bs[buf][s + 4 * q + cc][wn0 + 16 * j + r];
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+        }
+      }
+      if (c + 1 < nch) store(buf ^ 1);
+      dr_lds_barrier();
+    }
+  }
+  float* P = part + (long long)split * ca * N;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm0 + 16 * i + 4 * q + e;
+        const int nn = n0 + wn0 + 16 * j + r;
+        if (m < ca) P[(long long)m * N + nn] = acc[i][j][e];
+      }
+}
+
+// dW[a][b][tap] (+)= scale * sum_s part[s][a][tap*cb + b]   (b < cbo)
+__global__ void k_wgrad_reduce(int ca, int cb, int cbo, int nsplit, const float* __restrict__ part,
+                               float* __restrict__ dw, float scale, int accumulate) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over [a][tap][b] (coalesced partial reads)
+  const int N = 16 * cb;
+  if (i >= ca * N) return;
+  const int a = i / N, nn = i - a * N;
+  const int tap = nn / cb, b = nn - tap * cb;
+  if (b >= cbo) return;
+  float s = 0.0f;
+  for (int k = 0; k < nsplit; ++k) s += part[(long long)k * ca * N + i];
+  float* o = dw + ((long long)a * cbo + b) * 16 + tap;
+  *o = accumulate ? *o + scale * s : scale * s;
+}
+
+static void wgrad_plan(int n, int h, int w, int ca, int cb, int& bm, int& nsplit, int& chunk) {
+  bm = ca <= 32 ? 32 : 64;
+  const int tiles = ((ca + bm - 1) / bm) * (16 * cb / 64);
+  const long long K = (long long)n * h * w;
+  const long long kch = (K + WBK - 1) / WBK;
+  long long ns = (2048 + tiles - 1) / tiles;
+  const long long ns_max = (kch + 1) / 2;  // at least 2 chunks per split
+  if (ns > ns_max) ns = ns_max;
+  if (ns < 1) ns = 1;
+  const long long ch = ((kch + ns - 1) / ns) * WBK;
+  chunk = (int)ch;
+  nsplit = (int)((K + ch - 1) / ch);
+}
+
+size_t op_conv_wgrad_ws_floats(int n, int h, int w, int ca, int cb) {
+  int bm, ns, ch;
+  wgrad_plan(n, h, w, ca, cb, bm, ns, ch);
+  return (size_t)ns * ca * 16 * cb;
+}
+
+int op_conv_wgrad(int n, int h, int w, int ca, int cb, const float* lo, int lda, int lo_silu, const float* hi, int ldb,
+                  float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s) {
+  if (n <= 0 || ca % 4 || cb % 4 || lda % 4 || ldb % 4 || lda < ca || ldb < cb || cbo < 1 || cbo > cb || !lo || !hi ||
+      !dw) {
+    dr_set_error("conv_wgrad: bad arguments (channels and strides must be multiples of 4)");
+    return DR_E_INVALID;
+  }
+  int bm, ns, ch;
+  wgrad_plan(n, h, w, ca, cb, bm, ns, ch);
+  if ((size_t)ns * ca * 16 * cb > ws_floats) {
+    dr_set_error("conv_wgrad: workspace too small");
+    return DR_E_WORKSPACE;
+  }
+  const int tiles = ((ca + bm - 1) / bm) * (16 * cb / 64);
+  dim3 grid((unsigned)(tiles * ns));
+  if (bm == 32)
+    hipLaunchKernelGGL(k_conv_wgrad<32>, grid, dim3(256), 0, s, n, h, w, ca, cb, lo, lda, lo_silu, hi, ldb, ns, ch, ws);
+  else
+    hipLaunchKernelGGL(k_conv_wgrad<64>, grid, dim3(256), 0, s, n, h, w, ca, cb, lo, lda, lo_silu, hi, ldb, ns, ch, ws);
+  DR_TRY(dr_check_launch("conv_wgrad"));
+  const int total = ca * 16 * cb;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((total + 255) / 256), dim3(256), 0, s, ca, cb, cbo, ns, ws, dw, scale,
+                     accumulate);
+  return dr_check_launch("wgrad_reduce");
+}
+
+// ---------------------------------------------------------------------------
+// per-channel sums over many rows (bias gradients of the conv layers)
+// ---------------------------------------------------------------------------
+static int chan_pow2(int C) {
+  int p = 1;
+  while (p < C) p <<= 1;
+  return p;
+}
+static int chan_blocks(long long rows, int C) {
+  const int rpp = 256 / chan_pow2(C);
+  long long b = (rows + (long long)rpp * 16 - 1) / ((long long)rpp * 16);
+  return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+}
+
+__global__ __launch_bounds__(256) void k_chan_sum_part(long long rows, int C, int Cp, const float* __restrict__ X,
+                                                       int ldx, long long chunk, float* __restrict__ part) {
+  __shared__ float red[256];
+  const int tid = threadIdx.x;
+  const int c = tid % Cp, rl = tid / Cp, rpp = 256 / Cp;
+  const long long r0 = (long long)blockIdx.x * chunk;
+  const long long r1 = r0 + chunk < rows ? r0 + chunk : rows;
+  float s = 0.0f;
+  if (c < C)
+    for (long long rr = r0 + rl; rr < r1; rr += rpp) s += X[rr * ldx + c];
+  red[tid] = s;
+  __syncthreads();
+  if (tid < Cp) {
+    float t = 0.0f;
+    for (int k = 0; k < rpp; ++k) t += red[k * Cp + tid];
+    if (tid < C) part[(long long)blockIdx.x * C + tid] = t;
+  }
+}
+
+__global__ void k_chan_sum_final(int nb, int C, const float* __restrict__ part, float* __restrict__ out,
+                                 int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.0f;
+  for (int b = 0; b < nb; ++b) s += part[(long long)b * C + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+size_t op_chan_sum_ws_floats(long long rows, int C) { return (size_t)chan_blocks(rows, C) * C; }
+
+int op_chan_sum(long long rows, int C, const float* X, int ldx, float* out, int accumulate, float* ws,
+                size_t ws_floats, hipStream_t s) {
+  if (C <= 0 || C > 256 || rows <= 0 || ldx < C) {
+    dr_set_error("chan_sum: bad arguments");
+    return DR_E_INVALID;
+  }
+  const int nb = chan_blocks(rows, C);
+  if ((size_t)nb * C > ws_floats) {
+    dr_set_error("chan_sum: workspace too small");
+    return DR_E_WORKSPACE;
+  }
+  const long long chunk = (rows + nb - 1) / nb;
+  hipLaunchKernelGGL(k_chan_sum_part, dim3(nb), dim3(256), 0, s, rows, C, chan_pow2(C), X, ldx, chunk, ws);
+  DR_TRY(dr_check_launch("chan_sum_part"));
+  hipLaunchKernelGGL(k_chan_sum_final, dim3((C + 255) / 256), dim3(256), 0, s, nb, C, ws, out, accumulate);
+  return dr_check_launch("chan_sum_final");
+}

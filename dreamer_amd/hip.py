@@ -22,6 +22,16 @@ def mlp3(seq):
     return L.dr_mlp3(linear(seq[0]), linear(seq[1]), linear(seq[3]), linear(seq[4]), linear(seq[6]))
 
 
+def linear_grad(mod):
+    """dr_linear pointing at the .grad tensors of an nn.Linear / LayerNorm / conv."""
+    return L.dr_linear(L.ptr(mod.weight.grad), L.ptr(mod.bias.grad))
+
+
+def mlp3_grad(seq):
+    return L.dr_mlp3(linear_grad(seq[0]), linear_grad(seq[1]), linear_grad(seq[3]), linear_grad(seq[4]),
+                     linear_grad(seq[6]))
+
+
 def flat_linear(flat, offsets, key_w, key_b):
     base = flat.data_ptr()
     return L.dr_linear(base + 4 * offsets[key_w], base + 4 * offsets[key_b])

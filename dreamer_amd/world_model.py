@@ -1,7 +1,8 @@
 """WorldModel with the reference's constructor, attributes and methods
-(WorldModel.py).  imagine_step / observe_step run on libdreamer_hip; the
-training step (SURVEY §8f "next") runs its unroll with the modules' own
-PyTorch-ROCm forward so gradients reach every world-model weight."""
+(WorldModel.py).  imagine_step / observe_step and the whole training step
+(loss, backward, clip_grad_norm_, AdamW: WorldModel.py:148-202) run on
+libdreamer_hip; unroll_model keeps a PyTorch-ROCm autograd version for
+callers that want the reference's intermediate tensors."""
 import torch
 import torch.nn as nn
 
@@ -43,6 +44,8 @@ class WorldModel(nn.Module):
         self.optimiser = torch.optim.AdamW(self.parameters(), lr=WM_lr, betas=(WM_betas[0], WM_betas[1]), eps=WM_eps,
                                            weight_decay=1e-6)
         self.scalar = torch.amp.GradScaler(enabled=self.device.type == "cuda")
+        self._flat = None
+        self.last_losses = None  # device [total, loss_pred, KL_dyn, KL_rep] of the last training_step
 
     # ---- libdreamer_hip packing ---------------------------------------------
     def dims(self, agent=None):
@@ -55,6 +58,9 @@ class WorldModel(nn.Module):
         d.rew_h1, d.rew_h2 = rp[0].out_features, rp[3].out_features
         d.cont_h1, d.cont_h2 = cp[0].out_features, cp[3].out_features
         d.buckets = self.buckets
+        ib = self.decoder.image_builder
+        d.dec_f1, d.dec_f2 = ib[4].out_channels, ib[2].out_channels
+        d.dec_hidden = self.decoder.upscaler[0].out_features
         if agent is not None:
             a, c = agent.actor.base_net, agent.critic.value_net
             d.actor_h1, d.actor_h2 = a[0].out_features, a[3].out_features
@@ -71,6 +77,44 @@ class WorldModel(nn.Module):
         wm.cont = hip.mlp3(self.continue_predictor.logit_generator)
         wm.buckets_rew = L.ptr(self.reward_predictor.buckets_rew)
         return wm
+
+    def packed_decoder(self):
+        dc = self.decoder
+        up, ib = dc.upscaler, dc.image_builder
+        out = L.dr_decoder(hip.linear(up[0]), hip.linear(up[1]), hip.linear(up[3]))
+        for i, j in enumerate((0, 2, 4, 6)):
+            out.convt[i] = hip.linear(ib[j])
+        return out
+
+    def _grad_structs(self):
+        """C structs pointing at the parameters' .grad views (one flat buffer)."""
+        e, g = self.encoder, L.dr_world_model()
+        for i, j in enumerate((0, 2, 4, 6)):
+            g.conv[i] = hip.linear_grad(e.feature_extractor[j])
+        g.map0, g.map1, g.map3 = (hip.linear_grad(e.latent_mapper[j]) for j in (0, 1, 3))
+        gru = self.sequence_model.GRU
+        g.w_ih, g.w_hh, g.b_ih, g.b_hh = (L.ptr(t.grad) for t in (gru.weight_ih, gru.weight_hh, gru.bias_ih,
+                                                                   gru.bias_hh))
+        g.prior = hip.mlp3_grad(self.dynamics_predictor.logit_net)
+        g.reward = hip.mlp3_grad(self.reward_predictor.logit_net)
+        g.cont = hip.mlp3_grad(self.continue_predictor.logit_generator)
+        up, ib = self.decoder.upscaler, self.decoder.image_builder
+        gd = L.dr_decoder(hip.linear_grad(up[0]), hip.linear_grad(up[1]), hip.linear_grad(up[3]))
+        for i, j in enumerate((0, 2, 4, 6)):
+            gd.convt[i] = hip.linear_grad(ib[j])
+        return g, gd
+
+    def _ensure_flat(self):
+        """Parameters as views of one flat buffer, gradients in another, and
+        the optimiser as the fused HIP AdamW over them (same hyper-parameters
+        as the reference's torch.optim.AdamW, WorldModel.py:63-69)."""
+        from .agent import FlatAdamW, _Flat
+        if self._flat is not None and self._flat.intact():
+            return self._flat
+        g = self.optimiser.param_groups[0]
+        self._flat = _Flat(self)
+        self.optimiser = FlatAdamW(self._flat, g["lr"], g["betas"], g["eps"], g["weight_decay"])
+        return self._flat
 
     def params_key(self):
         return tuple(p.data_ptr() for p in self.parameters())
@@ -158,35 +202,63 @@ class WorldModel(nn.Module):
         return prior_logits[:, 1:], post_logits[:, 1:], obs_ll[:, 1:], rew_ll, cont_ll
 
     def training_step(self, observation_sequences, action_sequences, reward_sequences, continue_sequences):
-        """WorldModel.training_step (WorldModel.py:148-202)."""
-        obs = (observation_sequences.float() / 255.0) - 0.5
-        H = self.horizon
-        dev_type = self.device.type
-        with torch.autocast(device_type=dev_type, dtype=torch.float16):
-            prior_l, post_l, obs_ll, rew_ll, cont_ll = self.unroll_model(
-                obs[:, :H], action_sequences[:, :H], reward_sequences[:, :H], continue_sequences[:, :H])
-            mask = continue_sequences[:, :H - 1]
-            obs_ll = obs_ll * mask.squeeze(-1)
-            rew_ll = rew_ll * mask
-            cont_ll = cont_ll * mask
-            Cat = torch.distributions.Categorical
-            kl = torch.distributions.kl.kl_divergence
-            kl_dyn = kl(Cat(logits=post_l.detach().float()), Cat(logits=prior_l.float())).sum(dim=-1)
-            kl_rep = kl(Cat(logits=post_l.float()), Cat(logits=prior_l.detach().float())).sum(dim=-1)
-            kl_dyn = torch.mean(kl_dyn * mask.squeeze(-1))
-            kl_rep = torch.mean(kl_rep * mask.squeeze(-1))
-            denom = mask.sum() + 1e-5
-            loss_pred = (-obs_ll.sum() - rew_ll.sum() + cont_ll.sum()) / denom
-            one = torch.tensor(1.0, device=obs.device)
-            total = self.beta_pred * loss_pred + self.beta_dyn * torch.max(one, kl_dyn) + \
-                self.beta_rep * torch.max(one, kl_rep)
-            if torch.isnan(total) or torch.isinf(total):
-                print("World Model loss is nan or inf, skipping update.")
-                return total
-        self.optimiser.zero_grad()
-        self.scalar.scale(total).backward()
-        self.scalar.unscale_(self.optimiser)
-        nn.utils.clip_grad_norm_(self.parameters(), 100.0)
-        self.scalar.step(self.optimiser)
-        self.scalar.update()
-        return total
+        """WorldModel.training_step (WorldModel.py:148-202) on libdreamer_hip:
+        posterior scan, heads, decoder, losses and the full backward in one
+        launch sequence (dr_wm_train_grads), then clip_grad_norm_(100) and
+        AdamW fused over the flat parameter buffer.  fp32 throughout: the
+        reference's fp16 autocast + GradScaler reduce, in fp32, to the plain
+        backward plus a skipped step when the loss or a gradient is non-finite
+        (the reference prints and returns before its backward, 191-193).
+        Returns the total loss as a 0-d device tensor."""
+        return self.train_step_hip(observation_sequences, action_sequences, reward_sequences, continue_sequences)
+
+    def train_step_hip(self, obs, act, rew, cont, noise_q=None, outputs=None, step=True):
+        """obs (B,S,3,H,W) holding 0..255 (Buffer.sample_sequences), act
+        (B,S,A), rew / cont (B,S,1).  noise_q: explicit Exp(1) draws
+        (T, B*rows, cols) for the posterior samples (parity tests), else
+        Philox.  outputs: optional dict that receives the time-major posterior
+        hiddens / latents / logits.  step=False leaves the parameters alone
+        (gradients only)."""
+        L.require_gpu(obs)
+        dev = obs.device
+        B, S = act.shape[:2]
+        T = self.horizon
+        if S < T or T < 2:
+            raise ValueError(f"training_step needs sequences of at least horizon={T} >= 2 steps (got {S})")
+        Hh, Ww = self.observation_dim_x, self.observation_dim_y
+        A, Hd = self.action_dims, self.hidden_dims
+        R, C = self.latent_num_rows, self.latent_num_columns
+        f = self._ensure_flat()
+        obs = obs.float().contiguous()
+        act = act.float().contiguous()
+        rew = rew.float().reshape(B, S).contiguous()
+        cont = cont.float().reshape(B, S).contiguous()
+        d = self.dims()
+        fr = L.dr_frames(None, 0, None, L.ptr(obs), S * 3 * Hh * Ww, 3 * Hh * Ww, 1, 0)
+        bt = L.dr_wm_batch(L.ptr(act), S * A, A, L.ptr(rew), L.ptr(cont), S, 1)
+        noise = hip.explicit_noise(q=noise_q, device=dev) if noise_q is not None else hip.rng(dev).noise()
+        cfg = L.dr_wm_loss_cfg(self.beta_pred, self.beta_dyn, self.beta_rep)
+        losses = torch.empty(4, device=dev)
+        skip = torch.zeros(1, dtype=torch.int32, device=dev)
+        hid = lat = plog = None
+        if outputs is not None:
+            hid = torch.empty(T, B, Hd, device=dev)
+            lat = torch.empty(T, B, R, C, device=dev)
+            plog = torch.empty(T, B, R, C, device=dev)
+        gw, gd = self._grad_structs()
+        ws = hip.workspace(dev).get("wm_train", L.query("dr_wm_train_workspace_bytes", d, B, T))
+        st = hip.stream()
+        L.call("dr_wm_train_grads", d, self.packed(), self.packed_decoder(), B, T, fr, bt, noise, cfg,
+               L.ptr(losses), L.ptr(skip), gw, gd, L.ptr(hid), L.ptr(lat), L.ptr(plog), L.ptr(ws), ws.numel(), st)
+        if outputs is not None:
+            outputs.update(hiddens=hid, latents=lat, post_logits=plog)
+        if step:
+            # GradScaler semantics: no update when the loss or a gradient is non-finite
+            L.call("dr_nonfinite", f.numel, f.grad.data_ptr(), skip.data_ptr(), st)
+            sq = torch.zeros(1, device=dev)
+            L.call("dr_sqnorm", f.numel, f.grad.data_ptr(), sq.data_ptr(), st)
+            self.optimiser.fused_step(sqnorm=sq, max_norm=100.0, skip=skip)
+            self.last_sqnorm = sq
+        self.last_losses = losses
+        self.last_skip = skip
+        return losses[0]

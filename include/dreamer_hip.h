@@ -55,6 +55,8 @@ typedef struct {
   int prior_h1, prior_h2, rew_h1, rew_h2, cont_h1, cont_h2;
   int actor_h1, actor_h2, critic_h1, critic_h2;
   int buckets;         /* critic_reward_buckets (255) */
+  int dec_f1, dec_f2;  /* decoder_filter_num_1/2 (32, 64): convT channels 4*f2 -> 2*f2 -> f2 -> f1 -> 3 */
+  int dec_hidden;      /* decoder_hidden_layer_nodes (200) */
 } dr_dims;
 
 /* WorldModel parameters (WorldModel.py:55-60). */
@@ -67,6 +69,12 @@ typedef struct {
   dr_mlp3 cont;                   /* continue_predictor.logit_generator */
   float* buckets_rew;             /* reward_predictor.buckets_rew */
 } dr_world_model;
+
+/* Decoder parameters (VariationalAutoEncoder.py:118-137). */
+typedef struct {
+  dr_linear up0, up1, up3;        /* decoder.upscaler.{0, 1 (LN), 3} */
+  dr_linear convt[4];             /* decoder.image_builder.{0,2,4,6}: ConvTranspose2d w [in][out][4][4] */
+} dr_decoder;
 
 /* Actor (Agent.py:174-200): base_net.{0,1,3,4}, mu_head, log_sig_head. */
 typedef struct { dr_linear l0, n1, l3, n4, mu, ls; } dr_actor;
@@ -207,6 +215,33 @@ int dr_ema(long long n, float* target, const float* src, float keep, float tau, 
            hipStream_t stream);
 /* non-finite flag: *flag = any(!isfinite(x[0..n))) (OR-accumulate) */
 int dr_nonfinite(long long n, const float* x, int* flag, hipStream_t stream);
+
+/* ---- a19/a20  world-model training step (WorldModel.training_step,
+ *      WorldModel.py:148-198; unroll_model 84-146; Decoder.forward VAE.py:139-161)
+ * Loss and gradients of one step over a window of T = horizon frames per row:
+ * posterior scan (observe_step with the GRU run from zeros at t = 0), batched
+ * prior / decoder / reward / continue heads on steps 1..T-1, the masked
+ * reconstruction / reward / continue / KL losses with the max(1, KL) free-bit
+ * clamps, and backprop through everything (decoder and encoder convolutions,
+ * the posterior scan's GRU and straight-through samples) into `g_wm` /
+ * `g_dec` (overwrite).  Arithmetic is fp32: the reference's fp16 autocast +
+ * GradScaler is, in fp32, the plain backward (the scaler only skips steps with
+ * non-finite gradients -- `skip` reports a non-finite loss; callers OR in a
+ * gradient check).  losses (device, 4 floats): total, loss_pred, KL_dyn,
+ * KL_rep (both KL means; the free-bit clamp is applied in `total`).
+ * Frames: src frame (b, t) is window step t (time-major f = t*B + b).
+ * Optional outputs (time-major [T][B][...]): posterior hiddens, latents, logits. */
+typedef struct {
+  const float* actions; long long act_sb, act_st;                     /* (b,t,i) at b*sb + t*st + i */
+  const float* rewards; const float* continues; long long rc_sb, rc_st; /* (b,t) at b*sb + t*st */
+} dr_wm_batch;
+typedef struct { float beta_pred, beta_dyn, beta_rep; } dr_wm_loss_cfg;
+size_t dr_wm_train_workspace_bytes(const dr_dims* d, int B, int T);
+int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, const dr_decoder* dec, int B, int T,
+                      const dr_frames* src, const dr_wm_batch* batch, dr_noise noise, dr_wm_loss_cfg cfg,
+                      float* losses, int* skip, const dr_world_model* g_wm, const dr_decoder* g_dec,
+                      float* hiddens_out, float* latents_out, float* post_logits_out, void* ws, size_t ws_bytes,
+                      hipStream_t stream);
 
 /* ---- a1  replay gather (Buffer.sample_sequences, Buffer.py:49-61) --------- */
 int dr_replay_gather(long long cap, int B, int S, int frame_elems, int A, const unsigned char* frames,
