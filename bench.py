@@ -77,6 +77,57 @@ def encoder_flops_per_frame(c):
     return fl + 2 * F * c["encoder_hidden_layer_nodes"]
 
 
+def wm_step_flops(c, B, T):
+    """Algorithmic (dense) FLOPs of one WorldModel.training_step on B windows
+    of T steps: encoder on all B*T frames, posterior scan, prior / reward /
+    continue heads and decoder on the B*(T-1) rows the losses read
+    (WorldModel.py:141-145), backward = 2x forward minus the first conv's
+    (unneeded) input gradient."""
+    Hd, (R, C), A = c["hidden_state_dims"], c["latent_state_dims"], c["action_dims"]
+    L = R * C
+    eh, dh = c["encoder_hidden_layer_nodes"], c["decoder_hidden_layer_nodes"]
+    h, w = c["observation_dims"]
+    M, M1 = B * T, B * (T - 1)
+    f1, f2 = c["decoder_filter_num_1"], c["decoder_filter_num_2"]
+    conv1 = 2 * (h // 2) * (w // 2) * c["encoder_filter_num_1"] * 3 * 16
+    enc = encoder_flops_per_frame(c) * M
+    scan = M * 2 * (3 * Hd * (L + A + Hd) + eh * Hd + L * eh)
+    p1, p2 = c["dyn_pred_hidden_num_nodes_1"], c["dyn_pred_hidden_num_nodes_2"]
+    r1, r2 = c["rew_pred_hidden_num_nodes_1"], c["rew_pred_hidden_num_nodes_2"]
+    q1, q2 = c["cont_pred_hidden_num_nodes_1"], c["cont_pred_hidden_num_nodes_2"]
+    nb = c["critic_reward_buckets"]
+    Fd = 4 * f2 * (h // 16) * (w // 16)
+    heads = 2 * (Hd * p1 + p1 * p2 + p2 * L + (Hd + L) * r1 + r1 * r2 + r2 * nb + (Hd + L) * q1 + q1 * q2 + q2
+                 + (Hd + L) * dh + dh * Fd)
+    chans = [4 * f2, 2 * f2, f2, f1, 3]
+    dec = 0
+    hh, ww = h // 16, w // 16
+    for i in range(4):
+        dec += 2 * hh * ww * chans[i] * chans[i + 1] * 16
+        hh, ww = 2 * hh, 2 * ww
+    fwd = enc + scan + M1 * (heads + dec)
+    return 3 * fwd - conv1 * M
+
+
+def bench_wm(d, B, steps, warmup):
+    """WorldModel.training_step throughput (sequences/s) fed from the device
+    replay ring (Dreamer.train_world_model's unit of work)."""
+    wm = d.world_model
+    for _ in range(warmup):
+        wm.train_step_ring(d.buffer, d.buffer.sample_start_indices(B))
+    torch.cuda.synchronize()
+    st = [d.buffer.sample_start_indices(B) for _ in range(steps)]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for s in st:
+        wm.train_step_ring(d.buffer, s)
+    ev1.record()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return el / steps, ev0.elapsed_time(ev1) / 1e3 / steps, float(wm.last_losses[0])
+
+
 def cpu_baseline(cfg, B, S, H, budget_s=15.0, threads=None):
     """Reference-faithful CPU epoch (oracle restatement of Dreamer.train_Agent:
     warm start with the un-detached graph, dream, train_step with backward into
@@ -152,6 +203,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--phases", action="store_true", help="print per-phase ms to stderr")
+    ap.add_argument("--wm-steps", type=int, default=10, help="world-model training steps timed (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -251,6 +303,22 @@ def main():
                                 "unit": "TFLOP/s", "frac": round(tf / FP32_MFMA_PEAK_TFLOPS, 4),
                                 "mflop_per_imagined_step": mf,
                                 "note": "whole train_Agent epoch, SURVEY §8d necessary FLOPs x imagined steps/s"}
+    if args.wm_steps > 0:
+        wm_s, wm_gpu_s, wm_loss = bench_wm(d, B, args.wm_steps, 2)
+        fl = wm_step_flops(cfg, B, H)
+        ac_s = el / args.steps
+        out["secondary"] = {
+            "wm_step": {"value": round(world * B / wm_s, 1), "unit": "sequences/s", "ms_per_step": round(wm_s * 1e3, 3),
+                        "gpu_ms_per_step": round(wm_gpu_s * 1e3, 3), "B_per_gpu": B, "T": H, "loss": wm_loss,
+                        "mfma_tflops": round(fl / wm_s / 1e12, 2),
+                        "mfma_frac": round(fl / wm_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+                        "algorithmic_gflop": round(fl / 1e9, 2),
+                        "note": "WorldModel.training_step (posterior scan, decoder, losses, full backward, clip, "
+                                "AdamW) from the device replay ring; world-model grads not all-reduced"},
+            "full_iteration": {"value": round(world * B * H / (wm_s + ac_s), 1), "unit": "imagined latent-steps/s",
+                               "ms_per_iteration": round((wm_s + ac_s) * 1e3, 3),
+                               "note": "1 WM step + 1 train_Agent epoch per iteration (WM_epochs = AC_epochs = 1)"},
+        }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(CAR_RACER, B, S, H, budget_s=args.cpu_budget)
     print(json.dumps(out))

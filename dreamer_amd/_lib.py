@@ -103,6 +103,7 @@ _SIGS = {
     "dr_critic_loss_bwd": (_i, [_P(dr_dims), _P(dr_critic), _i, _i, fp, fp, fp, fp, _f, fp, _P(dr_critic),
                                 fp, _sz, fp]),
     "dr_sqnorm": (_i, [_ll, fp, fp, fp]),
+    "dr_sqnorm_multi": (_i, [_ll, fp, fp, fp, fp]),
     "dr_adamw": (_i, [_ll, fp, fp, fp, fp, fp, _f, _f, _f, _f, _f, _f, fp, fp, fp, fp]),
     "dr_ema": (_i, [_ll, fp, fp, _f, _f, fp, fp]),
     "dr_nonfinite": (_i, [_ll, fp, fp, fp]),

@@ -43,6 +43,9 @@ struct ConvTArgs {
 int op_convT_repack(int cin, int cout, const float* wt, float* wq, hipStream_t s);
 int op_convT_nhwc(int epi, const ConvTArgs& a, hipStream_t s);
 int op_convT_mse_parts(int h, int w);  // partial sums per frame written by CT_EPI_TANH_MSE
+// CT_EPI_TANH_MSE runs a direct VALU kernel (cout = 3): wq must come from
+// op_convT_out3_repack ([ci][4 classes][4 taps][3]), out has ldc = 4
+int op_convT_out3_repack(int cin, const float* wt, float* wq, hipStream_t s);
 
 // Weight gradient of a k4 s2 p1 (transposed) convolution:
 //   dW[a][b][ky][kx] (+)= scale * sum_{f,y,x} lo[f][y][x][a] * hi[f][2y-1+ky][2x-1+kx][b]

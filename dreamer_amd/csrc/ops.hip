@@ -793,6 +793,60 @@ extern "C" int dr_sqnorm(long long n, const float* g, float* acc, hipStream_t st
   return dr_check_launch("sqnorm");
 }
 
+// multi-block squared norm for large buffers (world-model gradients, 7.8 M
+// floats): pass 1 writes one partial per block (contiguous chunks, float4
+// loads), pass 2 adds them in a fixed order -- deterministic, no atomics
+#define SQ_BLOCKS 512
+__global__ __launch_bounds__(256) void k_sqnorm_part(long long n4, const float4* __restrict__ g4, long long chunk,
+                                                     float* __restrict__ part) {
+  __shared__ float red[256];
+  const long long b0 = (long long)blockIdx.x * chunk;
+  const long long b1 = b0 + chunk < n4 ? b0 + chunk : n4;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  for (long long i = b0 + threadIdx.x; i < b1; i += 256) {
+    const float4 v = g4[i];
+    s0 += v.x * v.x;
+    s1 += v.y * v.y;
+    s2 += v.z * v.z;
+    s3 += v.w * v.w;
+  }
+  red[threadIdx.x] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(256) void k_sqnorm_final(int nb, const float* __restrict__ part, long long n,
+                                                      long long n4, const float* __restrict__ g, float* acc) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 256) s += part[i];
+  for (long long i = 4 * n4 + threadIdx.x; i < n; i += 256) s += g[i] * g[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *acc = *acc + red[0];
+}
+
+extern "C" int dr_sqnorm_multi(long long n, const float* g, float* acc, float* scratch, hipStream_t stream) {
+  if (((uintptr_t)g & 15) || !scratch) return dr_sqnorm(n, g, acc, stream);
+  const long long n4 = n / 4;
+  long long nb = (n4 + 4095) / 4096;
+  nb = nb < 1 ? 1 : (nb > SQ_BLOCKS ? SQ_BLOCKS : nb);
+  const long long chunk = (n4 + nb - 1) / nb;
+  hipLaunchKernelGGL(k_sqnorm_part, dim3((unsigned)nb), dim3(256), 0, stream, n4,
+                     reinterpret_cast<const float4*>(g), chunk, scratch);
+  DR_TRY(dr_check_launch("sqnorm_part"));
+  hipLaunchKernelGGL(k_sqnorm_final, dim3(1), dim3(256), 0, stream, (int)nb, scratch, n, n4, g, acc);
+  return dr_check_launch("sqnorm_final");
+}
+
 // prelude: step += 1 (unless skipped), bias corrections in double like
 // torch's python scalars (adam.py: bias_correction1 = 1 - beta1**step ...)
 __global__ void k_adamw_prelude(int* step, float* hyper, float lr, float b1, float b2, const int* skip) {

@@ -9,6 +9,8 @@
 // never computed.  The backward mirrors it: batched head backward into dL/dh,
 // dL/dz, then the reverse scan (straight-through sampler, latent_mapper, GRU),
 // then the encoder convolutions over all M frames.
+#include <algorithm>
+
 #include "engine_util.h"
 
 // ---------------------------------------------------------------------------
@@ -211,6 +213,13 @@ __global__ void k_perm_rows(int C, int P, int K, const float* __restrict__ in, f
 
 static int blocks(long long n, int t) { return (int)((n + t - 1) / t); }
 
+// split-K scratch for one launch's problems (disjoint slices of the pool)
+static void splitk_all(GemmArgs* p, int n, float* pool, long long pool_n) {
+  float* cur = pool;
+  long long left = pool_n;
+  for (int i = 0; i < n; ++i) give_splitk(p[i], cur, left);
+}
+
 static int perm_rows(int C, int P, int K, const float* in, float* out, int to_nhwc, hipStream_t s) {
   const long long n = (long long)C * P * K;
   hipLaunchKernelGGL(k_perm_rows, dim3(blocks(n, 256)), dim3(256), 0, s, C, P, K, in, out, to_nhwc);
@@ -253,6 +262,8 @@ struct WmWs {
       *w0tp;
   float *cws;  // conv weight-gradient / channel-sum scratch
   long long cws_n;
+  float* sk;  // split-K partial planes of the tile GEMMs (reused launch to launch)
+  long long sk_n;
 };
 
 struct WmDims {
@@ -359,6 +370,15 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
   w.t_whh = c.f((long long)3 * Hd * Hd); w.w0tp = c.f((long long)D.F * eh);
   w.cws_n = wm_conv_scratch(D);
   w.cws = c.f(w.cws_n);
+  {
+    const long long hd = D.Hd, L = D.L, eh = D.eh;
+    long long mx = splitk_floats(1, L * eh + eh * (D.F + hd) + 3 * hd * (L + D.A) + 3 * hd * hd);
+    mx = std::max(mx, splitk_floats(1, (long long)D.Fd * D.dh + (long long)D.dh * (hd + L)));
+    mx = std::max(mx, splitk_floats(M, std::max(eh, (long long)D.dh)));
+    mx = std::max(mx, splitk_floats(1, (long long)D.nb * D.rh2 + (long long)D.rh2 * D.rh1 + D.rh1 * (hd + L)));
+    w.sk_n = mx;
+    w.sk = c.f(w.sk_n);
+  }
 }
 
 extern "C" size_t dr_wm_train_workspace_bytes(const dr_dims* d, int B, int T) {
@@ -375,7 +395,7 @@ extern "C" size_t dr_wm_train_workspace_bytes(const dr_dims* d, int B, int T) {
 static int head_bwd(const WmDims& D, const dr_mlp3& m, const dr_mlp3& g, int w1, int w2, int nout, const float* glog,
                     const float* t6, const float* t3, const float* t0, const float* x1, const float* x2,
                     const float* pre1, const float* pre2, int in_z, const float* hB, const float* zB, float* gHB,
-                    float* gZB, MlpBwd& b, hipStream_t s) {
+                    float* gZB, MlpBwd& b, float* sk, long long sk_n, hipStream_t s) {
   const int M1 = D.M1, Hd = D.Hd, L = D.L;
   DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M1, w2, nout, glog, nout, t6, b.gx2, w2, 0), s));
   DR_TRY(lnbwd_nt(M1, w1, w2, b.gx2, w2, pre2, w2, m.n4, t3, b.gx1, w1, 0, b.gp2, w2, b.gy2, b.xh2, nullptr, 0,
@@ -389,6 +409,7 @@ static int head_bwd(const WmDims& D, const dr_mlp3& m, const dr_mlp3& g, int w1,
   if (in_z) {
     p[2].W2 = zB; p[2].ldb2 = L; p[2].nsplitB = Hd;
   }
+  splitk_all(p, 3, sk, sk_n);
   DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 3, s));
   ColsumJob cj[7] = {
       {nout, glog, nout, nullptr, 0, g.l6.b}, {w2, b.gp2, w2, nullptr, 0, g.l3.b},
@@ -406,8 +427,7 @@ extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, con
                                  size_t ws_bytes, hipStream_t s) {
   DR_REQUIRE(d && wm && dec && src && bt && losses && gw && gd && B > 0 && T >= 2, "null argument or T < 2");
   DR_REQUIRE(bt->actions && bt->rewards && bt->continues, "window actions / rewards / continues required");
-  DR_REQUIRE(d->img_h % 32 == 0 && d->img_w % 32 == 0 && (d->img_h / 2) * (d->img_w / 2) % 128 == 0,
-             "image size must be a multiple of 32 with (H/2)*(W/2) % 128 == 0");
+  DR_REQUIRE(d->img_h % 16 == 0 && d->img_w % 16 == 0, "image size must be a multiple of 16");
   DR_REQUIRE(d->enc_f1 % 8 == 0 && d->enc_f2 % 8 == 0 && d->dec_f1 % 8 == 0 && d->dec_f2 % 8 == 0,
              "encoder / decoder filter counts must be multiples of 8");
   DR_REQUIRE(d->cols <= 64, "latent classes must be <= 64");
@@ -434,7 +454,8 @@ extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, con
   DR_TRY(op_convT_repack(D.c4, D.c3, wm->conv[3].w, w.wqe4, s));
   const int cin_t[4] = {D.C0, 2 * D.d2, D.d2, D.d1}, cout_t[4] = {2 * D.d2, D.d2, D.d1, 3};
   for (int k = 0; k < 4; ++k) {
-    DR_TRY(op_convT_repack(cin_t[k], cout_t[k], dec->convt[k].w, w.wqd[k], s));
+    if (k < 3) DR_TRY(op_convT_repack(cin_t[k], cout_t[k], dec->convt[k].w, w.wqd[k], s));
+    else DR_TRY(op_convT_out3_repack(cin_t[k], dec->convt[k].w, w.wqd[k], s));
     // ConvTranspose2d data gradient = strided Conv2d with the weight read as [out=ci][in=co]
     DR_TRY(op_conv_repack_pad(cin_t[k], cout_t[k], k == 3 ? 4 : cout_t[k], dec->convt[k].w, w.wrd[k], s));
   }
@@ -474,7 +495,11 @@ extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, con
   DR_TRY(op_conv_nhwc_ex(M, D.c1, IH / 2, IW / 2, D.c2, w.a1, w.wr2, wm->conv[1].b, w.a2, 0, w.pre2, CONV_EPI_FWD, s));
   DR_TRY(op_conv_nhwc_ex(M, D.c2, IH / 4, IW / 4, D.c3, w.a2, w.wr3, wm->conv[2].b, w.a3, 0, w.pre3, CONV_EPI_FWD, s));
   DR_TRY(op_conv_nhwc_ex(M, D.c3, IH / 8, IW / 8, D.c4, w.a3, w.wr4, wm->conv[3].b, w.a4, 1, w.pre4, CONV_EPI_FWD, s));
-  DR_TRY(run(G_NT, AM_PLAIN, lin(M, eh, F, w.a4, F, wm->map0.w, F + Hd, wm->map0.b, w.feat, eh), s));
+  {
+    GemmArgs g = lin(M, eh, F, w.a4, F, wm->map0.w, F + Hd, wm->map0.b, w.feat, eh);
+    splitk_all(&g, 1, w.sk, w.sk_n);
+    DR_TRY(run(G_NT, AM_PLAIN, g, s));
+  }
 
   // ---- posterior scan (unroll_model, WorldModel.py:97-107) ----
   const long long idx_stride = 2LL * B * R;
@@ -578,11 +603,11 @@ extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, con
   DR_TRY(zero(w.gH, (long long)M * Hd, s));
   DR_TRY(zero(w.gZ, (long long)M * L, s));
   DR_TRY(head_bwd(D, wm->prior, gw->prior, D.ph1, D.ph2, L, w.g_prior, w.t_pl6, w.t_pl3, w.t_pl0, w.px1, w.px2, w.pp1,
-                  w.pp2, 0, hB, zB, gHB, gZB, w.bp, s));
+                  w.pp2, 0, hB, zB, gHB, gZB, w.bp, w.sk, w.sk_n, s));
   DR_TRY(head_bwd(D, wm->reward, gw->reward, D.rh1, D.rh2, nb, w.g_rew, w.t_rl6, w.t_rl3, w.t_rl0, w.rx1, w.rx2, w.rp1,
-                  w.rp2, 1, hB, zB, gHB, gZB, w.br, s));
+                  w.rp2, 1, hB, zB, gHB, gZB, w.br, w.sk, w.sk_n, s));
   DR_TRY(head_bwd(D, wm->cont, gw->cont, D.ch1, D.ch2, 1, w.g_cont, w.t_cl6, w.t_cl3, w.t_cl0, w.cx1, w.cx2, w.cp1,
-                  w.cp2, 1, hB, zB, gHB, gZB, w.bc, s));
+                  w.cp2, 1, hB, zB, gHB, gZB, w.bc, w.sk, w.sk_n, s));
   // decoder: image_builder.6 .. .0 (data grads as strided convs, weight grads, bias sums)
   {
     float* gins[4] = {w.dgu2, w.dgq1, w.dgq2, w.dgq3};   // dL/d(pre-activation) of each convT input
@@ -599,7 +624,11 @@ extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, con
     }
   }
   // decoder.upscaler: .3 (permuted rows) then LN-SiLU(.1) and .0 into dL/d[h | z]
-  DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M1, D.dh, D.Fd, w.dgu2, D.Fd, w.t_up3, w.gxu, D.dh, 0), s));
+  {
+    GemmArgs g = bwd_nt(M1, D.dh, D.Fd, w.dgu2, D.Fd, w.t_up3, w.gxu, D.dh, 0);
+    splitk_all(&g, 1, w.sk, w.sk_n);
+    DR_TRY(run(G_NT, AM_PLAIN, g, s));
+  }
   DR_TRY(lnbwd_nt(M1, Hd + L, D.dh, w.gxu, D.dh, w.du1, D.dh, dec->up1, w.t_up0, gHB, Hd, 1, w.gpu, D.dh, w.gyu, w.xhu,
                   gZB, L, Hd, s));
   {
@@ -607,6 +636,7 @@ extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, con
     p[0] = bwd_w(D.Fd, D.dh, M1, w.dgu2, D.Fd, w.dx1, D.dh, w.dw3p);
     p[1] = bwd_w(D.dh, Hd + L, M1, w.gpu, D.dh, hB, Hd, gd->up0.w);
     p[1].W2 = zB; p[1].ldb2 = L; p[1].nsplitB = Hd;
+    splitk_all(p, 2, w.sk, w.sk_n);
     DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 2, s));
     ColsumJob cj[4] = {
         {D.Fd, w.dgu2, D.Fd, nullptr, 0, w.db3p},
@@ -654,6 +684,7 @@ extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, con
     p[2] = bwd_w(3 * Hd, L + A, M1, w.ggi + (long long)B * 3 * Hd, 3 * Hd, w.z_all, L, gw->w_ih);
     p[2].W2 = w.act_tm; p[2].ldb2 = A; p[2].nsplitB = L;
     p[3] = bwd_w(3 * Hd, Hd, M1, w.ggh + (long long)B * 3 * Hd, 3 * Hd, w.h_all, Hd, gw->w_hh);
+    splitk_all(p, 4, w.sk, w.sk_n);
     DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 4, s));
     ColsumJob cj[6] = {
         {L, w.glog, L, nullptr, 0, gw->map3.b},       {eh, w.gpre_m, eh, nullptr, 0, gw->map0.b},

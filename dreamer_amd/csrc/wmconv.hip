@@ -12,6 +12,9 @@
 #include "conv.h"
 
 #define TBK 32
+#define O3_TY 8
+#define O3_TX 32
+int op_convT_mse_parts(int h, int w);
 #define TLDS (TBK + 8)  // 160-byte rows: conflict-free ds_read_b128 fragments (as conv.hip)
 
 // wq[cls][co][tap][ci] = wt[ci][co][ky][kx], cls = py*2+px, tap = dy*2+dx
@@ -201,7 +204,7 @@ __global__ __launch_bounds__(256) void k_convT_nhwc(ConvTArgs a) {
   }
 }
 
-int op_convT_mse_parts(int h, int w) { return 4 * (h * w / 128); }
+int op_convT_mse_parts(int h, int w) { return (h / O3_TY) * ((w + O3_TX - 1) / O3_TX); }
 
 template <int BM, int BN, int CIN, int EPI>
 static int launch_convT(const ConvTArgs& a, hipStream_t s) {
@@ -219,15 +222,140 @@ static int launch_convT(const ConvTArgs& a, hipStream_t s) {
   return dr_check_launch("convT");
 }
 
+// ---------------------------------------------------------------------------
+// The decoder's last layer (ConvTranspose2d(f1 -> 3) + Tanh, VAE.py:135-136)
+// fused with the reconstruction loss (WorldModel.py:129).  Three output
+// channels leave an MFMA tile 3/16 full and make every input pixel a 16-fold
+// re-read, so this layer runs on the VALU instead: a workgroup stages an
+// (8+2) x (32+2) halo patch of the input in LDS once, and each thread owns one
+// input-resolution anchor (y, x) and its 2 x 2 output pixels (all 4 parity
+// classes x 3 channels = 12 accumulators).  Per input channel a thread reads
+// its 9 neighbours from LDS (row pitch cin + 1: conflict-free) and the 48
+// weights of that channel are wave-uniform (scalar loads).
+// ---------------------------------------------------------------------------
+template <int CIN>
+__global__ __launch_bounds__(256) void k_convT_out3(ConvTArgs a) {
+  constexpr int PW = O3_TX + 2, PH = O3_TY + 2, PITCH = CIN + 1;
+  __shared__ float patch[PH * PW * PITCH];
+  __shared__ float red[4];
+  const int h = a.h, w = a.w;
+  const int tiles_x = (w + O3_TX - 1) / O3_TX, tiles_y = h / O3_TY;
+  const int per_frame = tiles_x * tiles_y;
+  const long long f = blockIdx.x / per_frame;
+  const int tile = (int)(blockIdx.x - f * per_frame);
+  const int y0 = (tile / tiles_x) * O3_TY, x0 = (tile % tiles_x) * O3_TX;
+  const int tid = threadIdx.x;
+  const float* __restrict__ in = a.in + f * h * w * CIN;
+  // stage the halo patch (SiLU of the pre-activations; zero outside the image)
+  for (int e = tid; e < PH * PW * (CIN / 4); e += 256) {
+    const int c4 = e % (CIN / 4), pix = e / (CIN / 4);
+    const int py = pix / PW, px = pix - py * PW;
+    const int y = y0 - 1 + py, x = x0 - 1 + px;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (y >= 0 && y < h && x >= 0 && x < w) {
+      v = *reinterpret_cast<const float4*>(in + ((long long)y * w + x) * CIN + 4 * c4);
+      if (a.silu_in) v = make_float4(dr_silu(v.x), dr_silu(v.y), dr_silu(v.z), dr_silu(v.w));
+    }
+    float* d = patch + pix * PITCH + 4 * c4;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  }
+  __syncthreads();
+  const int ty = tid / O3_TX, tx = tid - ty * O3_TX;
+  float acc[4][3];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int o = 0; o < 3; ++o) acc[c][o] = 0.0f;
+  const float* __restrict__ wo = a.wq;  // [ci][cls][tap][co]
+  const float* pb = patch + (ty * PW + tx) * PITCH;
+  for (int ci = 0; ci < CIN; ++ci) {
+    float xv[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) xv[r][c] = pb[(r * PW + c) * PITCH + ci];
+    const float* wc = wo + ci * 48;
+#pragma unroll
+    for (int cls = 0; cls < 4; ++cls) {
+      const int py = cls >> 1, px = cls & 1;
+#pragma unroll
+      for (int tap = 0; tap < 4; ++tap) {
+        const int dy = tap >> 1, dx = tap & 1;
+        const float x = xv[1 + py - dy][1 + px - dx];
+#pragma unroll
+        for (int o = 0; o < 3; ++o) acc[cls][o] = fmaf(x, wc[(cls * 4 + tap) * 3 + o], acc[cls][o]);
+      }
+    }
+  }
+  // epilogue: tanh, squared error vs the target frame, dL/d(pre-tanh)
+  const int y = y0 + ty, x = x0 + tx;
+  float sq = 0.0f;
+  if (y < h && x < w) {
+    const int OW = 2 * w;
+    const float cf = a.coef[f];
+#pragma unroll
+    for (int cls = 0; cls < 4; ++cls) {
+      const int py = cls >> 1, px = cls & 1;
+      const long long opix = (f * 2 * h + 2 * y + py) * OW + 2 * x + px;
+      const float* tg = a.target + opix * a.tstride;
+      float g[3];
+#pragma unroll
+      for (int o = 0; o < 3; ++o) {
+        const float mu = tanhf(acc[cls][o] + a.bias[o]);
+        const float err = mu - tg[o];
+        sq += err * err;
+        g[o] = cf * err * (1.0f - mu * mu);
+      }
+      *reinterpret_cast<float4*>(a.out + opix * 4) = make_float4(g[0], g[1], g[2], 0.0f);
+    }
+  }
+  sq = wave_sum(sq);
+  if ((tid & 63) == 0) red[tid >> 6] = sq;
+  __syncthreads();
+  if (tid == 0) a.part[f * per_frame + tile] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// [cin][3][4][4] -> [ci][cls][tap][co] (48 weights per input channel)
+__global__ void k_convT_out3_repack(int cin, const float* __restrict__ wt, float* __restrict__ wo) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cin * 48) return;
+  const int ci = i / 48, r = i - ci * 48;
+  const int ct = r / 3, co = r - ct * 3;
+  const int cls = ct >> 2, tap = ct & 3;
+  const int py = cls >> 1, px = cls & 1, dy = tap >> 1, dx = tap & 1;
+  const int ky = 1 - py + 2 * dy, kx = 1 - px + 2 * dx;
+  wo[i] = wt[(((long long)ci * 3 + co) * 4 + ky) * 4 + kx];
+}
+
+int op_convT_out3_repack(int cin, const float* wt, float* wo, hipStream_t s) {
+  hipLaunchKernelGGL(k_convT_out3_repack, dim3((cin * 48 + 255) / 256), dim3(256), 0, s, cin, wt, wo);
+  return dr_check_launch("convT_out3_repack");
+}
+
+int op_convT_out3(const ConvTArgs& a, hipStream_t s) {
+  if (a.cout != 3 || a.ldc != 4 || a.tstride < 3 || a.h % O3_TY != 0 || !a.target || !a.coef || !a.part || !a.bias ||
+      !a.in || !a.wq || !a.out) {
+    dr_set_error("convT_out3: needs cout 3, ldc 4, h %% 8 == 0 and target/coef/part/bias");
+    return DR_E_INVALID;
+  }
+  const long long blocks = (long long)a.n * op_convT_mse_parts(a.h, a.w);
+  if (blocks >= (1LL << 31)) {
+    dr_set_error("convT_out3: too many frames");
+    return DR_E_INVALID;
+  }
+  switch (a.cin) {
+    case 8: hipLaunchKernelGGL(k_convT_out3<8>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+    case 16: hipLaunchKernelGGL(k_convT_out3<16>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+    case 32: hipLaunchKernelGGL(k_convT_out3<32>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+    case 64: hipLaunchKernelGGL(k_convT_out3<64>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+    default: dr_set_error("convT_out3: unsupported input channels %d", a.cin); return DR_E_INVALID;
+  }
+  return dr_check_launch("convT_out3");
+}
+
 template <int CIN>
 static int convT_cin(int epi, const ConvTArgs& a, hipStream_t s) {
-  if (epi == CT_EPI_TANH_MSE) {
-    if (a.cout > 16 || (a.h * a.w) % 128 != 0 || !a.target || !a.coef || !a.part || !a.bias) {
-      dr_set_error("convT: the tanh/MSE epilogue needs cout <= 16, h*w %% 128 == 0 and target/coef/part/bias");
-      return DR_E_INVALID;
-    }
-    return launch_convT<128, 16, CIN, CT_EPI_TANH_MSE>(a, s);
-  }
+  if (epi == CT_EPI_TANH_MSE) return op_convT_out3(a, s);
   if (epi == CT_EPI_DSILU) {
     if (!a.pre || a.ldc != a.cout) {
       dr_set_error("convT: the SiLU-backward epilogue needs pre and ldc == cout");
@@ -386,18 +514,32 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(int n, int h, int w, int ca,
 }
 
 // dW[a][b][tap] (+)= scale * sum_s part[s][a][tap*cb + b]   (b < cbo)
-__global__ void k_wgrad_reduce(int ca, int cb, int cbo, int nsplit, const float* __restrict__ part,
-                               float* __restrict__ dw, float scale, int accumulate) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // over [a][tap][b] (coalesced partial reads)
+// 64 consecutive outputs per workgroup, 16 split-lanes per output (coalesced
+// 256-byte partial rows), fixed-order combine in LDS
+__global__ __launch_bounds__(1024) void k_wgrad_reduce(int ca, int cb, int cbo, int nsplit,
+                                                       const float* __restrict__ part, float* __restrict__ dw,
+                                                       float scale, int accumulate) {
+  __shared__ float red[16][65];
   const int N = 16 * cb;
-  if (i >= ca * N) return;
-  const int a = i / N, nn = i - a * N;
-  const int tap = nn / cb, b = nn - tap * cb;
-  if (b >= cbo) return;
+  const long long total = (long long)ca * N;
+  const int lo = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const long long i = (long long)blockIdx.x * 64 + lo;
   float s = 0.0f;
-  for (int k = 0; k < nsplit; ++k) s += part[(long long)k * ca * N + i];
-  float* o = dw + ((long long)a * cbo + b) * 16 + tap;
-  *o = accumulate ? *o + scale * s : scale * s;
+  if (i < total)
+    for (int k = sl; k < nsplit; k += 16) s += part[(long long)k * total + i];
+  red[sl][lo] = s;
+  __syncthreads();
+  if (sl == 0 && i < total) {
+    float t = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][lo];
+    const int a = (int)(i / N), nn = (int)(i - (long long)a * N);
+    const int tap = nn / cb, b = nn - tap * cb;
+    if (b < cbo) {
+      float* o = dw + ((long long)a * cbo + b) * 16 + tap;
+      *o = accumulate ? *o + scale * t : scale * t;
+    }
+  }
 }
 
 static void wgrad_plan(int n, int h, int w, int ca, int cb, int& bm, int& nsplit, int& chunk) {
@@ -405,7 +547,7 @@ static void wgrad_plan(int n, int h, int w, int ca, int cb, int& bm, int& nsplit
   const int tiles = ((ca + bm - 1) / bm) * (16 * cb / 64);
   const long long K = (long long)n * h * w;
   const long long kch = (K + WBK - 1) / WBK;
-  long long ns = (2048 + tiles - 1) / tiles;
+  long long ns = (1024 + tiles - 1) / tiles;  // about 4 workgroups per CU
   const long long ns_max = (kch + 1) / 2;  // at least 2 chunks per split
   if (ns > ns_max) ns = ns_max;
   if (ns < 1) ns = 1;
@@ -441,7 +583,7 @@ int op_conv_wgrad(int n, int h, int w, int ca, int cb, const float* lo, int lda,
     hipLaunchKernelGGL(k_conv_wgrad<64>, grid, dim3(256), 0, s, n, h, w, ca, cb, lo, lda, lo_silu, hi, ldb, ns, ch, ws);
   DR_TRY(dr_check_launch("conv_wgrad"));
   const int total = ca * 16 * cb;
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3((total + 255) / 256), dim3(256), 0, s, ca, cb, cbo, ns, ws, dw, scale,
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((total + 63) / 64), dim3(1024), 0, s, ca, cb, cbo, ns, ws, dw, scale,
                      accumulate);
   return dr_check_launch("wgrad_reduce");
 }
@@ -479,13 +621,20 @@ __global__ __launch_bounds__(256) void k_chan_sum_part(long long rows, int C, in
   }
 }
 
-__global__ void k_chan_sum_final(int nb, int C, const float* __restrict__ part, float* __restrict__ out,
-                                 int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// one workgroup per channel: strided partial sums, then a fixed-order tree
+__global__ __launch_bounds__(256) void k_chan_sum_final(int nb, int C, const float* __restrict__ part,
+                                                        float* __restrict__ out, int accumulate) {
+  __shared__ float red[256];
+  const int c = blockIdx.x;
   float s = 0.0f;
-  for (int b = 0; b < nb; ++b) s += part[(long long)b * C + c];
-  out[c] = accumulate ? out[c] + s : s;
+  for (int b = threadIdx.x; b < nb; b += 256) s += part[(long long)b * C + c];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[c] = accumulate ? out[c] + red[0] : red[0];
 }
 
 size_t op_chan_sum_ws_floats(long long rows, int C) { return (size_t)chan_blocks(rows, C) * C; }
@@ -504,6 +653,6 @@ int op_chan_sum(long long rows, int C, const float* X, int ldx, float* out, int 
   const long long chunk = (rows + nb - 1) / nb;
   hipLaunchKernelGGL(k_chan_sum_part, dim3(nb), dim3(256), 0, s, rows, C, chan_pow2(C), X, ldx, chunk, ws);
   DR_TRY(dr_check_launch("chan_sum_part"));
-  hipLaunchKernelGGL(k_chan_sum_final, dim3((C + 255) / 256), dim3(256), 0, s, nb, C, ws, out, accumulate);
+  hipLaunchKernelGGL(k_chan_sum_final, dim3(C), dim3(256), 0, s, nb, C, ws, out, accumulate);
   return dr_check_launch("chan_sum_final");
 }

@@ -181,8 +181,13 @@ class Dreamer(nn.Module):
     def train_world_model(self):  # Dreamer.py:228-242
         out = []
         for _ in tqdm(range(self.WM_epochs), desc="Training World Model On Buffer Data", leave=False):
-            obs, act, rew, cont, _ = self.buffer.sample_sequences(batch_size=self.batch_size)
-            out.append(self.world_model.training_step(obs, act, rew, cont))
+            if self.device.type == "cuda":
+                # same np.random draws as sample_sequences; frames stay u8 in HBM
+                starts = self.buffer.sample_start_indices(self.batch_size)
+                out.append(self.world_model.train_step_ring(self.buffer, starts))
+            else:
+                obs, act, rew, cont, _ = self.buffer.sample_sequences(batch_size=self.batch_size)
+                out.append(self.world_model.training_step(obs, act, rew, cont))
         return out
 
     def load_pretrained_dreamer(self, path):

@@ -3,6 +3,7 @@
 (loss, backward, clip_grad_norm_, AdamW: WorldModel.py:148-202) run on
 libdreamer_hip; unroll_model keeps a PyTorch-ROCm autograd version for
 callers that want the reference's intermediate tensors."""
+import numpy as np
 import torch
 import torch.nn as nn
 
@@ -220,26 +221,52 @@ class WorldModel(nn.Module):
         hiddens / latents / logits.  step=False leaves the parameters alone
         (gradients only)."""
         L.require_gpu(obs)
-        dev = obs.device
         B, S = act.shape[:2]
-        T = self.horizon
-        if S < T or T < 2:
-            raise ValueError(f"training_step needs sequences of at least horizon={T} >= 2 steps (got {S})")
-        Hh, Ww = self.observation_dim_x, self.observation_dim_y
-        A, Hd = self.action_dims, self.hidden_dims
-        R, C = self.latent_num_rows, self.latent_num_columns
-        f = self._ensure_flat()
+        Hh, Ww, A = self.observation_dim_x, self.observation_dim_y, self.action_dims
         obs = obs.float().contiguous()
         act = act.float().contiguous()
         rew = rew.float().reshape(B, S).contiguous()
         cont = cont.float().reshape(B, S).contiguous()
-        d = self.dims()
         fr = L.dr_frames(None, 0, None, L.ptr(obs), S * 3 * Hh * Ww, 3 * Hh * Ww, 1, 0)
         bt = L.dr_wm_batch(L.ptr(act), S * A, A, L.ptr(rew), L.ptr(cont), S, 1)
+        return self._train(fr, bt, B, S, obs.device, noise_q, outputs, step)
+
+    def train_step_ring(self, buffer, starts, noise_q=None, outputs=None, step=True):
+        """The same step fed straight from the device replay ring: frames are
+        read as u8 by the first conv's loader, actions / rewards / continues
+        gathered for the first `horizon` steps of each window (no float32
+        observation tensor is materialised, Buffer.py:58-61)."""
+        dev = buffer.device
+        B, T = len(starts), self.horizon
+        st = torch.as_tensor(np.asarray(starts), dtype=torch.int64).to(dev, non_blocking=True) \
+            if not isinstance(starts, torch.Tensor) else starts
+        win = self._win.get((B, T)) if hasattr(self, "_win") else None
+        if win is None:
+            self._win = getattr(self, "_win", {})
+            win = self._win[(B, T)] = (torch.empty(B, T, self.action_dims, device=dev), torch.empty(B, T, device=dev),
+                                       torch.empty(B, T, device=dev))
+        act, rew, cont = win
+        m = buffer._mirror()
+        L.call("dr_replay_gather", buffer.capacity, B, T, 0, self.action_dims, None, L.ptr(m["actions"]),
+               L.ptr(m["rewards"]), L.ptr(m["continues"]), L.ptr(st), None, L.ptr(act), L.ptr(rew), L.ptr(cont),
+               hip.stream())
+        fr = buffer.frames_struct(st)
+        bt = L.dr_wm_batch(L.ptr(act), T * self.action_dims, self.action_dims, L.ptr(rew), L.ptr(cont), T, 1)
+        return self._train(fr, bt, B, T, dev, noise_q, outputs, step)
+
+    def _train(self, fr, bt, B, S, dev, noise_q, outputs, step):
+        T = self.horizon
+        if S < T or T < 2:
+            raise ValueError(f"training_step needs sequences of at least horizon={T} >= 2 steps (got {S})")
+        Hd, R, C = self.hidden_dims, self.latent_num_rows, self.latent_num_columns
+        f = self._ensure_flat()
+        d = self.dims()
         noise = hip.explicit_noise(q=noise_q, device=dev) if noise_q is not None else hip.rng(dev).noise()
         cfg = L.dr_wm_loss_cfg(self.beta_pred, self.beta_dyn, self.beta_rep)
-        losses = torch.empty(4, device=dev)
-        skip = torch.zeros(1, dtype=torch.int32, device=dev)
+        if getattr(self, "_scratch", None) is None or self._scratch[0].device != torch.device(dev):
+            self._scratch = (torch.empty(4, device=dev), torch.zeros(1, dtype=torch.int32, device=dev),
+                             torch.zeros(1, device=dev), torch.empty(512, device=dev))
+        losses, skip, sq, sq_part = self._scratch
         hid = lat = plog = None
         if outputs is not None:
             hid = torch.empty(T, B, Hd, device=dev)
@@ -255,10 +282,8 @@ class WorldModel(nn.Module):
         if step:
             # GradScaler semantics: no update when the loss or a gradient is non-finite
             L.call("dr_nonfinite", f.numel, f.grad.data_ptr(), skip.data_ptr(), st)
-            sq = torch.zeros(1, device=dev)
-            L.call("dr_sqnorm", f.numel, f.grad.data_ptr(), sq.data_ptr(), st)
+            sq.zero_()
+            L.call("dr_sqnorm_multi", f.numel, f.grad.data_ptr(), sq.data_ptr(), sq_part.data_ptr(), st)
             self.optimiser.fused_step(sqnorm=sq, max_norm=100.0, skip=skip)
-            self.last_sqnorm = sq
-        self.last_losses = losses
-        self.last_skip = skip
-        return losses[0]
+        self.last_losses, self.last_skip, self.last_sqnorm = losses, skip, sq
+        return losses[0].clone()

@@ -202,6 +202,8 @@ int dr_critic_loss_bwd(const dr_dims* d, const dr_critic* c, int B, int H, const
 
 /* ---- optimiser (torch.optim.AdamW + clip_grad_norm_ + soft target) -------- */
 int dr_sqnorm(long long n, const float* g, float* acc, hipStream_t stream);
+/* as dr_sqnorm, many workgroups (large buffers); scratch >= 512 floats */
+int dr_sqnorm_multi(long long n, const float* g, float* acc, float* scratch, hipStream_t stream);
 /* p <- AdamW(p, g*clip) (torch.optim.AdamW single-tensor op order) where
  * clip = min(1, max_norm/(sqrt(*sqnorm)+1e-6)) (sqnorm NULL: no clip).  The
  * step counter lives on the device: a prelude increments *step and writes
