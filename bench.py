@@ -230,6 +230,8 @@ def main():
     d.buffer._mirror()
     eng = ImaginationEngine(d, B=B, world=(rank, world, group) if world > 1 else None)
     d._engine = eng
+    if world > 1:
+        d.world_model.set_data_parallel(rank, world, group)
     np.random.seed(1000 + rank)
 
     def barrier():
@@ -314,7 +316,8 @@ def main():
                         "mfma_frac": round(fl / wm_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
                         "algorithmic_gflop": round(fl / 1e9, 2),
                         "note": "WorldModel.training_step (posterior scan, decoder, losses, full backward, clip, "
-                                "AdamW) from the device replay ring; world-model grads not all-reduced"},
+                                "AdamW) from the device replay ring; under DP the mask / loss sums and the flat "
+                                "gradient are all-reduced (RCCL)"},
             "full_iteration": {"value": round(world * B * H / (wm_s + ac_s), 1), "unit": "imagined latent-steps/s",
                                "ms_per_iteration": round((wm_s + ac_s) * 1e3, 3),
                                "note": "1 WM step + 1 train_Agent epoch per iteration (WM_epochs = AC_epochs = 1)"},

@@ -42,14 +42,21 @@ __device__ float block_sum256(float v, float* red) {
 
 // mask = continues[:, :T-1] (WorldModel.py:170); row i < M1 of every head /
 // decoder frame is (t = i/B + 1, b) and its mask is cont_tm[i].
-// scal[0] = mask.sum() + 1e-5 (185); coef_row = beta_pred * mask / denom (the
-// factor of every prediction-loss gradient); coef_obs = 2 * coef_row.
-__global__ __launch_bounds__(256) void k_wm_prep(int M1, const float* cont_tm, float beta_pred, float* scal,
-                                                 float* coef_row, float* coef_obs) {
+// stats[0] = local mask.sum() (all-reduced by a data-parallel caller)
+__global__ __launch_bounds__(256) void k_wm_masksum(int M1, const float* cont_tm, float* stats) {
   __shared__ float red[256];
   float s = 0.0f;
   for (int i = threadIdx.x; i < M1; i += 256) s += cont_tm[i];
-  const float denom = block_sum256(s, red) + 1e-5f;
+  s = block_sum256(s, red);
+  if (threadIdx.x == 0) stats[0] = s;
+}
+
+// scal[0] = mask.sum() + 1e-5 (WorldModel.py:185, global); coef_row =
+// beta_pred * mask / denom (the factor of every prediction-loss gradient);
+// coef_obs = 2 * coef_row
+__global__ __launch_bounds__(256) void k_wm_coef(int M1, const float* cont_tm, float beta_pred, const float* stats,
+                                                 float* scal, float* coef_row, float* coef_obs) {
+  const float denom = stats[0] + 1e-5f;
   if (threadIdx.x == 0) scal[0] = denom;
   for (int i = threadIdx.x; i < M1; i += 256) {
     const float c = beta_pred * cont_tm[i] / denom;
@@ -133,13 +140,13 @@ __global__ __launch_bounds__(256) void k_wm_heads(int M1, int nb, const float* _
   }
 }
 
-// losses (WorldModel.py:170-189) and the KL-gradient factors of the free-bit
-// clamp max(1, KL): d max(1, k)/dk = 1 (k > 1), 1/2 (k == 1), 0 (k < 1)
-__global__ __launch_bounds__(256) void k_wm_final(int M1, int R, int nparts, const float* __restrict__ obs_part,
+// local masked sums of the loss terms: stats[1..4] = sum mask * (squared
+// error, reward log-lik, continue BCE, KL) over this rank's rows
+__global__ __launch_bounds__(256) void k_wm_stats(int M1, int R, int nparts, const float* __restrict__ obs_part,
                                                   const float* __restrict__ rew_row,
                                                   const float* __restrict__ cont_row,
                                                   const float* __restrict__ kl_grp, const float* __restrict__ cont_tm,
-                                                  dr_wm_loss_cfg cfg, float* scal, float* losses, int* skip) {
+                                                  float* stats) {
   __shared__ float red[256];
   float so = 0.f, sr = 0.f, sc = 0.f, sk = 0.f;
   for (int i = threadIdx.x; i < M1; i += 256) {
@@ -158,19 +165,30 @@ __global__ __launch_bounds__(256) void k_wm_final(int M1, int R, int nparts, con
   sc = block_sum256(sc, red);
   sk = block_sum256(sk, red);
   if (threadIdx.x == 0) {
-    const float denom = scal[0];
-    const float pred = (so - sr + sc) / denom;
-    const float kl = sk / (float)M1;
-    const float total = cfg.beta_pred * pred + cfg.beta_dyn * fmaxf(1.0f, kl) + cfg.beta_rep * fmaxf(1.0f, kl);
-    const float wk = kl > 1.0f ? 1.0f : (kl == 1.0f ? 0.5f : 0.0f);
-    scal[1] = cfg.beta_dyn * wk / (float)M1;
-    scal[2] = cfg.beta_rep * wk / (float)M1;
-    losses[0] = total;
-    losses[1] = pred;
-    losses[2] = kl;
-    losses[3] = kl;
-    if (skip) *skip = isfinite(total) ? 0 : 1;
+    stats[1] = so;
+    stats[2] = sr;
+    stats[3] = sc;
+    stats[4] = sk;
   }
+}
+
+// losses (WorldModel.py:170-189) from the (global) sums and the KL-gradient
+// factors of the free-bit clamp max(1, KL): d max(1, k)/dk = 1 (k > 1),
+// 1/2 (k == 1), 0 (k < 1).  rows = B_global * (T - 1) (torch.mean's count).
+__global__ void k_wm_final(const float* stats, int rows, dr_wm_loss_cfg cfg, float* scal, float* losses, int* skip) {
+  if (threadIdx.x != 0) return;
+  const float denom = stats[0] + 1e-5f;
+  const float pred = (stats[1] - stats[2] + stats[3]) / denom;
+  const float kl = stats[4] / (float)rows;
+  const float total = cfg.beta_pred * pred + cfg.beta_dyn * fmaxf(1.0f, kl) + cfg.beta_rep * fmaxf(1.0f, kl);
+  const float wk = kl > 1.0f ? 1.0f : (kl == 1.0f ? 0.5f : 0.0f);
+  scal[1] = cfg.beta_dyn * wk / (float)rows;
+  scal[2] = cfg.beta_rep * wk / (float)rows;
+  losses[0] = total;
+  losses[1] = pred;
+  losses[2] = kl;
+  losses[3] = kl;
+  if (skip) *skip = isfinite(total) ? 0 : 1;
 }
 
 // gl = 0.99 * softmax-backward(gz) (+ extra): the straight-through sampler's
@@ -250,7 +268,7 @@ struct WmWs {
   float *pp1, *px1, *pp2, *px2, *prior_lg, *rp1, *rx1, *rp2, *rx2, *rew_lg, *cp1, *cx1, *cp2, *cx2, *cont_lg;
   float *du1, *dx1, *du2, *dq1, *dq2, *dq3, *dg4, *w3p, *b3p, *wqd[4], *wrd[4];
   // loss
-  float *coef_row, *coef_obs, *obs_part, *kl_grp, *rew_row, *cont_row, *scal;
+  float *coef_row, *coef_obs, *obs_part, *kl_grp, *rew_row, *cont_row, *scal, *stats;
   // backward
   float *gH, *gZ, *glog, *gpost, *g_prior, *g_rew, *g_cont;
   MlpBwd bp, br, bc;
@@ -347,7 +365,7 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
   }
   w.coef_row = c.f(M1); w.coef_obs = c.f(M1);
   w.obs_part = c.f(M1 * op_convT_mse_parts(D.IH / 2, D.IW / 2));
-  w.kl_grp = c.f(M1 * d->rows); w.rew_row = c.f(M1); w.cont_row = c.f(M1); w.scal = c.f(8);
+  w.kl_grp = c.f(M1 * d->rows); w.rew_row = c.f(M1); w.cont_row = c.f(M1); w.scal = c.f(8); w.stats = c.f(8);
   w.gH = c.f(M * Hd); w.gZ = c.f(M * L); w.glog = c.f(M * L); w.gpost = c.f(M1 * L);
   w.g_prior = c.f(M1 * L); w.g_rew = c.f(M1 * D.nb); w.g_cont = c.f(M1);
   mlp_bwd_carve(c, M1, D.ph1, D.ph2, w.bp);
@@ -420,12 +438,12 @@ static int head_bwd(const WmDims& D, const dr_mlp3& m, const dr_mlp3& g, int w1,
   return op_colsum_multi(M1, cj, 7, s);
 }
 
-extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, const dr_decoder* dec, int B, int T,
-                                 const dr_frames* src, const dr_wm_batch* bt, dr_noise noise, dr_wm_loss_cfg cfg,
-                                 float* losses, int* skip, const dr_world_model* gw, const dr_decoder* gd,
-                                 float* hiddens_out, float* latents_out, float* post_logits_out, void* ws,
-                                 size_t ws_bytes, hipStream_t s) {
-  DR_REQUIRE(d && wm && dec && src && bt && losses && gw && gd && B > 0 && T >= 2, "null argument or T < 2");
+static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const dr_decoder* dec, int B, int T,
+                  const dr_frames* src, const dr_wm_batch* bt, dr_noise noise, dr_wm_loss_cfg cfg, float* stats,
+                  int rows_global, float* losses, int* skip, const dr_world_model* gw, const dr_decoder* gd,
+                  float* hiddens_out, float* latents_out, float* post_logits_out, void* ws, size_t ws_bytes,
+                  hipStream_t s) {
+  DR_REQUIRE(d && wm && dec && src && bt && losses && gw && gd && stats && B > 0 && T >= 2, "null argument or T < 2");
   DR_REQUIRE(bt->actions && bt->rewards && bt->continues, "window actions / rewards / continues required");
   DR_REQUIRE(d->img_h % 16 == 0 && d->img_w % 16 == 0, "image size must be a multiple of 16");
   DR_REQUIRE(d->enc_f1 % 8 == 0 && d->enc_f2 % 8 == 0 && d->dec_f1 % 8 == 0 && d->dec_f2 % 8 == 0,
@@ -443,6 +461,9 @@ extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, con
   float* gHB = w.gH + (long long)B * Hd;
   float* gZB = w.gZ + (long long)B * L;
 
+  const int cin_t[4] = {D.C0, 2 * D.d2, D.d2, D.d1}, cout_t[4] = {2 * D.d2, D.d2, D.d1, 3};
+  if (rows_global <= 0) rows_global = M1;
+  if (phases & DR_WM_PREP) {
   // ---- weights: repacks, transposes, permutations (fixed for the call) ----
   DR_TRY(op_conv_repack_pad(D.c1, 3, 4, wm->conv[0].w, w.wr1, s));
   DR_TRY(op_conv_repack_pad(D.c2, D.c1, D.c1, wm->conv[1].w, w.wr2, s));
@@ -452,7 +473,6 @@ extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, con
   DR_TRY(op_convT_repack(D.c2, D.c1, wm->conv[1].w, w.wqe2, s));
   DR_TRY(op_convT_repack(D.c3, D.c2, wm->conv[2].w, w.wqe3, s));
   DR_TRY(op_convT_repack(D.c4, D.c3, wm->conv[3].w, w.wqe4, s));
-  const int cin_t[4] = {D.C0, 2 * D.d2, D.d2, D.d1}, cout_t[4] = {2 * D.d2, D.d2, D.d1, 3};
   for (int k = 0; k < 4; ++k) {
     if (k < 3) DR_TRY(op_convT_repack(cin_t[k], cout_t[k], dec->convt[k].w, w.wqd[k], s));
     else DR_TRY(op_convT_out3_repack(cin_t[k], dec->convt[k].w, w.wqd[k], s));
@@ -485,9 +505,14 @@ extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, con
   hipLaunchKernelGGL(k_wm_gather, dim3(blocks(M, 256)), dim3(256), 0, s, B, T, A, *bt, w.act_tm, w.rew_tm, w.cont_tm);
   DR_TRY(dr_check_launch("wm_gather"));
   DR_TRY(zero(w.zeros, (long long)B * (L + A + Hd), s));
-  hipLaunchKernelGGL(k_wm_prep, dim3(1), dim3(256), 0, s, M1, w.cont_tm, cfg.beta_pred, w.scal, w.coef_row,
+  hipLaunchKernelGGL(k_wm_masksum, dim3(1), dim3(256), 0, s, M1, w.cont_tm, stats);
+  DR_TRY(dr_check_launch("wm_masksum"));
+  }  // DR_WM_PREP
+
+  if (phases & DR_WM_FWD) {
+  hipLaunchKernelGGL(k_wm_coef, dim3(1), dim3(256), 0, s, M1, w.cont_tm, cfg.beta_pred, stats, w.scal, w.coef_row,
                      w.coef_obs);
-  DR_TRY(dr_check_launch("wm_prep"));
+  DR_TRY(dr_check_launch("wm_coef"));
 
   // ---- encoder over all M frames (VAE.py:57-75), activations kept ----
   DR_TRY(op_frames_nhwc4(M, B, IH, IW, src, w.x0, s));
@@ -591,8 +616,21 @@ extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, con
     hipLaunchKernelGGL(k_wm_heads, dim3(blocks(M1, 4)), dim3(256), 0, s, M1, nb, w.rew_lg, w.cont_lg, w.rew_tm,
                        w.cont_tm, wm->buckets_rew, w.coef_row, w.rew_row, w.cont_row, w.g_rew, w.g_cont);
     DR_TRY(dr_check_launch("wm_heads"));
-    hipLaunchKernelGGL(k_wm_final, dim3(1), dim3(256), 0, s, M1, R, op_convT_mse_parts(IH / 2, IW / 2), w.obs_part,
-                       w.rew_row, w.cont_row, w.kl_grp, w.cont_tm, cfg, w.scal, losses, skip);
+    hipLaunchKernelGGL(k_wm_stats, dim3(1), dim3(256), 0, s, M1, R, op_convT_mse_parts(IH / 2, IW / 2), w.obs_part,
+                       w.rew_row, w.cont_row, w.kl_grp, w.cont_tm, stats);
+    DR_TRY(dr_check_launch("wm_stats"));
+  }
+  if (hiddens_out) DR_TRY(copy2d(hiddens_out, Hd, w.h_all, Hd, Hd, M, s));
+  if (latents_out) DR_TRY(copy2d(latents_out, L, w.z_all, L, L, M, s));
+  if (post_logits_out) DR_TRY(copy2d(post_logits_out, L, w.plog, L, L, M, s));
+  }  // DR_WM_FWD
+
+  if (!(phases & DR_WM_BWD)) return DR_OK;
+  {
+    const int W = pow2_ge(d->cols);
+    const long long th = (long long)M1 * R * W;
+    const float* post1 = w.plog + (long long)B * L;
+    hipLaunchKernelGGL(k_wm_final, dim3(1), dim3(64), 0, s, stats, rows_global, cfg, w.scal, losses, skip);
     DR_TRY(dr_check_launch("wm_final"));
     hipLaunchKernelGGL(k_wm_kl<1>, dim3(blocks(th, 256)), dim3(256), 0, s, M1, R, d->cols, W, w.prior_lg, post1,
                        w.cont_tm, w.scal, nullptr, w.g_prior, w.gpost);
@@ -719,8 +757,29 @@ extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, con
     }
   }
 
-  if (hiddens_out) DR_TRY(copy2d(hiddens_out, Hd, w.h_all, Hd, Hd, M, s));
-  if (latents_out) DR_TRY(copy2d(latents_out, L, w.z_all, L, L, M, s));
-  if (post_logits_out) DR_TRY(copy2d(post_logits_out, L, w.plog, L, L, M, s));
   return DR_OK;
+}
+
+extern "C" int dr_wm_train_phase(const dr_dims* d, const dr_world_model* wm, const dr_decoder* dec, int B, int T,
+                                 const dr_frames* src, const dr_wm_batch* bt, dr_noise noise, dr_wm_loss_cfg cfg,
+                                 int phases, float* stats, int rows_global, float* losses, int* skip,
+                                 const dr_world_model* gw, const dr_decoder* gd, float* hiddens_out,
+                                 float* latents_out, float* post_logits_out, void* ws, size_t ws_bytes,
+                                 hipStream_t s) {
+  return wm_run(phases, d, wm, dec, B, T, src, bt, noise, cfg, stats, rows_global, losses, skip, gw, gd, hiddens_out,
+                latents_out, post_logits_out, ws, ws_bytes, s);
+}
+
+extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, const dr_decoder* dec, int B, int T,
+                                 const dr_frames* src, const dr_wm_batch* bt, dr_noise noise, dr_wm_loss_cfg cfg,
+                                 float* losses, int* skip, const dr_world_model* gw, const dr_decoder* gd,
+                                 float* hiddens_out, float* latents_out, float* post_logits_out, void* ws,
+                                 size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(d && B > 0 && T >= 2, "null argument or T < 2");
+  Carve c(ws);
+  WmWs w;
+  wm_carve(c, d, wm_dims(d, B, T), w);
+  WS_CHECK(c, ws_bytes);
+  return wm_run(DR_WM_PREP | DR_WM_FWD | DR_WM_BWD, d, wm, dec, B, T, src, bt, noise, cfg, w.stats, 0, losses, skip,
+                gw, gd, hiddens_out, latents_out, post_logits_out, ws, ws_bytes, s);
 }

@@ -46,6 +46,7 @@ class WorldModel(nn.Module):
                                            weight_decay=1e-6)
         self.scalar = torch.amp.GradScaler(enabled=self.device.type == "cuda")
         self._flat = None
+        self._dp = None  # (rank, world, group) under data parallelism
         self.last_losses = None  # device [total, loss_pred, KL_dyn, KL_rep] of the last training_step
 
     # ---- libdreamer_hip packing ---------------------------------------------
@@ -116,6 +117,13 @@ class WorldModel(nn.Module):
         self._flat = _Flat(self)
         self.optimiser = FlatAdamW(self._flat, g["lr"], g["betas"], g["eps"], g["weight_decay"])
         return self._flat
+
+    def set_data_parallel(self, rank, world, group=None):
+        """Shard training_step's batch over `world` ranks (one per GPU): the
+        mask sum and the loss sums are all-reduced between the step's phases,
+        so losses, free-bit clamps and gradients are the global ones, and the
+        flat gradient is all-reduced (sum) before clip_grad_norm_."""
+        self._dp = (rank, world, group) if world > 1 else None
 
     def params_key(self):
         return tuple(p.data_ptr() for p in self.parameters())
@@ -261,12 +269,13 @@ class WorldModel(nn.Module):
         Hd, R, C = self.hidden_dims, self.latent_num_rows, self.latent_num_columns
         f = self._ensure_flat()
         d = self.dims()
-        noise = hip.explicit_noise(q=noise_q, device=dev) if noise_q is not None else hip.rng(dev).noise()
+        row0 = 0 if self._dp is None else self._dp[0] * B  # Philox keyed by the global row
+        noise = hip.explicit_noise(q=noise_q, device=dev) if noise_q is not None else hip.rng(dev).noise(row0=row0)
         cfg = L.dr_wm_loss_cfg(self.beta_pred, self.beta_dyn, self.beta_rep)
         if getattr(self, "_scratch", None) is None or self._scratch[0].device != torch.device(dev):
             self._scratch = (torch.empty(4, device=dev), torch.zeros(1, dtype=torch.int32, device=dev),
-                             torch.zeros(1, device=dev), torch.empty(512, device=dev))
-        losses, skip, sq, sq_part = self._scratch
+                             torch.zeros(1, device=dev), torch.empty(512, device=dev), torch.zeros(8, device=dev))
+        losses, skip, sq, sq_part, stats = self._scratch
         hid = lat = plog = None
         if outputs is not None:
             hid = torch.empty(T, B, Hd, device=dev)
@@ -275,8 +284,20 @@ class WorldModel(nn.Module):
         gw, gd = self._grad_structs()
         ws = hip.workspace(dev).get("wm_train", L.query("dr_wm_train_workspace_bytes", d, B, T))
         st = hip.stream()
-        L.call("dr_wm_train_grads", d, self.packed(), self.packed_decoder(), B, T, fr, bt, noise, cfg,
-               L.ptr(losses), L.ptr(skip), gw, gd, L.ptr(hid), L.ptr(lat), L.ptr(plog), L.ptr(ws), ws.numel(), st)
+        args = (d, self.packed(), self.packed_decoder(), B, T, fr, bt)
+        tail = (L.ptr(losses), L.ptr(skip), gw, gd, L.ptr(hid), L.ptr(lat), L.ptr(plog), L.ptr(ws), ws.numel(), st)
+        if self._dp is None:
+            L.call("dr_wm_train_phase", *args, noise, cfg, 7, L.ptr(stats), 0, *tail)
+        else:
+            import torch.distributed as dist
+            rank, world, group = self._dp
+            rows = world * B * (T - 1)
+            L.call("dr_wm_train_phase", *args, noise, cfg, 1, L.ptr(stats), rows, *tail)
+            dist.all_reduce(stats[0:1], group=group)
+            L.call("dr_wm_train_phase", *args, noise, cfg, 2, L.ptr(stats), rows, *tail)
+            dist.all_reduce(stats[1:5], group=group)
+            L.call("dr_wm_train_phase", *args, noise, cfg, 4, L.ptr(stats), rows, *tail)
+            dist.all_reduce(f.grad, group=group)
         if outputs is not None:
             outputs.update(hiddens=hid, latents=lat, post_logits=plog)
         if step:

@@ -239,6 +239,21 @@ typedef struct {
 } dr_wm_batch;
 typedef struct { float beta_pred, beta_dyn, beta_rep; } dr_wm_loss_cfg;
 size_t dr_wm_train_workspace_bytes(const dr_dims* d, int B, int T);
+/* The same step in three phases for data parallelism (one shard of B rows per
+ * rank, same workspace across the phases).  `stats` (device, 8 floats) carries
+ * the loss sums that must be global: after DR_WM_PREP the caller all-reduces
+ * (sum) stats[0] (mask.sum(), WorldModel.py:185), after DR_WM_FWD stats[1..4]
+ * (masked squared-error, reward, continue and KL sums); DR_WM_BWD then forms
+ * the global losses (rows_global = global B * (T-1) for the KL means,
+ * 182-183) and gradients whose all-reduce SUM is the global gradient. */
+#define DR_WM_PREP 1
+#define DR_WM_FWD 2
+#define DR_WM_BWD 4
+int dr_wm_train_phase(const dr_dims* d, const dr_world_model* wm, const dr_decoder* dec, int B, int T,
+                      const dr_frames* src, const dr_wm_batch* batch, dr_noise noise, dr_wm_loss_cfg cfg, int phases,
+                      float* stats, int rows_global, float* losses, int* skip, const dr_world_model* g_wm,
+                      const dr_decoder* g_dec, float* hiddens_out, float* latents_out, float* post_logits_out,
+                      void* ws, size_t ws_bytes, hipStream_t stream);
 int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, const dr_decoder* dec, int B, int T,
                       const dr_frames* src, const dr_wm_batch* batch, dr_noise noise, dr_wm_loss_cfg cfg,
                       float* losses, int* skip, const dr_world_model* g_wm, const dr_decoder* g_dec,

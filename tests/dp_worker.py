@@ -52,3 +52,33 @@ def worker(rank, world, port, B_global, starts_list, out_path, backend):
         torch.save(res, out_path)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def run_wm_steps(d, starts_list, seed=98765):
+    """world-model training steps from the device ring; returns losses and the flat parameters"""
+    from dreamer_amd import hip
+    hip.rng(d.device).reseed(seed)
+    out = []
+    for st in starts_list:
+        loss = d.world_model.train_step_ring(d.buffer, st)
+        torch.cuda.synchronize()
+        out.append(float(loss))
+    return out, d.world_model._flat.flat.cpu()
+
+
+def wm_worker(rank, world, port, B_global, starts_list, out_path, backend):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    b = B_global // world
+    d = make_dreamer(dev, b)
+    d.world_model.set_data_parallel(rank, world, dist.group.WORLD)
+    mine = [st[rank * b:(rank + 1) * b] for st in starts_list]
+    res = run_wm_steps(d, mine)
+    if rank == 0:
+        torch.save(res, out_path)
+    dist.barrier()
+    dist.destroy_process_group()

@@ -41,3 +41,22 @@ def test_two_rank_matches_single(gpu, tmp_path):
     for a, b, name in zip(single[1:4], dp[1:4], ("actor", "critic", "target")):
         assert torch.allclose(a, b, rtol=0, atol=5e-6), (name, float((a - b).abs().max()))
     assert abs(single[4] - dp[4]) < 1e-6
+
+
+def test_two_rank_world_model_matches_single(gpu, tmp_path):
+    """WorldModel.training_step sharded over 2 ranks (mask and loss sums
+    all-reduced between the phases, gradient all-reduced before the clip) vs
+    one process on the whole batch: same losses, same parameters after 3 steps
+    up to summation order."""
+    B = 8
+    rng = np.random.RandomState(12)
+    starts = [rng.randint(0, 64 - 8 + 1, size=B) for _ in range(3)]
+    out = str(tmp_path / "dpwm.pt")
+    mp.spawn(dp_worker.wm_worker, args=(2, _port(), B, starts, out, "gloo"), nprocs=2, join=True)
+    dp = torch.load(out, weights_only=True)
+    d = dp_worker.make_dreamer(gpu, B)
+    single = dp_worker.run_wm_steps(d, starts)
+    for l1, l2 in zip(single[0], dp[0]):
+        assert abs(l1 - l2) <= 1e-4 * max(1.0, abs(l1)), (l1, l2)
+    err = float((single[1] - dp[1]).abs().max())
+    assert err <= 5e-6, err
