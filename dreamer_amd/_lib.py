@@ -110,6 +110,8 @@ _SIGS = {
     "dr_replay_gather": (_i, [_ll, _i, _i, _i, _i, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp]),
     "dr_rng_advance": (_i, [fp, C.c_ulonglong, fp]),
     "dr_wm_train_workspace_bytes": (_sz, [_P(dr_dims), _i, _i]),
+    "dr_decoder_workspace_bytes": (_sz, [_P(dr_dims), _i]),
+    "dr_decoder_fwd": (_i, [_P(dr_dims), _P(dr_decoder), _i, fp, _ll, fp, _ll, fp, fp, _sz, fp]),
     "dr_wm_train_phase": (_i, [_P(dr_dims), _P(dr_world_model), _P(dr_decoder), _i, _i, _P(dr_frames),
                                _P(dr_wm_batch), dr_noise, dr_wm_loss_cfg, _i, fp, _i, fp, fp, _P(dr_world_model),
                                _P(dr_decoder), fp, fp, fp, fp, _sz, fp]),

@@ -31,6 +31,8 @@ struct ConvTArgs {
   const float* wq;
   const float* bias;    // CT_EPI_BIAS / CT_EPI_TANH_MSE
   float* out;           // NHWC [n][2h][2w][ldc]
+  float* out2;          // CT_EPI_BIAS: optional SiLU(acc + bias) (same layout), for the consumers
+  int silu_out;         // CT_EPI_BIAS: out receives SiLU(acc + bias) instead of acc + bias
   int ldc;              // channel stride of out (>= cout; extra channels written as 0)
   const float* pre;     // CT_EPI_DSILU: out = acc * SiLU'(pre) (pre NHWC, stride cout)
   // CT_EPI_TANH_MSE: mu = tanh(acc + bias); err = mu - target; out = coef[f] * err * (1 - mu^2)
@@ -46,6 +48,8 @@ int op_convT_mse_parts(int h, int w);  // partial sums per frame written by CT_E
 // CT_EPI_TANH_MSE runs a direct VALU kernel (cout = 3): wq must come from
 // op_convT_out3_repack ([ci][4 classes][4 taps][3]), out has ldc = 4
 int op_convT_out3_repack(int cin, const float* wt, float* wq, hipStream_t s);
+// the same direct kernel; target == NULL: mu = tanh(acc + bias) written NCHW [n][3][2h][2w]
+int op_convT_out3(const ConvTArgs& a, hipStream_t s);
 
 // Weight gradient of a k4 s2 p1 (transposed) convolution:
 //   dW[a][b][ky][kx] (+)= scale * sum_{f,y,x} lo[f][y][x][a] * hi[f][2y-1+ky][2x-1+kx][b]

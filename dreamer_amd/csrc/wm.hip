@@ -229,6 +229,11 @@ __global__ void k_perm_rows(int C, int P, int K, const float* __restrict__ in, f
   else out[i] = in[nh];
 }
 
+__global__ void k_silu(long long n, const float* __restrict__ x, float* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = dr_silu(x[i]);
+}
+
 static int blocks(long long n, int t) { return (int)((n + t - 1) / t); }
 
 // split-K scratch for one launch's problems (disjoint slices of the pool)
@@ -267,6 +272,7 @@ struct WmWs {
   // heads (M1 rows)
   float *pp1, *px1, *pp2, *px2, *prior_lg, *rp1, *rx1, *rp2, *rx2, *rew_lg, *cp1, *cx1, *cp2, *cx2, *cont_lg;
   float *du1, *dx1, *du2, *dq1, *dq2, *dq3, *dg4, *w3p, *b3p, *wqd[4], *wrd[4];
+  float *du2p, *dq1p, *dq2p, *dq3p;  // SiLU of the decoder pre-activations (what the next layer reads)
   // loss
   float *coef_row, *coef_obs, *obs_part, *kl_grp, *rew_row, *cont_row, *scal, *stats;
   // backward
@@ -356,6 +362,8 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
   w.cont_lg = c.f(M1);
   w.du1 = c.f(M1 * D.dh); w.dx1 = c.f(M1 * D.dh); w.du2 = c.f(M1 * D.Fd);
   w.dq1 = c.f(M1 * D.p3 * 2 * D.d2); w.dq2 = c.f(M1 * D.p2 * D.d2); w.dq3 = c.f(M1 * D.p1 * D.d1);
+  w.du2p = c.f(M1 * D.Fd);
+  w.dq1p = c.f(M1 * D.p3 * 2 * D.d2); w.dq2p = c.f(M1 * D.p2 * D.d2); w.dq3p = c.f(M1 * D.p1 * D.d1);
   w.dg4 = c.f(M1 * D.p0 * 4);
   w.w3p = c.f((long long)D.Fd * D.dh); w.b3p = c.f(D.Fd);
   const int cin_t[4] = {D.C0, 2 * D.d2, D.d2, D.d1}, cout_t[4] = {2 * D.d2, D.d2, D.d1, 3};
@@ -586,14 +594,18 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     DR_TRY(run(G_NT, AM_LNSILU, g, s));
   }
   {
-    const float* ins[4] = {w.du2, w.dq1, w.dq2, w.dq3};
+    hipLaunchKernelGGL(k_silu, dim3(blocks((long long)M1 * D.Fd, 256)), dim3(256), 0, s, (long long)M1 * D.Fd,
+                       w.du2, w.du2p);
+    DR_TRY(dr_check_launch("silu"));
+    const float* ins[4] = {w.du2p, w.dq1p, w.dq2p, w.dq3p};
     float* outs[3] = {w.dq1, w.dq2, w.dq3};
+    float* posts[3] = {w.dq1p, w.dq2p, w.dq3p};
     for (int k = 0; k < 4; ++k) {
       ConvTArgs a = {};
       a.n = M1; a.cin = cin_t[k]; a.h = IH >> (4 - k); a.w = IW >> (4 - k); a.cout = cout_t[k];
-      a.in = ins[k]; a.silu_in = 1; a.wq = w.wqd[k]; a.bias = dec->convt[k].b;
+      a.in = ins[k]; a.silu_in = 0; a.wq = w.wqd[k]; a.bias = dec->convt[k].b;
       if (k < 3) {
-        a.out = outs[k]; a.ldc = cout_t[k];
+        a.out = outs[k]; a.out2 = posts[k]; a.ldc = cout_t[k];
         DR_TRY(op_convT_nhwc(CT_EPI_BIAS, a, s));
       } else {
         // Tanh + squared error against frames t >= 1 (WorldModel.py:129); writes dL/d(pre-tanh)
@@ -650,13 +662,14 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   {
     float* gins[4] = {w.dgu2, w.dgq1, w.dgq2, w.dgq3};   // dL/d(pre-activation) of each convT input
     const float* pres[4] = {w.du2, w.dq1, w.dq2, w.dq3};
+    const float* posts[4] = {w.du2p, w.dq1p, w.dq2p, w.dq3p};
     const float* gouts[4] = {w.dgq1, w.dgq2, w.dgq3, w.dg4};
     for (int k = 3; k >= 0; --k) {
       const int ih = IH >> (3 - k), iw = IW >> (3 - k);  // output (high-res) size of convT k
       const int co = cout_t[k], co_st = (k == 3) ? 4 : co;
       DR_TRY(op_conv_nhwc_ex(M1, co_st, ih, iw, cin_t[k], gouts[k], w.wrd[k], nullptr, gins[k], 0,
                              const_cast<float*>(pres[k]), CONV_EPI_DSILU, s));
-      DR_TRY(op_conv_wgrad(M1, ih / 2, iw / 2, cin_t[k], co_st, pres[k], cin_t[k], 1, gouts[k], co_st, gd->convt[k].w,
+      DR_TRY(op_conv_wgrad(M1, ih / 2, iw / 2, cin_t[k], co_st, posts[k], cin_t[k], 0, gouts[k], co_st, gd->convt[k].w,
                            co, 1.0f, 0, w.cws, w.cws_n, s));
       DR_TRY(op_chan_sum((long long)M1 * ih * iw, co, gouts[k], co_st, gd->convt[k].b, 0, w.cws, w.cws_n, s));
     }
@@ -782,4 +795,70 @@ extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, con
   WS_CHECK(c, ws_bytes);
   return wm_run(DR_WM_PREP | DR_WM_FWD | DR_WM_BWD, d, wm, dec, B, T, src, bt, noise, cfg, w.stats, 0, losses, skip,
                 gw, gd, hiddens_out, latents_out, post_logits_out, ws, ws_bytes, s);
+}
+
+// ===========================================================================
+// a20  Decoder.forward (VariationalAutoEncoder.py:139-161), inference
+// ===========================================================================
+struct DecWs {
+  float *u1, *u2, *q[3], *w3p, *b3p, *wq[4];
+};
+static void dec_carve(Carve& c, const dr_dims* d, int M, DecWs& w) {
+  const WmDims D = wm_dims(d, 1, 2);
+  const int cin_t[4] = {D.C0, 2 * D.d2, D.d2, D.d1}, cout_t[4] = {2 * D.d2, D.d2, D.d1, 3};
+  w.u1 = c.f((long long)M * D.dh);
+  w.u2 = c.f((long long)M * D.Fd);
+  w.q[0] = c.f((long long)M * D.p3 * cout_t[0]);
+  w.q[1] = c.f((long long)M * D.p2 * cout_t[1]);
+  w.q[2] = c.f((long long)M * D.p1 * cout_t[2]);
+  w.w3p = c.f((long long)D.Fd * D.dh);
+  w.b3p = c.f(D.Fd);
+  for (int k = 0; k < 4; ++k) w.wq[k] = c.f((long long)16 * cin_t[k] * cout_t[k]);
+}
+
+extern "C" size_t dr_decoder_workspace_bytes(const dr_dims* d, int M) {
+  if (!d || M <= 0) return 0;
+  Carve c(nullptr);
+  DecWs w;
+  dec_carve(c, d, M, w);
+  return c.off;
+}
+
+extern "C" int dr_decoder_fwd(const dr_dims* d, const dr_decoder* dec, int M, const float* h, long long ldh,
+                              const float* z, long long ldz, float* mu, void* ws, size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(d && dec && h && z && mu && M > 0, "null argument or empty batch");
+  DR_REQUIRE(d->img_h % 16 == 0 && d->img_w % 16 == 0, "image size must be a multiple of 16");
+  DR_REQUIRE(d->dec_f1 % 8 == 0 && d->dec_f2 % 8 == 0, "decoder filter counts must be multiples of 8");
+  Carve c(ws);
+  DecWs w;
+  dec_carve(c, d, M, w);
+  WS_CHECK(c, ws_bytes);
+  const WmDims D = wm_dims(d, 1, 2);
+  const int cin_t[4] = {D.C0, 2 * D.d2, D.d2, D.d1}, cout_t[4] = {2 * D.d2, D.d2, D.d1, 3};
+  const int Hd = D.Hd, L = D.L;
+  DR_TRY(perm_rows(D.C0, D.P16, D.dh, dec->up3.w, w.w3p, 1, s));
+  DR_TRY(perm_rows(D.C0, D.P16, 1, dec->up3.b, w.b3p, 1, s));
+  for (int k = 0; k < 3; ++k) DR_TRY(op_convT_repack(cin_t[k], cout_t[k], dec->convt[k].w, w.wq[k], s));
+  DR_TRY(op_convT_out3_repack(cin_t[3], dec->convt[3].w, w.wq[3], s));
+  // upscaler: cat(h, flatten z) -> Linear -> LN -> SiLU -> Linear (rows permuted to NHWC); its SiLU runs in convT1's loader
+  DR_TRY(run(G_NT, AM_PLAIN, lin2(M, D.dh, h, ldh, Hd, z, ldz, L, dec->up0.w, dec->up0.b, w.u1, D.dh), s));
+  {
+    GemmArgs g = lin_ln(M, D.Fd, D.dh, w.u1, D.dh, dec->up1, w.w3p, w.b3p, w.u2, D.Fd);
+    g.act = 1;  // upscaler.4 SiLU
+    DR_TRY(run(G_NT, AM_LNSILU, g, s));
+  }
+  const float* ins[4] = {w.u2, w.q[0], w.q[1], w.q[2]};
+  for (int k = 0; k < 4; ++k) {
+    ConvTArgs a = {};
+    a.n = M; a.cin = cin_t[k]; a.h = D.IH >> (4 - k); a.w = D.IW >> (4 - k); a.cout = cout_t[k];
+    a.in = ins[k]; a.silu_in = 0; a.wq = w.wq[k]; a.bias = dec->convt[k].b;
+    if (k < 3) {
+      a.out = w.q[k]; a.silu_out = 1; a.ldc = cout_t[k];
+      DR_TRY(op_convT_nhwc(CT_EPI_BIAS, a, s));
+    } else {
+      a.out = mu; a.ldc = 3;
+      DR_TRY(op_convT_out3(a, s));
+    }
+  }
+  return DR_OK;
 }

@@ -178,7 +178,10 @@ __global__ __launch_bounds__(256) void k_convT_nhwc(ConvTArgs a) {
         }
         const float v = acc[i][j][e];
         if (EPI == CT_EPI_BIAS) {
-          a.out[opix * ldc + co] = v + a.bias[co];
+          const float pv = v + a.bias[co];
+          const float sv = (a.out2 || a.silu_out) ? dr_silu(pv) : 0.0f;
+          a.out[opix * ldc + co] = a.silu_out ? sv : pv;
+          if (a.out2) a.out2[opix * ldc + co] = sv;
         } else if (EPI == CT_EPI_DSILU) {
           a.out[opix * ldc + co] = v * dr_dsilu(a.pre[opix * cout + co]);
         } else {  // CT_EPI_TANH_MSE (VAE.py:136 Tanh; WorldModel.py:129 squared error)
@@ -233,7 +236,7 @@ static int launch_convT(const ConvTArgs& a, hipStream_t s) {
 // its 9 neighbours from LDS (row pitch cin + 1: conflict-free) and the 48
 // weights of that channel are wave-uniform (scalar loads).
 // ---------------------------------------------------------------------------
-template <int CIN>
+template <int CIN, bool LOSS>
 __global__ __launch_bounds__(256) void k_convT_out3(ConvTArgs a) {
   constexpr int PW = O3_TX + 2, PH = O3_TY + 2, PITCH = CIN + 1;
   __shared__ float patch[PH * PW * PITCH];
@@ -287,8 +290,21 @@ __global__ __launch_bounds__(256) void k_convT_out3(ConvTArgs a) {
       }
     }
   }
-  // epilogue: tanh, squared error vs the target frame, dL/d(pre-tanh)
   const int y = y0 + ty, x = x0 + tx;
+  if (!LOSS) {  // Decoder.forward: mu = tanh(.) written NCHW [f][3][2h][2w] (VAE.py:153-161)
+    if (y < h && x < w) {
+      const long long plane = 4LL * h * w;
+#pragma unroll
+      for (int cls = 0; cls < 4; ++cls) {
+        const int py = cls >> 1, px = cls & 1;
+        const long long pix = (long long)(2 * y + py) * (2 * w) + 2 * x + px;
+#pragma unroll
+        for (int o = 0; o < 3; ++o) a.out[(f * 3 + o) * plane + pix] = tanhf(acc[cls][o] + a.bias[o]);
+      }
+    }
+    return;
+  }
+  // epilogue: tanh, squared error vs the target frame, dL/d(pre-tanh)
   float sq = 0.0f;
   if (y < h && x < w) {
     const int OW = 2 * w;
@@ -333,9 +349,10 @@ int op_convT_out3_repack(int cin, const float* wt, float* wo, hipStream_t s) {
 }
 
 int op_convT_out3(const ConvTArgs& a, hipStream_t s) {
-  if (a.cout != 3 || a.ldc != 4 || a.tstride < 3 || a.h % O3_TY != 0 || !a.target || !a.coef || !a.part || !a.bias ||
-      !a.in || !a.wq || !a.out) {
-    dr_set_error("convT_out3: needs cout 3, ldc 4, h %% 8 == 0 and target/coef/part/bias");
+  const bool loss = a.target != nullptr;
+  if (a.cout != 3 || a.h % O3_TY != 0 || !a.bias || !a.in || !a.wq || !a.out ||
+      (loss && (a.ldc != 4 || a.tstride < 3 || !a.coef || !a.part))) {
+    dr_set_error("convT_out3: needs cout 3, h %% 8 == 0, bias (and ldc 4, coef, part with a target)");
     return DR_E_INVALID;
   }
   const long long blocks = (long long)a.n * op_convT_mse_parts(a.h, a.w);
@@ -343,13 +360,21 @@ int op_convT_out3(const ConvTArgs& a, hipStream_t s) {
     dr_set_error("convT_out3: too many frames");
     return DR_E_INVALID;
   }
+#define DR_O3(C)                                                                       \
+  do {                                                                                 \
+    if (loss)                                                                          \
+      hipLaunchKernelGGL((k_convT_out3<C, true>), dim3((unsigned)blocks), dim3(256), 0, s, a);  \
+    else                                                                               \
+      hipLaunchKernelGGL((k_convT_out3<C, false>), dim3((unsigned)blocks), dim3(256), 0, s, a); \
+  } while (0)
   switch (a.cin) {
-    case 8: hipLaunchKernelGGL(k_convT_out3<8>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
-    case 16: hipLaunchKernelGGL(k_convT_out3<16>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
-    case 32: hipLaunchKernelGGL(k_convT_out3<32>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
-    case 64: hipLaunchKernelGGL(k_convT_out3<64>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+    case 8: DR_O3(8); break;
+    case 16: DR_O3(16); break;
+    case 32: DR_O3(32); break;
+    case 64: DR_O3(64); break;
     default: dr_set_error("convT_out3: unsupported input channels %d", a.cin); return DR_E_INVALID;
   }
+#undef DR_O3
   return dr_check_launch("convT_out3");
 }
 
@@ -543,7 +568,7 @@ __global__ __launch_bounds__(1024) void k_wgrad_reduce(int ca, int cb, int cbo, 
 }
 
 static void wgrad_plan(int n, int h, int w, int ca, int cb, int& bm, int& nsplit, int& chunk) {
-  bm = ca <= 32 ? 32 : 64;
+  bm = ca <= 32 ? 32 : (ca <= 64 ? 64 : 128);
   const int tiles = ((ca + bm - 1) / bm) * (16 * cb / 64);
   const long long K = (long long)n * h * w;
   const long long kch = (K + WBK - 1) / WBK;
@@ -579,6 +604,8 @@ int op_conv_wgrad(int n, int h, int w, int ca, int cb, const float* lo, int lda,
   dim3 grid((unsigned)(tiles * ns));
   if (bm == 32)
     hipLaunchKernelGGL(k_conv_wgrad<32>, grid, dim3(256), 0, s, n, h, w, ca, cb, lo, lda, lo_silu, hi, ldb, ns, ch, ws);
+  else if (bm == 128)
+    hipLaunchKernelGGL(k_conv_wgrad<128>, grid, dim3(256), 0, s, n, h, w, ca, cb, lo, lda, lo_silu, hi, ldb, ns, ch, ws);
   else
     hipLaunchKernelGGL(k_conv_wgrad<64>, grid, dim3(256), 0, s, n, h, w, ca, cb, lo, lda, lo_silu, hi, ldb, ns, ch, ws);
   DR_TRY(dr_check_launch("conv_wgrad"));

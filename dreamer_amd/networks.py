@@ -267,8 +267,10 @@ class Encoder(nn.Module):
 
 class Decoder(nn.Module):
     """cat(h, z) -> Linear-LN-SiLU -> Linear-SiLU -> 4x ConvTranspose2d (SiLU,
-    Tanh out) (VariationalAutoEncoder.py:101-166).  Used only by the world-model
-    training step; runs as PyTorch-ROCm this round."""
+    Tanh out) (VariationalAutoEncoder.py:101-166).  Inference runs
+    dr_decoder_fwd (parity-class transposed-conv implicit GEMMs, direct
+    3-channel output kernel); the world-model training step runs the decoder
+    inside dr_wm_train_grads.  Autograd callers get the nn.Module forward."""
 
     def __init__(self, latent_num_rows, latent_num_columns, observation_dim, hidden_state_dim, num_filters_1,
                  num_filters_2, hidden_layer_nodes, device="cpu"):
@@ -293,10 +295,33 @@ class Decoder(nn.Module):
 
     def forward(self, hidden, latent):
         B, S, _ = hidden.shape
+        if not hip.needs_torch_grad(self):
+            return self._hip(hidden, latent)
         x = torch.cat((hidden.reshape(B * S, self.hidden_dim), self.flatten(latent.reshape(B * S, -1))), dim=-1)
         x = self.upscaler(x).view(-1, self.num_filters_start, self.start_height, self.start_width)
         mu = self.image_builder(x)
         return mu.view(B, S, *mu.shape[1:])
+
+    def _hip(self, hidden, latent):
+        L.require_gpu(hidden)
+        B, S, _ = hidden.shape
+        M = B * S
+        h = hidden.reshape(M, self.hidden_dim).float().contiguous()
+        z = latent.reshape(M, -1).float().contiguous()
+        d = L.dr_dims()
+        d.hidden, d.rows, d.cols = self.hidden_dim, self.latent_row_dim, self.latent_col_dim
+        d.img_h, d.img_w = 16 * self.start_height, 16 * self.start_width
+        ib = self.image_builder
+        d.dec_f1, d.dec_f2 = ib[4].out_channels, ib[2].out_channels
+        d.dec_hidden = self.upscaler[0].out_features
+        dec = L.dr_decoder(hip.linear(self.upscaler[0]), hip.linear(self.upscaler[1]), hip.linear(self.upscaler[3]))
+        for i, j in enumerate((0, 2, 4, 6)):
+            dec.convt[i] = hip.linear(ib[j])
+        mu = torch.empty(B, S, 3, d.img_h, d.img_w, device=h.device)
+        ws = hip.workspace(h.device).get("dec", L.query("dr_decoder_workspace_bytes", d, M))
+        L.call("dr_decoder_fwd", d, dec, M, L.ptr(h), h.shape[1], L.ptr(z), z.shape[1], L.ptr(mu), L.ptr(ws),
+               ws.numel(), hip.stream())
+        return mu
 
     def decode(self, hidden_state, latent_state):
         return self.forward(hidden_state, latent_state)

@@ -260,6 +260,12 @@ int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, const dr_decod
                       float* hiddens_out, float* latents_out, float* post_logits_out, void* ws, size_t ws_bytes,
                       hipStream_t stream);
 
+/* ---- a20  Decoder.forward (VAE.py:139-161), inference: mu [M][3][H][W] (NCHW)
+ * from cat(h, flatten z) rows (h row stride ldh, z row stride ldz). */
+size_t dr_decoder_workspace_bytes(const dr_dims* d, int M);
+int dr_decoder_fwd(const dr_dims* d, const dr_decoder* dec, int M, const float* h, long long ldh, const float* z,
+                   long long ldz, float* mu, void* ws, size_t ws_bytes, hipStream_t stream);
+
 /* ---- a1  replay gather (Buffer.sample_sequences, Buffer.py:49-61) --------- */
 int dr_replay_gather(long long cap, int B, int S, int frame_elems, int A, const unsigned char* frames,
                      const float* actions, const float* rewards, const float* continues,

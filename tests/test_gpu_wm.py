@@ -98,3 +98,22 @@ def test_wm_step_skips_nonfinite(gpu):
     assert int(wm.last_skip.item()) == 1
     for b, p in zip(before, wm.parameters()):
         assert torch.equal(b, p.detach())
+
+
+@pytest.mark.parametrize("which", ["small", "full"])
+def test_decoder_forward(which, gpu):
+    """Decoder.forward on HIP (dr_decoder_fwd) vs the oracle's restatement
+    (pinned by the WM fixtures' losses) on random states; rtol 1e-4 / atol 1e-5."""
+    from oracle import dreamer_oracle as O
+    fx = load_fixture(which + "_wm")
+    d, P = build(which, gpu, fx)
+    R, C = int(fx["cfg_rows"]), int(fx["cfg_cols"])
+    Hd = d.world_model.hidden_dims
+    g = torch.Generator().manual_seed(3)
+    h = torch.randn(3, 2, Hd, generator=g)
+    lg = torch.randn(3, 2, R, C, generator=g)
+    z = torch.nn.functional.one_hot(lg.argmax(-1), C).float()
+    with torch.no_grad():
+        mu = d.world_model.decoder(h.to(gpu), z.to(gpu))
+    ref = O.decoder_forward(h, z, P, (d.world_model.observation_dim_x, d.world_model.observation_dim_y))
+    close(mu, ref, 1e-4, 1e-5, "decoder mu")
