@@ -209,12 +209,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("DREAMER_DIST_BACKEND") == "gloo":
+        local %= max(1, torch.cuda.device_count())  # rehearsal: several ranks may share one GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     group = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        # nccl = RCCL over xGMI; DREAMER_DIST_BACKEND=gloo rehearses N ranks on one GPU
+        backend = os.environ.get("DREAMER_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
         group = dist.group.WORLD
 
     from dreamer_amd import Dreamer
@@ -265,7 +269,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t)
     la, lc = float(d.agent.loss_buffer[0]), float(d.agent.loss_buffer[1])
+    # the world-model step all-reduces under DP: every rank runs it (max over ranks)
+    wm = None
+    if args.wm_steps > 0:
+        wm_s, wm_gpu_s, wm_loss = bench_wm(d, B, args.wm_steps, 2)
+        if world > 1:
+            import torch.distributed as dist
+            t = torch.tensor([wm_s, wm_gpu_s], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            wm_s, wm_gpu_s = (float(x) for x in t.cpu())
+        wm = (wm_s, wm_gpu_s, wm_loss)
     if rank != 0:
+        barrier()
         if world > 1:
             import torch.distributed as dist
             dist.destroy_process_group()
@@ -305,8 +320,8 @@ def main():
                                 "unit": "TFLOP/s", "frac": round(tf / FP32_MFMA_PEAK_TFLOPS, 4),
                                 "mflop_per_imagined_step": mf,
                                 "note": "whole train_Agent epoch, SURVEY §8d necessary FLOPs x imagined steps/s"}
-    if args.wm_steps > 0:
-        wm_s, wm_gpu_s, wm_loss = bench_wm(d, B, args.wm_steps, 2)
+    if wm is not None:
+        wm_s, wm_gpu_s, wm_loss = wm
         fl = wm_step_flops(cfg, B, H)
         ac_s = el / args.steps
         out["secondary"] = {
@@ -324,8 +339,9 @@ def main():
         }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(CAR_RACER, B, S, H, budget_s=args.cpu_budget)
-    print(json.dumps(out))
+    print(json.dumps(out), flush=True)
     if world > 1:
+        barrier()
         import torch.distributed as dist
         dist.destroy_process_group()
 

@@ -623,13 +623,89 @@ __global__ __launch_bounds__(1024) void k_update_S(int n, int n2, const float* R
   }
 }
 
+// Above DR_SORT_MAX returns (e.g. 8 ranks x 256 rows x H 15 = 30720 under
+// data parallelism) the four order statistics torch.quantile interpolates
+// between are found by an exact radix select instead of a full sort: the
+// float bits are mapped to order-preserving u32 keys and 4 passes of 8-bit
+// LDS histograms narrow each target rank to a single key.  One workgroup;
+// the returns (<= a few MB) stream from L2 once per pass.
+__device__ __forceinline__ unsigned f2key(float x) {
+  const unsigned u = __float_as_uint(x);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(unsigned k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+__global__ __launch_bounds__(1024) void k_update_S_select(int n, const float* R, float* S, float* norm_out) {
+  __shared__ unsigned hist[4][256];
+  __shared__ unsigned prefix[4], want[4];
+  __shared__ int bad;
+  const float r95 = 0.95f * (float)(n - 1), r05 = 0.05f * (float)(n - 1);
+  if (threadIdx.x == 0) {
+    bad = 0;
+    want[0] = (unsigned)(int)r95;
+    want[1] = (unsigned)(int)ceilf(r95);
+    want[2] = (unsigned)(int)r05;
+    want[3] = (unsigned)(int)ceilf(r05);
+  }
+  if (threadIdx.x < 4) prefix[threadIdx.x] = 0u;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    const unsigned hi_mask = pass == 0 ? 0u : (0xffffffffu << (shift + 8));
+    for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) (&hist[0][0])[i] = 0u;
+    __syncthreads();
+    unsigned pf[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) pf[t] = prefix[t];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const float x = R[i];
+      if (pass == 0 && !isfinite(x)) bad = 1;
+      const unsigned k = f2key(x);
+      const unsigned bin = (k >> shift) & 255u;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if ((k & hi_mask) == pf[t]) atomicAdd(&hist[t][bin], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+      const int t = threadIdx.x;
+      unsigned below = 0u, w = want[t];
+      int b = 0;
+      for (; b < 255; ++b) {
+        const unsigned c = hist[t][b];
+        if (below + c > w) break;
+        below += c;
+      }
+      prefix[t] = pf[t] | ((unsigned)b << shift);
+      want[t] = w - below;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    float s = *S;
+    if (!bad) {
+      const float q95 = torch_lerp(key2f(prefix[0]), key2f(prefix[1]), r95 - (float)(int)r95);
+      const float q05 = torch_lerp(key2f(prefix[2]), key2f(prefix[3]), r05 - (float)(int)r05);
+      const float range = fmaxf(q95 - q05, 1.0f);
+      s = 0.99f * s + 0.01f * range;
+      *S = s;
+    }
+    if (norm_out) *norm_out = fmaxf(s, 1.0f);
+  }
+}
+
 extern "C" int dr_update_S(int n, const float* R, float* S, float* norm_out, void* ws, size_t ws_bytes,
                            hipStream_t stream) {
   (void)ws;
   (void)ws_bytes;
-  if (n <= 0 || n > DR_SORT_MAX) {
-    dr_set_error("update_S: n=%d outside [1,%d]", n, DR_SORT_MAX);
+  if (n <= 0 || !R || !S) {
+    dr_set_error("update_S: n=%d or null pointer", n);
     return DR_E_INVALID;
+  }
+  if (n > DR_SORT_MAX) {
+    hipLaunchKernelGGL(k_update_S_select, dim3(1), dim3(1024), 0, stream, n, R, S, norm_out);
+    return dr_check_launch("update_S_select");
   }
   int n2 = 1;
   while (n2 < n) n2 <<= 1;

@@ -202,3 +202,32 @@ def test_graph_replay_matches_eager(gpu):
     for a, b in zip(*res):
         assert torch.isfinite(a).all()
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n", [3840, 16384, 16385, 30720, 262144])
+def test_update_S_quantile_exact(n, gpu):
+    """Agent.update_S (Agent.py:78-88) on n returns: bitonic LDS sort up to
+    16384 values, exact radix select above (8 ranks x 256 rows x H 15 =
+    30720 under DP).  torch.quantile's two order statistics and its linear
+    interpolation are reproduced bit-exactly; ties and signed zeros are
+    included; a NaN leaves S unchanged."""
+    from dreamer_amd import _lib as L
+    g = torch.Generator().manual_seed(n)
+    R = (torch.randn(n, generator=g) * 7.0).round(decimals=2)  # many ties
+    R[: n // 50] = 0.0
+    R[n // 50: n // 25] = -0.0
+    for S0 in (1.0, 3.5):
+        Sd = torch.tensor([S0], device=gpu)
+        norm = torch.zeros(1, device=gpu)
+        Rd = R.to(gpu)
+        L.call("dr_update_S", n, L.ptr(Rd), L.ptr(Sd), L.ptr(norm), None, 0, 0)
+        torch.cuda.synchronize()
+        ref = O.update_S(torch.tensor(S0), R)
+        assert float(Sd) == float(ref), (n, float(Sd), float(ref))
+        assert float(norm) == max(float(ref), 1.0)
+    Rn = R.clone()
+    Rn[n // 3] = float("nan")
+    Sd = torch.tensor([2.0], device=gpu)
+    L.call("dr_update_S", n, L.ptr(Rn.to(gpu)), L.ptr(Sd), None, None, 0, 0)
+    torch.cuda.synchronize()
+    assert float(Sd) == 2.0
