@@ -104,6 +104,7 @@ _SIGS = {
                                 fp, _sz, fp]),
     "dr_sqnorm": (_i, [_ll, fp, fp, fp]),
     "dr_sqnorm_multi": (_i, [_ll, fp, fp, fp, fp]),
+    "dr_clip_stats": (_i, [_ll, fp, _ll, fp, _i, fp, fp, fp, fp, fp]),
     "dr_adamw": (_i, [_ll, fp, fp, fp, fp, fp, _f, _f, _f, _f, _f, _f, fp, fp, fp, fp]),
     "dr_ema": (_i, [_ll, fp, fp, _f, _f, fp, fp]),
     "dr_nonfinite": (_i, [_ll, fp, fp, fp]),

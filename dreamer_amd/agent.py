@@ -287,11 +287,10 @@ class Agent(nn.Module):
         """NaN/Inf loss -> skip (Agent.py:137-139), clip_grad_norm_(100) per
         network (Agent.py:147-148), AdamW steps (150-151), target EMA (153)."""
         st = hip.stream()
-        skip.zero_()
-        L.call("dr_nonfinite", 2, self.loss_buffer.data_ptr(), skip.data_ptr(), st)
-        sq.zero_()
-        L.call("dr_sqnorm", self.fa.numel, self.fa.grad.data_ptr(), sq.data_ptr(), st)
-        L.call("dr_sqnorm", self.fc.numel, self.fc.grad.data_ptr(), sq.data_ptr() + 4, st)
+        if getattr(self, "_clip_scratch", None) is None or self._clip_scratch.device != sq.device:
+            self._clip_scratch = torch.zeros(1024, device=sq.device)  # DR_CLIP_SCRATCH_FLOATS
+        L.call("dr_clip_stats", self.fa.numel, self.fa.grad.data_ptr(), self.fc.numel, self.fc.grad.data_ptr(), 2,
+               self.loss_buffer.data_ptr(), sq.data_ptr(), skip.data_ptr(), self._clip_scratch.data_ptr(), st)
         self.critic_optimiser.fused_step(sq[1:2], 100.0, skip)
         self.actor_optimiser.fused_step(sq[0:1], 100.0, skip)
         self.soft_update_target(skip=skip)

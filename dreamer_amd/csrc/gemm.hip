@@ -957,6 +957,7 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, int m, int n, 
 // partial tile to splitk_ws and k_splitk_finish sums the splits in order and
 // applies the epilogue.
 // ---------------------------------------------------------------------------
+#define DR_TILE_SPLITS 4  // = DR_SPLITK_MAX (engine_util.h): scratch sized for it
 #define TBK 32  // k-chunk granularity of the split-K ranges (kernel chunks are a multiple)
 
 __device__ __forceinline__ float tile_b_kn(const GemmArgs& g, const float* W, int ldb, int n, int k) {
@@ -1030,9 +1031,13 @@ __global__ __launch_bounds__(256) void k_gemm_tile(GemmBatch gb, int splits) {
         }
       } else {
         const int kk = tid / AR4 + AKS * i, k = k0 + kk, m = m0 + 4 * (tid % AR4);
-        float* v = &ra[sl][i].x;
+        if (VEC && k < K && m + 3 < M) {
+          ra[sl][i] = dr_ld4(A, (unsigned)(k * lda + m));
+        } else {
+          float* v = &ra[sl][i].x;
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) v[cc] = (k < K && m + cc < M) ? dr_ld1(A, (unsigned)(k * lda + m + cc)) : 0.f;
+          for (int cc = 0; cc < 4; ++cc) v[cc] = (k < K && m + cc < M) ? dr_ld1(A, (unsigned)(k * lda + m + cc)) : 0.f;
+        }
       }
     }
 #pragma unroll
@@ -1050,9 +1055,16 @@ __global__ __launch_bounds__(256) void k_gemm_tile(GemmBatch gb, int splits) {
         }
       } else {
         const int kk = tid / BR4 + BKS * i, k = k0 + kk, n = n0 + 4 * (tid % BR4);
-        float* v = &rb[sl][i].x;
+        if (VEC && k < K && n + 3 < N) {
+          // 4 columns in one segment (the host checked nsplitB % 4 == 0, ldb2 % 4 == 0)
+          if (k >= g.ksplitB) rb[sl][i] = dr_ld4(g.W2 + (long long)(k - g.ksplitB) * g.ldb2, (unsigned)n);
+          else if (n >= g.nsplitB) rb[sl][i] = dr_ld4(g.W2 + (long long)k * g.ldb2, (unsigned)(n - g.nsplitB));
+          else rb[sl][i] = dr_ld4(W, (unsigned)(k * ldb + n));
+        } else {
+          float* v = &rb[sl][i].x;
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) v[cc] = (k < K && n + cc < N) ? tile_b_kn(g, W, ldb, n + cc, k) : 0.f;
+          for (int cc = 0; cc < 4; ++cc) v[cc] = (k < K && n + cc < N) ? tile_b_kn(g, W, ldb, n + cc, k) : 0.f;
+        }
       }
     }
   };
@@ -1279,25 +1291,36 @@ static void launch_tile(const GemmBatch& gb, int count, hipStream_t s) {
 // is too small to fill the chip and every problem brought scratch for it
 template <int BM, int BN, int KC, bool A_KM, bool B_KN>
 static void launch_tile2(GemmBatch& gb, int count, hipStream_t s) {
-  int maxt = 0, nch = 1 << 30;
+  int maxt = 0, nch = 1 << 30, tot = 0;
   long long maxMN = 0;
   bool vec = true, ws = true;
   for (int i = 0; i < count; ++i) {
     const GemmArgs& g = gb.p[i];
-    maxt = std::max(maxt, dr_cdiv(g.M, BM) * dr_cdiv(g.N, BN));
+    const int t = dr_cdiv(g.M, BM) * dr_cdiv(g.N, BN);
+    maxt = std::max(maxt, t);
+    tot += t;
     nch = std::min(nch, dr_cdiv(g.K, KC));
     maxMN = std::max(maxMN, (long long)g.M * g.N);
     if (!A_KM) {
       vec = vec && g.K % 4 == 0 && g.lda % 4 == 0 && aligned16(g.A);
       if (g.ksplitA < g.K) vec = vec && g.lda2 % 4 == 0 && g.ksplitA % 4 == 0 && aligned16(g.A2);
+    } else {
+      vec = vec && g.lda % 4 == 0 && aligned16(g.A);
     }
-    if (!B_KN) vec = vec && g.ldb % 4 == 0 && aligned16(g.W);
+    if (!B_KN) {
+      vec = vec && g.ldb % 4 == 0 && aligned16(g.W);
+    } else {
+      vec = vec && g.ldb % 4 == 0 && aligned16(g.W);
+      if (g.W2) vec = vec && g.ldb2 % 4 == 0 && aligned16(g.W2) && (g.nsplitB >= g.N || g.nsplitB % 4 == 0);
+    }
     ws = ws && g.splitk_ws != nullptr;
   }
   if (maxt == 0) return;
   int splits = 1;
   if (ws) {
-    splits = std::max(1, std::min(8, dr_cdiv(256, maxt * count)));
+    // about two workgroups per CU over the problems' real tiles (the grid's
+    // surplus blocks of the smaller problems exit at once)
+    splits = std::max(1, std::min(DR_TILE_SPLITS, dr_cdiv(512, tot)));
     splits = std::min(splits, std::max(1, nch / 2));  // at least 2 chunks per split
     for (int i = 0; i < count; ++i)
       while (splits > 1 && (long long)splits * gb.p[i].M * gb.p[i].N > gb.p[i].splitk_floats) --splits;

@@ -923,6 +923,84 @@ extern "C" int dr_sqnorm_multi(long long n, const float* g, float* acc, float* s
   return dr_check_launch("sqnorm_final");
 }
 
+// The agent's clip statistics in ONE launch (Agent.py:137-148): sq[0] =
+// |g_a|^2, sq[1] = |g_c|^2 (written, not accumulated) and skip = any
+// non-finite value in the loss slots.  Blocks [0, nba) take contiguous float4
+// chunks of buffer a, the rest buffer b; each writes one partial, and the
+// last block to arrive (device-scope ticket) adds the partials in a fixed
+// order -- deterministic, no float atomics -- and re-arms the ticket.
+__global__ __launch_bounds__(256) void k_clip_stats(long long na, const float* __restrict__ ga, long long nb,
+                                                    const float* __restrict__ gb, int nba, long long cha,
+                                                    long long chb, int nloss, const float* __restrict__ loss,
+                                                    float* part, unsigned* ticket, float* sq, int* skip) {
+  __shared__ float red[256];
+  __shared__ int last;
+  const bool isa = (int)blockIdx.x < nba;
+  const float4* g4 = reinterpret_cast<const float4*>(isa ? ga : gb);
+  const long long n4 = (isa ? na : nb) / 4;
+  const long long ch = isa ? cha : chb;
+  const long long b0 = (long long)(isa ? blockIdx.x : blockIdx.x - nba) * ch;
+  const long long b1 = b0 + ch < n4 ? b0 + ch : n4;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  for (long long i = b0 + threadIdx.x; i < b1; i += 256) {
+    const float4 v = g4[i];
+    s0 += v.x * v.x;
+    s1 += v.y * v.y;
+    s2 += v.z * v.z;
+    s3 += v.w * v.w;
+  }
+  red[threadIdx.x] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = red[0];
+    __threadfence();
+    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  for (int w = 0; w < 2; ++w) {
+    const int p0 = w ? nba : 0, p1 = w ? (int)gridDim.x : nba;
+    const float* g = w ? gb : ga;
+    const long long n = w ? nb : na;
+    float v = 0.f;
+    for (int i = p0 + (int)threadIdx.x; i < p1; i += 256) v += __builtin_nontemporal_load(&part[i]);
+    for (long long i = 4 * (n / 4) + threadIdx.x; i < n; i += 256) v += g[i] * g[i];
+    __syncthreads();
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+      if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) sq[w] = red[0];
+  }
+  if (threadIdx.x == 0) {
+    int bad = 0;
+    for (int i = 0; i < nloss; ++i) bad |= !isfinite(loss[i]);
+    *skip = bad;
+    *ticket = 0u;
+  }
+}
+
+extern "C" int dr_clip_stats(long long na, const float* ga, long long nb, const float* gb, int nloss,
+                             const float* loss, float* sq, int* skip, void* scratch, hipStream_t stream) {
+  DR_REQUIRE(ga && gb && sq && skip && scratch && na > 0 && nb > 0, "dr_clip_stats: bad arguments");
+  DR_REQUIRE(!(((uintptr_t)ga | (uintptr_t)gb) & 15), "dr_clip_stats: buffers must be 16-byte aligned");
+  auto blocks = [](long long n4) { long long b = (n4 + 2047) / 2048; return (int)(b < 1 ? 1 : (b > 256 ? 256 : b)); };
+  const int nba = blocks(na / 4), nbb = blocks(nb / 4);
+  const long long cha = (na / 4 + nba - 1) / nba, chb = (nb / 4 + nbb - 1) / nbb;
+  float* part = static_cast<float*>(scratch);
+  unsigned* ticket = reinterpret_cast<unsigned*>(part + DR_CLIP_SCRATCH_FLOATS - 1);
+  hipLaunchKernelGGL(k_clip_stats, dim3(nba + nbb), dim3(256), 0, stream, na, ga, nb, gb, nba, cha, chb, nloss,
+                     loss, part, ticket, sq, skip);
+  return dr_check_launch("clip_stats");
+}
+
 // prelude: step += 1 (unless skipped), bias corrections in double like
 // torch's python scalars (adam.py: bias_correction1 = 1 - beta1**step ...)
 __global__ void k_adamw_prelude(int* step, float* hyper, float lr, float b1, float b2, const int* skip) {

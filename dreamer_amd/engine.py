@@ -120,15 +120,17 @@ class ImaginationEngine:
         L.call("dr_observe_scan", d, wm, self.B, self.T, L.ptr(self.feat), L.ptr(self.act_win), self.S * A, A, None,
                None, nz, L.ptr(self.z0), L.ptr(self.h0), None, L.ptr(self.ws_obs), self.ws_obs.numel(), st)
 
-    def imagine(self, eps=None, q=None, deterministic=False):
-        """a7: unroll H steps from (self.z0, self.h0)."""
+    def imagine(self, eps=None, q=None, deterministic=False, z0=None, h0=None):
+        """a7: unroll H steps from (self.z0, self.h0) (or the given slot)."""
         d = self.d
+        z0 = self.z0 if z0 is None else z0
+        h0 = self.h0 if h0 is None else h0
         if eps is not None or q is not None:
             nz = hip.explicit_noise(q=q, eps=eps, device=self.dev)
         else:
             nz = L.dr_noise(None, None, self.rng.state.data_ptr(), self.rank * self.B, DREAM_STREAM)
         L.call("dr_imagine_fwd", d, self.dr.world_model.packed(), self.dr.agent.actor_struct(), self.B, self.H,
-               L.ptr(self.z0), L.ptr(self.h0), nz, int(deterministic), L.ptr(self.latents), L.ptr(self.hiddens),
+               L.ptr(z0), L.ptr(h0), nz, int(deterministic), L.ptr(self.latents), L.ptr(self.hiddens),
                L.ptr(self.actions), L.ptr(self.rewards), L.ptr(self.continues), L.ptr(self.mus),
                L.ptr(self.sigmas), L.ptr(self.tape), L.ptr(self.ws_im), self.ws_im.numel(), hip.stream())
 
@@ -308,6 +310,103 @@ class ImaginationEngine:
         names = [p[0] for p in self.phases()]
         ev = self.last_events
         return {n: ev[k].elapsed_time(ev[k + 1]) for k, n in enumerate(names)}
+
+    # ------------------------------------------------- pipelined epochs
+    # Everything the warm start reads (world-model parameters, the replay
+    # ring, the window starts, its own noise) is untouched by the actor-critic
+    # update, so the warm start of epoch e+1 (conv encoder + posterior scan)
+    # can run on a second stream beside the imagination / update chain of
+    # epoch e.  The results are those of the sequential epochs bit for bit:
+    # the warm start keeps its own copy of the Philox state, advanced once per
+    # epoch like the main one, and (z0, h0) are double-buffered.
+    def _pipe_capture(self, key):
+        dev, B, H = self.dev, self.B, self.H
+        if getattr(self, "_pipe", None) is None:
+            self._pipe = dict(
+                stream=torch.cuda.Stream(dev),
+                rng=torch.zeros(2, dtype=torch.int64, device=dev),
+                z0=[self.z0, torch.zeros_like(self.z0)],
+                h0=[self.h0, torch.zeros_like(self.h0)],
+                key=None)
+        P = self._pipe
+        if P["key"] == key:
+            return P
+        d, A = self.d, self.d.action
+
+        def warm(s):
+            st = torch.cuda.current_stream(dev).cuda_stream
+            self.dr.buffer.gather_actions(self.starts, self.act_win)
+            self._encode_chunk(0, self.T, st)
+            nz = L.dr_noise(None, None, P["rng"].data_ptr(), self.rank * B, WARM_STREAM)
+            L.call("dr_observe_scan", d, self.dr.world_model.packed(), B, self.T, L.ptr(self.feat),
+                   L.ptr(self.act_win), self.S * A, A, None, None, nz, L.ptr(P["z0"][s]), L.ptr(P["h0"][s]), None,
+                   L.ptr(self.ws_obs), self.ws_obs.numel(), st)
+            L.call("dr_rng_advance", P["rng"].data_ptr(), 1, st)
+
+        cs = torch.cuda.Stream(dev)
+        cs.wait_stream(torch.cuda.current_stream(dev))
+        graphs = {}
+        with torch.cuda.stream(cs):
+            for s in (0, 1):
+                for name, body in (("warm", lambda s=s: warm(s)),
+                                   ("imagine", lambda s=s: self.imagine(z0=P["z0"][s], h0=P["h0"][s]))):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=cs):
+                        body()
+                    graphs[(name, s)] = g
+            for name, body, _ in self.phases()[2:]:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=cs):
+                    body()
+                graphs[name] = g
+        torch.cuda.current_stream(dev).wait_stream(cs)
+        P["graphs"], P["key"] = graphs, key
+        return P
+
+    def run_many(self, starts_list):
+        """len(starts_list) consecutive train_Agent epochs, pipelined (see
+        above).  Returns a [K, 2] device tensor of (actor, critic) losses."""
+        K = len(starts_list)
+        ag = self.dr.agent
+        key = (ag.params_key(), self.dr.world_model.params_key(), self.dr.buffer.device_key())
+        P = self._pipe_capture(key)
+        G = P["graphs"]
+        main = torch.cuda.current_stream(self.dev)
+        ws = P["stream"]
+        host = torch.from_numpy(np.stack([np.asarray(x, dtype=np.int64) for x in starts_list])).pin_memory()
+        losses = torch.empty(K, 2, device=self.dev)
+        ws.wait_stream(main)
+        with torch.cuda.stream(ws):
+            dst = host.to(self.dev, non_blocking=True)
+            P["rng"].copy_(self.rng.state)
+        ev_w, ev_i = [None] * K, [None] * K
+
+        def issue_warm(e):
+            with torch.cuda.stream(ws):
+                if e >= 2:
+                    ws.wait_event(ev_i[e - 2])
+                self.starts.copy_(dst[e])
+                G[("warm", e & 1)].replay()
+                ev_w[e] = torch.cuda.Event()
+                ev_w[e].record(ws)
+
+        issue_warm(0)
+        for e in range(K):
+            if e + 1 < K:
+                issue_warm(e + 1)
+            main.wait_event(ev_w[e])
+            G[("imagine", e & 1)].replay()
+            ev_i[e] = torch.cuda.Event()
+            ev_i[e].record(main)
+            for name, _, coll in self.phases()[2:]:
+                G[name].replay()
+                if coll is not None:
+                    coll()
+            losses[e].copy_(ag.loss_buffer[0:2])
+        main.wait_stream(ws)
+        self.epochs += K
+        self._pipe_host = host  # keep the pinned source alive until the H2D copy ran
+        return losses
 
     def _capture(self, key):
         """Record each phase into its own HIP graph (capture does not execute;

@@ -204,6 +204,15 @@ int dr_critic_loss_bwd(const dr_dims* d, const dr_critic* c, int B, int H, const
 int dr_sqnorm(long long n, const float* g, float* acc, hipStream_t stream);
 /* as dr_sqnorm, many workgroups (large buffers); scratch >= 512 floats */
 int dr_sqnorm_multi(long long n, const float* g, float* acc, float* scratch, hipStream_t stream);
+/* The agent's pre-update statistics in one launch (Agent.py:137-148):
+ * sq[0] = |ga|^2 (actor grads), sq[1] = |gb|^2 (critic grads), *skip = any
+ * non-finite value among loss[0..nloss).  Replaces the NaN check and the two
+ * clip_grad_norm_ reductions.  scratch: DR_CLIP_SCRATCH_FLOATS floats,
+ * zeroed once by the caller (holds the partials and an arrival ticket the
+ * kernel re-arms); buffers 16-byte aligned.  Deterministic. */
+#define DR_CLIP_SCRATCH_FLOATS 1024
+int dr_clip_stats(long long na, const float* ga, long long nb, const float* gb, int nloss, const float* loss,
+                  float* sq, int* skip, void* scratch, hipStream_t stream);
 /* p <- AdamW(p, g*clip) (torch.optim.AdamW single-tensor op order) where
  * clip = min(1, max_norm/(sqrt(*sqnorm)+1e-6)) (sqnorm NULL: no clip).  The
  * step counter lives on the device: a prelude increments *step and writes

@@ -204,6 +204,41 @@ def test_graph_replay_matches_eager(gpu):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("which", ["small", "full"])
+def test_pipelined_epochs_match_sequential(which, gpu):
+    """run_many (warm start of epoch e+1 on a second stream beside epoch e's
+    actor-critic chain) == the same epochs run one after another, bit for
+    bit: losses of every epoch, actor / critic / target parameters, S."""
+    from dreamer_amd.engine import ImaginationEngine
+    from formula import replay_data
+    fx = load_fixture("small_epoch")
+    hw = (32, 32) if which == "small" else (64, 64)
+    B, S, H, K = (8, 8, 5, 5) if which == "small" else (16, 16, 6, 4)
+    res = []
+    for pipe in (False, True):
+        d, P = build(which, gpu, fx if which == "small" else None, B=B, S=S, H=H)
+        fr, ac, rw, ct = replay_data(64, hw, 3, seed=3)
+        d.buffer.load_arrays(fr, ac, O.symlog(torch.tensor(rw)).numpy(), ct)
+        eng = ImaginationEngine(d)
+        eng.rng.reseed(4321)
+        np.random.seed(5)
+        starts = [d.buffer.sample_start_indices(B) for _ in range(K)]
+        if pipe:
+            losses = eng.run_many(starts).cpu()
+        else:
+            ls = []
+            for st in starts:
+                la, lc = eng.run(st)
+                ls.append(torch.cat([la, lc]).clone())
+            losses = torch.stack(ls).cpu()
+        torch.cuda.synchronize()
+        res.append((losses, cpu(d.agent.fa.flat), cpu(d.agent.fc.flat), cpu(d.agent.ft.flat), cpu(d.agent.S_dev),
+                    cpu(eng.rng.state)))
+    for a, b in zip(*res):
+        assert torch.isfinite(a.float()).all()
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("n", [3840, 16384, 16385, 30720, 262144])
 def test_update_S_quantile_exact(n, gpu):
     """Agent.update_S (Agent.py:78-88) on n returns: bitonic LDS sort up to
