@@ -1249,6 +1249,10 @@ static void launch_skinny(const GemmBatch& gb, int count, bool vec, hipStream_t 
 }
 
 
+// skinny-GEMM tile knob (microbenchmark): 1 = 64-row tiles for M <= 64, 2 = never 32-column tiles
+static int g_skinny_variant = 0;
+extern "C" void dr_debug_skinny_variant(int v) { g_skinny_variant = v; }
+
 template <int AMODE, bool B_KN>
 static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
   int maxM = 0, epi = EPI_NONE;
@@ -1263,6 +1267,14 @@ static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
     vec = vec && skinny_vec_ok(g, B_KN);
   }
   if (maxM > 4096) return false;
+  if (g_skinny_variant == 1 && maxM > 16) maxM = 65;
+  // 16-column tiles by default; 32-column tiles when the 16-column grid would
+  // exceed one workgroup per CU (these 512-thread tiles hold 1 per CU by VGPRs,
+  // so a second dispatch round costs more than the wider tile's extra MFMAs)
+  int tiles16 = 0;
+  for (int i = 0; i < count; ++i)
+    tiles16 += dr_cdiv(gb.p[i].M, maxM > 64 ? 64 : 16) * dr_cdiv(gb.p[i].N, 16);
+  const bool wide = g_skinny_variant != 2 && maxM <= 64 && tiles16 > 256;
   if (epi == EPI_SAMPLE) {
     if (maxM > 64) launch_skinny<64, 32, AMODE, B_KN, EPI_SAMPLE>(gb, count, vec, s);
     else launch_skinny<16, 32, AMODE, B_KN, EPI_SAMPLE>(gb, count, vec, s);
@@ -1271,6 +1283,7 @@ static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
     else launch_skinny<16, 16, AMODE, B_KN, EPI_ACTOR>(gb, count, vec, s);
   } else {
     if (maxM > 64) launch_skinny<64, 16, AMODE, B_KN, EPI_NONE>(gb, count, vec, s);
+    else if (wide) launch_skinny<16, 32, AMODE, B_KN, EPI_NONE>(gb, count, vec, s);
     else launch_skinny<16, 16, AMODE, B_KN, EPI_NONE>(gb, count, vec, s);
   }
   return true;

@@ -170,6 +170,14 @@ class Dreamer(nn.Module):
 
     def train_Agent(self):
         """Dreamer.train_Agent (Dreamer.py:264-287): AC_epochs fused epochs."""
+        if self.AC_epochs > 1:
+            # the epochs' window starts are drawn up front (same np.random
+            # order); the warm start of epoch e+1 then overlaps epoch e's
+            # update (engine.run_many: identical results, pipelined)
+            B = self.batch_size if self.world is None else self.engine.B
+            starts = [self.buffer.sample_start_indices(B) for _ in range(self.AC_epochs)]
+            losses = self.engine.run_many(starts)
+            return losses[:, 0].mean(dim=0), losses[:, 1].mean(dim=0)
         la, lc = [], []
         for _ in tqdm(range(self.AC_epochs), desc="Training Agent in Dreams", leave=False):
             starts = self.buffer.sample_start_indices(self.batch_size if self.world is None else self.engine.B)

@@ -24,10 +24,13 @@ def make_dreamer(dev, B, S=8, H=5):
     return d
 
 
-def run_epochs(d, eng, starts_list, seed=4321):
+def run_epochs(d, eng, starts_list, seed=4321, pipelined=False):
     eng.rng.reseed(seed)
     out = []
-    for st in starts_list:
+    if pipelined:  # warm start of epoch e+1 beside epoch e's update (run_many)
+        ls = eng.run_many(starts_list).cpu()
+        out = [(float(a), float(c)) for a, c in ls]
+    for st in ([] if pipelined else starts_list):
         la, lc = eng.run(st)
         torch.cuda.synchronize()
         out.append((float(la), float(lc)))
@@ -35,7 +38,7 @@ def run_epochs(d, eng, starts_list, seed=4321):
     return out, ag.fa.flat.cpu(), ag.fc.flat.cpu(), ag.ft.flat.cpu(), float(ag.S_dev)
 
 
-def worker(rank, world, port, B_global, starts_list, out_path, backend):
+def worker(rank, world, port, B_global, starts_list, out_path, backend, pipelined=False):
     import torch.distributed as dist
     from dreamer_amd.engine import ImaginationEngine
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -47,7 +50,7 @@ def worker(rank, world, port, B_global, starts_list, out_path, backend):
     d = make_dreamer(dev, b)
     eng = ImaginationEngine(d, B=b, world=(rank, world, dist.group.WORLD))
     mine = [st[rank * b:(rank + 1) * b] for st in starts_list]
-    res = run_epochs(d, eng, mine)
+    res = run_epochs(d, eng, mine, pipelined=pipelined)
     if rank == 0:
         torch.save(res, out_path)
     dist.barrier()

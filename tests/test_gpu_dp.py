@@ -24,13 +24,14 @@ def _port():
     return p
 
 
-def test_two_rank_matches_single(gpu, tmp_path):
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_two_rank_matches_single(pipelined, gpu, tmp_path):
     from dreamer_amd.engine import ImaginationEngine
     B = 8
     rng = np.random.RandomState(11)
     starts = [rng.randint(0, 64 - 8 + 1, size=B) for _ in range(3)]
     out = str(tmp_path / "dp.pt")
-    mp.spawn(dp_worker.worker, args=(2, _port(), B, starts, out, "gloo"), nprocs=2, join=True)
+    mp.spawn(dp_worker.worker, args=(2, _port(), B, starts, out, "gloo", pipelined), nprocs=2, join=True)
     dp = torch.load(out, weights_only=False)
     d = dp_worker.make_dreamer(gpu, B)
     eng = ImaginationEngine(d, B=B)

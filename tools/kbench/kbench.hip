@@ -19,6 +19,7 @@ static int g_reps = 200;
 extern "C" int dr_debug_tbuf_gru(long long* out, int n);
 extern "C" int dr_debug_tbuf_gemm(long long* out, int n);
 extern "C" void dr_debug_tile_variant(int v);
+extern "C" void dr_debug_skinny_variant(int v);
 
 // one more launch, then the per-phase times of wave 0 of each workgroup
 // (relative to its own start) averaged over the workgroups that wrote them
@@ -364,6 +365,24 @@ int main(int argc, char** argv) {
     snprintf(buf, sizeof buf, "NN plain M%d N%d K%d", sh[0], sh[1], sh[2]);
     timeit(buf, [&](hipStream_t st) { gemm_launch(G_NN, AM_PLAIN, &gk, 1, st); }, s);
   }
+  // per-step shapes of the imagination / BPTT chain, both row-tile variants
+  for (int var = 0; var < 3; var += 2) {
+    dr_debug_skinny_variant(var);
+    int sh2[][3] = {{64, 1027, 1800}, {64, 600, 1800}, {64, 200, 1624}, {64, 1024, 200}, {64, 200, 1024}};
+    for (auto& sh : sh2) {
+      GemmArgs g = nt_(sh[0], sh[1], sh[2]);
+      snprintf(buf, sizeof buf, "s%d NT plain M%d N%d K%d", var, sh[0], sh[1], sh[2]);
+      timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, &g, 1, st); }, s);
+    }
+    GemmArgs gp[2] = {nt_(64, 1027, 1800), nt_(64, 600, 1800)};
+    snprintf(buf, sizeof buf, "s%d NT plain grouped BPTT gZ+gH", var);
+    timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, gp, 2, st); }, s);
+    GemmArgs gb2 = nt_(64, 1624, 200);
+    gb2.ln_g = lng; gb2.ln_b = lnb; gb2.pre = X; gb2.ld_pre = 200;
+    snprintf(buf, sizeof buf, "s%d NT lnbwd M64 N1624 K200", var);
+    timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_LNBWD, &gb2, 1, st); }, s);
+  }
+  dr_debug_skinny_variant(0);
   // mid-size shapes (tile GEMM, split-K scratch when given)
   {
     float* skw = frand((size_t)8 << 20);
