@@ -64,8 +64,14 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
     pix[i] = 2 * ox - 1;
   }
 
-  float4 ra[APT], rb[BPT];
-  auto load = [&](int k0) {
+  // register ring: the global loads of chunk c+PIPE are issued while chunk c
+  // computes (an L2/HBM round trip outlasts one chunk's MFMAs)
+  constexpr int NCH = K / CBK;
+  constexpr int PIPE = NCH >= 8 ? 3 : 1;
+  float4 ra_[PIPE][APT], rb_[PIPE][BPT];
+  auto load = [&](int k0, int sl) {
+    float4* ra = ra_[sl];
+    float4* rb = rb_[sl];
     const int k = k0 + 4 * quad;
     const int tap = k / CIN, ci = k - tap * CIN;
     const int ky = tap >> 2, kx = tap & 3;
@@ -84,7 +90,9 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int sl, int buf) {
+    const float4* ra = ra_[sl];
+    const float4* rb = rb_[sl];
 #pragma unroll
     for (int i = 0; i < APT; ++i) *reinterpret_cast<float4*>(&As[buf][prow + 32 * i][4 * quad]) = ra[i];
 #pragma unroll
@@ -100,41 +108,52 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  load(0);
-  store(0);
+#pragma unroll
+  for (int u = 0; u < PIPE; ++u)
+    if (u < NCH) load(u * CBK, u);
+  store(0, 0);
   __syncthreads();
-  constexpr int NCH = K / CBK;
-  for (int c = 0; c < NCH; ++c) {
-    const int buf = c & 1;
-    if (c + 1 < NCH) load((c + 1) * CBK);
+  if (PIPE == 1 && NCH > 1) load(CBK, 0);
+  for (int cb = 0; cb < NCH; cb += PIPE) {
 #pragma unroll
-    for (int s = 0; s < CBK; s += 16) {
-      float4 a[FM], b[FN];
+    for (int u = 0; u < PIPE; ++u) {
+      const int c = cb + u;  // slot of chunk c is u (cb is a multiple of PIPE)
+      if (c >= NCH) break;
+      const int buf = c & 1;
+      // slot u was stored to LDS at the end of the previous chunk: refill it
+      if (PIPE > 1 && c + PIPE < NCH) load((c + PIPE) * CBK, u);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const float4*>(&As[buf][wm0 + 16 * i + r][s + 4 * q]);
+      for (int s = 0; s < CBK; s += 16) {
+        float4 a[FM], b[FN];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const float4*>(&Bs[buf][wn0 + 16 * j + r][s + 4 * q]);
-      // k-step outer, independent accumulators inner: consecutive MFMAs never
-      // wait on each other's result (40-cycle latency vs 32-cycle issue)
+        for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const float4*>(&As[buf][wm0 + 16 * i + r][s + 4 * q]);
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const float4*>(&Bs[buf][wn0 + 16 * j + r][s + 4 * q]);
+        // k-step outer, independent accumulators inner: consecutive MFMAs never
+        // wait on each other's result (40-cycle latency vs 32-cycle issue)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+      }
+      if (c + 1 < NCH) {
+        store((u + 1) % PIPE, buf ^ 1);
+        if (PIPE == 1 && c + 2 < NCH) load((c + 2) * CBK, 0);
+      }
+      dr_lds_barrier();
     }
-    if (c + 1 < NCH) store(buf ^ 1);
-    dr_lds_barrier();
   }
 
 #pragma unroll
@@ -163,6 +182,12 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
       }
 }
 
+// Extra dynamic LDS per conv workgroup (bytes).  Padding past half the CU's
+// LDS leaves one conv workgroup per CU, so that latency-bound kernels of a
+// concurrent stream find room beside it (pipelined epochs, engine.py).
+static int g_conv_lds_pad = 0;
+extern "C" void dr_set_conv_lds_pad(int bytes) { g_conv_lds_pad = bytes < 0 ? 0 : bytes; }
+
 template <int BM, int BN, int CIN, bool OUT_NCHW, int EPI>
 static int launch_conv(int n, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
                        float* out, float* pre, hipStream_t s) {
@@ -173,8 +198,14 @@ static int launch_conv(int n, int ih, int iw, int cout, const float* in, const f
     return DR_E_INVALID;
   }
   dim3 grid((unsigned)dr_xcd_grid((int)tiles));
-  hipLaunchKernelGGL((k_conv_nhwc<BM, BN, CIN, OUT_NCHW, EPI>), grid, dim3(256), 0, s, n, ih, iw, cout, in, wr,
-                     bias, out, pre);
+  static bool raised = [] {
+    (void)hipFuncSetAttribute((const void*)k_conv_nhwc<BM, BN, CIN, OUT_NCHW, EPI>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    return true;
+  }();
+  (void)raised;
+  hipLaunchKernelGGL((k_conv_nhwc<BM, BN, CIN, OUT_NCHW, EPI>), grid, dim3(256), g_conv_lds_pad, s, n, ih, iw, cout,
+                     in, wr, bias, out, pre);
   return dr_check_launch("conv");
 }
 

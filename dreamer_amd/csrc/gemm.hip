@@ -1002,6 +1002,14 @@ __global__ __launch_bounds__(256) void k_gemm_tile(GemmBatch gb, int splits) {
   static_assert(APT >= 1 && BPT >= 1 && AKS >= 1 && BKS >= 1, "tile");
   static_assert(A_KM ? APTT == APT : true, "loader");
   static_assert(B_KN ? BPTT == BPT : true, "loader");
+  // transposed (KM / KN) operands: float4 loads along m / n where this
+  // problem's strides and bases allow (decided per problem, wave-uniform)
+  const bool v4a = A_KM && (lda & 3) == 0 && (((uintptr_t)A) & 15) == 0;
+  const float* W2u = dr_uni(g.W2);
+  const int nsB = dr_uni(g.nsplitB);
+  const bool v4b = B_KN && (ldb & 3) == 0 && (((uintptr_t)W) & 15) == 0 &&
+                   (W2u == nullptr || (((int)g.ldb2 & 3) == 0 && (((uintptr_t)W2u) & 15) == 0 &&
+                                       (nsB >= N || (nsB & 3) == 0)));
   // register ring: chunk loads are issued PIPE chunks ahead of their use
   constexpr int PIPE = 3;
   float4 ra[PIPE][APT], rb[PIPE][BPT];
@@ -1031,7 +1039,7 @@ __global__ __launch_bounds__(256) void k_gemm_tile(GemmBatch gb, int splits) {
         }
       } else {
         const int kk = tid / AR4 + AKS * i, k = k0 + kk, m = m0 + 4 * (tid % AR4);
-        if (VEC && k < K && m + 3 < M) {
+        if (v4a && k < K && m + 3 < M) {
           ra[sl][i] = dr_ld4(A, (unsigned)(k * lda + m));
         } else {
           float* v = &ra[sl][i].x;
@@ -1055,8 +1063,8 @@ __global__ __launch_bounds__(256) void k_gemm_tile(GemmBatch gb, int splits) {
         }
       } else {
         const int kk = tid / BR4 + BKS * i, k = k0 + kk, n = n0 + 4 * (tid % BR4);
-        if (VEC && k < K && n + 3 < N) {
-          // 4 columns in one segment (the host checked nsplitB % 4 == 0, ldb2 % 4 == 0)
+        if (v4b && k < K && n + 3 < N) {
+          // 4 columns in one segment (nsplitB % 4 == 0, ldb2 % 4 == 0: v4b)
           if (k >= g.ksplitB) rb[sl][i] = dr_ld4(g.W2 + (long long)(k - g.ksplitB) * g.ldb2, (unsigned)n);
           else if (n >= g.nsplitB) rb[sl][i] = dr_ld4(g.W2 + (long long)k * g.ldb2, (unsigned)(n - g.nsplitB));
           else rb[sl][i] = dr_ld4(W, (unsigned)(k * ldb + n));
@@ -1317,15 +1325,8 @@ static void launch_tile2(GemmBatch& gb, int count, hipStream_t s) {
     if (!A_KM) {
       vec = vec && g.K % 4 == 0 && g.lda % 4 == 0 && aligned16(g.A);
       if (g.ksplitA < g.K) vec = vec && g.lda2 % 4 == 0 && g.ksplitA % 4 == 0 && aligned16(g.A2);
-    } else {
-      vec = vec && g.lda % 4 == 0 && aligned16(g.A);
     }
-    if (!B_KN) {
-      vec = vec && g.ldb % 4 == 0 && aligned16(g.W);
-    } else {
-      vec = vec && g.ldb % 4 == 0 && aligned16(g.W);
-      if (g.W2) vec = vec && g.ldb2 % 4 == 0 && aligned16(g.W2) && (g.nsplitB >= g.N || g.nsplitB % 4 == 0);
-    }
+    if (!B_KN) vec = vec && g.ldb % 4 == 0 && aligned16(g.W);
     ws = ws && g.splitk_ws != nullptr;
   }
   if (maxt == 0) return;

@@ -284,6 +284,13 @@ int dr_replay_gather(long long cap, int B, int S, int frame_elems, int A, const 
 /* Philox offset bump (keeps graph replays drawing fresh noise) */
 int dr_rng_advance(unsigned long long* rng, unsigned long long delta, hipStream_t stream);
 
+/* Occupancy of the conv encoder kernels (dr_encoder_features, the world-model
+ * step's convolutions): extra dynamic LDS per workgroup, in bytes, applied to
+ * launches made (or graph-captured) after the call.  0 (default) = densest
+ * packing; padding past half the CU's LDS keeps one conv workgroup per CU so a
+ * concurrent stream's latency-bound kernels find room (pipelined epochs). */
+void dr_set_conv_lds_pad(int bytes);
+
 #ifdef __cplusplus
 }
 #endif

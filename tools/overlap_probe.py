@@ -99,29 +99,23 @@ def main():
                     run_chain()
         return f
 
-    lo, hi = torch.cuda.Stream(dev), torch.cuda.Stream(dev, priority=-1)
-    hi2 = torch.cuda.Stream(dev, priority=-1)
-    warm = lambda: (genc.replay(), gscan.replay())
-    out["warm|chain plain"] = timed(two(lo, torch.cuda.Stream(dev), warm, run_chain))
-    out["warm|chain(hi)"] = timed(two(lo, hi, warm, run_chain))
-    out["enc|scan+chain(hi)"] = timed(two(lo, hi, genc.replay, lambda: (gscan.replay(), run_chain())))
-    out["enc|scan(hi)|chain(hi)"] = timed(three(lo, hi, hi2))
-    print(json.dumps(out), flush=True)
-    for k in (2, 4, 8, 12, 16):
-        lat = [i for i in range(256) if i % 32 < k]
-        rest = [i for i in range(256) if i % 32 >= k]
-        s_lat, s_lat2, s_rest, s_all = masked_stream(lat), masked_stream(lat), masked_stream(rest), \
-            masked_stream(range(256))
-        with torch.cuda.stream(s_lat):
-            out[f"chain@{k}/xcc"] = timed(lambda: [run_chain() for _ in range(N)])
-            out[f"scan@{k}/xcc"] = timed(lambda: [gscan.replay() for _ in range(N)])
-        with torch.cuda.stream(s_rest):
-            out[f"enc@{32 - k}/xcc"] = timed(lambda: [genc.replay() for _ in range(N)])
-        out[f"warm@rest|chain@{k}"] = timed(two(s_rest, s_lat, warm, run_chain))
-        out[f"enc@rest|scan+chain@{k}"] = timed(two(s_rest, s_lat, genc.replay, lambda: (gscan.replay(), run_chain())))
-        out[f"enc@rest|scan@{k}|chain@{k}"] = timed(three(s_rest, s_lat, s_lat2))
-        out[f"enc@all|scan@{k}|chain@{k}"] = timed(three(s_all, s_lat, s_lat2))
+    for nch in [int(x) for x in os.environ.get("CHUNKS", "2,4,8").split(",")]:
+        ge = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(cap):
+            with torch.cuda.graph(ge, stream=cap):
+                for t0, t1 in eng.warm_chunks(eng.T, (eng.T + nch - 1) // nch):
+                    eng._encode_chunk(t0, t1, cap.cuda_stream)
+        torch.cuda.synchronize()
+        warm = lambda: (ge.replay(), gscan.replay())
+        out[f"chunks{nch} enc"] = timed(lambda: [ge.replay() for _ in range(N)])
+        out[f"chunks{nch} warm|chain"] = timed(two(torch.cuda.Stream(dev), torch.cuda.Stream(dev), warm, run_chain))
+        out[f"chunks{nch} warm|chain(hi)"] = timed(two(torch.cuda.Stream(dev), torch.cuda.Stream(dev, priority=-1),
+                                                       warm, run_chain))
         print(json.dumps(out), flush=True)
+    # the scan alone beside the chain, and the encoder alone beside the chain
+    out["scan|chain"] = timed(two(torch.cuda.Stream(dev), torch.cuda.Stream(dev), gscan.replay, run_chain))
+    out["enc|chain"] = timed(two(torch.cuda.Stream(dev), torch.cuda.Stream(dev), genc.replay, run_chain))
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
