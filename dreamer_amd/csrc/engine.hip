@@ -399,9 +399,20 @@ extern "C" int dr_imagine_bwd(const dr_dims* d, const dr_world_model* wm, const 
     const bool state_grad = upstream_state || t < H - 1;
     if (state_grad) {
       // z_{t+1} = STE(prior(h_{t+1}))   (DynamicsPredictors.py:31-40)
-      DR_TRY(op_softmax_ste_bwd(B, d->rows, d->cols, gZ_n, ldL, tp.soft + (long long)t * B * L, L, w.glog, s));
       const int h1 = d->prior_h1, h2 = d->prior_h2;
-      DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, h2, L, w.glog, L, w.tl6p, w.gx2, h2, 0), s));
+      const int gl = d->cols / 4;
+      if (B <= 64 && L <= 1024 && d->cols % 4 == 0 && gl <= 64 && (gl & (gl - 1)) == 0) {
+        // straight-through softmax backward fused into the prior head's
+        // input-gradient GEMM (its A-operand prologue)
+        GemmArgs g = bwd_nt(B, h2, L, gZ_n, ldL, w.tl6p, w.gx2, h2, 0);
+        g.pre = tp.soft + (long long)t * B * L;
+        g.ld_pre = L;
+        g.C = d->cols;
+        DR_TRY(run(G_NT, AM_STEBWD, g, s));
+      } else {
+        DR_TRY(op_softmax_ste_bwd(B, d->rows, d->cols, gZ_n, ldL, tp.soft + (long long)t * B * L, L, w.glog, s));
+        DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, h2, L, w.glog, L, w.tl6p, w.gx2, h2, 0), s));
+      }
       // dynamic_predictor.4/.3 and .1/.0: LN-SiLU backward fused into the next input-gradient GEMM
       DR_TRY(lnbwd_nt(B, h1, h2, w.gx2, h2, tp.pre2p + (long long)t * B * h2, h2, wm->prior.n4, w.tl3p, w.gx1, h1, 0,
                       w.gp2, h2, nullptr, nullptr, nullptr, 0, INT_MAX, s));
@@ -424,12 +435,10 @@ extern "C" int dr_imagine_bwd(const dr_dims* d, const dr_world_model* wm, const 
     // actor at step t: heads, then base_net (Agent.py:191-210)
     const long long ot = (long long)t * A;
     float* gh_t = w.gheads + (long long)t * 2 * A;
-    DR_TRY(op_actor_head_bwd(B, A, w.gA + ot, ldA, g_mus ? g_mus + ot : nullptr, g_sigmas ? g_sigmas + ot : nullptr,
-                             ldA, actions + ot, ldA, nullptr, 0, tp.ls_raw + ot, ldA, tp.eps + (long long)t * B * A,
-                             gh_t, (long long)H * 2 * A, s));
-    {
-      DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(B, a2, 2 * A, gh_t, (long long)H * 2 * A, w.thead, w.gx2a, a2, 0), s));
-    }
+    // head backward + its input gradient (K = 2A) in one launch
+    DR_TRY(op_actor_head_bwd_x(B, A, a2, w.gA + ot, ldA, g_mus ? g_mus + ot : nullptr,
+                               g_sigmas ? g_sigmas + ot : nullptr, ldA, actions + ot, ldA, tp.ls_raw + ot, ldA,
+                               tp.eps + (long long)t * B * A, gh_t, (long long)H * 2 * A, w.thead, w.gx2a, a2, s));
     const long long o2 = (long long)t * a2, o1 = (long long)t * a1;
     // base_net.4/.3: LN-SiLU backward fused into the .3 input-gradient GEMM; the
     // prologue also writes g_pre and the LN-parameter saves for the weight grads

@@ -7,7 +7,11 @@
 #pragma once
 #include "common.h"
 
-enum { AM_PLAIN = 0, AM_LNSILU = 1, AM_CONV = 2, AM_CONV_SRC = 3, AM_LNBWD = 4 };
+enum { AM_PLAIN = 0, AM_LNSILU = 1, AM_CONV = 2, AM_CONV_SRC = 3, AM_LNBWD = 4, AM_STEBWD = 5 };
+// AM_STEBWD (NT skinny only): A = d/d(logits) of the straight-through
+// categorical sample (DynamicsPredictors.py:31-40) given dL/dz = A-argument
+// rows and the unimixed softmax `pre` rows: per group of C classes,
+// a = s * (0.99 g - sum_group(0.99 g * s))  (ops.hip k_softmax_ste_bwd).
 // AM_LNBWD (NT skinny only): A = d/d(pre) of SiLU(LayerNorm(pre)) given the
 // upstream gradient gx = A-argument rows; the LN input `pre` and gamma/beta
 // (ln_g/ln_b) come from the fields below.  a_out receives g_pre, sv_gy /

@@ -425,7 +425,8 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
   const bool store_a = (a_out != nullptr) && (tn == 0);
   // (measured: staging pays only where the LayerNorm needs the barrier anyway;
   // a plain GEMM is faster with direct fragment loads, profiles/r01_v5_kbench.txt)
-  const bool staged = (AMODE == AM_LNSILU || AMODE == AM_LNBWD) && VEC && !B_KN && (K4 <= 64 * SV) &&
+  const bool staged = (AMODE == AM_LNSILU || AMODE == AM_LNBWD || AMODE == AM_STEBWD) && VEC && !B_KN &&
+                     (K4 <= 64 * SV) &&
                      ((MT + NT) * KP <= SK_LN_MAXF);
   // with few accumulator tiles, alternate 16-k chunks between two accumulator
   // sets so consecutive MFMAs are independent (40-cycle result latency)
@@ -439,7 +440,7 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
   if (staged) {
     float* sA = smem;
     float* sB = smem + MT * KP;
-    constexpr int PRW = (AMODE == AM_LNBWD) ? RPW : 1;
+    constexpr int PRW = (AMODE == AM_LNBWD || AMODE == AM_STEBWD) ? RPW : 1;
     float4 xa[RPW][SV], xb[BPW][SV], gv[SV], bv[SV], xp[PRW][SV];
     const float* lg = dr_uni(g.ln_g);
     const float* lb = dr_uni(g.ln_b);
@@ -459,7 +460,7 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
         const unsigned e = ok ? (unsigned)(seg1 ? m * o.lda + k : m * o.lda2 + k - o.ksA) : 0u;
         xa[rr][i] = dr_ld4(ok ? base : o.W, e);
         if (!ok) xa[rr][i] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (AMODE == AM_LNBWD) {
+        if (AMODE == AM_LNBWD || AMODE == AM_STEBWD) {
           xp[rr][i] = dr_ld4(pre, ok ? (unsigned)(m * ld_pre + k) : 0u);
           if (!ok) xp[rr][i] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -507,6 +508,25 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
           x.y = dr_silu_fast((x.y - mean) * rstd * gv[i].y + bv[i].y);
           x.z = dr_silu_fast((x.z - mean) * rstd * gv[i].z + bv[i].z);
           x.w = dr_silu_fast((x.w - mean) * rstd * gv[i].w + bv[i].w);
+          if (m >= M) x = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+      if (AMODE == AM_STEBWD) {
+        // straight-through softmax backward: a group of C classes is C/4
+        // consecutive lanes of one float4 chunk (K % C == 0, host-checked)
+        const int gl = dr_uni(g.C) >> 2;
+#pragma unroll
+        for (int i = 0; i < SV; ++i) {
+          if (64 * i >= K4) break;
+          float4& x = xa[rr][i];
+          const float4& sv = xp[rr][i];
+          const float gx = 0.99f * x.x, gy = 0.99f * x.y, gz = 0.99f * x.z, gw = 0.99f * x.w;
+          float dot = (gx * sv.x + gy * sv.y) + (gz * sv.z + gw * sv.w);
+          for (int o = 1; o < gl; o <<= 1) dot += __shfl_xor(dot, o, 64);
+          x.x = sv.x * (gx - dot);
+          x.y = sv.y * (gy - dot);
+          x.z = sv.z * (gz - dot);
+          x.w = sv.w * (gw - dot);
           if (m >= M) x = make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
@@ -1220,7 +1240,8 @@ static size_t skinny_lds_floats(const GemmBatch& gb, int count, bool vec) {
   for (int i = 0; i < count; ++i) {
     const size_t K = gb.p[i].K, KP = K + ((8 - (K & 15)) & 15);
     const size_t staged = (size_t)(MT + NT) * KP, rows = (size_t)MT * KP;
-    if ((AMODE == AM_LNSILU || AMODE == AM_LNBWD) && !B_KN && K / 4 <= 64 * (MT == 16 ? 4 : 1) &&
+    if ((AMODE == AM_LNSILU || AMODE == AM_LNBWD || AMODE == AM_STEBWD) && !B_KN &&
+        K / 4 <= 64 * (MT == 16 ? 4 : 1) &&
         staged <= SK_LN_MAXF)
       need = std::max(need, staged);  // kernel's `staged`
     else if (AMODE == AM_LNSILU && rows <= SK_LN_MAXF && K / 4 <= 64 * (MT == 16 ? 8 : 2))
@@ -1386,6 +1407,11 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
     dr_set_error("gemm: LayerNorm-backward prologue needs the staged NT skinny path");
     return;
   }
+  if (AMODE == AM_STEBWD) {
+    if (!A_KM && !B_KN && try_skinny<AM_STEBWD, false>(gb, count, s)) return;
+    dr_set_error("gemm: softmax-STE-backward prologue needs the staged NT skinny path");
+    return;
+  }
   if (!A_KM && (AMODE == AM_PLAIN || AMODE == AM_LNSILU)) {
     if (try_skinny<(AMODE == AM_LNSILU ? AM_LNSILU : AM_PLAIN), B_KN>(gb, count, s)) return;
   }
@@ -1444,6 +1470,22 @@ int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hip
             }
           }
           launch_pick<AM_LNBWD, false, false>(gb, count, s);
+          break;
+        }
+        case AM_STEBWD: {
+          for (int i = 0; i < count; ++i) {
+            const GemmArgs& g = probs[i];
+            const int lim = (g.M <= 64) ? 1024 : 256;
+            const int gl = g.C / 4;
+            if (g.K % 4 || g.K > lim || g.lda % 4 || g.ld_pre % 4 || g.ldb % 4 || g.C < 4 || g.C % 4 ||
+                (gl & (gl - 1)) || gl > 64 || g.K % g.C || g.M > 64 ||
+                ((uintptr_t)g.A | (uintptr_t)g.pre | (uintptr_t)g.W) & 15) {
+              dr_set_error("gemm_launch: AM_STEBWD needs M <= 64, K %% C == 0, C/4 a power of two, K <= %d, "
+                           "16-byte aligned rows (K=%d C=%d)", lim, g.K, g.C);
+              return DR_E_INVALID;
+            }
+          }
+          launch_pick<AM_STEBWD, false, false>(gb, count, s);
           break;
         }
         default: dr_set_error("gemm_launch: bad amode"); return DR_E_INVALID;

@@ -41,6 +41,10 @@ int op_sigmoid(int M, const float* x, long long ldx, float* out, long long ostri
 int op_actor_head(int M, int A, const float* mu_raw, long long ldm, const float* ls_raw, long long ldl,
                   const dr_noise* nz, int step, int deterministic, float* a, long long lda, float* mu,
                   long long ldmu, float* sigma, long long lds, float* eps_save, hipStream_t s);
+int op_actor_head_bwd_x(int M, int A, int N, const float* g_a, long long ldga, const float* g_mu_l,
+                        const float* g_sig_l, long long ldgl, const float* a, long long lda, const float* ls_raw,
+                        long long ldl, const float* eps, float* g_heads, long long ldh, const float* wt, float* gx,
+                        long long ldx, hipStream_t s);
 int op_actor_head_bwd(int M, int A, const float* g_a, long long ldga, const float* g_mu_l, const float* g_sig_l,
                       long long ldgl, const float* a, long long lda, const float* sigma, long long lds,
                       const float* ls_raw, long long ldl, const float* eps, float* g_heads, long long ldh,

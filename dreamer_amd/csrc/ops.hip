@@ -528,6 +528,78 @@ int op_actor_head_bwd(int M, int A, const float* g_a, long long ldga, const floa
   return dr_check_launch("actor_head_bwd");
 }
 
+// The same head backward fused with the input gradient of the stacked
+// mu / log-sigma heads: gx[m][n] = sum_k g_heads[m][k] * wt[n][k] (wt = the
+// heads' weights transposed, [N][2A]).  A block owns 16 rows x 64 columns:
+// it forms the 16 x 2A head gradients in LDS (the blockIdx.x == 0 column of
+// blocks also stores them for the weight gradients), then its outputs.
+__global__ __launch_bounds__(256) void k_actor_head_bwd_x(int M, int A, int N, const float* g_a, long long ldga,
+                                                          const float* g_mu_l, const float* g_sig_l, long long ldgl,
+                                                          const float* a, long long lda, const float* ls_raw,
+                                                          long long ldl, const float* eps, float* g_heads,
+                                                          long long ldh, const float* wt, float* gx, long long ldx) {
+  __shared__ float gh[16][2 * 8];
+  const int m0 = blockIdx.y * 16, n0 = blockIdx.x * 64, tid = threadIdx.x;
+  // weights of this thread's column, issued first
+  const int nl = tid & 63, mq = tid >> 6;  // column, row quarter (4 rows each)
+  const int n = n0 + nl;
+  float w[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = (k < 2 * A && n < N) ? wt[(long long)n * 2 * A + k] : 0.f;
+  if (tid < 16 * A) {
+    const int ml = tid / A, k = tid - ml * A, m = m0 + ml;
+    float gmu = 0.f, gls = 0.f;
+    if (m < M) {
+      gmu = g_mu_l ? g_mu_l[(long long)m * ldgl + k] : 0.0f;
+      float gsg = g_sig_l ? g_sig_l[(long long)m * ldgl + k] : 0.0f;
+      if (g_a) {
+        const float av = a[(long long)m * lda + k];
+        const float gp = g_a[(long long)m * ldga + k] * (1.0f - av * av);
+        gmu = gmu + gp;
+        gsg = gsg + gp * eps[(long long)m * A + k];
+      }
+      const float lr = ls_raw[(long long)m * ldl + k];
+      const float lc = fminf(fmaxf(lr, -5.0f), 2.0f);
+      if (lr >= -5.0f && lr <= 2.0f) {
+        const float ez = expf(lc);
+        gls = (lc > 20.0f) ? gsg : gsg * ez / (ez + 1.0f);
+      }
+      if (blockIdx.x == 0) {
+        g_heads[(long long)m * ldh + k] = gmu;
+        g_heads[(long long)m * ldh + A + k] = gls;
+      }
+    }
+    gh[ml][k] = gmu;
+    gh[ml][A + k] = gls;
+  }
+  __syncthreads();
+  if (n >= N) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ml = 4 * mq + i, m = m0 + ml;
+    if (m >= M) break;
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k < 2 * A) v = fmaf(gh[ml][k], w[k], v);
+    gx[(long long)m * ldx + n] = v;
+  }
+}
+
+int op_actor_head_bwd_x(int M, int A, int N, const float* g_a, long long ldga, const float* g_mu_l,
+                        const float* g_sig_l, long long ldgl, const float* a, long long lda, const float* ls_raw,
+                        long long ldl, const float* eps, float* g_heads, long long ldh, const float* wt, float* gx,
+                        long long ldx, hipStream_t s) {
+  if (M == 0) return DR_OK;
+  if (A > 8) {
+    dr_set_error("actor_head_bwd_x: at most 8 actions");
+    return DR_E_INVALID;
+  }
+  hipLaunchKernelGGL(k_actor_head_bwd_x, dim3(dr_cdiv(N, 64), dr_cdiv(M, 16)), dim3(256), 0, s, M, A, N, g_a, ldga,
+                     g_mu_l, g_sig_l, ldgl, a, lda, ls_raw, ldl, eps, g_heads, ldh, wt, gx, ldx);
+  return dr_check_launch("actor_head_bwd_x");
+}
+
 // ---------------------------------------------------------------------------
 // lambda returns (Agent.py:156-172), one thread per batch row
 // ---------------------------------------------------------------------------
