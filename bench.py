@@ -29,7 +29,7 @@ HBM_PEAK_GBS = 8000.0
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_traffic.json")
 # SURVEY.md §8d figure of record: necessary dense FLOPs per imagined step at
 # 64x64, S=64, H=15 (warm start 131.07 + dream 8.88 + update 11.17 MFLOP)
-PATH_MFLOP_PER_STEP = {(64, 15): 151.12, (50, 15): 122.36}
+PATH_MFLOP_PER_STEP = {(64, 15, 64): 151.12, (50, 15, 64): 122.36, (64, 20, 128): 383.00}
 
 CAR_RACER = dict(
     hidden_state_dims=600, latent_state_dims=[32, 32], action_dims=3, observation_dims=[64, 64],
@@ -189,7 +189,8 @@ def cpu_baseline(cfg, B, S, H, budget_s=15.0, threads=None):
             break
     return dict(value=B * H * n / el, unit="imagined latent-steps/s", cores=threads, kind="port",
                 sample=f"{n} reference-faithful train_Agent epochs (oracle CPU restatement, fp32, warm-start "
-                       f"backward included) at B={B} S={S} H={H} 64x64x3, {el:.1f} s on {threads} threads")
+                       f"backward included) at B={B} S={S} H={H} {c['observation_dims'][0]}x{c['observation_dims'][1]}x3, "
+                       f"{el:.1f} s on {threads} threads")
 
 
 def main():
@@ -200,6 +201,9 @@ def main():
     ap.add_argument("--batch", type=int, default=64, help="imagination rows per GPU (configs[1]: 64)")
     ap.add_argument("--seq", type=int, default=64)
     ap.add_argument("--horizon", type=int, default=15)
+    ap.add_argument("--res", type=int, default=64,
+                    help="frame side (64: CarRacing configs[1]; 128: configs[3]'s frames with the reference's "
+                         "4-conv encoder -- the 'deeper VAE' is not in the reference)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--phases", action="store_true", help="print per-phase ms to stderr")
@@ -227,7 +231,7 @@ def main():
     from dreamer_amd.engine import ImaginationEngine
     B, S, H = args.batch, args.seq, args.horizon
     cfg = dict(CAR_RACER)
-    cfg.update(batch_size=B, sequence_length=S, horizon=H)
+    cfg.update(batch_size=B, sequence_length=S, horizon=H, observation_dims=[args.res, args.res])
     torch.manual_seed(0)
     d = Dreamer(cfg, dev)
     n_rep = max(4096, 8 * S)
@@ -316,7 +320,8 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"Dreamer.train_Agent epoch (replay sample + warm start S/2 + H-step imagination + "
-                               f"actor-critic update), B={B}/GPU S={S} H={H} 64x64x3 (BASELINE configs[1])",
+                               f"actor-critic update), B={B}/GPU S={S} H={H} {args.res}x{args.res}x3"
+                               + (" (BASELINE configs[1])" if (args.res, B, S, H) == (64, 64, 64, 15) else ""),
                    "global_batch": B * world, "seq_len": S, "horizon": H, "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": f"encoder conv stack + feature projection ({len(eng.chunks)} time chunks x 5 launches)",
                      "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -332,7 +337,7 @@ def main():
                    "sequential_value": round(world * B * H * args.steps / el_seq, 1),
                    "sequential_ms_per_step": round(el_seq / args.steps * 1e3, 4)},
     }
-    mf = PATH_MFLOP_PER_STEP.get((S, H))
+    mf = PATH_MFLOP_PER_STEP.get((S, H, args.res))
     if mf is not None:
         tf = value * mf * 1e6 / 1e12
         out["path_roofline"] = {"bound": "mfma", "achieved": round(tf, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
@@ -357,7 +362,7 @@ def main():
                                "note": "1 WM step + 1 train_Agent epoch per iteration (WM_epochs = AC_epochs = 1)"},
         }
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(CAR_RACER, B, S, H, budget_s=args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(cfg, B, S, H, budget_s=args.cpu_budget)
     print(json.dumps(out), flush=True)
     if world > 1:
         barrier()
