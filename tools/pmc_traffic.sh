@@ -8,8 +8,8 @@ R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $R/gpurun_out/pmc_$c$TAG -o p \
-    -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/pmc_$c$TAG.log 2>&1 \
+    -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --wm-steps 0 > $R/gpurun_out/pmc_$c$TAG.log 2>&1 \
     || { tail -20 $R/gpurun_out/pmc_$c$TAG.log; exit 1; }
 done
-cd $R && python3 tools/pmc_traffic.py gpurun_out/pmc_FETCH_SIZE$TAG gpurun_out/pmc_WRITE_SIZE$TAG > gpurun_out/traffic$TAG.txt
+cd $R && python3 tools/pmc_traffic.py gpurun_out/pmc_FETCH_SIZE$TAG gpurun_out/pmc_WRITE_SIZE$TAG --json gpurun_out/traffic$TAG.json > gpurun_out/traffic$TAG.txt
 cat gpurun_out/traffic$TAG.txt
