@@ -86,6 +86,9 @@ _SIGS = {
                             fp, fp, fp, fp, fp, fp, fp, fp, fp, _sz, fp]),
     "dr_imagine_bwd": (_i, [_P(dr_dims), _P(dr_world_model), _P(dr_actor), _i, _i, fp, fp, fp, fp, fp,
                             fp, fp, fp, fp, _P(dr_actor), fp, _sz, fp]),
+    "dr_imagine_bwd_prep": (_i, [_P(dr_dims), _P(dr_world_model), _P(dr_actor), _i, _i, fp, fp, fp, fp, _sz, fp]),
+    "dr_imagine_bwd_main": (_i, [_P(dr_dims), _P(dr_world_model), _P(dr_actor), _i, _i, fp, fp, fp, fp, fp, _i,
+                                 fp, _P(dr_actor), fp, _sz, fp]),
     "dr_step_workspace_bytes": (_sz, [_P(dr_dims), _i]),
     "dr_imagine_step": (_i, [_P(dr_dims), _P(dr_world_model), _i, fp, fp, fp, dr_noise, fp, fp, fp, fp,
                              fp, _sz, fp]),

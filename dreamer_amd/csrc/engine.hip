@@ -346,24 +346,63 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
   return DR_OK;
 }
 
+// part 1 of the backward: upstream state gradients into the workspace and the
+// transposed weights (independent of dL/dmus, dL/dsigmas: may run early, on
+// another stream).  part 2 (main) is the reverse loop + weight gradients.
+static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, int B, int H,
+                            const float* latents, const float* hiddens, const float* actions,
+                            const float* g_mus, const float* g_sigmas,
+                            const float* g_actions, const float* g_latents, const float* g_hiddens,
+                            const void* tape, const dr_actor* gr, void* ws, size_t ws_bytes, hipStream_t s,
+                            bool do_prep, bool do_main);
+
 extern "C" int dr_imagine_bwd(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, int B, int H,
                               const float* latents, const float* hiddens, const float* actions,
                               const float* g_mus, const float* g_sigmas,
                               const float* g_actions, const float* g_latents, const float* g_hiddens,
                               const void* tape, const dr_actor* gr, void* ws, size_t ws_bytes, hipStream_t s) {
-  DR_REQUIRE(d && wm && ac && latents && hiddens && actions && tape && gr && B > 0 && H > 0,
-             "null argument or empty batch");
+  return imagine_bwd_impl(d, wm, ac, B, H, latents, hiddens, actions, g_mus, g_sigmas, g_actions, g_latents,
+                          g_hiddens, tape, gr, ws, ws_bytes, s, true, true);
+}
+
+extern "C" int dr_imagine_bwd_prep(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, int B, int H,
+                                   const float* g_actions, const float* g_latents, const float* g_hiddens, void* ws,
+                                   size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(d && wm && ac && B > 0 && H > 0, "null argument or empty batch");
+  return imagine_bwd_impl(d, wm, ac, B, H, nullptr, nullptr, nullptr, nullptr, nullptr, g_actions, g_latents,
+                          g_hiddens, nullptr, nullptr, ws, ws_bytes, s, true, false);
+}
+
+extern "C" int dr_imagine_bwd_main(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, int B, int H,
+                                   const float* latents, const float* hiddens, const float* actions,
+                                   const float* g_mus, const float* g_sigmas, int upstream_state, const void* tape,
+                                   const dr_actor* gr, void* ws, size_t ws_bytes, hipStream_t s) {
+  const float* flag = upstream_state ? reinterpret_cast<const float*>(ws) : nullptr;  // non-NULL marker only
+  return imagine_bwd_impl(d, wm, ac, B, H, latents, hiddens, actions, g_mus, g_sigmas, nullptr, flag, nullptr, tape,
+                          gr, ws, ws_bytes, s, false, true);
+}
+
+static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, int B, int H,
+                            const float* latents, const float* hiddens, const float* actions,
+                            const float* g_mus, const float* g_sigmas,
+                            const float* g_actions, const float* g_latents, const float* g_hiddens,
+                            const void* tape, const dr_actor* gr, void* ws, size_t ws_bytes, hipStream_t s,
+                            bool do_prep, bool do_main) {
+  DR_REQUIRE(d && wm && ac && B > 0 && H > 0, "null argument or empty batch");
+  DR_REQUIRE(!do_main || (latents && hiddens && actions && tape && gr), "null argument");
   Carve c(ws);
   ImWs w;
   imws_carve(c, d, B, H, w);
   WS_CHECK(c, ws_bytes);
   Carve ct((void*)tape);
   Tape tp;
-  tape_carve(ct, d, B, H, tp);
+  if (do_main) tape_carve(ct, d, B, H, tp);
   const int L = latent(d), Hd = d->hidden, A = d->action, a1 = d->actor_h1, a2 = d->actor_h2;
   const long long ldH = (long long)(H + 1) * Hd, ldL = (long long)(H + 1) * L, ldA = (long long)H * A;
   const long long lda1 = (long long)H * a1, lda2 = (long long)H * a2;
   const int BH = B * H;
+  const bool upstream_state = g_latents || g_hiddens;
+  if (do_prep) {
   // upstream gradients
   if (g_hiddens) DR_TRY(copy2d(w.gH, Hd, g_hiddens, Hd, Hd, (long long)B * (H + 1), s));
   else DR_TRY(zero(w.gH, (long long)B * (H + 1) * Hd, s));
@@ -371,7 +410,6 @@ extern "C" int dr_imagine_bwd(const dr_dims* d, const dr_world_model* wm, const 
   else DR_TRY(zero(w.gZ, (long long)B * (H + 1) * L, s));
   if (g_actions) DR_TRY(copy2d(w.gA, A, g_actions, A, A, (long long)BH, s));
   else DR_TRY(zero(w.gA, (long long)BH * A, s));
-  const bool upstream_state = g_latents || g_hiddens;
   {
     // weights are constant over the backward: transpose them once (one launch)
     // so every input-gradient GEMM below runs NT with 16-byte weight loads
@@ -389,6 +427,8 @@ extern "C" int dr_imagine_bwd(const dr_dims* d, const dr_world_model* wm, const 
     };
     DR_TRY(op_transpose_multi(tj, 9, s));
   }
+  }  // do_prep
+  if (!do_main) return DR_OK;
 
   for (int t = H - 1; t >= 0; --t) {
     const long long hb = (long long)Hd * B * t;

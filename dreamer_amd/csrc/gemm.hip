@@ -1016,20 +1016,16 @@ __global__ __launch_bounds__(256) void k_gemm_tile(GemmBatch gb, int splits) {
   // row-major loader (MK / NK): thread -> (row prow + RS i, float4 quad)
   constexpr int RS = 256 / KQ;
   constexpr int APT = BM * KQ / 256, BPT = BN * KQ / 256;
-  // transposed loader (KM / KN): thread -> (k row kk0 + KS i, 4 consecutive m)
-  constexpr int AR4 = BM / 4, AKS = 256 / AR4, BR4 = BN / 4, BKS = 256 / BR4;
-  constexpr int APTT = KC * AR4 / 256, BPTT = KC * BR4 / 256;
-  static_assert(APT >= 1 && BPT >= 1 && AKS >= 1 && BKS >= 1, "tile");
+  // transposed loader (KM / KN): thread -> (m = tid % BM, k quad tid / BM + AQ i):
+  // four scalar loads down k, each coalesced over the wave's consecutive m,
+  // land as ONE float4 row piece in LDS -- the same [m][k] layout and
+  // conflict-free ds_write_b128 as the row-major path (a transposing scatter
+  // of float4-along-m loads hits one LDS bank 16 times)
+  constexpr int AQ = 256 / BM, BQ = 256 / BN;
+  constexpr int APTT = KQ / AQ, BPTT = KQ / BQ;
+  static_assert(APT >= 1 && BPT >= 1 && AQ >= 1 && BQ >= 1, "tile");
   static_assert(A_KM ? APTT == APT : true, "loader");
   static_assert(B_KN ? BPTT == BPT : true, "loader");
-  // transposed (KM / KN) operands: float4 loads along m / n where this
-  // problem's strides and bases allow (decided per problem, wave-uniform)
-  const bool v4a = A_KM && (lda & 3) == 0 && (((uintptr_t)A) & 15) == 0;
-  const float* W2u = dr_uni(g.W2);
-  const int nsB = dr_uni(g.nsplitB);
-  const bool v4b = B_KN && (ldb & 3) == 0 && (((uintptr_t)W) & 15) == 0 &&
-                   (W2u == nullptr || (((int)g.ldb2 & 3) == 0 && (((uintptr_t)W2u) & 15) == 0 &&
-                                       (nsB >= N || (nsB & 3) == 0)));
   // register ring: chunk loads are issued PIPE chunks ahead of their use
   constexpr int PIPE = 3;
   float4 ra[PIPE][APT], rb[PIPE][BPT];
@@ -1058,14 +1054,10 @@ __global__ __launch_bounds__(256) void k_gemm_tile(GemmBatch gb, int splits) {
           }
         }
       } else {
-        const int kk = tid / AR4 + AKS * i, k = k0 + kk, m = m0 + 4 * (tid % AR4);
-        if (v4a && k < K && m + 3 < M) {
-          ra[sl][i] = dr_ld4(A, (unsigned)(k * lda + m));
-        } else {
-          float* v = &ra[sl][i].x;
+        const int m = m0 + tid % BM, k = k0 + 4 * (tid / BM + AQ * i);
+        float* v = &ra[sl][i].x;
 #pragma unroll
-          for (int cc = 0; cc < 4; ++cc) v[cc] = (k < K && m + cc < M) ? dr_ld1(A, (unsigned)(k * lda + m + cc)) : 0.f;
-        }
+        for (int cc = 0; cc < 4; ++cc) v[cc] = (k + cc < K && m < M) ? dr_ld1(A, (unsigned)((k + cc) * lda + m)) : 0.f;
       }
     }
 #pragma unroll
@@ -1082,17 +1074,10 @@ __global__ __launch_bounds__(256) void k_gemm_tile(GemmBatch gb, int splits) {
           for (int cc = 0; cc < 4; ++cc) v[cc] = (n < N && k + cc < K) ? dr_ld1(W, (unsigned)(n * ldb + k + cc)) : 0.f;
         }
       } else {
-        const int kk = tid / BR4 + BKS * i, k = k0 + kk, n = n0 + 4 * (tid % BR4);
-        if (v4b && k < K && n + 3 < N) {
-          // 4 columns in one segment (nsplitB % 4 == 0, ldb2 % 4 == 0: v4b)
-          if (k >= g.ksplitB) rb[sl][i] = dr_ld4(g.W2 + (long long)(k - g.ksplitB) * g.ldb2, (unsigned)n);
-          else if (n >= g.nsplitB) rb[sl][i] = dr_ld4(g.W2 + (long long)k * g.ldb2, (unsigned)(n - g.nsplitB));
-          else rb[sl][i] = dr_ld4(W, (unsigned)(k * ldb + n));
-        } else {
-          float* v = &rb[sl][i].x;
+        const int n = n0 + tid % BN, k = k0 + 4 * (tid / BN + BQ * i);
+        float* v = &rb[sl][i].x;
 #pragma unroll
-          for (int cc = 0; cc < 4; ++cc) v[cc] = (k < K && n + cc < N) ? tile_b_kn(g, W, ldb, n + cc, k) : 0.f;
-        }
+        for (int cc = 0; cc < 4; ++cc) v[cc] = (k + cc < K && n < N) ? tile_b_kn(g, W, ldb, n, k + cc) : 0.f;
       }
     }
   };
@@ -1102,13 +1087,7 @@ __global__ __launch_bounds__(256) void k_gemm_tile(GemmBatch gb, int splits) {
       if (!A_KM) {
         *reinterpret_cast<float4*>(&As[buf][prow + RS * i][4 * quad]) = ra[sl][i];
       } else {
-        const int kk = tid / AR4 + AKS * i, ml = 4 * (tid % AR4);
-        if (kk < KC) {
-          As[buf][ml + 0][kk] = ra[sl][i].x;
-          As[buf][ml + 1][kk] = ra[sl][i].y;
-          As[buf][ml + 2][kk] = ra[sl][i].z;
-          As[buf][ml + 3][kk] = ra[sl][i].w;
-        }
+        *reinterpret_cast<float4*>(&As[buf][tid % BM][4 * (tid / BM + AQ * i)]) = ra[sl][i];
       }
     }
 #pragma unroll
@@ -1116,13 +1095,7 @@ __global__ __launch_bounds__(256) void k_gemm_tile(GemmBatch gb, int splits) {
       if (!B_KN) {
         *reinterpret_cast<float4*>(&Bs[buf][prow + RS * i][4 * quad]) = rb[sl][i];
       } else {
-        const int kk = tid / BR4 + BKS * i, nl = 4 * (tid % BR4);
-        if (kk < KC) {
-          Bs[buf][nl + 0][kk] = rb[sl][i].x;
-          Bs[buf][nl + 1][kk] = rb[sl][i].y;
-          Bs[buf][nl + 2][kk] = rb[sl][i].z;
-          Bs[buf][nl + 3][kk] = rb[sl][i].w;
-        }
+        *reinterpret_cast<float4*>(&Bs[buf][tid % BN][4 * (tid / BN + BQ * i)]) = rb[sl][i];
       }
     }
   };

@@ -105,8 +105,12 @@ int op_onehot_index(int M, int R, int C, const float* z, long long ldz, int* idx
 //              z_value * w in group order, then actions and bias.
 // The two halves run concurrently (one MFMA wave and one gather wave per SIMD)
 // and meet at a single barrier before the gate math.
+#ifndef GRU_MW
 #define GRU_MW 4       // MFMA waves
-#define GRU_PRE 8      // 16-k chunks per MFMA wave held in registers
+#endif
+#ifndef GRU_PRE
+#define GRU_PRE 10     // 16-k chunks per MFMA wave held in registers (K = 600 over 4 waves: one batch)
+#endif
 #define GRU_MAXR 32    // latent groups
 #define GRU_MAXA 8     // actions
 

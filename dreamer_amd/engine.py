@@ -102,6 +102,9 @@ class ImaginationEngine:
         self.ws_im = hip.workspace(dev).get("e_im", L.query("dr_imagine_workspace_bytes", d, B, H))
         self.ctape = torch.zeros(L.query("dr_critic_tape_bytes", d, M), dtype=torch.uint8, device=dev)
         self.ws_cr = hip.workspace(dev).get("e_cr", L.query("dr_critic_workspace_bytes", d, B, H))
+        # the online critic's forward / loss backward run on a side stream
+        # beside the target critic and the BPTT (run_many): own workspace
+        self.ws_cr2 = hip.workspace(dev).get("e_cr2", L.query("dr_critic_workspace_bytes", d, B, H))
         self.rng = hip.rng(dev)
 
     # ------------------------------------------------------------- the phases
@@ -175,6 +178,44 @@ class ImaginationEngine:
         ag.loss_slot(0).copy_(self.loss_a[0:1])
         if fork:
             main.wait_stream(self.side)
+
+    # pieces of losses_and_grads for the two-stream update of run_many
+    def _x_critic_fwd_and_prep(self):
+        """side stream: online critic forward (Agent.py:105) and the BPTT's
+        upstream-gradient / transposed-weight prep."""
+        ag, d, st = self.dr.agent, self.d, hip.stream()
+        M = self.B * (self.H + 1)
+        L.call("dr_critic_fwd", d, ag.critic_struct(), M, L.ptr(self.hiddens), d.hidden, L.ptr(self.latents),
+               d.rows * d.cols, None, L.ptr(self.V_c), L.ptr(self.ctape), L.ptr(self.ws_cr2), self.ws_cr2.numel(),
+               st)
+        L.call("dr_imagine_bwd_prep", d, self.dr.world_model.packed(), ag.actor_struct(), self.B, self.H, None,
+               None, None, L.ptr(self.ws_im), self.ws_im.numel(), st)
+
+    def _actor_loss(self):
+        """update_S and the actor loss / its gradient w.r.t. mu, sigma (Agent.py:78-125)."""
+        ag, d, st = self.dr.agent, self.d, hip.stream()
+        B, H = self.B, self.H
+        scale = 1.0 / float(B * self.wsize * H)
+        L.call("dr_update_S", self.R_all.numel(), L.ptr(self.R_all), L.ptr(ag.S_dev), L.ptr(self.norm), None, 0, st)
+        L.call("dr_actor_loss_grad", B, H, d.action, L.ptr(self.mus), L.ptr(self.sigmas), L.ptr(self.actions),
+               L.ptr(self.R), L.ptr(self.V_c), L.ptr(self.norm), ag.nu, scale, L.ptr(self.loss_a), L.ptr(self.g_mu),
+               L.ptr(self.g_sig), st)
+
+    def _x_critic_bwd(self):
+        """side stream: two-hot CE of the critic and its backward (Agent.py:127-145)."""
+        ag, d = self.dr.agent, self.d
+        B, H = self.B, self.H
+        scale = 1.0 / float(B * self.wsize * H)
+        L.call("dr_critic_loss_bwd", d, ag.critic_struct(), B, H, L.ptr(self.hiddens), L.ptr(self.latents),
+               L.ptr(self.R), L.ptr(self.ctape), scale, L.ptr(ag.loss_slot(1)), ag.critic_struct(grad=True),
+               L.ptr(self.ws_cr2), self.ws_cr2.numel(), hip.stream())
+
+    def _bptt(self):
+        ag, d = self.dr.agent, self.d
+        L.call("dr_imagine_bwd_main", d, self.dr.world_model.packed(), ag.actor_struct(), self.B, self.H,
+               L.ptr(self.latents), L.ptr(self.hiddens), L.ptr(self.actions), L.ptr(self.g_mu), L.ptr(self.g_sig),
+               0, L.ptr(self.tape), ag.actor_struct(grad=True), L.ptr(self.ws_im), self.ws_im.numel(), hip.stream())
+        ag.loss_slot(0).copy_(self.loss_a[0:1])
 
     def optimise(self):
         """non-finite skip, clip_grad_norm_(100) x2, AdamW x2, soft target (Agent.py:137-153)."""
@@ -323,7 +364,7 @@ class ImaginationEngine:
         dev, B, H = self.dev, self.B, self.H
         if getattr(self, "_pipe", None) is None:
             self._pipe = dict(
-                stream=torch.cuda.Stream(dev),
+                stream=torch.cuda.Stream(dev), side=torch.cuda.Stream(dev),
                 rng=torch.zeros(2, dtype=torch.int64, device=dev),
                 z0=[self.z0, torch.zeros_like(self.z0)],
                 h0=[self.h0, torch.zeros_like(self.h0)],
@@ -354,7 +395,9 @@ class ImaginationEngine:
                     with torch.cuda.graph(g, stream=cs):
                         body()
                     graphs[(name, s)] = g
-            for name, body, _ in self.phases()[2:]:
+            for name, body in (("returns", self.returns), ("xfwd", self._x_critic_fwd_and_prep),
+                               ("actor_loss", self._actor_loss), ("xbwd", self._x_critic_bwd),
+                               ("bptt", self._bptt), ("optim", self._ph_optim)):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=cs):
                     body()
@@ -390,20 +433,57 @@ class ImaginationEngine:
                 ev_w[e] = torch.cuda.Event()
                 ev_w[e].record(ws)
 
+        xs = P["side"]
+        import os
+        # Which update pieces run on a third stream: the online critic forward
+        # + BPTT prep ("fwd", beside the target critic) and/or the critic
+        # loss backward ("bwd", beside the BPTT).  Measured at B = 64
+        # (bench, 30 epochs): none 242.3k, bwd 235.4k, both 228.7k, fwd
+        # 224.3k steps/s -- a third stream of latency-bound launches slows
+        # the critical chain more than it hides, so the default is "none".
+        side = os.environ.get("DREAMER_SIDE", "none")
+
+        def record(stream):
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            return ev
+
         issue_warm(0)
         for e in range(K):
             if e + 1 < K:
                 issue_warm(e + 1)
             main.wait_event(ev_w[e])
             G[("imagine", e & 1)].replay()
-            ev_i[e] = torch.cuda.Event()
-            ev_i[e].record(main)
-            for name, _, coll in self.phases()[2:]:
-                G[name].replay()
-                if coll is not None:
-                    coll()
+            ev_i[e] = record(main)
+            # side stream: online critic forward + BPTT prep beside the target
+            # critic / lambda returns; later the critic loss backward beside
+            # the actor's BPTT (they share only read-only inputs)
+            s1 = xs if side in ("both", "fwd") else main
+            s2 = xs if side in ("both", "bwd") else main
+            if s1 is xs:
+                xs.wait_event(ev_i[e])
+            with torch.cuda.stream(s1):
+                G["xfwd"].replay()
+            ev_x1 = record(s1)
+            G["returns"].replay()
+            if self.wsize > 1:
+                self._allgather_R()
+            ev_r = record(main)
+            main.wait_event(ev_x1)
+            G["actor_loss"].replay()
+            if s2 is xs:
+                xs.wait_event(record(main) if s1 is main else ev_r)
+            with torch.cuda.stream(s2):
+                G["xbwd"].replay()
+            ev_x2 = record(s2)
+            G["bptt"].replay()
+            main.wait_event(ev_x2)
+            if self.wsize > 1:
+                self._allreduce_grads()
+            G["optim"].replay()
             losses[e].copy_(ag.loss_buffer[0:2])
         main.wait_stream(ws)
+        main.wait_stream(xs)
         self.epochs += K
         self._pipe_host = host  # keep the pinned source alive until the H2D copy ran
         return losses

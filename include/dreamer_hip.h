@@ -150,6 +150,18 @@ int dr_imagine_bwd(const dr_dims* d, const dr_world_model* wm, const dr_actor* a
                    const float* g_sigmas,
                    const float* g_actions, const float* g_latents, const float* g_hiddens,
                    const void* tape, const dr_actor* grad, void* ws, size_t ws_bytes, hipStream_t stream);
+/* dr_imagine_bwd in two parts on the same workspace: _prep writes the upstream
+ * state gradients (NULL = 0) and the transposed weights -- it needs neither
+ * dL/dmus nor the tape, so it can run on a second stream while the returns and
+ * losses are formed; _main runs the reverse loop and the weight gradients
+ * (upstream_state: 1 if _prep was given dL/dlatents or dL/dhiddens). */
+int dr_imagine_bwd_prep(const dr_dims* d, const dr_world_model* wm, const dr_actor* actor, int B, int H,
+                        const float* g_actions, const float* g_latents, const float* g_hiddens, void* ws,
+                        size_t ws_bytes, hipStream_t stream);
+int dr_imagine_bwd_main(const dr_dims* d, const dr_world_model* wm, const dr_actor* actor, int B, int H,
+                        const float* latents, const float* hiddens, const float* actions, const float* g_mus,
+                        const float* g_sigmas, int upstream_state, const void* tape, const dr_actor* grad, void* ws,
+                        size_t ws_bytes, hipStream_t stream);
 
 /* ---- single steps (batch-1 acting path and per-block API) ------------------ */
 /* imagine_step (WorldModel.py:72-77): h' = GRU(z,h,a); z' ~ prior(h'); r; c */

@@ -15,7 +15,8 @@ objs = [o for o in glob.glob(os.path.join(ROOT, "dreamer_amd", "_build", "*.o"))
         if os.path.basename(o) not in ("gemm.o", "gru.o")]
 for src in ("gemm", "gru"):
     o = os.path.join(HERE, src + "_ts.o")
-    r = subprocess.run([B.HIPCC, *B.CFLAGS, "-DDR_PHASE_TIMING", "-c", os.path.join(B.CSRC, src + ".hip"), "-o", o],
+    extra = os.environ.get("KB_DEFS", "").split()
+    r = subprocess.run([B.HIPCC, *B.CFLAGS, "-DDR_PHASE_TIMING", *extra, "-c", os.path.join(B.CSRC, src + ".hip"), "-o", o],
                        capture_output=True, text=True)
     if r.returncode:
         print(r.stdout, r.stderr)
@@ -23,7 +24,7 @@ for src in ("gemm", "gru"):
     objs.append(o)
 obj = os.path.join(HERE, "kbench.o")
 for cmd in ([B.HIPCC, *B.CFLAGS, "-c", os.path.join(HERE, "kbench.hip"), "-o", obj],
-            [B.HIPCC, f"--offload-arch={B.ARCH}", obj, *objs, "-o", os.path.join(HERE, "kbench")]):
+            [B.HIPCC, f"--offload-arch={B.ARCH}", obj, *objs, "-o", os.path.join(HERE, os.environ.get("KB_OUT", "kbench"))]):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode:
         print(r.stdout, r.stderr)
