@@ -1302,6 +1302,10 @@ static void launch_tile(const GemmBatch& gb, int count, hipStream_t s) {
   hipLaunchKernelGGL((k_gemm<BM, BN, AMODE, A_KM, B_KN>), dim3(maxt, 1, count), dim3(256), 0, s, gb);
 }
 
+// split-K target: workgroups per launch over the problems' real tiles
+static int g_tile_wgs = 512;
+extern "C" void dr_debug_tile_wgs(int v) { g_tile_wgs = v > 0 ? v : 512; }
+
 // mid-size GEMMs: LDS double-buffered tile kernel, split-K when the tile grid
 // is too small to fill the chip and every problem brought scratch for it
 template <int BM, int BN, int KC, bool A_KM, bool B_KN>
@@ -1328,7 +1332,7 @@ static void launch_tile2(GemmBatch& gb, int count, hipStream_t s) {
   if (ws) {
     // about two workgroups per CU over the problems' real tiles (the grid's
     // surplus blocks of the smaller problems exit at once)
-    splits = std::max(1, std::min(DR_TILE_SPLITS, dr_cdiv(512, tot)));
+    splits = std::max(1, std::min(DR_TILE_SPLITS, dr_cdiv(g_tile_wgs, tot)));
     splits = std::min(splits, std::max(1, nch / 2));  // at least 2 chunks per split
     for (int i = 0; i < count; ++i)
       while (splits > 1 && (long long)splits * gb.p[i].M * gb.p[i].N > gb.p[i].splitk_floats) --splits;

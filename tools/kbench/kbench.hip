@@ -20,6 +20,7 @@ extern "C" int dr_debug_tbuf_gru(long long* out, int n);
 extern "C" int dr_debug_tbuf_gemm(long long* out, int n);
 extern "C" void dr_debug_tile_variant(int v);
 extern "C" void dr_debug_skinny_variant(int v);
+extern "C" void dr_debug_tile_wgs(int v);
 
 // one more launch, then the per-phase times of wave 0 of each workgroup
 // (relative to its own start) averaged over the workgroups that wrote them
@@ -392,9 +393,10 @@ int main(int argc, char** argv) {
     struct Mid { int M, N, K; bool tn; bool sk; } mids[] = {
         {1024, 200, 1624, false, false}, {1024, 200, 1624, false, true}, {2048, 200, 4096, false, true},
         {200, 1624, 960, true, false},   {200, 1624, 960, true, true},   {200, 200, 1024, true, true}};
-    for (int var = 0; var < 4; ++var)
+    for (int var = 0; var < 6; ++var)
     for (auto& c : mids) {
-      dr_debug_tile_variant(var);
+      dr_debug_tile_variant(var < 4 ? var : 0);
+      dr_debug_tile_wgs(var == 4 ? 256 : var == 5 ? 1024 : 512);
       GemmArgs g = gemm_args();
       g.M = c.M; g.N = c.N; g.K = c.K;
       if (!c.tn) { g.A = Xm; g.lda = c.K; g.W = Wm; g.ldb = c.K; }
