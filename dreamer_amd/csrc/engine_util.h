@@ -174,6 +174,21 @@ static inline void with_sampler(GemmArgs& g, const dr_dims* d, const dr_noise& n
   g.zval_out = idx ? onehot_vals(idx, g.M, d->rows) : nullptr;
 }
 
+// LN-SiLU -> Linear -> LN-SiLU -> Linear tail of a 3-layer head (mlp2_launch)
+// from the first Linear's output X; e = the last Linear (plus its epilogue)
+static inline Mlp2Args mlp2(int M, int K1, int K2, const float* X, long long ldx, const dr_linear& ln1,
+                            const dr_linear& l3, const dr_linear& ln4, const GemmArgs& e) {
+  Mlp2Args a;
+  memset(&a, 0, sizeof(a));
+  a.M = M; a.K1 = K1; a.K2 = K2;
+  a.X = X; a.ldx = ldx;
+  a.ln1_g = ln1.w; a.ln1_b = ln1.b;
+  a.W3 = l3.w; a.b3 = l3.b;
+  a.ln4_g = ln4.w; a.ln4_b = ln4.b;
+  a.e = e;
+  return a;
+}
+
 // fused actor-head epilogue on the stacked [mu_head; log_sig_head] GEMM
 static inline void with_actor_head(GemmArgs& g, int A, const dr_noise& nz, int step, int det, float* act, long long ld_act,
                             float* mu, long long ld_mu, float* sig, long long ld_sig, float* eps_save, float* ls_save,

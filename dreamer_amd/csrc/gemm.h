@@ -60,3 +60,24 @@ enum GemmLayout { G_NT = 0, G_NN = 1, G_TN = 2 };
 GemmArgs gemm_args();  // zero-initialised with neutral defaults
 // Launch up to 4 problems sharing layout/A-mode in one dispatch.
 int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hipStream_t s);
+
+// The tail of the reference's 3-layer heads (Linear, LN, SiLU, Linear, LN,
+// SiLU, Linear -- DynamicsPredictors.py:15-23, Agent.py:180-190) from the
+// first Linear's output X on, in ONE launch:
+//   y1 = SiLU(LN1(X)); h2 = y1 W3^T + b3; y2 = SiLU(LN4(h2)); out = y2 W6^T + b6
+// followed by `e`'s epilogue (plain / activation store to e.Y, or EPI_SAMPLE,
+// or EPI_ACTOR).  A workgroup owns 16 rows x 128 output columns and computes
+// y1, h2, y2 for its rows itself (the two small layers are recomputed by
+// each column block instead of a grid-wide seam).  K1, K2 <= 256.
+struct alignas(16) Mlp2Args {
+  int M, K1, K2, pad_;
+  const float* X; long long ldx;     // [M][K1] first Linear's output (pre-LN1)
+  const float* ln1_g; const float* ln1_b;
+  const float* W3; const float* b3;  // [K2][K1]
+  const float* ln4_g; const float* ln4_b;
+  float* a1_out; long long ld_a1;    // optional y1 (column block 0 writes)
+  float* pre2; long long ld_pre2;    // optional h2
+  float* a2_out; long long ld_a2;    // optional y2
+  GemmArgs e;                        // last Linear: e.N, e.W [N][K2] (e.ldb), e.bias, epilogue
+};
+int mlp2_launch(const Mlp2Args* probs, int count, hipStream_t s);

@@ -356,9 +356,12 @@ __device__ __forceinline__ void epilogue_store_b(const GemmArgs& g, int m, int n
   else *dst = v;
 }
 
+#ifndef DR_SKW
+#define DR_SKW 8  // waves per skinny-GEMM workgroup (K split over them)
+#endif
 template <int MT, int NT, int AMODE, bool B_KN, bool VEC, int EPI>
-__global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
-  constexpr int NWAVE = 8, FT = MT / 16, FN = NT / 16;
+__global__ __launch_bounds__(64 * DR_SKW) void k_gemm_skinny(GemmBatch gb) {
+  constexpr int NWAVE = DR_SKW, NTH = 64 * DR_SKW, FT = MT / 16, FN = NT / 16;
   __shared__ GemmArgs s_args;
   dr_stage_args(gb.p[blockIdx.z], s_args, threadIdx.x);
   const GemmArgs& g = s_args;
@@ -388,13 +391,13 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
   __shared__ float s_out[MT][NT + 1];
   // bias of the output columns this thread finalises, issued now and waited
   // for only in the epilogue
-  constexpr int NEPI = (FT * FN * 256 + 511) / 512;
+  constexpr int NEPI = (FT * FN * 256 + NTH - 1) / NTH;
   float ebias[NEPI];
   {
     const float* bias = dr_uni(g.bias);
 #pragma unroll
     for (int i = 0; i < NEPI; ++i) {
-      const int x = tid + 512 * i;
+      const int x = tid + NTH * i;
       const int n = n0 + ((x >> 8) % FN) * 16 + (x & 15);
       const bool ok = bias && x < FT * FN * 256 && n < N;
       const float v = dr_ld1(ok ? bias : o.W, ok ? (unsigned)n : 0u);
@@ -868,7 +871,7 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
   // element (t, j, e, l): D[row 4*(l>>4)+e][col l&15] of tile (t, j)
 #pragma unroll
   for (int i = 0; i < NEPI; ++i) {
-    const int x = tid + 512 * i;
+    const int x = tid + NTH * i;
     if (x >= FT * FN * 256) break;
     const int l = x & 63, e = (x >> 6) & 3, tj = x >> 8;
     float v = 0.f;
@@ -937,7 +940,7 @@ __global__ __launch_bounds__(512) void k_gemm_skinny(GemmBatch gb) {
   } else if (EPI == EPI_ACTOR && g.epi == EPI_ACTOR) {
     __syncthreads();
     const int A = g.na;
-    for (int x = tid; x < MT * A; x += 512) {
+    for (int x = tid; x < MT * A; x += NTH) {
       const int ml = x / A, i = x - ml * A, m = m0 + ml;
       if (m >= M) continue;
       const float muv = s_out[ml][i];
@@ -1243,10 +1246,10 @@ static void launch_skinny(const GemmBatch& gb, int count, bool vec, hipStream_t 
     (void)raised;
   }
   if (vec)
-    hipLaunchKernelGGL((k_gemm_skinny<MT, NT, AMODE, B_KN, true, EPI>), dim3(dr_xcd_grid(maxt), 1, count), dim3(512),
+    hipLaunchKernelGGL((k_gemm_skinny<MT, NT, AMODE, B_KN, true, EPI>), dim3(dr_xcd_grid(maxt), 1, count), dim3(64 * DR_SKW),
                        lds, s, gb);
   else
-    hipLaunchKernelGGL((k_gemm_skinny<MT, NT, AMODE, B_KN, false, EPI>), dim3(dr_xcd_grid(maxt), 1, count), dim3(512),
+    hipLaunchKernelGGL((k_gemm_skinny<MT, NT, AMODE, B_KN, false, EPI>), dim3(dr_xcd_grid(maxt), 1, count), dim3(64 * DR_SKW),
                        lds, s, gb);
 }
 
@@ -1300,6 +1303,272 @@ static void launch_tile(const GemmBatch& gb, int count, hipStream_t s) {
   }
   if (maxt == 0) return;
   hipLaunchKernelGGL((k_gemm<BM, BN, AMODE, A_KM, B_KN>), dim3(maxt, 1, count), dim3(256), 0, s, gb);
+}
+
+// ---------------------------------------------------------------------------
+// k_mlp2_tail: LN-SiLU -> Linear -> LN-SiLU -> Linear (+ epilogue), one launch
+// ---------------------------------------------------------------------------
+#define MLP2_KMAX 208  // K1, K2 <= 208 (the reference heads are 200 wide)
+#define MLP2_NC 128
+struct Mlp2Batch {
+  Mlp2Args p[3];
+};
+
+// SiLU(LayerNorm(row)) of a row held one float4 per lane (k = 4 lane)
+__device__ __forceinline__ float4 mlp2_ln_silu(float4 x, bool ok, int K, const float* gam, const float* bet, int k) {
+  const float mean = wave_sum(ok ? (x.x + x.y) + (x.z + x.w) : 0.f) / (float)K;
+  float sq = 0.f;
+  if (ok) {
+    const float dx = x.x - mean, dy = x.y - mean, dz = x.z - mean, dw = x.w - mean;
+    sq = (dx * dx + dy * dy) + (dz * dz + dw * dw);
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)K + 1e-5f);
+  if (!ok) return make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 gv = dr_ld4(gam, (unsigned)k), bv = dr_ld4(bet, (unsigned)k);
+  return make_float4(dr_silu_fast((x.x - mean) * rstd * gv.x + bv.x), dr_silu_fast((x.y - mean) * rstd * gv.y + bv.y),
+                     dr_silu_fast((x.z - mean) * rstd * gv.z + bv.z), dr_silu_fast((x.w - mean) * rstd * gv.w + bv.w));
+}
+
+// [16 rows] x [16 cols of W] over K (padded to 16): lane (r, q) holds 4
+// consecutive k of weight row n (loaded up front by mlp2_wload) and reads the
+// matching 4 k of LDS row r; four accumulator chains keep consecutive MFMAs
+// independent
+#define MLP2_KS (MLP2_KMAX / 16)
+__device__ __forceinline__ void mlp2_wload(float4 (&wv)[MLP2_KS], const float* W, int ldw, int n, bool nok, int K,
+                                           int q) {
+  const int ks = (K + 15) >> 4;
+#pragma unroll
+  for (int s = 0; s < MLP2_KS; ++s) {
+    const int k = 16 * s + 4 * q;
+    const bool ok = s < ks && nok && k < K;
+    wv[s] = dr_ld4(W, ok ? (unsigned)(n * ldw + k) : 0u);
+    if (!ok) wv[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+template <int LP>
+__device__ __forceinline__ f32x4 mlp2_tile(const float (*ys)[LP], const float4 (&wv)[MLP2_KS], int K, int r, int q) {
+  const int ks = (K + 15) >> 4;
+  f32x4 c[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) c[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < MLP2_KS; ++s) {
+    if (s < ks) {
+      const float4 a = *reinterpret_cast<const float4*>(&ys[r][16 * s + 4 * q]);
+      c[s & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, wv[s].x, c[s & 3], 0, 0, 0);
+      c[s & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, wv[s].y, c[s & 3], 0, 0, 0);
+      c[s & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, wv[s].z, c[s & 3], 0, 0, 0);
+      c[s & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, wv[s].w, c[s & 3], 0, 0, 0);
+    }
+  }
+  f32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = (c[0][e] + c[1][e]) + (c[2][e] + c[3][e]);
+  return o;
+}
+
+__global__ __launch_bounds__(512) void k_mlp2_tail(Mlp2Batch mb) {
+  __shared__ Mlp2Args s_a;
+  dr_stage_args(mb.p[blockIdx.z], s_a, threadIdx.x);
+  const Mlp2Args& a = s_a;
+  const GemmArgs& g = a.e;
+  const int M = dr_uni(a.M), K1 = dr_uni(a.K1), K2 = dr_uni(a.K2), N = dr_uni(g.N);
+  const int n0 = blockIdx.x * MLP2_NC, m0 = blockIdx.y * 16;
+  if (n0 >= N || m0 >= M) return;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r = lane & 15, q = lane >> 4;
+  constexpr int LP = MLP2_KMAX + 8;  // 8 mod 16 dwords: conflict-free ds_read_b128 fragments
+  __shared__ __attribute__((aligned(16))) float ys[16][LP];
+  __shared__ __attribute__((aligned(16))) float hs[16][LP];
+  __shared__ float so[16][MLP2_NC + 1];
+  const bool c0 = blockIdx.x == 0;
+  const int k = 4 * lane;
+  const int ncols = min(MLP2_NC, N - n0);
+  // every global operand of this wave is issued before the first use: its two
+  // input rows, its (up to) two W3 tiles, its W6 tile
+  const float* X = dr_uni(a.X);
+  const int ldx = dr_uni((int)a.ldx);
+  float4 xr[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + wave + 8 * i;
+    const bool ok = m < M && k < K1;
+    xr[i] = dr_ld4(X, ok ? (unsigned)(m * ldx + k) : 0u);
+  }
+  const int nt3 = (K2 + 15) >> 4;
+  float4 w3[2][MLP2_KS];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int n = (wave + 8 * i) * 16 + r;
+    mlp2_wload(w3[i], a.W3, K1, n, wave + 8 * i < nt3 && n < K2, K1, q);
+  }
+  const int ntd = (ncols + 15) >> 4;
+  float4 w6[MLP2_KS];
+  {
+    const int nl = wave * 16 + r;
+    mlp2_wload(w6, dr_uni(g.W), dr_uni((int)g.ldb), n0 + nl, wave < ntd && nl < ncols, K2, q);
+  }
+
+  // A: y1 = SiLU(LN1(X)), two rows per wave
+  {
+    const int KP = (K1 + 15) & ~15;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rr = wave + 8 * i, m = m0 + rr;
+      const bool ok = m < M && k < K1;
+      const float4 y = mlp2_ln_silu(xr[i], ok, K1, a.ln1_g, a.ln1_b, k);
+      if (k < KP) *reinterpret_cast<float4*>(&ys[rr][k]) = y;
+      if (c0 && a.a1_out && ok) dr_st4(a.a1_out, (unsigned)(m * a.ld_a1 + k), y);
+    }
+  }
+  __syncthreads();
+  // B: h2 = y1 W3^T + b3 (16-column tiles over the 8 waves)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int tj = wave + 8 * i;
+    if (tj < nt3) {
+      const int n = tj * 16 + r;
+      const f32x4 acc = mlp2_tile<LP>(ys, w3[i], K1, r, q);
+      const float bv = (n < K2 && a.b3) ? dr_ld1(a.b3, (unsigned)n) : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int ml = 4 * q + e, m = m0 + ml;
+        const float v = (n < K2) ? acc[e] + bv : 0.f;
+        hs[ml][n] = v;
+        if (c0 && a.pre2 && m < M && n < K2) dr_g(a.pre2)[(long long)m * a.ld_pre2 + n] = v;
+      }
+    }
+  }
+  __syncthreads();
+  // C: y2 = SiLU(LN4(h2)), back into ys
+  {
+    const int KP = (K2 + 15) & ~15;
+    for (int rr = wave; rr < 16; rr += 8) {
+      const int m = m0 + rr;
+      const bool ok = k < K2;
+      float4 x = ok ? *reinterpret_cast<const float4*>(&hs[rr][k]) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 y = mlp2_ln_silu(x, ok, K2, a.ln4_g, a.ln4_b, k);
+      if (m >= M) y = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k < KP) *reinterpret_cast<float4*>(&ys[rr][k]) = y;
+      if (c0 && a.a2_out && ok && m < M) dr_st4(a.a2_out, (unsigned)(m * a.ld_a2 + k), y);
+    }
+  }
+  __syncthreads();
+  // D: out = y2 W6^T + b6 for columns [n0, n0 + 128): one 16-column tile per wave
+  if (wave < ntd) {
+    const int nl = wave * 16 + r, n = n0 + nl;
+    const f32x4 acc = mlp2_tile<LP>(ys, w6, K2, r, q);
+    const float bv = (nl < ncols && g.bias) ? dr_ld1(g.bias, (unsigned)n) : 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) so[4 * q + e][nl] = acc[e] + bv;
+  }
+  __syncthreads();
+  // E: epilogue
+  if (g.epi == EPI_SAMPLE) {
+    const int C = g.C;
+    int W = 1;
+    while (W < C) W <<= 1;
+    const int gpr = ncols / C, npairs = 16 * gpr, per_wave = 64 / W;
+    for (int pbase = wave * per_wave; pbase < npairs; pbase += 8 * per_wave) {
+      const int pidx = pbase + lane / W, c = lane % W;
+      const bool valid = pidx < npairs;
+      const int ml = valid ? pidx / gpr : 0, gl = valid ? pidx - ml * gpr : 0;
+      const int m = m0 + ml, grp = (n0 / C) + gl;
+      const bool act = valid && c < C && m < M;
+      const float x = act ? so[ml][gl * C + c] : -INFINITY;
+      if (act && g.Y) dr_g(g.Y)[(long long)m * g.ldy + n0 + gl * C + c] = x;
+      const float mx = group_max(x, W);
+      const float ex = act ? expf(x - mx) : 0.0f;
+      const float se = group_sum(ex, W);
+      const float p = ex / se;
+      const float pu = act ? (0.99f * p + g.unimix) : 0.0f;
+      const float sp = group_sum(pu, W);
+      const float ph = pu / sp;
+      float qv = 1.0f;
+      const int Rg = g.R;
+      if (act) {
+        if (g.noise.q) qv = dr_g(g.noise.q)[((long long)g.step * M * Rg + (long long)m * Rg + grp) * C + c];
+        else qv = dr_exp1(g.noise.rng, (uint32_t)(g.noise.stream + g.step), (uint32_t)(g.noise.row0 + m),
+                          (uint32_t)(grp * C + c));
+      }
+      float best = act ? ph / qv : -INFINITY;
+      int bi = act ? c : 0x7fffffff;
+      for (int o = W >> 1; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ob > best || (ob == best && oi < bi)) {
+          best = ob;
+          bi = oi;
+        }
+      }
+      if (act) {
+        dr_g(g.z_out)[(long long)m * g.ldz + grp * C + c] = (c == bi) ? ((1.0f + pu) - pu) : 0.0f;
+        if (g.soft_out) dr_g(g.soft_out)[(long long)m * g.ld_soft + grp * C + c] = p;
+        if (g.idx_out && c == 0) dr_g(g.idx_out)[m * Rg + grp] = bi;
+        if (g.zval_out && c == bi) dr_g(g.zval_out)[m * Rg + grp] = (1.0f + pu) - pu;
+      }
+    }
+  } else if (g.epi == EPI_ACTOR) {
+    const int A = g.na;
+    for (int x = tid; x < 16 * A; x += 512) {
+      const int ml = x / A, i = x - ml * A, m = m0 + ml;
+      if (m >= M) continue;
+      const float muv = so[ml][i];
+      const float lr = so[ml][A + i];
+      const float ls = fminf(fmaxf(lr, -5.0f), 2.0f);
+      const float sg = dr_softplus(ls) + 1e-3f;
+      float av;
+      if (g.det) {
+        av = tanhf(muv);
+      } else {
+        float e;
+        if (g.noise.eps) e = dr_g(g.noise.eps)[((long long)g.step * M + m) * A + i];
+        else e = dr_normal(g.noise.rng, (uint32_t)(g.noise.stream + g.step), (uint32_t)(g.noise.row0 + m),
+                           (uint32_t)i);
+        if (g.eps_save) dr_g(g.eps_save)[(long long)m * A + i] = e;
+        av = tanhf(muv + e * sg);
+      }
+      if (g.act_out) dr_g(g.act_out)[(long long)m * g.ld_act + i] = av;
+      if (g.mu_out) dr_g(g.mu_out)[(long long)m * g.ld_mu + i] = muv;
+      if (g.sig_out) dr_g(g.sig_out)[(long long)m * g.ld_sig + i] = sg;
+      if (g.ls_save) dr_g(g.ls_save)[(long long)m * g.ld_ls + i] = lr;
+    }
+  } else {
+    for (int x = tid; x < 16 * ncols; x += 512) {
+      const int ml = x / ncols, nl = x - ml * ncols, m = m0 + ml;
+      if (m >= M) continue;
+      dr_g(g.Y)[(long long)m * g.ldy + n0 + nl] = epi_act(g, so[ml][nl]);
+    }
+  }
+}
+
+int mlp2_launch(const Mlp2Args* probs, int count, hipStream_t s) {
+  if (count < 1 || count > 3) {
+    dr_set_error("mlp2_launch: bad problem count %d", count);
+    return DR_E_INVALID;
+  }
+  Mlp2Batch mb;
+  int gx = 1, gy = 1;
+  for (int i = 0; i < count; ++i) {
+    const Mlp2Args& a = probs[i];
+    const GemmArgs& g = a.e;
+    const bool al = !(((uintptr_t)a.X | (uintptr_t)a.W3 | (uintptr_t)g.W | (uintptr_t)a.ln1_g | (uintptr_t)a.ln1_b |
+                       (uintptr_t)a.ln4_g | (uintptr_t)a.ln4_b) & 15) &&
+                    !((uintptr_t)a.a1_out & 15) && !((uintptr_t)a.a2_out & 15);
+    if (a.M < 1 || a.K1 < 4 || a.K2 < 4 || a.K1 > MLP2_KMAX || a.K2 > MLP2_KMAX || a.K1 % 4 || a.K2 % 4 ||
+        a.ldx % 4 || g.ldb % 4 || a.ld_a1 % 4 || a.ld_a2 % 4 || g.K != a.K2 || g.N < 1 || !al ||
+        (g.epi == EPI_SAMPLE && (g.C < 1 || g.C > 32 || 32 % g.C != 0 || MLP2_NC % g.C != 0)) ||
+        (g.epi == EPI_ACTOR && (g.N != 2 * g.na || g.N > 16)) || (g.epi == EPI_NONE && !g.Y) ||
+        g.accumulate || g.addend || g.alpha != 1.0f) {
+      dr_set_error("mlp2_launch: unsupported problem (M=%d K1=%d K2=%d N=%d epi=%d)", a.M, a.K1, a.K2, g.N, g.epi);
+      return DR_E_INVALID;
+    }
+    mb.p[i] = a;
+    gx = std::max(gx, dr_cdiv(g.N, MLP2_NC));
+    gy = std::max(gy, dr_cdiv(a.M, 16));
+  }
+  hipLaunchKernelGGL(k_mlp2_tail, dim3(gx, gy, count), dim3(512), 0, s, mb);
+  return dr_check_launch("mlp2_tail");
 }
 
 // split-K target: workgroups per launch over the problems' real tiles

@@ -366,6 +366,25 @@ int main(int argc, char** argv) {
     snprintf(buf, sizeof buf, "NN plain M%d N%d K%d", sh[0], sh[1], sh[2]);
     timeit(buf, [&](hipStream_t st) { gemm_launch(G_NN, AM_PLAIN, &gk, 1, st); }, s);
   }
+  // fused head tail (LN-SiLU, Linear, LN-SiLU, Linear) vs its two launches
+  {
+    GemmArgs e = nt_(64, 1024, 200);
+    e.A = nullptr;
+    Mlp2Args a;
+    memset(&a, 0, sizeof(a));
+    a.M = 64; a.K1 = 200; a.K2 = 200; a.X = X; a.ldx = 200; a.ln1_g = lng; a.ln1_b = lnb; a.W3 = W; a.b3 = bias;
+    a.ln4_g = lng; a.ln4_b = lnb; a.pre2 = Y + 300000; a.ld_pre2 = 200; a.e = e;
+    timeit("mlp2 tail M64 200-200-1024", [&](hipStream_t st) { mlp2_launch(&a, 1, st); }, s);
+    Mlp2Args a3[3] = {a, a, a};
+    a3[0].e.N = 255; a3[1].e.N = 1; a3[2].e.N = 6;
+    timeit("mlp2 tail x3 M64 200-200-{255,1,6}", [&](hipStream_t st) { mlp2_launch(a3, 3, st); }, s);
+    GemmArgs g1 = nt_(64, 200, 200);
+    g1.ln_g = lng; g1.ln_b = lnb; g1.Y = Y + 300000;
+    GemmArgs g2 = nt_(64, 1024, 200);
+    g2.A = Y + 300000; g2.ln_g = lng; g2.ln_b = lnb;
+    timeit("unfused 2x lnsilu M64 200-200-1024", [&](hipStream_t st) { gemm_launch(G_NT, AM_LNSILU, &g1, 1, st);
+                                                                       gemm_launch(G_NT, AM_LNSILU, &g2, 1, st); }, s);
+  }
   // per-step shapes of the imagination / BPTT chain, both row-tile variants
   for (int var = 0; var < 3; var += 2) {
     dr_debug_skinny_variant(var);
