@@ -114,6 +114,7 @@ _SIGS = {
     "dr_replay_gather": (_i, [_ll, _i, _i, _i, _i, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp]),
     "dr_rng_advance": (_i, [fp, C.c_ulonglong, fp]),
     "dr_set_conv_lds_pad": (None, [_i]),
+    "dr_set_conv1_direct": (None, [_i]),
     "dr_wm_train_workspace_bytes": (_sz, [_P(dr_dims), _i, _i]),
     "dr_decoder_workspace_bytes": (_sz, [_P(dr_dims), _i]),
     "dr_decoder_fwd": (_i, [_P(dr_dims), _P(dr_decoder), _i, fp, _ll, fp, _ll, fp, fp, _sz, fp]),
@@ -144,6 +145,8 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if os.environ.get("DREAMER_CONV1_DIRECT") is not None:  # A/B knob: 0 = LDS-tiled first conv
+        lib.dr_set_conv1_direct(int(os.environ["DREAMER_CONV1_DIRECT"]))
     _lib = lib
     return lib
 

@@ -182,6 +182,93 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
       }
 }
 
+// First layer (CIN = 4, K = 64): no LDS.  Every MFMA fragment piece is one
+// float4 of global memory -- lane (r, q) of A slice s is pixel r's tap
+// s/4 + q (4 channels), of B the 4 weights of that tap -- so each wave loads
+// all 16 of its fragments up front and runs its 32 x 32 tile on its own: no
+// barriers, occupancy bounded by VGPRs only (the LDS-tiled kernel spends this
+// short K loop waiting on its staging round trip).  Same k permutation and MFMA
+// order as k_conv_nhwc<.., 4, ..>: bitwise the same outputs.
+__global__ __launch_bounds__(256) void k_conv1_direct(int n_frames, int ih, int iw, int cout,
+                                                      const float* __restrict__ in, const float* __restrict__ wr,
+                                                      const float* __restrict__ bias, float* __restrict__ out,
+                                                      float* __restrict__ pre) {
+  constexpr int K = 64, WPX = 32;  // pixels per wave; 4 waves = 128 pixels x 32 channels per workgroup
+  const int oh = ih / 2, ow = iw / 2, hw = oh * ow;
+  const long long M = (long long)n_frames * hw;
+  const int tiles_n = cout / 32;
+  const long long tiles = ((M + 127) / 128) * tiles_n;
+  const int lt = dr_xcd_tile(blockIdx.x, (int)tiles);
+  if (lt < 0) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const long long m0 = (long long)(lt / tiles_n) * 128 + wave * WPX;
+  const int n0 = (lt % tiles_n) * 32;
+
+  float4 a[4][2], b[4][2];  // [slice][fragment]
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long long m = m0 + 16 * i + r;
+    const bool ok = m < M;
+    const long long mm = ok ? m : 0;
+    const long long f = mm / hw;
+    const int p = (int)(mm - f * hw), oy = p / ow, ox = p - oy * ow;
+    const float* base = in + f * ih * iw * 4;
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) {
+      const int tap = 4 * sl + q, y = 2 * oy - 1 + (tap >> 2), x = 2 * ox - 1 + (tap & 3);
+      a[sl][i] = (ok && y >= 0 && y < ih && x >= 0 && x < iw)
+                     ? *reinterpret_cast<const float4*>(base + ((long long)y * iw + x) * 4)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl)
+      b[sl][j] = *reinterpret_cast<const float4*>(wr + (long long)(n0 + 16 * j + r) * K + 16 * sl + 4 * q);
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int sl = 0; sl < 4; ++sl) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[sl][i].x, b[sl][j].x, acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[sl][i].y, b[sl][j].y, acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[sl][i].z, b[sl][j].z, acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[sl][i].w, b[sl][j].w, acc[i][j], 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const long long m = m0 + 16 * i + 4 * q + e;
+        const int co = n0 + 16 * j + r;
+        if (m >= M) continue;
+        float v = acc[i][j][e] + bias[co];
+        if (pre) pre[m * cout + co] = v;
+        out[m * cout + co] = v / (1.0f + expf(-v));
+      }
+}
+
+static int g_conv1_direct = 1;
+extern "C" void dr_set_conv1_direct(int on) { g_conv1_direct = on ? 1 : 0; }
+
 // Extra dynamic LDS per conv workgroup (bytes).  Padding past half the CU's
 // LDS leaves one conv workgroup per CU, so that latency-bound kernels of a
 // concurrent stream find room beside it (pipelined epochs, engine.py).
@@ -211,6 +298,16 @@ static int launch_conv(int n, int ih, int iw, int cout, const float* in, const f
 
 int op_conv_nhwc_ex(int n, int cin, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
                     float* out, int out_nchw, float* pre, int epi, hipStream_t s) {
+  if (g_conv1_direct && cin == 4 && epi == CONV_EPI_FWD && !out_nchw && cout % 32 == 0) {
+    const long long tiles = (((long long)n * (ih / 2) * (iw / 2) + 127) / 128) * (cout / 32);
+    if (tiles >= (1LL << 30)) {
+      dr_set_error("conv: too many tiles");
+      return DR_E_INVALID;
+    }
+    hipLaunchKernelGGL(k_conv1_direct, dim3((unsigned)dr_xcd_grid((int)tiles)), dim3(256), 0, s, n, ih, iw, cout, in, wr,
+                       bias, out, pre);
+    return dr_check_launch("conv1_direct");
+  }
   if (epi == CONV_EPI_DSILU && (out_nchw || !pre)) {
     dr_set_error("conv: the SiLU-backward epilogue needs NHWC output and a pre-activation tensor");
     return DR_E_INVALID;

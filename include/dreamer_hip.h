@@ -303,6 +303,12 @@ int dr_rng_advance(unsigned long long* rng, unsigned long long delta, hipStream_
  * concurrent stream's latency-bound kernels find room (pipelined epochs). */
 void dr_set_conv_lds_pad(int bytes);
 
+/* First encoder conv (3(4) input channels, dr_encoder_features and the
+ * world-model step): 1 (default) = the LDS-free direct-fragment MFMA kernel,
+ * 0 = the LDS-tiled implicit GEMM.  Bitwise the same outputs; applies to
+ * launches made (or graph-captured) after the call. */
+void dr_set_conv1_direct(int on);
+
 #ifdef __cplusplus
 }
 #endif

@@ -288,3 +288,22 @@ def test_imagine_fused_tails_match(gpu):
     assert torch.equal(outs[0][0].reshape(-1, C).argmax(-1), outs[1][0].reshape(-1, C).argmax(-1))
     for a, b, name in zip(outs[0][1:], outs[1][1:], ("hiddens", "actions", "rewards", "continues")):
         close(b, a, 1e-4, 1e-5, "fused tails " + name)
+
+
+@pytest.mark.parametrize("which", WHICH)
+def test_conv1_direct_bitwise(which, gpu):
+    """The LDS-free first conv (dr_set_conv1_direct(1), default) gives the
+    warm start of the LDS-tiled implicit GEMM bit for bit."""
+    from dreamer_amd import _lib as L
+    fx, d, P, eng = _engine_case(which, gpu)
+    d.buffer.gather_actions(eng.starts, eng.act_win)
+    outs = []
+    for on in (0, 1):
+        L.load().dr_set_conv1_direct(on)
+        try:
+            eng.encode_and_warm(d.buffer.frames_struct(eng.starts), noise_q=_t(fx["q_warm"], gpu))
+            torch.cuda.synchronize()
+        finally:
+            L.load().dr_set_conv1_direct(1)
+        outs.append((cpu(eng.z0).clone(), cpu(eng.h0).clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
