@@ -237,33 +237,38 @@ __global__ __launch_bounds__(256) void k_conv1_direct(int n_frames, int ih, int 
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[sl][i].x, b[sl][j].x, acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[sl][j].x, a[sl][i].x, acc[i][j], 0, 0, 0);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[sl][i].y, b[sl][j].y, acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[sl][j].y, a[sl][i].y, acc[i][j], 0, 0, 0);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[sl][i].z, b[sl][j].z, acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[sl][j].z, a[sl][i].z, acc[i][j], 0, 0, 0);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[sl][i].w, b[sl][j].w, acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[sl][j].w, a[sl][i].w, acc[i][j], 0, 0, 0);
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const long long m = m0 + 16 * i + 4 * q + e;
-        const int co = n0 + 16 * j + r;
-        if (m >= M) continue;
-        float v = acc[i][j][e] + bias[co];
-        if (pre) pre[m * cout + co] = v;
-        out[m * cout + co] = v / (1.0f + expf(-v));
-      }
+    for (int j = 0; j < 2; ++j) {
+      // weights are the MFMA A operand, pixels the B operand: lane (r, q) holds
+      // channels 4q..4q+3 of pixel r, stored as one float4 per tensor
+      const long long m = m0 + 16 * i + r;
+      if (m >= M) continue;
+      const int co = n0 + 16 * j + 4 * q;
+      const float4 bv = *reinterpret_cast<const float4*>(bias + co);
+      float4 v = make_float4(acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w);
+      if (pre) *reinterpret_cast<float4*>(pre + m * cout + co) = v;
+      v.x = v.x / (1.0f + expf(-v.x));
+      v.y = v.y / (1.0f + expf(-v.y));
+      v.z = v.z / (1.0f + expf(-v.z));
+      v.w = v.w / (1.0f + expf(-v.w));
+      *reinterpret_cast<float4*>(out + m * cout + co) = v;
+    }
 }
 
 static int g_conv1_direct = 1;
