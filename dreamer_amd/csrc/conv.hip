@@ -19,6 +19,11 @@
 // CONV_EPI_FWD: out = SiLU(acc + bias), optionally pre[m][co] = acc + bias
 // (NHWC, kept for the backward).  CONV_EPI_DSILU (world-model backward, a
 // transposed conv's input gradient): out[m][co] = acc * SiLU'(pre[m][co]).
+// MFMA operand order of the conv tile: the output layout decides which of
+// pixels / channels ends up 4-consecutive in a lane (see the epilogue)
+#define DR_CONV_MFMA(A_, B_, C_) \
+  (OUT_NCHW ? __builtin_amdgcn_mfma_f32_16x16x4f32(A_, B_, C_, 0, 0, 0) : __builtin_amdgcn_mfma_f32_16x16x4f32(B_, A_, C_, 0, 0, 0))
+
 template <int BM, int BN, int CIN, bool OUT_NCHW, int EPI>
 __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw, int cout,
                                                    const float* __restrict__ in, const float* __restrict__ wr,
@@ -134,19 +139,19 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j) acc[i][j] = DR_CONV_MFMA(a[i].x, b[j].x, acc[i][j]);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j) acc[i][j] = DR_CONV_MFMA(a[i].y, b[j].y, acc[i][j]);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j) acc[i][j] = DR_CONV_MFMA(a[i].z, b[j].z, acc[i][j]);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j) acc[i][j] = DR_CONV_MFMA(a[i].w, b[j].w, acc[i][j]);
       }
       if (c + 1 < NCH) {
         store((u + 1) % PIPE, buf ^ 1);
@@ -156,30 +161,48 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
     }
   }
 
+  // NHWC output: weights are the MFMA A operand (DR_CONV_MFMA), so lane (r, q)
+  // holds channels 4q..4q+3 of pixel r and stores float4s along c.  NCHW
+  // output: pixels are the A operand, so the lane holds 4 consecutive pixels
+  // of channel r, one float4 along the plane (hw % 4 == 0, checked on the host).
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const long long m = m0 + wm0 + 16 * i + 4 * q + e;
+    for (int j = 0; j < FN; ++j) {
+      if (OUT_NCHW) {
+        const long long m = m0 + wm0 + 16 * i + 4 * q;
         const int co = n0 + wn0 + 16 * j + r;
         if (m >= M || co >= cout) continue;
-        float v;
+        const float bv = bias[co];
+        f32x4 v = acc[i][j] + bv;
+        if (pre) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pre[(m + e) * cout + co] = v[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] / (1.0f + expf(-v[e]));
+        const long long f = m / hw;
+        *reinterpret_cast<f32x4*>(out + (f * cout + co) * hw + (m - f * hw)) = v;
+      } else {
+        const long long m = m0 + wm0 + 16 * i + r;
+        const int co = n0 + wn0 + 16 * j + 4 * q;
+        if (m >= M || co >= cout) continue;
+        f32x4 v;
         if (EPI == CONV_EPI_DSILU) {
-          v = acc[i][j][e] * dr_dsilu(pre[m * cout + co]);
+          const f32x4 pv = *reinterpret_cast<const f32x4*>(pre + m * cout + co);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * dr_dsilu(pv[e]);
         } else {
-          v = acc[i][j][e] + bias[co];
-          if (pre) pre[m * cout + co] = v;
-          v = v / (1.0f + expf(-v));
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + co);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
+          if (pre) *reinterpret_cast<f32x4*>(pre + m * cout + co) = v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] / (1.0f + expf(-v[e]));
         }
-        if (OUT_NCHW) {
-          const long long f = m / hw;
-          out[(f * cout + co) * hw + (m - f * hw)] = v;
-        } else {
-          out[m * cout + co] = v;
-        }
+        *reinterpret_cast<f32x4*>(out + m * cout + co) = v;
       }
+    }
 }
 
 // First layer (CIN = 4, K = 64): no LDS.  Every MFMA fragment piece is one
@@ -283,6 +306,10 @@ extern "C" void dr_set_conv_lds_pad(int bytes) { g_conv_lds_pad = bytes < 0 ? 0 
 template <int BM, int BN, int CIN, bool OUT_NCHW, int EPI>
 static int launch_conv(int n, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
                        float* out, float* pre, hipStream_t s) {
+  if (cout % 4 != 0 || (OUT_NCHW && ((ih / 2) * (iw / 2)) % 4 != 0)) {
+    dr_set_error("conv: float4 epilogue needs cout %% 4 == 0 (and oh*ow %% 4 == 0 for NCHW output)");
+    return DR_E_INVALID;
+  }
   const long long M = (long long)n * (ih / 2) * (iw / 2);
   const long long tiles = ((M + BM - 1) / BM) * ((cout + BN - 1) / BN);
   if (tiles >= (1LL << 30)) {
