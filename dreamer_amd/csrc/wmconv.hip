@@ -40,6 +40,10 @@ int op_convT_repack(int cin, int cout, const float* wt, float* wq, hipStream_t s
 template <int BM, int BN, int CIN, int EPI, bool SILU_IN>
 __global__ __launch_bounds__(256) void k_convT_nhwc(ConvTArgs a) {
   constexpr int K = CIN * 4;
+  // TR: weights are the MFMA A operand, so a lane's 4 accumulators are 4
+  // consecutive channels of one pixel (float4 epilogue); the TANH_MSE
+  // epilogue keeps pixels-as-A so its err^2 partial sums keep their order
+  constexpr bool TR = EPI != CT_EPI_TANH_MSE;
   constexpr int APT = BM / 32;
   constexpr int BPT = BN >= 32 ? BN / 32 : 1;
   constexpr int WN = BN >= 32 ? 2 : 1, WM = 4 / WN;
@@ -138,19 +142,23 @@ __global__ __launch_bounds__(256) void k_convT_nhwc(ConvTArgs a) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].x, bv[j].x, acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_16x16x4f32(bv[j].x, av[i].x, acc[i][j], 0, 0, 0)
+                                : __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].x, bv[j].x, acc[i][j], 0, 0, 0);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].y, bv[j].y, acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_16x16x4f32(bv[j].y, av[i].y, acc[i][j], 0, 0, 0)
+                                : __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].y, bv[j].y, acc[i][j], 0, 0, 0);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].z, bv[j].z, acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_16x16x4f32(bv[j].z, av[i].z, acc[i][j], 0, 0, 0)
+                                : __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].z, bv[j].z, acc[i][j], 0, 0, 0);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].w, bv[j].w, acc[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_16x16x4f32(bv[j].w, av[i].w, acc[i][j], 0, 0, 0)
+                                : __builtin_amdgcn_mfma_f32_16x16x4f32(av[i].w, bv[j].w, acc[i][j], 0, 0, 0);
     }
     if (c + 1 < NCH) store(buf ^ 1);
     dr_lds_barrier();
@@ -158,6 +166,60 @@ __global__ __launch_bounds__(256) void k_convT_nhwc(ConvTArgs a) {
 
   const int OW = 2 * w, OH = 2 * h, ldc = a.ldc;
   float sq = 0.0f;
+  if (TR) {
+    const bool vec = (cout % 4 == 0) && (ldc % 4 == 0);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const long long m = m0 + wm0 + 16 * i + r;
+      if (m >= M) continue;
+      const long long f = m / hw;
+      const int p = (int)(m - f * hw);
+      const int y = p / w, x = p - y * w;
+      const long long opix = (f * OH + 2 * y + py) * OW + 2 * x + px;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int co0 = n0 + wn0 + 16 * j + 4 * q;
+        if (co0 >= ldc) continue;
+        if (vec && co0 < cout) {
+          f32x4 v = acc[i][j];
+          if (EPI == CT_EPI_BIAS) {
+            v += *reinterpret_cast<const f32x4*>(a.bias + co0);
+            f32x4 sv = v;
+            if (a.out2 || a.silu_out) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) sv[e] = dr_silu(v[e]);
+            }
+            *reinterpret_cast<f32x4*>(a.out + opix * ldc + co0) = a.silu_out ? sv : v;
+            if (a.out2) *reinterpret_cast<f32x4*>(a.out2 + opix * ldc + co0) = sv;
+          } else {
+            const f32x4 pv = *reinterpret_cast<const f32x4*>(a.pre + opix * cout + co0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = v[e] * dr_dsilu(pv[e]);
+            *reinterpret_cast<f32x4*>(a.out + opix * ldc + co0) = v;
+          }
+          continue;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int co = co0 + e;
+          if (co >= ldc) break;
+          if (co >= cout) {
+            a.out[opix * ldc + co] = 0.0f;
+            continue;
+          }
+          const float v = acc[i][j][e];
+          if (EPI == CT_EPI_BIAS) {
+            const float pv = v + a.bias[co];
+            const float sv = (a.out2 || a.silu_out) ? dr_silu(pv) : 0.0f;
+            a.out[opix * ldc + co] = a.silu_out ? sv : pv;
+            if (a.out2) a.out2[opix * ldc + co] = sv;
+          } else {
+            a.out[opix * ldc + co] = v * dr_dsilu(a.pre[opix * cout + co]);
+          }
+        }
+      }
+    }
+  } else
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
