@@ -92,6 +92,7 @@ _SIGS = {
     "dr_step_workspace_bytes": (_sz, [_P(dr_dims), _i]),
     "dr_imagine_step": (_i, [_P(dr_dims), _P(dr_world_model), _i, fp, fp, fp, dr_noise, fp, fp, fp, fp,
                              fp, _sz, fp]),
+    "dr_actor_act_workspace_bytes": (_sz, [_P(dr_dims), _i]),
     "dr_actor_act": (_i, [_P(dr_dims), _P(dr_actor), _i, fp, fp, dr_noise, _i, fp, fp, fp, fp, _sz, fp]),
     "dr_gru_cell": (_i, [_P(dr_dims), _P(dr_world_model), _i, fp, fp, fp, fp, fp, _sz, fp]),
     "dr_categorical_sample": (_i, [_i, _i, _i, fp, dr_noise, fp, fp, fp, fp]),
@@ -113,8 +114,6 @@ _SIGS = {
     "dr_nonfinite": (_i, [_ll, fp, fp, fp]),
     "dr_replay_gather": (_i, [_ll, _i, _i, _i, _i, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp]),
     "dr_rng_advance": (_i, [fp, C.c_ulonglong, fp]),
-    "dr_set_conv_lds_pad": (None, [_i]),
-    "dr_set_conv1_direct": (None, [_i]),
     "dr_wm_train_workspace_bytes": (_sz, [_P(dr_dims), _i, _i]),
     "dr_decoder_workspace_bytes": (_sz, [_P(dr_dims), _i]),
     "dr_decoder_fwd": (_i, [_P(dr_dims), _P(dr_decoder), _i, fp, _ll, fp, _ll, fp, fp, _sz, fp]),
@@ -145,8 +144,6 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if os.environ.get("DREAMER_CONV1_DIRECT") is not None:  # A/B knob: 0 = LDS-tiled first conv
-        lib.dr_set_conv1_direct(int(os.environ["DREAMER_CONV1_DIRECT"]))
     _lib = lib
     return lib
 

@@ -139,8 +139,8 @@ class Actor(nn.Module):
         A = self.action_dim
         a, mu, sg = (torch.empty(B, A, device=h.device) for _ in range(3))
         d = self._dims(h.shape[1], z.shape[1])
-        ws = hip.workspace(h.device).get("act", 4 * B * (2 * self.base_net[0].out_features + A + 64))
-        L.call("dr_actor_act", d, self.struct(), B, L.ptr(h), L.ptr(z), hip.rng(h.device).noise(),
+        ws = hip.workspace(h.device).get("act", L.query("dr_actor_act_workspace_bytes", d, B))
+        L.call("dr_actor_act", d, self.struct(), B, L.ptr(h), L.ptr(z), hip.adhoc(h.device).noise(),
                int(deterministic), L.ptr(a), L.ptr(mu), L.ptr(sg), L.ptr(ws), ws.numel(), hip.stream())
         return a.view(*lead, A), mu.view(*lead, A), sg.view(*lead, A)
 

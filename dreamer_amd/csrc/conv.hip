@@ -294,14 +294,6 @@ __global__ __launch_bounds__(256) void k_conv1_direct(int n_frames, int ih, int 
     }
 }
 
-static int g_conv1_direct = 1;
-extern "C" void dr_set_conv1_direct(int on) { g_conv1_direct = on ? 1 : 0; }
-
-// Extra dynamic LDS per conv workgroup (bytes).  Padding past half the CU's
-// LDS leaves one conv workgroup per CU, so that latency-bound kernels of a
-// concurrent stream find room beside it (pipelined epochs, engine.py).
-static int g_conv_lds_pad = 0;
-extern "C" void dr_set_conv_lds_pad(int bytes) { g_conv_lds_pad = bytes < 0 ? 0 : bytes; }
 
 template <int BM, int BN, int CIN, bool OUT_NCHW, int EPI>
 static int launch_conv(int n, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
@@ -323,14 +315,14 @@ static int launch_conv(int n, int ih, int iw, int cout, const float* in, const f
     return true;
   }();
   (void)raised;
-  hipLaunchKernelGGL((k_conv_nhwc<BM, BN, CIN, OUT_NCHW, EPI>), grid, dim3(256), g_conv_lds_pad, s, n, ih, iw, cout,
+  hipLaunchKernelGGL((k_conv_nhwc<BM, BN, CIN, OUT_NCHW, EPI>), grid, dim3(256), 0, s, n, ih, iw, cout,
                      in, wr, bias, out, pre);
   return dr_check_launch("conv");
 }
 
 int op_conv_nhwc_ex(int n, int cin, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
                     float* out, int out_nchw, float* pre, int epi, hipStream_t s) {
-  if (g_conv1_direct && cin == 4 && epi == CONV_EPI_FWD && !out_nchw && cout % 32 == 0) {
+  if (cin == 4 && epi == CONV_EPI_FWD && !out_nchw && cout % 32 == 0) {
     const long long tiles = (((long long)n * (ih / 2) * (iw / 2) + 127) / 128) * (cout / 32);
     if (tiles >= (1LL << 30)) {
       dr_set_error("conv: too many tiles");

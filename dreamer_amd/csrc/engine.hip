@@ -125,7 +125,7 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
       float* hn = w.hb[hb];
       hb ^= 1;
       DR_TRY(gru_onehot(d, wm, B, w.idx, actions + ai * act_st, act_sb, h, Hd, hn, Hd, w.wt, nullptr,
-                        nullptr, nullptr, nullptr, s));
+                        nullptr, nullptr, nullptr, s, z_out, L));
       h = hn;
     }
     // latent_mapper.0 on cat(features, h): feature part precomputed in feat[t]
@@ -243,14 +243,6 @@ extern "C" size_t dr_imagine_workspace_bytes(const dr_dims* d, int B, int H) {
   return c.off;
 }
 
-// knob: fused head tails in the imagination unroll (mlp2_launch).  Off by
-// default: measured slower (tools/kbench "mlp2": one fused tail 16.6-18.9 us
-// against 10.3 us for its two skinny launches at B = 64) -- a workgroup that
-// owns all 200 columns of the middle layer serialises ~85 MFMAs per wave that
-// the split launches spread over 13 CUs.
-static int g_fuse_tails = 0;
-extern "C" void dr_debug_fuse_tails(int v) { g_fuse_tails = v; }
-
 extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, int B, int H,
                               const float* z0, const float* h0, dr_noise noise, int deterministic, float* latents,
                               float* hiddens, float* actions, float* rewards, float* continues, float* mus,
@@ -270,12 +262,6 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
   const long long lda1 = (long long)H * a1, lda2 = (long long)H * a2;
   DR_TRY(copy2d(latents, ldL, z0, L, L, B, s));
   DR_TRY(copy2d(hiddens, ldH, h0, Hd, Hd, B, s));
-  // the 3-layer heads' tails as one launch each (mlp2_launch) where the widths allow
-  const bool fuse_tails = g_fuse_tails && d->prior_h1 <= 256 && d->prior_h2 <= 256 && d->rew_h1 <= 256 &&
-                          d->rew_h2 <= 256 && d->cont_h1 <= 256 && d->cont_h2 <= 256 && a1 <= 256 && a2 <= 256 &&
-                          d->prior_h1 % 4 == 0 && d->prior_h2 % 4 == 0 && d->rew_h1 % 4 == 0 && d->rew_h2 % 4 == 0 &&
-                          d->cont_h1 % 4 == 0 && d->cont_h2 % 4 == 0 && a1 % 4 == 0 && a2 % 4 == 0 && 2 * A <= 16 &&
-                          32 % d->cols == 0;
   dr_noise nq = noise;  // Categorical draws: a Philox stream apart from the actor's
   nq.stream += 65536;
   DR_TRY(op_transpose(3 * Hd, L + A, wm->w_ih, w.wt, s));
@@ -301,24 +287,15 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
     float* z_n = latents + (long long)(t + 1) * L;
     // WorldModel.imagine_step (WorldModel.py:72-77)
     DR_TRY(gru_onehot(d, wm, B, w.idx[t & 1], actions + (long long)t * A, ldA, h_t, ldH, h_n, ldH, w.wt,
-                      tp.r + hb, tp.u + hb, tp.n + hb, tp.ghn + hb, s));
+                      tp.r + hb, tp.u + hb, tp.n + hb, tp.ghn + hb, s, z_t, ldL));
     float* p1 = tp.pre1p + (long long)t * B * d->prior_h1;
     float* p2 = tp.pre2p + (long long)t * B * d->prior_h2;
     DR_TRY(run(G_NT, AM_PLAIN, lin(B, d->prior_h1, Hd, h_n, ldH, wm->prior.l0.w, Hd, wm->prior.l0.b, p1, d->prior_h1), s));
-    if (fuse_tails) {
-      // prior tail (LN-SiLU, l3, LN-SiLU, l6 + sampler) in one launch
-      GemmArgs g = lin_ln(B, L, d->prior_h2, nullptr, 0, wm->prior.n4, wm->prior.l6.w, wm->prior.l6.b, nullptr, 0);
-      with_sampler(g, d, nq, t, z_n, ldL, w.idx[(t + 1) & 1], tp.soft + (long long)t * B * L, L);
-      Mlp2Args a = mlp2(B, d->prior_h1, d->prior_h2, p1, d->prior_h1, wm->prior.n1, wm->prior.l3, wm->prior.n4, g);
-      a.pre2 = p2; a.ld_pre2 = d->prior_h2;
-      DR_TRY(mlp2_launch(&a, 1, s));
-    } else {
-      DR_TRY(run(G_NT, AM_LNSILU, lin_ln(B, d->prior_h2, d->prior_h1, p1, d->prior_h1, wm->prior.n1, wm->prior.l3.w,
-                                         wm->prior.l3.b, p2, d->prior_h2), s));
-      GemmArgs g = lin_ln(B, L, d->prior_h2, p2, d->prior_h2, wm->prior.n4, wm->prior.l6.w, wm->prior.l6.b, nullptr, 0);
-      with_sampler(g, d, nq, t, z_n, ldL, w.idx[(t + 1) & 1], tp.soft + (long long)t * B * L, L);
-      DR_TRY(run(G_NT, AM_LNSILU, g, s));
-    }
+    DR_TRY(run(G_NT, AM_LNSILU, lin_ln(B, d->prior_h2, d->prior_h1, p1, d->prior_h1, wm->prior.n1, wm->prior.l3.w,
+                                       wm->prior.l3.b, p2, d->prior_h2), s));
+    GemmArgs g = lin_ln(B, L, d->prior_h2, p2, d->prior_h2, wm->prior.n4, wm->prior.l6.w, wm->prior.l6.b, nullptr, 0);
+    with_sampler(g, d, nq, t, z_n, ldL, w.idx[(t + 1) & 1], tp.soft + (long long)t * B * L, L);
+    DR_TRY(run(G_NT, AM_LNSILU, g, s));
     // reward / continue heads on (h', z') and the actor for step t+1, grouped
     const bool nxt = (t + 1 < H);
     {
@@ -328,29 +305,6 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
       if (nxt)
         p[2] = lin2(B, a1, h_n, ldH, Hd, z_n, ldL, L, ac->l0.w, ac->l0.b, tp.pre1a + (long long)(t + 1) * a1, lda1);
       DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, nxt ? 3 : 2, s));
-    }
-    if (fuse_tails) {
-      // reward / continue / next-step actor tails in one grouped launch
-      Mlp2Args q[3];
-      GemmArgs er = lin_ln(B, d->buckets, d->rew_h2, nullptr, 0, wm->reward.n4, wm->reward.l6.w, wm->reward.l6.b,
-                           w.rlog + (long long)t * d->buckets, (long long)H * d->buckets);
-      q[0] = mlp2(B, d->rew_h1, d->rew_h2, w.p1r, d->rew_h1, wm->reward.n1, wm->reward.l3, wm->reward.n4, er);
-      GemmArgs ec = lin_ln(B, 1, d->cont_h2, nullptr, 0, wm->cont.n4, wm->cont.l6.w, wm->cont.l6.b, continues + t, H);
-      ec.act = 2;
-      q[1] = mlp2(B, d->cont_h1, d->cont_h2, w.p1c, d->cont_h1, wm->cont.n1, wm->cont.l3, wm->cont.n4, ec);
-      if (nxt) {
-        const long long o = (long long)(t + 1) * A;
-        GemmArgs ea = lin_ln(B, 2 * A, a2, nullptr, 0, ac->n4, w.wst, w.bst, nullptr, 0);
-        with_actor_head(ea, A, noise, t + 1, deterministic, actions + o, ldA, mus + o, ldA, sigmas + o, ldA,
-                        tp.eps + (long long)(t + 1) * B * A, tp.ls_raw + o, ldA);
-        dr_linear l3 = {ac->l3.w, ac->l3.b};
-        q[2] = mlp2(B, a1, a2, tp.pre1a + (long long)(t + 1) * a1, lda1, ac->n1, l3, ac->n4, ea);
-        q[2].a1_out = tp.x1a + (long long)(t + 1) * a1; q[2].ld_a1 = lda1;
-        q[2].pre2 = tp.pre2a + (long long)(t + 1) * a2; q[2].ld_pre2 = lda2;
-        q[2].a2_out = tp.x2a + (long long)(t + 1) * a2; q[2].ld_a2 = lda2;
-      }
-      DR_TRY(mlp2_launch(q, nxt ? 3 : 2, s));
-      continue;
     }
     {
       GemmArgs p[3];
@@ -794,16 +748,32 @@ extern "C" int dr_imagine_step(const dr_dims* d, const dr_world_model* wm, int B
   return DR_OK;
 }
 
+struct ActWs {
+  float *p1, *p2, *ls;
+};
+static void act_carve(Carve& c, const dr_dims* d, int B, ActWs& w) {
+  w.p1 = c.f((long long)B * d->actor_h1);
+  w.p2 = c.f((long long)B * d->actor_h2);
+  w.ls = c.f((long long)B * d->action);
+}
+
+extern "C" size_t dr_actor_act_workspace_bytes(const dr_dims* d, int B) {
+  Carve c(nullptr);
+  ActWs w;
+  act_carve(c, d, B, w);
+  return c.off;
+}
+
 extern "C" int dr_actor_act(const dr_dims* d, const dr_actor* ac, int B, const float* h, const float* z,
                             dr_noise noise, int deterministic, float* a_out, float* mu_out, float* sigma_out,
                             void* ws, size_t ws_bytes, hipStream_t s) {
   DR_REQUIRE(d && ac && h && z && a_out && mu_out && sigma_out && B > 0, "null argument");
   const int L = latent(d), Hd = d->hidden, A = d->action, a1 = d->actor_h1, a2 = d->actor_h2;
   Carve c(ws);
-  float* p1 = c.f((long long)B * a1);
-  float* p2 = c.f((long long)B * a2);
-  float* ls = c.f((long long)B * A);
+  ActWs w;
+  act_carve(c, d, B, w);
   WS_CHECK(c, ws_bytes);
+  float *p1 = w.p1, *p2 = w.p2, *ls = w.ls;
   DR_TRY(run(G_NT, AM_PLAIN, lin2(B, a1, h, Hd, Hd, z, L, L, ac->l0.w, ac->l0.b, p1, a1), s));
   DR_TRY(run(G_NT, AM_LNSILU, lin_ln(B, a2, a1, p1, a1, ac->n1, ac->l3.w, ac->l3.b, p2, a2), s));
   GemmArgs p[2];

@@ -213,9 +213,13 @@ static inline int stack_heads(const dr_actor* ac, int A, int in, float* w, float
 }
 
 // GRU step on a sampled one-hot latent (idx) via the fused kernel
+// z / ldz: the latent rows idx came from (read only for dense-marked groups; NULL
+// where idx always comes from the sampler)
 static inline int gru_onehot(const dr_dims* d, const dr_world_model* wm, int B, int* idx, const float* a, long long lda, const float* h, long long ldh, float* hout,
-                      long long ldo, const float* wt, float* sr, float* su, float* sn, float* sghn, hipStream_t s) {
+                      long long ldo, const float* wt, float* sr, float* su, float* sn, float* sghn, hipStream_t s,
+                      const float* z = nullptr, long long ldz = 0) {
   GruArgs g;
+  g.z = z; g.ldz = ldz;
   g.B = B; g.Hd = d->hidden; g.R = d->rows; g.C = d->cols; g.A = d->action;
   g.idx = idx; g.zval = onehot_vals(idx, B, d->rows); g.a = a; g.lda = lda; g.h = h; g.ldh = ldh;
   g.wt = wt; g.b_ih = wm->b_ih; g.w_hh = wm->w_hh; g.b_hh = wm->b_hh;

@@ -1195,17 +1195,24 @@ static bool skinny_offsets_ok(const GemmArgs& g, bool b_kn) {
   return true;
 }
 
-// minimum dynamic LDS per skinny workgroup (bytes); a large value keeps one
-// workgroup per CU.  Set by dr_debug_gemm_min_lds / DREAMER_MIN_LDS.
-static size_t g_min_lds = (size_t)-1;
+// Microbenchmark A/B knobs (tools/kbench) exist only in the phase-timing
+// debug build; the product library has no process-wide mutable state here.
+#ifdef DR_PHASE_TIMING
+static size_t g_min_lds = 0;       // minimum dynamic LDS per skinny workgroup (bytes)
+static int g_skinny_variant = 0;   // 1 = 64-row tiles for M <= 64, 2 = never 32-column tiles
+static int g_tile_wgs = 512;       // split-K target: workgroups per launch
+static int g_tile_variant = 0;     // tile-GEMM shape variant
 extern "C" void dr_debug_gemm_min_lds(long long bytes) { g_min_lds = (size_t)bytes; }
-static size_t min_lds() {
-  if (g_min_lds == (size_t)-1) {
-    const char* e = getenv("DREAMER_MIN_LDS");
-    g_min_lds = e ? (size_t)atoll(e) : 0;
-  }
-  return g_min_lds;
-}
+extern "C" void dr_debug_skinny_variant(int v) { g_skinny_variant = v; }
+extern "C" void dr_debug_tile_wgs(int v) { g_tile_wgs = v > 0 ? v : 512; }
+extern "C" void dr_debug_tile_variant(int v) { g_tile_variant = v; }
+#else
+static constexpr size_t g_min_lds = 0;
+static constexpr int g_skinny_variant = 0;
+static constexpr int g_tile_wgs = 512;
+static constexpr int g_tile_variant = 0;
+#endif
+static size_t min_lds() { return g_min_lds; }
 
 // floats of dynamic LDS a skinny launch needs (mirrors the kernel's layout)
 template <int MT, int NT, int AMODE, bool B_KN>
@@ -1254,9 +1261,6 @@ static void launch_skinny(const GemmBatch& gb, int count, bool vec, hipStream_t 
 }
 
 
-// skinny-GEMM tile knob (microbenchmark): 1 = 64-row tiles for M <= 64, 2 = never 32-column tiles
-static int g_skinny_variant = 0;
-extern "C" void dr_debug_skinny_variant(int v) { g_skinny_variant = v; }
 
 template <int AMODE, bool B_KN>
 static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
@@ -1571,9 +1575,6 @@ int mlp2_launch(const Mlp2Args* probs, int count, hipStream_t s) {
   return dr_check_launch("mlp2_tail");
 }
 
-// split-K target: workgroups per launch over the problems' real tiles
-static int g_tile_wgs = 512;
-extern "C" void dr_debug_tile_wgs(int v) { g_tile_wgs = v > 0 ? v : 512; }
 
 // mid-size GEMMs: LDS double-buffered tile kernel, split-K when the tile grid
 // is too small to fill the chip and every problem brought scratch for it
@@ -1613,9 +1614,6 @@ static void launch_tile2(GemmBatch& gb, int count, hipStream_t s) {
     hipLaunchKernelGGL(k_splitk_finish, dim3((unsigned)((maxMN + 255) / 256), 1, count), dim3(256), 0, s, gb, splits);
 }
 
-// tile-GEMM shape variant (microbenchmark knob)
-static int g_tile_variant = 0;
-extern "C" void dr_debug_tile_variant(int v) { g_tile_variant = v; }
 
 static bool tile_offsets_ok(const GemmBatch& gb, int count) {
   const long long lim = 1LL << 30;

@@ -6,6 +6,8 @@ struct alignas(16) GruArgs {
   int B, Hd, R, C, A;
   const int* idx;       // [B][R] sampled class per latent group
   const float* zval;    // [B][R] straight-through latent value at idx
+  const float* z;       // the latent rows idx was taken from (row stride ldz), read only for
+  long long ldz;        //   groups marked dense (idx < 0: more than one non-zero class)
   const float* a;       // actions [B][A], row stride lda
   long long lda;
   const float* h;       // previous hidden (NULL = zeros), row stride ldh

@@ -71,22 +71,27 @@ int op_transpose_multi(const TransposeJob* jobs, int n, hipStream_t s) {
 }
 
 // index of the non-zero entry of each one-hot group (z values are exactly 0
-// off the sample) and its value; groups with no non-zero entry get (0, 0)
+// off the sample) and its value; groups with no non-zero entry get (0, 0).
+// A group with several non-zero classes (a soft / user-supplied latent) is
+// marked dense (idx -1, value 0): the fused GRU then sums all C classes of it
+// (SequenceModel.py:21 is a dense product over flatten(z)).
 __global__ void k_onehot_index(int M, int R, int C, const float* z, long long ldz, int* idx, float* zval) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M * R) return;
   const int m = i / R, g = i - m * R;
   const float* zz = z + (long long)m * ldz + g * C;
-  int k = 0;
+  int k = 0, nz = 0;
   float v = 0.f;
   for (int c = 0; c < C; ++c)
     if (zz[c] != 0.0f) {
-      k = c;
-      v = zz[c];
-      break;
+      if (nz == 0) {
+        k = c;
+        v = zz[c];
+      }
+      ++nz;
     }
-  idx[i] = k;
-  zval[i] = v;
+  idx[i] = nz > 1 ? -1 : k;
+  zval[i] = nz > 1 ? 0.f : v;
 }
 
 int op_onehot_index(int M, int R, int C, const float* z, long long ldz, int* idx, float* zval, hipStream_t s) {
@@ -231,7 +236,7 @@ __global__ __launch_bounds__(512) void k_gru_fused(GruArgs ga) {
 #pragma unroll
       for (int u = 0; u < GRU_MAXR; ++u) {
         const bool ok = live && u < R;
-        w[u] = dr_ld4(wt, ok ? (unsigned)(u * C + iv[u]) * ldw + col : 0u);
+        w[u] = dr_ld4(wt, (ok && iv[u] >= 0) ? (unsigned)(u * C + iv[u]) * ldw + col : 0u);
       }
       float4 wa[GRU_MAXA];
 #pragma unroll
@@ -247,6 +252,24 @@ __global__ __launch_bounds__(512) void k_gru_fused(GruArgs ga) {
           v.y = fmaf(w[u].y, zv[u], v.y);
           v.z = fmaf(w[u].z, zv[u], v.z);
           v.w = fmaf(w[u].w, zv[u], v.w);
+        }
+      }
+      // dense groups (k_onehot_index marker; zval = 0 above): every class
+      bool dense = false;
+#pragma unroll
+      for (int u = 0; u < GRU_MAXR; ++u) dense = dense || (u < R && iv[u] < 0);
+      if (dense && live) {
+        const float* zr = g.z + (long long)m * g.ldz;
+        for (int u = 0; u < R; ++u) {
+          if (iv[u] >= 0) continue;
+          for (int c = 0; c < C; ++c) {
+            const float zc = zr[u * C + c];
+            const float4 wc = dr_ld4(wt, (unsigned)(u * C + c) * ldw + col);
+            v.x = fmaf(wc.x, zc, v.x);
+            v.y = fmaf(wc.y, zc, v.y);
+            v.z = fmaf(wc.z, zc, v.z);
+            v.w = fmaf(wc.w, zc, v.w);
+          }
         }
       }
 #pragma unroll

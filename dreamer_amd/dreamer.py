@@ -116,7 +116,7 @@ class Dreamer(nn.Module):
         tape = torch.empty(L.query("dr_imagine_tape_bytes", d, B, H), dtype=torch.uint8, device=dev)
         ws = hip.workspace(dev).get("im", L.query("dr_imagine_workspace_bytes", d, B, H))
         if eps is None and q is None:
-            nz = hip.rng(dev).noise()
+            nz = hip.adhoc(dev).noise()
         else:
             nz = hip.explicit_noise(q=q, eps=eps, device=dev)
         z = z0.reshape(B, -1).float().contiguous()
@@ -157,7 +157,7 @@ class Dreamer(nn.Module):
         h = torch.empty(B, 1, self.hidden_state_dims, device=dev)
         ws2 = hip.workspace(dev).get("obs", L.query("dr_observe_workspace_bytes", d, B))
         L.call("dr_observe_scan", d, wm, B, T, L.ptr(feat), L.ptr(act), act.shape[1] * A, A, None, None,
-               hip.rng(dev).noise(), L.ptr(z), L.ptr(h), None, L.ptr(ws2), ws2.numel(), st)
+               hip.adhoc(dev).noise(), L.ptr(z), L.ptr(h), None, L.ptr(ws2), ws2.numel(), st)
         return z, h
 
     # --------------------------------------------------------------- training

@@ -65,30 +65,53 @@ def workspace(device):
 
 class Rng:
     """Device Philox state {seed, offset} (uint64 x2).  The seed is drawn from
-    torch's CPU generator so torch.manual_seed controls it; each call site
-    gets a fresh 32-bit stream id."""
+    torch's CPU generator so torch.manual_seed controls it.
 
-    def __init__(self, device):
-        seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    Two generators per device: `rng(dev)` is the engine's (its call sites use
+    fixed stream ids, WARM_STREAM / DREAM_STREAM in engine.py), and
+    `adhoc(dev)` serves the one-off API calls (acting, encode, observe_step,
+    the world-model step) with a different seed, so the two can never draw the
+    same variates.  Each ad-hoc call gets a fresh stream id counter << 17 (a
+    call's kernels add at most 65536 + a step index to it); when the 14-bit
+    counter wraps, the device offset is advanced so ids are never reused."""
+
+    STREAM_SHIFT = 17
+    COUNTER_MASK = (1 << 14) - 1
+
+    def __init__(self, device, salt=0):
+        seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item()) ^ salt
         self.state = torch.tensor([seed, 0], dtype=torch.int64, device=device)
-        self.counter = 1
+        self.counter = 0
 
     def reseed(self, seed):
         self.state.copy_(torch.tensor([seed, 0], dtype=torch.int64))
 
     def noise(self, row0=0):
-        self.counter = (self.counter + 1) & 0x3FFFFFFF
-        return L.dr_noise(None, None, self.state.data_ptr(), row0, self.counter << 1)
+        self.counter = (self.counter + 1) & self.COUNTER_MASK
+        if self.counter == 0:
+            L.call("dr_rng_advance", self.state.data_ptr(), 1, stream())
+            self.counter = 1
+        return L.dr_noise(None, None, self.state.data_ptr(), row0, self.counter << self.STREAM_SHIFT)
 
 
 _rngs = {}
+_adhoc = {}
 
 
 def rng(device):
+    """The engine's generator (fixed per-call-site stream ids)."""
     key = torch.device(device).index or 0
     if key not in _rngs:
         _rngs[key] = Rng(torch.device("cuda", key))
     return _rngs[key]
+
+
+def adhoc(device):
+    """The generator of one-off API calls (see Rng)."""
+    key = torch.device(device).index or 0
+    if key not in _adhoc:
+        _adhoc[key] = Rng(torch.device("cuda", key), salt=0x5DEECE66D)
+    return _adhoc[key]
 
 
 def explicit_noise(q=None, eps=None, device=None):

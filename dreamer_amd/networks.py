@@ -119,7 +119,7 @@ def sample_latent(logits, rows, cols, noise=None):
     lg = logits.reshape(-1, rows * cols).contiguous().float()
     M = lg.shape[0]
     z = torch.empty(M, rows * cols, device=lg.device)
-    nz = noise if noise is not None else hip.rng(lg.device).noise()
+    nz = noise if noise is not None else hip.adhoc(lg.device).noise()
     L.call("dr_categorical_sample", M, rows, cols, L.ptr(lg), nz, L.ptr(z), None, None, hip.stream())
     return z.view(*lead, rows, cols)
 
@@ -250,7 +250,7 @@ class Encoder(nn.Module):
         z = torch.empty(n, self.latent_size, device=dev)
         logits = torch.empty(n, self.latent_size, device=dev)
         ws2 = hip.workspace(dev).get("obs", L.query("dr_observe_workspace_bytes", d, n))
-        nz = noise if noise is not None else hip.rng(dev).noise()
+        nz = noise if noise is not None else hip.adhoc(dev).noise()
         hout = torch.empty_like(h)
         L.call("dr_observe_scan", d, wm, n, 1, L.ptr(feat), None, 0, 0, L.ptr(h), None, nz, L.ptr(z), L.ptr(hout),
                L.ptr(logits), L.ptr(ws2), ws2.numel(), st)

@@ -142,7 +142,7 @@ class WorldModel(nn.Module):
         r, c = torch.empty(B, 1, 1, device=dev), torch.empty(B, 1, 1, device=dev)
         d = self.dims()
         ws = hip.workspace(dev).get("istep", L.query("dr_step_workspace_bytes", d, B))
-        L.call("dr_imagine_step", d, self.packed(), B, L.ptr(h), L.ptr(z), L.ptr(a), hip.rng(dev).noise(), L.ptr(h2),
+        L.call("dr_imagine_step", d, self.packed(), B, L.ptr(h), L.ptr(z), L.ptr(a), hip.adhoc(dev).noise(), L.ptr(h2),
                L.ptr(z2), L.ptr(r), L.ptr(c), L.ptr(ws), ws.numel(), hip.stream())
         return h2, z2, r, c
 
@@ -169,7 +169,7 @@ class WorldModel(nn.Module):
         lg = torch.empty(B, 1, self.latent_num_rows, self.latent_num_columns, device=dev)
         ws2 = hip.workspace(dev).get("obs", L.query("dr_observe_workspace_bytes", d, B))
         L.call("dr_observe_scan", d, wm, B, 1, L.ptr(feat), L.ptr(a), self.action_dims, 0, L.ptr(h_in), L.ptr(z_in),
-               hip.rng(dev).noise(), L.ptr(z), L.ptr(h), L.ptr(lg), L.ptr(ws2), ws2.numel(), st)
+               hip.adhoc(dev).noise(), L.ptr(z), L.ptr(h), L.ptr(lg), L.ptr(ws2), ws2.numel(), st)
         return z, h, lg
 
     # ---- world-model training (PyTorch-ROCm this round) ----------------------
@@ -270,7 +270,7 @@ class WorldModel(nn.Module):
         f = self._ensure_flat()
         d = self.dims()
         row0 = 0 if self._dp is None else self._dp[0] * B  # Philox keyed by the global row
-        noise = hip.explicit_noise(q=noise_q, device=dev) if noise_q is not None else hip.rng(dev).noise(row0=row0)
+        noise = hip.explicit_noise(q=noise_q, device=dev) if noise_q is not None else hip.adhoc(dev).noise(row0=row0)
         cfg = L.dr_wm_loss_cfg(self.beta_pred, self.beta_dyn, self.beta_rep)
         if getattr(self, "_scratch", None) is None or self._scratch[0].device != torch.device(dev):
             self._scratch = (torch.empty(4, device=dev), torch.zeros(1, dtype=torch.int32, device=dev),

@@ -168,7 +168,8 @@ int dr_imagine_bwd_main(const dr_dims* d, const dr_world_model* wm, const dr_act
 int dr_imagine_step(const dr_dims* d, const dr_world_model* wm, int B, const float* h, const float* z,
                     const float* a, dr_noise noise, float* h_out, float* z_out, float* r_out, float* c_out,
                     void* ws, size_t ws_bytes, hipStream_t stream);
-/* Actor.act (Agent.py:202-210) */
+/* Actor.act (Agent.py:202-210); workspace from dr_actor_act_workspace_bytes */
+size_t dr_actor_act_workspace_bytes(const dr_dims* d, int B);
 int dr_actor_act(const dr_dims* d, const dr_actor* actor, int B, const float* h, const float* z,
                  dr_noise noise, int deterministic, float* a_out, float* mu_out, float* sigma_out, void* ws,
                  size_t ws_bytes, hipStream_t stream);
@@ -295,19 +296,6 @@ int dr_replay_gather(long long cap, int B, int S, int frame_elems, int A, const 
 
 /* Philox offset bump (keeps graph replays drawing fresh noise) */
 int dr_rng_advance(unsigned long long* rng, unsigned long long delta, hipStream_t stream);
-
-/* Occupancy of the conv encoder kernels (dr_encoder_features, the world-model
- * step's convolutions): extra dynamic LDS per workgroup, in bytes, applied to
- * launches made (or graph-captured) after the call.  0 (default) = densest
- * packing; padding past half the CU's LDS keeps one conv workgroup per CU so a
- * concurrent stream's latency-bound kernels find room (pipelined epochs). */
-void dr_set_conv_lds_pad(int bytes);
-
-/* First encoder conv (3(4) input channels, dr_encoder_features and the
- * world-model step): 1 (default) = the LDS-free direct-fragment MFMA kernel,
- * 0 = the LDS-tiled implicit GEMM.  Bitwise the same outputs; applies to
- * launches made (or graph-captured) after the call. */
-void dr_set_conv1_direct(int on);
 
 #ifdef __cplusplus
 }

@@ -266,44 +266,3 @@ def test_update_S_quantile_exact(n, gpu):
     L.call("dr_update_S", n, L.ptr(Rn.to(gpu)), L.ptr(Sd), None, None, 0, 0)
     torch.cuda.synchronize()
     assert float(Sd) == 2.0
-
-
-def test_imagine_fused_tails_match(gpu):
-    """The fused head-tail kernel (mlp2_launch; off by default, measured
-    slower) computes the same unroll as the split launches."""
-    from dreamer_amd import _lib as L
-    fx, d, P, eng = _engine_case("full", gpu)
-    outs = []
-    for fuse in (0, 1):
-        L.load().dr_debug_fuse_tails(fuse)
-        try:
-            eng.z0.copy_(_t(fx["z0"]).reshape(eng.z0.shape))
-            eng.h0.copy_(_t(fx["h0"]).reshape(eng.h0.shape))
-            eng.imagine(eps=_t(fx["eps"], gpu), q=_t(fx["q"], gpu))
-            torch.cuda.synchronize()
-        finally:
-            L.load().dr_debug_fuse_tails(0)
-        outs.append([cpu(x).clone() for x in (eng.latents, eng.hiddens, eng.actions, eng.rewards, eng.continues)])
-    C = int(fx["cfg_cols"])
-    assert torch.equal(outs[0][0].reshape(-1, C).argmax(-1), outs[1][0].reshape(-1, C).argmax(-1))
-    for a, b, name in zip(outs[0][1:], outs[1][1:], ("hiddens", "actions", "rewards", "continues")):
-        close(b, a, 1e-4, 1e-5, "fused tails " + name)
-
-
-@pytest.mark.parametrize("which", WHICH)
-def test_conv1_direct_bitwise(which, gpu):
-    """The LDS-free first conv (dr_set_conv1_direct(1), default) gives the
-    warm start of the LDS-tiled implicit GEMM bit for bit."""
-    from dreamer_amd import _lib as L
-    fx, d, P, eng = _engine_case(which, gpu)
-    d.buffer.gather_actions(eng.starts, eng.act_win)
-    outs = []
-    for on in (0, 1):
-        L.load().dr_set_conv1_direct(on)
-        try:
-            eng.encode_and_warm(d.buffer.frames_struct(eng.starts), noise_q=_t(fx["q_warm"], gpu))
-            torch.cuda.synchronize()
-        finally:
-            L.load().dr_set_conv1_direct(1)
-        outs.append((cpu(eng.z0).clone(), cpu(eng.h0).clone()))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
