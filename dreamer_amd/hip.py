@@ -82,11 +82,16 @@ class Rng:
         seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item()) ^ salt
         self.state = torch.tensor([seed, 0], dtype=torch.int64, device=device)
         self.counter = 0
+        self.salt = salt
 
     def reseed(self, seed):
         self.state.copy_(torch.tensor([seed, 0], dtype=torch.int64))
 
     def noise(self, row0=0):
+        if _override and self.salt:
+            q, eps = _override[-1]
+            return L.dr_noise(L.ptr(q) if q is not None else None, L.ptr(eps) if eps is not None else None,
+                              self.state.data_ptr(), row0, 0)
         self.counter = (self.counter + 1) & self.COUNTER_MASK
         if self.counter == 0:
             L.call("dr_rng_advance", self.state.data_ptr(), 1, stream())
@@ -112,6 +117,28 @@ def adhoc(device):
     if key not in _adhoc:
         _adhoc[key] = Rng(torch.device("cuda", key), salt=0x5DEECE66D)
     return _adhoc[key]
+
+
+_override = []
+
+
+class noise_override:
+    """Parity mode for the one-off API calls (SURVEY §5 "noise: explicit"):
+    inside the block every ad-hoc draw reads the given variates instead of
+    Philox -- q: Exp(1) [steps][rows*R][C] for categorical samples, eps:
+    N(0,1) [steps][rows][A] for actor samples (device tensors; the caller
+    keeps them alive).  The engine's own draws are not affected."""
+
+    def __init__(self, q=None, eps=None):
+        self.q, self.eps = q, eps
+
+    def __enter__(self):
+        _override.append((self.q, self.eps))
+        return self
+
+    def __exit__(self, *exc):
+        _override.pop()
+        return False
 
 
 def explicit_noise(q=None, eps=None, device=None):

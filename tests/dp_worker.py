@@ -11,14 +11,19 @@ for p in (os.path.dirname(HERE), HERE, os.path.join(HERE, "golden")):
         sys.path.insert(0, p)
 
 
-def make_dreamer(dev, B, S=8, H=5):
-    from formula import SMALL, replay_data
+def make_dreamer(dev, B, S=8, H=5, full=False):
+    """small widths on 32x32 frames, or (full=True) the CarRacing widths on
+    64x64 frames with S=64, H=15 (BASELINE configs[1] per rank)."""
+    from formula import FULL, SMALL, replay_data
     from dreamer_amd import Dreamer
-    cfg = dict(SMALL)
-    cfg.update(batch_size=B, sequence_length=S, horizon=H, buffer_size=64)
+    cfg = dict(FULL if full else SMALL)
+    n = 1024 if full else 64
+    if full:
+        S, H = 64, 15
+    cfg.update(batch_size=B, sequence_length=S, horizon=H, buffer_size=n)
     torch.manual_seed(0)
     d = Dreamer(cfg, dev)
-    fr, ac, rw, ct = replay_data(64, (32, 32), 3, seed=3)
+    fr, ac, rw, ct = replay_data(n, (64, 64) if full else (32, 32), 3, seed=3)
     rw = (np.sign(rw) * np.log1p(np.abs(rw))).astype(np.float32)
     d.buffer.load_arrays(fr, ac, rw, ct)
     return d
@@ -38,7 +43,7 @@ def run_epochs(d, eng, starts_list, seed=4321, pipelined=False):
     return out, ag.fa.flat.cpu(), ag.fc.flat.cpu(), ag.ft.flat.cpu(), float(ag.S_dev)
 
 
-def worker(rank, world, port, B_global, starts_list, out_path, backend, pipelined=False):
+def worker(rank, world, port, B_global, starts_list, out_path, backend, pipelined=False, full=False):
     import torch.distributed as dist
     from dreamer_amd.engine import ImaginationEngine
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -47,7 +52,7 @@ def worker(rank, world, port, B_global, starts_list, out_path, backend, pipeline
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     b = B_global // world
-    d = make_dreamer(dev, b)
+    d = make_dreamer(dev, b, full=full)
     eng = ImaginationEngine(d, B=b, world=(rank, world, dist.group.WORLD))
     mine = [st[rank * b:(rank + 1) * b] for st in starts_list]
     res = run_epochs(d, eng, mine, pipelined=pipelined)

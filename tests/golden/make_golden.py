@@ -42,7 +42,7 @@ def build_reference(cfg, weights):
     return d
 
 
-def run_case(cfg, weights, n_fill, np_seed, torch_seed):
+def run_case(cfg, weights, n_fill, np_seed, torch_seed, S0=1.0):
     d = build_reference(cfg, weights)
     sd0 = {k: v.detach().clone() for k, v in d.state_dict().items()}
     hw = tuple(cfg["observation_dims"])
@@ -76,6 +76,7 @@ def run_case(cfg, weights, n_fill, np_seed, torch_seed):
     lat, hid, acts_d, rews_d, conts_d, mus, sigs = outs
     with torch.no_grad():
         R = ag.compute_batched_R_lambda_returns(hid, lat, rews_d, conts_d, conts_d.shape[1])
+    ag.S = S0  # return-range normaliser state before the update (Agent.py:60, 78-88)
     la, lc = ag.train_step(lat, hid, rews_d, conts_d, acts_d, mus, sigs)
     S_after = float(ag.S)
     sd1 = {k: v.detach().clone() for k, v in d.state_dict().items()}
@@ -109,7 +110,7 @@ def run_case(cfg, weights, n_fill, np_seed, torch_seed):
     for a_, b_ in zip(d_o, outs):
         assert torch.equal(a_, b_), "dream mismatch"
     zz, hh, aa, rr, cc, mm, ss = d_o
-    ts = O.train_step(zz, hh, rr, cc, aa, mm, ss, P2, 1.0, ao, co)
+    ts = O.train_step(zz, hh, rr, cc, aa, mm, ss, P2, S0, ao, co)
     assert torch.equal(ts["loss_actor"], la.detach()) and torch.equal(ts["loss_critic"], lc.detach())
     assert torch.equal(ts["R"], R)
     maxd = max(float((g1 - g2).abs().max()) for g1, g2 in zip(ts["grad_actor_clipped"], rec["ga"]))

@@ -1,0 +1,260 @@
+"""The reference's public API on the HIP path (drop-in contract),
+called exactly as train_car_racer.py / Dreamer.train_dreamer call it, against
+the CPU oracle on the same inputs.  One-off calls draw their noise from the
+ad-hoc generator; ``hip.noise_override`` feeds them the oracle's explicit
+variates (parity mode).  Run on the MI355X box: pytest -m gpu.
+
+Tolerances as test_gpu_baseline.py: |d| <= 1e-5 + 1e-4 |ref| on hidden
+states, logits and heads; categorical indices exact (inputs are tie-guarded)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from baseline_case import TieGuard
+from conftest import state_layout
+from formula import FULL, formula_state_dict, replay_data
+from gpu_helpers import close, cpu
+from oracle import dreamer_oracle as O
+
+pytestmark = pytest.mark.gpu
+R, C, A, HD = 32, 32, 3, 600
+
+
+def _dreamer(dev, **over):
+    from dreamer_amd import Dreamer
+    cfg = dict(FULL)
+    cfg.update(over)
+    torch.manual_seed(0)
+    d = Dreamer(cfg, dev)
+    P = formula_state_dict(dict(state_layout("full")))
+    d.load_state_dict({k: v.to(dev) for k, v in P.items()})
+    return d, P
+
+
+def _inputs(B, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    h = torch.randn(B, 1, HD, generator=g)
+    lg = torch.randn(B, 1, R, C, generator=g) * 2
+    z = torch.nn.functional.one_hot(lg.argmax(-1), C).float()
+    a = torch.rand(B, 1, A, generator=g) * 2 - 1
+    obs = torch.randint(0, 256, (B, 1, 3, 64, 64), generator=g).float() / 255.0 - 0.5
+    q = torch.empty(1, B * R, C).exponential_(generator=g)
+    eps = torch.randn(1, B, A, generator=g)
+    return h, z, a, obs, q, eps
+
+
+def _idx(z):
+    return cpu(z).reshape(-1, C).argmax(-1)
+
+
+def test_warm_start_generator_api(gpu):
+    """Dreamer.warm_start_generator(obs 0..255, act, S) (Dreamer.py:244-262)."""
+    from dreamer_amd import hip
+    B, S = 4, 16
+    d, P = _dreamer(gpu, batch_size=B, sequence_length=S)
+    fr, ac, _, _ = replay_data(64, (64, 64), A, seed=5)
+    idx = np.arange(S)[None, :] + np.array([0, 7, 21, 40])[:, None]
+    obs = torch.tensor(fr[idx], dtype=torch.float32)
+    act = torch.tensor(ac[idx])
+    q = torch.empty(S // 2, B * R, C).exponential_(generator=torch.Generator().manual_seed(9))
+    with TieGuard():
+        z_ref, h_ref = O.warm_start(obs, act, S, P, q, R, C)
+    with hip.noise_override(q=q.to(gpu)):
+        z, h = d.warm_start_generator(obs.to(gpu), act.to(gpu), S)
+    assert torch.equal(_idx(z), _idx(z_ref))
+    close(h, h_ref, 1e-4, 1e-5, "warm_start_generator h")
+    close(z, z_ref, 0, 1.2e-7, "warm_start_generator z (straight-through value)")
+
+
+@pytest.mark.parametrize("soft", [False, True])
+def test_observe_step_and_encode_api(soft, gpu):
+    """WorldModel.observe_step (WorldModel.py:79-82) and Encoder.encode
+    (VAE.py:77-99); soft=True feeds a non-one-hot latent (dense GRU groups)."""
+    from dreamer_amd import hip
+    B = 3
+    d, P = _dreamer(gpu)
+    h, z, a, obs, q, _ = _inputs(B)
+    if soft:
+        z = torch.softmax(torch.randn(B, 1, R, C, generator=torch.Generator().manual_seed(4)), -1)
+    with TieGuard():
+        z_ref, h_ref, lg_ref = O.observe_step(z, h, a, obs, P, q[0], R, C)
+        ze_ref, le_ref = O.encode(h, obs, P, q[0], R, C)
+    wm = d.world_model
+    with torch.no_grad(), hip.noise_override(q=q.to(gpu)):
+        z2, h2, lg = wm.observe_step(z.to(gpu), h.to(gpu), a.to(gpu), obs.to(gpu))
+        ze, le = wm.encoder.encode(h.to(gpu), obs.to(gpu))
+    close(h2, h_ref, 1e-4, 1e-5, "observe_step h")
+    close(lg, lg_ref, 1e-4, 1e-5, "observe_step logits")
+    assert torch.equal(_idx(z2), _idx(z_ref))
+    close(le, le_ref, 1e-4, 1e-5, "encode logits")
+    assert torch.equal(_idx(ze), _idx(ze_ref))
+
+
+@pytest.mark.parametrize("soft", [False, True])
+def test_imagine_step_api(soft, gpu):
+    """WorldModel.imagine_step (WorldModel.py:72-77) and SequenceModel."""
+    from dreamer_amd import hip
+    B = 3
+    d, P = _dreamer(gpu)
+    h, z, a, _, q, _ = _inputs(B, seed=6)
+    if soft:
+        z = torch.softmax(torch.randn(B, 1, R, C, generator=torch.Generator().manual_seed(5)), -1)
+    with TieGuard():
+        h_ref, z_ref, r_ref, c_ref = O.imagine_step(h, z, a, P, q[0], R, C)
+    wm = d.world_model
+    with torch.no_grad(), hip.noise_override(q=q.to(gpu)):
+        h2, z2, r, c = wm.imagine_step(h.to(gpu), z.to(gpu), a.to(gpu))
+        hs = wm.sequence_model(z.to(gpu), h.to(gpu), a.to(gpu))
+    close(hs, O.gru(z, h, a, P), 1e-4, 1e-5, "SequenceModel")
+    close(h2, h_ref, 1e-4, 1e-5, "imagine_step h")
+    assert torch.equal(_idx(z2), _idx(z_ref))
+    close(r, r_ref, 1e-4, 1e-5, "imagine_step reward")
+    close(c, c_ref, 1e-4, 1e-6, "imagine_step continue")
+
+
+@pytest.mark.parametrize("widths", [(200, 200), (64, 256)])
+def test_actor_act_batch1(widths, gpu):
+    """Actor.act at B = 1 (rollout_policy / evaluate_agent / Run) with the
+    CarRacing widths and with actor_h2 > actor_h1 (workspace)."""
+    from dreamer_amd import hip
+    d, _ = _dreamer(gpu, hidden_layer_actor_1_size=widths[0], hidden_layer_actor_2_size=widths[1])
+    P = {k: v.detach().cpu() for k, v in d.state_dict().items()}
+    h, z, _, _, _, eps = _inputs(1, seed=8)
+    mu_ref, sg_ref = O.actor_forward(h, z, P)
+    with torch.no_grad():
+        a, mu, sg = d.agent.actor.act(h.to(gpu), z.to(gpu), deterministic=True)
+        close(mu, mu_ref, 1e-4, 1e-5, "act mu")
+        close(sg, sg_ref, 1e-4, 1e-6, "act sigma")
+        close(a, torch.tanh(mu_ref), 1e-4, 1e-6, "act deterministic")
+        with hip.noise_override(eps=eps.to(gpu)):
+            a2, _, _ = d.agent.actor.act(h.to(gpu), z.to(gpu), deterministic=False)
+    close(a2, torch.tanh(mu_ref + eps.view(1, 1, A) * sg_ref), 1e-4, 1e-6, "act sample")
+
+
+def test_dream_episodes_from_soft_latent(gpu):
+    """Dreamer.dream_episodes (Dreamer.py:143-175) from a non-one-hot z0."""
+    B, H = 4, 5
+    d, P = _dreamer(gpu, batch_size=B, horizon=H)
+    g = torch.Generator().manual_seed(12)
+    h0 = torch.randn(B, 1, HD, generator=g)
+    z0 = torch.softmax(torch.randn(B, 1, R, C, generator=g), -1)
+    eps = torch.randn(H, B, 1, A, generator=g)
+    q = torch.empty(H, B * R, C).exponential_(generator=g)
+    with TieGuard():
+        ref = O.dream(z0, h0, P, eps, q, H, R, C)
+    out = d._imagine_raw(z0.to(gpu), h0.to(gpu), eps=eps.to(gpu), q=q.to(gpu))[0]
+    close(out[1], ref[1], 1e-4, 1e-5, "dream hiddens (soft z0)")
+    assert torch.equal(_idx(out[0][:, 1:]), _idx(ref[0][:, 1:]))
+    close(out[3], ref[3], 1e-4, 1e-5, "dream rewards (soft z0)")
+
+
+def test_train_world_model_api(gpu):
+    """Dreamer.train_world_model (Dreamer.py:228-242): the losses it returns
+    equal the oracle's WorldModel.training_step loss on the same windows."""
+    from dreamer_amd import hip
+    B, S, H = 4, 16, 6
+    d, P = _dreamer(gpu, batch_size=B, sequence_length=S, horizon=H, buffer_size=64)
+    fr, ac, rw, ct = replay_data(64, (64, 64), A, seed=7)
+    rws = O.symlog(torch.tensor(rw)).numpy()
+    d.buffer.load_arrays(fr, ac, rws, ct)
+    np.random.seed(3)
+    starts = d.buffer.sample_start_indices(B)
+    q = torch.empty(H, B * R, C).exponential_(generator=torch.Generator().manual_seed(13))
+    idx = starts[:, None] + np.arange(S)[None, :]
+    with TieGuard():
+        ref = O.wm_losses(torch.tensor(fr[idx], dtype=torch.float32), torch.tensor(ac[idx]),
+                          torch.tensor(rws[idx]).unsqueeze(-1), torch.tensor(ct[idx]).unsqueeze(-1), P, q, R, C, H)
+    np.random.seed(3)
+    with hip.noise_override(q=q.to(gpu)):
+        losses = d.train_world_model()
+    assert len(losses) == 1 and losses[0].dim() == 0
+    assert abs(float(losses[0]) - float(ref["total"])) <= 1e-4 * abs(float(ref["total"])), \
+        (float(losses[0]), float(ref["total"]))
+
+
+def test_train_agent_api_matches_engine(gpu):
+    """Dreamer.train_Agent() (Dreamer.py:264-287) with AC_epochs = 1 and 2 is
+    the engine's epoch(s) on the same np.random window draws, bit for bit."""
+    from dreamer_amd.engine import ImaginationEngine
+    B, S, H = 8, 16, 5
+    res = []
+    for mode in ("api", "engine"):
+        d, _ = _dreamer(gpu, batch_size=B, sequence_length=S, horizon=H, buffer_size=128, AC_epochs=2)
+        fr, ac, rw, ct = replay_data(128, (64, 64), A, seed=2)
+        d.buffer.load_arrays(fr, ac, O.symlog(torch.tensor(rw)).numpy(), ct)
+        d._engine = ImaginationEngine(d)
+        d._engine.rng.reseed(77)
+        np.random.seed(21)
+        if mode == "api":
+            la, lc = d.train_Agent()
+            la, lc = float(la), float(lc)
+        else:
+            ls = [d._engine.run(d.buffer.sample_start_indices(B)) for _ in range(2)]
+            ls = [(float(a), float(c)) for a, c in ls]
+            la, lc = np.mean([x[0] for x in ls], dtype=np.float32), np.mean([x[1] for x in ls], dtype=np.float32)
+        torch.cuda.synchronize()
+        res.append((la, lc, cpu(d.agent.fa.flat), cpu(d.agent.fc.flat)))
+    (a1, c1, fa1, fc1), (a2, c2, fa2, fc2) = res
+    assert abs(a1 - a2) <= 1e-6 * max(1.0, abs(a2)) and abs(c1 - c2) <= 1e-6 * abs(c2)
+    assert torch.equal(fa1, fa2) and torch.equal(fc1, fc2)
+
+
+class _Space:
+    def __init__(self, rng):
+        self.rng = rng
+
+    def sample(self):
+        return self.rng.uniform(-1, 1, size=3).astype(np.float32)
+
+
+class FakeCarRacing:
+    """gymnasium-shaped env (reset / step / action_space.sample) with 64x64x3
+    u8 frames, ending an episode every `length` steps."""
+
+    def __init__(self, length=9, seed=0):
+        self.rng = np.random.default_rng(seed)
+        self.action_space = _Space(self.rng)
+        self.length = length
+        self.t = 0
+
+    def _obs(self):
+        return self.rng.integers(0, 256, size=(64, 64, 3), dtype=np.uint8)
+
+    def reset(self, seed=None):
+        self.t = 0
+        return self._obs(), {}
+
+    def step(self, action):
+        a = np.asarray(action, dtype=np.float32)
+        assert a.shape == (3,) and np.all(np.isfinite(a)) and np.all(np.abs(a) <= 1.0)
+        self.t += 1
+        return self._obs(), float(np.tanh(a.sum())), self.t >= self.length, False, {}
+
+    def render(self):
+        pass
+
+
+def test_train_dreamer_with_fake_env(gpu, tmp_path, monkeypatch):
+    """Dreamer.train_dreamer(env, eval_env) end to end (train_car_racer.py:38):
+    random kick-start, world-model and agent training iterations, evaluation,
+    checkpoint + training-log files; then Run() and a reference-format reload."""
+    monkeypatch.chdir(tmp_path)
+    d, _ = _dreamer(gpu, batch_size=4, sequence_length=16, horizon=5, buffer_size=256, random_iterations=2,
+                    training_iterations=2, AC_epochs=2)
+    env, eval_env = FakeCarRacing(seed=1), FakeCarRacing(seed=2)
+    wm, al, cl, ev = d.train_dreamer(env, eval_env)
+    assert len(wm) == 2 + 2 and len(al) == 2 and len(cl) == 2 and len(ev) == 1 + 1 + 1
+    for x in [v for row in wm for v in row] + al + cl + ev:
+        assert np.isfinite(x)
+    assert d.buffer.size == (2 + 2) * 16
+    assert os.path.exists("models/agent_latest.pth") and os.path.exists("models/agent_checkpoint_0.pth")
+    with np.load("models/training_logs.npz", allow_pickle=False) as f:
+        assert set(f.files) == {"world_model_loss", "actor_loss", "critic_loss", "rewards"}
+    total = d.Run(FakeCarRacing(seed=3), env_seed=0, render=True)
+    assert np.isfinite(total)
+    sd = torch.load("models/agent_latest.pth", weights_only=True)
+    d2, _ = _dreamer(gpu, batch_size=4, sequence_length=16, horizon=5)
+    d2.load_pretrained_dreamer("models/agent_latest.pth")
+    assert all(torch.equal(v.cpu(), sd[k].cpu()) for k, v in d2.state_dict().items())

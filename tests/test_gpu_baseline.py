@@ -1,0 +1,199 @@
+"""Parity of the HIP train_Agent epoch at BASELINE.json's shapes (run on the
+MI355X box: pytest -m gpu).
+
+* configs[0] shape (CarRacing widths, B=16 S=50 H=15, S0 = 5): against the
+  reference's own outputs (tests/golden/baseline_b16.npz) and the oracle;
+* configs[1] (B=64 S=64 H=15) and the north-star batch (B=256 S=64 H=15):
+  against the CPU oracle run on the box's host cores on the same inputs and
+  noise (default reference init under torch.manual_seed(0), SURVEY §8d
+  synthetic replay, S0 = 3 so the max(S, 1) normaliser is > 1).
+
+The noise is tie-guarded (tests/baseline_case.py), so every categorical index
+of the 31-step warm start and the 15-step dream must match exactly.
+
+Tolerances (fp32; the GPU differs from the CPU only in summation order and in
+the ~2-ulp hardware exp2/rcp of the LayerNorm-SiLU GEMM prologues):
+  warm-start h0, imagined hiddens / actions / mus / sigmas: |d| <= 1e-5 + 1e-4 |ref|
+  rewards / continues / lambda returns:                       |d| <= 1e-5 + 1e-4 |ref|
+  losses: relative 1e-4; S: 1e-6 relative
+  clipped gradients: |d| <= 1e-4 |ref| + 1e-5 max|ref| per tensor
+  post-AdamW parameters: against the oracle's AdamW applied to the GPU's own
+    clipped gradients (pins the fused optimiser): |d| <= 1e-7 + 1e-6 |p|;
+    against the oracle's post-step parameters: |d| <= 1e-6 + 1e-6 |p| on every
+    element whose oracle gradient is not within 1e-3 of AdamW's eps scale
+    (there Adam's first step is sign(g) * lr, so a tiny gradient of either sign
+    moves the weight by a full lr; those elements are counted and bounded).
+"""
+import numpy as np
+import pytest
+import torch
+
+from baseline_case import oracle_epoch, regen_fixture
+from conftest import load_fixture, state_layout
+from gpu_helpers import close, cpu
+from oracle import dreamer_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CAR = dict(
+    hidden_state_dims=600, latent_state_dims=[32, 32], action_dims=3, observation_dims=[64, 64],
+    encoder_filter_num_1=32, encoder_filter_num_2=64, encoder_hidden_layer_nodes=200,
+    decoder_filter_num_1=32, decoder_filter_num_2=64, decoder_hidden_layer_nodes=200,
+    dyn_pred_hidden_num_nodes_1=200, dyn_pred_hidden_num_nodes_2=200,
+    rew_pred_hidden_num_nodes_1=200, rew_pred_hidden_num_nodes_2=200,
+    cont_pred_hidden_num_nodes_1=200, cont_pred_hidden_num_nodes_2=200,
+    hidden_layer_actor_1_size=200, hidden_layer_actor_2_size=200,
+    hidden_layer_critic_1_size=200, hidden_layer_critic_2_size=200, device="cuda",
+    horizon=15, batch_size=64, nu=0.0003, lambda_=0.95, gamma=0.99, buffer_size=4096,
+    sequence_length=64, seed=42, training_iterations=1, random_iterations=1,
+    actor_lr=0.00008, actor_betas=[0.9, 0.999], actor_eps=0.00001, critic_lr=0.0001,
+    critic_betas=[0.9, 0.999], critic_eps=0.00001, AC_epochs=1, world_model_lr=0.0001,
+    world_model_betas=[0.9, 0.999], world_model_eps=0.00001, WM_epochs=1,
+    beta_prediction=1.0, beta_dynamics=0.5, beta_representation=0.1, critic_reward_buckets=255,
+)
+
+
+def _t(a):
+    return torch.from_numpy(np.asarray(a).copy())
+
+
+def _err(a, b):
+    a, b = cpu(a), cpu(b)
+    return float((a - b).abs().max()), float(b.abs().max())
+
+
+def run_gpu_epoch(d, frames, acts, rews, conts, size, next_idx, starts, q_warm, eps, q, S0):
+    """One HIP train_Agent epoch with explicit noise through the engine phases."""
+    from dreamer_amd.engine import ImaginationEngine
+    dev = d.device
+    buf = d.buffer
+    buf.load_arrays(frames, acts, rews, conts)
+    buf.size, buf.next_idx = size, next_idx
+    d.agent.S = S0
+    eng = ImaginationEngine(d, use_graph=False)
+    eng.starts.copy_(torch.as_tensor(starts, dtype=torch.int64))
+    buf.gather_actions(eng.starts, eng.act_win)
+    eng.encode_and_warm(buf.frames_struct(eng.starts), noise_q=q_warm.to(dev))
+    eng.imagine(eps=eps.to(dev), q=q.to(dev))
+    eng.returns()
+    eng.losses_and_grads()
+    torch.cuda.synchronize()
+    ag = d.agent
+    pre = dict(la=float(ag.loss_buffer[0]), lc=float(ag.loss_buffer[1]), S=float(ag.S_dev),
+               R=cpu(eng.R).clone())
+    eng.optimise()
+    torch.cuda.synchronize()
+    return eng, pre
+
+
+def compare(d, eng, pre, ref, C, label, S0):
+    """Every observable of the epoch against the oracle (see module doc)."""
+    ag = d.agent
+    za, zb = cpu(eng.z0).reshape(-1, C).argmax(-1), ref["z0"].reshape(-1, C).argmax(-1)
+    assert torch.equal(za, zb), f"{label}: warm-start index flips {int((za != zb).sum())}"
+    close(eng.h0, ref["h0"].reshape(eng.h0.shape), 1e-4, 1e-5, label + " warm-start h0")
+    lat, hid, act, rew, cont, mu, sg = ref["dream"]
+    la_, lb_ = cpu(eng.latents).reshape(-1, C).argmax(-1), lat.reshape(-1, C).argmax(-1)
+    assert torch.equal(la_, lb_), f"{label}: imagined index flips {int((la_ != lb_).sum())}"
+    for got, want, name in ((eng.hiddens, hid, "hiddens"), (eng.actions, act, "actions"), (eng.mus, mu, "mus"),
+                            (eng.sigmas, sg, "sigmas"), (eng.rewards, rew, "rewards"),
+                            (eng.continues, cont, "continues")):
+        close(got, want.reshape(got.shape), 1e-4, 1e-5, f"{label} {name}")
+    ts = ref["ts"]
+    close(pre["R"], ts["R"].reshape(pre["R"].shape), 1e-4, 1e-5, label + " lambda returns")
+    assert abs(pre["la"] - float(ts["loss_actor"])) <= 1e-4 * max(1e-3, abs(float(ts["loss_actor"]))), \
+        (label, pre["la"], float(ts["loss_actor"]))
+    assert abs(pre["lc"] - float(ts["loss_critic"])) <= 1e-4 * abs(float(ts["loss_critic"])), \
+        (label, pre["lc"], float(ts["loss_critic"]))
+    assert abs(pre["S"] - float(ts["S"])) <= 1e-6 * abs(float(ts["S"])), (label, pre["S"], float(ts["S"]))
+    assert float(ts["S"]) > 1.0 and S0 > 1.0
+    sd = d.state_dict()
+    n_tiny = 0
+    for f, keys, grads, lr in ((ag.fa, O.ACTOR_KEYS, ts["grad_actor_clipped"], 8e-5),
+                               (ag.fc, O.CRITIC_KEYS, ts["grad_critic_clipped"], 1e-4)):
+        for k, g_ref in zip(keys, grads):
+            name = k.split(".", 1)[1]
+            o = f.offsets[name]
+            g_gpu = cpu(f.grad[o:o + g_ref.numel()]).view(g_ref.shape)
+            scale = float(g_ref.abs().max()) + 1e-30
+            close(g_gpu, g_ref, 1e-4, 1e-5 * scale, f"{label} clipped grad {k}")
+            p0 = ref["P0"]["agent." + k]
+            # the fused AdamW on the GPU's own gradients
+            pn, _, _ = O.adamw_step(p0, g_gpu, torch.zeros_like(p0), torch.zeros_like(p0), 1, lr)
+            got = cpu(sd["agent." + k])
+            close(got, pn, 1e-6, 1e-7, f"{label} AdamW(step 1) {k}")
+            # against the oracle's own post-step parameters, away from Adam's sign ambiguity
+            want = ref["post"]["agent." + k]
+            live = g_ref.abs() > 1e-3 * 1e-5
+            n_tiny += int((~live).sum())
+            err = (got - want).abs()
+            bad = live & (err > 1e-6 + 1e-6 * want.abs())
+            assert not bool(bad.any()), (label, k, int(bad.sum()), float(err[live].max()))
+    for k in O.CRITIC_KEYS:
+        tk = "agent.target_" + k
+        close(sd[tk], ref["post"][tk], 1e-6, 2e-8, f"{label} target {k}")
+    return n_tiny
+
+
+def test_baseline_b16_vs_reference(gpu):
+    """configs[0] shape against the reference's own recorded outputs."""
+    from gpu_helpers import build
+    fx = load_fixture("baseline_b16")
+    B, S, H, R, C = (int(fx[k]) for k in ("cfg_B", "cfg_S", "cfg_H", "cfg_rows", "cfg_cols"))
+    P, frames, q_warm, eps, q = regen_fixture(fx, dict(state_layout("full")))
+    cap = int(fx["buf_capacity"])
+    idx = (fx["starts"][:, None] + np.arange(S)[None, :]) % cap
+    obs = torch.tensor(frames[idx], dtype=torch.float32)
+    act = torch.tensor(fx["buf_actions"][idx])
+    ref = oracle_epoch(P, obs, act, S, H, R, C, q_warm, eps, q, float(fx["S0"]))
+    ref["P0"] = P
+    # the oracle IS the reference here (pinned bit-exactly by test_oracle_golden)
+    assert torch.equal(ref["h0"].reshape(-1), _t(fx["h0"]).reshape(-1))
+    assert float(ref["ts"]["loss_actor"]) == float(fx["loss_actor"])
+    from formula import FULL
+    from dreamer_amd import Dreamer
+    cfg = dict(FULL)
+    cfg.update(batch_size=B, sequence_length=S, horizon=H, buffer_size=cap)
+    d = Dreamer(cfg, gpu)
+    d.load_state_dict({k: v.to(gpu) for k, v in P.items()})
+    eng, pre = run_gpu_epoch(d, frames, fx["buf_actions"], fx["buf_rewards"], fx["buf_continues"],
+                             int(fx["buf_size"]), int(fx["buf_next_idx"]), fx["starts"], q_warm, eps, q,
+                             float(fx["S0"]))
+    n_tiny = compare(d, eng, pre, ref, C, "B16", float(fx["S0"]))
+    print(f"B16: guarded {ref['guarded']}/{ref['draws']} draws, {n_tiny} near-zero-gradient params")
+    # the reference's own numbers, directly
+    assert np.array_equal(cpu(eng.z0).reshape(-1, C).argmax(-1).numpy(), fx["z0_idx"].astype(np.int64))
+    assert abs(pre["la"] - float(fx["loss_actor"])) <= 1e-4 * abs(float(fx["loss_actor"]))
+    assert abs(pre["S"] - float(fx["S_after"])) <= 1e-6 * float(fx["S_after"])
+
+
+@pytest.mark.parametrize("B", [64, 256])
+def test_epoch_vs_oracle_at_baseline_shape(B, gpu):
+    """configs[1] (B=64) and the north-star batch (B=256), S=64 H=15, full
+    widths, reference default init, synthetic replay."""
+    import bench
+    from dreamer_amd import Dreamer
+    S, H, R, C, A = 64, 15, 32, 32, 3
+    cfg = dict(CAR)
+    cfg.update(batch_size=B, sequence_length=S, horizon=H)
+    torch.manual_seed(0)
+    d = Dreamer(cfg, gpu)
+    P = {k: v.detach().cpu().clone() for k, v in d.state_dict().items()}
+    n = 4096
+    frames, acts, rews, conts = bench.synthetic_replay(n, (64, 64), A, seed=0)
+    rng = np.random.RandomState(100 + B)
+    starts = rng.randint(0, n - S + 1, size=B)
+    g = torch.Generator().manual_seed(200 + B)
+    q_warm = torch.empty(S // 2, B * R, C).exponential_(generator=g)
+    eps = torch.randn(H, B, 1, A, generator=g)
+    q = torch.empty(H, B * R, C).exponential_(generator=g)
+    idx = starts[:, None] + np.arange(S)[None, :]
+    obs = torch.tensor(frames[idx], dtype=torch.float32)
+    act = torch.tensor(acts[idx])
+    S0 = 3.0
+    torch.set_num_threads(16)
+    ref = oracle_epoch(P, obs, act, S, H, R, C, q_warm, eps, q, S0)
+    ref["P0"] = P
+    eng, pre = run_gpu_epoch(d, frames, acts, rews, conts, n, 0, starts, q_warm, eps, q, S0)
+    n_tiny = compare(d, eng, pre, ref, C, f"B{B}", S0)
+    print(f"B{B}: guarded {ref['guarded']}/{ref['draws']} draws, {n_tiny} near-zero-gradient params")

@@ -115,3 +115,44 @@ def test_unimix_scalar_semantics():
     ref = 0.99 * p + 0.01 * (1.0 / 32)
     f32 = (p.numpy() * np.float32(0.99)) + np.float32(0.01 * (1.0 / 32))
     assert np.array_equal(ref.numpy(), f32)
+
+
+# ---------------------------------------------------------------------------
+# BASELINE configs[0] shape (CarRacing widths, B=16 S=50 H=15, S0 = 5):
+# tests/golden/baseline_b16.npz, inputs regenerated (tests/baseline_case.py)
+# ---------------------------------------------------------------------------
+def test_baseline_b16_oracle_matches_reference():
+    from baseline_case import regen_fixture
+    from conftest import state_layout
+    fx = load_fixture("baseline_b16")
+    B, S, H, R, C = (int(fx[k]) for k in ("cfg_B", "cfg_S", "cfg_H", "cfg_rows", "cfg_cols"))
+    P, frames, q_warm, eps, q = regen_fixture(fx, dict(state_layout("full")))
+    np.random.seed(int(fx["np_seed"]))
+    st = O.replay_starts(int(fx["buf_size"]), int(fx["buf_capacity"]), int(fx["buf_next_idx"]), S, B)
+    assert np.array_equal(st, fx["starts"])
+    idx = (st[:, None] + np.arange(S)[None, :]) % int(fx["buf_capacity"])
+    obs = torch.tensor(frames[idx], dtype=torch.float32)
+    act = torch.tensor(fx["buf_actions"][idx])
+    z0, h0 = O.warm_start(obs, act, S, P, q_warm, R, C)
+    assert np.array_equal(z0.reshape(-1, C).argmax(-1).numpy(), fx["z0_idx"])
+    assert torch.equal(h0, _t(fx["h0"]))
+    ap = [P["agent." + k].clone().requires_grad_(True) for k in O.ACTOR_KEYS]
+    cp = [P["agent." + k].clone().requires_grad_(True) for k in O.CRITIC_KEYS]
+    P2 = dict(P)
+    P2.update({"agent." + k: t for k, t in zip(O.ACTOR_KEYS, ap)})
+    P2.update({"agent." + k: t for k, t in zip(O.CRITIC_KEYS, cp)})
+    z, h, a, r, c, mu, sg = O.dream(z0, h0, P2, eps, q, H, R, C)
+    assert np.array_equal(z.reshape(-1, C).argmax(-1).numpy(), fx["latents_idx"])
+    for got, key in ((h, "hiddens"), (a, "actions"), (r, "rewards"), (c, "continues"), (mu, "mus"), (sg, "sigmas")):
+        assert torch.equal(got.detach(), _t(fx[key])), key
+    ts = O.train_step(z, h, r, c, a, mu, sg, P2, float(fx["S0"]), ap, cp)
+    assert torch.equal(ts["loss_actor"], _t(fx["loss_actor"])) and torch.equal(ts["loss_critic"], _t(fx["loss_critic"]))
+    assert torch.equal(ts["R"], _t(fx["R"]))
+    assert float(ts["S"]) == float(fx["S_after"]) and float(fx["S_after"]) > 1.0  # normaliser max(S, 1) > 1
+    st_ = int(fx["sample_stride"])
+    for keys, grads in ((O.ACTOR_KEYS, ts["grad_actor_clipped"]), (O.CRITIC_KEYS, ts["grad_critic_clipped"])):
+        for k, g in zip(keys, grads):
+            flat = g.reshape(-1)
+            ref = _t(fx["gradc_agent." + k])
+            got = flat if flat.numel() < int(fx["small_tensor"]) else flat[::st_]
+            assert torch.equal(got, ref), k
