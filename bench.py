@@ -1,8 +1,12 @@
 """Benchmark: imagined latent-steps/sec (B x H) of Dreamer.train_Agent epochs
 on MI355X (BASELINE.json metric), 64x64x3 CarRacing-shaped synthetic replay.
 
-  python bench.py [--gpus N --steps K --warmup W --batch B --seq S --horizon H]
+  python bench.py [--gpus N --steps K --warmup W --batch B --seq S --horizon H --precision fp32|bf16]
 
+Headline: K calls of Dreamer.train_Agent() with AC_epochs=1 at the north-star
+batch (B=256 per GPU, S=64, H=15), window draws inside the timed region.
+Secondaries: AC_epochs=2 (pipelined epochs), BASELINE configs[1] (B=64), the
+world-model step and the full iteration.
 Multi-GPU: launched by torch.distributed.run, one process per GPU; weak
 scaling (B rows per GPU), RCCL all-gather of lambda returns + one all-reduce
 of the flat [actor|critic|loss] gradient buffer per epoch.  Rank 0 prints ONE
@@ -23,10 +27,8 @@ sys.path.insert(0, REPO)
 
 METRIC = "imagined latent-steps/sec (B×H) at 64×64 CarRacing, 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 = f32 vector peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 HBM_PEAK_GBS = 8000.0
-# HBM-side bytes of the encoder group per epoch, measured by tools/pmc_traffic.sh
-# (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, gfx950 correction)
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_traffic.json")
 # SURVEY.md §8d figure of record: necessary dense FLOPs per imagined step at
 # 64x64, S=64, H=15 (warm start 131.07 + dream 8.88 + update 11.17 MFLOP)
 PATH_MFLOP_PER_STEP = {(64, 15, 64): 151.12, (50, 15, 64): 122.36, (64, 20, 128): 383.00}
@@ -128,87 +130,170 @@ def bench_wm(d, B, steps, warmup):
     return el / steps, ev0.elapsed_time(ev1) / 1e3 / steps, float(wm.last_losses[0])
 
 
-def cpu_baseline(cfg, B, S, H, budget_s=15.0, threads=None):
-    """Reference-faithful CPU epoch (oracle restatement of Dreamer.train_Agent:
-    warm start with the un-detached graph, dream, train_step with backward into
-    everything, AdamW, EMA) timed on the host cores."""
-    from oracle import dreamer_oracle as O
-    from dreamer_amd import Dreamer
-    threads = threads or min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    c = dict(cfg)
-    c.update(device="cpu", batch_size=B, sequence_length=S, horizon=H)
-    torch.manual_seed(0)
-    d = Dreamer(c, torch.device("cpu"))
-    P = {k: v.detach().clone().requires_grad_(v.dtype == torch.float32 and "buckets" not in k)
-         for k, v in d.state_dict().items()}
-    R, C = c["latent_state_dims"]
-    A = c["action_dims"]
-    frames, acts, rews, conts = synthetic_replay(max(4096, 8 * S), c["observation_dims"], A, seed=0)
-    rng = np.random.default_rng(1)
-    actor = [P["agent." + k] for k in O.ACTOR_KEYS]
-    critic = [P["agent." + k] for k in O.CRITIC_KEYS]
-    m = {id(p): (torch.zeros_like(p), torch.zeros_like(p)) for p in actor + critic}
-    S_val = 1.0
+def cpu_info():
+    """CPU model and core counts of this host (for the cpu_baseline record)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        import psutil
+        phys = psutil.cpu_count(logical=False)
+    except Exception:
+        phys = None
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    return model, phys, affinity
 
-    def epoch(step):
-        nonlocal S_val
-        st = rng.integers(0, len(frames) - S, size=B)
-        idx = st[:, None] + np.arange(S)[None, :]
-        obs = torch.tensor(frames[idx], dtype=torch.float32)
-        act = torch.tensor(acts[idx])
-        qw = torch.empty(S // 2, B * R, C).exponential_()
-        z0, h0 = O.warm_start(obs, act, S, P, qw, R, C)
-        eps = torch.randn(H, B, 1, A)
-        q = torch.empty(H, B * R, C).exponential_()
-        z, h, a, r, cc, mu, sg = O.dream(z0, h0, P, eps, q, H, R, C)
-        la, lc, Rl, S_val = O.ac_losses(z, h, r, cc, a, mu, sg, P, S_val)
-        for p in actor + critic:
+
+class CpuEpoch:
+    """Reference-faithful CPU train_Agent epoch (the oracle restatement of
+    Dreamer.train_Agent, Dreamer.py:264-287): warm start with the un-detached
+    graph, dream, train_step with the backward into everything (warm start
+    included), two clip_grad_norm_ + AdamW steps, EMA target.  The same op
+    sequence as the reference; tools/cpu_fidelity.py times it against the
+    imported reference in the build container (profiles/r02_cpu_fidelity.json)."""
+
+    def __init__(self, cfg, B, S, H, seed=0):
+        from oracle import dreamer_oracle as O
+        from dreamer_amd import Dreamer
+        self.O = O
+        c = dict(cfg)
+        c.update(device="cpu", batch_size=B, sequence_length=S, horizon=H)
+        torch.manual_seed(seed)
+        d = Dreamer(c, torch.device("cpu"))
+        self.P = {k: v.detach().clone().requires_grad_(v.dtype == torch.float32 and "buckets" not in k)
+                  for k, v in d.state_dict().items()}
+        self.R, self.C = c["latent_state_dims"]
+        self.A = c["action_dims"]
+        self.B, self.S, self.H = B, S, H
+        self.frames, self.acts, _, _ = synthetic_replay(max(4096, 8 * S), c["observation_dims"], self.A, seed=0)
+        self.rng = np.random.default_rng(1)
+        self.actor = [self.P["agent." + k] for k in O.ACTOR_KEYS]
+        self.critic = [self.P["agent." + k] for k in O.CRITIC_KEYS]
+        self.m = {id(p): (torch.zeros_like(p), torch.zeros_like(p)) for p in self.actor + self.critic}
+        self.S_val = 1.0
+        self.step = 0
+
+    def set_inputs(self, obs, act, q_warm, eps, q):
+        """Feed explicit inputs/noise for the next epoch (fidelity timing)."""
+        self._fixed = (obs, act, q_warm, eps, q)
+
+    def epoch(self):
+        O, B, S, H, R, C, A = self.O, self.B, self.S, self.H, self.R, self.C, self.A
+        self.step += 1
+        fixed = getattr(self, "_fixed", None)
+        if fixed is None:
+            st = self.rng.integers(0, len(self.frames) - S, size=B)
+            idx = st[:, None] + np.arange(S)[None, :]
+            obs = torch.tensor(self.frames[idx], dtype=torch.float32)
+            act = torch.tensor(self.acts[idx])
+            qw = torch.empty(S // 2, B * R, C).exponential_()
+            eps = torch.randn(H, B, 1, A)
+            q = torch.empty(H, B * R, C).exponential_()
+        else:
+            obs, act, qw, eps, q = fixed
+        z0, h0 = O.warm_start(obs, act, S, self.P, qw, R, C)
+        z, h, a, r, cc, mu, sg = O.dream(z0, h0, self.P, eps, q, H, R, C)
+        la, lc, Rl, self.S_val = O.ac_losses(z, h, r, cc, a, mu, sg, self.P, self.S_val)
+        for p in self.actor + self.critic:
             p.grad = None
         lc.backward()
         la.backward()  # traverses the dream AND the warm-start graph, as the reference does
-        for ps, lr in ((critic, 1e-4), (actor, 8e-5)):
+        for ps, lr in ((self.critic, 1e-4), (self.actor, 8e-5)):
             gs, _ = O.clip_grad_norm([p.grad for p in ps])
             with torch.no_grad():
                 for p, g in zip(ps, gs):
-                    mm, vv = m[id(p)]
-                    pn, mn, vn = O.adamw_step(p, g, mm, vv, step, lr)
+                    mm, vv = self.m[id(p)]
+                    pn, mn, vn = O.adamw_step(p, g, mm, vv, self.step, lr)
                     p.copy_(pn); mm.copy_(mn); vv.copy_(vn)
         with torch.no_grad():
             for k in O.CRITIC_KEYS:
-                t = P["agent.target_" + k]
-                t.mul_(0.98).add_(0.02 * P["agent." + k])
+                t = self.P["agent.target_" + k]
+                t.mul_(0.98).add_(0.02 * self.P["agent." + k])
+        return float(la), float(lc)
 
-    epoch(1)  # warm-up (not timed)
-    n, t0 = 0, time.perf_counter()
-    while True:
-        epoch(2 + n)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or n >= 50:
-            break
-    return dict(value=B * H * n / el, unit="imagined latent-steps/s", cores=threads, kind="port",
-                sample=f"{n} reference-faithful train_Agent epochs (oracle CPU restatement, fp32, warm-start "
-                       f"backward included) at B={B} S={S} H={H} {c['observation_dims'][0]}x{c['observation_dims'][1]}x3, "
-                       f"{el:.1f} s on {threads} threads")
+
+def cpu_baseline(cfg, B, S, H, budget_s=30.0, threads=None):
+    """The reference-faithful CPU epoch timed on the host cores: one warm-up
+    epoch, then three timed samples (each >= one epoch, stopping once a sample
+    passes budget_s / 3); min and median imagined steps/s are reported."""
+    model, phys, affinity = cpu_info()
+    threads = threads or min(16, affinity or 1)
+    torch.set_num_threads(threads)
+    ce = CpuEpoch(cfg, B, S, H)
+    ce.epoch()  # warm-up (not timed)
+    rates = []
+    for _ in range(3):
+        n, t0 = 0, time.perf_counter()
+        while True:
+            ce.epoch()
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s / 3 or n >= 20:
+                break
+        rates.append(B * H * n / el)
+    rates.sort()
+    return dict(value=round(rates[1], 1), unit="imagined latent-steps/s", cores=threads, kind="port",
+                min_of_3=round(rates[0], 1), median_of_3=round(rates[1], 1), max_of_3=round(rates[2], 1),
+                cpu_model=model, physical_cores_host=phys, cpus_available=affinity,
+                fidelity="profiles/r02_cpu_fidelity.json (oracle reference-faithful epoch vs the imported "
+                         "reference, same inputs, build container)",
+                sample=f"3 samples of >= 1 reference-faithful train_Agent epoch (oracle CPU restatement, fp32, "
+                       f"warm-start backward included) at B={B} S={S} H={H} "
+                       f"{cfg['observation_dims'][0]}x{cfg['observation_dims'][1]}x3 on {threads} threads; "
+                       f"value = median")
+
+
+def traffic_for(B, res, precision):
+    """HBM-side bytes of the encoder group per epoch measured by
+    tools/pmc_traffic.sh for this workload (profiles/r02_traffic_*.json)."""
+    path = os.path.join(REPO, "profiles", f"r02_traffic_B{B}_r{res}_{precision}.json")
+    if not os.path.exists(path):
+        return None, None
+    t = json.load(open(path))
+    return t.get("encoder_bytes_per_epoch"), os.path.relpath(path, REPO)
+
+
+def make_dreamer(cfg, dev, B, S, H, res, ac_epochs, world, rank, group, precision):
+    from dreamer_amd import Dreamer
+    from dreamer_amd.engine import ImaginationEngine
+    c = dict(cfg)
+    c.update(batch_size=B, sequence_length=S, horizon=H, observation_dims=[res, res], AC_epochs=ac_epochs,
+             buffer_size=max(4096, 8 * S), precision=precision)
+    torch.manual_seed(0)
+    d = Dreamer(c, dev)
+    fr, ac, rw, ct = synthetic_replay(c["buffer_size"], c["observation_dims"], c["action_dims"], seed=0)
+    d.buffer.load_arrays(fr, ac, rw, ct)
+    d.buffer._mirror()
+    if world > 1:
+        d.world = (rank, world, group)
+        d.world_model.set_data_parallel(rank, world, group)
+    d._engine = ImaginationEngine(d, B=B, world=(rank, world, group) if world > 1 else None)
+    return c, d
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=20, help="timed train_Agent() calls")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64, help="imagination rows per GPU (configs[1]: 64)")
+    ap.add_argument("--batch", type=int, default=256, help="imagination rows per GPU (north star: 256)")
     ap.add_argument("--seq", type=int, default=64)
     ap.add_argument("--horizon", type=int, default=15)
     ap.add_argument("--res", type=int, default=64,
-                    help="frame side (64: CarRacing configs[1]; 128: configs[3]'s frames with the reference's "
-                         "4-conv encoder -- the 'deeper VAE' is not in the reference)")
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
+                    help="frame side (64: CarRacing; 128: configs[3]'s frames with the reference's 4-conv encoder)")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
+                    help="fp32: parity mode (bit-exact indices vs the reference); bf16: perf mode")
+    ap.add_argument("--cpu-budget", type=float, default=24.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--phases", action="store_true", help="print per-phase ms to stderr")
-    ap.add_argument("--sequential", action="store_true",
-                    help="report the epochs run one after another (no warm-start / update overlap)")
+    ap.add_argument("--no-secondary", action="store_true", help="headline only")
     ap.add_argument("--wm-steps", type=int, default=10, help="world-model training steps timed (0: skip)")
     args = ap.parse_args()
 
@@ -227,140 +312,124 @@ def main():
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
         group = dist.group.WORLD
 
-    from dreamer_amd import Dreamer
-    from dreamer_amd.engine import ImaginationEngine
-    B, S, H = args.batch, args.seq, args.horizon
-    cfg = dict(CAR_RACER)
-    cfg.update(batch_size=B, sequence_length=S, horizon=H, observation_dims=[args.res, args.res])
-    torch.manual_seed(0)
-    d = Dreamer(cfg, dev)
-    n_rep = max(4096, 8 * S)
-    fr, ac, rw, ct = synthetic_replay(n_rep, cfg["observation_dims"], cfg["action_dims"], seed=0)
-    d.buffer.load_arrays(fr, ac, rw, ct)
-    d.buffer._mirror()
-    eng = ImaginationEngine(d, B=B, world=(rank, world, group) if world > 1 else None)
-    d._engine = eng
-    if world > 1:
-        d.world_model.set_data_parallel(rank, world, group)
-    np.random.seed(1000 + rank)
-
     def barrier():
         if world > 1:
             import torch.distributed as dist
             dist.barrier()
         torch.cuda.synchronize()
 
-    def timed_epochs(pipelined):
-        """K consecutive train_Agent epochs after W warm-up ones.  Pipelined:
-        the warm start of epoch e+1 overlaps epoch e's actor-critic chain
-        (ImaginationEngine.run_many; the pipeline fills and drains inside the
-        timed region).  Sequential: one epoch after the other (engine.run)."""
-        if pipelined:
-            eng.run_many([d.buffer.sample_start_indices(B) for _ in range(args.warmup)])
-        else:
-            for _ in range(args.warmup):
-                eng.run(d.buffer.sample_start_indices(B))
-        starts = [d.buffer.sample_start_indices(B) for _ in range(args.steps)]
-        barrier()
-        t0 = time.perf_counter()
-        phase_tot = {}
-        if pipelined:
-            eng.run_many(starts)
-        else:
-            for st in starts:
-                eng.run(st, timing=True)
-                if args.phases:
-                    torch.cuda.current_stream().synchronize()
-                    for k, v in eng.phase_ms().items():
-                        phase_tot[k] = phase_tot.get(k, 0.0) + v
-        barrier()
-        el = time.perf_counter() - t0
+    def max_over_ranks(x):
         if world > 1:
             import torch.distributed as dist
-            t = torch.tensor([el], device=dev)
+            t = torch.tensor([x], device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t)
-        return el, phase_tot
+            return float(t)
+        return x
 
-    el_seq, phase_tot = timed_epochs(False)
-    el = el_seq if args.sequential else timed_epochs(True)[0]
-    la, lc = float(d.agent.loss_buffer[0]), float(d.agent.loss_buffer[1])
-    # the world-model step all-reduces under DP: every rank runs it (max over ranks)
+    def time_train_agent(d, steps, warmup):
+        """K calls of Dreamer.train_Agent() (Dreamer.py:264-287) after W
+        untimed ones.  Each call draws its window starts (np.random, the
+        reference's Buffer sampling) inside the timed region."""
+        for _ in range(warmup):
+            d.train_Agent()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            la, lc = d.train_Agent()
+        barrier()
+        return max_over_ranks(time.perf_counter() - t0), (float(la), float(lc))
+
+    B, S, H, res = args.batch, args.seq, args.horizon, args.res
+    np.random.seed(1000 + rank)
+    cfg, d = make_dreamer(CAR_RACER, dev, B, S, H, res, 1, world, rank, group, args.precision)
+    el, (la, lc) = time_train_agent(d, args.steps, args.warmup)
+    value = world * B * H * args.steps / el
+    eng = d._engine
+    frames = B * (S // 2)
+    enc_flops = encoder_flops_per_frame(cfg) * frames
+    secondary = {}
+    if not args.no_secondary:
+        # AC_epochs = 2 (car_racer_config.yaml): the warm start of epoch e+1 overlaps epoch e's update
+        d.AC_epochs = 2
+        el2, _ = time_train_agent(d, max(2, args.steps // 2), 2)
+        d.AC_epochs = 1
+        secondary["ac_epochs2_pipelined"] = {
+            "value": round(world * B * H * 2 * max(2, args.steps // 2) / el2, 1), "unit": "imagined latent-steps/s",
+            "ms_per_epoch": round(el2 / (2 * max(2, args.steps // 2)) * 1e3, 4),
+            "note": "Dreamer.train_Agent() with AC_epochs=2 (the reference config's value): epochs pipelined on two "
+                    "streams, results equal the sequential epochs bit for bit "
+                    "(tests/test_gpu_parity.py::test_pipelined_epochs_match_sequential)"}
+        if (B, S, H, res) != (64, 64, 15, 64):
+            _, d64 = make_dreamer(CAR_RACER, dev, 64, 64, 15, 64, 1, world, rank, group, args.precision)
+            el64, _ = time_train_agent(d64, args.steps, args.warmup)
+            secondary["configs1_B64"] = {
+                "value": round(world * 64 * 15 * args.steps / el64, 1), "unit": "imagined latent-steps/s",
+                "ms_per_epoch": round(el64 / args.steps * 1e3, 4),
+                "note": "BASELINE configs[1] shape (B=64/GPU S=64 H=15), Dreamer.train_Agent() AC_epochs=1"}
+            del d64
     wm = None
     if args.wm_steps > 0:
         wm_s, wm_gpu_s, wm_loss = bench_wm(d, B, args.wm_steps, 2)
-        if world > 1:
-            import torch.distributed as dist
-            t = torch.tensor([wm_s, wm_gpu_s], device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            wm_s, wm_gpu_s = (float(x) for x in t.cpu())
-        wm = (wm_s, wm_gpu_s, wm_loss)
+        wm = (max_over_ranks(wm_s), max_over_ranks(wm_gpu_s), wm_loss)
     if rank != 0:
         barrier()
         if world > 1:
             import torch.distributed as dist
             dist.destroy_process_group()
         return
-    value = world * B * H * args.steps / el
-    frames = B * (S // 2)
-    enc_flops = encoder_flops_per_frame(cfg) * frames
-    # the dominant kernel group (conv encoder + feature projection, all time
-    # chunks) timed live with HIP events on the engine's stream, back to back
-    # without the overlapping scan, after the timed region
+    # the dominant kernel group (conv encoder + feature projection) timed live
+    # with HIP events on the engine's stream, back to back, after the timed region
     enc_s = eng.time_encoder(reps=5) / 1e3
+    peak = BF16_MFMA_PEAK_TFLOPS if args.precision == "bf16" else FP32_MFMA_PEAK_TFLOPS
     achieved = enc_flops / enc_s / 1e12
-    if args.phases:
-        print(json.dumps({k: round(v / args.steps, 4) for k, v in phase_tot.items()}), file=sys.stderr)
-    traffic, traffic_src = None, None
-    if os.path.exists(TRAFFIC_FILE):
-        t = json.load(open(TRAFFIC_FILE))
-        traffic, traffic_src = t.get("encoder_bytes_per_epoch"), os.path.relpath(TRAFFIC_FILE, REPO)
+    traffic, traffic_src = traffic_for(B, res, args.precision)
+    dtype = "bf16" if args.precision == "bf16" else "f32"
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "imagined latent-steps/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"Dreamer.train_Agent epoch (replay sample + warm start S/2 + H-step imagination + "
-                               f"actor-critic update), B={B}/GPU S={S} H={H} {args.res}x{args.res}x3"
-                               + (" (BASELINE configs[1])" if (args.res, B, S, H) == (64, 64, 64, 15) else ""),
-                   "global_batch": B * world, "seq_len": S, "horizon": H, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": f"encoder conv stack + feature projection ({len(eng.chunks)} time chunks x 5 launches)",
-                     "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                     "traffic_unit": "bytes per epoch (HBM side)", "traffic_source": traffic_src,
-                     "algorithmic_flops_per_launch": enc_flops, "encoder_ms": round(enc_s * 1e3, 4)},
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dtype,
+        "data": "synthetic (SURVEY §8d replay: u8 uniform frames, U(-1,1) actions, symlog N(0,1) rewards); "
+                "reference default init under torch.manual_seed(0)",
+        "config": {"workload": f"Dreamer.train_Agent() with AC_epochs=1 (replay sample + warm start S/2 + "
+                               f"H-step imagination + actor-critic update), B={B}/GPU S={S} H={H} {res}x{res}x3, "
+                               f"precision={args.precision}"
+                               + (" (north-star batch per GPU)" if (B, S, H, res) == (256, 64, 15, 64) else ""),
+                   "global_batch": B * world, "seq_len": S, "horizon": H, "parallelism": f"dp{world}",
+                   "precision": args.precision},
+        "roofline": {"bound": "mfma", "kernel": "encoder conv stack + feature projection (one train_Agent epoch's "
+                                                 f"{frames} warm-start frames)",
+                     "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4), "traffic": traffic,
+                     "traffic_unit": "HBM-side bytes per launch group (per epoch)", "traffic_source": traffic_src,
+                     "algorithmic_flops_per_launch": enc_flops,
+                     "algorithmic_unit": "55.77 MFLOP per 64x64 frame (SURVEY §8d) x B*S/2 frames",
+                     "encoder_ms": round(enc_s * 1e3, 4)},
         "losses": {"actor": la, "critic": lc},
-        "epochs": {"mode": "sequential" if args.sequential else "pipelined",
-                   "pipelined_note": "warm start (encoder + posterior scan, world-model parameters only) of epoch "
-                                     "e+1 runs on a second stream beside epoch e's imagination / actor-critic "
-                                     "update; results equal the sequential epochs bit for bit "
-                                     "(tests/test_gpu_parity.py::test_pipelined_epochs_match_sequential)",
-                   "sequential_value": round(world * B * H * args.steps / el_seq, 1),
-                   "sequential_ms_per_step": round(el_seq / args.steps * 1e3, 4)},
     }
-    mf = PATH_MFLOP_PER_STEP.get((S, H, args.res))
+    mf = PATH_MFLOP_PER_STEP.get((S, H, res))
     if mf is not None:
         tf = value * mf * 1e6 / 1e12
-        out["path_roofline"] = {"bound": "mfma", "achieved": round(tf, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                                "unit": "TFLOP/s", "frac": round(tf / FP32_MFMA_PEAK_TFLOPS, 4),
+        out["path_roofline"] = {"bound": "mfma", "achieved": round(tf, 2), "peak": peak,
+                                "unit": "TFLOP/s", "frac": round(tf / peak, 4),
                                 "mflop_per_imagined_step": mf,
                                 "note": "whole train_Agent epoch, SURVEY §8d necessary FLOPs x imagined steps/s"}
     if wm is not None:
         wm_s, wm_gpu_s, wm_loss = wm
         fl = wm_step_flops(cfg, B, H)
         ac_s = el / args.steps
-        out["secondary"] = {
-            "wm_step": {"value": round(world * B / wm_s, 1), "unit": "sequences/s", "ms_per_step": round(wm_s * 1e3, 3),
-                        "gpu_ms_per_step": round(wm_gpu_s * 1e3, 3), "B_per_gpu": B, "T": H, "loss": wm_loss,
-                        "mfma_tflops": round(fl / wm_s / 1e12, 2),
-                        "mfma_frac": round(fl / wm_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
-                        "algorithmic_gflop": round(fl / 1e9, 2),
-                        "note": "WorldModel.training_step (posterior scan, decoder, losses, full backward, clip, "
-                                "AdamW) from the device replay ring; under DP the mask / loss sums and the flat "
-                                "gradient are all-reduced (RCCL)"},
-            "full_iteration": {"value": round(world * B * H / (wm_s + ac_s), 1), "unit": "imagined latent-steps/s",
-                               "ms_per_iteration": round((wm_s + ac_s) * 1e3, 3),
-                               "note": "1 WM step + 1 train_Agent epoch per iteration (WM_epochs = AC_epochs = 1)"},
-        }
+        secondary["wm_step"] = {
+            "value": round(world * B / wm_s, 1), "unit": "sequences/s", "ms_per_step": round(wm_s * 1e3, 3),
+            "gpu_ms_per_step": round(wm_gpu_s * 1e3, 3), "B_per_gpu": B, "T": H, "loss": wm_loss,
+            "mfma_tflops": round(fl / wm_s / 1e12, 2), "mfma_frac_f32": round(fl / wm_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+            "algorithmic_gflop": round(fl / 1e9, 2),
+            "note": "WorldModel.training_step (posterior scan, decoder, losses, full backward, clip, AdamW) from the "
+                    "device replay ring; under DP the mask / loss sums and the flat gradient are all-reduced (RCCL)"}
+        secondary["full_iteration"] = {
+            "value": round(world * B * H / (wm_s + ac_s), 1), "unit": "imagined latent-steps/s",
+            "ms_per_iteration": round((wm_s + ac_s) * 1e3, 3),
+            "note": "1 WM step + 1 train_Agent epoch per iteration (WM_epochs = AC_epochs = 1)"}
+    if secondary:
+        out["secondary"] = secondary
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, B, S, H, budget_s=args.cpu_budget)
     print(json.dumps(out), flush=True)

@@ -93,6 +93,10 @@ class Dreamer(nn.Module):
         self.WM_epochs = c["WM_epochs"]
         self.AC_epochs = c["AC_epochs"]
         self.seed = c["seed"]
+        # extra config key: "fp32" parity mode (default) or "bf16" perf mode
+        self.precision = c.get("precision", "fp32")
+        if self.precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {self.precision!r}")
         self.device = device
         self.agent_obs = None
         self.agent_hidden = None

@@ -86,6 +86,7 @@ class Rng:
 
     def reseed(self, seed):
         self.state.copy_(torch.tensor([seed, 0], dtype=torch.int64))
+        self.counter = 0
 
     def noise(self, row0=0):
         if _override and self.salt:

@@ -65,7 +65,7 @@ def worker(rank, world, port, B_global, starts_list, out_path, backend, pipeline
 def run_wm_steps(d, starts_list, seed=98765):
     """world-model training steps from the device ring; returns losses and the flat parameters"""
     from dreamer_amd import hip
-    hip.rng(d.device).reseed(seed)
+    hip.adhoc(d.device).reseed(seed)  # the world-model step draws from the ad-hoc generator
     out = []
     for st in starts_list:
         loss = d.world_model.train_step_ring(d.buffer, st)

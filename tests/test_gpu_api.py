@@ -22,12 +22,15 @@ pytestmark = pytest.mark.gpu
 R, C, A, HD = 32, 32, 3, 600
 
 
-def _dreamer(dev, **over):
+def _dreamer(dev, formula=True, **over):
+    """CarRacing widths; formula weights (or the default init for other widths)."""
     from dreamer_amd import Dreamer
     cfg = dict(FULL)
     cfg.update(over)
     torch.manual_seed(0)
     d = Dreamer(cfg, dev)
+    if not formula:
+        return d, None
     P = formula_state_dict(dict(state_layout("full")))
     d.load_state_dict({k: v.to(dev) for k, v in P.items()})
     return d, P
@@ -119,7 +122,8 @@ def test_actor_act_batch1(widths, gpu):
     """Actor.act at B = 1 (rollout_policy / evaluate_agent / Run) with the
     CarRacing widths and with actor_h2 > actor_h1 (workspace)."""
     from dreamer_amd import hip
-    d, _ = _dreamer(gpu, hidden_layer_actor_1_size=widths[0], hidden_layer_actor_2_size=widths[1])
+    d, _ = _dreamer(gpu, formula=widths == (200, 200), hidden_layer_actor_1_size=widths[0],
+                    hidden_layer_actor_2_size=widths[1])
     P = {k: v.detach().cpu() for k, v in d.state_dict().items()}
     h, z, _, _, _, eps = _inputs(1, seed=8)
     mu_ref, sg_ref = O.actor_forward(h, z, P)
@@ -191,8 +195,10 @@ def test_train_agent_api_matches_engine(gpu):
             la, lc = d.train_Agent()
             la, lc = float(la), float(lc)
         else:
-            ls = [d._engine.run(d.buffer.sample_start_indices(B)) for _ in range(2)]
-            ls = [(float(a), float(c)) for a, c in ls]
+            ls = []
+            for _ in range(2):
+                a, c = d._engine.run(d.buffer.sample_start_indices(B))  # views of the loss slots
+                ls.append((float(a), float(c)))
             la, lc = np.mean([x[0] for x in ls], dtype=np.float32), np.mean([x[1] for x in ls], dtype=np.float32)
         torch.cuda.synchronize()
         res.append((la, lc, cpu(d.agent.fa.flat), cpu(d.agent.fc.flat)))

