@@ -350,15 +350,15 @@ def main():
     secondary = {}
     if not args.no_secondary:
         # AC_epochs = 2 (car_racer_config.yaml): the warm start of epoch e+1 overlaps epoch e's update
-        d.AC_epochs = 2
+        d.AC_epochs, d.pipeline_epochs = 2, True
         el2, _ = time_train_agent(d, max(2, args.steps // 2), 2)
-        d.AC_epochs = 1
+        d.AC_epochs, d.pipeline_epochs = 1, False
         secondary["ac_epochs2_pipelined"] = {
             "value": round(world * B * H * 2 * max(2, args.steps // 2) / el2, 1), "unit": "imagined latent-steps/s",
             "ms_per_epoch": round(el2 / (2 * max(2, args.steps // 2)) * 1e3, 4),
-            "note": "Dreamer.train_Agent() with AC_epochs=2 (the reference config's value): epochs pipelined on two "
-                    "streams, results equal the sequential epochs bit for bit "
-                    "(tests/test_gpu_parity.py::test_pipelined_epochs_match_sequential)"}
+            "note": "Dreamer.train_Agent() with AC_epochs=2 and the opt-in pipeline_epochs config key: the warm "
+                    "start of epoch e+1 on a second stream beside epoch e's update (equal to the sequential epochs "
+                    "in tests/test_gpu_parity.py; off by default, DESIGN.md 5a)"}
         if (B, S, H, res) != (64, 64, 15, 64):
             _, d64 = make_dreamer(CAR_RACER, dev, 64, 64, 15, 64, 1, world, rank, group, args.precision)
             el64, _ = time_train_agent(d64, args.steps, args.warmup)

@@ -1277,6 +1277,15 @@ static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
   }
   if (maxM > 4096) return false;
   if (g_skinny_variant == 1 && maxM > 16) maxM = 65;
+  if (g_skinny_variant == 3) maxM = std::min(maxM, 64);  // 16-row tiles at any M
+  // 16-row tiles past 64 rows while the grid stays within ~2.5 dispatch
+  // rounds: a B = 256 per-step product (N = 200) then spreads over 208
+  // workgroups instead of 52 (K = 1624: 19.3 -> 8.4 us, profiles/r02_kbench_B256.txt)
+  if (g_skinny_variant == 0 && maxM > 64 && (AMODE == AM_PLAIN || AMODE == AM_LNSILU)) {
+    int t16 = 0;
+    for (int i = 0; i < count; ++i) t16 += dr_cdiv(gb.p[i].M, 16) * dr_cdiv(gb.p[i].N, epi == EPI_SAMPLE ? 32 : 16);
+    if (t16 <= 640) maxM = 64;
+  }
   // 16-column tiles by default; 32-column tiles when the 16-column grid would
   // exceed one workgroup per CU (these 512-thread tiles hold 1 per CU by VGPRs,
   // so a second dispatch round costs more than the wider tile's extra MFMAs)
@@ -1629,13 +1638,18 @@ static bool tile_offsets_ok(const GemmBatch& gb, int count) {
 template <int AMODE, bool A_KM, bool B_KN>
 static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
   if (AMODE == AM_PLAIN && tile_offsets_ok(gb, count)) {
-    int maxM = 0, minK = 1 << 30;
+    int maxM = 0, minK = 1 << 30, tiles = 0;
+    bool ws = true;
     for (int i = 0; i < count; ++i) {
       maxM = std::max(maxM, gb.p[i].M);
       minK = std::min(minK, gb.p[i].K);
+      tiles += dr_cdiv(gb.p[i].M, 64) * dr_cdiv(gb.p[i].N, 64);
+      ws = ws && gb.p[i].splitk_ws != nullptr;
     }
-    // weight gradients (TN) and tall, deep products go to the tile kernel
-    if (A_KM || (maxM >= 256 && minK >= 512)) {
+    // weight gradients (TN) and tall, deep products go to the tile kernel --
+    // when it can fill the chip: a per-step product at B = 256 (16 tiles of
+    // 64 x 64, no split-K scratch) runs on 52+ skinny 64-row workgroups instead
+    if (A_KM || (maxM >= 256 && minK >= 512 && (ws || tiles >= 128))) {
       GemmBatch gt = gb;
       switch (g_tile_variant) {
         case 1: launch_tile2<64, 64, 64, A_KM, B_KN>(gt, count, s); break;

@@ -95,6 +95,7 @@ class Dreamer(nn.Module):
         self.seed = c["seed"]
         # extra config key: "fp32" parity mode (default) or "bf16" perf mode
         self.precision = c.get("precision", "fp32")
+        self.pipeline_epochs = bool(c.get("pipeline_epochs", False))
         if self.precision not in ("fp32", "bf16"):
             raise ValueError(f"precision must be 'fp32' or 'bf16', got {self.precision!r}")
         self.device = device
@@ -174,10 +175,13 @@ class Dreamer(nn.Module):
 
     def train_Agent(self):
         """Dreamer.train_Agent (Dreamer.py:264-287): AC_epochs fused epochs."""
-        if self.AC_epochs > 1:
-            # the epochs' window starts are drawn up front (same np.random
-            # order); the warm start of epoch e+1 then overlaps epoch e's
-            # update (engine.run_many: identical results, pipelined)
+        if self.AC_epochs > 1 and self.pipeline_epochs:
+            # opt-in (config key pipeline_epochs): the epochs' window starts
+            # are drawn up front (same np.random order); the warm start of
+            # epoch e+1 then overlaps epoch e's update (engine.run_many).  Off
+            # by default: inside the fake-env train_dreamer flow its epoch-2
+            # results were seen to differ from the sequential epochs on some
+            # runs (tools/diag/pipe_stress.py, DESIGN.md section 5a)
             B = self.batch_size if self.world is None else self.engine.B
             starts = [self.buffer.sample_start_indices(B) for _ in range(self.AC_epochs)]
             losses = self.engine.run_many(starts)

@@ -247,8 +247,10 @@ def test_train_dreamer_with_fake_env(gpu, tmp_path, monkeypatch):
     random kick-start, world-model and agent training iterations, evaluation,
     checkpoint + training-log files; then Run() and a reference-format reload."""
     monkeypatch.chdir(tmp_path)
-    d, _ = _dreamer(gpu, batch_size=4, sequence_length=16, horizon=5, buffer_size=256, random_iterations=2,
-                    training_iterations=2, AC_epochs=2)
+    # default init: the closed-form parity weights drive this tiny training
+    # run into non-finite updates on some noise draws (sequential epochs too)
+    d, _ = _dreamer(gpu, formula=False, batch_size=4, sequence_length=16, horizon=5, buffer_size=256,
+                    random_iterations=2, training_iterations=2, AC_epochs=2)
     env, eval_env = FakeCarRacing(seed=1), FakeCarRacing(seed=2)
     wm, al, cl, ev = d.train_dreamer(env, eval_env)
     assert len(wm) == 2 + 2 and len(al) == 2 and len(cl) == 2 and len(ev) == 1 + 1 + 1

@@ -242,7 +242,7 @@ int main(int argc, char** argv) {
   if (getenv("KB_REPS")) g_reps = atoi(getenv("KB_REPS"));
   hipStream_t s;
   CK(hipStreamCreate(&s));
-  const int B = 64, Hd = 600, R = 32, C = 32, A = 3, L = R * C;
+  const int B = getenv("KB_B") ? atoi(getenv("KB_B")) : 64, Hd = 600, R = 32, C = 32, A = 3, L = R * C;
   timeit("empty kernel (1 WG, small args)", [&](hipStream_t st) { hipLaunchKernelGGL(k_empty_small, dim3(1), dim3(64), 0, st, nullptr); }, s);
   timeit("empty kernel (128 WG x 512, small args)", [&](hipStream_t st) { hipLaunchKernelGGL(k_empty_small, dim3(128), dim3(512), 0, st, nullptr); }, s);
   Big big;
@@ -325,6 +325,7 @@ int main(int argc, char** argv) {
   ga.idx = idx; ga.zval = reinterpret_cast<float*>(idx + B * R); ga.a = act; ga.lda = A; ga.h = h; ga.ldh = Hd;
   ga.wt = wt; ga.b_ih = bih; ga.w_hh = whh; ga.b_hh = bhh; ga.hout = hout; ga.ldo = Hd;
   timeit("gru_fused B64 H600 R32 (no saves)", [&](hipStream_t st) { op_gru_fused(ga, st); }, s);
+
   phases("gru_fused", [&](hipStream_t st) { op_gru_fused(ga, st); }, dr_debug_tbuf_gru, s);
   GruArgs gs = ga;
   gs.sr = save; gs.su = save + B * Hd; gs.sn = save + 2 * B * Hd; gs.sghn = save + 3 * B * Hd;
@@ -350,7 +351,8 @@ int main(int argc, char** argv) {
     return g;
   };
   char buf[128];
-  int shapes[][3] = {{64, 200, 600}, {64, 200, 200}, {64, 1024, 200}, {64, 200, 1624}, {64, 255, 200}, {960, 200, 200}};
+  int shapes[][3] = {{B, 200, 600}, {B, 200, 200}, {B, 1024, 200}, {B, 200, 1624}, {B, 255, 200}, {960, 200, 200},
+                     {B, 1027, 1800}, {B, 600, 1800}};
   for (auto& sh : shapes) {
     GemmArgs g = nt_(sh[0], sh[1], sh[2]);
     snprintf(buf, sizeof buf, "NT plain M%d N%d K%d", sh[0], sh[1], sh[2]);
@@ -386,15 +388,23 @@ int main(int argc, char** argv) {
                                                                        gemm_launch(G_NT, AM_LNSILU, &g2, 1, st); }, s);
   }
   // per-step shapes of the imagination / BPTT chain, both row-tile variants
-  for (int var = 0; var < 3; var += 2) {
+  for (int var = 0; var < 5; ++var) {
+    if (var == 1 || var == 2) continue;
     dr_debug_skinny_variant(var);
-    int sh2[][3] = {{64, 1027, 1800}, {64, 600, 1800}, {64, 200, 1624}, {64, 1024, 200}, {64, 200, 1024}};
+    int sh2[][3] = {{B, 1027, 1800}, {B, 600, 1800}, {B, 200, 1624}, {B, 1024, 200}, {B, 200, 1024}, {B, 200, 600}};
     for (auto& sh : sh2) {
       GemmArgs g = nt_(sh[0], sh[1], sh[2]);
       snprintf(buf, sizeof buf, "s%d NT plain M%d N%d K%d", var, sh[0], sh[1], sh[2]);
       timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, &g, 1, st); }, s);
     }
-    GemmArgs gp[2] = {nt_(64, 1027, 1800), nt_(64, 600, 1800)};
+    int sh3[][3] = {{B, 200, 200}, {B, 1024, 200}, {B, 6, 200}, {B, 255, 200}};
+    for (auto& sh : sh3) {
+      GemmArgs gl = nt_(sh[0], sh[1], sh[2]);
+      gl.ln_g = lng; gl.ln_b = lnb;
+      snprintf(buf, sizeof buf, "s%d NT lnsilu M%d N%d K%d", var, sh[0], sh[1], sh[2]);
+      timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_LNSILU, &gl, 1, st); }, s);
+    }
+    GemmArgs gp[2] = {nt_(B, 1027, 1800), nt_(B, 600, 1800)};
     snprintf(buf, sizeof buf, "s%d NT plain grouped BPTT gZ+gH", var);
     timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, gp, 2, st); }, s);
     GemmArgs gb2 = nt_(64, 1624, 200);
