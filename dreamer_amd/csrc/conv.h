@@ -17,6 +17,20 @@ int op_conv_nhwc_ex(int n, int cin, int ih, int iw, int cout, const float* in, c
 int op_frames_nhwc4(int n, int nb, int h, int w, const dr_frames* src, float* out, hipStream_t s);
 int op_conv_repack_pad(int cout, int cin, int cin_pad, const float* w, float* wr, hipStream_t s);
 
+// ---- conv_bf16.hip (bf16 perf mode; activations bf16, accumulation f32) ----
+// weights: Conv2d [co][ci][4][4] f32 -> bf16 [co][tap][cin_pad]; matrix slice -> bf16 [rows][cols]
+int op_conv_repack_bf16(int cout, int cin, int cin_pad, const float* w, void* wr, hipStream_t s);
+int op_to_bf16_2d(int rows, int cols, const float* x, long long ld, void* y, hipStream_t s);
+// first conv from the frames (u8 ring or f32): out bf16 NHWC [n][h/2][w/2][cout]; wr cin_pad = 4
+int op_conv1_bf16(int n, int nb, int h, int w, int cout, const dr_frames* src, const void* wr, const float* bias,
+                  void* out, hipStream_t s);
+// k4 s2 p1 conv + bias + SiLU, bf16 NHWC in -> bf16 NHWC (or NCHW) out
+int op_conv_bf16(int n, int cin, int ih, int iw, int cout, const void* in, const void* wr, const float* bias,
+                 void* out, int out_nchw, hipStream_t s);
+// Y (f32) = X W^T + bias with X [M][K], W [N][K] bf16
+int op_gemm_nt_bf16(int M, int N, int K, const void* X, int ldx, const void* W, const float* bias, float* Y, int ldy,
+                    hipStream_t s);
+
 // ---- wmconv.hip -------------------------------------------------------------
 // Upsampling k4 s2 p1 (ConvTranspose2d, or the data gradient of a Conv2d):
 //   out[f][Y][X][co] = sum_{ci, (y,ky): Y = 2y-1+ky, (x,kx): X = 2x-1+kx} in[f][y][x][ci] * wt[ci][co][ky][kx]

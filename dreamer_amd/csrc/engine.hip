@@ -10,22 +10,28 @@
 struct EncWs {
   float *x0, *a1, *a2, *a3, *a4, *wr1, *wr2, *wr3, *wr4, *sk;
   long long sk_n;
+  void* wproj;  // bf16 mode: latent_mapper.0 feature columns as bf16 [enc_hidden][F]
 };
 
+// bf16 mode stores activations / repacked weights as bf16 (2 bytes): the same
+// carve with half-size regions (a4 holds the NCHW flatten, x0 is unused)
 static void enc_carve(Carve& c, const dr_dims* d, int n, EncWs& w) {
+  const bool bf = d->precision == DR_PREC_BF16;
   const int c1 = d->enc_f1, c2 = d->enc_f2, c3 = 2 * d->enc_f2, c4 = 4 * d->enc_f2;
   const long long p0 = (long long)d->img_h * d->img_w, p1 = p0 / 4, p2 = p1 / 4, p3 = p2 / 4, p4 = p3 / 4;
-  w.sk_n = splitk_floats(n, d->enc_hidden);
-  w.sk = c.f(w.sk_n);
-  w.x0 = c.f((long long)n * p0 * 4);
-  w.a1 = c.f((long long)n * p1 * c1);
-  w.a2 = c.f((long long)n * p2 * c2);
-  w.a3 = c.f((long long)n * p3 * c3);
-  w.a4 = c.f((long long)n * p4 * c4);
-  w.wr1 = c.f((long long)c1 * 4 * 16);
-  w.wr2 = c.f((long long)c2 * c1 * 16);
-  w.wr3 = c.f((long long)c3 * c2 * 16);
-  w.wr4 = c.f((long long)c4 * c3 * 16);
+  auto e = [&](long long elems) { return bf ? (float*)c.raw(elems * 2) : c.f(elems); };
+  w.sk_n = bf ? 0 : splitk_floats(n, d->enc_hidden);
+  w.sk = bf ? nullptr : c.f(w.sk_n);
+  w.x0 = bf ? nullptr : c.f((long long)n * p0 * 4);
+  w.a1 = e((long long)n * p1 * c1);
+  w.a2 = e((long long)n * p2 * c2);
+  w.a3 = e((long long)n * p3 * c3);
+  w.a4 = e((long long)n * p4 * c4);
+  w.wr1 = e((long long)c1 * 4 * 16);
+  w.wr2 = e((long long)c2 * c1 * 16);
+  w.wr3 = e((long long)c3 * c2 * 16);
+  w.wr4 = e((long long)c4 * c3 * 16);
+  w.wproj = bf ? c.raw((size_t)d->enc_hidden * c4 * p4 * 2) : nullptr;
 }
 
 extern "C" size_t dr_encoder_workspace_bytes(const dr_dims* d, int n_frames) {
@@ -35,16 +41,37 @@ extern "C" size_t dr_encoder_workspace_bytes(const dr_dims* d, int n_frames) {
   return c.off;
 }
 
+// bf16 perf mode (conv_bf16.hip): conv1 straight from the frames, conv2..4 as
+// bf16 NHWC implicit GEMMs, the feature projection as a bf16 NT GEMM
+static int encoder_bf16(const dr_dims* d, const dr_world_model* wm, const dr_frames* src, int B, int n, float* feat,
+                        const EncWs& w, hipStream_t s) {
+  const int c1 = d->enc_f1, c2 = d->enc_f2, c3 = 2 * d->enc_f2, c4 = 4 * d->enc_f2;
+  const int h0 = d->img_h, w0 = d->img_w;
+  const int F = c4 * (h0 / 16) * (w0 / 16);
+  DR_TRY(op_conv_repack_bf16(c1, 3, 4, wm->conv[0].w, w.wr1, s));
+  DR_TRY(op_conv_repack_bf16(c2, c1, c1, wm->conv[1].w, w.wr2, s));
+  DR_TRY(op_conv_repack_bf16(c3, c2, c2, wm->conv[2].w, w.wr3, s));
+  DR_TRY(op_conv_repack_bf16(c4, c3, c3, wm->conv[3].w, w.wr4, s));
+  DR_TRY(op_to_bf16_2d(d->enc_hidden, F, wm->map0.w, F + d->hidden, w.wproj, s));
+  DR_TRY(op_conv1_bf16(n, B, h0, w0, c1, src, w.wr1, wm->conv[0].b, w.a1, s));
+  DR_TRY(op_conv_bf16(n, c1, h0 / 2, w0 / 2, c2, w.a1, w.wr2, wm->conv[1].b, w.a2, 0, s));
+  DR_TRY(op_conv_bf16(n, c2, h0 / 4, w0 / 4, c3, w.a2, w.wr3, wm->conv[2].b, w.a3, 0, s));
+  DR_TRY(op_conv_bf16(n, c3, h0 / 8, w0 / 8, c4, w.a3, w.wr4, wm->conv[3].b, w.a4, 1, s));
+  return op_gemm_nt_bf16(n, d->enc_hidden, F, w.a4, F, w.wproj, wm->map0.b, feat, d->enc_hidden, s);
+}
+
 extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, const dr_frames* src, int B, int T,
                                    float* feat, void* ws, size_t ws_bytes, hipStream_t s) {
   DR_REQUIRE(d && wm && src && feat && B > 0 && T > 0, "null argument or empty batch");
   DR_REQUIRE(d->img_h % 16 == 0 && d->img_w % 16 == 0, "image size must be a multiple of 16");
   DR_REQUIRE(d->enc_f1 % 4 == 0 && d->enc_f2 % 4 == 0, "encoder filter counts must be multiples of 4");
+  DR_REQUIRE(d->precision == DR_PREC_FP32 || d->precision == DR_PREC_BF16, "precision must be DR_PREC_FP32/BF16");
   const int n = B * T;
   Carve c(ws);
   EncWs w;
   enc_carve(c, d, n, w);
   WS_CHECK(c, ws_bytes);
+  if (d->precision == DR_PREC_BF16) return encoder_bf16(d, wm, src, B, n, feat, w, s);
   const int c1 = d->enc_f1, c2 = d->enc_f2, c3 = 2 * d->enc_f2, c4 = 4 * d->enc_f2;
   const int h0 = d->img_h, w0 = d->img_w;
   DR_TRY(op_conv_repack_pad(c1, 3, 4, wm->conv[0].w, w.wr1, s));

@@ -96,6 +96,7 @@ class Dreamer(nn.Module):
         # extra config key: "fp32" parity mode (default) or "bf16" perf mode
         self.precision = c.get("precision", "fp32")
         self.pipeline_epochs = bool(c.get("pipeline_epochs", False))
+        self.world_model.precision = self.precision  # encoder kernels: bf16 MFMA in perf mode
         if self.precision not in ("fp32", "bf16"):
             raise ValueError(f"precision must be 'fp32' or 'bf16', got {self.precision!r}")
         self.device = device

@@ -63,6 +63,7 @@ class WorldModel(nn.Module):
         ib = self.decoder.image_builder
         d.dec_f1, d.dec_f2 = ib[4].out_channels, ib[2].out_channels
         d.dec_hidden = self.decoder.upscaler[0].out_features
+        d.precision = 1 if getattr(self, "precision", "fp32") == "bf16" else 0  # DR_PREC_BF16 / DR_PREC_FP32
         if agent is not None:
             a, c = agent.actor.base_net, agent.critic.value_net
             d.actor_h1, d.actor_h2 = a[0].out_features, a[3].out_features

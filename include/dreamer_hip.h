@@ -19,8 +19,10 @@
  *    whole train_Agent epoch can be captured into one hipGraph.
  *  - parameters are read in PyTorch's own layouts (Linear weight [out][in],
  *    GRUCell weight_ih [3H][in] gate order r,z,n, Conv2d [out][in][4][4]).
- *  - arithmetic is fp32 (parity mode): GEMMs use the exact-f32 MFMA
- *    (v_mfma_f32_16x16x4_f32), elementwise code is built -ffp-contract=off.
+ *  - arithmetic is fp32 (parity mode) unless dr_dims.precision selects bf16:
+ *    fp32 GEMMs use the exact-f32 MFMA (v_mfma_f32_16x16x4_f32), elementwise
+ *    code is built -ffp-contract=off; bf16 mode runs the encoder convolutions
+ *    and feature projection on v_mfma_f32_16x16x32_bf16 (f32 accumulate).
  */
 #ifndef DREAMER_HIP_H
 #define DREAMER_HIP_H
@@ -57,7 +59,11 @@ typedef struct {
   int buckets;         /* critic_reward_buckets (255) */
   int dec_f1, dec_f2;  /* decoder_filter_num_1/2 (32, 64): convT channels 4*f2 -> 2*f2 -> f2 -> f1 -> 3 */
   int dec_hidden;      /* decoder_hidden_layer_nodes (200) */
+  int precision;       /* DR_PREC_FP32 (parity mode, default) or DR_PREC_BF16 (perf mode: bf16 MFMA
+                          operands, f32 accumulation; the extra `precision` config key) */
 } dr_dims;
+#define DR_PREC_FP32 0
+#define DR_PREC_BF16 1
 
 /* WorldModel parameters (WorldModel.py:55-60). */
 typedef struct {

@@ -1,0 +1,105 @@
+"""bf16 perf mode (config key precision="bf16"; SURVEY.md section 5, BASELINE
+configs[1]): the encoder's four convolutions and the latent_mapper.0 feature
+projection (VariationalAutoEncoder.py:57-75) run on the bf16 MFMA with f32
+accumulation.
+
+Two checks, both through the C ABI (dr_encoder_features):
+  * kernel exactness: against a torch emulation that rounds to bf16 at the
+    same points (normalised frame, weights, every activation) and accumulates
+    in f32 -- normwise relative error <= 2e-3 (differences are f32 summation
+    order and the odd 1-ulp bf16 rounding flip they cause downstream);
+  * precision cost: against the fp32 parity path -- normwise relative error
+    <= 2e-2 (the stated bf16 tolerance of the features).
+A full train_Agent epoch in bf16 mode at BASELINE configs[1] shape must give
+finite losses, and its warm-start latents are compared with the fp32 mode's:
+the flip fraction is reported (bf16 does not promise identical indices).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def _emulate(frames_u8, P, pre=""):
+    """bf16-rounded reference of Encoder.forward's conv stack + feature columns."""
+    x = _bf(frames_u8.float() / 255.0 - 0.5)
+    for i in range(4):
+        w, b = P[f"{pre}feature_extractor.{2 * i}.weight"], P[f"{pre}feature_extractor.{2 * i}.bias"]
+        x = F.conv2d(x, _bf(w), b.float(), stride=2, padding=1)
+        x = _bf(F.silu(x))
+    flat = x.flatten(1)
+    W = P[f"{pre}latent_mapper.0.weight"][:, :flat.shape[1]]
+    return flat @ _bf(W).t() + P[f"{pre}latent_mapper.0.bias"]
+
+
+def _features(enc, d, frames_u8, dev):
+    """dr_encoder_features over a (n, 3, H, W) u8 batch via a one-slot-per-frame ring."""
+    from dreamer_amd import _lib as L
+    from dreamer_amd import hip
+    n = frames_u8.shape[0]
+    ring = frames_u8.contiguous().to(dev)
+    starts = torch.arange(n, dtype=torch.int64, device=dev)
+    fr = L.dr_frames(L.ptr(ring), n, L.ptr(starts), None, 0, 0, 1, 0)
+    feat = torch.empty(n, d.enc_hidden, device=dev)
+    ws = torch.empty(L.query("dr_encoder_workspace_bytes", d, n), dtype=torch.uint8, device=dev)
+    L.call("dr_encoder_features", d, enc, fr, n, 1, L.ptr(feat), L.ptr(ws), ws.numel(), hip.stream())
+    torch.cuda.synchronize()
+    return feat.cpu()
+
+
+@pytest.mark.parametrize("res", [64, 128])
+def test_encoder_bf16_matches_emulation(gpu, res):
+    from dreamer_amd import Dreamer
+    from formula import FULL
+    cfg = dict(FULL)
+    cfg.update(observation_dims=[res, res], precision="bf16")
+    torch.manual_seed(0)
+    d = Dreamer(cfg, gpu)
+    wm = d.world_model
+    g = torch.Generator().manual_seed(1)
+    n = 40 if res == 64 else 12
+    frames = torch.randint(0, 256, (n, 3, res, res), generator=g, dtype=torch.uint8)
+    dims = wm.dims(d.agent)
+    assert dims.precision == 1
+    got = _features(wm.packed(), dims, frames, gpu)
+    P = {k: v.detach().cpu() for k, v in wm.encoder.state_dict().items()}
+    ref = _emulate(frames, P)
+    err = float((got - ref).norm() / ref.norm())
+    assert err <= 2e-3, f"bf16 encoder vs bf16 emulation: normwise rel err {err:.3g}"
+    # the fp32 parity path on the same frames: the precision cost of bf16
+    dims.precision = 0
+    f32 = _features(wm.packed(), dims, frames, gpu)
+    err32 = float((got - f32).norm() / f32.norm())
+    print(f"res {res}: bf16 vs emulation {err:.2e}, bf16 vs fp32 {err32:.2e}")
+    assert err32 <= 2e-2, f"bf16 encoder vs fp32: normwise rel err {err32:.3g}"
+
+
+def test_train_agent_bf16_epoch(gpu):
+    """One train_Agent epoch per precision at configs[1] (B=64 S=64 H=15) from
+    the same replay, weights and noise: bf16 losses finite and near fp32."""
+    from dreamer_amd import Dreamer
+    from formula import FULL, replay_data
+    out = {}
+    for prec in ("fp32", "bf16"):
+        cfg = dict(FULL)
+        cfg.update(batch_size=64, sequence_length=64, horizon=15, buffer_size=1024, precision=prec)
+        torch.manual_seed(0)
+        d = Dreamer(cfg, gpu)
+        fr, ac, rw, ct = replay_data(1024, (64, 64), 3, seed=3)
+        d.buffer.load_arrays(fr, ac, rw, ct)
+        d.engine.rng.reseed(77)
+        np.random.seed(5)
+        la, lc = d.train_Agent()
+        torch.cuda.synchronize()
+        out[prec] = (float(la), float(lc), d.engine.latents[:, 0].cpu().clone())
+    (a32, c32, z32), (a16, c16, z16) = out["fp32"], out["bf16"]
+    assert np.isfinite(a16) and np.isfinite(c16)
+    flips = float((z32.reshape(-1, 32).argmax(-1) != z16.reshape(-1, 32).argmax(-1)).float().mean())
+    print(f"fp32 losses ({a32:.5f}, {c32:.5f}), bf16 ({a16:.5f}, {c16:.5f}); warm-start index flips {flips:.3%}")
+    assert abs(c16 - c32) <= 0.05 * abs(c32)
