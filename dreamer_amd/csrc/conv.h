@@ -24,6 +24,9 @@ int op_to_bf16_2d(int rows, int cols, const float* x, long long ld, void* y, hip
 // first conv from the frames (u8 ring or f32): out bf16 NHWC [n][h/2][w/2][cout]; wr cin_pad = 4
 int op_conv1_bf16(int n, int nb, int h, int w, int cout, const dr_frames* src, const void* wr, const float* bias,
                   void* out, hipStream_t s);
+// conv1 + conv2 fused (c1 = 32, c2 = 64, square 64 / 128 frames); DR_E_INVALID = shape not covered
+int op_enc12_bf16(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const void* wr1, const float* b1,
+                  const void* wr2, const float* b2, void* out, hipStream_t s);
 // k4 s2 p1 conv + bias + SiLU, bf16 NHWC in -> bf16 NHWC (or NCHW) out
 int op_conv_bf16(int n, int cin, int ih, int iw, int cout, const void* in, const void* wr, const float* bias,
                  void* out, int out_nchw, hipStream_t s);

@@ -53,8 +53,10 @@ static int encoder_bf16(const dr_dims* d, const dr_world_model* wm, const dr_fra
   DR_TRY(op_conv_repack_bf16(c3, c2, c2, wm->conv[2].w, w.wr3, s));
   DR_TRY(op_conv_repack_bf16(c4, c3, c3, wm->conv[3].w, w.wr4, s));
   DR_TRY(op_to_bf16_2d(d->enc_hidden, F, wm->map0.w, F + d->hidden, w.wproj, s));
-  DR_TRY(op_conv1_bf16(n, B, h0, w0, c1, src, w.wr1, wm->conv[0].b, w.a1, s));
-  DR_TRY(op_conv_bf16(n, c1, h0 / 2, w0 / 2, c2, w.a1, w.wr2, wm->conv[1].b, w.a2, 0, s));
+  if (op_enc12_bf16(n, B, h0, w0, c1, c2, src, w.wr1, wm->conv[0].b, w.wr2, wm->conv[1].b, w.a2, s) != DR_OK) {
+    DR_TRY(op_conv1_bf16(n, B, h0, w0, c1, src, w.wr1, wm->conv[0].b, w.a1, s));
+    DR_TRY(op_conv_bf16(n, c1, h0 / 2, w0 / 2, c2, w.a1, w.wr2, wm->conv[1].b, w.a2, 0, s));
+  }
   DR_TRY(op_conv_bf16(n, c2, h0 / 4, w0 / 4, c3, w.a2, w.wr3, wm->conv[2].b, w.a3, 0, s));
   DR_TRY(op_conv_bf16(n, c3, h0 / 8, w0 / 8, c4, w.a3, w.wr4, wm->conv[3].b, w.a4, 1, s));
   return op_gemm_nt_bf16(n, d->enc_hidden, F, w.a4, F, w.wproj, wm->map0.b, feat, d->enc_hidden, s);

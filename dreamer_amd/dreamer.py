@@ -213,41 +213,155 @@ class Dreamer(nn.Module):
     def save_trained_Dreamer(self, save_path):
         torch.save(self.state_dict(), save_path)
 
+    # ---- true resume (beyond the reference, whose checkpoints are weights only:
+    # Dreamer.py:289-293, 347-354).  One torch.save file of tensors and plain
+    # scalars (loads with weights_only=True): the reference-layout state_dict,
+    # the three AdamW states (moments + step), S, the engine / ad-hoc Philox
+    # states, numpy's and torch's CPU generators (window sampling), the replay
+    # ring and the env seed counter.  Resuming reproduces the uninterrupted run
+    # bit for bit (tests/test_gpu_api.py::test_training_state_resume).
+    TRAINING_STATE_FORMAT = "dreamer_amd.training_state.v1"
+
+    def training_state(self):
+        ag, wm, buf = self.agent, self.world_model, self.buffer
+        ag._ensure_flat()
+        wm._ensure_flat()
+        cpu = lambda t: t.detach().cpu().clone()
+        opt = lambda o: {"exp_avg": cpu(o.exp_avg), "exp_avg_sq": cpu(o.exp_avg_sq), "step": cpu(o.step_dev)}
+        name, keys, pos, has_gauss, gauss = np.random.get_state()
+        er, ar = hip.rng(self.device), hip.adhoc(self.device)
+        return {
+            "format": self.TRAINING_STATE_FORMAT,
+            "model": {k: cpu(v) for k, v in self.state_dict().items()},
+            "opt_actor": opt(ag.actor_optimiser), "opt_critic": opt(ag.critic_optimiser), "opt_wm": opt(wm.optimiser),
+            "S": cpu(ag.S_dev),
+            "rng_engine": cpu(er.state), "rng_engine_counter": int(er.counter),
+            "rng_adhoc": cpu(ar.state), "rng_adhoc_counter": int(ar.counter),
+            "np_rng": {"keys": torch.from_numpy(np.asarray(keys, dtype=np.int64)), "pos": int(pos),
+                       "has_gauss": int(has_gauss), "gauss": float(gauss)},
+            "torch_rng": torch.get_rng_state(),
+            "buffer": {"obs": torch.from_numpy(buf.observation_buffer.copy()),
+                       "act": torch.from_numpy(buf.action_buffer.copy()),
+                       "rew": torch.from_numpy(buf.reward_buffer.copy()),
+                       "cont": torch.from_numpy(buf.continue_buffer.copy()),
+                       "next_idx": int(buf.next_idx), "size": int(buf.size)},
+            "seed": int(self.seed),
+        }
+
+    def save_training_state(self, path):
+        torch.save(self.training_state(), path)
+
+    def load_training_state(self, path_or_state):
+        st = path_or_state if isinstance(path_or_state, dict) else torch.load(path_or_state, weights_only=True)
+        if st.get("format") != self.TRAINING_STATE_FORMAT:
+            raise ValueError(f"not a {self.TRAINING_STATE_FORMAT} file: {st.get('format')!r}")
+        self.load_state_dict({k: v.to(self.device) for k, v in st["model"].items()})
+        ag, wm, buf = self.agent, self.world_model, self.buffer
+        ag._ensure_flat()
+        wm._ensure_flat()
+        for o, k in ((ag.actor_optimiser, "opt_actor"), (ag.critic_optimiser, "opt_critic"), (wm.optimiser, "opt_wm")):
+            o.exp_avg.copy_(st[k]["exp_avg"])
+            o.exp_avg_sq.copy_(st[k]["exp_avg_sq"])
+            o.step_dev.copy_(st[k]["step"])
+        ag.S_dev.copy_(st["S"])
+        er, ar = hip.rng(self.device), hip.adhoc(self.device)
+        er.state.copy_(st["rng_engine"])
+        er.counter = int(st["rng_engine_counter"])
+        ar.state.copy_(st["rng_adhoc"])
+        ar.counter = int(st["rng_adhoc_counter"])
+        r = st["np_rng"]
+        np.random.set_state(("MT19937", r["keys"].numpy().astype(np.uint32), int(r["pos"]), int(r["has_gauss"]),
+                             float(r["gauss"])))
+        torch.set_rng_state(st["torch_rng"])
+        b = st["buffer"]
+        buf.observation_buffer[...] = b["obs"].numpy()
+        buf.action_buffer[...] = b["act"].numpy()
+        buf.reward_buffer[...] = b["rew"].numpy()
+        buf.continue_buffer[...] = b["cont"].numpy()
+        buf.next_idx, buf.size = int(b["next_idx"]), int(b["size"])
+        buf._dirty = list(range(buf.capacity))  # the device mirror re-uploads on next use
+        self.seed = int(st["seed"])
+
     # ------------------------------------------------- acting (batch-1, HIP)
     def _obs_tensor(self, observation):
         obs = observation.transpose(2, 0, 1).astype(np.uint8)
         norm = (obs.astype(np.float32) / 255.0) - 0.5
         return norm, torch.tensor(norm, dtype=torch.float32, device=self.device).unsqueeze(0).unsqueeze(0)
 
+    def act_step(self, observation, z=None, h=None, a=None, deterministic=False):
+        """One env step of the acting loop in ONE launch (dr_act_step): with
+        (z, h, a) from the previous step, h' = GRU(z, h, a) (observe_step,
+        WorldModel.py:79-82); without them, h' = 0 (episode start,
+        Dreamer.py:186-187).  Then z' = Encoder.encode(h', observation) and
+        a' = Actor.act(h', z', deterministic).  observation: the env's H x W x 3
+        uint8 frame.  Returns (a', mu, sigma, z', h') shaped (1, 1, ...)."""
+        dev = self.device
+        L.require_gpu(torch.empty(0, device=dev))
+        d = self.world_model.dims(self.agent)
+        self.agent._ensure_flat()
+        R, C = self.latent_state_dims
+        A, Hd = self.action_dims, self.hidden_state_dims
+        st = getattr(self, "_act_bufs", None)
+        if st is None:
+            H_, W_ = self.observation_dims
+            st = self._act_bufs = dict(
+                pin=torch.empty(H_, W_, 3, dtype=torch.uint8).pin_memory(),
+                frame=torch.empty(H_, W_, 3, dtype=torch.uint8, device=dev),
+                h0=torch.zeros(Hd, device=dev),
+                ws=torch.empty(L.query("dr_act_step_workspace_bytes", d), dtype=torch.uint8, device=dev))
+        self._act_sync()  # the previous step's copy out of the pinned staging buffer has run
+        st["pin"].numpy()[...] = observation
+        st["frame"].copy_(st["pin"], non_blocking=True)
+        has_prev = z is not None
+        zp = z.reshape(-1).float().contiguous() if has_prev else None
+        hp = h.reshape(-1).float().contiguous() if has_prev else st["h0"]
+        ap = a.reshape(-1).float().contiguous() if has_prev else None
+        z2 = torch.empty(1, 1, R, C, device=dev)
+        h2 = torch.empty(1, 1, Hd, device=dev)
+        a2, mu, sg = (torch.empty(1, 1, A, device=dev) for _ in range(3))
+        L.call("dr_act_step", d, self.world_model.packed(), self.agent.actor_struct(), L.ptr(st["frame"]),
+               int(has_prev), L.ptr(zp), L.ptr(hp), L.ptr(ap), hip.adhoc(dev).noise(), int(deterministic),
+               L.ptr(z2), L.ptr(h2), L.ptr(a2), L.ptr(mu), L.ptr(sg), None, L.ptr(st["ws"]), st["ws"].numel(),
+               hip.stream())
+        self._act_ev = torch.cuda.Event()
+        self._act_ev.record()
+        return a2, mu, sg, z2, h2
+
+    def _act_sync(self):
+        ev = getattr(self, "_act_ev", None)
+        if ev is not None:
+            ev.synchronize()
+
     def rollout_policy(self, env, random_policy=False):  # Dreamer.py:177-226
+        """Same env / buffer sequence as the reference; the device work of each
+        env step (observe_step + the next step's act) is one dr_act_step launch."""
         with torch.no_grad():
             if self.agent_obs is None:
                 observation, _ = env.reset(seed=self.seed)
-                self.agent_obs, ot = self._obs_tensor(observation)
-                self.agent_hidden = torch.zeros(1, 1, self.hidden_state_dims, device=self.device)
-                self.agent_latent, _ = self.world_model.encoder.encode(self.agent_hidden, ot)
+                self.agent_obs = (observation.transpose(2, 0, 1).astype(np.float32) / 255.0) - 0.5
+                _, _, _, self.agent_latent, self.agent_hidden = self.act_step(observation)
+            action = None
+            if not random_policy:  # the current actor's action for the current state
+                action, _, _ = self.agent.actor.act(self.agent_hidden, self.agent_latent, deterministic=False)
             for _ in range(self.sequence_length):
                 if random_policy:
                     action_np = env.action_space.sample()
                     action = torch.tensor(action_np, dtype=torch.float32, device=self.device).view(1, 1, -1)
                 else:
-                    action, _, _ = self.agent.actor.act(self.agent_hidden, self.agent_latent, deterministic=False)
                     action_np = action.detach().cpu().numpy().reshape(-1)
                 observation_, reward, terminated, truncated, _ = env.step(action_np)
-                norm_, ot_ = self._obs_tensor(observation_)
                 done = terminated or truncated
                 current_u8 = ((self.agent_obs + 0.5) * 255.0).astype(np.uint8)
                 self.buffer.add_to_buffer(current_u8, action_np, reward, 1 - done)
                 if done:
                     self.seed += 1
                     observation, _ = env.reset(seed=self.seed)
-                    self.agent_obs, ot = self._obs_tensor(observation)
-                    self.agent_hidden = torch.zeros(1, 1, self.hidden_state_dims, device=self.device)
-                    self.agent_latent, _ = self.world_model.encoder.encode(self.agent_hidden, ot)
+                    self.agent_obs = (observation.transpose(2, 0, 1).astype(np.float32) / 255.0) - 0.5
+                    action, _, _, self.agent_latent, self.agent_hidden = self.act_step(observation)
                 else:
-                    self.agent_obs = norm_
-                    self.agent_latent, self.agent_hidden, _ = self.world_model.observe_step(
-                        self.agent_latent, self.agent_hidden, action, ot_)
+                    self.agent_obs = (observation_.transpose(2, 0, 1).astype(np.float32) / 255.0) - 0.5
+                    action, _, _, self.agent_latent, self.agent_hidden = self.act_step(
+                        observation_, self.agent_latent, self.agent_hidden, action)
 
     def evaluate_agent(self, env, eval_episodes):  # Dreamer.py:295-322
         rewards = []
@@ -256,18 +370,16 @@ class Dreamer(nn.Module):
                 self.seed += 1
                 total = 0
                 observation, _ = env.reset(seed=self.seed)
-                _, ot = self._obs_tensor(observation)
-                hidden = torch.zeros(1, 1, self.hidden_state_dims, device=self.device)
-                latent, _ = self.world_model.encoder.encode(hidden, ot)
+                action, _, _, latent, hidden = self.act_step(observation, deterministic=True)
                 done = False
                 while not done:
-                    action, _, _ = self.agent.actor.act(hidden, latent, deterministic=True)
                     observation_, reward, terminated, truncated, _ = env.step(
                         action.detach().cpu().numpy().squeeze(0).squeeze(0))
-                    _, ot = self._obs_tensor(observation_)
                     total += reward
                     done = terminated or truncated
-                    latent, hidden, _ = self.world_model.observe_step(latent, hidden, action, ot)
+                    if not done:
+                        action, _, _, latent, hidden = self.act_step(observation_, latent, hidden, action,
+                                                                     deterministic=True)
                 rewards.append(total)
         return torch.tensor(rewards, dtype=torch.float32, device=self.device).mean()
 
@@ -305,21 +417,18 @@ class Dreamer(nn.Module):
     def Run(self, env, env_seed, render=True):  # Dreamer.py:374-401
         total = 0
         observation, _ = env.reset(seed=env_seed)
-        _, ot = self._obs_tensor(observation)
-        hidden = torch.zeros(1, 1, self.hidden_state_dims, device=self.device)
         with torch.no_grad():
-            latent, _ = self.world_model.encoder.encode(hidden, ot)
+            action, _, _, latent, hidden = self.act_step(observation, deterministic=True)
         done = False
         while not done:
             if render:
                 env.render()
-            with torch.no_grad():
-                action, _, _ = self.agent.actor.act(hidden, latent, deterministic=True)
             observation_, reward, terminated, truncated, _ = env.step(
                 action.detach().cpu().numpy().squeeze(0).squeeze(0))
-            _, ot = self._obs_tensor(observation_)
             total += reward
             done = terminated or truncated
-            with torch.no_grad():
-                latent, hidden, _ = self.world_model.observe_step(latent, hidden, action, ot)
+            if not done:
+                with torch.no_grad():
+                    action, _, _, latent, hidden = self.act_step(observation_, latent, hidden, action,
+                                                                 deterministic=True)
         return total

@@ -266,3 +266,99 @@ def test_train_dreamer_with_fake_env(gpu, tmp_path, monkeypatch):
     d2, _ = _dreamer(gpu, batch_size=4, sequence_length=16, horizon=5)
     d2.load_pretrained_dreamer("models/agent_latest.pth")
     assert all(torch.equal(v.cpu(), sd[k].cpu()) for k, v in d2.state_dict().items())
+
+
+def test_training_state_resume(gpu, tmp_path):
+    """save_training_state / load_training_state (true resume: weights, the
+    three AdamW states, S, Philox / numpy / torch generators, replay ring):
+    a resumed run repeats the uninterrupted run's next iteration bit for bit
+    (the reference saves weights only, Dreamer.py:289-293)."""
+    from formula import replay_data
+    kw = dict(batch_size=8, sequence_length=16, horizon=5, buffer_size=256, AC_epochs=1, WM_epochs=1)
+    d, _ = _dreamer(gpu, formula=False, **kw)
+    fr, ac, rw, ct = replay_data(256, (64, 64), A, seed=11)
+    d.buffer.load_arrays(fr, ac, rw, ct)
+    np.random.seed(1)
+    d.train_world_model()
+    d.train_Agent()
+    path = tmp_path / "state.pt"
+    d.save_training_state(path)
+
+    def iteration(dr):
+        wm = float(dr.train_world_model()[0])
+        la, lc = dr.train_Agent()
+        torch.cuda.synchronize()
+        return wm, float(la), float(lc), {k: v.detach().cpu().clone() for k, v in dr.state_dict().items()}
+
+    ref = iteration(d)
+    torch.manual_seed(123)  # a different process state before the resume
+    np.random.seed(99)
+    d2, _ = _dreamer(gpu, formula=False, **kw)
+    d2.load_training_state(path)
+    got = iteration(d2)
+    assert got[:3] == ref[:3], (got[:3], ref[:3])
+    for k in ref[3]:
+        assert torch.equal(got[3][k], ref[3][k]), k
+    # the file is plain tensors / scalars: loads with weights_only=True
+    st = torch.load(path, weights_only=True)
+    assert st["format"] == "dreamer_amd.training_state.v1" and len(st["model"]) == len(ref[3])
+
+
+def test_act_step_matches_unfused(gpu):
+    """dr_act_step (one cooperative launch per env step) == the unfused API
+    path it replaces in rollout_policy / evaluate_agent / Run: Encoder.encode
+    or WorldModel.observe_step, then Actor.act (Dreamer.py:177-226, 295-322),
+    same explicit noise.  Indices exact; h, action, mu, sigma at 1e-5.
+    Prints the per-env-step device time of both paths."""
+    import time
+    from dreamer_amd import hip
+    d, P = _dreamer(gpu)
+    g = torch.Generator().manual_seed(21)
+    frames = [torch.randint(0, 256, (64, 64, 3), generator=g, dtype=torch.uint8).numpy() for _ in range(4)]
+    q = torch.empty(1, R, C).exponential_(generator=g).to(gpu)
+    eps = torch.randn(1, 1, A, generator=g).to(gpu)
+    wm, actor = d.world_model, d.agent.actor
+    with torch.no_grad(), hip.noise_override(q=q, eps=eps):
+        _, ot = d._obs_tensor(frames[0])
+        z_u, _ = wm.encoder.encode(torch.zeros(1, 1, HD, device=gpu), ot)
+        h_u = torch.zeros(1, 1, HD, device=gpu)
+        a_u, mu_u, sg_u = actor.act(h_u, z_u, deterministic=False)
+        a_f, mu_f, sg_f, z_f, h_f = d.act_step(frames[0])
+        for k in range(1, 4):
+            close(h_f, h_u, 1e-5, 1e-6, f"h step {k - 1}")  # step 0: both exactly 0
+            zi_f, zi_u = z_f.reshape(R, C).argmax(-1).cpu(), z_u.reshape(R, C).argmax(-1).cpu()
+            assert torch.equal(zi_f, zi_u), f"step {k - 1}: {int((zi_f != zi_u).sum())} latent groups differ"
+            close(z_f, z_u, 0, 1e-6, f"straight-through latent values step {k - 1}")
+            close(a_f, a_u, 1e-5, 1e-6, "action")
+            close(mu_f, mu_u, 1e-5, 1e-6, "mu")
+            close(sg_f, sg_u, 1e-5, 1e-6, "sigma")
+            _, ot = d._obs_tensor(frames[k])
+            z_u, h_u, _ = wm.observe_step(z_u, h_u, a_u, ot)
+            a_u, mu_u, sg_u = actor.act(h_u, z_u, deterministic=False)
+            a_f, mu_f, sg_f, z_f, h_f = d.act_step(frames[k], z_f, h_f, a_f)
+            close(h_f, h_u, 1e-5, 1e-6, f"h step {k}")
+    torch.cuda.synchronize()
+
+    def per_step(fn, n=50):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / n * 1e6
+
+    z, h, a = z_f, h_f, a_f
+    with torch.no_grad():
+        def unfused():
+            _, ot = d._obs_tensor(frames[1])
+            z2, h2, _ = wm.observe_step(z, h, a, ot)
+            actor.act(h2, z2, deterministic=True)
+
+        t_u = per_step(unfused)
+        t_f = per_step(lambda: d.act_step(frames[1], z, h, a, deterministic=True))
+    print(f"batch-1 env step (device work + H2D of the frame): unfused {t_u:.1f} us, fused dr_act_step {t_f:.1f} us")
+    ts = d._act_bufs["ws"][0:128].view(torch.int64).cpu()  # workgroup 0's stage clock (10 ns ticks)
+    marks = [0, 1, 2, 3, 4, 5, 6, 7, 15]
+    print("dr_act_step stage ends (us after kernel start):",
+          [round(float(ts[m] - ts[0]) / 100.0, 2) for m in marks[1:]])
