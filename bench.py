@@ -130,6 +130,40 @@ def bench_wm(d, B, steps, warmup):
     return el / steps, ev0.elapsed_time(ev1) / 1e3 / steps, float(wm.last_losses[0])
 
 
+def bench_acting(d, dev, n=100):
+    """Device work of one env step of rollout_policy / evaluate_agent / Run
+    (Dreamer.py:177-226, 295-322): the fused dr_act_step launch vs the unfused
+    observe_step + Actor.act calls it replaces (host wall, frame H2D included)."""
+    g = np.random.default_rng(7)
+    frames = [g.integers(0, 256, size=(64, 64, 3), dtype=np.uint8) for _ in range(4)]
+    with torch.no_grad():
+        a, _, _, z, h = d.act_step(frames[0])
+
+        def unfused(i):
+            _, ot = d._obs_tensor(frames[i % 4])
+            z2, h2, _ = d.world_model.observe_step(z, h, a, ot)
+            d.agent.actor.act(h2, z2, deterministic=True)
+
+        def fused(i):
+            d.act_step(frames[i % 4], z, h, a, deterministic=True)
+
+        out = {}
+        for name, fn in (("unfused_us", unfused), ("fused_us", fused)):
+            for i in range(5):
+                fn(i)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(n):
+                fn(i)
+            torch.cuda.synchronize()
+            out[name] = round((time.perf_counter() - t0) / n * 1e6, 1)
+    ts = d._act_bufs["ws"][0:128].view(torch.int64).cpu()
+    out["fused_kernel_us"] = round(float(ts[15] - ts[0]) / 100.0, 1)
+    out["note"] = ("per env step, batch 1: dr_act_step = GRU + conv encoder + sampler + actor in one launch "
+                   "(XCD-hierarchical grid barrier); fused_kernel_us from the kernel's own clock")
+    return out
+
+
 def cpu_info():
     """CPU model and core counts of this host (for the cpu_baseline record)."""
     model = "unknown"
@@ -367,6 +401,30 @@ def main():
                 "ms_per_epoch": round(el64 / args.steps * 1e3, 4),
                 "note": "BASELINE configs[1] shape (B=64/GPU S=64 H=15), Dreamer.train_Agent() AC_epochs=1"}
             del d64
+        if args.precision == "fp32":
+            # bf16 perf mode (config key precision="bf16"; BASELINE configs[1] names bf16):
+            # the encoder's convolutions and feature projection on the bf16 MFMA
+            bf = {}
+            for tag, bb in (("north_star_B256", B), ("configs1_B64", 64)):
+                if tag == "configs1_B64" and bb == B:
+                    continue
+                cb, db = make_dreamer(CAR_RACER, dev, bb, S, H, res, 1, world, rank, group, "bf16")
+                elb, (lab, lcb) = time_train_agent(db, args.steps, args.warmup)
+                enc_b = db._engine.time_encoder(reps=5) / 1e3
+                fl_b = encoder_flops_per_frame(cb) * bb * (S // 2)
+                ach = fl_b / enc_b / 1e12
+                bf[tag] = {"value": round(world * bb * H * args.steps / elb, 1), "unit": "imagined latent-steps/s",
+                           "ms_per_epoch": round(elb / args.steps * 1e3, 4), "dtype": "bf16", "B_per_gpu": bb,
+                           "losses": {"actor": lab, "critic": lcb},
+                           "roofline": {"bound": "mfma", "kernel": "encoder conv stack + feature projection",
+                                        "achieved": round(ach, 2), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                        "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4),
+                                        "encoder_ms": round(enc_b * 1e3, 4)}}
+                del db
+            bf["note"] = ("Dreamer(config with precision='bf16'): conv1+conv2 fused from the u8 ring, conv3/conv4 "
+                          "and the projection as bf16 implicit GEMMs (f32 accumulate); the imagination / update "
+                          "chain stays f32 (tests/test_gpu_bf16.py states the tolerances)")
+            secondary["bf16_perf_mode"] = bf
     wm = None
     if args.wm_steps > 0:
         wm_s, wm_gpu_s, wm_loss = bench_wm(d, B, args.wm_steps, 2)
@@ -428,6 +486,8 @@ def main():
             "value": round(world * B * H / (wm_s + ac_s), 1), "unit": "imagined latent-steps/s",
             "ms_per_iteration": round((wm_s + ac_s) * 1e3, 3),
             "note": "1 WM step + 1 train_Agent epoch per iteration (WM_epochs = AC_epochs = 1)"}
+    if not args.no_secondary and res == 64:
+        secondary["acting_batch1"] = bench_acting(d, dev)
     if secondary:
         out["secondary"] = secondary
     if world == 1 and not args.no_cpu_baseline:
