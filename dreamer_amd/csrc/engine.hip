@@ -333,6 +333,10 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
       p[1] = lin2(B, d->cont_h1, h_n, ldH, Hd, z_n, ldL, L, wm->cont.l0.w, wm->cont.l0.b, w.p1c, d->cont_h1);
       if (nxt)
         p[2] = lin2(B, a1, h_n, ldH, Hd, z_n, ldL, L, ac->l0.w, ac->l0.b, tp.pre1a + (long long)(t + 1) * a1, lda1);
+      // split-K scratch (the actor weight-gradient region, idle until the backward)
+      float* sk = w.sk;
+      long long skn = w.sk_n;
+      for (int i = 0; i < (nxt ? 3 : 2); ++i) give_splitk(p[i], sk, skn);
       DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, nxt ? 3 : 2, s));
     }
     {

@@ -989,8 +989,12 @@ __device__ __forceinline__ float tile_b_kn(const GemmArgs& g, const float* W, in
   return dr_ld1(W, (unsigned)(k * ldb + n));
 }
 
-template <int BM, int BN, int KC, bool A_KM, bool B_KN, bool VEC>
-__global__ __launch_bounds__(256) void k_gemm_tile(GemmBatch gb, int splits) {
+// NW waves: 4 as 2 x 2 (32 x 32 wave tiles at 64 x 64), 8 as 4 x 2 (16 x 16
+// wave tiles at 64 x 32: two waves per SIMD hide the per-chunk barrier and
+// LDS latency that one wave per SIMD exposes at these short K ranges)
+template <int BM, int BN, int KC, bool A_KM, bool B_KN, bool VEC, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void k_gemm_tile(GemmBatch gb, int splits) {
+  constexpr int NTH = 64 * NW;
   constexpr int TLDS = KC + 8;  // = 8 mod 16 dwords: conflict-free ds_read_b128 fragments
   constexpr int KQ = KC / 4;  // float4 per row piece
   __shared__ GemmArgs s_args;
@@ -1017,14 +1021,14 @@ __global__ __launch_bounds__(256) void k_gemm_tile(GemmBatch gb, int splits) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 
   // row-major loader (MK / NK): thread -> (row prow + RS i, float4 quad)
-  constexpr int RS = 256 / KQ;
-  constexpr int APT = BM * KQ / 256, BPT = BN * KQ / 256;
+  constexpr int RS = NTH / KQ;
+  constexpr int APT = BM * KQ / NTH, BPT = BN * KQ / NTH;
   // transposed loader (KM / KN): thread -> (m = tid % BM, k quad tid / BM + AQ i):
   // four scalar loads down k, each coalesced over the wave's consecutive m,
   // land as ONE float4 row piece in LDS -- the same [m][k] layout and
   // conflict-free ds_write_b128 as the row-major path (a transposing scatter
   // of float4-along-m loads hits one LDS bank 16 times)
-  constexpr int AQ = 256 / BM, BQ = 256 / BN;
+  constexpr int AQ = NTH / BM, BQ = NTH / BN;
   constexpr int APTT = KQ / AQ, BPTT = KQ / BQ;
   static_assert(APT >= 1 && BPT >= 1 && AQ >= 1 && BQ >= 1, "tile");
   static_assert(A_KM ? APTT == APT : true, "loader");
@@ -1103,7 +1107,9 @@ __global__ __launch_bounds__(256) void k_gemm_tile(GemmBatch gb, int splits) {
     }
   };
 
-  constexpr int WTM = BM / 2, WTN = BN / 2, FM = WTM / 16, FN = WTN / 16;
+  constexpr int WGM = NW / 2;  // waves along M (2 along N)
+  constexpr int WTM = BM / WGM, WTN = BN / 2, FM = WTM / 16, FN = WTN / 16;
+  static_assert(FM >= 1 && FN >= 1, "wave tile");
   const int wm0 = (wave >> 1) * WTM, wn0 = (wave & 1) * WTN;
   const int r = lane & 15, q = lane >> 4;
   f32x4 acc[FM][FN];
@@ -1587,7 +1593,7 @@ int mlp2_launch(const Mlp2Args* probs, int count, hipStream_t s) {
 
 // mid-size GEMMs: LDS double-buffered tile kernel, split-K when the tile grid
 // is too small to fill the chip and every problem brought scratch for it
-template <int BM, int BN, int KC, bool A_KM, bool B_KN>
+template <int BM, int BN, int KC, bool A_KM, bool B_KN, int NW = 4>
 static void launch_tile2(GemmBatch& gb, int count, hipStream_t s) {
   int maxt = 0, nch = 1 << 30, tot = 0;
   long long maxMN = 0;
@@ -1617,8 +1623,8 @@ static void launch_tile2(GemmBatch& gb, int count, hipStream_t s) {
       while (splits > 1 && (long long)splits * gb.p[i].M * gb.p[i].N > gb.p[i].splitk_floats) --splits;
   }
   dim3 grid(dr_xcd_grid(maxt), splits, count);
-  if (vec) hipLaunchKernelGGL((k_gemm_tile<BM, BN, KC, A_KM, B_KN, true>), grid, dim3(256), 0, s, gb, splits);
-  else hipLaunchKernelGGL((k_gemm_tile<BM, BN, KC, A_KM, B_KN, false>), grid, dim3(256), 0, s, gb, splits);
+  if (vec) hipLaunchKernelGGL((k_gemm_tile<BM, BN, KC, A_KM, B_KN, true, NW>), grid, dim3(64 * NW), 0, s, gb, splits);
+  else hipLaunchKernelGGL((k_gemm_tile<BM, BN, KC, A_KM, B_KN, false, NW>), grid, dim3(64 * NW), 0, s, gb, splits);
   if (splits > 1)
     hipLaunchKernelGGL(k_splitk_finish, dim3((unsigned)((maxMN + 255) / 256), 1, count), dim3(256), 0, s, gb, splits);
 }
@@ -1646,15 +1652,37 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
       tiles += dr_cdiv(gb.p[i].M, 64) * dr_cdiv(gb.p[i].N, 64);
       ws = ws && gb.p[i].splitk_ws != nullptr;
     }
+    // per-step products at 128-512 rows with a deep K (BPTT input gradients,
+    // K = 1800; the heads' first layers, K = 1624) or a wide N (the GRU's
+    // hidden product): 32 x 32 tiles, K chunks of 64, split-K only while the
+    // tile grid is under one workgroup per CU.  Against the 16/64-row skinny
+    // tiles, which re-read the weights per row tile and the activations per
+    // 16 columns: 44 -> 32 us (BPTT, 2 problems), 23 -> 15 us (heads, 3
+    // problems, split-K 4), profiles/r02h_kbench_tile_B256.txt
+    if (!A_KM && !B_KN && maxM >= 128 && maxM <= 512) {
+      int tiles32 = 0;
+      for (int i = 0; i < count; ++i) tiles32 += dr_cdiv(gb.p[i].M, 32) * dr_cdiv(gb.p[i].N, 32);
+      if (g_tile_variant == 0 && (minK >= 1024 || (minK >= 512 && tiles32 >= 256))) {
+        GemmBatch gt = gb;
+        if (tiles32 >= 256)
+          for (int i = 0; i < count; ++i) gt.p[i].splitk_ws = nullptr;
+        launch_tile2<32, 32, 64, false, false, 4>(gt, count, s);
+        return;
+      }
+    }
     // weight gradients (TN) and tall, deep products go to the tile kernel --
     // when it can fill the chip: a per-step product at B = 256 (16 tiles of
     // 64 x 64, no split-K scratch) runs on 52+ skinny 64-row workgroups instead
-    if (A_KM || (maxM >= 256 && minK >= 512 && (ws || tiles >= 128))) {
+    if (A_KM || (maxM >= 256 && minK >= 512 && (ws || tiles >= 128)) || (g_tile_variant >= 4 && maxM >= 128)) {
       GemmBatch gt = gb;
       switch (g_tile_variant) {
         case 1: launch_tile2<64, 64, 64, A_KM, B_KN>(gt, count, s); break;
         case 2: launch_tile2<128, 64, 32, A_KM, B_KN>(gt, count, s); break;
         case 3: launch_tile2<128, 64, 64, A_KM, B_KN>(gt, count, s); break;
+        case 4: launch_tile2<64, 32, 64, A_KM, B_KN, 8>(gt, count, s); break;
+        case 5: launch_tile2<128, 32, 64, A_KM, B_KN, 8>(gt, count, s); break;
+        case 6: launch_tile2<64, 64, 64, A_KM, B_KN, 8>(gt, count, s); break;
+        case 7: launch_tile2<32, 32, 64, A_KM, B_KN, 4>(gt, count, s); break;
         default: launch_tile2<64, 64, 32, A_KM, B_KN>(gt, count, s); break;
       }
       return;

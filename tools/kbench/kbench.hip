@@ -387,6 +387,34 @@ int main(int argc, char** argv) {
     timeit("unfused 2x lnsilu M64 200-200-1024", [&](hipStream_t st) { gemm_launch(G_NT, AM_LNSILU, &g1, 1, st);
                                                                        gemm_launch(G_NT, AM_LNSILU, &g2, 1, st); }, s);
   }
+  // B = 256 chain products: current routing (variant 0) against the 8-wave
+  // tile variants, without and with split-K scratch
+  {
+    float* skw = frand((size_t)8 * 256 * 2048);
+    for (int var : {0, 4, 5, 6, 7}) {
+      dr_debug_tile_variant(var);
+      for (int sk = 0; sk < 2; ++sk) {
+        if (var == 0 && sk) continue;
+        auto prep = [&](GemmArgs g) {
+          if (sk) { g.splitk_ws = skw; g.splitk_floats = 8LL * 256 * 2048; }
+          return g;
+        };
+        GemmArgs s1[2] = {prep(nt_(B, 1027, 1800)), prep(nt_(B, 600, 1800))};
+        snprintf(buf, sizeof buf, "tv%d%s BPTT gZ+gH N1027+600 K1800", var, sk ? " sk" : "");
+        timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, s1, 2, st); }, s);
+        GemmArgs s2[3] = {prep(nt_(B, 200, 1624)), prep(nt_(B, 200, 1624)), prep(nt_(B, 200, 1624))};
+        snprintf(buf, sizeof buf, "tv%d%s heads L1 3x N200 K1624", var, sk ? " sk" : "");
+        timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, s2, 3, st); }, s);
+        GemmArgs s3 = prep(nt_(B, 1800, 600));
+        snprintf(buf, sizeof buf, "tv%d%s GRU gh N1800 K600", var, sk ? " sk" : "");
+        timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, &s3, 1, st); }, s);
+        GemmArgs s4 = prep(nt_(B, 200, 600));
+        snprintf(buf, sizeof buf, "tv%d%s prior L1 N200 K600", var, sk ? " sk" : "");
+        timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, &s4, 1, st); }, s);
+      }
+    }
+    dr_debug_tile_variant(0);
+  }
   // per-step shapes of the imagination / BPTT chain, both row-tile variants
   for (int var = 0; var < 5; ++var) {
     if (var == 1 || var == 2) continue;
