@@ -71,6 +71,7 @@ _sz = C.c_size_t
 _i = C.c_int
 _ll = C.c_longlong
 _f = C.c_float
+_d = C.c_double
 
 _SIGS = {
     "dr_last_error": (C.c_char_p, []),
@@ -112,7 +113,7 @@ _SIGS = {
     "dr_sqnorm": (_i, [_ll, fp, fp, fp]),
     "dr_sqnorm_multi": (_i, [_ll, fp, fp, fp, fp]),
     "dr_clip_stats": (_i, [_ll, fp, _ll, fp, _i, fp, fp, fp, fp, fp]),
-    "dr_adamw": (_i, [_ll, fp, fp, fp, fp, fp, _f, _f, _f, _f, _f, _f, fp, fp, fp, fp]),
+    "dr_adamw": (_i, [_ll, fp, fp, fp, fp, fp, _f, _d, _d, _d, _d, _d, fp, fp, fp, fp]),
     "dr_ema": (_i, [_ll, fp, fp, _f, _f, fp, fp]),
     "dr_nonfinite": (_i, [_ll, fp, fp, fp]),
     "dr_replay_gather": (_i, [_ll, _i, _i, _i, _i, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp]),

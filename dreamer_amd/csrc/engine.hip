@@ -154,7 +154,7 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
       float* hn = w.hb[hb];
       hb ^= 1;
       DR_TRY(gru_onehot(d, wm, B, w.idx, actions + ai * act_st, act_sb, h, Hd, hn, Hd, w.wt, nullptr,
-                        nullptr, nullptr, nullptr, s, z_out, L));
+                        nullptr, nullptr, nullptr, s, z_out, L, w.gh));
       h = hn;
     }
     // latent_mapper.0 on cat(features, h): feature part precomputed in feat[t]
@@ -316,7 +316,7 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
     float* z_n = latents + (long long)(t + 1) * L;
     // WorldModel.imagine_step (WorldModel.py:72-77)
     DR_TRY(gru_onehot(d, wm, B, w.idx[t & 1], actions + (long long)t * A, ldA, h_t, ldH, h_n, ldH, w.wt,
-                      tp.r + hb, tp.u + hb, tp.n + hb, tp.ghn + hb, s, z_t, ldL));
+                      tp.r + hb, tp.u + hb, tp.n + hb, tp.ghn + hb, s, z_t, ldL, w.gh));
     float* p1 = tp.pre1p + (long long)t * B * d->prior_h1;
     float* p2 = tp.pre2p + (long long)t * B * d->prior_h2;
     DR_TRY(run(G_NT, AM_PLAIN, lin(B, d->prior_h1, Hd, h_n, ldH, wm->prior.l0.w, Hd, wm->prior.l0.b, p1, d->prior_h1), s));

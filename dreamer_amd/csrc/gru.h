@@ -19,6 +19,7 @@ struct alignas(16) GruArgs {
   float* hout;          // row stride ldo; must NOT alias h (other workgroups still read h)
   long long ldo;
   float *sr, *su, *sn, *sghn;  // optional saves [B][Hd] for the backward
+  float* gh_ws;                // optional [B][3*Hd] scratch: enables the split path at B >= 128
 };
 
 int op_gru_fused(const GruArgs& g, hipStream_t s);

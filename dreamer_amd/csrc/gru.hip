@@ -9,6 +9,7 @@
 // gh runs on the exact-f32 MFMA: a workgroup owns 16 batch rows x 16 hidden
 // units (3 gate column tiles of W_hh) and splits K over 8 waves.
 #include "gru.h"
+#include "gemm.h"
 
 #include <algorithm>
 
@@ -327,6 +328,169 @@ __global__ __launch_bounds__(512) void k_gru_fused(GruArgs ga) {
   DR_TS(dr_tbuf_gru, 5);
 }
 
+// ---------------------------------------------------------------------------
+// Split GRU step for larger batches (B >= 128 with caller scratch): the hidden
+// product gh = h W_hh^T + b_hh runs as a tile-GEMM launch (gemm.hip: 32 x 32
+// tiles, W_hh read 8x at B = 256 instead of 16x by the fused kernel's 16-row
+// tiles), then k_gru_gates gathers gi and applies the gates.  Workgroup =
+// 8 rows x 32 hidden units x 3 gates; thread (row, gate, 4 units): the 8
+// threads of a (row, gate) read one full 128-B line of every gathered W_ih^T
+// row (the fused kernel reads 64-B halves), and unit slices map to XCDs so
+// each XCD's L2 holds its columns of W_ih^T.  gi keeps the fused kernel's
+// summation order (groups ascending, then actions, then + b_ih): identical
+// gi; gh differs from the fused kernel's in f32 summation order only.
+// ---------------------------------------------------------------------------
+#define GG_ROWS 8
+#define GG_UNITS 32
+#define GG_NT (GG_ROWS * 3 * (GG_UNITS / 4))  // 192 threads
+
+template <int GB>  // gathered rows issued per batch (VGPRs vs round trips)
+__global__ __launch_bounds__(GG_NT) void k_gru_gates(GruArgs ga) {
+  __shared__ GruArgs g;
+  dr_stage_args(ga, g, threadIdx.x);
+  const int Hd = dr_uni(g.Hd), B = dr_uni(g.B);
+  const int R = dr_uni(g.R), C = dr_uni(g.C), A = dr_uni(g.A), L = R * C;
+  const int tiles_j = (Hd + GG_UNITS - 1) / GG_UNITS, tiles_m = (B + GG_ROWS - 1) / GG_ROWS;
+  const int lt = dr_xcd_tile(blockIdx.x, tiles_j * tiles_m);
+  if (lt < 0) return;
+  const int tj = lt / tiles_m, tm = lt - tj * tiles_m;
+  const int m0 = tm * GG_ROWS, j0 = tj * GG_UNITS;
+  const int tid = threadIdx.x;
+  __shared__ int s_idx[GG_ROWS][GRU_MAXR];
+  __shared__ float s_zv[GG_ROWS][GRU_MAXR];
+  __shared__ float4 s_gi[GG_ROWS][3][GG_UNITS / 4];
+  // round trip 1: the tile's indices / straight-through values, and (threads
+  // 0-63, one float4 of 4 units each for the gate phase) gh of the 3 gates
+  // and h -- independent of the gather, issued with it
+  const int gm = m0 + (tid >> 3), gj = j0 + 4 * (tid & 7);
+  const bool gate_thr = tid < GG_ROWS * (GG_UNITS / 4) && gm < B && gj < Hd;
+  const float* hp = dr_uni(g.h);
+  const float* gh = hp ? dr_uni(g.gh_ws) : nullptr;
+  float4 ghv[3], hv = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+    ghv[t] = gh ? dr_ld4(gh, gate_thr ? (unsigned)(gm * 3 * Hd + t * Hd + gj) : 0u)
+                : dr_ld4(dr_uni(g.b_hh), gate_thr ? (unsigned)(t * Hd + gj) : 0u);
+  if (hp) hv = dr_ld4(hp, gate_thr ? (unsigned)(gm * (int)g.ldh + gj) : 0u);
+  for (int x = tid; x < GG_ROWS * GRU_MAXR; x += GG_NT) {
+    const int ml = x / GRU_MAXR, u = x - ml * GRU_MAXR, m = m0 + ml;
+    const bool ok = m < B && u < R;
+    const int iv = ok ? dr_g(g.idx)[m * R + u] : 0;
+    const float zv = ok ? dr_g(g.zval)[m * R + u] : 0.f;
+    s_idx[ml][u] = iv;
+    s_zv[ml][u] = zv;
+  }
+  __syncthreads();
+  {
+    // round trip 2: every gathered W_ih^T row piece of this thread at once
+    const int j8 = tid & 7, t = (tid >> 3) % 3, ml = tid / 24;
+    const int m = m0 + ml, jj = j0 + 4 * j8;
+    const bool live = m < B && jj < Hd;
+    const float* wt = dr_uni(g.wt);
+    const unsigned ldw = 3u * Hd;
+    const unsigned col = (unsigned)(t * Hd + jj);
+    const float* act = dr_uni(g.a);
+    const int lda = dr_uni((int)g.lda);
+    float av[GRU_MAXA];
+    float4 wa[GRU_MAXA];
+#pragma unroll
+    for (int i = 0; i < GRU_MAXA; ++i) {
+      const bool ok = live && i < A;
+      av[i] = dr_ld1(act, ok ? (unsigned)(m * lda + i) : 0u);
+      wa[i] = dr_ld4(wt, ok ? (unsigned)(L + i) * ldw + col : 0u);
+    }
+    const float4 bb = dr_ld4(dr_uni(g.b_ih), live ? col : 0u);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool dense = false;
+#pragma unroll
+    for (int ub = 0; ub < GRU_MAXR; ub += GB) {
+      float4 w[GB];
+#pragma unroll
+      for (int q = 0; q < GB; ++q) {
+        const int u = ub + q;
+        const int iv = s_idx[ml][u];
+        const bool ok = live && u < R && iv >= 0;
+        w[q] = dr_ld4(wt, ok ? (unsigned)(u * C + iv) * ldw + col : 0u);
+      }
+#pragma unroll
+      for (int q = 0; q < GB; ++q) {
+        const int u = ub + q;
+        if (u < R) {
+          const float zv = s_zv[ml][u];
+          dense = dense || s_idx[ml][u] < 0;
+          v.x = fmaf(w[q].x, zv, v.x);
+          v.y = fmaf(w[q].y, zv, v.y);
+          v.z = fmaf(w[q].z, zv, v.z);
+          v.w = fmaf(w[q].w, zv, v.w);
+        }
+      }
+    }
+    if (dense && live) {  // groups with several non-zero classes: every class (as the fused kernel)
+      const float* zr = g.z + (long long)m * g.ldz;
+      for (int u = 0; u < R; ++u) {
+        if (s_idx[ml][u] >= 0) continue;
+        for (int c = 0; c < C; ++c) {
+          const float zc = zr[u * C + c];
+          const float4 wc = dr_ld4(wt, (unsigned)(u * C + c) * ldw + col);
+          v.x = fmaf(wc.x, zc, v.x);
+          v.y = fmaf(wc.y, zc, v.y);
+          v.z = fmaf(wc.z, zc, v.z);
+          v.w = fmaf(wc.w, zc, v.w);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < GRU_MAXA; ++i) {
+      if (i < A) {
+        v.x = fmaf(wa[i].x, av[i], v.x);
+        v.y = fmaf(wa[i].y, av[i], v.y);
+        v.z = fmaf(wa[i].z, av[i], v.z);
+        v.w = fmaf(wa[i].w, av[i], v.w);
+      }
+    }
+    s_gi[ml][t][j8] = make_float4(v.x + bb.x, v.y + bb.y, v.z + bb.z, v.w + bb.w);
+  }
+  __syncthreads();
+  // gates (torch gru_cell op order) for 4 units per thread, float4 stores
+  if (gate_thr) {
+    const int ml = tid >> 3, j8 = tid & 7;
+    const float4 gr = s_gi[ml][0][j8], gu = s_gi[ml][1][j8], gn = s_gi[ml][2][j8];
+    const float gi_r[4] = {gr.x, gr.y, gr.z, gr.w}, gi_u[4] = {gu.x, gu.y, gu.z, gu.w};
+    const float gi_n[4] = {gn.x, gn.y, gn.z, gn.w};
+    const float gh_r[4] = {ghv[0].x, ghv[0].y, ghv[0].z, ghv[0].w};
+    const float gh_u[4] = {ghv[1].x, ghv[1].y, ghv[1].z, ghv[1].w};
+    const float gh_n[4] = {ghv[2].x, ghv[2].y, ghv[2].z, ghv[2].w};
+    const float h4[4] = {hv.x, hv.y, hv.z, hv.w};
+    float ho[4], ro[4], uo[4], no[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float rr = 1.0f / (1.0f + expf(-(gh_r[e] + gi_r[e])));
+      const float uu = 1.0f / (1.0f + expf(-(gh_u[e] + gi_u[e])));
+      const float nn = tanhf(gi_n[e] + gh_n[e] * rr);
+      ho[e] = (h4[e] - nn) * uu + nn;
+      ro[e] = rr;
+      uo[e] = uu;
+      no[e] = nn;
+    }
+    dr_st4(g.hout, (unsigned)(gm * (int)g.ldo + gj), make_float4(ho[0], ho[1], ho[2], ho[3]));
+    if (g.sr) {
+      const unsigned o = (unsigned)(gm * Hd + gj);
+      dr_st4(g.sr, o, make_float4(ro[0], ro[1], ro[2], ro[3]));
+      dr_st4(g.su, o, make_float4(uo[0], uo[1], uo[2], uo[3]));
+      dr_st4(g.sn, o, make_float4(no[0], no[1], no[2], no[3]));
+      dr_st4(g.sghn, o, ghv[2]);
+    }
+  }
+}
+
+#ifdef DR_PHASE_TIMING  // microbenchmark knob (tools/kbench), not in the product library
+static int g_gates_batch = 8;
+extern "C" void dr_debug_gates_batch(int v) { g_gates_batch = v; }
+static int gates_batch() { return g_gates_batch; }
+#else
+static int gates_batch() { return 8; }
+#endif
+
 int op_gru_fused(const GruArgs& g, hipStream_t s) {
   if (g.R > GRU_MAXR || g.A > GRU_MAXA || g.B <= 0 || g.Hd <= 0 || g.Hd % 4 != 0 || g.ldh % 4 != 0 ||
       (((uintptr_t)g.h | (uintptr_t)g.w_hh | (uintptr_t)g.wt | (uintptr_t)g.b_ih | (uintptr_t)g.zval |
@@ -336,10 +500,31 @@ int op_gru_fused(const GruArgs& g, hipStream_t s) {
     return DR_E_INVALID;
   }
   const long long lim = 1LL << 30;
-  if ((long long)(g.R * g.C + g.A) * 3 * g.Hd >= lim || (long long)g.B * g.ldh >= lim ||
+  if ((long long)(g.R * g.C + g.A) * 3 * g.Hd >= lim || (long long)g.B * g.ldh >= lim || (long long)g.B * g.ldo >= lim ||
       3LL * g.Hd * g.Hd >= lim) {
     dr_set_error("gru_fused: operands exceed 32-bit offsets");
     return DR_E_INVALID;
+  }
+  if (g.gh_ws && g.B >= 128 && ((uintptr_t)g.gh_ws | (uintptr_t)g.hout | (uintptr_t)g.sr | (uintptr_t)g.su |
+                                 (uintptr_t)g.sn | (uintptr_t)g.sghn) % 16 == 0 && g.ldo % 4 == 0) {
+    // split path: hidden product on the tile GEMM, then gather + gates
+    if (g.h) {
+      GemmArgs p = gemm_args();
+      p.M = g.B; p.N = 3 * g.Hd; p.K = g.Hd;
+      p.A = g.h; p.lda = g.ldh; p.ksplitA = g.Hd;
+      p.W = g.w_hh; p.ldb = g.Hd;
+      p.bias = g.b_hh;
+      p.Y = g.gh_ws; p.ldy = 3 * g.Hd;
+      DR_TRY(gemm_launch(G_NT, AM_PLAIN, &p, 1, s));
+    }
+    const int tiles = ((g.Hd + GG_UNITS - 1) / GG_UNITS) * ((g.B + GG_ROWS - 1) / GG_ROWS);
+    switch (gates_batch()) {
+      case 4: hipLaunchKernelGGL(k_gru_gates<4>, dim3(dr_xcd_grid(tiles)), dim3(GG_NT), 0, s, g); break;
+      case 16: hipLaunchKernelGGL(k_gru_gates<16>, dim3(dr_xcd_grid(tiles)), dim3(GG_NT), 0, s, g); break;
+      case 32: hipLaunchKernelGGL(k_gru_gates<32>, dim3(dr_xcd_grid(tiles)), dim3(GG_NT), 0, s, g); break;
+      default: hipLaunchKernelGGL(k_gru_gates<8>, dim3(dr_xcd_grid(tiles)), dim3(GG_NT), 0, s, g); break;
+    }
+    return dr_check_launch("gru_gates");
   }
   const int tiles = ((g.Hd + 15) / 16) * ((g.B + 15) / 16);
   hipLaunchKernelGGL(k_gru_fused, dim3(dr_xcd_grid(tiles)), dim3(512), 0, s, g);

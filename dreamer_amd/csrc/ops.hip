@@ -1075,14 +1075,14 @@ extern "C" int dr_clip_stats(long long na, const float* ga, long long nb, const 
 
 // prelude: step += 1 (unless skipped), bias corrections in double like
 // torch's python scalars (adam.py: bias_correction1 = 1 - beta1**step ...)
-__global__ void k_adamw_prelude(int* step, float* hyper, float lr, float b1, float b2, const int* skip) {
+__global__ void k_adamw_prelude(int* step, float* hyper, double lr, double b1, double b2, const int* skip) {
   if (skip && *skip) return;
   const int st = *step + 1;
   *step = st;
-  const double bc1 = 1.0 - pow((double)b1, (double)st);
-  const double bc2 = 1.0 - pow((double)b2, (double)st);
-  hyper[0] = (float)((double)lr / bc1);  // step_size
-  hyper[1] = (float)sqrt(bc2);           // bias_correction2_sqrt
+  const double bc1 = 1.0 - pow(b1, (double)st);
+  const double bc2 = 1.0 - pow(b2, (double)st);
+  hyper[0] = (float)(lr / bc1);  // step_size
+  hyper[1] = (float)sqrt(bc2);   // bias_correction2_sqrt
 }
 
 __global__ void k_adamw(long long n, float* p, float* g, float* m, float* v, const float* sqnorm,
@@ -1109,15 +1109,18 @@ __global__ void k_adamw(long long n, float* p, float* g, float* m, float* v, con
 }
 
 extern "C" int dr_adamw(long long n, float* p, float* g, float* m, float* v, const float* sqnorm,
-                        float max_norm, float lr, float b1, float b2, float eps, float wd, int* step, float* hyper,
-                        const int* skip, hipStream_t stream) {
+                        float max_norm, double lr, double b1, double b2, double eps, double wd, int* step,
+                        float* hyper, const int* skip, hipStream_t stream) {
   if (n <= 0) return DR_OK;
   hipLaunchKernelGGL(k_adamw_prelude, dim3(1), dim3(1), 0, stream, step, hyper, lr, b1, b2, skip);
   DR_TRY(dr_check_launch("adamw_prelude"));
-  const float keep = (float)(1.0 - (double)lr * (double)wd);
-  const float omb1 = (float)(1.0 - (double)b1), omb2 = (float)(1.0 - (double)b2);
+  // torch's python-scalar math: 1 - lr*wd, 1 - beta in double, then one
+  // rounding to f32 where the tensor op consumes them (a beta passed as f32
+  // first would give 1 - 0.999f = 0.00099998713: 1.3e-5 off in exp_avg_sq)
+  const float keep = (float)(1.0 - lr * wd);
+  const float omb1 = (float)(1.0 - b1), omb2 = (float)(1.0 - b2);
   hipLaunchKernelGGL(k_adamw, dim3(blocks_for(n, 256)), dim3(256), 0, stream, n, p, g, m, v, sqnorm, max_norm, keep,
-                     omb1, b2, omb2, hyper, eps, skip);
+                     omb1, (float)b2, omb2, hyper, (float)eps, skip);
   return dr_check_launch("adamw");
 }
 

@@ -251,10 +251,11 @@ int dr_clip_stats(long long na, const float* ga, long long nb, const float* gb, 
  * clip = min(1, max_norm/(sqrt(*sqnorm)+1e-6)) (sqnorm NULL: no clip).  The
  * step counter lives on the device: a prelude increments *step and writes
  * hyper[0] = lr/(1-b1^step), hyper[1] = sqrt(1-b2^step) (double math, like
- * torch's python scalars).  g is scaled in place by clip (as clip_grad_norm_
- * does).  Everything is skipped when *skip != 0. */
+ * torch's python scalars; the hyperparameters are doubles, like the python
+ * floats torch.optim.AdamW computes 1 - beta etc. from).  g is scaled in place
+ * by clip (as clip_grad_norm_ does).  Everything is skipped when *skip != 0. */
 int dr_adamw(long long n, float* p, float* g, float* m, float* v, const float* sqnorm, float max_norm,
-             float lr, float b1, float b2, float eps, float wd, int* step, float* hyper, const int* skip,
+             double lr, double b1, double b2, double eps, double wd, int* step, float* hyper, const int* skip,
              hipStream_t stream);
 int dr_ema(long long n, float* target, const float* src, float keep, float tau, const int* skip,
            hipStream_t stream);

@@ -21,6 +21,7 @@ extern "C" int dr_debug_tbuf_gemm(long long* out, int n);
 extern "C" void dr_debug_tile_variant(int v);
 extern "C" void dr_debug_skinny_variant(int v);
 extern "C" void dr_debug_tile_wgs(int v);
+extern "C" void dr_debug_gates_batch(int v);
 
 // one more launch, then the per-phase times of wave 0 of each workgroup
 // (relative to its own start) averaged over the workgroups that wrote them
@@ -330,6 +331,22 @@ int main(int argc, char** argv) {
   GruArgs gs = ga;
   gs.sr = save; gs.su = save + B * Hd; gs.sn = save + 2 * B * Hd; gs.sghn = save + 3 * B * Hd;
   timeit("gru_fused B64 H600 R32 (saves)", [&](hipStream_t st) { op_gru_fused(gs, st); }, s);
+  {  // split path (tile-GEMM hidden product + gather/gates kernel) by gather batch
+    float* ghw = frand((size_t)B * 3 * Hd);
+    for (int gbv : {4, 8, 16, 32}) {
+      dr_debug_gates_batch(gbv);
+      GruArgs gsp = gs;
+      gsp.gh_ws = ghw;
+      char nm[96];
+      snprintf(nm, sizeof nm, "gru split B%d (saves) gather batch %d", B, gbv);
+      timeit(nm, [&](hipStream_t st) { op_gru_fused(gsp, st); }, s);
+      GruArgs gz = gsp;
+      gz.h = nullptr;  // gates kernel alone (no hidden product)
+      snprintf(nm, sizeof nm, "gru split B%d gates only, batch %d", B, gbv);
+      timeit(nm, [&](hipStream_t st) { op_gru_fused(gz, st); }, s);
+    }
+    dr_debug_gates_batch(8);
+  }
   GruArgs gn = ga;
   gn.h = nullptr;
   timeit("gru_fused h=NULL (gather only)", [&](hipStream_t st) { op_gru_fused(gn, st); }, s);

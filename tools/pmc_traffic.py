@@ -12,7 +12,7 @@ import glob
 import json
 import sys
 
-ENCODER = ("k_conv_nhwc", "k_frames_nhwc4")
+ENCODER = ("k_conv_nhwc", "k_frames_nhwc4", "k_conv1_direct", "k_enc12_bf16", "k_conv_bf16", "k_conv1_bf16")
 
 
 def load(d, counter):
@@ -41,7 +41,7 @@ def main():
         print(f"{tot / 1e6:14.3f} {fb / 1e6:9.3f} {wb / 1e6:9.3f} {n:10d}  {k[:110]}")
     enc = [(tot, n, k) for tot, fb, wb, n, k in rows if any(e in k for e in ENCODER)]
     enc_bytes = sum(t for t, n, k in enc)  # one dispatch of each per epoch
-    print(f"# encoder group (conv stack + frame conversion), bytes per epoch: {enc_bytes:.0f}")
+    print(f"# encoder group (conv stack + frame conversion; the feature-projection GEMM excluded), bytes per epoch: {enc_bytes:.0f}")
     if out_json:
         json.dump({"encoder_bytes_per_epoch": enc_bytes, "kernels": {k: t for t, n, k in enc},
                    "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, FETCH_SIZE x2 (gfx950)"},
