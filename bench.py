@@ -313,6 +313,33 @@ def make_dreamer(cfg, dev, B, S, H, res, ac_epochs, world, rank, group, precisio
     return c, d
 
 
+VEC_OBS_DIM = 24  # configs[4] proprioceptive vector observations (a walker-like state size)
+
+
+def make_vector_dreamer(cfg, dev, B, S, H, world, rank, group):
+    """BASELINE configs[4]: vector observations (observation_dims=[D], MLP
+    encoder / decoder, include/dreamer_hip.h dr_dims.obs_dim), synthetic f32
+    replay (N(0,1) observations, U(-1,1) actions, symlog N(0,1) rewards)."""
+    from dreamer_amd import Dreamer
+    from dreamer_amd.engine import ImaginationEngine
+    c = dict(cfg)
+    n = max(8192, 8 * S)
+    c.update(batch_size=B, sequence_length=S, horizon=H, observation_dims=[VEC_OBS_DIM], AC_epochs=1, buffer_size=n)
+    torch.manual_seed(0)
+    d = Dreamer(c, dev)
+    rng = np.random.default_rng(0)
+    rew = rng.standard_normal(n).astype(np.float32)
+    d.buffer.load_arrays(rng.standard_normal((n, VEC_OBS_DIM)).astype(np.float32),
+                         rng.uniform(-1, 1, (n, c["action_dims"])).astype(np.float32),
+                         np.sign(rew) * np.log1p(np.abs(rew)), np.ones(n, np.float32))
+    d.buffer._mirror()
+    if world > 1:
+        d.world = (rank, world, group)
+        d.world_model.set_data_parallel(rank, world, group)
+    d._engine = ImaginationEngine(d, B=B, world=(rank, world, group) if world > 1 else None)
+    return c, d
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -425,6 +452,17 @@ def main():
                           "and the projection as bf16 implicit GEMMs (f32 accumulate); the imagination / update "
                           "chain stays f32 (tests/test_gpu_bf16.py states the tolerances)")
             secondary["bf16_perf_mode"] = bf
+        # BASELINE configs[4]: vector observations, B = 4096 H = 15 (S = 64 assumed)
+        _, dv = make_vector_dreamer(CAR_RACER, dev, 4096, 64, 15, world, rank, group)
+        kv = max(3, args.steps // 4)
+        elv, (lav, lcv) = time_train_agent(dv, kv, 2)
+        secondary["configs4_vector_B4096"] = {
+            "value": round(world * 4096 * 15 * kv / elv, 1), "unit": "imagined latent-steps/s",
+            "ms_per_epoch": round(elv / kv * 1e3, 4), "dtype": "f32", "obs_dim": VEC_OBS_DIM,
+            "losses": {"actor": lav, "critic": lcv},
+            "note": "BASELINE configs[4] (B=4096/GPU, H=15, S=64): observation_dims=[24], MLP encoder instead of "
+                    "the conv stack (no reference counterpart), Dreamer.train_Agent() AC_epochs=1"}
+        del dv
     wm = None
     if args.wm_steps > 0:
         wm_s, wm_gpu_s, wm_loss = bench_wm(d, B, args.wm_steps, 2)

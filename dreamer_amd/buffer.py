@@ -17,7 +17,10 @@ from .utils import symlog_np
 
 class Buffer:
     def __init__(self, buffer_size, sequence_length, action_size, observation_dims, device="cpu"):
-        self.observation_buffer = np.zeros((buffer_size, 3, *observation_dims), dtype=np.uint8)
+        # observation_dims = [D]: f32 vector observations (BASELINE configs[4]); else u8 frames
+        self.vector = len(tuple(observation_dims)) == 1
+        self.observation_buffer = np.zeros((buffer_size, observation_dims[0]), dtype=np.float32) if self.vector \
+            else np.zeros((buffer_size, 3, *observation_dims), dtype=np.uint8)
         self.action_buffer = np.zeros((buffer_size, action_size), dtype=np.float32)
         self.reward_buffer = np.zeros((buffer_size, 1), dtype=np.float32)
         self.continue_buffer = np.zeros((buffer_size, 1), dtype=np.float32)
@@ -32,7 +35,7 @@ class Buffer:
     # ---- host side (Buffer.py:19-30) -----------------------------------------
     def add_to_buffer(self, observation, action, reward, continue_):
         i = self.next_idx
-        self.observation_buffer[i] = np.array(observation, dtype=np.uint8)
+        self.observation_buffer[i] = np.array(observation, dtype=self.observation_buffer.dtype)
         self.action_buffer[i] = np.array(action, dtype=np.float32)
         self.continue_buffer[i] = np.array(continue_, dtype=np.float32)
         self.reward_buffer[i] = symlog_np(np.array(reward, dtype=np.float32))
@@ -72,7 +75,8 @@ class Buffer:
             raise RuntimeError("dreamer_amd: the replay device mirror needs a GPU device")
         if self._dev is None:
             self._dev = dict(
-                frames=torch.zeros(self.observation_buffer.shape, dtype=torch.uint8, device=self.device),
+                frames=torch.zeros(self.observation_buffer.shape, dtype=torch.float32 if self.vector else torch.uint8,
+                                   device=self.device),
                 actions=torch.zeros(self.action_buffer.shape, device=self.device),
                 rewards=torch.zeros(self.reward_buffer.shape, device=self.device),
                 continues=torch.zeros(self.continue_buffer.shape, device=self.device))
@@ -93,9 +97,10 @@ class Buffer:
         return (m["frames"].data_ptr(), self.capacity)
 
     def frames_struct(self, starts_dev):
-        """dr_frames reading the warm-start frames straight from the u8 ring."""
+        """dr_frames reading the warm-start frames straight from the u8 ring
+        (vector observations: the f32 ring, dr_dims.obs_dim)."""
         m = self._mirror()
-        return L.dr_frames(L.ptr(m["frames"]), self.capacity, L.ptr(starts_dev), None, 0, 0, 1)
+        return L.dr_frames(L.ptr(m["frames"]), self.capacity, L.ptr(starts_dev), None, 0, 0, 0 if self.vector else 1)
 
     def gather_actions(self, starts_dev, out):
         """out[b][s][:] = action at slot (starts[b]+s) % capacity."""
@@ -117,6 +122,9 @@ class Buffer:
         m = self._mirror()
         dev = self.device
         st = torch.as_tensor(starts, dtype=torch.int64).to(dev)
+        if self.vector:  # f32 rows: a plain device gather
+            idx = (st[:, None] + torch.arange(S, device=dev)[None, :]) % self.capacity
+            return m["frames"][idx], m["actions"][idx], m["rewards"][idx], m["continues"][idx], S
         fe = int(np.prod(self.observation_buffer.shape[1:]))
         A = self.action_buffer.shape[1]
         obs = torch.empty(batch_size, S, *self.observation_buffer.shape[1:], device=dev)

@@ -501,6 +501,7 @@ extern "C" int dr_act_step(const dr_dims* d, const dr_world_model* wm, const dr_
                            float* sigma_out, float* logits_out, void* ws, size_t ws_bytes, hipStream_t s) {
   DR_REQUIRE(d && wm && ac && frame && h && z_out && h_out && a_out && mu_out && sigma_out && ws, "null argument");
   DR_REQUIRE(!has_prev || (z_prev && a_prev), "has_prev needs z_prev and a_prev");
+  DR_REQUIRE(d->obs_dim == 0, "dr_act_step: pixel observations only (vector observations use the unfused path)");
   const int F = 4 * d->enc_f2 * (d->img_h / 16) * (d->img_w / 16), L = d->rows * d->cols;
   // the stage helpers' register batches (KJ) and the LDS staging are sized for the
   // CarRacing encoder (Dreamer.py:20-64 config); other shapes use the unfused calls

@@ -16,6 +16,16 @@ struct EncWs {
 // bf16 mode stores activations / repacked weights as bf16 (2 bytes): the same
 // carve with half-size regions (a4 holds the NCHW flatten, x0 is unused)
 static void enc_carve(Carve& c, const dr_dims* d, int n, EncWs& w) {
+  if (d->obs_dim > 0) {  // vector observations: X [n][D], two MLP activations [n][F]
+    const int F = enc_feat_dim(d);
+    memset(&w, 0, sizeof(w));
+    w.x0 = c.f((long long)n * d->obs_dim);
+    w.a1 = c.f((long long)n * F);
+    w.a4 = c.f((long long)n * F);
+    w.sk_n = splitk_floats(n, d->enc_hidden);
+    w.sk = c.f(w.sk_n);
+    return;
+  }
   const bool bf = d->precision == DR_PREC_BF16;
   const int c1 = d->enc_f1, c2 = d->enc_f2, c3 = 2 * d->enc_f2, c4 = 4 * d->enc_f2;
   const long long p0 = (long long)d->img_h * d->img_w, p1 = p0 / 4, p2 = p1 / 4, p3 = p2 / 4, p4 = p3 / 4;
@@ -65,6 +75,28 @@ static int encoder_bf16(const dr_dims* d, const dr_world_model* wm, const dr_fra
 extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, const dr_frames* src, int B, int T,
                                    float* feat, void* ws, size_t ws_bytes, hipStream_t s) {
   DR_REQUIRE(d && wm && src && feat && B > 0 && T > 0, "null argument or empty batch");
+  if (d->obs_dim > 0) {
+    // vector observations (dr_dims.obs_dim): Linear-SiLU x2, then the feature
+    // columns of latent_mapper.0 -- the MLP stand-in for VAE.py:57-75's convs
+    DR_REQUIRE(d->enc_f2 > 0 && d->obs_dim % 4 == 0, "vector observations: obs_dim % 4 == 0 required");
+    const int n = B * T, F = enc_feat_dim(d), D = d->obs_dim;
+    Carve c(ws);
+    EncWs w;
+    enc_carve(c, d, n, w);
+    WS_CHECK(c, ws_bytes);
+    DR_TRY(op_vec_gather(n, B, D, src, w.x0, s));
+    GemmArgs g1 = lin(n, F, D, w.x0, D, wm->conv[0].w, D, wm->conv[0].b, w.a1, F);
+    g1.act = 1;
+    DR_TRY(run(G_NT, AM_PLAIN, g1, s));
+    GemmArgs g2 = lin(n, F, F, w.a1, F, wm->conv[1].w, F, wm->conv[1].b, w.a4, F);
+    g2.act = 1;
+    DR_TRY(run(G_NT, AM_PLAIN, g2, s));
+    GemmArgs gp = lin(n, d->enc_hidden, F, w.a4, F, wm->map0.w, F + d->hidden, wm->map0.b, feat, d->enc_hidden);
+    float* sk = w.sk;
+    long long skn = w.sk_n;
+    give_splitk(gp, sk, skn);
+    return run(G_NT, AM_PLAIN, gp, s);
+  }
   DR_REQUIRE(d->img_h % 16 == 0 && d->img_w % 16 == 0, "image size must be a multiple of 16");
   DR_REQUIRE(d->enc_f1 % 4 == 0 && d->enc_f2 % 4 == 0, "encoder filter counts must be multiples of 4");
   DR_REQUIRE(d->precision == DR_PREC_FP32 || d->precision == DR_PREC_BF16, "precision must be DR_PREC_FP32/BF16");
@@ -132,7 +164,7 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
   obs_carve(c, d, B, w);
   WS_CHECK(c, ws_bytes);
   const int L = latent(d), Hd = d->hidden, eh = d->enc_hidden;
-  const int F = 4 * d->enc_f2 * (d->img_h / 16) * (d->img_w / 16);
+  const int F = enc_feat_dim(d);
   // W_ih^T for the one-hot gather of the fused GRU (weights are fixed for the
   // call); only needed when a GRU step runs (an encode-only call passes a
   // world model without GRU weights)

@@ -59,6 +59,11 @@ static inline int zero(float* p, long long n, hipStream_t s) {
 }
 
 static inline int latent(const dr_dims* d) { return d->rows * d->cols; }
+// encoder feature width F (latent_mapper.0 input minus h): the flattened conv
+// stack, or the vector-observation MLP's width 4*enc_f2 (dr_dims.obs_dim > 0)
+static inline int enc_feat_dim(const dr_dims* d) {
+  return d->obs_dim > 0 ? 4 * d->enc_f2 : 4 * d->enc_f2 * (d->img_h / 16) * (d->img_w / 16);
+}
 
 // Y[M][N] = A[M][K] W^T + b  (torch Linear), A row stride lda
 static inline GemmArgs lin(int M, int N, int K, const float* A, long long lda, const float* W, long long ldw,

@@ -52,3 +52,7 @@ int op_actor_head_bwd(int M, int A, const float* g_a, long long ldga, const floa
 int op_conv_repack(int cout, int cin, const float* w, float* wr, hipStream_t s);
 int op_fill(long long n, float* x, float v, hipStream_t s);
 int op_mean(int n, const float* x, float* out, hipStream_t s);
+
+// Vector observations (dr_dims.obs_dim = D > 0): frame f = t*nb + b of `src`
+// (f32 ring rows [cap][D] or strided f32 obs) -> X[f][D]
+int op_vec_gather(int n, int nb, int D, const dr_frames* src, float* X, hipStream_t s);

@@ -1221,3 +1221,34 @@ extern "C" int dr_rng_advance(unsigned long long* rng, unsigned long long delta,
   hipLaunchKernelGGL(k_rng_advance, dim3(1), dim3(1), 0, stream, rng, delta);
   return dr_check_launch("rng_advance");
 }
+
+// ---------------------------------------------------------------------------
+// vector observations (BASELINE configs[4]): gather the window rows of the
+// f32 ring (Buffer.sample_sequences for D-float observations) time-major
+// ---------------------------------------------------------------------------
+__global__ void k_vec_gather(int n, int nb, int D, dr_frames src, float* __restrict__ X) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)n * D) return;
+  const long long f = i / D;
+  const int c = (int)(i - f * D);
+  const int b = (int)(f % nb), t = (int)(f / nb) + src.t0;
+  float v;
+  if (src.ring) {
+    const float* ring = reinterpret_cast<const float*>(src.ring);
+    v = ring[((src.starts[b] + t) % src.ring_cap) * D + c];
+  } else {
+    v = src.obs[(long long)b * src.stride_b + (long long)t * src.stride_t + c];
+  }
+  X[i] = v;
+}
+
+int op_vec_gather(int n, int nb, int D, const dr_frames* src, float* X, hipStream_t s) {
+  if (n <= 0) return DR_OK;
+  if (D <= 0 || nb <= 0 || (!src->ring && !src->obs) || (src->ring && (!src->starts || src->ring_cap <= 0))) {
+    dr_set_error("vec_gather: bad source (D=%d)", D);
+    return DR_E_INVALID;
+  }
+  const long long total = (long long)n * D;
+  hipLaunchKernelGGL(k_vec_gather, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, n, nb, D, *src, X);
+  return dr_check_launch("vec_gather");
+}

@@ -234,6 +234,27 @@ __global__ void k_silu(long long n, const float* __restrict__ x, float* __restri
   if (i < n) y[i] = dr_silu(x[i]);
 }
 
+// vector observations: decoder output mu (no Tanh) against the target rows,
+// squared error per row into part[row] (one part per frame for k_wm_stats)
+// and dL/dmu = coef[row] * (mu - x) (coef carries the 2 and the mask weights,
+// as CT_EPI_TANH_MSE's does before its (1 - mu^2)); a wave per row
+__global__ __launch_bounds__(256) void k_vec_mse(int M1, int D, const float* __restrict__ mu,
+                                                 const float* __restrict__ x, const float* __restrict__ coef,
+                                                 float* __restrict__ g, float* __restrict__ part) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M1) return;
+  const float cf = coef[row];
+  float sq = 0.f;
+  for (int c = lane; c < D; c += 64) {
+    const long long o = (long long)row * D + c;
+    const float err = mu[o] - x[o];
+    sq += err * err;
+    g[o] = cf * err;
+  }
+  sq = wave_sum(sq);
+  if (lane == 0) part[row] = sq;
+}
+
 static int blocks(long long n, int t) { return (int)((n + t - 1) / t); }
 
 // split-K scratch for one launch's problems (disjoint slices of the pool)
@@ -293,6 +314,7 @@ struct WmWs {
 struct WmDims {
   int B, T, M, M1, L, Hd, A, eh, nb, IH, IW, c1, c2, c3, c4, P16, F, d1, d2, C0, dh, Fd, ph1, ph2, rh1, rh2, ch1, ch2;
   long long p0, p1, p2, p3;
+  int Dv;  // vector observations (dr_dims.obs_dim): MLP encoder / decoder, no conv planes
 };
 static WmDims wm_dims(const dr_dims* d, int B, int T) {
   WmDims w;
@@ -305,6 +327,14 @@ static WmDims wm_dims(const dr_dims* d, int B, int T) {
   w.d1 = d->dec_f1; w.d2 = d->dec_f2; w.C0 = 4 * d->dec_f2; w.dh = d->dec_hidden; w.Fd = w.C0 * w.P16;
   w.ph1 = d->prior_h1; w.ph2 = d->prior_h2; w.rh1 = d->rew_h1; w.rh2 = d->rew_h2; w.ch1 = d->cont_h1; w.ch2 = d->cont_h2;
   w.p0 = (long long)w.IH * w.IW; w.p1 = w.p0 / 4; w.p2 = w.p0 / 16; w.p3 = w.p0 / 64;
+  w.Dv = d->obs_dim > 0 ? d->obs_dim : 0;
+  if (w.Dv) {  // widths of the MLP stand-ins (include/dreamer_hip.h, dr_dims.obs_dim)
+    w.IH = w.IW = 0;
+    w.P16 = 1;
+    w.F = w.c4;
+    w.Fd = w.C0;
+    w.p0 = w.p1 = w.p2 = w.p3 = 0;
+  }
   return w;
 }
 
@@ -314,6 +344,7 @@ static void mlp_bwd_carve(Carve& c, long long M1, int w1, int w2, MlpBwd& b) {
 }
 
 static long long wm_conv_scratch(const WmDims& D) {
+  if (D.Dv) return 0;  // vector observations: no convolution planes
   const int n = D.M, n1 = D.M1;
   long long m = 0;
   auto mx = [&](long long v) { if (v > m) m = v; };
@@ -336,8 +367,9 @@ static long long wm_conv_scratch(const WmDims& D) {
 static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
   const long long M = D.M, M1 = D.M1, B = D.B;
   const int L = D.L, Hd = D.Hd, A = D.A, eh = D.eh;
-  w.x0 = c.f(M * D.p0 * 4);
-  w.pre1 = c.f(M * D.p1 * D.c1); w.a1 = c.f(M * D.p1 * D.c1);
+  const long long Dv = D.Dv;
+  w.x0 = c.f(Dv ? M * Dv : M * D.p0 * 4);
+  w.pre1 = c.f(Dv ? M * D.F : M * D.p1 * D.c1); w.a1 = c.f(Dv ? M * D.F : M * D.p1 * D.c1);
   w.pre2 = c.f(M * D.p2 * D.c2); w.a2 = c.f(M * D.p2 * D.c2);
   w.pre3 = c.f(M * D.p3 * D.c3); w.a3 = c.f(M * D.p3 * D.c3);
   w.pre4 = c.f(M * D.F); w.a4 = c.f(M * D.F);
@@ -361,10 +393,12 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
   w.cp1 = c.f(M1 * D.ch1); w.cx1 = c.f(M1 * D.ch1); w.cp2 = c.f(M1 * D.ch2); w.cx2 = c.f(M1 * D.ch2);
   w.cont_lg = c.f(M1);
   w.du1 = c.f(M1 * D.dh); w.dx1 = c.f(M1 * D.dh); w.du2 = c.f(M1 * D.Fd);
-  w.dq1 = c.f(M1 * D.p3 * 2 * D.d2); w.dq2 = c.f(M1 * D.p2 * D.d2); w.dq3 = c.f(M1 * D.p1 * D.d1);
+  // vector mode: dq1 / dq1p = image_builder.0 pre / post SiLU [M1][Fd], dq2 = the output mu [M1][Dv]
+  w.dq1 = c.f(Dv ? M1 * D.Fd : M1 * D.p3 * 2 * D.d2); w.dq2 = c.f(Dv ? M1 * Dv : M1 * D.p2 * D.d2);
+  w.dq3 = c.f(M1 * D.p1 * D.d1);
   w.du2p = c.f(M1 * D.Fd);
-  w.dq1p = c.f(M1 * D.p3 * 2 * D.d2); w.dq2p = c.f(M1 * D.p2 * D.d2); w.dq3p = c.f(M1 * D.p1 * D.d1);
-  w.dg4 = c.f(M1 * D.p0 * 4);
+  w.dq1p = c.f(Dv ? M1 * D.Fd : M1 * D.p3 * 2 * D.d2); w.dq2p = c.f(M1 * D.p2 * D.d2); w.dq3p = c.f(M1 * D.p1 * D.d1);
+  w.dg4 = c.f(Dv ? M1 * Dv : M1 * D.p0 * 4);
   w.w3p = c.f((long long)D.Fd * D.dh); w.b3p = c.f(D.Fd);
   const int cin_t[4] = {D.C0, 2 * D.d2, D.d2, D.d1}, cout_t[4] = {2 * D.d2, D.d2, D.d1, 3};
   for (int k = 0; k < 4; ++k) {
@@ -372,7 +406,7 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
     w.wrd[k] = c.f((long long)16 * cin_t[k] * (k == 3 ? 4 : cout_t[k]));
   }
   w.coef_row = c.f(M1); w.coef_obs = c.f(M1);
-  w.obs_part = c.f(M1 * op_convT_mse_parts(D.IH / 2, D.IW / 2));
+  w.obs_part = c.f(Dv ? M1 : M1 * op_convT_mse_parts(D.IH / 2, D.IW / 2));
   w.kl_grp = c.f(M1 * d->rows); w.rew_row = c.f(M1); w.cont_row = c.f(M1); w.scal = c.f(8); w.stats = c.f(8);
   w.gH = c.f(M * Hd); w.gZ = c.f(M * L); w.glog = c.f(M * L); w.gpost = c.f(M1 * L);
   w.g_prior = c.f(M1 * L); w.g_rew = c.f(M1 * D.nb); w.g_cont = c.f(M1);
@@ -380,13 +414,14 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
   mlp_bwd_carve(c, M1, D.rh1, D.rh2, w.br);
   mlp_bwd_carve(c, M1, D.ch1, D.ch2, w.bc);
   w.gxu = c.f(M1 * D.dh); w.gpu = c.f(M1 * D.dh); w.gyu = c.f(M1 * D.dh); w.xhu = c.f(M1 * D.dh);
-  w.dgq3 = c.f(M1 * D.p1 * D.d1); w.dgq2 = c.f(M1 * D.p2 * D.d2); w.dgq1 = c.f(M1 * D.p3 * 2 * D.d2);
+  w.dgq3 = c.f(M1 * D.p1 * D.d1); w.dgq2 = c.f(M1 * D.p2 * D.d2); w.dgq1 = c.f(Dv ? M1 * D.Fd : M1 * D.p3 * 2 * D.d2);
   w.dgu2 = c.f(M1 * D.Fd);
   w.dw3p = c.f((long long)D.Fd * D.dh); w.db3p = c.f(D.Fd);
   w.ggi = c.f(M * 3 * Hd); w.ggh = c.f(M * 3 * Hd);
   w.gpre_m = c.f(M * eh); w.gy_m = c.f(M * eh); w.xh_m = c.f(M * eh);
   w.gx_s = c.f(B * eh); w.gh_dummy = c.f(B * Hd);
-  w.ga4 = c.f(M * D.F); w.gp3 = c.f(M * D.p3 * D.c3); w.gp2 = c.f(M * D.p2 * D.c2); w.gp1 = c.f(M * D.p1 * D.c1);
+  w.ga4 = c.f(M * D.F); w.gp3 = c.f(M * D.p3 * D.c3); w.gp2 = c.f(M * D.p2 * D.c2);
+  w.gp1 = c.f(Dv ? M * D.F : M * D.p1 * D.c1);
   w.t_pl6 = c.f((long long)L * D.ph2); w.t_pl3 = c.f((long long)D.ph2 * D.ph1); w.t_pl0 = c.f((long long)D.ph1 * Hd);
   w.t_rl6 = c.f((long long)D.nb * D.rh2); w.t_rl3 = c.f((long long)D.rh2 * D.rh1);
   w.t_rl0 = c.f((long long)D.rh1 * (Hd + L));
@@ -453,11 +488,14 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
                   hipStream_t s) {
   DR_REQUIRE(d && wm && dec && src && bt && losses && gw && gd && stats && B > 0 && T >= 2, "null argument or T < 2");
   DR_REQUIRE(bt->actions && bt->rewards && bt->continues, "window actions / rewards / continues required");
-  DR_REQUIRE(d->img_h % 16 == 0 && d->img_w % 16 == 0, "image size must be a multiple of 16");
+  DR_REQUIRE(d->obs_dim > 0 || (d->img_h % 16 == 0 && d->img_w % 16 == 0), "image size must be a multiple of 16");
   DR_REQUIRE(d->enc_f1 % 8 == 0 && d->enc_f2 % 8 == 0 && d->dec_f1 % 8 == 0 && d->dec_f2 % 8 == 0,
              "encoder / decoder filter counts must be multiples of 8");
   DR_REQUIRE(d->cols <= 64, "latent classes must be <= 64");
+  DR_REQUIRE(d->obs_dim == 0 || d->obs_dim % 4 == 0, "vector observations: obs_dim % 4 == 0 required");
   const WmDims D = wm_dims(d, B, T);
+  const bool vec = D.Dv > 0;
+  const int Dv = D.Dv;
   Carve c(ws);
   WmWs w;
   wm_carve(c, d, D, w);
@@ -473,6 +511,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   if (rows_global <= 0) rows_global = M1;
   if (phases & DR_WM_PREP) {
   // ---- weights: repacks, transposes, permutations (fixed for the call) ----
+  if (!vec) {
   DR_TRY(op_conv_repack_pad(D.c1, 3, 4, wm->conv[0].w, w.wr1, s));
   DR_TRY(op_conv_repack_pad(D.c2, D.c1, D.c1, wm->conv[1].w, w.wr2, s));
   DR_TRY(op_conv_repack_pad(D.c3, D.c2, D.c2, wm->conv[2].w, w.wr3, s));
@@ -487,7 +526,8 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     // ConvTranspose2d data gradient = strided Conv2d with the weight read as [out=ci][in=co]
     DR_TRY(op_conv_repack_pad(cin_t[k], cout_t[k], k == 3 ? 4 : cout_t[k], dec->convt[k].w, w.wrd[k], s));
   }
-  // decoder.upscaler.3 rows to NHWC order, so its output is the first convT's NHWC input
+  }  // !vec
+  // decoder.upscaler.3 rows to NHWC order (vector mode: P16 = 1, the identity), so its output is the first convT's NHWC input
   DR_TRY(perm_rows(D.C0, D.P16, D.dh, dec->up3.w, w.w3p, 1, s));
   DR_TRY(perm_rows(D.C0, D.P16, 1, dec->up3.b, w.b3p, 1, s));
   {
@@ -523,11 +563,21 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   DR_TRY(dr_check_launch("wm_coef"));
 
   // ---- encoder over all M frames (VAE.py:57-75), activations kept ----
+  if (vec) {  // MLP stand-in: pre1 = X W1^T + b1, a1 = SiLU, pre4 = a1 W2^T + b2, a4 = SiLU
+    DR_TRY(op_vec_gather(M, B, Dv, src, w.x0, s));
+    DR_TRY(run(G_NT, AM_PLAIN, lin(M, F, Dv, w.x0, Dv, wm->conv[0].w, Dv, wm->conv[0].b, w.pre1, F), s));
+    hipLaunchKernelGGL(k_silu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, w.pre1, w.a1);
+    DR_TRY(dr_check_launch("silu"));
+    DR_TRY(run(G_NT, AM_PLAIN, lin(M, F, F, w.a1, F, wm->conv[1].w, F, wm->conv[1].b, w.pre4, F), s));
+    hipLaunchKernelGGL(k_silu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, w.pre4, w.a4);
+    DR_TRY(dr_check_launch("silu"));
+  } else {
   DR_TRY(op_frames_nhwc4(M, B, IH, IW, src, w.x0, s));
   DR_TRY(op_conv_nhwc_ex(M, 4, IH, IW, D.c1, w.x0, w.wr1, wm->conv[0].b, w.a1, 0, w.pre1, CONV_EPI_FWD, s));
   DR_TRY(op_conv_nhwc_ex(M, D.c1, IH / 2, IW / 2, D.c2, w.a1, w.wr2, wm->conv[1].b, w.a2, 0, w.pre2, CONV_EPI_FWD, s));
   DR_TRY(op_conv_nhwc_ex(M, D.c2, IH / 4, IW / 4, D.c3, w.a2, w.wr3, wm->conv[2].b, w.a3, 0, w.pre3, CONV_EPI_FWD, s));
   DR_TRY(op_conv_nhwc_ex(M, D.c3, IH / 8, IW / 8, D.c4, w.a3, w.wr4, wm->conv[3].b, w.a4, 1, w.pre4, CONV_EPI_FWD, s));
+  }
   {
     GemmArgs g = lin(M, eh, F, w.a4, F, wm->map0.w, F + Hd, wm->map0.b, w.feat, eh);
     splitk_all(&g, 1, w.sk, w.sk_n);
@@ -593,7 +643,19 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     g.a_out = w.dx1; g.ld_aout = D.dh;
     DR_TRY(run(G_NT, AM_LNSILU, g, s));
   }
-  {
+  if (vec) {
+    // image_builder stand-in: q = SiLU(du2) Wd1^T + bd1, mu = SiLU(q) Wd2^T + bd2; squared error vs rows t >= 1
+    const long long MF = (long long)M1 * D.Fd;
+    hipLaunchKernelGGL(k_silu, dim3(blocks(MF, 256)), dim3(256), 0, s, MF, w.du2, w.du2p);
+    DR_TRY(dr_check_launch("silu"));
+    DR_TRY(run(G_NT, AM_PLAIN, lin(M1, D.Fd, D.Fd, w.du2p, D.Fd, dec->convt[0].w, D.Fd, dec->convt[0].b, w.dq1, D.Fd), s));
+    hipLaunchKernelGGL(k_silu, dim3(blocks(MF, 256)), dim3(256), 0, s, MF, w.dq1, w.dq1p);
+    DR_TRY(dr_check_launch("silu"));
+    DR_TRY(run(G_NT, AM_PLAIN, lin(M1, Dv, D.Fd, w.dq1p, D.Fd, dec->convt[1].w, D.Fd, dec->convt[1].b, w.dq2, Dv), s));
+    hipLaunchKernelGGL(k_vec_mse, dim3(blocks(M1, 4)), dim3(256), 0, s, M1, Dv, w.dq2, w.x0 + (long long)B * Dv,
+                       w.coef_obs, w.dg4, w.obs_part);
+    DR_TRY(dr_check_launch("vec_mse"));
+  } else {
     hipLaunchKernelGGL(k_silu, dim3(blocks((long long)M1 * D.Fd, 256)), dim3(256), 0, s, (long long)M1 * D.Fd,
                        w.du2, w.du2p);
     DR_TRY(dr_check_launch("silu"));
@@ -628,7 +690,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     hipLaunchKernelGGL(k_wm_heads, dim3(blocks(M1, 4)), dim3(256), 0, s, M1, nb, w.rew_lg, w.cont_lg, w.rew_tm,
                        w.cont_tm, wm->buckets_rew, w.coef_row, w.rew_row, w.cont_row, w.g_rew, w.g_cont);
     DR_TRY(dr_check_launch("wm_heads"));
-    hipLaunchKernelGGL(k_wm_stats, dim3(1), dim3(256), 0, s, M1, R, op_convT_mse_parts(IH / 2, IW / 2), w.obs_part,
+    hipLaunchKernelGGL(k_wm_stats, dim3(1), dim3(256), 0, s, M1, R, vec ? 1 : op_convT_mse_parts(IH / 2, IW / 2), w.obs_part,
                        w.rew_row, w.cont_row, w.kl_grp, w.cont_tm, stats);
     DR_TRY(dr_check_launch("wm_stats"));
   }
@@ -637,7 +699,11 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   if (post_logits_out) DR_TRY(copy2d(post_logits_out, L, w.plog, L, L, M, s));
   }  // DR_WM_FWD
 
-  if (!(phases & DR_WM_BWD)) return DR_OK;
+  const bool bwd_heads = (phases & (DR_WM_BWD | DR_WM_BWD_HEADS)) != 0;
+  const bool bwd_scan = (phases & (DR_WM_BWD | DR_WM_BWD_SCAN)) != 0;
+  const bool bwd_enc = (phases & (DR_WM_BWD | DR_WM_BWD_ENC)) != 0;
+  if (!(bwd_heads || bwd_scan || bwd_enc)) return DR_OK;
+  if (bwd_heads) {
   {
     const int W = pow2_ge(d->cols);
     const long long th = (long long)M1 * R * W;
@@ -659,7 +725,29 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   DR_TRY(head_bwd(D, wm->cont, gw->cont, D.ch1, D.ch2, 1, w.g_cont, w.t_cl6, w.t_cl3, w.t_cl0, w.cx1, w.cx2, w.cp1,
                   w.cp2, 1, hB, zB, gHB, gZB, w.bc, w.sk, w.sk_n, s));
   // decoder: image_builder.6 .. .0 (data grads as strided convs, weight grads, bias sums)
-  {
+  if (vec) {
+    // image_builder stand-in backward: dg4 = dL/dmu -> Wd2 / bd2 grads, dL/dq = (dg4 Wd2) SiLU'(q)
+    // -> Wd1 / bd1 grads, dL/d du2 = (dL/dq Wd1) SiLU'(du2)  (NN products with the weights as stored)
+    const long long MF = (long long)M1 * D.Fd;
+    auto nn = [&](int N, int K, const float* A, const float* Wkn, float* Y) {
+      GemmArgs g = gemm_args();
+      g.M = M1; g.N = N; g.K = K; g.A = A; g.lda = K; g.W = Wkn; g.ldb = N; g.Y = Y; g.ldy = N;
+      return gemm_launch(G_NN, AM_PLAIN, &g, 1, s);
+    };
+    DR_TRY(nn(D.Fd, Dv, w.dg4, dec->convt[1].w, w.dgq1));
+    hipLaunchKernelGGL(k_mul_dsilu, dim3(blocks(MF, 256)), dim3(256), 0, s, MF, w.dgq1, w.dq1);
+    DR_TRY(dr_check_launch("mul_dsilu"));
+    DR_TRY(nn(D.Fd, D.Fd, w.dgq1, dec->convt[0].w, w.dgu2));
+    hipLaunchKernelGGL(k_mul_dsilu, dim3(blocks(MF, 256)), dim3(256), 0, s, MF, w.dgu2, w.du2);
+    DR_TRY(dr_check_launch("mul_dsilu"));
+    GemmArgs p[2];
+    p[0] = bwd_w(Dv, D.Fd, M1, w.dg4, Dv, w.dq1p, D.Fd, gd->convt[1].w);
+    p[1] = bwd_w(D.Fd, D.Fd, M1, w.dgq1, D.Fd, w.du2p, D.Fd, gd->convt[0].w);
+    splitk_all(p, 2, w.sk, w.sk_n);
+    DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 2, s));
+    ColsumJob cj[2] = {{Dv, w.dg4, Dv, nullptr, 0, gd->convt[1].b}, {D.Fd, w.dgq1, D.Fd, nullptr, 0, gd->convt[0].b}};
+    DR_TRY(op_colsum_multi(M1, cj, 2, s));
+  } else {
     float* gins[4] = {w.dgu2, w.dgq1, w.dgq2, w.dgq3};   // dL/d(pre-activation) of each convT input
     const float* pres[4] = {w.du2, w.dq1, w.dq2, w.dq3};
     const float* posts[4] = {w.du2p, w.dq1p, w.dq2p, w.dq3p};
@@ -699,7 +787,9 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     DR_TRY(perm_rows(D.C0, D.P16, D.dh, w.dw3p, gd->up3.w, 0, s));
     DR_TRY(perm_rows(D.C0, D.P16, 1, w.db3p, gd->up3.b, 0, s));
   }
+  }  // bwd_heads
 
+  if (bwd_scan) {
   // ---- backward through the posterior scan, t = T-1 .. 0 ----
   const int Wc = pow2_ge(d->cols);
   for (int t = T - 1; t >= 0; --t) {
@@ -744,13 +834,30 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     };
     DR_TRY(op_colsum_multi(M, cj, 6, s));
   }
+  }  // bwd_scan
 
+  if (bwd_enc) {
   // ---- backward through the encoder convolutions (all M frames) ----
   DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M, F, eh, w.gpre_m, eh, w.w0tp, w.ga4, F, 0), s));
   hipLaunchKernelGGL(k_mul_dsilu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, w.ga4,
                      w.pre4);
   DR_TRY(dr_check_launch("mul_dsilu"));
-  {
+  if (vec) {
+    // MLP stand-in backward: W2 / b2 grads from dL/d pre4, dL/d pre1 = (ga4 W2) SiLU'(pre1), W1 / b1 grads
+    GemmArgs g = gemm_args();
+    g.M = M; g.N = F; g.K = F; g.A = w.ga4; g.lda = F; g.W = wm->conv[1].w; g.ldb = F; g.Y = w.gp1; g.ldy = F;
+    DR_TRY(gemm_launch(G_NN, AM_PLAIN, &g, 1, s));
+    hipLaunchKernelGGL(k_mul_dsilu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, w.gp1,
+                       w.pre1);
+    DR_TRY(dr_check_launch("mul_dsilu"));
+    GemmArgs p[2];
+    p[0] = bwd_w(F, F, M, w.ga4, F, w.a1, F, gw->conv[1].w);
+    p[1] = bwd_w(F, Dv, M, w.gp1, F, w.x0, Dv, gw->conv[0].w);
+    splitk_all(p, 2, w.sk, w.sk_n);
+    DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 2, s));
+    ColsumJob cj[2] = {{F, w.ga4, F, nullptr, 0, gw->conv[1].b}, {F, w.gp1, F, nullptr, 0, gw->conv[0].b}};
+    DR_TRY(op_colsum_multi(M, cj, 2, s));
+  } else {
     float* go[4] = {w.gp1, w.gp2, w.gp3, w.ga4};           // dL/d pre-activation of conv k's output
     const float* pr[3] = {w.pre1, w.pre2, w.pre3};
     const float* hi[4] = {w.x0, w.a1, w.a2, w.a3};         // conv k's input
@@ -769,6 +876,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
       }
     }
   }
+  }  // bwd_enc
 
   return DR_OK;
 }
@@ -808,7 +916,7 @@ static void dec_carve(Carve& c, const dr_dims* d, int M, DecWs& w) {
   const int cin_t[4] = {D.C0, 2 * D.d2, D.d2, D.d1}, cout_t[4] = {2 * D.d2, D.d2, D.d1, 3};
   w.u1 = c.f((long long)M * D.dh);
   w.u2 = c.f((long long)M * D.Fd);
-  w.q[0] = c.f((long long)M * D.p3 * cout_t[0]);
+  w.q[0] = c.f(D.Dv ? (long long)M * D.Fd : (long long)M * D.p3 * cout_t[0]);
   w.q[1] = c.f((long long)M * D.p2 * cout_t[1]);
   w.q[2] = c.f((long long)M * D.p1 * cout_t[2]);
   w.w3p = c.f((long long)D.Fd * D.dh);
@@ -827,7 +935,7 @@ extern "C" size_t dr_decoder_workspace_bytes(const dr_dims* d, int M) {
 extern "C" int dr_decoder_fwd(const dr_dims* d, const dr_decoder* dec, int M, const float* h, long long ldh,
                               const float* z, long long ldz, float* mu, void* ws, size_t ws_bytes, hipStream_t s) {
   DR_REQUIRE(d && dec && h && z && mu && M > 0, "null argument or empty batch");
-  DR_REQUIRE(d->img_h % 16 == 0 && d->img_w % 16 == 0, "image size must be a multiple of 16");
+  DR_REQUIRE(d->obs_dim > 0 || (d->img_h % 16 == 0 && d->img_w % 16 == 0), "image size must be a multiple of 16");
   DR_REQUIRE(d->dec_f1 % 8 == 0 && d->dec_f2 % 8 == 0, "decoder filter counts must be multiples of 8");
   Carve c(ws);
   DecWs w;
@@ -836,6 +944,16 @@ extern "C" int dr_decoder_fwd(const dr_dims* d, const dr_decoder* dec, int M, co
   const WmDims D = wm_dims(d, 1, 2);
   const int cin_t[4] = {D.C0, 2 * D.d2, D.d2, D.d1}, cout_t[4] = {2 * D.d2, D.d2, D.d1, 3};
   const int Hd = D.Hd, L = D.L;
+  if (D.Dv) {  // vector observations: upscaler, then the image_builder MLP stand-in -> mu [M][D]
+    DR_TRY(run(G_NT, AM_PLAIN, lin2(M, D.dh, h, ldh, Hd, z, ldz, L, dec->up0.w, dec->up0.b, w.u1, D.dh), s));
+    GemmArgs g = lin_ln(M, D.Fd, D.dh, w.u1, D.dh, dec->up1, dec->up3.w, dec->up3.b, w.u2, D.Fd);
+    g.act = 1;
+    DR_TRY(run(G_NT, AM_LNSILU, g, s));
+    GemmArgs g1 = lin(M, D.Fd, D.Fd, w.u2, D.Fd, dec->convt[0].w, D.Fd, dec->convt[0].b, w.q[0], D.Fd);
+    g1.act = 1;
+    DR_TRY(run(G_NT, AM_PLAIN, g1, s));
+    return run(G_NT, AM_PLAIN, lin(M, D.Dv, D.Fd, w.q[0], D.Fd, dec->convt[1].w, D.Fd, dec->convt[1].b, mu, D.Dv), s);
+  }
   DR_TRY(perm_rows(D.C0, D.P16, D.dh, dec->up3.w, w.w3p, 1, s));
   DR_TRY(perm_rows(D.C0, D.P16, 1, dec->up3.b, w.b3p, 1, s));
   for (int k = 0; k < 3; ++k) DR_TRY(op_convT_repack(cin_t[k], cout_t[k], dec->convt[k].w, w.wq[k], s));

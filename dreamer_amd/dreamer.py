@@ -297,6 +297,8 @@ class Dreamer(nn.Module):
         uint8 frame.  Returns (a', mu, sigma, z', h') shaped (1, 1, ...)."""
         dev = self.device
         L.require_gpu(torch.empty(0, device=dev))
+        if self.world_model.vector_obs:
+            return self._act_step_vector(observation, z, h, a, deterministic)
         d = self.world_model.dims(self.agent)
         self.agent._ensure_flat()
         R, C = self.latent_state_dims
@@ -327,6 +329,33 @@ class Dreamer(nn.Module):
         self._act_ev.record()
         return a2, mu, sg, z2, h2
 
+    def _act_step_vector(self, observation, z, h, a, deterministic):
+        """Vector observations (BASELINE configs[4]): the same step through the
+        unfused HIP launches -- dr_gru_cell, dr_encoder_features +
+        dr_observe_scan (Encoder.encode), dr_actor_act."""
+        dev = self.device
+        wm = self.world_model
+        obs = torch.as_tensor(np.asarray(observation, dtype=np.float32), device=dev).view(1, 1, -1)
+        if z is None:
+            h2 = torch.zeros(1, 1, self.hidden_state_dims, device=dev)
+        else:
+            h2 = wm.sequence_model(z.reshape(1, 1, -1), h.reshape(1, 1, -1), a.reshape(1, 1, -1))
+        z2, _ = wm.encoder.encode(h2, obs)
+        a2, mu, sg = self.agent.actor.act(h2, z2, deterministic=deterministic)
+        return a2, mu, sg, z2, h2
+
+    def _agent_obs(self, observation):
+        """The env observation as the agent keeps it (Dreamer.py:181-183): a
+        normalised CHW frame, or the raw f32 vector."""
+        if self.world_model.vector_obs:
+            return np.asarray(observation, dtype=np.float32)
+        return (observation.transpose(2, 0, 1).astype(np.float32) / 255.0) - 0.5
+
+    def _buffer_obs(self, agent_obs):
+        if self.world_model.vector_obs:
+            return agent_obs
+        return ((agent_obs + 0.5) * 255.0).astype(np.uint8)
+
     def _act_sync(self):
         ev = getattr(self, "_act_ev", None)
         if ev is not None:
@@ -338,7 +367,7 @@ class Dreamer(nn.Module):
         with torch.no_grad():
             if self.agent_obs is None:
                 observation, _ = env.reset(seed=self.seed)
-                self.agent_obs = (observation.transpose(2, 0, 1).astype(np.float32) / 255.0) - 0.5
+                self.agent_obs = self._agent_obs(observation)
                 _, _, _, self.agent_latent, self.agent_hidden = self.act_step(observation)
             action = None
             if not random_policy:  # the current actor's action for the current state
@@ -351,15 +380,14 @@ class Dreamer(nn.Module):
                     action_np = action.detach().cpu().numpy().reshape(-1)
                 observation_, reward, terminated, truncated, _ = env.step(action_np)
                 done = terminated or truncated
-                current_u8 = ((self.agent_obs + 0.5) * 255.0).astype(np.uint8)
-                self.buffer.add_to_buffer(current_u8, action_np, reward, 1 - done)
+                self.buffer.add_to_buffer(self._buffer_obs(self.agent_obs), action_np, reward, 1 - done)
                 if done:
                     self.seed += 1
                     observation, _ = env.reset(seed=self.seed)
-                    self.agent_obs = (observation.transpose(2, 0, 1).astype(np.float32) / 255.0) - 0.5
+                    self.agent_obs = self._agent_obs(observation)
                     action, _, _, self.agent_latent, self.agent_hidden = self.act_step(observation)
                 else:
-                    self.agent_obs = (observation_.transpose(2, 0, 1).astype(np.float32) / 255.0) - 0.5
+                    self.agent_obs = self._agent_obs(observation_)
                     action, _, _, self.agent_latent, self.agent_hidden = self.act_step(
                         observation_, self.agent_latent, self.agent_hidden, action)
 

@@ -187,18 +187,31 @@ class Encoder(nn.Module):
         super().__init__()
         self.latent_size = latent_num_rows * latent_num_columns
         self.latent_num_rows, self.latent_num_columns = latent_num_rows, latent_num_columns
-        self.final_height = observation_dims[0] // 16
-        self.final_width = observation_dims[1] // 16
-        if self.final_height < 1 or self.final_width < 1:
-            raise ValueError(f"Input image {observation_dims} is too small for 4 layers of downsampling.")
         self.observation_dims = tuple(observation_dims)
         self.hidden_state_dim = hidden_state_dim
-        chans = [3, num_filters_1, num_filters_2, 2 * num_filters_2, 4 * num_filters_2]
-        layers = []
-        for cin, cout in zip(chans[:-1], chans[1:]):
-            layers += [nn.Conv2d(cin, cout, kernel_size=4, stride=2, padding=1, device=device), nn.SiLU()]
-        self.feature_extractor = nn.Sequential(*layers)
-        n_feat = chans[-1] * self.final_height * self.final_width
+        self.num_filters_1 = num_filters_1
+        # observation_dims = [D]: proprioceptive vector observations (BASELINE
+        # configs[4]).  The reference encoder is always convolutional
+        # (VAE.py:33-42); the stand-in is Linear(D, 4 f2)-SiLU-Linear(4 f2, 4 f2)-SiLU
+        # with the same latent_mapper (include/dreamer_hip.h dr_dims.obs_dim).
+        self.vector = len(self.observation_dims) == 1
+        if self.vector:
+            D, F = self.observation_dims[0], 4 * num_filters_2
+            self.final_height = self.final_width = 1
+            self.feature_extractor = nn.Sequential(nn.Linear(D, F, device=device), nn.SiLU(),
+                                                   nn.Linear(F, F, device=device), nn.SiLU())
+            n_feat = F
+        else:
+            self.final_height = observation_dims[0] // 16
+            self.final_width = observation_dims[1] // 16
+            if self.final_height < 1 or self.final_width < 1:
+                raise ValueError(f"Input image {observation_dims} is too small for 4 layers of downsampling.")
+            chans = [3, num_filters_1, num_filters_2, 2 * num_filters_2, 4 * num_filters_2]
+            layers = []
+            for cin, cout in zip(chans[:-1], chans[1:]):
+                layers += [nn.Conv2d(cin, cout, kernel_size=4, stride=2, padding=1, device=device), nn.SiLU()]
+            self.feature_extractor = nn.Sequential(*layers)
+            n_feat = chans[-1] * self.final_height * self.final_width
         self.flatten = nn.Flatten(start_dim=2)
         self.latent_mapper = nn.Sequential(
             nn.Linear(n_feat + hidden_state_dim, hidden_layer_nodes, device=device),
@@ -207,22 +220,33 @@ class Encoder(nn.Module):
 
     # -- packing for libdreamer_hip -------------------------------------------
     def fill_dims(self, d):
-        d.img_h, d.img_w = self.observation_dims
-        d.enc_f1 = self.feature_extractor[0].out_channels
-        d.enc_f2 = self.feature_extractor[2].out_channels
+        if self.vector:
+            d.img_h = d.img_w = 0
+            d.obs_dim = self.observation_dims[0]
+            d.enc_f1 = self.num_filters_1
+            d.enc_f2 = self.feature_extractor[0].out_features // 4
+        else:
+            d.img_h, d.img_w = self.observation_dims
+            d.obs_dim = 0
+            d.enc_f1 = self.feature_extractor[0].out_channels
+            d.enc_f2 = self.feature_extractor[2].out_channels
         d.enc_hidden = self.latent_mapper[0].out_features
         d.hidden = self.hidden_state_dim
         d.rows, d.cols = self.latent_num_rows, self.latent_num_columns
 
     def fill(self, wm):
         fe = self.feature_extractor
-        for i, j in enumerate((0, 2, 4, 6)):
+        for i, j in enumerate((0, 2, 4, 6)[:len(fe) // 2]):
             wm.conv[i] = hip.linear(fe[j])
         wm.map0, wm.map1, wm.map3 = (hip.linear(self.latent_mapper[j]) for j in (0, 1, 3))
 
     def forward(self, hidden, observation):
-        B, S, C, H, W = observation.shape
+        B, S = observation.shape[:2]
+        if hip.needs_torch_grad(self) and self.vector:
+            feat = self.feature_extractor(observation.reshape(B, S, -1))
+            return self.latent_mapper(torch.cat((feat, hidden), dim=-1))
         if hip.needs_torch_grad(self):
+            C, H, W = observation.shape[2:]
             feat = self.feature_extractor(observation.reshape(B * S, C, H, W))
             feat = self.flatten(feat.view(B, S, *feat.shape[1:]))
             return self.latent_mapper(torch.cat((feat, hidden), dim=-1))
@@ -275,8 +299,13 @@ class Decoder(nn.Module):
     def __init__(self, latent_num_rows, latent_num_columns, observation_dim, hidden_state_dim, num_filters_1,
                  num_filters_2, hidden_layer_nodes, device="cpu"):
         super().__init__()
-        self.start_height = observation_dim[0] // 16
-        self.start_width = observation_dim[1] // 16
+        # observation_dim = [D]: vector observations (Encoder's note); the
+        # image_builder stand-in is Linear(4 f2, 4 f2)-SiLU-Linear(4 f2, D), no Tanh
+        self.vector = len(observation_dim) == 1
+        self.observation_dim = tuple(observation_dim)
+        self.num_filters_1, self.num_filters_2 = num_filters_1, num_filters_2
+        self.start_height = 1 if self.vector else observation_dim[0] // 16
+        self.start_width = 1 if self.vector else observation_dim[1] // 16
         self.num_filters_start = num_filters_2 * 4
         self.hidden_dim = hidden_state_dim
         self.latent_row_dim, self.latent_col_dim = latent_num_rows, latent_num_columns
@@ -286,6 +315,10 @@ class Decoder(nn.Module):
             nn.Linear(latent_num_rows * latent_num_columns + hidden_state_dim, hidden_layer_nodes, device=device),
             nn.LayerNorm(hidden_layer_nodes, device=device), nn.SiLU(),
             nn.Linear(hidden_layer_nodes, n_start, device=device), nn.SiLU())
+        if self.vector:
+            self.image_builder = nn.Sequential(nn.Linear(n_start, n_start, device=device), nn.SiLU(),
+                                               nn.Linear(n_start, observation_dim[0], device=device))
+            return
         chans = [self.num_filters_start, 2 * num_filters_2, num_filters_2, num_filters_1, 3]
         layers = []
         for i, (cin, cout) in enumerate(zip(chans[:-1], chans[1:])):
@@ -293,11 +326,30 @@ class Decoder(nn.Module):
             layers.append(nn.Tanh() if i == 3 else nn.SiLU())
         self.image_builder = nn.Sequential(*layers)
 
+    def fill_dims(self, d):
+        d.dec_f1, d.dec_f2 = self.num_filters_1, self.num_filters_2
+        d.dec_hidden = self.upscaler[0].out_features
+        if self.vector:
+            d.obs_dim = self.observation_dim[0]
+            d.img_h = d.img_w = 0
+        else:
+            d.obs_dim = 0
+            d.img_h, d.img_w = 16 * self.start_height, 16 * self.start_width
+
+    def packed(self):
+        ib = self.image_builder
+        dec = L.dr_decoder(hip.linear(self.upscaler[0]), hip.linear(self.upscaler[1]), hip.linear(self.upscaler[3]))
+        for i, j in enumerate((0, 2, 4, 6)[:(len(ib) + 1) // 2]):
+            dec.convt[i] = hip.linear(ib[j])
+        return dec
+
     def forward(self, hidden, latent):
         B, S, _ = hidden.shape
         if not hip.needs_torch_grad(self):
             return self._hip(hidden, latent)
         x = torch.cat((hidden.reshape(B * S, self.hidden_dim), self.flatten(latent.reshape(B * S, -1))), dim=-1)
+        if self.vector:
+            return self.image_builder(self.upscaler(x)).view(B, S, -1)
         x = self.upscaler(x).view(-1, self.num_filters_start, self.start_height, self.start_width)
         mu = self.image_builder(x)
         return mu.view(B, S, *mu.shape[1:])
@@ -310,14 +362,9 @@ class Decoder(nn.Module):
         z = latent.reshape(M, -1).float().contiguous()
         d = L.dr_dims()
         d.hidden, d.rows, d.cols = self.hidden_dim, self.latent_row_dim, self.latent_col_dim
-        d.img_h, d.img_w = 16 * self.start_height, 16 * self.start_width
-        ib = self.image_builder
-        d.dec_f1, d.dec_f2 = ib[4].out_channels, ib[2].out_channels
-        d.dec_hidden = self.upscaler[0].out_features
-        dec = L.dr_decoder(hip.linear(self.upscaler[0]), hip.linear(self.upscaler[1]), hip.linear(self.upscaler[3]))
-        for i, j in enumerate((0, 2, 4, 6)):
-            dec.convt[i] = hip.linear(ib[j])
-        mu = torch.empty(B, S, 3, d.img_h, d.img_w, device=h.device)
+        self.fill_dims(d)
+        dec = self.packed()
+        mu = torch.empty(B, S, *((d.obs_dim,) if self.vector else (3, d.img_h, d.img_w)), device=h.device)
         ws = hip.workspace(h.device).get("dec", L.query("dr_decoder_workspace_bytes", d, M))
         L.call("dr_decoder_fwd", d, dec, M, L.ptr(h), h.shape[1], L.ptr(z), z.shape[1], L.ptr(mu), L.ptr(ws),
                ws.numel(), hip.stream())

@@ -24,7 +24,9 @@ class WorldModel(nn.Module):
         self.latent_num_rows, self.latent_num_columns = latent_dims
         self.hidden_dims = hidden_dims
         self.action_dims = action_dims
-        self.observation_dim_x, self.observation_dim_y = observation_dims
+        self.vector_obs = len(observation_dims) == 1  # BASELINE configs[4] (networks.Encoder)
+        self.observation_dim_x, self.observation_dim_y = (observation_dims[0], 1) if self.vector_obs \
+            else tuple(observation_dims)
         self.horizon = training_horizon
         self.buckets = reward_buckets
         self.beta_pred, self.beta_dyn, self.beta_rep = beta_pred, beta_dyn, beta_rep
@@ -60,9 +62,7 @@ class WorldModel(nn.Module):
         d.rew_h1, d.rew_h2 = rp[0].out_features, rp[3].out_features
         d.cont_h1, d.cont_h2 = cp[0].out_features, cp[3].out_features
         d.buckets = self.buckets
-        ib = self.decoder.image_builder
-        d.dec_f1, d.dec_f2 = ib[4].out_channels, ib[2].out_channels
-        d.dec_hidden = self.decoder.upscaler[0].out_features
+        self.decoder.fill_dims(d)
         d.precision = 1 if getattr(self, "precision", "fp32") == "bf16" else 0  # DR_PREC_BF16 / DR_PREC_FP32
         if agent is not None:
             a, c = agent.actor.base_net, agent.critic.value_net
@@ -82,17 +82,12 @@ class WorldModel(nn.Module):
         return wm
 
     def packed_decoder(self):
-        dc = self.decoder
-        up, ib = dc.upscaler, dc.image_builder
-        out = L.dr_decoder(hip.linear(up[0]), hip.linear(up[1]), hip.linear(up[3]))
-        for i, j in enumerate((0, 2, 4, 6)):
-            out.convt[i] = hip.linear(ib[j])
-        return out
+        return self.decoder.packed()
 
     def _grad_structs(self):
         """C structs pointing at the parameters' .grad views (one flat buffer)."""
         e, g = self.encoder, L.dr_world_model()
-        for i, j in enumerate((0, 2, 4, 6)):
+        for i, j in enumerate((0, 2, 4, 6)[:len(e.feature_extractor) // 2]):
             g.conv[i] = hip.linear_grad(e.feature_extractor[j])
         g.map0, g.map1, g.map3 = (hip.linear_grad(e.latent_mapper[j]) for j in (0, 1, 3))
         gru = self.sequence_model.GRU
@@ -103,9 +98,37 @@ class WorldModel(nn.Module):
         g.cont = hip.mlp3_grad(self.continue_predictor.logit_generator)
         up, ib = self.decoder.upscaler, self.decoder.image_builder
         gd = L.dr_decoder(hip.linear_grad(up[0]), hip.linear_grad(up[1]), hip.linear_grad(up[3]))
-        for i, j in enumerate((0, 2, 4, 6)):
+        for i, j in enumerate((0, 2, 4, 6)[:(len(ib) + 1) // 2]):
             gd.convt[i] = hip.linear_grad(ib[j])
         return g, gd
+
+    def _grad_buckets(self, f):
+        """Flat-gradient ranges final after each backward stage of
+        dr_wm_train_phase (DR_WM_BWD_HEADS, _SCAN, _ENC): the heads and the
+        decoder; latent_mapper and the GRU; the encoder convolutions.  They
+        are contiguous in the flat buffer (parameter registration order:
+        encoder convs, latent_mapper, GRU, heads, decoder)."""
+        key = (f.numel, tuple(f.names))
+        if getattr(self, "_buckets", (None,))[0] == key:
+            return self._buckets[1]
+        def stage(n):
+            if n.startswith("encoder.feature_extractor."):
+                return 2
+            if n.startswith("encoder.latent_mapper.") or n.startswith("sequence_model."):
+                return 1
+            return 0
+        lo, hi = [f.numel] * 3, [0] * 3
+        for n, p in zip(f.names, f.params):
+            k, o = stage(n), f.offsets[n]
+            lo[k], hi[k] = min(lo[k], o), max(hi[k], o + -(-p.numel() // 64) * 64)
+        for n in f.names:  # each range holds only its own stage's parameters
+            o = f.offsets[n]
+            for k in range(3):
+                if lo[k] <= o < hi[k] and stage(n) != k:
+                    raise RuntimeError(f"world-model gradient buckets are not contiguous ({n})")
+        out = [(lo[k], hi[k]) if hi[k] > lo[k] else (0, 0) for k in range(3)]
+        self._buckets = (key, out)
+        return out
 
     def _ensure_flat(self):
         """Parameters as views of one flat buffer, gradients in another, and
@@ -205,7 +228,7 @@ class WorldModel(nn.Module):
         obs_t = observation_sequence_batch[:, :self.horizon]
         rew_t = reward_sequence_batch[:, :self.horizon - 1]
         cont_t = continue_sequence_batch[:, :self.horizon - 1]
-        obs_ll = -(dec_mu.float() - obs_t.float()).pow(2).sum(dim=[-3, -2, -1])
+        obs_ll = -(dec_mu.float() - obs_t.float()).pow(2).sum(dim=[-1] if self.vector_obs else [-3, -2, -1])
         cont_ll = torch.nn.functional.binary_cross_entropy_with_logits(cont_logits, cont_t, reduction="none")
         rew_ll = torch.sum(to_twohot(rew_t, self.reward_predictor.buckets_rew)
                            * torch.nn.functional.log_softmax(reward_logits, dim=-1), dim=-1, keepdim=True)
@@ -236,7 +259,10 @@ class WorldModel(nn.Module):
         act = act.float().contiguous()
         rew = rew.float().reshape(B, S).contiguous()
         cont = cont.float().reshape(B, S).contiguous()
-        fr = L.dr_frames(None, 0, None, L.ptr(obs), S * 3 * Hh * Ww, 3 * Hh * Ww, 1, 0)
+        if self.vector_obs:  # (B, S, D) f32 observations, used as given
+            fr = L.dr_frames(None, 0, None, L.ptr(obs), S * Hh, Hh, 0, 0)
+        else:
+            fr = L.dr_frames(None, 0, None, L.ptr(obs), S * 3 * Hh * Ww, 3 * Hh * Ww, 1, 0)
         bt = L.dr_wm_batch(L.ptr(act), S * A, A, L.ptr(rew), L.ptr(cont), S, 1)
         return self._train(fr, bt, B, S, obs.device, noise_q, outputs, step)
 
@@ -297,8 +323,15 @@ class WorldModel(nn.Module):
             dist.all_reduce(stats[0:1], group=group)
             L.call("dr_wm_train_phase", *args, noise, cfg, 2, L.ptr(stats), rows, *tail)
             dist.all_reduce(stats[1:5], group=group)
-            L.call("dr_wm_train_phase", *args, noise, cfg, 4, L.ptr(stats), rows, *tail)
-            dist.all_reduce(f.grad, group=group)
+            # backward in three stages, each gradient bucket all-reduced (on
+            # the communicator's stream) while the next stage computes
+            works = []
+            for bit, (lo, hi) in zip((8, 16, 32), self._grad_buckets(f)):
+                L.call("dr_wm_train_phase", *args, noise, cfg, bit, L.ptr(stats), rows, *tail)
+                if hi > lo:
+                    works.append(dist.all_reduce(f.grad[lo:hi], group=group, async_op=True))
+            for w in works:
+                w.wait()
         if outputs is not None:
             outputs.update(hiddens=hid, latents=lat, post_logits=plog)
         if step:

@@ -61,6 +61,13 @@ typedef struct {
   int dec_hidden;      /* decoder_hidden_layer_nodes (200) */
   int precision;       /* DR_PREC_FP32 (parity mode, default) or DR_PREC_BF16 (perf mode: bf16 MFMA
                           operands, f32 accumulation; the extra `precision` config key) */
+  int obs_dim;         /* 0: pixel observations img_h x img_w x 3 (the reference).  D > 0: proprioceptive
+                          vector observations of D floats (BASELINE configs[4]; the reference has no such
+                          encoder, VAE.py:33-42 is always convolutional).  The convolution slots then hold
+                          an MLP: encoder conv[0] = Linear(D, 4*enc_f2), conv[1] =
+                          Linear(4*enc_f2, 4*enc_f2), each + SiLU (F = 4*enc_f2 features, conv[2..3]
+                          unused); decoder upscaler.3 -> 4*dec_f2, convt[0] = Linear(4*dec_f2, 4*dec_f2)
+                          + SiLU, convt[1] = Linear(4*dec_f2, D) (no Tanh; convt[2..3] unused). */
 } dr_dims;
 #define DR_PREC_FP32 0
 #define DR_PREC_BF16 1
@@ -102,7 +109,8 @@ typedef struct {
 
 /* Source of observation frames for the encoder.  Frame f = t*B + b. */
 typedef struct {
-  const unsigned char* ring; /* u8 replay ring [cap][3][H][W] (Buffer.py:7), or NULL */
+  const unsigned char* ring; /* u8 replay ring [cap][3][H][W] (Buffer.py:7), or NULL; with dr_dims.obs_dim
+                                = D > 0 the ring holds f32 rows [cap][D] (pointer cast) */
   long long ring_cap;
   const long long* starts;   /* device [B] window starts (Buffer.py:36-50) */
   const float* obs;          /* f32 frames (when ring == NULL) */
@@ -293,6 +301,18 @@ size_t dr_wm_train_workspace_bytes(const dr_dims* d, int B, int T);
 #define DR_WM_PREP 1
 #define DR_WM_FWD 2
 #define DR_WM_BWD 4
+/* DR_WM_BWD in three stages, called in this order with the same workspace;
+ * each leaves one bucket of the gradient final, so a data-parallel caller can
+ * all-reduce it while the next stage runs (WorldModel.py:195-200 backward +
+ * SURVEY 8e "bucketed to overlap the backward"):
+ *   HEADS: the loss grads, prior / reward / continue heads and the decoder
+ *          (g_wm->prior, ->reward, ->cont, every g_dec field) final;
+ *   SCAN:  the posterior scan: latent_mapper and GRU (->map0/1/3, ->w_ih,
+ *          ->w_hh, ->b_ih, ->b_hh) final;
+ *   ENC:   the encoder convolutions (->conv[0..3]) final. */
+#define DR_WM_BWD_HEADS 8
+#define DR_WM_BWD_SCAN 16
+#define DR_WM_BWD_ENC 32
 int dr_wm_train_phase(const dr_dims* d, const dr_world_model* wm, const dr_decoder* dec, int B, int T,
                       const dr_frames* src, const dr_wm_batch* batch, dr_noise noise, dr_wm_loss_cfg cfg, int phases,
                       float* stats, int rows_global, float* losses, int* skip, const dr_world_model* g_wm,

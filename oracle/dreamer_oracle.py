@@ -117,7 +117,19 @@ def gru_manual(x, h, w_ih, w_hh, b_ih, b_hh):
 
 
 def encoder_logits(h, obs, P):
-    """Encoder.forward (VariationalAutoEncoder.py:57-75). obs already normalised."""
+    """Encoder.forward (VariationalAutoEncoder.py:57-75). obs already normalised.
+    obs (B, S, D): the vector-observation stand-in of BASELINE configs[4]
+    (Linear-SiLU x2; NOT in the reference -- parity of that mode is pinned
+    only against this restatement of the framework's own definition,
+    include/dreamer_hip.h dr_dims.obs_dim)."""
+    if obs.dim() == 3:
+        x = obs
+        for i in (0, 2):
+            x = F.silu(_lin(x, P, WM + f"encoder.feature_extractor.{i}"))
+        feat = x
+        inp = torch.cat((feat, h), dim=-1)
+        y = F.silu(_ln(_lin(inp, P, WM + "encoder.latent_mapper.0"), P, WM + "encoder.latent_mapper.1"))
+        return _lin(y, P, WM + "encoder.latent_mapper.3")
     B, S, C, Hh, Ww = obs.shape
     x = obs.reshape(B * S, C, Hh, Ww)
     for i in (0, 2, 4, 6):
@@ -372,6 +384,9 @@ def decoder_forward(h, z, P, img_hw):
     D = WM + "decoder."
     x = F.silu(_ln(_lin(x, P, D + "upscaler.0"), P, D + "upscaler.1"))
     x = F.silu(_lin(x, P, D + "upscaler.3"))
+    if D + "image_builder.4.weight" not in P:  # vector-observation stand-in (encoder_logits' note)
+        x = F.silu(_lin(x, P, D + "image_builder.0"))
+        return _lin(x, P, D + "image_builder.2").view(B, S, -1)
     c0 = P[D + "image_builder.0.weight"].shape[0]
     x = x.view(-1, c0, img_hw[0] // 16, img_hw[1] // 16)
     for j, i in enumerate((0, 2, 4, 6)):
@@ -403,7 +418,7 @@ def wm_unroll(obs, act, rew, cont, P, q, rows, cols, horizon):
     cont_logits = mlp3(rin, P, WM + "continue_predictor.logit_generator")
     obs_t, rew_t, cont_t = obs[:, :horizon], rew[:, :horizon - 1], cont[:, :horizon - 1]
     th = twohot(rew_t, P[WM + "reward_predictor.buckets_rew"])
-    obs_ll = -(dec_mu.float() - obs_t.float()).pow(2).sum(dim=[-3, -2, -1])
+    obs_ll = -(dec_mu.float() - obs_t.float()).pow(2).sum(dim=[-1] if obs.dim() == 3 else [-3, -2, -1])
     cont_ll = F.binary_cross_entropy_with_logits(cont_logits, cont_t, reduction="none")
     rew_ll = torch.sum(th * F.log_softmax(rew_logits, dim=-1), dim=-1, keepdim=True)
     return dict(prior=prior[:, 1:], post=post_logits[:, 1:], obs_ll=obs_ll[:, 1:], rew_ll=rew_ll,
@@ -423,7 +438,7 @@ def wm_losses(obs_u8, act, rew, cont, P, q, rows, cols, horizon, betas=(1.0, 0.5
     """WorldModel.training_step loss construction (WorldModel.py:148-189) with
     autocast disabled (fp32).  Returns a dict of losses (0-d tensors) and the
     unroll outputs."""
-    obs = normalise_obs(obs_u8)
+    obs = obs_u8 if obs_u8.dim() == 3 else normalise_obs(obs_u8)  # vector observations: as given
     H = horizon
     u = wm_unroll(obs[:, :H], act[:, :H], rew[:, :H], cont[:, :H], P, q, rows, cols, H)
     mask = cont[:, :H - 1]

@@ -121,3 +121,47 @@ def test_hot_path_refuses_cpu_tensors():
         d.world_model.imagine_step(h, z, a)
     with pytest.raises(RuntimeError, match="GPU"):
         d.dream_episodes(z, h)
+
+
+def test_world_model_gradient_buckets_partition_the_flat_buffer():
+    """The three DP all-reduce buckets (DR_WM_BWD_HEADS / _SCAN / _ENC, world_model._grad_buckets)
+    are disjoint, contiguous, cover every parameter, and hold exactly the
+    parameters each backward stage finalises (include/dreamer_hip.h)."""
+    from dreamer_amd import Dreamer
+    from dreamer_amd.agent import _Flat
+    d = Dreamer(dict(FULL), torch.device("cpu"))
+    wm = d.world_model
+    f = _Flat(wm)
+    (h0, h1), (s0, s1), (e0, e1) = wm._grad_buckets(f)
+    assert e0 == 0 and e1 == s0 and s1 == h0 and h1 == f.numel
+    for n in f.names:
+        o = f.offsets[n]
+        if n.startswith("encoder.feature_extractor."):
+            assert e0 <= o < e1, n
+        elif n.startswith(("encoder.latent_mapper.", "sequence_model.")):
+            assert s0 <= o < s1, n
+        else:
+            assert h0 <= o < h1, n
+    print(f"bucket MB: heads+decoder {(h1 - h0) * 4e-6:.1f}, scan {(s1 - s0) * 4e-6:.1f}, "
+          f"encoder {(e1 - e0) * 4e-6:.1f}")
+
+
+def test_vector_observation_mode_host_side():
+    """configs[4] vector observations: module shapes, dims and every workspace
+    query computed on the host without a GPU (a zero conv-plane size must not
+    reach an integer division)."""
+    from dreamer_amd import Dreamer
+    from dreamer_amd import _lib as L
+    cfg = dict(FULL)
+    cfg.update(observation_dims=[24], batch_size=4, sequence_length=8, horizon=6)
+    d = Dreamer(cfg, torch.device("cpu"))
+    sd = d.state_dict()
+    assert tuple(sd["world_model.encoder.feature_extractor.0.weight"].shape) == (256, 24)
+    assert tuple(sd["world_model.decoder.image_builder.2.weight"].shape) == (24, 256)
+    assert d.buffer.observation_buffer.dtype == np.float32
+    dims = d.world_model.dims(d.agent)
+    assert dims.obs_dim == 24 and dims.img_h == 0
+    for name, args in (("dr_encoder_workspace_bytes", (100,)), ("dr_observe_workspace_bytes", (100,)),
+                       ("dr_decoder_workspace_bytes", (100,)), ("dr_wm_train_workspace_bytes", (4, 6)),
+                       ("dr_imagine_workspace_bytes", (4, 6))):
+        assert L.query(name, dims, *args) > 0, name
