@@ -232,6 +232,23 @@ __device__ __forceinline__ dr_u4 dr_rand4(const unsigned long long* so, uint32_t
   dr_u4 c = {(uint32_t)off, (uint32_t)(off >> 32) ^ (stream * 0x85EBCA6Bu), row, elem};
   return philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
+// the same with the {seed, offset} pair already in registers (prefetched at
+// kernel entry: the epilogue then pays no dependent load of the RNG state)
+__device__ __forceinline__ dr_u4 dr_rand4_k(unsigned long long seed, unsigned long long off, uint32_t stream,
+                                            uint32_t row, uint32_t elem) {
+  dr_u4 c = {(uint32_t)off, (uint32_t)(off >> 32) ^ (stream * 0x85EBCA6Bu), row, elem};
+  return philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+__device__ __forceinline__ float dr_exp1_k(unsigned long long seed, unsigned long long off, uint32_t stream,
+                                           uint32_t row, uint32_t elem) {
+  return -logf(dr_u01(dr_rand4_k(seed, off, stream, row, elem).x));
+}
+__device__ __forceinline__ float dr_normal_k(unsigned long long seed, unsigned long long off, uint32_t stream,
+                                             uint32_t row, uint32_t elem) {
+  dr_u4 r = dr_rand4_k(seed, off, stream, row, elem);
+  float u1 = dr_u01(r.x), u2 = dr_u01(r.y);
+  return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+}
 // Exp(1) variate for (stream,row,elem) -- element-exact, independent of launch shape
 __device__ __forceinline__ float dr_exp1(const unsigned long long* so, uint32_t stream, uint32_t row,
                                          uint32_t elem) {

@@ -405,6 +405,12 @@ __global__ __launch_bounds__(64 * DR_SKW) void k_gemm_skinny(GemmBatch gb) {
     }
   }
 
+  // Philox state of the sampler / actor epilogues, fetched now (not after the K loop)
+  unsigned long long rng_seed = 0, rng_off = 0;
+  if ((EPI == EPI_SAMPLE || EPI == EPI_ACTOR) && g.epi != EPI_NONE && !g.noise.q && !g.noise.eps && g.noise.rng) {
+    rng_seed = g.noise.rng[0];
+    rng_off = g.noise.rng[1];
+  }
   const int kw = ((K + NWAVE * 16 - 1) / (NWAVE * 16)) * 16;
   const int kb = wave * kw;
   const int ke = min(K, kb + kw);
@@ -917,8 +923,8 @@ __global__ __launch_bounds__(64 * DR_SKW) void k_gemm_skinny(GemmBatch gb) {
       const int Rg = g.R;
       if (act) {
         if (g.noise.q) qv = dr_g(g.noise.q)[((long long)g.step * M * Rg + (long long)m * Rg + grp) * C + c];
-        else qv = dr_exp1(g.noise.rng, (uint32_t)(g.noise.stream + g.step), (uint32_t)(g.noise.row0 + m),
-                          (uint32_t)(grp * C + c));
+        else qv = dr_exp1_k(rng_seed, rng_off, (uint32_t)(g.noise.stream + g.step), (uint32_t)(g.noise.row0 + m),
+                            (uint32_t)(grp * C + c));
       }
       float best = act ? ph / qv : -INFINITY;
       int bi = act ? c : 0x7fffffff;
@@ -953,8 +959,8 @@ __global__ __launch_bounds__(64 * DR_SKW) void k_gemm_skinny(GemmBatch gb) {
       } else {
         float e;
         if (g.noise.eps) e = dr_g(g.noise.eps)[((long long)g.step * M + m) * A + i];
-        else e = dr_normal(g.noise.rng, (uint32_t)(g.noise.stream + g.step), (uint32_t)(g.noise.row0 + m),
-                           (uint32_t)i);
+        else e = dr_normal_k(rng_seed, rng_off, (uint32_t)(g.noise.stream + g.step), (uint32_t)(g.noise.row0 + m),
+                             (uint32_t)i);
         if (g.eps_save) dr_g(g.eps_save)[(long long)m * A + i] = e;
         av = tanhf(muv + e * sg);
       }
@@ -1205,7 +1211,7 @@ static bool skinny_offsets_ok(const GemmArgs& g, bool b_kn) {
 // debug build; the product library has no process-wide mutable state here.
 #ifdef DR_PHASE_TIMING
 static size_t g_min_lds = 0;       // minimum dynamic LDS per skinny workgroup (bytes)
-static int g_skinny_variant = 0;   // 1 = 64-row tiles for M <= 64, 2 = never 32-column tiles
+static int g_skinny_variant = 0;   // 1 = 64-row tiles for M <= 64, 2 = never 32-column tiles, 5 = 64-row sampler tiles
 static int g_tile_wgs = 512;       // split-K target: workgroups per launch
 static int g_tile_variant = 0;     // tile-GEMM shape variant
 extern "C" void dr_debug_gemm_min_lds(long long bytes) { g_min_lds = (size_t)bytes; }
@@ -1287,7 +1293,8 @@ static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
   // 16-row tiles past 64 rows while the grid stays within ~2.5 dispatch
   // rounds: a B = 256 per-step product (N = 200) then spreads over 208
   // workgroups instead of 52 (K = 1624: 19.3 -> 8.4 us, profiles/r02_kbench_B256.txt)
-  if (g_skinny_variant == 0 && maxM > 64 && (AMODE == AM_PLAIN || AMODE == AM_LNSILU)) {
+  if ((g_skinny_variant == 0 || g_skinny_variant == 5) && maxM > 64 && (AMODE == AM_PLAIN || AMODE == AM_LNSILU) &&
+      !(g_skinny_variant == 5 && epi == EPI_SAMPLE)) {
     int t16 = 0;
     for (int i = 0; i < count; ++i) t16 += dr_cdiv(gb.p[i].M, 16) * dr_cdiv(gb.p[i].N, epi == EPI_SAMPLE ? 32 : 16);
     if (t16 <= 640) maxM = 64;
@@ -1662,7 +1669,7 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
     if (!A_KM && !B_KN && maxM >= 128 && maxM <= 512) {
       int tiles32 = 0;
       for (int i = 0; i < count; ++i) tiles32 += dr_cdiv(gb.p[i].M, 32) * dr_cdiv(gb.p[i].N, 32);
-      if (g_tile_variant == 0 && (minK >= 1024 || (minK >= 512 && tiles32 >= 256))) {
+      if (g_tile_variant == 0 && maxM <= 512 && (minK >= 1024 || (minK >= 512 && tiles32 >= 256))) {
         GemmBatch gt = gb;
         if (tiles32 >= 256)
           for (int i = 0; i < count; ++i) gt.p[i].splitk_ws = nullptr;
@@ -1675,6 +1682,14 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
     // 64 x 64, no split-K scratch) runs on 52+ skinny 64-row workgroups instead
     if (A_KM || (maxM >= 256 && minK >= 512 && (ws || tiles >= 128)) || (g_tile_variant >= 4 && maxM >= 128)) {
       GemmBatch gt = gb;
+      // tall NT products with a deep K (the encoder feature projection, the
+      // critic's first layer over B*(H+1) rows): 8 waves as 4 x 2 over 64 x 64
+      // with K chunks of 64 -- 198 -> 171 us (M 8192, K 4096), 51 -> 47 us
+      // (M 4096, K 1624), profiles/r02m_kbench_tall_tiles.txt
+      if (g_tile_variant == 0 && !A_KM && !B_KN && minK >= 1024) {
+        launch_tile2<64, 64, 64, false, false, 8>(gt, count, s);
+        return;
+      }
       switch (g_tile_variant) {
         case 1: launch_tile2<64, 64, 64, A_KM, B_KN>(gt, count, s); break;
         case 2: launch_tile2<128, 64, 32, A_KM, B_KN>(gt, count, s); break;

@@ -432,6 +432,49 @@ int main(int argc, char** argv) {
     }
     dr_debug_tile_variant(0);
   }
+  // tall products: the encoder feature projection (M = B*S/2 frames, K = 4096)
+  // and the critic's first layer over B*(H+1) rows, by tile variant
+  {
+    float* Xb = frand((size_t)8192 * 4096);
+    float* Wb = frand((size_t)256 * 4096);
+    float* Yb = frand((size_t)8192 * 256);
+    float* skw = frand((size_t)4 * 8192 * 256);
+    for (int var : {0, 4, 5, 6, 7}) {
+      dr_debug_tile_variant(var);
+      int shp[][3] = {{8192, 200, 4096}, {4096, 200, 1624}, {2048, 200, 4096}};
+      for (auto& sh : shp) {
+        GemmArgs g = gemm_args();
+        g.M = sh[0]; g.N = sh[1]; g.K = sh[2]; g.A = Xb; g.lda = sh[2]; g.ksplitA = sh[2]; g.W = Wb; g.ldb = sh[2];
+        g.bias = bias; g.Y = Yb; g.ldy = sh[1];
+        g.splitk_ws = skw; g.splitk_floats = 4LL * 8192 * 256;
+        snprintf(buf, sizeof buf, "tw%d NT M%d N%d K%d (split-K scratch)", var, sh[0], sh[1], sh[2]);
+        timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, &g, 1, st); }, s);
+      }
+    }
+    dr_debug_tile_variant(0);
+  }
+  // the prior head's last layer with the sampler epilogue (LN-SiLU prologue,
+  // N = 1024 = 32 groups x 32 classes): default 16-row tiles vs 64-row tiles
+  {
+    unsigned long long* rng;
+    CK(hipMalloc(&rng, 16));
+    CK(hipMemset(rng, 0, 16));
+    float* zo = frand((size_t)B * 1024);
+    int* io;
+    CK(hipMalloc(&io, (size_t)B * 32 * 8));
+    for (int var : {0, 5}) {
+      dr_debug_skinny_variant(var);
+      GemmArgs g = nt_(B, 1024, 200);
+      g.ln_g = lng; g.ln_b = lnb;
+      g.epi = EPI_SAMPLE; g.R = 32; g.C = 32; g.unimix = 0.01f / 32;
+      g.noise.rng = rng; g.noise.stream = 7;
+      g.z_out = zo; g.ldz = 1024; g.idx_out = io; g.zval_out = reinterpret_cast<float*>(io + B * 32);
+      g.soft_out = Y; g.ld_soft = 1024; g.Y = nullptr;
+      snprintf(buf, sizeof buf, "ts%d sampler lnsilu M%d N1024 K200", var, B);
+      timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_LNSILU, &g, 1, st); }, s);
+    }
+    dr_debug_skinny_variant(0);
+  }
   // per-step shapes of the imagination / BPTT chain, both row-tile variants
   for (int var = 0; var < 5; ++var) {
     if (var == 1 || var == 2) continue;
