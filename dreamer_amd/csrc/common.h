@@ -201,6 +201,28 @@ __device__ __forceinline__ float group_max(float v, int width) {
   return v;
 }
 
+// (max, lowest index) over the same sub-groups: the pair combine is
+// commutative and associative, so the DPP tree gives the shuffle loop's
+// result -- with 4 DPP moves instead of a chain of LDS-crossbar permutes
+template <int CTRL>
+__device__ __forceinline__ int dr_dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ void arg_step(float& best, int& bi, float ob, int oi) {
+  if (ob > best || (ob == best && oi < bi)) {
+    best = ob;
+    bi = oi;
+  }
+}
+__device__ __forceinline__ void group_argmax(float& best, int& bi, int width) {
+  if (width >= 2) arg_step(best, bi, dr_dpp<0xB1>(best), dr_dpp_i<0xB1>(bi));
+  if (width >= 4) arg_step(best, bi, dr_dpp<0x4E>(best), dr_dpp_i<0x4E>(bi));
+  if (width >= 8) arg_step(best, bi, dr_dpp<0x141>(best), dr_dpp_i<0x141>(bi));
+  if (width >= 16) arg_step(best, bi, dr_dpp<0x140>(best), dr_dpp_i<0x140>(bi));
+  if (width >= 32) arg_step(best, bi, __shfl_xor(best, 16, 64), __shfl_xor(bi, 16, 64));
+  if (width >= 64) arg_step(best, bi, __shfl_xor(best, 32, 64), __shfl_xor(bi, 32, 64));
+}
+
 // ---------------------------------------------------------------------------
 // Philox4x32-10 counter RNG (perf-mode noise).  Keys: (seed), counter:
 // (offset_lo, offset_hi ^ stream, row, element) so a row's noise does not

@@ -138,7 +138,11 @@ static inline int lnbwd_nt(int M, int N, int K, const float* gx, long long ldgx,
   g.Y2 = Y2; g.ldy2 = ldy2; g.nsplitY = nsplitY;
   const bool ok = K % 4 == 0 && K <= (M <= 64 ? 1024 : 256) && M <= 4096 && ldgx % 4 == 0 && ld_pre % 4 == 0 &&
                   ((((uintptr_t)gx | (uintptr_t)pre | (uintptr_t)WT | (uintptr_t)ln.w | (uintptr_t)ln.b) & 15) == 0);
-  if (ok) {
+  // at 128+ rows the staged prologue (recomputed by every column tile, 64-row
+  // tiles) costs more than one elementwise pass + a plain GEMM: B = 256,
+  // N = 1624: 26.5 us fused vs the two launches below
+  const bool split = gpre != nullptr && M >= 128;
+  if (ok && !split) {
     g.pre = pre; g.ld_pre = ld_pre; g.ln_g = ln.w; g.ln_b = ln.b;
     g.a_out = gpre; g.ld_aout = ld_gpre;
     g.sv_gy = gy; g.sv_xh = xh; g.ld_sv = ld_gpre;

@@ -928,14 +928,7 @@ __global__ __launch_bounds__(64 * DR_SKW) void k_gemm_skinny(GemmBatch gb) {
       }
       float best = act ? ph / qv : -INFINITY;
       int bi = act ? c : 0x7fffffff;
-      for (int o = W >> 1; o > 0; o >>= 1) {
-        const float ob = __shfl_xor(best, o, 64);
-        const int oi = __shfl_xor(bi, o, 64);
-        if (ob > best || (ob == best && oi < bi)) {
-          best = ob;
-          bi = oi;
-        }
-      }
+      group_argmax(best, bi, W);
       if (act) {
         dr_g(g.z_out)[(long long)m * g.ldz + grp * C + c] = (c == bi) ? ((1.0f + pu) - pu) : 0.0f;
         if (g.soft_out) dr_g(g.soft_out)[(long long)m * g.ld_soft + grp * C + c] = p;
@@ -943,6 +936,7 @@ __global__ __launch_bounds__(64 * DR_SKW) void k_gemm_skinny(GemmBatch gb) {
         if (g.zval_out && c == bi) dr_g(g.zval_out)[m * Rg + grp] = (1.0f + pu) - pu;
       }
     }
+    DR_TS(dr_tbuf_gemm, 7);
   } else if (EPI == EPI_ACTOR && g.epi == EPI_ACTOR) {
     __syncthreads();
     const int A = g.na;
@@ -1519,14 +1513,7 @@ __global__ __launch_bounds__(512) void k_mlp2_tail(Mlp2Batch mb) {
       }
       float best = act ? ph / qv : -INFINITY;
       int bi = act ? c : 0x7fffffff;
-      for (int o = W >> 1; o > 0; o >>= 1) {
-        const float ob = __shfl_xor(best, o, 64);
-        const int oi = __shfl_xor(bi, o, 64);
-        if (ob > best || (ob == best && oi < bi)) {
-          best = ob;
-          bi = oi;
-        }
-      }
+      group_argmax(best, bi, W);
       if (act) {
         dr_g(g.z_out)[(long long)m * g.ldz + grp * C + c] = (c == bi) ? ((1.0f + pu) - pu) : 0.0f;
         if (g.soft_out) dr_g(g.soft_out)[(long long)m * g.ld_soft + grp * C + c] = p;

@@ -138,14 +138,7 @@ __global__ void k_sample(int M, int R, int C, int W, const float* __restrict__ l
   }
   float best = act ? ph / q : -INFINITY;
   int bi = act ? c : 0x7fffffff;
-  for (int o = W >> 1; o > 0; o >>= 1) {
-    const float ob = __shfl_xor(best, o, 64);
-    const int oi = __shfl_xor(bi, o, 64);
-    if (ob > best || (ob == best && oi < bi)) {
-      best = ob;
-      bi = oi;
-    }
-  }
+  group_argmax(best, bi, W);
   if (act) {
     z[(long long)m * ldz + r * C + c] = (c == bi) ? ((1.0f + pu) - pu) : 0.0f;
     if (soft) soft[(long long)m * lds + r * C + c] = p;

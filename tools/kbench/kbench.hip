@@ -472,6 +472,12 @@ int main(int argc, char** argv) {
       g.soft_out = Y; g.ld_soft = 1024; g.Y = nullptr;
       snprintf(buf, sizeof buf, "ts%d sampler lnsilu M%d N1024 K200", var, B);
       timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_LNSILU, &g, 1, st); }, s);
+      phases(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_LNSILU, &g, 1, st); }, dr_debug_tbuf_gemm, s);
+      GemmArgs gn = g;
+      gn.epi = EPI_NONE; gn.Y = Y; gn.ldy = 1024;
+      snprintf(buf, sizeof buf, "ts%d same, plain epilogue", var);
+      timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_LNSILU, &gn, 1, st); }, s);
+      phases(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_LNSILU, &gn, 1, st); }, dr_debug_tbuf_gemm, s);
     }
     dr_debug_skinny_variant(0);
   }
