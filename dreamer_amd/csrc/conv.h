@@ -15,6 +15,12 @@ enum { CONV_EPI_FWD = 0, CONV_EPI_DSILU = 1 };
 int op_conv_nhwc_ex(int n, int cin, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
                     float* out, int out_nchw, float* pre, int epi, hipStream_t s);
 int op_frames_nhwc4(int n, int nb, int h, int w, const dr_frames* src, float* out, hipStream_t s);
+// first conv straight from the frames (u8 ring or f32 tensor): the frame rows
+// a tile reads are normalised into LDS once, no NHWC4 f32 copy in HBM.  Same
+// fragments and MFMA order as op_frames_nhwc4 + k_conv1_direct: bitwise equal.
+// Returns DR_E_INVALID (nothing launched) for shapes it does not tile.
+int op_conv1_frames(int n, int nb, int ih, int iw, int cout, const dr_frames* src, const float* wr, const float* bias,
+                    float* out, hipStream_t s);
 int op_conv_repack_pad(int cout, int cin, int cin_pad, const float* w, float* wr, hipStream_t s);
 
 // ---- conv_bf16.hip (bf16 perf mode; activations bf16, accumulation f32) ----

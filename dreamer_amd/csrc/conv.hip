@@ -295,6 +295,208 @@ __global__ __launch_bounds__(256) void k_conv1_direct(int n_frames, int ih, int 
 }
 
 
+// k_conv1_direct fed from the frames themselves (with the hardware-exp2 SiLU,
+// so no longer bitwise equal to it: ~2 ulp, tests/test_gpu_bf16.py checks the
+// fp32 stack against torch at 1e-5).  A workgroup's 128 output
+// pixels are 128 / ow whole output rows of one frame, which read 2*128/ow + 2
+// input rows: the workgroup loads them once (u8 NCHW planes as 4-byte loads
+// along x, or f32 float4s), applies x/255 - 0.5 (Dreamer.py:251, the same IEEE
+// div-then-sub as k_frames_nhwc4) and writes NHWC4 with zero rows / columns
+// for the padding into LDS; every lane then reads its A fragments (4 channels
+// of one pixel-tap) from LDS exactly as k_conv1_direct reads them from HBM.
+#define C1F_MAXW 130  // iw + 2 pad columns, iw <= 128
+#define C1F_MAXR 10   // 2 * (128 / ow) + 2 input rows, ow >= 32
+template <int IW>  // frame width (64: CarRacing, 128: configs[3]); the frame height is a runtime multiple
+__global__ __launch_bounds__(256) void k_conv1_frames(int n_frames, int nb, int ih, int cout, int tpw, dr_frames src,
+                                                      const float* __restrict__ wr, const float* __restrict__ bias,
+                                                      float* __restrict__ out) {
+  constexpr int K = 64, WPX = 32, iw = IW, ow = IW / 2, ro = 128 / ow, ri = 2 * ro + 2, xw = iw + 2;
+  static_assert(ri <= C1F_MAXR && xw <= C1F_MAXW, "conv1_frames tile");
+  constexpr int x4n = iw / 4, items = ri * 3 * x4n, NIT = (items + 255) / 256;
+  // staged frame rows (NHWC4 + pad columns) and the output tile (128 x 36 floats)
+  __shared__ __attribute__((aligned(16))) float xs[ri * xw * 4];
+  __shared__ __attribute__((aligned(16))) float os[128 * 36];
+  // 32-bit index math throughout (n_frames * hw < 2^31, host-checked)
+  const int oh = ih / 2, hw = oh * ow;
+  const int tiles_n = cout / 32;
+  const int tiles = (n_frames * hw / 128) * tiles_n;
+  const int groups = (tiles + tpw - 1) / tpw;
+  const int lg = dr_xcd_tile(blockIdx.x, groups);
+  if (lg < 0) return;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
+  const int plane = ih * iw;
+  const int t_begin = lg * tpw, t_end = min(tiles, t_begin + tpw);
+  // u8 -> x/255 - 0.5 by table: the same IEEE div-then-sub values, one LDS read each
+  __shared__ float lut[256];
+  lut[tid] = src.raw255 ? (float)tid / 255.0f - 0.5f : (float)tid;
+
+  // this workgroup's run of tiles, software-pipelined: the frame rows of tile
+  // k+1 (a window-start load, then the row loads) are in flight while tile k
+  // runs its MFMAs and stores
+  float vv[NIT][4];
+  int cur_n0 = 0;
+#define C1F_ISSUE(LT)                                                                                   \
+  do {                                                                                                  \
+    const int mt_ = ((LT) / tiles_n) * 128, f_ = mt_ / hw;                                             \
+    const int b_ = (int)(f_ % nb), t_ = (int)(f_ / nb) + src.t0;                                       \
+    const unsigned char* fr8 =                                                                          \
+        src.ring ? src.ring + ((src.starts[b_] + t_) % src.ring_cap) * 3 * plane : nullptr;             \
+    const float* fr32 = src.ring ? nullptr : src.obs + (long long)b_ * src.stride_b + (long long)t_ * src.stride_t; \
+    const int y0_ = 2 * ((int)(mt_ - f_ * hw) / ow) - 1;                                                \
+    _Pragma("unroll") for (int k = 0; k < NIT; ++k) {                                                   \
+      const int it = tid + 256 * k;                                                                     \
+      const int yy = it / (3 * x4n), rem = it - yy * 3 * x4n, c = rem / x4n, x4 = rem - c * x4n;      \
+      const int y = y0_ + yy;                                                                           \
+      const bool ok = it < items && y >= 0 && y < ih;                                                   \
+      const int o = ok ? c * plane + y * iw + 4 * x4 : 0;                                               \
+      if (fr8) {                                                                                        \
+        const uchar4 u = *reinterpret_cast<const uchar4*>(fr8 + o);                                     \
+        vv[k][0] = (float)u.x; vv[k][1] = (float)u.y; vv[k][2] = (float)u.z; vv[k][3] = (float)u.w;    \
+      } else {                                                                                          \
+        const float4 w4 = *reinterpret_cast<const float4*>(fr32 + o);                                   \
+        vv[k][0] = w4.x; vv[k][1] = w4.y; vv[k][2] = w4.z; vv[k][3] = w4.w;                            \
+      }                                                                                                 \
+    }                                                                                                   \
+  } while (0)
+  // zero pad columns / channel 3 once: the staging pass never writes them
+  for (int i = tid; i < ri * xw; i += 256) {
+    const int xx = i % xw;
+    xs[i * 4 + 3] = 0.f;
+    if (xx == 0 || xx == xw - 1) {
+      xs[i * 4 + 0] = 0.f;
+      xs[i * 4 + 1] = 0.f;
+      xs[i * 4 + 2] = 0.f;
+    }
+  }
+  float4 bw[4][2];  // this channel tile's weights, reloaded only when the channel tile changes
+  if (t_begin < t_end) C1F_ISSUE(t_begin);
+  for (int lt = t_begin; lt < t_end; ++lt) {
+    const int mt = (lt / tiles_n) * 128;
+    const int n0 = (lt % tiles_n) * 32;
+    const int f = mt / hw;
+    const int y0 = 2 * ((int)(mt - f * hw) / ow) - 1;
+    if (lt == t_begin || n0 != cur_n0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int sl = 0; sl < 4; ++sl)
+          bw[sl][j] = *reinterpret_cast<const float4*>(wr + (long long)(n0 + 16 * j + r) * K + 16 * sl + 4 * q);
+      cur_n0 = n0;
+    }
+    __syncthreads();  // the previous tile's fragment reads of xs are done
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int it = tid + 256 * k;
+      if (it >= items) break;
+      const int yy = it / (3 * x4n), rem = it - yy * 3 * x4n, c = rem / x4n, x4 = rem - c * x4n;
+      const int y = y0 + yy;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (y >= 0 && y < ih) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = src.ring ? lut[(int)vv[k][e]] : (src.raw255 ? vv[k][e] / 255.0f - 0.5f : vv[k][e]);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xs[(yy * xw + 4 * x4 + e + 1) * 4 + c] = v[e];
+    }
+    __syncthreads();
+    if (lt + 1 < t_end) C1F_ISSUE(lt + 1);
+
+    float4 a[4][2];
+    const int m0 = mt + wave * WPX;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int p = (int)(m0 + 16 * i + r - f * hw), oy = p / ow, ox = p - oy * ow;
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl) {
+        const int tap = 4 * sl + q;
+        const int yy = 2 * oy - 1 + (tap >> 2) - y0, xx = 2 * ox + (tap & 3);  // xx = x + 1 (pad column)
+        a[sl][i] = *reinterpret_cast<const float4*>(&xs[(yy * xw + xx) * 4]);
+      }
+    }
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bw[sl][j].x, a[sl][i].x, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bw[sl][j].y, a[sl][i].y, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bw[sl][j].z, a[sl][i].z, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bw[sl][j].w, a[sl][i].w, acc[i][j], 0, 0, 0);
+    }
+    // the tile is one contiguous 16 KB NHWC run when cout == 32: stage it in
+    // LDS and store whole 1 KB pieces per wave instruction
+    const bool contiguous = cout == 32;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const long long m = m0 + 16 * i + r;
+        const int co = n0 + 16 * j + 4 * q;
+        const float4 bv = *reinterpret_cast<const float4*>(bias + co);
+        float4 v = make_float4(acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w);
+        // hardware exp2 / reciprocal SiLU (~2 ulp; this output-heavy layer
+        // spent most of its VALU time in the IEEE expf + division)
+        v.x = dr_silu_fast(v.x);
+        v.y = dr_silu_fast(v.y);
+        v.z = dr_silu_fast(v.z);
+        v.w = dr_silu_fast(v.w);
+        if (contiguous)
+          *reinterpret_cast<float4*>(&os[(wave * WPX + 16 * i + r) * 36 + 16 * j + 4 * q]) = v;
+        else
+          *reinterpret_cast<float4*>(out + m * cout + co) = v;
+      }
+    if (contiguous) {
+      __syncthreads();
+      float* dst = out + (long long)mt * 32;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = tid + 256 * k, px = e >> 3, c4 = e & 7;
+        *reinterpret_cast<float4*>(dst + 4 * e) = *reinterpret_cast<const float4*>(&os[px * 36 + 4 * c4]);
+      }
+    }
+  }
+#undef C1F_ISSUE
+}
+
+int op_conv1_frames(int n, int nb, int ih, int iw, int cout, const dr_frames* src, const float* wr, const float* bias,
+                    float* out, hipStream_t s) {
+  const int ow = iw / 2, hw = (ih / 2) * ow;
+  const bool src_ok = src->ring ? (src->starts && src->ring_cap > 0)
+                                : (src->obs && src->stride_b % 4 == 0 && src->stride_t % 4 == 0 &&
+                                   ((uintptr_t)src->obs & 15) == 0);
+  if (n <= 0 || nb <= 0 || cout % 32 != 0 || ih % 2 || iw % 8 || ow < 32 || ow > 128 || 128 % ow != 0 ||
+      hw % 128 != 0 || 2 * (128 / ow) + 2 > C1F_MAXR || iw + 2 > C1F_MAXW || !src_ok) {
+    dr_set_error("conv1_frames: unsupported shape (ih=%d iw=%d cout=%d)", ih, iw, cout);
+    return DR_E_INVALID;
+  }
+  const long long tiles = ((long long)n * hw / 128) * (cout / 32);
+  if (tiles >= (1LL << 30) || (long long)n * hw >= (1LL << 31) || (iw != 64 && iw != 128)) {
+    dr_set_error("conv1_frames: too many tiles or width not 64 / 128");
+    return DR_E_INVALID;
+  }
+  // one tile per workgroup: a 4-tile pipelined run was measured slower
+  // (688 vs 620 us at 8192 frames: fewer waves resident, more barriers)
+  const int tpw = 1;
+  const dim3 grid((unsigned)dr_xcd_grid((int)((tiles + tpw - 1) / tpw)));
+  if (iw == 64) hipLaunchKernelGGL(k_conv1_frames<64>, grid, dim3(256), 0, s, n, nb, ih, cout, tpw, *src, wr, bias, out);
+  else hipLaunchKernelGGL(k_conv1_frames<128>, grid, dim3(256), 0, s, n, nb, ih, cout, tpw, *src, wr, bias, out);
+  return dr_check_launch("conv1_frames");
+}
+
 template <int BM, int BN, int CIN, bool OUT_NCHW, int EPI>
 static int launch_conv(int n, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
                        float* out, float* pre, hipStream_t s) {

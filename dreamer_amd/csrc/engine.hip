@@ -112,9 +112,12 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
   DR_TRY(op_conv_repack_pad(c2, c1, c1, wm->conv[1].w, w.wr2, s));
   DR_TRY(op_conv_repack_pad(c3, c2, c2, wm->conv[2].w, w.wr3, s));
   DR_TRY(op_conv_repack_pad(c4, c3, c3, wm->conv[3].w, w.wr4, s));
-  // frames (u8 ring or f32) -> normalised NHWC4, then four NHWC implicit GEMMs
-  DR_TRY(op_frames_nhwc4(n, B, h0, w0, src, w.x0, s));
-  DR_TRY(op_conv_nhwc(n, 4, h0, w0, c1, w.x0, w.wr1, wm->conv[0].b, w.a1, 0, s));
+  // the first conv straight from the frames (u8 ring or f32); shapes it does
+  // not tile go through the normalised NHWC4 copy.  Then NHWC implicit GEMMs
+  if (op_conv1_frames(n, B, h0, w0, c1, src, w.wr1, wm->conv[0].b, w.a1, s) != DR_OK) {
+    DR_TRY(op_frames_nhwc4(n, B, h0, w0, src, w.x0, s));
+    DR_TRY(op_conv_nhwc(n, 4, h0, w0, c1, w.x0, w.wr1, wm->conv[0].b, w.a1, 0, s));
+  }
   DR_TRY(op_conv_nhwc(n, c1, h0 / 2, w0 / 2, c2, w.a1, w.wr2, wm->conv[1].b, w.a2, 0, s));
   DR_TRY(op_conv_nhwc(n, c2, h0 / 4, w0 / 4, c3, w.a2, w.wr3, wm->conv[2].b, w.a3, 0, s));
   // last layer in NCHW == nn.Flatten order of Encoder.forward (VAE.py:72)

@@ -103,3 +103,33 @@ def test_train_agent_bf16_epoch(gpu):
     flips = float((z32.reshape(-1, 32).argmax(-1) != z16.reshape(-1, 32).argmax(-1)).float().mean())
     print(f"fp32 losses ({a32:.5f}, {c32:.5f}), bf16 ({a16:.5f}, {c16:.5f}); warm-start index flips {flips:.3%}")
     assert abs(c16 - c32) <= 0.05 * abs(c32)
+
+
+@pytest.mark.parametrize("res", [64, 128])
+def test_encoder_fp32_from_frames_matches_torch(gpu, res):
+    """fp32 parity mode: dr_encoder_features (first conv straight from the u8
+    frames, k_conv1_frames; then the NHWC implicit GEMMs) against the plain
+    torch fp32 conv stack on the same frames: normwise relative error <= 1e-5
+    (f32 summation order only)."""
+    from dreamer_amd import Dreamer
+    from formula import FULL
+    cfg = dict(FULL)
+    cfg.update(observation_dims=[res, res])
+    torch.manual_seed(0)
+    d = Dreamer(cfg, gpu)
+    wm = d.world_model
+    g = torch.Generator().manual_seed(2)
+    n = 40 if res == 64 else 12
+    frames = torch.randint(0, 256, (n, 3, res, res), generator=g, dtype=torch.uint8)
+    dims = wm.dims(d.agent)
+    got = _features(wm.packed(), dims, frames, gpu)
+    P = {k: v.detach().cpu() for k, v in wm.encoder.state_dict().items()}
+    x = frames.float() / 255.0 - 0.5
+    for i in range(4):
+        x = F.silu(F.conv2d(x, P[f"feature_extractor.{2 * i}.weight"], P[f"feature_extractor.{2 * i}.bias"],
+                            stride=2, padding=1))
+    flat = x.flatten(1)
+    ref = flat @ P["latent_mapper.0.weight"][:, :flat.shape[1]].t() + P["latent_mapper.0.bias"]
+    err = float((got - ref).norm() / ref.norm())
+    print(f"res {res}: fp32 encoder vs torch {err:.2e}")
+    assert err <= 1e-5
