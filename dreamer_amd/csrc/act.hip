@@ -21,6 +21,7 @@
 // agent-scope acquire loads; a bounded spin turns a lost workgroup into NaN
 // outputs instead of a hung GPU.
 #include "common.h"
+#include "ops.h"
 
 #include <string.h>
 
@@ -531,11 +532,9 @@ extern "C" int dr_act_step(const dr_dims* d, const dr_world_model* wm, const dr_
   size_t off = 0;
   act_carve((char*)ws, d, a, off);
   DR_REQUIRE(off <= ws_bytes, "workspace too small");
-  hipError_t e = hipMemsetAsync(a.bar, 0, ACT_BAR_BYTES + 512, s);  // barrier lines + fail flag
-  if (e != hipSuccess) {
-    dr_set_error("dr_act_step: %s", hipGetErrorString(e));
-    return DR_E_HIP;
-  }
+  // barrier lines + fail flag (a kernel, so a captured graph re-arms them too)
+  static_assert((ACT_BAR_BYTES + 512) % 4 == 0, "barrier bytes");
+  DR_TRY(op_fill((ACT_BAR_BYTES + 512) / 4, reinterpret_cast<float*>(a.bar), 0.f, s));
   static const bool raised = [] {
     (void)hipFuncSetAttribute((const void*)k_act_step, hipFuncAttributeMaxDynamicSharedMemorySize, ACT_LDS * 4);
     return true;

@@ -160,6 +160,7 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
                                const float* z_init, dr_noise noise, float* z_out, float* h_out, float* logits_out,
                                void* ws, size_t ws_bytes, hipStream_t s) {
   DR_REQUIRE(d && wm && feat && z_out && h_out && B > 0 && T > 0, "null argument or empty batch");
+  GemmBf16Scope bf16_scope(d->precision == DR_PREC_BF16);
   DR_REQUIRE(T == 1 || (z_init == nullptr ? T > 1 : true), "bad T");
   DR_REQUIRE(actions || (z_init == nullptr && T == 1), "actions required");
   Carve c(ws);
@@ -314,6 +315,7 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
   DR_REQUIRE(d && wm && ac && z0 && h0 && latents && hiddens && actions && rewards && continues && mus && sigmas &&
                  tape && B > 0 && H > 0,
              "null argument or empty batch");
+  GemmBf16Scope bf16_scope(d->precision == DR_PREC_BF16);
   Carve c(ws);
   ImWs w;
   imws_carve(c, d, B, H, w);
@@ -455,6 +457,7 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
                             const void* tape, const dr_actor* gr, void* ws, size_t ws_bytes, hipStream_t s,
                             bool do_prep, bool do_main) {
   DR_REQUIRE(d && wm && ac && B > 0 && H > 0, "null argument or empty batch");
+  GemmBf16Scope bf16_scope(d->precision == DR_PREC_BF16);
   DR_REQUIRE(!do_main || (latents && hiddens && actions && tape && gr), "null argument");
   Carve c(ws);
   ImWs w;
@@ -619,6 +622,7 @@ extern "C" int dr_critic_fwd(const dr_dims* d, const dr_critic* cr, int M, const
                              const float* z, long long ldz, float* logits, float* values, void* tape, void* ws,
                              size_t ws_bytes, hipStream_t s) {
   DR_REQUIRE(d && cr && h && z && M > 0, "null argument or empty batch");
+  GemmBf16Scope bf16_scope(d->precision == DR_PREC_BF16);
   CTape t;
   float* sk = nullptr;
   long long skn = 0;
@@ -696,6 +700,7 @@ extern "C" int dr_critic_loss_bwd(const dr_dims* d, const dr_critic* cr, int B, 
                                   const float* latents, const float* R, const void* tape, float scale,
                                   float* loss_out, const dr_critic* gr, void* ws, size_t ws_bytes, hipStream_t s) {
   DR_REQUIRE(d && cr && hiddens && latents && R && tape && loss_out && gr && B > 0 && H > 0, "null argument");
+  GemmBf16Scope bf16_scope(d->precision == DR_PREC_BF16);
   Carve c(ws);
   CBws w;
   cbws_carve(c, d, B, H, w);

@@ -36,27 +36,13 @@ struct Carve {
     }                                                                                      \
   } while (0)
 
+// kernels, not hipMemcpy2DAsync / hipMemsetAsync: see op_fill in ops.hip
 static inline int copy2d(float* dst, long long dpitch, const float* src, long long spitch, long long width, long long rows,
                   hipStream_t s) {
-  if (rows == 0 || width == 0) return DR_OK;
-  hipError_t e = hipMemcpy2DAsync(dst, dpitch * sizeof(float), src, spitch * sizeof(float), width * sizeof(float),
-                                  rows, hipMemcpyDeviceToDevice, s);
-  if (e != hipSuccess) {
-    dr_set_error("copy2d: %s", hipGetErrorString(e));
-    return DR_E_HIP;
-  }
-  return DR_OK;
+  return op_copy2d(dst, dpitch, src, spitch, width, rows, s);
 }
 
-static inline int zero(float* p, long long n, hipStream_t s) {
-  if (n == 0) return DR_OK;
-  hipError_t e = hipMemsetAsync(p, 0, n * sizeof(float), s);
-  if (e != hipSuccess) {
-    dr_set_error("memset: %s", hipGetErrorString(e));
-    return DR_E_HIP;
-  }
-  return DR_OK;
-}
+static inline int zero(float* p, long long n, hipStream_t s) { return op_fill(n, p, 0.f, s); }
 
 static inline int latent(const dr_dims* d) { return d->rows * d->cols; }
 // encoder feature width F (latent_mapper.0 input minus h): the flattened conv

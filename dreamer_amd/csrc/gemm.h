@@ -51,6 +51,10 @@ struct alignas(16) GemmArgs {
   int na, det;
   float* act_out; long long ld_act; float* mu_out; long long ld_mu; float* sig_out; long long ld_sig;
   float* eps_save; float* ls_save; long long ld_ls;
+  // bf16 perf mode (dr_dims.precision): NT products that take the tile route
+  // run on v_mfma_f32_16x16x32_bf16 with operands rounded to bf16 as they are
+  // staged (f32 accumulation, f32 in / out); set by the engine per call
+  int bf16;
 };
 
 enum { EPI_NONE = 0, EPI_SAMPLE = 1, EPI_ACTOR = 2 };
@@ -58,6 +62,13 @@ enum { EPI_NONE = 0, EPI_SAMPLE = 1, EPI_ACTOR = 2 };
 enum GemmLayout { G_NT = 0, G_NN = 1, G_TN = 2 };
 
 GemmArgs gemm_args();  // zero-initialised with neutral defaults
+// While alive, gemm_args() returns bf16 = on (the engine's bf16 perf mode
+// around the imagination-epoch entry points); restores the previous value.
+struct GemmBf16Scope {
+  explicit GemmBf16Scope(bool on);
+  ~GemmBf16Scope();
+  int prev;
+};
 // Launch up to 4 problems sharing layout/A-mode in one dispatch.
 int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hipStream_t s);
 

@@ -23,9 +23,14 @@ struct GemmBatch {
   GemmArgs p[4];
 };
 
+static thread_local int g_gemm_bf16 = 0;
+GemmBf16Scope::GemmBf16Scope(bool on) : prev(g_gemm_bf16) { g_gemm_bf16 = on ? 1 : 0; }
+GemmBf16Scope::~GemmBf16Scope() { g_gemm_bf16 = prev; }
+
 GemmArgs gemm_args() {
   GemmArgs g;
   memset(&g, 0, sizeof(g));
+  g.bf16 = g_gemm_bf16;
   g.ksplitA = INT_MAX;
   g.ksplitB = INT_MAX;
   g.nsplitB = INT_MAX;
@@ -1171,6 +1176,132 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tile(GemmBatch gb, int splits)
       }
 }
 
+// ---------------------------------------------------------------------------
+// bf16 perf-mode tile GEMM (GemmArgs.bf16): NT, f32 operands in HBM rounded to
+// bf16 (RNE) as they are staged into LDS, v_mfma_f32_16x16x32_bf16 with f32
+// accumulation, the f32 tile kernel's epilogue / split-K.  K chunks of 64:
+// a thread stages units of 8 consecutive k (two float4 loads -> one 16-byte
+// LDS row piece); rows are 40 dwords (8 mod 16): conflict-free ds_read_b128
+// fragments, lane (r, q) reading k = 8q..8q+7 of its row.
+// ---------------------------------------------------------------------------
+typedef __bf16 dr_bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ uint32_t dr_pack_bf16x2(float a, float b) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+template <int BM, int BN, int NW>
+__global__ __launch_bounds__(64 * NW) void k_gemm_tile_b16(GemmBatch gb, int splits) {
+  constexpr int NTH = 64 * NW, KC = 64, UPR = KC / 8, TL = KC / 2 + 8;
+  __shared__ GemmArgs s_args;
+  dr_stage_args(gb.p[blockIdx.z], s_args, threadIdx.x);
+  const GemmArgs& g = s_args;
+  const int M = dr_uni(g.M), N = dr_uni(g.N), K = dr_uni(g.K);
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const int lt = dr_xcd_tile(blockIdx.x, tiles_m * tiles_n);
+  if (lt < 0) return;
+  const int tn = lt / tiles_m, tm = lt - tn * tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nch = (K + KC - 1) / KC;
+  const int per = (nch + splits - 1) / splits;
+  const int c0 = blockIdx.y * per, c1 = min(nch, c0 + per);
+  const float* A = dr_uni(g.A);
+  const float* A2 = dr_uni(g.A2);
+  const float* W = dr_uni(g.W);
+  const int lda = dr_uni((int)g.lda), lda2 = dr_uni((int)g.lda2), ldb = dr_uni((int)g.ldb);
+  const int ksA = dr_uni(g.ksplitA);
+  __shared__ __attribute__((aligned(16))) uint32_t As[2][BM][TL];
+  __shared__ __attribute__((aligned(16))) uint32_t Bs[2][BN][TL];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  constexpr int APT = (BM * UPR + NTH - 1) / NTH, BPT = (BN * UPR + NTH - 1) / NTH;
+  uint4 ra[APT], rb[BPT];
+  auto load = [&](int c) {
+    const int k0 = c * KC;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const int u = tid + NTH * i, row = u / UPR, k = k0 + 8 * (u - row * UPR), m = m0 + row;
+      const bool ok = u < BM * UPR && m < M && k < K;
+      const bool s1 = k < ksA;
+      const float* base = s1 ? A : A2;
+      const unsigned e = ok ? (unsigned)(s1 ? m * lda + k : m * lda2 + k - ksA) : 0u;
+      float4 x0 = dr_ld4(ok ? base : W, e), x1 = dr_ld4(ok ? base : W, e + 4u);
+      if (!ok) x0 = x1 = make_float4(0.f, 0.f, 0.f, 0.f);
+      ra[i] = make_uint4(dr_pack_bf16x2(x0.x, x0.y), dr_pack_bf16x2(x0.z, x0.w), dr_pack_bf16x2(x1.x, x1.y),
+                         dr_pack_bf16x2(x1.z, x1.w));
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int u = tid + NTH * i, row = u / UPR, k = k0 + 8 * (u - row * UPR), n = n0 + row;
+      const bool ok = u < BN * UPR && n < N && k < K;
+      const unsigned e = ok ? (unsigned)(n * ldb + k) : 0u;
+      float4 x0 = dr_ld4(W, e), x1 = dr_ld4(W, e + 4u);
+      if (!ok) x0 = x1 = make_float4(0.f, 0.f, 0.f, 0.f);
+      rb[i] = make_uint4(dr_pack_bf16x2(x0.x, x0.y), dr_pack_bf16x2(x0.z, x0.w), dr_pack_bf16x2(x1.x, x1.y),
+                         dr_pack_bf16x2(x1.z, x1.w));
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const int u = tid + NTH * i, row = u / UPR, uc = u - row * UPR;
+      if (u < BM * UPR) *reinterpret_cast<uint4*>(&As[buf][row][4 * uc]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int u = tid + NTH * i, row = u / UPR, uc = u - row * UPR;
+      if (u < BN * UPR) *reinterpret_cast<uint4*>(&Bs[buf][row][4 * uc]) = rb[i];
+    }
+  };
+  constexpr int WGM = NW / 2;
+  constexpr int WTM = BM / WGM, WTN = BN / 2, FM = WTM / 16, FN = WTN / 16;
+  static_assert(FM >= 1 && FN >= 1, "wave tile");
+  const int wm0 = (wave >> 1) * WTM, wn0 = (wave & 1) * WTN;
+  const int r = lane & 15, q = lane >> 4;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (c0 < c1) {
+    load(c0);
+    store(0);
+  }
+  __syncthreads();
+  for (int c = c0; c < c1; ++c) {
+    const int buf = (c - c0) & 1;
+    if (c + 1 < c1) load(c + 1);  // in flight while this chunk's MFMAs run
+#pragma unroll
+    for (int s = 0; s < KC / 32; ++s) {
+      uint4 a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const uint4*>(&As[buf][wm0 + 16 * i + r][16 * s + 4 * q]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const uint4*>(&Bs[buf][wn0 + 16 * j + r][16 * s + 4 * q]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(dr_bf16x8, a[i]),
+                                                              __builtin_bit_cast(dr_bf16x8, b[j]), acc[i][j], 0, 0, 0);
+    }
+    if (c + 1 < c1) store(buf ^ 1);
+    __syncthreads();
+  }
+  float* part = g.splitk_ws;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm0 + 16 * i + 4 * q + e, n = n0 + wn0 + 16 * j + r;
+        if (m >= M || n >= N) continue;
+        if (splits == 1) epilogue_store(g, m, n, acc[i][j][e]);
+        else dr_g(part)[((long long)blockIdx.y * M + m) * N + n] = acc[i][j][e];
+      }
+}
+
 __global__ __launch_bounds__(256) void k_splitk_finish(GemmBatch gb, int splits) {
   const GemmArgs& g = gb.p[blockIdx.z];
   const long long MN = (long long)g.M * g.N;
@@ -1624,6 +1755,46 @@ static void launch_tile2(GemmBatch& gb, int count, hipStream_t s) {
 }
 
 
+// bf16 tile launcher: split-K as launch_tile2 (partials + k_splitk_finish)
+template <int BM, int BN, int NW>
+static void launch_tile_b16(GemmBatch& gb, int count, hipStream_t s) {
+  int maxt = 0, nch = 1 << 30, tot = 0;
+  long long maxMN = 0;
+  bool ws = true;
+  for (int i = 0; i < count; ++i) {
+    const GemmArgs& g = gb.p[i];
+    const int t = dr_cdiv(g.M, BM) * dr_cdiv(g.N, BN);
+    maxt = std::max(maxt, t);
+    tot += t;
+    nch = std::min(nch, dr_cdiv(g.K, 64));
+    maxMN = std::max(maxMN, (long long)g.M * g.N);
+    ws = ws && g.splitk_ws != nullptr;
+  }
+  if (maxt == 0) return;
+  int splits = 1;
+  if (ws && tot < 256) {
+    splits = std::max(1, std::min(DR_TILE_SPLITS, dr_cdiv(512, tot)));
+    splits = std::min(splits, std::max(1, nch / 2));
+    for (int i = 0; i < count; ++i)
+      while (splits > 1 && (long long)splits * gb.p[i].M * gb.p[i].N > gb.p[i].splitk_floats) --splits;
+  }
+  dim3 grid(dr_xcd_grid(maxt), splits, count);
+  hipLaunchKernelGGL((k_gemm_tile_b16<BM, BN, NW>), grid, dim3(64 * NW), 0, s, gb, splits);
+  if (splits > 1)
+    hipLaunchKernelGGL(k_splitk_finish, dim3((unsigned)((maxMN + 255) / 256), 1, count), dim3(256), 0, s, gb, splits);
+}
+
+// every problem bf16 and 16-byte-aligned 8-wide k runs (ksplitA on an 8 boundary)
+static bool b16_ok(const GemmBatch& gb, int count) {
+  for (int i = 0; i < count; ++i) {
+    const GemmArgs& g = gb.p[i];
+    if (!g.bf16 || g.K % 8 || g.lda % 4 || g.ldb % 4 || ((uintptr_t)g.A & 15) || ((uintptr_t)g.W & 15)) return false;
+    if (g.ksplitA < g.K && (g.ksplitA % 8 || g.lda2 % 4 || ((uintptr_t)g.A2 & 15))) return false;
+    if (g.W2 || g.epi != EPI_NONE || g.out_conv) return false;
+  }
+  return true;
+}
+
 static bool tile_offsets_ok(const GemmBatch& gb, int count) {
   const long long lim = 1LL << 30;
   for (int i = 0; i < count; ++i) {
@@ -1660,7 +1831,8 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
         GemmBatch gt = gb;
         if (tiles32 >= 256)
           for (int i = 0; i < count; ++i) gt.p[i].splitk_ws = nullptr;
-        launch_tile2<32, 32, 64, false, false, 4>(gt, count, s);
+        if (b16_ok(gb, count)) launch_tile_b16<32, 32, 4>(gt, count, s);
+        else launch_tile2<32, 32, 64, false, false, 4>(gt, count, s);
         return;
       }
     }
@@ -1674,7 +1846,8 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
       // with K chunks of 64 -- 198 -> 171 us (M 8192, K 4096), 51 -> 47 us
       // (M 4096, K 1624), profiles/r02m_kbench_tall_tiles.txt
       if (g_tile_variant == 0 && !A_KM && !B_KN && minK >= 1024) {
-        launch_tile2<64, 64, 64, false, false, 8>(gt, count, s);
+        if (b16_ok(gb, count)) launch_tile_b16<64, 64, 8>(gt, count, s);
+        else launch_tile2<64, 64, 64, false, false, 8>(gt, count, s);
         return;
       }
       switch (g_tile_variant) {

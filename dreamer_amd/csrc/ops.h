@@ -51,6 +51,8 @@ int op_actor_head_bwd(int M, int A, const float* g_a, long long ldga, const floa
                       hipStream_t s);
 int op_conv_repack(int cout, int cin, const float* w, float* wr, hipStream_t s);
 int op_fill(long long n, float* x, float v, hipStream_t s);
+int op_copy2d(float* dst, long long dp, const float* src, long long sp, long long width, long long rows,
+              hipStream_t s);
 int op_mean(int n, const float* x, float* out, hipStream_t s);
 
 // Vector observations (dr_dims.obs_dim = D > 0): frame f = t*nb + b of `src`

@@ -3,6 +3,8 @@
 // optimiser.  Built with -ffp-contract=off: each expression rounds like the
 // corresponding PyTorch CPU op sequence of the reference (cited per kernel).
 #include <stdarg.h>
+
+#include <algorithm>
 #include <stdio.h>
 
 #include "ops.h"
@@ -1147,15 +1149,54 @@ extern "C" int dr_nonfinite(long long n, const float* x, int* flag, hipStream_t 
 // ---------------------------------------------------------------------------
 // misc
 // ---------------------------------------------------------------------------
+// Fills and strided copies are kernels, not hipMemsetAsync / hipMemcpy2DAsync:
+// inside a captured phase graph the runtime's memset / 2-D copy nodes were
+// seen not to re-execute on replay on this stack (the BPTT's zeroed gradient
+// accumulators then carried the previous epoch's values:
+// tests/test_gpu_determinism.py), while kernel nodes always do.
 __global__ void k_fill(long long n, float* x, float v) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] = v;
 }
+__global__ void k_fill4(long long n4, float4* x, float v) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x)
+    x[i] = make_float4(v, v, v, v);
+}
 
 int op_fill(long long n, float* x, float v, hipStream_t s) {
   if (n <= 0) return DR_OK;
-  hipLaunchKernelGGL(k_fill, dim3(blocks_for(n, 256)), dim3(256), 0, s, n, x, v);
+  if (((uintptr_t)x & 15) == 0 && n % 4 == 0) {
+    const long long n4 = n / 4;
+    hipLaunchKernelGGL(k_fill4, dim3((unsigned)std::min<long long>(blocks_for(n4, 256), 2048)), dim3(256), 0, s, n4,
+                       reinterpret_cast<float4*>(x), v);
+  } else {
+    hipLaunchKernelGGL(k_fill, dim3(blocks_for(n, 256)), dim3(256), 0, s, n, x, v);
+  }
   return dr_check_launch("fill");
+}
+
+// rows x width floats, row pitches dp / sp (floats); float4 when everything is
+// 16-byte aligned
+template <bool V4>
+__global__ void k_copy2d(float* dst, long long dp, const float* src, long long sp, long long width, long long rows) {
+  const long long wv = V4 ? width / 4 : width;
+  const long long total = wv * rows;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / wv, c = i - r * wv;
+    if (V4) reinterpret_cast<float4*>(dst + r * dp)[c] = reinterpret_cast<const float4*>(src + r * sp)[c];
+    else dst[r * dp + c] = src[r * sp + c];
+  }
+}
+
+int op_copy2d(float* dst, long long dp, const float* src, long long sp, long long width, long long rows,
+              hipStream_t s) {
+  if (rows <= 0 || width <= 0) return DR_OK;
+  const bool v4 = ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) && dp % 4 == 0 && sp % 4 == 0 && width % 4 == 0;
+  const long long total = (v4 ? width / 4 : width) * rows;
+  const unsigned blocks = (unsigned)std::min<long long>(blocks_for(total, 256), 2048);
+  if (v4) hipLaunchKernelGGL(k_copy2d<true>, dim3(blocks), dim3(256), 0, s, dst, dp, src, sp, width, rows);
+  else hipLaunchKernelGGL(k_copy2d<false>, dim3(blocks), dim3(256), 0, s, dst, dp, src, sp, width, rows);
+  return dr_check_launch("copy2d");
 }
 
 // Conv2d weight [co][ci][4][4] -> [co][tap][ci] for NHWC implicit GEMM

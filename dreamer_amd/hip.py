@@ -1,6 +1,7 @@
 """Glue between the reference-shaped nn.Modules and libdreamer_hip: packs
 parameters (in PyTorch's own layout, no copies) into the C structs, owns
 per-device workspaces and the Philox RNG state."""
+import os
 import threading
 
 import torch
@@ -38,7 +39,11 @@ def flat_linear(flat, offsets, key_w, key_b):
 
 
 class Workspace:
-    """Grow-only scratch buffers on one device, keyed by name."""
+    """Grow-only scratch buffers on one device, keyed by name.
+
+    DREAMER_WS_POISON=all (or a comma list of names) fills new buffers with
+    0xFF bytes (f32 NaN): a kernel that reads scratch it has not written
+    then poisons its outputs (tests/test_gpu_api.py workspace test)."""
 
     def __init__(self, device):
         self.device = device
@@ -49,6 +54,9 @@ class Workspace:
         b = self.bufs.get(name)
         if b is None or b.numel() < nbytes:
             b = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            poison = os.environ.get("DREAMER_WS_POISON", "")
+            if poison == "all" or name in poison.split(","):
+                b.fill_(0xFF)
             self.bufs[name] = b
         return b
 

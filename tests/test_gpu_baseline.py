@@ -169,12 +169,15 @@ def test_baseline_b16_vs_reference(gpu):
     assert abs(pre["S"] - float(fx["S_after"])) <= 1e-6 * float(fx["S_after"])
 
 
-@pytest.mark.parametrize("B", [64, 256])
-def test_epoch_vs_oracle_at_baseline_shape(B, gpu):
+@pytest.mark.parametrize("B,data", [(64, "synthetic"), (256, "synthetic"), (16, "fixture")])
+def test_epoch_vs_oracle_at_baseline_shape(B, data, gpu):
     """configs[1] (B=64) and the north-star batch (B=256), S=64 H=15, full
-    widths, reference default init, synthetic replay."""
+    widths, reference default init, synthetic replay; and B=16 on the tests'
+    fixture replay (formula.replay_data: raw N(0,1) rewards, a terminal at
+    index 37)."""
     import bench
     from dreamer_amd import Dreamer
+    from formula import replay_data
     S, H, R, C, A = 64, 15, 32, 32, 3
     cfg = dict(CAR)
     cfg.update(batch_size=B, sequence_length=S, horizon=H)
@@ -182,7 +185,10 @@ def test_epoch_vs_oracle_at_baseline_shape(B, gpu):
     d = Dreamer(cfg, gpu)
     P = {k: v.detach().cpu().clone() for k, v in d.state_dict().items()}
     n = 4096
-    frames, acts, rews, conts = bench.synthetic_replay(n, (64, 64), A, seed=0)
+    if data == "synthetic":
+        frames, acts, rews, conts = bench.synthetic_replay(n, (64, 64), A, seed=0)
+    else:
+        frames, acts, rews, conts = replay_data(n, (64, 64), A, seed=3)
     rng = np.random.RandomState(100 + B)
     starts = rng.randint(0, n - S + 1, size=B)
     g = torch.Generator().manual_seed(200 + B)
@@ -198,4 +204,4 @@ def test_epoch_vs_oracle_at_baseline_shape(B, gpu):
     ref["P0"] = P
     eng, pre = run_gpu_epoch(d, frames, acts, rews, conts, n, 0, starts, q_warm, eps, q, S0)
     n_tiny = compare(d, eng, pre, ref, C, f"B{B}", S0)
-    print(f"B{B}: guarded {ref['guarded']}/{ref['draws']} draws, {n_tiny} near-zero-gradient params")
+    print(f"B{B} {data}: actor grad norm {float(ref['ts']['norm_actor']):.4g}, guarded {ref['guarded']}/{ref['draws']} draws, {n_tiny} near-zero-gradient params")

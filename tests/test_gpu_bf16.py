@@ -133,3 +133,42 @@ def test_encoder_fp32_from_frames_matches_torch(gpu, res):
     err = float((got - ref).norm() / ref.norm())
     print(f"res {res}: fp32 encoder vs torch {err:.2e}")
     assert err <= 1e-5
+
+
+def test_critic_fwd_bf16_chain_gemm(gpu):
+    """bf16 mode's chain GEMMs (k_gemm_tile_b16: NT tile-route products with
+    operands rounded to bf16, f32 accumulation) through dr_critic_fwd at the
+    headline row count M = 256 (ValueNetwork, ActorCriticNetworks.py critic
+    MLP): first layer K = hidden + R*C takes the bf16 tile.  Against the fp32
+    mode on the same inputs: normwise relative error of the bucket logits in
+    (1e-6, 2e-2] -- non-zero proves the bf16 kernel ran, the bound is the
+    stated bf16 tolerance."""
+    from dreamer_amd import Dreamer
+    from dreamer_amd import _lib as L
+    from dreamer_amd import hip
+    from formula import FULL
+    torch.manual_seed(0)
+    d = Dreamer(dict(FULL), gpu)
+    crit = d.agent.critic
+    M = 256
+    g = torch.Generator().manual_seed(4)
+    h = torch.randn(M, d.hidden_state_dims, generator=g).to(gpu)
+    R, C = d.latent_state_dims
+    z = torch.nn.functional.one_hot(torch.randint(0, C, (M, R), generator=g), C).float().reshape(M, -1).to(gpu)
+    out = {}
+    for prec in (0, 1):
+        dm = L.dr_dims()
+        dm.hidden, dm.rows, dm.cols = h.shape[1], z.shape[1], 1
+        dm.critic_h1, dm.critic_h2 = crit.value_net[0].out_features, crit.value_net[3].out_features
+        dm.buckets = crit.num_buckets
+        dm.precision = prec
+        lg = torch.empty(M, crit.num_buckets, device=gpu)
+        v = torch.empty(M, device=gpu)
+        ws = torch.empty(L.query("dr_critic_tape_bytes", dm, M), dtype=torch.uint8, device=gpu)
+        L.call("dr_critic_fwd", dm, crit.struct(), M, L.ptr(h), h.shape[1], L.ptr(z), z.shape[1], L.ptr(lg),
+               L.ptr(v), None, L.ptr(ws), ws.numel(), hip.stream())
+        torch.cuda.synchronize()
+        out[prec] = lg.cpu()
+    err = float((out[1] - out[0]).norm() / out[0].norm())
+    print(f"critic logits bf16 vs fp32: normwise rel err {err:.2e}")
+    assert 1e-6 < err <= 2e-2
