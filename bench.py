@@ -27,6 +27,9 @@ sys.path.insert(0, REPO)
 
 METRIC = "imagined latent-steps/sec (B×H) at 64×64 CarRacing, 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 = f32 vector peak
+# fp32 encoder convs 2-4 run f32-accurate on the bf16 MFMA with a 3-term split,
+# 6 bf16 products per f32 product (conv_split.hip): their ceiling is 2500 / 6
+SPLIT3_PEAK_TFLOPS = round(2500.0 / 6, 1)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 HBM_PEAK_GBS = 8000.0
 # SURVEY.md §8d figure of record: necessary dense FLOPs per imagined step at
@@ -476,7 +479,8 @@ def main():
     # the dominant kernel group (conv encoder + feature projection) timed live
     # with HIP events on the engine's stream, back to back, after the timed region
     enc_s = eng.time_encoder(reps=5) / 1e3
-    peak = BF16_MFMA_PEAK_TFLOPS if args.precision == "bf16" else FP32_MFMA_PEAK_TFLOPS
+    peak = BF16_MFMA_PEAK_TFLOPS if args.precision == "bf16" else SPLIT3_PEAK_TFLOPS
+    path_peak = BF16_MFMA_PEAK_TFLOPS if args.precision == "bf16" else FP32_MFMA_PEAK_TFLOPS
     achieved = enc_flops / enc_s / 1e12
     traffic, traffic_src = traffic_for(B, res, args.precision)
     dtype = "bf16" if args.precision == "bf16" else "f32"
@@ -499,14 +503,17 @@ def main():
                      "traffic_unit": "HBM-side bytes per launch group (per epoch)", "traffic_source": traffic_src,
                      "algorithmic_flops_per_launch": enc_flops,
                      "algorithmic_unit": "55.77 MFLOP per 64x64 frame (SURVEY §8d) x B*S/2 frames",
-                     "encoder_ms": round(enc_s * 1e3, 4)},
+                     "encoder_ms": round(enc_s * 1e3, 4),
+                     "peak_note": ("bf16 MFMA dense peak" if args.precision == "bf16" else
+                                   "f32 work on the bf16 MFMA, 6 split products per f32 product (2500/6); "
+                                   "the f32-input MFMA peak is 157.3")},
         "losses": {"actor": la, "critic": lc},
     }
     mf = PATH_MFLOP_PER_STEP.get((S, H, res))
     if mf is not None:
         tf = value * mf * 1e6 / 1e12
-        out["path_roofline"] = {"bound": "mfma", "achieved": round(tf, 2), "peak": peak,
-                                "unit": "TFLOP/s", "frac": round(tf / peak, 4),
+        out["path_roofline"] = {"bound": "mfma", "achieved": round(tf, 2), "peak": path_peak,
+                                "unit": "TFLOP/s", "frac": round(tf / path_peak, 4),
                                 "mflop_per_imagined_step": mf,
                                 "note": "whole train_Agent epoch, SURVEY §8d necessary FLOPs x imagined steps/s"}
     if wm is not None:

@@ -23,6 +23,14 @@ int op_conv1_frames(int n, int nb, int ih, int iw, int cout, const dr_frames* sr
                     float* out, hipStream_t s);
 int op_conv_repack_pad(int cout, int cin, int cin_pad, const float* w, float* wr, hipStream_t s);
 
+// ---- conv_split.hip (fp32-accurate convs on the bf16 MFMA: 3-term split) ----
+// weights: Conv2d [co][ci][4][4] f32 -> 3 bf16 planes [3][co][16][cin] (6 bytes per weight)
+int op_conv_repack_split3(int cout, int cin, const float* w, void* wr, hipStream_t s);
+bool op_conv_split3_supported(int cin, int ih, int iw, int cout);
+// k4 s2 p1 conv + bias + SiLU, f32 NHWC in -> f32 NHWC (or NCHW) out, as op_conv_nhwc
+int op_conv_split3(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
+                   float* out, int out_nchw, hipStream_t s);
+
 // ---- conv_bf16.hip (bf16 perf mode; activations bf16, accumulation f32) ----
 // weights: Conv2d [co][ci][4][4] f32 -> bf16 [co][tap][cin_pad]; matrix slice -> bf16 [rows][cols]
 int op_conv_repack_bf16(int cout, int cin, int cin_pad, const float* w, void* wr, hipStream_t s);

@@ -74,20 +74,25 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
   constexpr int NCH = K / CBK;
   constexpr int PIPE = NCH >= 8 ? 3 : 1;
   float4 ra_[PIPE][APT], rb_[PIPE][BPT];
+  unsigned okm_[PIPE];  // bit i: A row i's tap lies inside the frame
   auto load = [&](int k0, int sl) {
     float4* ra = ra_[sl];
     float4* rb = rb_[sl];
     const int k = k0 + 4 * quad;
     const int tap = k / CIN, ci = k - tap * CIN;
     const int ky = tap >> 2, kx = tap & 3;
+    unsigned okm = 0;
 #pragma unroll
     for (int i = 0; i < APT; ++i) {
+      // unconditional load (padding taps read a valid address, zeroed at the
+      // LDS store): a conditional load compiled to a branch that waited for
+      // each load before issuing the next
       const int y = piy[i] + ky, x = pix[i] + kx;
-      if (pvalid[i] && y >= 0 && y < ih && x >= 0 && x < iw)
-        ra[i] = *reinterpret_cast<const float4*>(in + pbase[i] + ((long long)y * iw + x) * CIN + ci);
-      else
-        ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      const bool ok = pvalid[i] && y >= 0 && y < ih && x >= 0 && x < iw;
+      ra[i] = *reinterpret_cast<const float4*>(in + (ok ? pbase[i] + ((long long)y * iw + x) * CIN + ci : 0));
+      okm |= ok ? (1u << i) : 0u;
     }
+    okm_[sl] = okm;
 #pragma unroll
     for (int i = 0; i < BPT; ++i) {
       const int co = n0 + prow + 32 * i;
@@ -99,7 +104,9 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
     const float4* ra = ra_[sl];
     const float4* rb = rb_[sl];
 #pragma unroll
-    for (int i = 0; i < APT; ++i) *reinterpret_cast<float4*>(&As[buf][prow + 32 * i][4 * quad]) = ra[i];
+    for (int i = 0; i < APT; ++i)
+      *reinterpret_cast<float4*>(&As[buf][prow + 32 * i][4 * quad]) =
+          (okm_[sl] >> i) & 1u ? ra[i] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int i = 0; i < BPT; ++i)
       if (prow + 32 * i < BN) *reinterpret_cast<float4*>(&Bs[buf][prow + 32 * i][4 * quad]) = rb[i];
@@ -126,7 +133,9 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
       if (c >= NCH) break;
       const int buf = c & 1;
       // slot u was stored to LDS at the end of the previous chunk: refill it
-      if (PIPE > 1 && c + PIPE < NCH) load((c + PIPE) * CBK, u);
+      // (unconditional: the last chunks reload chunk NCH - 1, unused; a
+      // conditional refill made every LDS store wait for all loads in flight)
+      if (PIPE > 1) load(min(c + PIPE, NCH - 1) * CBK, u);
 #pragma unroll
       for (int s = 0; s < CBK; s += 16) {
         float4 a[FM], b[FN];

@@ -38,9 +38,12 @@ static void enc_carve(Carve& c, const dr_dims* d, int n, EncWs& w) {
   w.a3 = e((long long)n * p3 * c3);
   w.a4 = e((long long)n * p4 * c4);
   w.wr1 = e((long long)c1 * 4 * 16);
-  w.wr2 = e((long long)c2 * c1 * 16);
-  w.wr3 = e((long long)c3 * c2 * 16);
-  w.wr4 = e((long long)c4 * c3 * 16);
+  // fp32: conv2..4 weights as three bf16 planes (op_conv_repack_split3, 6 bytes
+  // per weight; the f32 repack of the fallback fits in the same slot)
+  auto wsl = [&](long long elems) { return bf ? (float*)c.raw(elems * 2) : (float*)c.raw(elems * 6); };
+  w.wr2 = wsl((long long)c2 * c1 * 16);
+  w.wr3 = wsl((long long)c3 * c2 * 16);
+  w.wr4 = wsl((long long)c4 * c3 * 16);
   w.wproj = bf ? c.raw((size_t)d->enc_hidden * c4 * p4 * 2) : nullptr;
 }
 
@@ -109,19 +112,31 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
   const int c1 = d->enc_f1, c2 = d->enc_f2, c3 = 2 * d->enc_f2, c4 = 4 * d->enc_f2;
   const int h0 = d->img_h, w0 = d->img_w;
   DR_TRY(op_conv_repack_pad(c1, 3, 4, wm->conv[0].w, w.wr1, s));
-  DR_TRY(op_conv_repack_pad(c2, c1, c1, wm->conv[1].w, w.wr2, s));
-  DR_TRY(op_conv_repack_pad(c3, c2, c2, wm->conv[2].w, w.wr3, s));
-  DR_TRY(op_conv_repack_pad(c4, c3, c3, wm->conv[3].w, w.wr4, s));
   // the first conv straight from the frames (u8 ring or f32); shapes it does
-  // not tile go through the normalised NHWC4 copy.  Then NHWC implicit GEMMs
+  // not tile go through the normalised NHWC4 copy
   if (op_conv1_frames(n, B, h0, w0, c1, src, w.wr1, wm->conv[0].b, w.a1, s) != DR_OK) {
     DR_TRY(op_frames_nhwc4(n, B, h0, w0, src, w.x0, s));
     DR_TRY(op_conv_nhwc(n, 4, h0, w0, c1, w.x0, w.wr1, wm->conv[0].b, w.a1, 0, s));
   }
-  DR_TRY(op_conv_nhwc(n, c1, h0 / 2, w0 / 2, c2, w.a1, w.wr2, wm->conv[1].b, w.a2, 0, s));
-  DR_TRY(op_conv_nhwc(n, c2, h0 / 4, w0 / 4, c3, w.a2, w.wr3, wm->conv[2].b, w.a3, 0, s));
-  // last layer in NCHW == nn.Flatten order of Encoder.forward (VAE.py:72)
-  DR_TRY(op_conv_nhwc(n, c3, h0 / 8, w0 / 8, c4, w.a3, w.wr4, wm->conv[3].b, w.a4, 1, s));
+  // conv2..4: NHWC implicit GEMMs, f32-accurate on the bf16 MFMA (3-term split,
+  // conv_split.hip) where the shape tiles, else on the f32 MFMA; the last layer
+  // in NCHW == nn.Flatten order of Encoder.forward (VAE.py:72)
+  const int cin_[3] = {c1, c2, c3}, cout_[3] = {c2, c3, c4}, hin_[3] = {h0 / 2, h0 / 4, h0 / 8},
+            win_[3] = {w0 / 2, w0 / 4, w0 / 8};
+  const float* xin_[3] = {w.a1, w.a2, w.a3};
+  float* wr_[3] = {w.wr2, w.wr3, w.wr4};
+  float* y_[3] = {w.a2, w.a3, w.a4};
+  for (int l = 0; l < 3; ++l) {
+    const float* cw = wm->conv[l + 1].w;
+    const float* cb = wm->conv[l + 1].b;
+    if (op_conv_split3_supported(cin_[l], hin_[l], win_[l], cout_[l])) {
+      DR_TRY(op_conv_repack_split3(cout_[l], cin_[l], cw, wr_[l], s));
+      DR_TRY(op_conv_split3(n, cin_[l], hin_[l], win_[l], cout_[l], xin_[l], wr_[l], cb, y_[l], l == 2, s));
+    } else {
+      DR_TRY(op_conv_repack_pad(cout_[l], cin_[l], cin_[l], cw, wr_[l], s));
+      DR_TRY(op_conv_nhwc(n, cin_[l], hin_[l], win_[l], cout_[l], xin_[l], wr_[l], cb, y_[l], l == 2, s));
+    }
+  }
   const int F = c4 * (h0 / 16) * (w0 / 16);
   GemmArgs gp = lin(n, d->enc_hidden, F, w.a4, F, wm->map0.w, F + d->hidden, wm->map0.b, feat, d->enc_hidden);
   float* sk = w.sk;
