@@ -993,6 +993,16 @@ __device__ __forceinline__ float tile_b_kn(const GemmArgs& g, const float* W, in
   if (n >= g.nsplitB) return dr_g(g.W2)[(long long)k * g.ldb2 + (n - g.nsplitB)];
   return dr_ld1(W, (unsigned)(k * ldb + n));
 }
+// the same element as tile_b_kn as ONE branch-free load (address by select):
+// a load inside a branch is waited for before the branch joins, which turned
+// the tile kernel's load-ahead ring into one round trip per chunk
+__device__ __forceinline__ float tile_b_kn_ld(const GemmArgs& g, const float* W, int ldb, int n, int k) {
+  const bool w2k = k >= g.ksplitB, w2n = n >= g.nsplitB;
+  const float* base = (w2k || w2n) ? g.W2 : W;
+  const long long e = w2k ? (long long)(k - g.ksplitB) * g.ldb2 + n
+                          : (w2n ? (long long)k * g.ldb2 + (n - g.nsplitB) : (long long)k * ldb + n);
+  return dr_g(base)[e];
+}
 
 // NW waves: 4 as 2 x 2 (32 x 32 wave tiles at 64 x 64), 8 as 4 x 2 (16 x 16
 // wave tiles at 64 x 32: two waves per SIMD hide the per-chunk barrier and
@@ -1041,9 +1051,14 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tile(GemmBatch gb, int splits)
   // register ring: chunk loads are issued PIPE chunks ahead of their use
   constexpr int PIPE = 3;
   float4 ra[PIPE][APT], rb[PIPE][BPT];
+  // every load is issued unconditionally (out-of-range elements read a valid
+  // address) and zeroed at the LDS store by these masks: loads under a
+  // condition were each waited for before the next could issue
+  unsigned mka[PIPE], mkb[PIPE];  // bit (4 i + cc) of A / B: element in range
   const int quad = tid % KQ, prow = tid / KQ;
   auto load = [&](int c, int sl) {
     const int k0 = c * KC;
+    unsigned ma = 0u, mb = 0u;
 #pragma unroll
     for (int i = 0; i < APT; ++i) {
       if (!A_KM) {
@@ -1054,8 +1069,9 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tile(GemmBatch gb, int splits)
           const float* base = s1 ? A : A2;
           const unsigned e = ok ? (unsigned)(s1 ? m * lda + k : m * lda2 + k - ksA) : 0u;
           ra[sl][i] = dr_ld4(ok ? base : W, e);
-          if (!ok) ra[sl][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+          ma |= ok ? (15u << (4 * i)) : 0u;
         } else {
+          // (unaligned operands, rare: conditional scalar loads as before)
           float* v = &ra[sl][i].x;
 #pragma unroll
           for (int cc = 0; cc < 4; ++cc) {
@@ -1064,12 +1080,17 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tile(GemmBatch gb, int splits)
                                                     : dr_ld1(A2, (unsigned)(m * lda2 + kk - ksA)))
                                       : 0.f;
           }
+          ma |= 15u << (4 * i);
         }
       } else {
         const int m = m0 + tid % BM, k = k0 + 4 * (tid / BM + AQ * i);
         float* v = &ra[sl][i].x;
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) v[cc] = (k + cc < K && m < M) ? dr_ld1(A, (unsigned)((k + cc) * lda + m)) : 0.f;
+        for (int cc = 0; cc < 4; ++cc) {
+          const bool ok = k + cc < K && m < M;
+          v[cc] = dr_ld1(A, ok ? (unsigned)((k + cc) * lda + m) : 0u);
+          ma |= ok ? (1u << (4 * i + cc)) : 0u;
+        }
       }
     }
 #pragma unroll
@@ -1079,35 +1100,48 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tile(GemmBatch gb, int splits)
         if (VEC) {
           const bool ok = n < N && k < K;
           rb[sl][i] = dr_ld4(W, ok ? (unsigned)(n * ldb + k) : 0u);
-          if (!ok) rb[sl][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+          mb |= ok ? (15u << (4 * i)) : 0u;
         } else {
           float* v = &rb[sl][i].x;
 #pragma unroll
           for (int cc = 0; cc < 4; ++cc) v[cc] = (n < N && k + cc < K) ? dr_ld1(W, (unsigned)(n * ldb + k + cc)) : 0.f;
+          mb |= 15u << (4 * i);
         }
       } else {
         const int n = n0 + tid % BN, k = k0 + 4 * (tid / BN + BQ * i);
         float* v = &rb[sl][i].x;
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) v[cc] = (k + cc < K && n < N) ? tile_b_kn(g, W, ldb, n, k + cc) : 0.f;
+        for (int cc = 0; cc < 4; ++cc) {
+          const bool ok = k + cc < K && n < N;
+          v[cc] = tile_b_kn_ld(g, W, ldb, ok ? n : 0, ok ? k + cc : 0);
+          mb |= ok ? (1u << (4 * i + cc)) : 0u;
+        }
       }
     }
+    mka[sl] = ma;
+    mkb[sl] = mb;
+  };
+  auto masked = [](float4 v, unsigned m, int i) {
+    const unsigned b = m >> (4 * i);
+    return make_float4(b & 1u ? v.x : 0.f, b & 2u ? v.y : 0.f, b & 4u ? v.z : 0.f, b & 8u ? v.w : 0.f);
   };
   auto store = [&](int sl, int buf) {
 #pragma unroll
     for (int i = 0; i < APT; ++i) {
+      const float4 v = masked(ra[sl][i], mka[sl], i);
       if (!A_KM) {
-        *reinterpret_cast<float4*>(&As[buf][prow + RS * i][4 * quad]) = ra[sl][i];
+        *reinterpret_cast<float4*>(&As[buf][prow + RS * i][4 * quad]) = v;
       } else {
-        *reinterpret_cast<float4*>(&As[buf][tid % BM][4 * (tid / BM + AQ * i)]) = ra[sl][i];
+        *reinterpret_cast<float4*>(&As[buf][tid % BM][4 * (tid / BM + AQ * i)]) = v;
       }
     }
 #pragma unroll
     for (int i = 0; i < BPT; ++i) {
+      const float4 v = masked(rb[sl][i], mkb[sl], i);
       if (!B_KN) {
-        *reinterpret_cast<float4*>(&Bs[buf][prow + RS * i][4 * quad]) = rb[sl][i];
+        *reinterpret_cast<float4*>(&Bs[buf][prow + RS * i][4 * quad]) = v;
       } else {
-        *reinterpret_cast<float4*>(&Bs[buf][tid % BN][4 * (tid / BN + BQ * i)]) = rb[sl][i];
+        *reinterpret_cast<float4*>(&Bs[buf][tid % BN][4 * (tid / BN + BQ * i)]) = v;
       }
     }
   };
@@ -1122,9 +1156,10 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tile(GemmBatch gb, int splits)
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // (a split past the last chunk, c0 >= c1, loads chunk 0 and computes nothing)
+  const int clast = max(c1 - 1, 0);
 #pragma unroll
-  for (int u = 0; u < PIPE; ++u)
-    if (c0 + u < c1) load(c0 + u, u);
+  for (int u = 0; u < PIPE; ++u) load(min(c0 + u, clast), u);
   if (c0 < c1) store(0, 0);
   __syncthreads();
   for (int cb = c0; cb < c1; cb += PIPE) {
@@ -1133,7 +1168,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tile(GemmBatch gb, int splits)
       const int c = cb + u;
       if (c >= c1) break;
       const int buf = (c - c0) & 1;
-      if (c + PIPE < c1) load(c + PIPE, u);  // slot u was stored to LDS last iteration
+      load(min(c + PIPE, clast), u);  // slot u was stored to LDS last iteration; past the end: unused
 #pragma unroll
       for (int s = 0; s < KC; s += 16) {
         float4 a[FM], b[FN];
