@@ -26,7 +26,7 @@ int op_conv_repack_pad(int cout, int cin, int cin_pad, const float* w, float* wr
 // ---- conv_split.hip (fp32-accurate convs on the bf16 MFMA: 3-term split) ----
 // weights: Conv2d [co][ci][4][4] f32 -> 3 bf16 planes [3][co][16][cin] (6 bytes per weight)
 int op_conv_repack_split3(int cout, int cin, const float* w, void* wr, hipStream_t s);
-bool op_conv_split3_supported(int cin, int ih, int iw, int cout);
+bool op_conv_split3_supported(int n, int cin, int ih, int iw, int cout);
 // k4 s2 p1 conv + bias + SiLU, f32 NHWC in -> f32 NHWC (or NCHW) out, as op_conv_nhwc
 int op_conv_split3(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
                    float* out, int out_nchw, hipStream_t s);

@@ -129,7 +129,7 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
   for (int l = 0; l < 3; ++l) {
     const float* cw = wm->conv[l + 1].w;
     const float* cb = wm->conv[l + 1].b;
-    if (op_conv_split3_supported(cin_[l], hin_[l], win_[l], cout_[l])) {
+    if (op_conv_split3_supported(n, cin_[l], hin_[l], win_[l], cout_[l])) {
       DR_TRY(op_conv_repack_split3(cout_[l], cin_[l], cw, wr_[l], s));
       DR_TRY(op_conv_split3(n, cin_[l], hin_[l], win_[l], cout_[l], xin_[l], wr_[l], cb, y_[l], l == 2, s));
     } else {
