@@ -135,6 +135,36 @@ def test_encoder_fp32_from_frames_matches_torch(gpu, res):
     assert err <= 1e-5
 
 
+def test_encoder_fp32_split_is_f32_accurate(gpu):
+    """The fp32 encoder's conv2..4 run on the bf16 MFMA with a 3-term split
+    (conv_split.hip): its error against a float64 conv stack must be of the
+    order of torch's own float32 stack (<= 4x its normwise error), i.e. f32
+    accuracy, not bf16 (which sits ~1e-3 away, test above)."""
+    from dreamer_amd import Dreamer
+    from formula import FULL
+    torch.manual_seed(0)
+    d = Dreamer(dict(FULL), gpu)
+    wm = d.world_model
+    g = torch.Generator().manual_seed(5)
+    frames = torch.randint(0, 256, (64, 3, 64, 64), generator=g, dtype=torch.uint8)
+    got = _features(wm.packed(), wm.dims(d.agent), frames, gpu).double()
+    P = {k: v.detach().cpu() for k, v in wm.encoder.state_dict().items()}
+
+    def stack(dt):
+        x = (frames.float() / 255.0 - 0.5).to(dt)
+        for i in range(4):
+            x = F.silu(F.conv2d(x, P[f"feature_extractor.{2 * i}.weight"].to(dt),
+                                P[f"feature_extractor.{2 * i}.bias"].to(dt), stride=2, padding=1))
+        flat = x.flatten(1)
+        return flat @ P["latent_mapper.0.weight"][:, :flat.shape[1]].to(dt).t() + P["latent_mapper.0.bias"].to(dt)
+
+    ref64 = stack(torch.float64)
+    err = float((got - ref64).norm() / ref64.norm())
+    err32 = float((stack(torch.float32).double() - ref64).norm() / ref64.norm())
+    print(f"fp32 encoder vs float64: {err:.2e}; torch float32 vs float64: {err32:.2e}")
+    assert err <= 4 * err32 + 1e-7, (err, err32)
+
+
 def test_critic_fwd_bf16_chain_gemm(gpu):
     """bf16 mode's chain GEMMs (k_gemm_tile_b16: NT tile-route products with
     operands rounded to bf16, f32 accumulation) through dr_critic_fwd at the
