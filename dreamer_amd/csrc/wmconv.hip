@@ -86,35 +86,44 @@ __global__ __launch_bounds__(256) void k_convT_nhwc(ConvTArgs a) {
     pix[i] = x + px;
   }
 
+  // loads are issued unconditionally (out-of-range taps read offset 0) and
+  // masked / activated at the LDS store: a bounds-checked load compiled to a
+  // branch that waited for it at once, so chunk c+1's loads did not overlap
+  // chunk c's MFMAs
   float4 ra[APT], rb[BPT];
+  unsigned mka = 0u, mkb = 0u;
   auto load = [&](int k0) {
     const int k = k0 + 4 * quad;
     const int tap = k / CIN, ci = k - tap * CIN;
     const int dy = tap >> 1, dx = tap & 1;
+    mka = mkb = 0u;
 #pragma unroll
     for (int i = 0; i < APT; ++i) {
       const int y = piy[i] - dy, x = pix[i] - dx;
-      if (pvalid[i] && y >= 0 && y < h && x >= 0 && x < w) {
-        float4 v = *reinterpret_cast<const float4*>(in + pbase[i] + ((long long)y * w + x) * CIN + ci);
-        if (SILU_IN) v = make_float4(dr_silu(v.x), dr_silu(v.y), dr_silu(v.z), dr_silu(v.w));
-        ra[i] = v;
-      } else {
-        ra[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+      const bool ok = pvalid[i] && y >= 0 && y < h && x >= 0 && x < w;
+      ra[i] = *reinterpret_cast<const float4*>(in + (ok ? pbase[i] + ((long long)y * w + x) * CIN + ci : 0));
+      mka |= ok ? (1u << i) : 0u;
     }
 #pragma unroll
     for (int i = 0; i < BPT; ++i) {
       const int co = n0 + prow + 32 * i;
-      rb[i] = (co < cout && prow + 32 * i < BN) ? *reinterpret_cast<const float4*>(wq + (long long)co * K + k)
-                                                : make_float4(0.f, 0.f, 0.f, 0.f);
+      const bool ok = co < cout && prow + 32 * i < BN;
+      rb[i] = *reinterpret_cast<const float4*>(wq + (ok ? (long long)co * K + k : 0));
+      mkb |= ok ? (1u << i) : 0u;
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < APT; ++i) *reinterpret_cast<float4*>(&As[buf][prow + 32 * i][4 * quad]) = ra[i];
+    for (int i = 0; i < APT; ++i) {
+      float4 v = (mka >> i) & 1u ? ra[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (SILU_IN) v = make_float4(dr_silu(v.x), dr_silu(v.y), dr_silu(v.z), dr_silu(v.w));
+      *reinterpret_cast<float4*>(&As[buf][prow + 32 * i][4 * quad]) = v;
+    }
 #pragma unroll
     for (int i = 0; i < BPT; ++i)
-      if (prow + 32 * i < BN) *reinterpret_cast<float4*>(&Bs[buf][prow + 32 * i][4 * quad]) = rb[i];
+      if (prow + 32 * i < BN)
+        *reinterpret_cast<float4*>(&Bs[buf][prow + 32 * i][4 * quad]) =
+            (mkb >> i) & 1u ? rb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
 
   const int wm0 = (wave / WN) * WTM, wn0 = (wave % WN) * WTN;
@@ -131,7 +140,7 @@ __global__ __launch_bounds__(256) void k_convT_nhwc(ConvTArgs a) {
   constexpr int NCH = K / TBK;
   for (int c = 0; c < NCH; ++c) {
     const int buf = c & 1;
-    if (c + 1 < NCH) load((c + 1) * TBK);
+    load(min(c + 1, NCH - 1) * TBK);  // (the last chunk reloads itself, unused)
 #pragma unroll
     for (int s = 0; s < TBK; s += 16) {
       float4 av[FM], bv[FN];
@@ -518,38 +527,41 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(int n, int h, int w, int ca,
   const int bky = btap >> 2, bkx = btap & 3;
   const int am = m0 + 4 * acol;
 
+  // unconditional loads, masked (and activated) at the LDS store: see k_convT_nhwc
   float4 ra[APT], rb[BPT];
+  unsigned mka = 0u, mkb = 0u;
   auto load = [&](long long k0) {
+    mka = mkb = 0u;
 #pragma unroll
     for (int i = 0; i < APT; ++i) {
       const long long k = k0 + arow + AROWS * i;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (k < k_end && am < ca) {
-        v = *reinterpret_cast<const float4*>(lo + k * lda + am);
-        if (lo_silu) v = make_float4(dr_silu(v.x), dr_silu(v.y), dr_silu(v.z), dr_silu(v.w));
-      }
-      ra[i] = v;
+      const bool ok = k < k_end && am < ca;
+      ra[i] = *reinterpret_cast<const float4*>(lo + (ok ? k * lda + am : 0));
+      mka |= ok ? (1u << i) : 0u;
     }
 #pragma unroll
     for (int i = 0; i < BPT; ++i) {
       const long long k = k0 + brow + BROWS * i;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (k < k_end) {
-        const long long f = k / hw;
-        const int p = (int)(k - f * hw);
-        const int y = p / w, x = p - y * w;
-        const int Y = 2 * y - 1 + bky, X = 2 * x - 1 + bkx;
-        if (Y >= 0 && Y < H2 && X >= 0 && X < W2)
-          v = *reinterpret_cast<const float4*>(hi + ((f * H2 + Y) * W2 + X) * ldb + bch);
-      }
-      rb[i] = v;
+      const long long f = k / hw;
+      const int p = (int)(k - f * hw);
+      const int y = p / w, x = p - y * w;
+      const int Y = 2 * y - 1 + bky, X = 2 * x - 1 + bkx;
+      const bool ok = k < k_end && Y >= 0 && Y < H2 && X >= 0 && X < W2;
+      rb[i] = *reinterpret_cast<const float4*>(hi + (ok ? ((f * H2 + Y) * W2 + X) * ldb + bch : 0));
+      mkb |= ok ? (1u << i) : 0u;
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < APT; ++i) *reinterpret_cast<float4*>(&As[buf][arow + AROWS * i][4 * acol]) = ra[i];
+    for (int i = 0; i < APT; ++i) {
+      float4 v = (mka >> i) & 1u ? ra[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (lo_silu) v = make_float4(dr_silu(v.x), dr_silu(v.y), dr_silu(v.z), dr_silu(v.w));
+      *reinterpret_cast<float4*>(&As[buf][arow + AROWS * i][4 * acol]) = v;
+    }
 #pragma unroll
-    for (int i = 0; i < BPT; ++i) *reinterpret_cast<float4*>(&Bs[buf][brow + BROWS * i][4 * bcol]) = rb[i];
+    for (int i = 0; i < BPT; ++i)
+      *reinterpret_cast<float4*>(&Bs[buf][brow + BROWS * i][4 * bcol]) =
+          (mkb >> i) & 1u ? rb[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
 
   const int wm0 = (wave >> 1) * WTM, wn0 = (wave & 1) * WTN;
@@ -567,7 +579,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(int n, int h, int w, int ca,
     const int nch = (int)((k_end - k_begin + WBK - 1) / WBK);
     for (int c = 0; c < nch; ++c) {
       const int buf = c & 1;
-      if (c + 1 < nch) load(k_begin + (long long)(c + 1) * WBK);
+      load(k_begin + (long long)min(c + 1, nch - 1) * WBK);  // (the last chunk reloads itself, unused)
 #pragma unroll
       for (int s = 0; s < WBK; s += 16) {
 #pragma unroll
