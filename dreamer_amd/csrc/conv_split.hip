@@ -245,7 +245,7 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
         const float bv = bias[co];
         f32x4 v = acc[i][j] + bv;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = v[e] / (1.0f + expf(-v[e]));
+        for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(v[e]);
         const long long f = m / hw;
         *reinterpret_cast<f32x4*>(out + (f * cout + co) * hw + (m - f * hw)) = v;
       } else {
@@ -256,8 +256,7 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
         f32x4 v;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] = acc[i][j][e] + bv[e];
-          v[e] = v[e] / (1.0f + expf(-v[e]));
+          v[e] = dr_silu_fast(acc[i][j][e] + bv[e]);
         }
         *reinterpret_cast<f32x4*>(out + m * cout + co) = v;
       }
@@ -312,17 +311,17 @@ int op_conv_split3(int n, int cin, int ih, int iw, int cout, const float* in, co
     dr_set_error("conv_split3: unsupported shape (cin=%d ih=%d iw=%d cout=%d)", cin, ih, iw, cout);
     return DR_E_INVALID;
   }
-  // measured at 8192 frames (tools/conv_ab.py): 64 output channels on 128 x 64
-  // tiles at two workgroups per CU (1.18 ms; 256 x 64: 1.23), 128 / 256
-  // channels on 256 x 128 tiles, one 8-wave workgroup per CU (0.77 / 0.74 ms;
-  // 128 x 128: 1.13 / 1.06): the weights are re-read once per pixel tile
+  // measured at 8192 frames (tools/conv_ab.py): 256 x 64 tiles
+  // for 64 output channels (980 us; 128 x 64 at two workgroups per CU: 1004),
+  // 256 x 128 for 128 / 256 channels (709 / 658 us; 128 x 128: ~1.1 ms): the
+  // weights are re-read once per pixel tile, so taller tiles pay
 #define DR_S3L(C)                                                                                          \
   if (cin == C) {                                                                                          \
     if (cout % 128 == 0)                                                                                   \
       return out_nchw ? launch_s3<256, 128, C, true, 2>(n, ih, iw, cout, in, wr, bias, out, s)            \
                       : launch_s3<256, 128, C, false, 2>(n, ih, iw, cout, in, wr, bias, out, s);          \
-    return out_nchw ? launch_s3<128, 64, C, true, 2>(n, ih, iw, cout, in, wr, bias, out, s)               \
-                    : launch_s3<128, 64, C, false, 2>(n, ih, iw, cout, in, wr, bias, out, s);             \
+    return out_nchw ? launch_s3<256, 64, C, true, 2>(n, ih, iw, cout, in, wr, bias, out, s)               \
+                    : launch_s3<256, 64, C, false, 2>(n, ih, iw, cout, in, wr, bias, out, s);             \
   }
   DR_S3L(32)
   DR_S3L(64)
