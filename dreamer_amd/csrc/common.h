@@ -285,3 +285,19 @@ __device__ __forceinline__ float dr_normal(const unsigned long long* so, uint32_
 }
 
 static inline int dr_cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// fp32 operands on the bf16 MFMA (conv_split.hip, k_gemm_tile_s3): f32 values
+// split by truncation: h = x with the low 16 bits cleared (the
+// bf16 head), r1 = x - h and r2 = r1 - m (m = r1 truncated) are exact, l = r2
+// truncated: |x - (h + m + l)| < 2^-23 |x|.  Pairs of elements are packed into
+// bf16x2 words by v_perm_b32 (the high halves of two f32 words)
+__device__ __forceinline__ void split3_pair(float x0, float x1, unsigned& h, unsigned& m, unsigned& l) {
+  constexpr unsigned HI = 0xFFFF0000u, SEL = 0x07060302u;  // bytes 2,3 of S1 then 2,3 of S0
+  const unsigned b0 = __builtin_bit_cast(unsigned, x0), b1 = __builtin_bit_cast(unsigned, x1);
+  const float r10 = x0 - __builtin_bit_cast(float, b0 & HI), r11 = x1 - __builtin_bit_cast(float, b1 & HI);
+  const unsigned c0 = __builtin_bit_cast(unsigned, r10), c1 = __builtin_bit_cast(unsigned, r11);
+  const float r20 = r10 - __builtin_bit_cast(float, c0 & HI), r21 = r11 - __builtin_bit_cast(float, c1 & HI);
+  h = __builtin_amdgcn_perm(b1, b0, SEL);
+  m = __builtin_amdgcn_perm(c1, c0, SEL);
+  l = __builtin_amdgcn_perm(__builtin_bit_cast(unsigned, r21), __builtin_bit_cast(unsigned, r20), SEL);
+}
