@@ -1250,44 +1250,54 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tile_b16(GemmBatch gb, int spl
   __shared__ __attribute__((aligned(16))) uint32_t Bs[2][BN][TL];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   constexpr int APT = (BM * UPR + NTH - 1) / NTH, BPT = (BN * UPR + NTH - 1) / NTH;
-  uint4 ra[APT], rb[BPT];
-  auto load = [&](int c) {
-    const int k0 = c * KC;
-#pragma unroll
-    for (int i = 0; i < APT; ++i) {
-      const int u = tid + NTH * i, row = u / UPR, k = k0 + 8 * (u - row * UPR), m = m0 + row;
-      const bool ok = u < BM * UPR && m < M && k < K;
-      const bool s1 = k < ksA;
-      const float* base = s1 ? A : A2;
-      const unsigned e = ok ? (unsigned)(s1 ? m * lda + k : m * lda2 + k - ksA) : 0u;
-      float4 x0 = dr_ld4(ok ? base : W, e), x1 = dr_ld4(ok ? base : W, e + 4u);
-      if (!ok) x0 = x1 = make_float4(0.f, 0.f, 0.f, 0.f);
-      ra[i] = make_uint4(dr_pack_bf16x2(x0.x, x0.y), dr_pack_bf16x2(x0.z, x0.w), dr_pack_bf16x2(x1.x, x1.y),
-                         dr_pack_bf16x2(x1.z, x1.w));
-    }
-#pragma unroll
-    for (int i = 0; i < BPT; ++i) {
-      const int u = tid + NTH * i, row = u / UPR, k = k0 + 8 * (u - row * UPR), n = n0 + row;
-      const bool ok = u < BN * UPR && n < N && k < K;
-      const unsigned e = ok ? (unsigned)(n * ldb + k) : 0u;
-      float4 x0 = dr_ld4(W, e), x1 = dr_ld4(W, e + 4u);
-      if (!ok) x0 = x1 = make_float4(0.f, 0.f, 0.f, 0.f);
-      rb[i] = make_uint4(dr_pack_bf16x2(x0.x, x0.y), dr_pack_bf16x2(x0.z, x0.w), dr_pack_bf16x2(x1.x, x1.y),
-                         dr_pack_bf16x2(x1.z, x1.w));
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < APT; ++i) {
-      const int u = tid + NTH * i, row = u / UPR, uc = u - row * UPR;
-      if (u < BM * UPR) *reinterpret_cast<uint4*>(&As[buf][row][4 * uc]) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < BPT; ++i) {
-      const int u = tid + NTH * i, row = u / UPR, uc = u - row * UPR;
-      if (u < BN * UPR) *reinterpret_cast<uint4*>(&Bs[buf][row][4 * uc]) = rb[i];
-    }
-  };
+  // the chunk in flight stays f32 in registers, masked and rounded to bf16 at
+  // the LDS store (rounding in the loader waited for the loads at once, so the
+  // next chunk's loads did not overlap this chunk's MFMAs); macros, not
+  // lambdas: capturing lambdas left the kernel's scalars in scratch memory
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  f32x4 ra0[APT], ra1[APT], rb0[BPT], rb1[BPT];
+  unsigned mka = 0u, mkb = 0u;
+#define B16_LOAD(C_)                                                                                 \
+  do {                                                                                               \
+    const int k0 = (C_) * KC;                                                                        \
+    mka = mkb = 0u;                                                                                  \
+    _Pragma("unroll") for (int i = 0; i < APT; ++i) {                                                \
+      const int u = tid + NTH * i, row = u / UPR, k = k0 + 8 * (u - row * UPR), m = m0 + row;        \
+      const bool ok = u < BM * UPR && m < M && k < K;                                                \
+      const bool s1 = k < ksA;                                                                       \
+      const float* base = ok ? (s1 ? A : A2) : W;                                                    \
+      const unsigned e = ok ? (unsigned)(s1 ? m * lda + k : m * lda2 + k - ksA) : 0u;                \
+      ra0[i] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)base + (e << 2));                    \
+      ra1[i] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)base + ((e + 4u) << 2));             \
+      mka |= ok ? (1u << i) : 0u;                                                                    \
+    }                                                                                                \
+    _Pragma("unroll") for (int i = 0; i < BPT; ++i) {                                                \
+      const int u = tid + NTH * i, row = u / UPR, k = k0 + 8 * (u - row * UPR), n = n0 + row;        \
+      const bool ok = u < BN * UPR && n < N && k < K;                                                \
+      const unsigned e = ok ? (unsigned)(n * ldb + k) : 0u;                                          \
+      rb0[i] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)W + (e << 2));                       \
+      rb1[i] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)W + ((e + 4u) << 2));                \
+      mkb |= ok ? (1u << i) : 0u;                                                                    \
+    }                                                                                                \
+  } while (0)
+#define B16_PACK(X0_, X1_, OK_)                                                                      \
+  (u32x4_t){dr_pack_bf16x2((OK_) ? (X0_)[0] : 0.f, (OK_) ? (X0_)[1] : 0.f),                          \
+            dr_pack_bf16x2((OK_) ? (X0_)[2] : 0.f, (OK_) ? (X0_)[3] : 0.f),                          \
+            dr_pack_bf16x2((OK_) ? (X1_)[0] : 0.f, (OK_) ? (X1_)[1] : 0.f),                          \
+            dr_pack_bf16x2((OK_) ? (X1_)[2] : 0.f, (OK_) ? (X1_)[3] : 0.f)}
+#define B16_STORE(BUF_)                                                                              \
+  do {                                                                                               \
+    _Pragma("unroll") for (int i = 0; i < APT; ++i) {                                                \
+      const int u = tid + NTH * i, row = u / UPR, uc = u - row * UPR;                                \
+      const bool ok = (mka >> i) & 1u;                                                               \
+      if (u < BM * UPR) *reinterpret_cast<u32x4_t*>(&As[BUF_][row][4 * uc]) = B16_PACK(ra0[i], ra1[i], ok); \
+    }                                                                                                \
+    _Pragma("unroll") for (int i = 0; i < BPT; ++i) {                                                \
+      const int u = tid + NTH * i, row = u / UPR, uc = u - row * UPR;                                \
+      const bool ok = (mkb >> i) & 1u;                                                               \
+      if (u < BN * UPR) *reinterpret_cast<u32x4_t*>(&Bs[BUF_][row][4 * uc]) = B16_PACK(rb0[i], rb1[i], ok); \
+    }                                                                                                \
+  } while (0)
   constexpr int WGM = NW / 2;
   constexpr int WTM = BM / WGM, WTN = BN / 2, FM = WTM / 16, FN = WTN / 16;
   static_assert(FM >= 1 && FN >= 1, "wave tile");
@@ -1298,14 +1308,13 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tile_b16(GemmBatch gb, int spl
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  if (c0 < c1) {
-    load(c0);
-    store(0);
-  }
+  const int clast = max(c1 - 1, 0);  // (a split past the last chunk loads chunk 0 and computes nothing)
+  B16_LOAD(min(c0, clast));
+  if (c0 < c1) B16_STORE(0);
   __syncthreads();
   for (int c = c0; c < c1; ++c) {
     const int buf = (c - c0) & 1;
-    if (c + 1 < c1) load(c + 1);  // in flight while this chunk's MFMAs run
+    B16_LOAD(min(c + 1, clast));  // in flight while this chunk's MFMAs run (past the end: unused)
 #pragma unroll
     for (int s = 0; s < KC / 32; ++s) {
       uint4 a[FM], b[FN];
@@ -1320,9 +1329,12 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tile_b16(GemmBatch gb, int spl
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(dr_bf16x8, a[i]),
                                                               __builtin_bit_cast(dr_bf16x8, b[j]), acc[i][j], 0, 0, 0);
     }
-    if (c + 1 < c1) store(buf ^ 1);
+    if (c + 1 < c1) B16_STORE(buf ^ 1);
     __syncthreads();
   }
+#undef B16_LOAD
+#undef B16_PACK
+#undef B16_STORE
   float* part = g.splitk_ws;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
