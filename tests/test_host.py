@@ -165,3 +165,37 @@ def test_vector_observation_mode_host_side():
                        ("dr_decoder_workspace_bytes", (100,)), ("dr_wm_train_workspace_bytes", (4, 6)),
                        ("dr_imagine_workspace_bytes", (4, 6))):
         assert L.query(name, dims, *args) > 0, name
+
+
+def _trunc16(x):
+    """f32 -> the f32 value of its bf16 head (low 16 bits cleared), as split3_pair."""
+    return (np.asarray(x, np.float32).view(np.uint32) & np.uint32(0xFFFF0000)).view(np.float32)
+
+
+def test_split3_numerics_bound():
+    """Host restatement of the fp32-on-bf16 split (common.h split3_pair,
+    conv_split.hip): x = h + m + l with h, m truncated bf16 heads and l the
+    truncated remainder; the residual subtractions are exact in f32, every
+    term is a bf16 value, |x - (h + m + l)| < 2^-23 |x|, and the six-term
+    product h_a h_b + h_a m_b + m_a h_b + h_a l_b + m_a m_b + l_a h_b is within
+    2^-21 |a b| of the exact product (the order of one f32 rounding)."""
+    rng = np.random.default_rng(0)
+    x = (rng.standard_normal(200000) * np.exp(rng.uniform(-20, 20, 200000))).astype(np.float32)
+    h = _trunc16(x)
+    r1 = (x - h).astype(np.float32)
+    m = _trunc16(r1)
+    r2 = (r1 - m).astype(np.float32)
+    l = _trunc16(r2)
+    # the subtractions are exact: recomposition in float64 gives x back up to l's truncation
+    assert np.array_equal(h.astype(np.float64) + r1.astype(np.float64), x.astype(np.float64))
+    assert np.array_equal(m.astype(np.float64) + r2.astype(np.float64), r1.astype(np.float64))
+    for t in (h, m, l):  # every term is exactly a bf16 value
+        assert not np.any(t.view(np.uint32) & np.uint32(0xFFFF))
+    xs = x.astype(np.float64)
+    rec = h.astype(np.float64) + m.astype(np.float64) + l.astype(np.float64)
+    assert np.all(np.abs(xs - rec) <= 2.0 ** -23 * np.abs(xs))
+    a, b = xs[:100000], xs[100000:]
+    ha, ma, la = (t.astype(np.float64)[:100000] for t in (h, m, l))
+    hb, mb, lb = (t.astype(np.float64)[100000:] for t in (h, m, l))
+    six = ha * hb + ha * mb + ma * hb + ha * lb + ma * mb + la * hb
+    assert np.all(np.abs(six - a * b) <= 2.0 ** -21 * np.abs(a * b))
