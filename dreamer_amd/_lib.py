@@ -97,7 +97,7 @@ _SIGS = {
     "dr_actor_act": (_i, [_P(dr_dims), _P(dr_actor), _i, fp, fp, dr_noise, _i, fp, fp, fp, fp, _sz, fp]),
     "dr_act_step_workspace_bytes": (_sz, [_P(dr_dims)]),
     "dr_act_step": (_i, [_P(dr_dims), _P(dr_world_model), _P(dr_actor), fp, _i, fp, fp, fp, dr_noise, _i,
-                         fp, fp, fp, fp, fp, fp, fp, _sz, fp]),
+                         fp, fp, fp, fp, fp, fp, fp, fp, _sz, fp]),
     "dr_gru_cell": (_i, [_P(dr_dims), _P(dr_world_model), _i, fp, fp, fp, fp, fp, _sz, fp]),
     "dr_categorical_sample": (_i, [_i, _i, _i, fp, dr_noise, fp, fp, fp, fp]),
     "dr_mlp3_fwd": (_i, [_P(dr_mlp3), _i, _i, fp, _ll, _i, fp, _ll, _i, _i, _i, fp, _ll, fp, _sz, fp]),

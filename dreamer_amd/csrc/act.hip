@@ -40,6 +40,7 @@ struct alignas(16) ActArgs {
   const float *z_prev, *h, *a_prev;
   dr_noise noise;
   float *z_out, *h_out, *a_out, *mu_out, *sig_out, *logits_out;
+  int* status;  // caller's status word (may be NULL): set to 1 if a grid barrier timed out
   // workspace
   unsigned* bar;
   float *c1, *c2, *c3, *c4, *gi, *gh, *hn, *pre1, *prea;
@@ -354,7 +355,7 @@ __global__ __launch_bounds__(ACT_NT) void k_act_step(ActArgs ga) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) xv[j] = lane + 64 * j < d.enc_hidden ? x1[lane + 64 * j] : 0.f;
     float mylg = 0.f;
-    for (int u0 = 0; u0 < 32; u0 += 16) {
+    for (int u0 = 0; u0 < C; u0 += 16) {
       float wv[16][4];
 #pragma unroll
       for (int u = 0; u < 16; ++u)
@@ -412,13 +413,26 @@ __global__ __launch_bounds__(ACT_NT) void k_act_step(ActArgs ga) {
   }
   if (ok) ok = act_sync(a.bar, round, &s_ok);
   ACT_TS(a, 7);
-  // ---- stage 8 (workgroup 0): LN-SiLU, base_net.3, LN-SiLU, mu / log_sigma heads, tanh(mu + eps sigma) ----
-  if (blockIdx.x != 0) return;
+  // A barrier that timed out (a workgroup never arrived: the grid was not
+  // co-resident) is reported, never silent: every workgroup that saw it raises
+  // the status word the host checks after the step, and workgroup 0 writes NaN
+  // to every output (action, mu, sigma, z', h') so nothing downstream can
+  // mistake them for a state.
   if (!ok) {
-    if (threadIdx.x < A) a.a_out[threadIdx.x] = a.mu_out[threadIdx.x] = a.sig_out[threadIdx.x] = __int_as_float(0x7fc00000);
-    if (threadIdx.x == 0) *a.fail = 1;
+    if (threadIdx.x == 0) {
+      *a.fail = 1;
+      if (a.status) __hip_atomic_store(a.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (blockIdx.x == 0) {
+      const float qnan = __int_as_float(0x7fc00000);
+      for (int i = threadIdx.x; i < A; i += ACT_NT) a.a_out[i] = a.mu_out[i] = a.sig_out[i] = qnan;
+      for (int i = threadIdx.x; i < L; i += ACT_NT) a.z_out[i] = qnan;
+      for (int i = threadIdx.x; i < Hd; i += ACT_NT) a.h_out[i] = qnan;
+    }
     return;
   }
+  // ---- stage 8 (workgroup 0): LN-SiLU, base_net.3, LN-SiLU, mu / log_sigma heads, tanh(mu + eps sigma) ----
+  if (blockIdx.x != 0) return;
   const int wave = threadIdx.x >> 6;
   const int a1 = d.actor_h1, a2 = d.actor_h2;
   float* x1 = xs;          // SiLU(LN(pre1))
@@ -499,7 +513,8 @@ extern "C" size_t dr_act_step_workspace_bytes(const dr_dims* d) {
 extern "C" int dr_act_step(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, const unsigned char* frame,
                            int has_prev, const float* z_prev, const float* h, const float* a_prev, dr_noise noise,
                            int deterministic, float* z_out, float* h_out, float* a_out, float* mu_out,
-                           float* sigma_out, float* logits_out, void* ws, size_t ws_bytes, hipStream_t s) {
+                           float* sigma_out, float* logits_out, int* status, void* ws, size_t ws_bytes,
+                           hipStream_t s) {
   DR_REQUIRE(d && wm && ac && frame && h && z_out && h_out && a_out && mu_out && sigma_out && ws, "null argument");
   DR_REQUIRE(!has_prev || (z_prev && a_prev), "has_prev needs z_prev and a_prev");
   DR_REQUIRE(d->obs_dim == 0, "dr_act_step: pixel observations only (vector observations use the unfused path)");
@@ -529,20 +544,33 @@ extern "C" int dr_act_step(const dr_dims* d, const dr_world_model* wm, const dr_
   a.mu_out = mu_out;
   a.sig_out = sigma_out;
   a.logits_out = logits_out;
+  a.status = status;
   size_t off = 0;
   act_carve((char*)ws, d, a, off);
   DR_REQUIRE(off <= ws_bytes, "workspace too small");
   // barrier lines + fail flag (a kernel, so a captured graph re-arms them too)
   static_assert((ACT_BAR_BYTES + 512) % 4 == 0, "barrier bytes");
   DR_TRY(op_fill((ACT_BAR_BYTES + 512) / 4, reinterpret_cast<float*>(a.bar), 0.f, s));
-  static const bool raised = [] {
+  // A plain launch whose grid barrier needs all ACT_NB workgroups resident at
+  // once.  The cooperative launch would add exactly that check at +15-19 us of
+  // host time per env step (MI355X_MICROARCH.md coop-launch), so it is made
+  // once per device here instead: the occupancy API's blocks per CU (one lower
+  // than reported, the guide's sgpr-count margin) times the CU count must
+  // cover the grid, else the call fails and the caller runs the unfused path.
+  // What no launch-time check can cover -- other work holding CUs for longer
+  // than the bounded spin -- comes back through `status` (and NaN outputs).
+  static int resident_ok[64];  // per device: 0 unknown, 1 ok, -1 too small (idempotent, benign race)
+  int dev = 0;
+  DR_TRY_HIP(hipGetDevice(&dev));
+  DR_REQUIRE(dev >= 0 && dev < 64, "device index");
+  if (resident_ok[dev] == 0) {
     (void)hipFuncSetAttribute((const void*)k_act_step, hipFuncAttributeMaxDynamicSharedMemorySize, ACT_LDS * 4);
-    return true;
-  }();
-  (void)raised;
-  // a plain launch: ACT_NB (128) workgroups of 256 threads with 25 KB of LDS are
-  // co-resident on the 256 CUs (the cooperative launch's only addition is that
-  // check, at +15-19 us of host time per launch: MI355X_MICROARCH.md coop-launch)
+    int per_cu = 0, cus = 0;
+    DR_TRY_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_act_step, ACT_NT, ACT_LDS * 4));
+    DR_TRY_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    resident_ok[dev] = (long long)(per_cu - 1 > 0 ? per_cu - 1 : per_cu) * cus >= ACT_NB ? 1 : -1;
+  }
+  DR_REQUIRE(resident_ok[dev] == 1, "dr_act_step: the device cannot hold the acting grid co-resident");
   hipLaunchKernelGGL(k_act_step, dim3(ACT_NB), dim3(ACT_NT), ACT_LDS * 4, s, a);
   return dr_check_launch("act_step");
 }

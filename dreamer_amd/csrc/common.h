@@ -21,6 +21,15 @@ int dr_check_launch(const char* what);
     if (_rc != 0) return _rc;             \
   } while (0)
 
+#define DR_TRY_HIP(expr)                                                          \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess) {                                                       \
+      dr_set_error("%s: %s: %s", __func__, #expr, hipGetErrorString(_e));         \
+      return DR_E_HIP;                                                            \
+    }                                                                             \
+  } while (0)
+
 #define DR_REQUIRE(cond, msg)                         \
   do {                                                \
     if (!(cond)) {                                    \

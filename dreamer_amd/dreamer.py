@@ -218,8 +218,12 @@ class Dreamer(nn.Module):
     # scalars (loads with weights_only=True): the reference-layout state_dict,
     # the three AdamW states (moments + step), S, the engine / ad-hoc Philox
     # states, numpy's and torch's CPU generators (window sampling), the replay
-    # ring and the env seed counter.  Resuming reproduces the uninterrupted run
-    # bit for bit (tests/test_gpu_api.py::test_training_state_resume).
+    # ring and the env seed counter.  Resuming reproduces the uninterrupted
+    # run's TRAINING UPDATES (train_world_model / train_Agent) bit for bit
+    # (tests/test_gpu_api.py::test_training_state_resume).  The in-progress env
+    # episode is not part of the state (the env object, agent_obs / hidden /
+    # latent): after a resume rollout_policy starts a fresh episode with
+    # env.reset(seed), so runs that resume mid-episode diverge from there.
     TRAINING_STATE_FORMAT = "dreamer_amd.training_state.v1"
 
     def training_state(self):
@@ -297,8 +301,8 @@ class Dreamer(nn.Module):
         uint8 frame.  Returns (a', mu, sigma, z', h') shaped (1, 1, ...)."""
         dev = self.device
         L.require_gpu(torch.empty(0, device=dev))
-        if self.world_model.vector_obs:
-            return self._act_step_vector(observation, z, h, a, deterministic)
+        if self.world_model.vector_obs or getattr(self, "_act_unfused", False):
+            return self._act_step_unfused(observation, z, h, a, deterministic)
         d = self.world_model.dims(self.agent)
         self.agent._ensure_flat()
         R, C = self.latent_state_dims
@@ -310,8 +314,10 @@ class Dreamer(nn.Module):
                 pin=torch.empty(H_, W_, 3, dtype=torch.uint8).pin_memory(),
                 frame=torch.empty(H_, W_, 3, dtype=torch.uint8, device=dev),
                 h0=torch.zeros(Hd, device=dev),
+                status=torch.zeros(1, dtype=torch.int32, device=dev),
+                status_host=torch.zeros(1, dtype=torch.int32).pin_memory(),
                 ws=torch.empty(L.query("dr_act_step_workspace_bytes", d), dtype=torch.uint8, device=dev))
-        self._act_sync()  # the previous step's copy out of the pinned staging buffer has run
+        self._act_sync()  # the previous step's copy out of the pinned staging buffer has run (and it was ok)
         st["pin"].numpy()[...] = observation
         st["frame"].copy_(st["pin"], non_blocking=True)
         has_prev = z is not None
@@ -321,21 +327,40 @@ class Dreamer(nn.Module):
         z2 = torch.empty(1, 1, R, C, device=dev)
         h2 = torch.empty(1, 1, Hd, device=dev)
         a2, mu, sg = (torch.empty(1, 1, A, device=dev) for _ in range(3))
-        L.call("dr_act_step", d, self.world_model.packed(), self.agent.actor_struct(), L.ptr(st["frame"]),
-               int(has_prev), L.ptr(zp), L.ptr(hp), L.ptr(ap), hip.adhoc(dev).noise(), int(deterministic),
-               L.ptr(z2), L.ptr(h2), L.ptr(a2), L.ptr(mu), L.ptr(sg), None, L.ptr(st["ws"]), st["ws"].numel(),
-               hip.stream())
+        try:
+            L.call("dr_act_step", d, self.world_model.packed(), self.agent.actor_struct(), L.ptr(st["frame"]),
+                   int(has_prev), L.ptr(zp), L.ptr(hp), L.ptr(ap), hip.adhoc(dev).noise(), int(deterministic),
+                   L.ptr(z2), L.ptr(h2), L.ptr(a2), L.ptr(mu), L.ptr(sg), None, L.ptr(st["status"]),
+                   L.ptr(st["ws"]), st["ws"].numel(), hip.stream())
+        except RuntimeError as e:
+            if "co-resident" not in str(e):
+                raise
+            # the device cannot hold the one-launch grid: the unfused launches from now on
+            self._act_unfused = True
+            return self._act_step_unfused(observation, z, h, a, deterministic)
+        # the status word travels back with the step (4 bytes behind the kernel);
+        # _act_sync / act_check raise on a timed-out grid barrier
+        st["status_host"].copy_(st["status"], non_blocking=True)
         self._act_ev = torch.cuda.Event()
         self._act_ev.record()
         return a2, mu, sg, z2, h2
 
-    def _act_step_vector(self, observation, z, h, a, deterministic):
-        """Vector observations (BASELINE configs[4]): the same step through the
-        unfused HIP launches -- dr_gru_cell, dr_encoder_features +
-        dr_observe_scan (Encoder.encode), dr_actor_act."""
+    def act_check(self):
+        """Wait for the last act_step and raise if its one-launch kernel hit a
+        grid-barrier timeout (its outputs are then NaN, never a state)."""
+        self._act_sync()
+
+    def _act_step_unfused(self, observation, z, h, a, deterministic):
+        """The same step through the unfused HIP launches -- dr_gru_cell,
+        dr_encoder_features + dr_observe_scan (Encoder.encode), dr_actor_act:
+        vector observations (BASELINE configs[4]) and devices that cannot hold
+        dr_act_step's grid co-resident."""
         dev = self.device
         wm = self.world_model
-        obs = torch.as_tensor(np.asarray(observation, dtype=np.float32), device=dev).view(1, 1, -1)
+        if wm.vector_obs:
+            obs = torch.as_tensor(np.asarray(observation, dtype=np.float32), device=dev).view(1, 1, -1)
+        else:
+            _, obs = self._obs_tensor(observation)
         if z is None:
             h2 = torch.zeros(1, 1, self.hidden_state_dims, device=dev)
         else:
@@ -358,8 +383,16 @@ class Dreamer(nn.Module):
 
     def _act_sync(self):
         ev = getattr(self, "_act_ev", None)
-        if ev is not None:
-            ev.synchronize()
+        if ev is None:
+            return
+        ev.synchronize()
+        st = self._act_bufs
+        if int(st["status_host"][0]) != 0:
+            st["status"].zero_()
+            st["status_host"].zero_()
+            self._act_ev = None
+            raise RuntimeError("dr_act_step: a grid barrier timed out (the acting grid was not co-resident, e.g. "
+                               "beside a long-running kernel); that step's outputs are NaN")
 
     def rollout_policy(self, env, random_policy=False):  # Dreamer.py:177-226
         """Same env / buffer sequence as the reference; the device work of each
@@ -378,6 +411,7 @@ class Dreamer(nn.Module):
                     action = torch.tensor(action_np, dtype=torch.float32, device=self.device).view(1, 1, -1)
                 else:
                     action_np = action.detach().cpu().numpy().reshape(-1)
+                    self.act_check()
                 observation_, reward, terminated, truncated, _ = env.step(action_np)
                 done = terminated or truncated
                 self.buffer.add_to_buffer(self._buffer_obs(self.agent_obs), action_np, reward, 1 - done)
@@ -401,8 +435,9 @@ class Dreamer(nn.Module):
                 action, _, _, latent, hidden = self.act_step(observation, deterministic=True)
                 done = False
                 while not done:
-                    observation_, reward, terminated, truncated, _ = env.step(
-                        action.detach().cpu().numpy().squeeze(0).squeeze(0))
+                    action_np = action.detach().cpu().numpy().squeeze(0).squeeze(0)
+                    self.act_check()
+                    observation_, reward, terminated, truncated, _ = env.step(action_np)
                     total += reward
                     done = terminated or truncated
                     if not done:
@@ -451,8 +486,9 @@ class Dreamer(nn.Module):
         while not done:
             if render:
                 env.render()
-            observation_, reward, terminated, truncated, _ = env.step(
-                action.detach().cpu().numpy().squeeze(0).squeeze(0))
+            action_np = action.detach().cpu().numpy().squeeze(0).squeeze(0)
+            self.act_check()
+            observation_, reward, terminated, truncated, _ = env.step(action_np)
             total += reward
             done = terminated or truncated
             if not done:

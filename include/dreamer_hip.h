@@ -187,22 +187,27 @@ size_t dr_actor_act_workspace_bytes(const dr_dims* d, int B);
 int dr_actor_act(const dr_dims* d, const dr_actor* actor, int B, const float* h, const float* z,
                  dr_noise noise, int deterministic, float* a_out, float* mu_out, float* sigma_out, void* ws,
                  size_t ws_bytes, hipStream_t stream);
-/* GRU cell (SequenceModel.py:19-24) */
-/* Batch-1 acting step in ONE cooperative launch (rollout_policy / evaluate_agent
- * / Run, Dreamer.py:177-226, 295-322, 374-401): if has_prev,
+/* Batch-1 acting step in ONE launch with in-kernel grid barriers (rollout_policy
+ * / evaluate_agent / Run, Dreamer.py:177-226, 295-322, 374-401): if has_prev,
  * h' = GRU(z_prev, h, a_prev) (observe_step, WorldModel.py:79-82), else h' = h
  * (episode start, h = 0: Dreamer.py:186-187); z' = Encoder.encode(h', frame)
  * (VAE.py:57-99); a = Actor.act(h', z', deterministic) (Agent.py:202-210).
  * frame: the env observation [H][W][3] u8 on the device.  Noise: the sampler
  * draws stream `noise.stream`, the actor `noise.stream + 1` (explicit q [R*C],
  * eps [A] when given).  logits_out may be NULL.  Inputs and outputs may alias
- * (h / h_out, z_prev / z_out, a_prev / a_out). */
+ * (h / h_out, z_prev / z_out, a_prev / a_out).
+ * Co-residency of the grid is checked once per device (occupancy query); the
+ * call returns DR_E_INVALID when the device cannot hold it (callers then use
+ * the unfused entry points).  status (device int, may be NULL; the caller
+ * zeroes it): set to 1 if a grid barrier timed out at run time, in which case
+ * every output holds NaN -- callers must check it before using the outputs. */
 size_t dr_act_step_workspace_bytes(const dr_dims* d);
 int dr_act_step(const dr_dims* d, const dr_world_model* wm, const dr_actor* actor, const unsigned char* frame,
                 int has_prev, const float* z_prev, const float* h, const float* a_prev, dr_noise noise,
                 int deterministic, float* z_out, float* h_out, float* a_out, float* mu_out, float* sigma_out,
-                float* logits_out, void* ws, size_t ws_bytes, hipStream_t stream);
+                float* logits_out, int* status, void* ws, size_t ws_bytes, hipStream_t stream);
 
+/* GRU cell (SequenceModel.py:19-24) */
 int dr_gru_cell(const dr_dims* d, const dr_world_model* wm, int B, const float* z, const float* h,
                 const float* a, float* h_out, void* ws, size_t ws_bytes, hipStream_t stream);
 /* Categorical sampler with unimix + straight-through value (VAE.py:88-98,

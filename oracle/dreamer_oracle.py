@@ -260,8 +260,9 @@ def normalise_obs(obs):  # Dreamer.py:251, WorldModel.py:156
 def warm_start(obs, act, S, P, q_warm, rows, cols, batch_size=None):
     """Dreamer.warm_start_generator (Dreamer.py:244-262).
 
-    obs (B,S,3,H,W) holding 0..255, act (B,S,A), q_warm (S//2, B*rows, cols)."""
-    obs = normalise_obs(obs)
+    obs (B,S,3,H,W) holding 0..255, act (B,S,A), q_warm (S//2, B*rows, cols).
+    obs (B,S,D): vector observations, used as given (encoder_logits' note)."""
+    obs = obs if obs.dim() == 3 else normalise_obs(obs)
     B = obs.shape[0] if batch_size is None else batch_size
     hidden = P[WM + "sequence_model.GRU.weight_hh"].shape[1]
     h = torch.zeros(B, 1, hidden, dtype=torch.float32)

@@ -32,6 +32,8 @@ def make_dreamer(dev, B, S=8, H=5, full=False):
 def run_epochs(d, eng, starts_list, seed=4321, pipelined=False):
     eng.rng.reseed(seed)
     out = []
+    ag = d.agent
+    grads, svals = [], []
     if pipelined:  # warm start of epoch e+1 beside epoch e's update (run_many)
         ls = eng.run_many(starts_list).cpu()
         out = [(float(a), float(c)) for a, c in ls]
@@ -39,8 +41,10 @@ def run_epochs(d, eng, starts_list, seed=4321, pipelined=False):
         la, lc = eng.run(st)
         torch.cuda.synchronize()
         out.append((float(la), float(lc)))
-    ag = d.agent
-    return out, ag.fa.flat.cpu(), ag.fc.flat.cpu(), ag.ft.flat.cpu(), float(ag.S_dev)
+        # after each step the flat gradient buffer holds the clipped (global) gradients
+        grads.append(ag.grad_buffer[:ag.fa.numel + ag.fc.numel].cpu())
+        svals.append(float(ag.S_dev))
+    return out, ag.fa.flat.cpu(), ag.fc.flat.cpu(), ag.ft.flat.cpu(), float(ag.S_dev), grads, svals
 
 
 def worker(rank, world, port, B_global, starts_list, out_path, backend, pipelined=False, full=False):

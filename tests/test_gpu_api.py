@@ -304,8 +304,53 @@ def test_training_state_resume(gpu, tmp_path):
     assert st["format"] == "dreamer_amd.training_state.v1" and len(st["model"]) == len(ref[3])
 
 
+def test_act_step_matches_oracle(gpu):
+    """dr_act_step (the one-launch env step) against the CPU oracle directly:
+    O.encode at an episode start (h = 0, Dreamer.py:186-187), then
+    O.observe_step (WorldModel.py:79-82) and O.actor_act (Agent.py:202-210)
+    for 5 further env steps on the same frames and explicit noise (fresh
+    tie-guarded q / eps per step).  Latent indices exact; h, z values, action,
+    mu, sigma at |d| <= 1e-6 + 1e-4 |ref|; the status word stays 0."""
+    from dreamer_amd import hip
+    d, P = _dreamer(gpu)
+    g = torch.Generator().manual_seed(33)
+    n_steps = 6
+    frames = [torch.randint(0, 256, (64, 64, 3), generator=g, dtype=torch.uint8).numpy() for _ in range(n_steps)]
+    z_o = h_o = a_o = None
+    z_f = h_f = a_f = None
+    guarded = 0
+    with torch.no_grad():
+        for k in range(n_steps):
+            obs = torch.tensor(frames[k].transpose(2, 0, 1), dtype=torch.float32).view(1, 1, 3, 64, 64) / 255.0 - 0.5
+            q = torch.empty(1, R, C).exponential_(generator=g)
+            eps = torch.randn(1, 1, A, generator=g)
+            with TieGuard() as tg:  # widens near-tie margins in q (in place) without changing the oracle's draw
+                if k == 0:
+                    h_o = torch.zeros(1, 1, HD)
+                    z_o, _ = O.encode(h_o, obs, P, q[0], R, C)
+                else:
+                    z_o, h_o, _ = O.observe_step(z_o, h_o, a_o, obs, P, q[0], R, C)
+            guarded += tg.guarded
+            a_o, mu_o, sg_o = O.actor_act(h_o, z_o, P, eps.view(1, 1, A))
+            with hip.noise_override(q=q.to(gpu), eps=eps.to(gpu)):
+                if k == 0:
+                    a_f, mu_f, sg_f, z_f, h_f = d.act_step(frames[k])
+                else:
+                    a_f, mu_f, sg_f, z_f, h_f = d.act_step(frames[k], z_f, h_f, a_f)
+                d.act_check()
+            zi_f, zi_o = _idx(z_f), z_o.reshape(-1, C).argmax(-1)
+            assert torch.equal(zi_f, zi_o), f"step {k}: {int((zi_f != zi_o).sum())} latent groups differ"
+            close(h_f, h_o, 1e-4, 1e-6, f"h' step {k}")
+            close(z_f, z_o.reshape(z_f.shape), 0, 1e-6, f"straight-through latent values step {k}")
+            close(mu_f, mu_o, 1e-4, 1e-6, f"mu step {k}")
+            close(sg_f, sg_o, 1e-4, 1e-6, f"sigma step {k}")
+            close(a_f, a_o, 1e-4, 1e-6, f"action step {k}")
+    assert int(d._act_bufs["status"].item()) == 0
+    print(f"act_step vs oracle: {n_steps} env steps, {guarded} tie-guarded groups")
+
+
 def test_act_step_matches_unfused(gpu):
-    """dr_act_step (one cooperative launch per env step) == the unfused API
+    """dr_act_step (one launch per env step, grid barriers inside) == the unfused API
     path it replaces in rollout_policy / evaluate_agent / Run: Encoder.encode
     or WorldModel.observe_step, then Actor.act (Dreamer.py:177-226, 295-322),
     same explicit noise.  Indices exact; h, action, mu, sigma at 1e-5.

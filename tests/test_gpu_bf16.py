@@ -10,9 +10,9 @@ Two checks, both through the C ABI (dr_encoder_features):
     order and the odd 1-ulp bf16 rounding flip they cause downstream);
   * precision cost: against the fp32 parity path -- normwise relative error
     <= 2e-2 (the stated bf16 tolerance of the features).
-A full train_Agent epoch in bf16 mode at BASELINE configs[1] shape must give
-finite losses, and its warm-start latents are compared with the fp32 mode's:
-the flip fraction is reported (bf16 does not promise identical indices).
+A full train_Agent epoch in bf16 mode at configs[1] (B = 64) and the north-star
+batch (B = 256) is bounded element-wise against the fp32 oracle on widely
+tie-guarded noise (test_train_agent_bf16_epoch_vs_oracle states the bounds).
 """
 import numpy as np
 import pytest
@@ -80,29 +80,91 @@ def test_encoder_bf16_matches_emulation(gpu, res):
     assert err32 <= 2e-2, f"bf16 encoder vs fp32: normwise rel err {err32:.3g}"
 
 
-def test_train_agent_bf16_epoch(gpu):
-    """One train_Agent epoch per precision at configs[1] (B=64 S=64 H=15) from
-    the same replay, weights and noise: bf16 losses finite and near fp32."""
+# bf16 mode does not promise the fp32 mode's categorical draws: a feature
+# error of ~1e-3 flips any draw whose top-2 scores are that close, and one
+# flip changes the row's whole trajectory.  The epoch test therefore widens
+# every near-tie of the (fp32) oracle's draws to a margin far above bf16 error
+# (TieGuard: runners-up within 3 % of the top score pushed down by 10 %), so
+# bf16 and the oracle walk the same trajectories and every output can be
+# bounded element-wise.
+BF16_TIE_REL, BF16_TIE_SCALE = 3e-2, 1.10
+
+
+def _nw(a, b):
+    a, b = a.detach().float().cpu().reshape(-1), b.detach().float().cpu().reshape(-1)
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+@pytest.mark.parametrize("B", [64, 256])
+def test_train_agent_bf16_epoch_vs_oracle(B, gpu):
+    """One train_Agent epoch in bf16 perf mode (precision="bf16") at configs[1]
+    (B = 64) and the north-star batch (B = 256; its chain tile GEMMs are bf16
+    too), S = 64, H = 15, against the fp32 CPU oracle on the same replay
+    windows, weights (default init) and widely tie-guarded noise (above).
+
+    Bounds (the stated bf16 tolerances of the epoch):
+      warm-start and imagined categorical indices: flip fraction <= 1e-3
+        (measured 0 on the guarded noise);
+      warm-start h0, imagined hiddens / mus / sigmas, lambda returns:
+        normwise relative error <= 1e-2;
+      critic loss: relative 1e-2; actor loss: |d| <= 1e-2 max(|ref|, 0.1);
+      S: relative 1e-3;
+      clipped actor and critic gradients: normwise relative 5e-2 per buffer.
+    The measured values are printed."""
+    import bench
+    from baseline_case import TieGuard, oracle_epoch
+    from test_gpu_baseline import CAR, run_gpu_epoch
     from dreamer_amd import Dreamer
-    from formula import FULL, replay_data
-    out = {}
-    for prec in ("fp32", "bf16"):
-        cfg = dict(FULL)
-        cfg.update(batch_size=64, sequence_length=64, horizon=15, buffer_size=1024, precision=prec)
-        torch.manual_seed(0)
-        d = Dreamer(cfg, gpu)
-        fr, ac, rw, ct = replay_data(1024, (64, 64), 3, seed=3)
-        d.buffer.load_arrays(fr, ac, rw, ct)
-        d.engine.rng.reseed(77)
-        np.random.seed(5)
-        la, lc = d.train_Agent()
-        torch.cuda.synchronize()
-        out[prec] = (float(la), float(lc), d.engine.latents[:, 0].cpu().clone())
-    (a32, c32, z32), (a16, c16, z16) = out["fp32"], out["bf16"]
-    assert np.isfinite(a16) and np.isfinite(c16)
-    flips = float((z32.reshape(-1, 32).argmax(-1) != z16.reshape(-1, 32).argmax(-1)).float().mean())
-    print(f"fp32 losses ({a32:.5f}, {c32:.5f}), bf16 ({a16:.5f}, {c16:.5f}); warm-start index flips {flips:.3%}")
-    assert abs(c16 - c32) <= 0.05 * abs(c32)
+    from oracle import dreamer_oracle as O
+    S, H, R, C, A = 64, 15, 32, 32, 3
+    cfg = dict(CAR)
+    cfg.update(batch_size=B, sequence_length=S, horizon=H, precision="bf16")
+    torch.manual_seed(0)
+    d = Dreamer(cfg, gpu)
+    P = {k: v.detach().cpu().clone() for k, v in d.state_dict().items()}
+    n = 4096
+    frames, acts, rews, conts = bench.synthetic_replay(n, (64, 64), A, seed=0)
+    starts = np.random.RandomState(500 + B).randint(0, n - S + 1, size=B)
+    g = torch.Generator().manual_seed(600 + B)
+    q_warm = torch.empty(S // 2, B * R, C).exponential_(generator=g)
+    eps = torch.randn(H, B, 1, A, generator=g)
+    q = torch.empty(H, B * R, C).exponential_(generator=g)
+    idx = starts[:, None] + np.arange(S)[None, :]
+    obs = torch.tensor(frames[idx], dtype=torch.float32)
+    act = torch.tensor(acts[idx])
+    S0 = 3.0
+    torch.set_num_threads(16)
+    ref = oracle_epoch(P, obs, act, S, H, R, C, q_warm, eps, q, S0, guard=TieGuard(BF16_TIE_REL, BF16_TIE_SCALE))
+    eng, pre = run_gpu_epoch(d, frames, acts, rews, conts, n, 0, starts, q_warm, eps, q, S0)
+    ag = d.agent
+    m = {}
+    zw = (eng.z0.cpu().reshape(-1, C).argmax(-1) != ref["z0"].reshape(-1, C).argmax(-1)).float().mean()
+    lat, hid, act_r, rew, cont, mu, sg = ref["dream"]
+    zd = (eng.latents.cpu().reshape(-1, C).argmax(-1) != lat.reshape(-1, C).argmax(-1)).float().mean()
+    m["flip_warm"], m["flip_dream"] = float(zw), float(zd)
+    m["h0"] = _nw(eng.h0, ref["h0"])
+    m["hiddens"] = _nw(eng.hiddens, hid)
+    m["mus"] = _nw(eng.mus, mu)
+    m["sigmas"] = _nw(eng.sigmas, sg)
+    m["R"] = _nw(pre["R"], ref["ts"]["R"])
+    la_ref, lc_ref = float(ref["ts"]["loss_actor"]), float(ref["ts"]["loss_critic"])
+    m["loss_actor"] = (pre["la"], la_ref)
+    m["loss_critic"] = (pre["lc"], lc_ref)
+    m["S"] = (pre["S"], float(ref["ts"]["S"]))
+    for f, keys, grads, name in ((ag.fa, O.ACTOR_KEYS, ref["ts"]["grad_actor_clipped"], "grad_actor"),
+                                 (ag.fc, O.CRITIC_KEYS, ref["ts"]["grad_critic_clipped"], "grad_critic")):
+        want = torch.cat([gr.reshape(-1) for gr in grads])
+        got = torch.cat([f.grad[f.offsets[k.split(".", 1)[1]]:f.offsets[k.split(".", 1)[1]] + gr.numel()].cpu()
+                         for k, gr in zip(keys, grads)])
+        m[name] = _nw(got, want)
+    print(f"bf16 epoch B={B} vs fp32 oracle (guarded {ref['guarded']}/{ref['draws']} draws): {m}")
+    assert m["flip_warm"] <= 1e-3 and m["flip_dream"] <= 1e-3, m
+    for k in ("h0", "hiddens", "mus", "sigmas", "R"):
+        assert m[k] <= 1e-2, (k, m[k])
+    assert abs(pre["lc"] - lc_ref) <= 1e-2 * abs(lc_ref), m["loss_critic"]
+    assert abs(pre["la"] - la_ref) <= 1e-2 * max(abs(la_ref), 0.1), m["loss_actor"]
+    assert abs(pre["S"] - float(ref["ts"]["S"])) <= 1e-3 * abs(float(ref["ts"]["S"])), m["S"]
+    assert m["grad_actor"] <= 5e-2 and m["grad_critic"] <= 5e-2, m
 
 
 @pytest.mark.parametrize("res", [64, 128])

@@ -101,6 +101,49 @@ def test_vector_wm_step_matches_oracle(gpu):
         close(p.grad.reshape(gr.shape), gr, 2e-3, 2e-4 * max(float(gr.abs().max()), 1e-6), "grad " + n)
 
 
+def test_vector_epoch_vs_oracle_B4096(gpu):
+    """BASELINE configs[4] at its batch: one train_Agent epoch (Dreamer.py:264-287)
+    with vector observations at B = 4096, S = 64, H = 15 (M = 4096-row chain
+    tiles, 61,440 returns through update_S's radix select) against the CPU
+    oracle on the same replay windows and tie-guarded explicit noise, with
+    test_gpu_baseline.compare's checks and tolerances: exact warm-start and
+    imagined indices, h0 / hiddens / actions / heads / returns at 1e-4, losses
+    1e-4, S 1e-6, clipped gradients, post-AdamW parameters.  Unpinned against
+    the reference (it has no vector encoder); everything past the MLP encoder
+    is the pinned image-mode code."""
+    from baseline_case import oracle_epoch
+    from test_gpu_baseline import compare, run_gpu_epoch
+    B, S, H = 4096, 64, 15
+    n = 8192
+    d = _dreamer(gpu, batch_size=B, sequence_length=S, horizon=H, buffer_size=n)
+    R, C = d.latent_state_dims
+    A = d.action_dims
+    P = _params(d)
+    rng = np.random.default_rng(0)
+    frames = rng.standard_normal((n, D_OBS)).astype(np.float32)
+    acts = rng.uniform(-1, 1, (n, A)).astype(np.float32)
+    r = rng.standard_normal(n).astype(np.float32)
+    rews = (np.sign(r) * np.log1p(np.abs(r))).astype(np.float32)
+    conts = np.ones(n, np.float32)
+    conts[::1000] = 0.0
+    starts = np.random.RandomState(4096).randint(0, n - S + 1, size=B)
+    g = torch.Generator().manual_seed(4097)
+    q_warm = torch.empty(S // 2, B * R, C).exponential_(generator=g)
+    eps = torch.randn(H, B, 1, A, generator=g)
+    q = torch.empty(H, B * R, C).exponential_(generator=g)
+    idx = starts[:, None] + np.arange(S)[None, :]
+    obs = torch.tensor(frames[idx])
+    act = torch.tensor(acts[idx])
+    S0 = 3.0
+    torch.set_num_threads(16)
+    ref = oracle_epoch(P, obs, act, S, H, R, C, q_warm, eps, q, S0)
+    ref["P0"] = P
+    eng, pre = run_gpu_epoch(d, frames, acts, rews, conts, n, 0, starts, q_warm, eps, q, S0)
+    n_tiny = compare(d, eng, pre, ref, C, "vector B4096", S0)
+    print(f"configs[4] B=4096 epoch: guarded {ref['guarded']}/{ref['draws']} draws, {n_tiny} near-zero-gradient "
+          f"params, actor loss {pre['la']:.6g}, critic loss {pre['lc']:.6g}, S {pre['S']:.6g}")
+
+
 def test_vector_train_agent_and_acting(gpu):
     """train_Agent from an f32 vector replay ring at B=256 (configs[4] widths,
     smaller batch): finite losses, one-hot warm-start latents; the unfused
