@@ -70,16 +70,30 @@ def synthetic_replay(n, hw, A, seed=0):
 
 def encoder_flops_per_frame(c):
     """Algorithmic FLOPs of the conv stack + latent_mapper.0 feature columns
-    for one 64x64 frame (dense conv FLOPs; SURVEY §8d counting)."""
+    for one frame (dense conv FLOPs; SURVEY §8d counting; encoder_depth 5 =
+    configs[3]'s deeper VAE, one more 4 f2 -> 4 f2 conv)."""
+    depth = int(c.get("encoder_depth", 4))
     ch = [3, c["encoder_filter_num_1"], c["encoder_filter_num_2"], 2 * c["encoder_filter_num_2"],
-          4 * c["encoder_filter_num_2"]]
+          4 * c["encoder_filter_num_2"]] + ([4 * c["encoder_filter_num_2"]] if depth == 5 else [])
     h, w = c["observation_dims"]
     fl = 0
-    for i in range(4):
+    for i in range(depth):
         h, w = h // 2, w // 2
         fl += 2 * h * w * ch[i + 1] * ch[i] * 16
-    F = ch[4] * h * w
+    F = ch[depth] * h * w
     return fl + 2 * F * c["encoder_hidden_layer_nodes"]
+
+
+def path_mflop_per_step(c, S, H):
+    """SURVEY §8d necessary MFLOP per imagined step; for the deeper VAE the
+    4-conv figure of the same resolution plus the encoder's per-frame delta
+    over the S/2 warm-start frames of each window (per imagined step: x S/2 / H)."""
+    res = c["observation_dims"][0]
+    base = PATH_MFLOP_PER_STEP.get((S, H, res))
+    if base is None or int(c.get("encoder_depth", 4)) == 4:
+        return base
+    c4 = dict(c, encoder_depth=4)
+    return round(base + (encoder_flops_per_frame(c) - encoder_flops_per_frame(c4)) / 1e6 * (S // 2) / H, 2)
 
 
 def wm_step_flops(c, B, T):
@@ -298,12 +312,13 @@ def traffic_for(B, res, precision):
     return t.get("encoder_bytes_per_epoch"), os.path.relpath(path, REPO)
 
 
-def make_dreamer(cfg, dev, B, S, H, res, ac_epochs, world, rank, group, precision):
+def make_dreamer(cfg, dev, B, S, H, res, ac_epochs, world, rank, group, precision, depth=4):
     from dreamer_amd import Dreamer
     from dreamer_amd.engine import ImaginationEngine
     c = dict(cfg)
     c.update(batch_size=B, sequence_length=S, horizon=H, observation_dims=[res, res], AC_epochs=ac_epochs,
-             buffer_size=max(4096, 8 * S), precision=precision)
+             buffer_size=max(4096, 8 * S) if res <= 64 else max(1024, 8 * S), precision=precision,
+             encoder_depth=depth)
     torch.manual_seed(0)
     d = Dreamer(c, dev)
     fr, ac, rw, ct = synthetic_replay(c["buffer_size"], c["observation_dims"], c["action_dims"], seed=0)
@@ -455,6 +470,31 @@ def main():
                           "and the projection as bf16 implicit GEMMs (f32 accumulate); the imagination / update "
                           "chain stays f32 (tests/test_gpu_bf16.py states the tolerances)")
             secondary["bf16_perf_mode"] = bf
+        # BASELINE configs[3]: 128x128 frames, the deeper VAE (encoder_depth = 5), H = 20, S = 64 at its
+        # per-GPU share of the global batch 256 over 8 GPUs (B = 32) and at the whole batch on one GPU
+        c3 = {}
+        for bb in (32, 256):
+            cc, dc = make_dreamer(CAR_RACER, dev, bb, 64, 20, 128, 1, world, rank, group, "fp32", depth=5)
+            k3 = max(3, args.steps // 2)
+            el3, (la3, lc3) = time_train_agent(dc, k3, 2)
+            v3 = world * bb * 20 * k3 / el3
+            mf3 = path_mflop_per_step(cc, 64, 20)
+            enc3 = dc._engine.time_encoder(reps=3) / 1e3
+            fl3 = encoder_flops_per_frame(cc) * bb * 32
+            c3[f"B{bb}"] = {"value": round(v3, 1), "unit": "imagined latent-steps/s",
+                            "ms_per_epoch": round(el3 / k3 * 1e3, 4), "B_per_gpu": bb, "dtype": "f32",
+                            "losses": {"actor": la3, "critic": lc3},
+                            "path_roofline": {"mflop_per_imagined_step": mf3,
+                                              "achieved": round(v3 * mf3 * 1e6 / 1e12, 2),
+                                              "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                              "frac": round(v3 * mf3 * 1e6 / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)},
+                            "encoder": {"ms": round(enc3 * 1e3, 4), "tflops": round(fl3 / enc3 / 1e12, 2),
+                                        "gflop": round(fl3 / 1e9, 2)}}
+            del dc
+        c3["note"] = ("BASELINE configs[3] (128x128 frames, deeper VAE, S=64, H=20; global B=256 on 8 GPUs = 32 per "
+                      "GPU): Dreamer.train_Agent() AC_epochs=1 with encoder_depth=5 (one more k4 s2 conv each way, "
+                      "the framework's definition: the reference has no deeper VAE); fp32 parity mode")
+        secondary["configs3_deep_vae_128px_H20"] = c3
         # BASELINE configs[4]: vector observations, B = 4096 H = 15 (S = 64 assumed)
         _, dv = make_vector_dreamer(CAR_RACER, dev, 4096, 64, 15, world, rank, group)
         kv = max(3, args.steps // 4)

@@ -26,17 +26,19 @@ class dr_dims(C.Structure):
     _fields_ = [(n, C.c_int) for n in (
         "hidden", "rows", "cols", "action", "img_h", "img_w", "enc_f1", "enc_f2", "enc_hidden",
         "prior_h1", "prior_h2", "rew_h1", "rew_h2", "cont_h1", "cont_h2",
-        "actor_h1", "actor_h2", "critic_h1", "critic_h2", "buckets", "dec_f1", "dec_f2", "dec_hidden", "precision", "obs_dim")]
+        "actor_h1", "actor_h2", "critic_h1", "critic_h2", "buckets", "dec_f1", "dec_f2", "dec_hidden", "precision", "obs_dim", "enc_depth")]
+
+DR_MAX_DEPTH = 5  # include/dreamer_hip.h: conv / convt slots (dr_dims.enc_depth <= 5)
 
 
 class dr_world_model(C.Structure):
-    _fields_ = [("conv", dr_linear * 4), ("map0", dr_linear), ("map1", dr_linear), ("map3", dr_linear),
+    _fields_ = [("conv", dr_linear * DR_MAX_DEPTH), ("map0", dr_linear), ("map1", dr_linear), ("map3", dr_linear),
                 ("w_ih", fp), ("w_hh", fp), ("b_ih", fp), ("b_hh", fp),
                 ("prior", dr_mlp3), ("reward", dr_mlp3), ("cont", dr_mlp3), ("buckets_rew", fp)]
 
 
 class dr_decoder(C.Structure):
-    _fields_ = [("up0", dr_linear), ("up1", dr_linear), ("up3", dr_linear), ("convt", dr_linear * 4)]
+    _fields_ = [("up0", dr_linear), ("up1", dr_linear), ("up3", dr_linear), ("convt", dr_linear * DR_MAX_DEPTH)]
 
 
 class dr_wm_batch(C.Structure):

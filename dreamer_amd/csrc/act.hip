@@ -521,7 +521,7 @@ extern "C" int dr_act_step(const dr_dims* d, const dr_world_model* wm, const dr_
   const int F = 4 * d->enc_f2 * (d->img_h / 16) * (d->img_w / 16), L = d->rows * d->cols;
   // the stage helpers' register batches (KJ) and the LDS staging are sized for the
   // CarRacing encoder (Dreamer.py:20-64 config); other shapes use the unfused calls
-  DR_REQUIRE(d->img_h == 64 && d->img_w == 64 && d->enc_f1 == 32 && d->enc_f2 == 64 && F + d->hidden <= 64 * 74 &&
+  DR_REQUIRE((d->enc_depth == 0 || d->enc_depth == 4) && d->img_h == 64 && d->img_w == 64 && d->enc_f1 == 32 && d->enc_f2 == 64 && F + d->hidden <= 64 * 74 &&
                  L + d->action <= 64 * 17 && d->hidden <= 64 * 10 && d->hidden + L <= 64 * 26 && d->cols <= 64 &&
                  d->rows <= ACT_NB * (ACT_NT / 64) && d->enc_hidden <= 256 && d->actor_h1 <= 256 &&
                  d->actor_h2 <= 1024 && d->action <= 64,

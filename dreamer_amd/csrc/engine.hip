@@ -8,43 +8,41 @@
 // a3  encoder features
 // ===========================================================================
 struct EncWs {
-  float *x0, *a1, *a2, *a3, *a4, *wr1, *wr2, *wr3, *wr4, *sk;
+  float *x0, *a[DR_MAX_DEPTH], *wr[DR_MAX_DEPTH], *sk;  // a[k] / wr[k]: conv k's output / repacked weight
   long long sk_n;
   void* wproj;  // bf16 mode: latent_mapper.0 feature columns as bf16 [enc_hidden][F]
 };
 
 // bf16 mode stores activations / repacked weights as bf16 (2 bytes): the same
-// carve with half-size regions (a4 holds the NCHW flatten, x0 is unused)
+// carve with half-size regions (the last a[] holds the NCHW flatten, x0 is unused)
 static void enc_carve(Carve& c, const dr_dims* d, int n, EncWs& w) {
-  if (d->obs_dim > 0) {  // vector observations: X [n][D], two MLP activations [n][F]
+  memset(&w, 0, sizeof(w));
+  if (d->obs_dim > 0) {  // vector observations: X [n][D], two MLP activations [n][F] (a[0], a[1])
     const int F = enc_feat_dim(d);
-    memset(&w, 0, sizeof(w));
     w.x0 = c.f((long long)n * d->obs_dim);
-    w.a1 = c.f((long long)n * F);
-    w.a4 = c.f((long long)n * F);
+    w.a[0] = c.f((long long)n * F);
+    w.a[1] = c.f((long long)n * F);
     w.sk_n = splitk_floats(n, d->enc_hidden);
     w.sk = c.f(w.sk_n);
     return;
   }
   const bool bf = d->precision == DR_PREC_BF16;
-  const int c1 = d->enc_f1, c2 = d->enc_f2, c3 = 2 * d->enc_f2, c4 = 4 * d->enc_f2;
-  const long long p0 = (long long)d->img_h * d->img_w, p1 = p0 / 4, p2 = p1 / 4, p3 = p2 / 4, p4 = p3 / 4;
-  auto e = [&](long long elems) { return bf ? (float*)c.raw(elems * 2) : c.f(elems); };
+  int e[DR_MAX_DEPTH + 1];
+  const int N = enc_chans(d, e);
+  const long long p0 = (long long)d->img_h * d->img_w;
+  auto act = [&](long long elems) { return bf ? (float*)c.raw(elems * 2) : c.f(elems); };
   w.sk_n = bf ? 0 : splitk_floats(n, d->enc_hidden);
   w.sk = bf ? nullptr : c.f(w.sk_n);
   w.x0 = bf ? nullptr : c.f((long long)n * p0 * 4);
-  w.a1 = e((long long)n * p1 * c1);
-  w.a2 = e((long long)n * p2 * c2);
-  w.a3 = e((long long)n * p3 * c3);
-  w.a4 = e((long long)n * p4 * c4);
-  w.wr1 = e((long long)c1 * 4 * 16);
-  // fp32: conv2..4 weights as three bf16 planes (op_conv_repack_split3, 6 bytes
+  for (int k = 0; k < N; ++k) w.a[k] = act((long long)n * (p0 >> (2 * (k + 1))) * e[k + 1]);
+  w.wr[0] = act((long long)e[1] * 4 * 16);
+  // fp32: conv2..N weights as three bf16 planes (op_conv_repack_split3, 6 bytes
   // per weight; the f32 repack of the fallback fits in the same slot)
-  auto wsl = [&](long long elems) { return bf ? (float*)c.raw(elems * 2) : (float*)c.raw(elems * 6); };
-  w.wr2 = wsl((long long)c2 * c1 * 16);
-  w.wr3 = wsl((long long)c3 * c2 * 16);
-  w.wr4 = wsl((long long)c4 * c3 * 16);
-  w.wproj = bf ? c.raw((size_t)d->enc_hidden * c4 * p4 * 2) : nullptr;
+  for (int k = 1; k < N; ++k) {
+    const long long elems = (long long)e[k + 1] * e[k] * 16;
+    w.wr[k] = bf ? (float*)c.raw(elems * 2) : (float*)c.raw(elems * 6);
+  }
+  w.wproj = bf ? c.raw((size_t)d->enc_hidden * enc_feat_dim(d) * 2) : nullptr;
 }
 
 extern "C" size_t dr_encoder_workspace_bytes(const dr_dims* d, int n_frames) {
@@ -54,30 +52,33 @@ extern "C" size_t dr_encoder_workspace_bytes(const dr_dims* d, int n_frames) {
   return c.off;
 }
 
-// bf16 perf mode (conv_bf16.hip): conv1 straight from the frames, conv2..4 as
-// bf16 NHWC implicit GEMMs, the feature projection as a bf16 NT GEMM
+// bf16 perf mode (conv_bf16.hip): conv1 straight from the frames (fused with
+// conv2 where the shape allows), conv3..N as bf16 NHWC implicit GEMMs, the
+// feature projection as a bf16 NT GEMM
 static int encoder_bf16(const dr_dims* d, const dr_world_model* wm, const dr_frames* src, int B, int n, float* feat,
                         const EncWs& w, hipStream_t s) {
-  const int c1 = d->enc_f1, c2 = d->enc_f2, c3 = 2 * d->enc_f2, c4 = 4 * d->enc_f2;
+  int e[DR_MAX_DEPTH + 1];
+  const int N = enc_chans(d, e);
   const int h0 = d->img_h, w0 = d->img_w;
-  const int F = c4 * (h0 / 16) * (w0 / 16);
-  DR_TRY(op_conv_repack_bf16(c1, 3, 4, wm->conv[0].w, w.wr1, s));
-  DR_TRY(op_conv_repack_bf16(c2, c1, c1, wm->conv[1].w, w.wr2, s));
-  DR_TRY(op_conv_repack_bf16(c3, c2, c2, wm->conv[2].w, w.wr3, s));
-  DR_TRY(op_conv_repack_bf16(c4, c3, c3, wm->conv[3].w, w.wr4, s));
+  const int F = enc_feat_dim(d);
+  DR_TRY(op_conv_repack_bf16(e[1], 3, 4, wm->conv[0].w, w.wr[0], s));
+  for (int k = 1; k < N; ++k) DR_TRY(op_conv_repack_bf16(e[k + 1], e[k], e[k], wm->conv[k].w, w.wr[k], s));
   DR_TRY(op_to_bf16_2d(d->enc_hidden, F, wm->map0.w, F + d->hidden, w.wproj, s));
-  if (op_enc12_bf16(n, B, h0, w0, c1, c2, src, w.wr1, wm->conv[0].b, w.wr2, wm->conv[1].b, w.a2, s) != DR_OK) {
-    DR_TRY(op_conv1_bf16(n, B, h0, w0, c1, src, w.wr1, wm->conv[0].b, w.a1, s));
-    DR_TRY(op_conv_bf16(n, c1, h0 / 2, w0 / 2, c2, w.a1, w.wr2, wm->conv[1].b, w.a2, 0, s));
+  if (op_enc12_bf16(n, B, h0, w0, e[1], e[2], src, w.wr[0], wm->conv[0].b, w.wr[1], wm->conv[1].b, w.a[1], s) !=
+      DR_OK) {
+    DR_TRY(op_conv1_bf16(n, B, h0, w0, e[1], src, w.wr[0], wm->conv[0].b, w.a[0], s));
+    DR_TRY(op_conv_bf16(n, e[1], h0 / 2, w0 / 2, e[2], w.a[0], w.wr[1], wm->conv[1].b, w.a[1], 0, s));
   }
-  DR_TRY(op_conv_bf16(n, c2, h0 / 4, w0 / 4, c3, w.a2, w.wr3, wm->conv[2].b, w.a3, 0, s));
-  DR_TRY(op_conv_bf16(n, c3, h0 / 8, w0 / 8, c4, w.a3, w.wr4, wm->conv[3].b, w.a4, 1, s));
-  return op_gemm_nt_bf16(n, d->enc_hidden, F, w.a4, F, w.wproj, wm->map0.b, feat, d->enc_hidden, s);
+  for (int k = 2; k < N; ++k)
+    DR_TRY(op_conv_bf16(n, e[k], h0 >> k, w0 >> k, e[k + 1], w.a[k - 1], w.wr[k], wm->conv[k].b, w.a[k],
+                        k == N - 1 ? 1 : 0, s));
+  return op_gemm_nt_bf16(n, d->enc_hidden, F, w.a[N - 1], F, w.wproj, wm->map0.b, feat, d->enc_hidden, s);
 }
 
 extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, const dr_frames* src, int B, int T,
                                    float* feat, void* ws, size_t ws_bytes, hipStream_t s) {
   DR_REQUIRE(d && wm && src && feat && B > 0 && T > 0, "null argument or empty batch");
+  DR_REQUIRE(vae_depth_ok(d), "enc_depth must be 0, 4 or 5");
   if (d->obs_dim > 0) {
     // vector observations (dr_dims.obs_dim): Linear-SiLU x2, then the feature
     // columns of latent_mapper.0 -- the MLP stand-in for VAE.py:57-75's convs
@@ -88,19 +89,22 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
     enc_carve(c, d, n, w);
     WS_CHECK(c, ws_bytes);
     DR_TRY(op_vec_gather(n, B, D, src, w.x0, s));
-    GemmArgs g1 = lin(n, F, D, w.x0, D, wm->conv[0].w, D, wm->conv[0].b, w.a1, F);
+    GemmArgs g1 = lin(n, F, D, w.x0, D, wm->conv[0].w, D, wm->conv[0].b, w.a[0], F);
     g1.act = 1;
     DR_TRY(run(G_NT, AM_PLAIN, g1, s));
-    GemmArgs g2 = lin(n, F, F, w.a1, F, wm->conv[1].w, F, wm->conv[1].b, w.a4, F);
+    GemmArgs g2 = lin(n, F, F, w.a[0], F, wm->conv[1].w, F, wm->conv[1].b, w.a[1], F);
     g2.act = 1;
     DR_TRY(run(G_NT, AM_PLAIN, g2, s));
-    GemmArgs gp = lin(n, d->enc_hidden, F, w.a4, F, wm->map0.w, F + d->hidden, wm->map0.b, feat, d->enc_hidden);
+    GemmArgs gp = lin(n, d->enc_hidden, F, w.a[1], F, wm->map0.w, F + d->hidden, wm->map0.b, feat, d->enc_hidden);
     float* sk = w.sk;
     long long skn = w.sk_n;
     give_splitk(gp, sk, skn);
     return run(G_NT, AM_PLAIN, gp, s);
   }
-  DR_REQUIRE(d->img_h % 16 == 0 && d->img_w % 16 == 0, "image size must be a multiple of 16");
+  int e[DR_MAX_DEPTH + 1];
+  const int N = enc_chans(d, e);
+  DR_REQUIRE(d->img_h % (1 << N) == 0 && d->img_w % (1 << N) == 0,
+             "image size must be a multiple of 2^depth (16, or 32 for the 5-layer encoder)");
   DR_REQUIRE(d->enc_f1 % 4 == 0 && d->enc_f2 % 4 == 0, "encoder filter counts must be multiples of 4");
   DR_REQUIRE(d->precision == DR_PREC_FP32 || d->precision == DR_PREC_BF16, "precision must be DR_PREC_FP32/BF16");
   const int n = B * T;
@@ -109,36 +113,31 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
   enc_carve(c, d, n, w);
   WS_CHECK(c, ws_bytes);
   if (d->precision == DR_PREC_BF16) return encoder_bf16(d, wm, src, B, n, feat, w, s);
-  const int c1 = d->enc_f1, c2 = d->enc_f2, c3 = 2 * d->enc_f2, c4 = 4 * d->enc_f2;
   const int h0 = d->img_h, w0 = d->img_w;
-  DR_TRY(op_conv_repack_pad(c1, 3, 4, wm->conv[0].w, w.wr1, s));
+  DR_TRY(op_conv_repack_pad(e[1], 3, 4, wm->conv[0].w, w.wr[0], s));
   // the first conv straight from the frames (u8 ring or f32); shapes it does
   // not tile go through the normalised NHWC4 copy
-  if (op_conv1_frames(n, B, h0, w0, c1, src, w.wr1, wm->conv[0].b, w.a1, s) != DR_OK) {
+  if (op_conv1_frames(n, B, h0, w0, e[1], src, w.wr[0], wm->conv[0].b, w.a[0], s) != DR_OK) {
     DR_TRY(op_frames_nhwc4(n, B, h0, w0, src, w.x0, s));
-    DR_TRY(op_conv_nhwc(n, 4, h0, w0, c1, w.x0, w.wr1, wm->conv[0].b, w.a1, 0, s));
+    DR_TRY(op_conv_nhwc(n, 4, h0, w0, e[1], w.x0, w.wr[0], wm->conv[0].b, w.a[0], 0, s));
   }
-  // conv2..4: NHWC implicit GEMMs, f32-accurate on the bf16 MFMA (3-term split,
+  // conv2..N: NHWC implicit GEMMs, f32-accurate on the bf16 MFMA (3-term split,
   // conv_split.hip) where the shape tiles, else on the f32 MFMA; the last layer
   // in NCHW == nn.Flatten order of Encoder.forward (VAE.py:72)
-  const int cin_[3] = {c1, c2, c3}, cout_[3] = {c2, c3, c4}, hin_[3] = {h0 / 2, h0 / 4, h0 / 8},
-            win_[3] = {w0 / 2, w0 / 4, w0 / 8};
-  const float* xin_[3] = {w.a1, w.a2, w.a3};
-  float* wr_[3] = {w.wr2, w.wr3, w.wr4};
-  float* y_[3] = {w.a2, w.a3, w.a4};
-  for (int l = 0; l < 3; ++l) {
-    const float* cw = wm->conv[l + 1].w;
-    const float* cb = wm->conv[l + 1].b;
-    if (op_conv_split3_supported(n, cin_[l], hin_[l], win_[l], cout_[l])) {
-      DR_TRY(op_conv_repack_split3(cout_[l], cin_[l], cw, wr_[l], s));
-      DR_TRY(op_conv_split3(n, cin_[l], hin_[l], win_[l], cout_[l], xin_[l], wr_[l], cb, y_[l], l == 2, s));
+  for (int k = 1; k < N; ++k) {
+    const int cin = e[k], cout = e[k + 1], hin = h0 >> k, win = w0 >> k, last = k == N - 1;
+    const float* cw = wm->conv[k].w;
+    const float* cb = wm->conv[k].b;
+    if (op_conv_split3_supported(n, cin, hin, win, cout)) {
+      DR_TRY(op_conv_repack_split3(cout, cin, cw, w.wr[k], s));
+      DR_TRY(op_conv_split3(n, cin, hin, win, cout, w.a[k - 1], w.wr[k], cb, w.a[k], last, s));
     } else {
-      DR_TRY(op_conv_repack_pad(cout_[l], cin_[l], cin_[l], cw, wr_[l], s));
-      DR_TRY(op_conv_nhwc(n, cin_[l], hin_[l], win_[l], cout_[l], xin_[l], wr_[l], cb, y_[l], l == 2, s));
+      DR_TRY(op_conv_repack_pad(cout, cin, cin, cw, w.wr[k], s));
+      DR_TRY(op_conv_nhwc(n, cin, hin, win, cout, w.a[k - 1], w.wr[k], cb, w.a[k], last, s));
     }
   }
-  const int F = c4 * (h0 / 16) * (w0 / 16);
-  GemmArgs gp = lin(n, d->enc_hidden, F, w.a4, F, wm->map0.w, F + d->hidden, wm->map0.b, feat, d->enc_hidden);
+  const int F = enc_feat_dim(d);
+  GemmArgs gp = lin(n, d->enc_hidden, F, w.a[N - 1], F, wm->map0.w, F + d->hidden, wm->map0.b, feat, d->enc_hidden);
   float* sk = w.sk;
   long long skn = w.sk_n;
   give_splitk(gp, sk, skn);

@@ -45,10 +45,30 @@ static inline int copy2d(float* dst, long long dpitch, const float* src, long lo
 static inline int zero(float* p, long long n, hipStream_t s) { return op_fill(n, p, 0.f, s); }
 
 static inline int latent(const dr_dims* d) { return d->rows * d->cols; }
+// stride-2 layers of the VAE (dr_dims.enc_depth: 0 / 4 = the reference's, 5 = configs[3]'s deeper VAE)
+static inline int vae_depth(const dr_dims* d) { return d->enc_depth == 5 ? 5 : 4; }
+static inline bool vae_depth_ok(const dr_dims* d) { return d->enc_depth == 0 || d->enc_depth == 4 || d->enc_depth == 5; }
+// encoder channels e[0..N]: 3, f1, f2, 2 f2, 4 f2 (, 4 f2)  (VAE.py:33-42 and its one-layer deepening)
+static inline int enc_chans(const dr_dims* d, int* e) {
+  const int N = vae_depth(d);
+  e[0] = 3; e[1] = d->enc_f1; e[2] = d->enc_f2; e[3] = 2 * d->enc_f2; e[4] = 4 * d->enc_f2;
+  if (N == 5) e[5] = 4 * d->enc_f2;
+  return N;
+}
+// decoder channels c[0..N]: 4 d2 (, 4 d2), 2 d2, d2, d1, 3  (VAE.py:128-137 and its mirror of the deepening)
+static inline int dec_chans(const dr_dims* d, int* c) {
+  const int N = vae_depth(d);
+  int k = 0;
+  c[k++] = 4 * d->dec_f2;
+  if (N == 5) c[k++] = 4 * d->dec_f2;
+  c[k++] = 2 * d->dec_f2; c[k++] = d->dec_f2; c[k++] = d->dec_f1; c[k++] = 3;
+  return N;
+}
 // encoder feature width F (latent_mapper.0 input minus h): the flattened conv
 // stack, or the vector-observation MLP's width 4*enc_f2 (dr_dims.obs_dim > 0)
 static inline int enc_feat_dim(const dr_dims* d) {
-  return d->obs_dim > 0 ? 4 * d->enc_f2 : 4 * d->enc_f2 * (d->img_h / 16) * (d->img_w / 16);
+  const int N = vae_depth(d);
+  return d->obs_dim > 0 ? 4 * d->enc_f2 : 4 * d->enc_f2 * (d->img_h >> N) * (d->img_w >> N);
 }
 
 // Y[M][N] = A[M][K] W^T + b  (torch Linear), A row stride lda

@@ -283,25 +283,27 @@ struct MlpBwd {  // backward scratch of one 3-layer head (and its LayerNorm save
   float *gx2, *gp2, *gy2, *xh2, *gx1, *gp1, *gy1, *xh1;
 };
 struct WmWs {
-  // encoder (all M frames)
-  float *x0, *pre1, *a1, *pre2, *a2, *pre3, *a3, *pre4, *a4, *feat;
-  float *wr1, *wr2, *wr3, *wr4, *wqe2, *wqe3, *wqe4;
+  // encoder (all M frames): conv k's pre-activation (NHWC) and output (NHWC; the last NCHW = the flatten order)
+  float *x0, *pre[DR_MAX_DEPTH], *a[DR_MAX_DEPTH], *feat;
+  float *wr[DR_MAX_DEPTH], *wqe[DR_MAX_DEPTH];  // conv k repacked (forward) / as a convT (data gradient, k >= 1)
   // window data, scan tape
   float *act_tm, *rew_tm, *cont_tm, *zeros, *h_all, *z_all, *soft, *plog, *pre_m, *x_m, *sr, *su, *sn, *sghn, *gi, *gh,
       *wt;
   int* idx;
   // heads (M1 rows)
   float *pp1, *px1, *pp2, *px2, *prior_lg, *rp1, *rx1, *rp2, *rx2, *rew_lg, *cp1, *cx1, *cp2, *cx2, *cont_lg;
-  float *du1, *dx1, *du2, *dq1, *dq2, *dq3, *dg4, *w3p, *b3p, *wqd[4], *wrd[4];
-  float *du2p, *dq1p, *dq2p, *dq3p;  // SiLU of the decoder pre-activations (what the next layer reads)
+  // decoder: upscaler pre-activations (du1, du2 = .3 output NHWC), convT k's output pre-activation dq[k] (k < N-1;
+  // vector mode: dq[0] = image_builder.0 pre, dq[1] = mu) and its SiLU dqp[k]; dgout = dL/d(pre-tanh output)
+  float *du1, *dx1, *du2, *du2p, *dq[DR_MAX_DEPTH], *dqp[DR_MAX_DEPTH], *dgout, *w3p, *b3p;
+  float *wqd[DR_MAX_DEPTH], *wrd[DR_MAX_DEPTH];
   // loss
   float *coef_row, *coef_obs, *obs_part, *kl_grp, *rew_row, *cont_row, *scal, *stats;
   // backward
   float *gH, *gZ, *glog, *gpost, *g_prior, *g_rew, *g_cont;
   MlpBwd bp, br, bc;
-  float *gxu, *gpu, *gyu, *xhu, *dgq3, *dgq2, *dgq1, *dgu2, *dw3p, *db3p;
+  float *gxu, *gpu, *gyu, *xhu, *dgq[DR_MAX_DEPTH], *dgu2, *dw3p, *db3p;  // dgq[k]: dL/d dq[k]
   float *ggi, *ggh, *gpre_m, *gy_m, *xh_m, *gx_s, *gh_dummy;
-  float *ga4, *gp3, *gp2, *gp1;
+  float* gp[DR_MAX_DEPTH];  // dL/d pre[k]
   // transposed / permuted weights
   float *t_pl6, *t_pl3, *t_pl0, *t_rl6, *t_rl3, *t_rl0, *t_cl6, *t_cl3, *t_cl0, *t_up3, *t_up0, *t_map3, *t_map0, *t_whh,
       *w0tp;
@@ -312,31 +314,38 @@ struct WmWs {
 };
 
 struct WmDims {
-  int B, T, M, M1, L, Hd, A, eh, nb, IH, IW, c1, c2, c3, c4, P16, F, d1, d2, C0, dh, Fd, ph1, ph2, rh1, rh2, ch1, ch2;
-  long long p0, p1, p2, p3;
+  int B, T, M, M1, L, Hd, A, eh, nb, IH, IW, Pf, F, d1, d2, C0, dh, Fd, ph1, ph2, rh1, rh2, ch1, ch2;
+  int N;                                        // VAE depth (4 = the reference, 5 = configs[3]'s deeper VAE)
+  int e[DR_MAX_DEPTH + 1], cd[DR_MAX_DEPTH + 1];  // encoder / decoder channels (engine_util.h enc_chans / dec_chans)
+  long long pix[DR_MAX_DEPTH + 1];              // pixels per frame at resolution level k: (IH >> k) (IW >> k)
   int Dv;  // vector observations (dr_dims.obs_dim): MLP encoder / decoder, no conv planes
 };
 static WmDims wm_dims(const dr_dims* d, int B, int T) {
   WmDims w;
+  memset(&w, 0, sizeof(w));
   w.B = B; w.T = T; w.M = B * T; w.M1 = B * (T - 1);
   w.L = latent(d); w.Hd = d->hidden; w.A = d->action; w.eh = d->enc_hidden; w.nb = d->buckets;
   w.IH = d->img_h; w.IW = d->img_w;
-  w.c1 = d->enc_f1; w.c2 = d->enc_f2; w.c3 = 2 * d->enc_f2; w.c4 = 4 * d->enc_f2;
-  w.P16 = (w.IH / 16) * (w.IW / 16);
-  w.F = w.c4 * w.P16;
-  w.d1 = d->dec_f1; w.d2 = d->dec_f2; w.C0 = 4 * d->dec_f2; w.dh = d->dec_hidden; w.Fd = w.C0 * w.P16;
+  w.N = enc_chans(d, w.e);
+  dec_chans(d, w.cd);
+  for (int k = 0; k <= w.N; ++k) w.pix[k] = (long long)(w.IH >> k) * (w.IW >> k);
+  w.Pf = (int)w.pix[w.N];
+  w.F = w.e[w.N] * w.Pf;
+  w.d1 = d->dec_f1; w.d2 = d->dec_f2; w.C0 = 4 * d->dec_f2; w.dh = d->dec_hidden; w.Fd = w.C0 * w.Pf;
   w.ph1 = d->prior_h1; w.ph2 = d->prior_h2; w.rh1 = d->rew_h1; w.rh2 = d->rew_h2; w.ch1 = d->cont_h1; w.ch2 = d->cont_h2;
-  w.p0 = (long long)w.IH * w.IW; w.p1 = w.p0 / 4; w.p2 = w.p0 / 16; w.p3 = w.p0 / 64;
   w.Dv = d->obs_dim > 0 ? d->obs_dim : 0;
   if (w.Dv) {  // widths of the MLP stand-ins (include/dreamer_hip.h, dr_dims.obs_dim)
     w.IH = w.IW = 0;
-    w.P16 = 1;
-    w.F = w.c4;
+    w.Pf = 1;
+    w.F = 4 * d->enc_f2;
     w.Fd = w.C0;
-    w.p0 = w.p1 = w.p2 = w.p3 = 0;
+    for (int k = 0; k <= w.N; ++k) w.pix[k] = 0;
   }
   return w;
 }
+// channel stride of conv k's input (the frames are padded to 4 channels) and of convT k's output (3 -> 4)
+static inline int enc_cin_st(const WmDims& D, int k) { return k == 0 ? 4 : D.e[k]; }
+static inline int dec_cout_st(const WmDims& D, int k) { return k == D.N - 1 ? 4 : D.cd[k + 1]; }
 
 static void mlp_bwd_carve(Carve& c, long long M1, int w1, int w2, MlpBwd& b) {
   b.gx2 = c.f(M1 * w2); b.gp2 = c.f(M1 * w2); b.gy2 = c.f(M1 * w2); b.xh2 = c.f(M1 * w2);
@@ -345,39 +354,40 @@ static void mlp_bwd_carve(Carve& c, long long M1, int w1, int w2, MlpBwd& b) {
 
 static long long wm_conv_scratch(const WmDims& D) {
   if (D.Dv) return 0;  // vector observations: no convolution planes
-  const int n = D.M, n1 = D.M1;
+  const int n = D.M, n1 = D.M1, N = D.N;
   long long m = 0;
   auto mx = [&](long long v) { if (v > m) m = v; };
-  // encoder weight grads: lo = output grad (h, w), hi = input
-  mx(op_conv_wgrad_ws_floats(n, D.IH / 2, D.IW / 2, D.c1, 4));
-  mx(op_conv_wgrad_ws_floats(n, D.IH / 4, D.IW / 4, D.c2, D.c1));
-  mx(op_conv_wgrad_ws_floats(n, D.IH / 8, D.IW / 8, D.c3, D.c2));
-  mx(op_conv_wgrad_ws_floats(n, D.IH / 16, D.IW / 16, D.c4, D.c3));
-  // decoder weight grads: lo = convT input, hi = output grad
-  mx(op_conv_wgrad_ws_floats(n1, D.IH / 16, D.IW / 16, D.C0, 2 * D.d2));
-  mx(op_conv_wgrad_ws_floats(n1, D.IH / 8, D.IW / 8, 2 * D.d2, D.d2));
-  mx(op_conv_wgrad_ws_floats(n1, D.IH / 4, D.IW / 4, D.d2, D.d1));
-  mx(op_conv_wgrad_ws_floats(n1, D.IH / 2, D.IW / 2, D.d1, 4));
-  mx(op_chan_sum_ws_floats((long long)n * D.p1, D.c1));
-  mx(op_chan_sum_ws_floats((long long)n1 * D.p0, 3));
-  mx(op_chan_sum_ws_floats((long long)n1 * D.p1, D.d1));
+  for (int k = 0; k < N; ++k) {
+    // encoder conv k: lo = output grad (res k + 1), hi = input; its bias sum
+    mx(op_conv_wgrad_ws_floats(n, D.IH >> (k + 1), D.IW >> (k + 1), D.e[k + 1], enc_cin_st(D, k)));
+    mx(op_chan_sum_ws_floats((long long)n * D.pix[k + 1], D.e[k + 1]));
+    // decoder convT k: lo = input (res N - k), hi = output grad; its bias sum
+    mx(op_conv_wgrad_ws_floats(n1, D.IH >> (N - k), D.IW >> (N - k), D.cd[k], dec_cout_st(D, k)));
+    mx(op_chan_sum_ws_floats((long long)n1 * D.pix[N - k - 1], D.cd[k + 1]));
+  }
   return m;
 }
 
 static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
+  memset(&w, 0, sizeof(w));
   const long long M = D.M, M1 = D.M1, B = D.B;
-  const int L = D.L, Hd = D.Hd, A = D.A, eh = D.eh;
+  const int L = D.L, Hd = D.Hd, A = D.A, eh = D.eh, N = D.N;
   const long long Dv = D.Dv;
-  w.x0 = c.f(Dv ? M * Dv : M * D.p0 * 4);
-  w.pre1 = c.f(Dv ? M * D.F : M * D.p1 * D.c1); w.a1 = c.f(Dv ? M * D.F : M * D.p1 * D.c1);
-  w.pre2 = c.f(M * D.p2 * D.c2); w.a2 = c.f(M * D.p2 * D.c2);
-  w.pre3 = c.f(M * D.p3 * D.c3); w.a3 = c.f(M * D.p3 * D.c3);
-  w.pre4 = c.f(M * D.F); w.a4 = c.f(M * D.F);
+  w.x0 = c.f(Dv ? M * Dv : M * D.pix[0] * 4);
+  if (Dv) {  // MLP stand-in: layer 0 and the last layer of the conv slots, [M][F] each
+    w.pre[0] = c.f(M * D.F); w.a[0] = c.f(M * D.F);
+    w.pre[N - 1] = c.f(M * D.F); w.a[N - 1] = c.f(M * D.F);
+  } else {
+    for (int k = 0; k < N; ++k) {
+      w.pre[k] = c.f(M * D.pix[k + 1] * D.e[k + 1]);
+      w.a[k] = c.f(M * D.pix[k + 1] * D.e[k + 1]);
+    }
+  }
   w.feat = c.f(M * eh);
-  w.wr1 = c.f((long long)D.c1 * 16 * 4); w.wr2 = c.f((long long)D.c2 * 16 * D.c1);
-  w.wr3 = c.f((long long)D.c3 * 16 * D.c2); w.wr4 = c.f((long long)D.c4 * 16 * D.c3);
-  w.wqe2 = c.f((long long)16 * D.c2 * D.c1); w.wqe3 = c.f((long long)16 * D.c3 * D.c2);
-  w.wqe4 = c.f((long long)16 * D.c4 * D.c3);
+  for (int k = 0; k < N; ++k) {
+    w.wr[k] = c.f((long long)D.e[k + 1] * 16 * enc_cin_st(D, k));
+    if (k > 0) w.wqe[k] = c.f((long long)16 * D.e[k + 1] * D.e[k]);
+  }
   w.act_tm = c.f(M * A); w.rew_tm = c.f(M); w.cont_tm = c.f(M);
   w.zeros = c.f(B * (L + A + Hd));
   w.h_all = c.f(M * Hd); w.z_all = c.f(M * L); w.soft = c.f(M * L); w.plog = c.f(M * L);
@@ -392,18 +402,21 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
   w.rew_lg = c.f(M1 * D.nb);
   w.cp1 = c.f(M1 * D.ch1); w.cx1 = c.f(M1 * D.ch1); w.cp2 = c.f(M1 * D.ch2); w.cx2 = c.f(M1 * D.ch2);
   w.cont_lg = c.f(M1);
-  w.du1 = c.f(M1 * D.dh); w.dx1 = c.f(M1 * D.dh); w.du2 = c.f(M1 * D.Fd);
-  // vector mode: dq1 / dq1p = image_builder.0 pre / post SiLU [M1][Fd], dq2 = the output mu [M1][Dv]
-  w.dq1 = c.f(Dv ? M1 * D.Fd : M1 * D.p3 * 2 * D.d2); w.dq2 = c.f(Dv ? M1 * Dv : M1 * D.p2 * D.d2);
-  w.dq3 = c.f(M1 * D.p1 * D.d1);
-  w.du2p = c.f(M1 * D.Fd);
-  w.dq1p = c.f(Dv ? M1 * D.Fd : M1 * D.p3 * 2 * D.d2); w.dq2p = c.f(M1 * D.p2 * D.d2); w.dq3p = c.f(M1 * D.p1 * D.d1);
-  w.dg4 = c.f(Dv ? M1 * Dv : M1 * D.p0 * 4);
+  w.du1 = c.f(M1 * D.dh); w.dx1 = c.f(M1 * D.dh); w.du2 = c.f(M1 * D.Fd); w.du2p = c.f(M1 * D.Fd);
+  if (Dv) {  // dq[0] / dqp[0] = image_builder.0 pre / post SiLU [M1][Fd], dq[1] = the output mu [M1][Dv]
+    w.dq[0] = c.f(M1 * D.Fd); w.dqp[0] = c.f(M1 * D.Fd); w.dq[1] = c.f(M1 * Dv);
+    w.dgq[0] = c.f(M1 * D.Fd);
+  } else {
+    for (int k = 0; k + 1 < N; ++k) {  // convT k output at resolution level N - k - 1
+      const long long sz = M1 * D.pix[N - k - 1] * D.cd[k + 1];
+      w.dq[k] = c.f(sz); w.dqp[k] = c.f(sz); w.dgq[k] = c.f(sz);
+    }
+  }
+  w.dgout = c.f(Dv ? M1 * Dv : M1 * D.pix[0] * 4);
   w.w3p = c.f((long long)D.Fd * D.dh); w.b3p = c.f(D.Fd);
-  const int cin_t[4] = {D.C0, 2 * D.d2, D.d2, D.d1}, cout_t[4] = {2 * D.d2, D.d2, D.d1, 3};
-  for (int k = 0; k < 4; ++k) {
-    w.wqd[k] = c.f((long long)16 * cin_t[k] * cout_t[k]);
-    w.wrd[k] = c.f((long long)16 * cin_t[k] * (k == 3 ? 4 : cout_t[k]));
+  for (int k = 0; k < N; ++k) {
+    w.wqd[k] = c.f((long long)16 * D.cd[k] * D.cd[k + 1]);
+    w.wrd[k] = c.f((long long)16 * D.cd[k] * dec_cout_st(D, k));
   }
   w.coef_row = c.f(M1); w.coef_obs = c.f(M1);
   w.obs_part = c.f(Dv ? M1 : M1 * op_convT_mse_parts(D.IH / 2, D.IW / 2));
@@ -414,14 +427,16 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
   mlp_bwd_carve(c, M1, D.rh1, D.rh2, w.br);
   mlp_bwd_carve(c, M1, D.ch1, D.ch2, w.bc);
   w.gxu = c.f(M1 * D.dh); w.gpu = c.f(M1 * D.dh); w.gyu = c.f(M1 * D.dh); w.xhu = c.f(M1 * D.dh);
-  w.dgq3 = c.f(M1 * D.p1 * D.d1); w.dgq2 = c.f(M1 * D.p2 * D.d2); w.dgq1 = c.f(Dv ? M1 * D.Fd : M1 * D.p3 * 2 * D.d2);
   w.dgu2 = c.f(M1 * D.Fd);
   w.dw3p = c.f((long long)D.Fd * D.dh); w.db3p = c.f(D.Fd);
   w.ggi = c.f(M * 3 * Hd); w.ggh = c.f(M * 3 * Hd);
   w.gpre_m = c.f(M * eh); w.gy_m = c.f(M * eh); w.xh_m = c.f(M * eh);
   w.gx_s = c.f(B * eh); w.gh_dummy = c.f(B * Hd);
-  w.ga4 = c.f(M * D.F); w.gp3 = c.f(M * D.p3 * D.c3); w.gp2 = c.f(M * D.p2 * D.c2);
-  w.gp1 = c.f(Dv ? M * D.F : M * D.p1 * D.c1);
+  if (Dv) {
+    w.gp[0] = c.f(M * D.F); w.gp[N - 1] = c.f(M * D.F);
+  } else {
+    for (int k = 0; k < N; ++k) w.gp[k] = c.f(M * D.pix[k + 1] * D.e[k + 1]);
+  }
   w.t_pl6 = c.f((long long)L * D.ph2); w.t_pl3 = c.f((long long)D.ph2 * D.ph1); w.t_pl0 = c.f((long long)D.ph1 * Hd);
   w.t_rl6 = c.f((long long)D.nb * D.rh2); w.t_rl3 = c.f((long long)D.rh2 * D.rh1);
   w.t_rl0 = c.f((long long)D.rh1 * (Hd + L));
@@ -488,7 +503,9 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
                   hipStream_t s) {
   DR_REQUIRE(d && wm && dec && src && bt && losses && gw && gd && stats && B > 0 && T >= 2, "null argument or T < 2");
   DR_REQUIRE(bt->actions && bt->rewards && bt->continues, "window actions / rewards / continues required");
-  DR_REQUIRE(d->obs_dim > 0 || (d->img_h % 16 == 0 && d->img_w % 16 == 0), "image size must be a multiple of 16");
+  DR_REQUIRE(vae_depth_ok(d), "enc_depth must be 0, 4 or 5");
+  DR_REQUIRE(d->obs_dim > 0 || (d->img_h % (1 << vae_depth(d)) == 0 && d->img_w % (1 << vae_depth(d)) == 0),
+             "image size must be a multiple of 2^depth (16, or 32 for the 5-layer VAE)");
   DR_REQUIRE(d->enc_f1 % 8 == 0 && d->enc_f2 % 8 == 0 && d->dec_f1 % 8 == 0 && d->dec_f2 % 8 == 0,
              "encoder / decoder filter counts must be multiples of 8");
   DR_REQUIRE(d->cols <= 64, "latent classes must be <= 64");
@@ -501,35 +518,33 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   wm_carve(c, d, D, w);
   WS_CHECK(c, ws_bytes);
   const int M = D.M, M1 = D.M1, L = D.L, Hd = D.Hd, A = D.A, eh = D.eh, nb = D.nb, F = D.F, R = d->rows;
-  const int IH = D.IH, IW = D.IW;
+  const int IH = D.IH, IW = D.IW, N = D.N;
   const float* hB = w.h_all + (long long)B * Hd;
   const float* zB = w.z_all + (long long)B * L;
   float* gHB = w.gH + (long long)B * Hd;
   float* gZB = w.gZ + (long long)B * L;
 
-  const int cin_t[4] = {D.C0, 2 * D.d2, D.d2, D.d1}, cout_t[4] = {2 * D.d2, D.d2, D.d1, 3};
+  const int* cin_t = D.cd;       // convT k: cd[k] -> cd[k + 1] channels
+  const int* cout_t = D.cd + 1;
   if (rows_global <= 0) rows_global = M1;
   if (phases & DR_WM_PREP) {
   // ---- weights: repacks, transposes, permutations (fixed for the call) ----
   if (!vec) {
-  DR_TRY(op_conv_repack_pad(D.c1, 3, 4, wm->conv[0].w, w.wr1, s));
-  DR_TRY(op_conv_repack_pad(D.c2, D.c1, D.c1, wm->conv[1].w, w.wr2, s));
-  DR_TRY(op_conv_repack_pad(D.c3, D.c2, D.c2, wm->conv[2].w, w.wr3, s));
-  DR_TRY(op_conv_repack_pad(D.c4, D.c3, D.c3, wm->conv[3].w, w.wr4, s));
-  // Conv2d data gradient = upsampling conv with the weight read as [cin=co][cout=ci]
-  DR_TRY(op_convT_repack(D.c2, D.c1, wm->conv[1].w, w.wqe2, s));
-  DR_TRY(op_convT_repack(D.c3, D.c2, wm->conv[2].w, w.wqe3, s));
-  DR_TRY(op_convT_repack(D.c4, D.c3, wm->conv[3].w, w.wqe4, s));
-  for (int k = 0; k < 4; ++k) {
-    if (k < 3) DR_TRY(op_convT_repack(cin_t[k], cout_t[k], dec->convt[k].w, w.wqd[k], s));
+  for (int k = 0; k < N; ++k) {
+    DR_TRY(op_conv_repack_pad(D.e[k + 1], D.e[k], enc_cin_st(D, k), wm->conv[k].w, w.wr[k], s));
+    // Conv2d data gradient = upsampling conv with the weight read as [cin=co][cout=ci]
+    if (k > 0) DR_TRY(op_convT_repack(D.e[k + 1], D.e[k], wm->conv[k].w, w.wqe[k], s));
+  }
+  for (int k = 0; k < N; ++k) {
+    if (k < N - 1) DR_TRY(op_convT_repack(cin_t[k], cout_t[k], dec->convt[k].w, w.wqd[k], s));
     else DR_TRY(op_convT_out3_repack(cin_t[k], dec->convt[k].w, w.wqd[k], s));
     // ConvTranspose2d data gradient = strided Conv2d with the weight read as [out=ci][in=co]
-    DR_TRY(op_conv_repack_pad(cin_t[k], cout_t[k], k == 3 ? 4 : cout_t[k], dec->convt[k].w, w.wrd[k], s));
+    DR_TRY(op_conv_repack_pad(cin_t[k], cout_t[k], dec_cout_st(D, k), dec->convt[k].w, w.wrd[k], s));
   }
   }  // !vec
-  // decoder.upscaler.3 rows to NHWC order (vector mode: P16 = 1, the identity), so its output is the first convT's NHWC input
-  DR_TRY(perm_rows(D.C0, D.P16, D.dh, dec->up3.w, w.w3p, 1, s));
-  DR_TRY(perm_rows(D.C0, D.P16, 1, dec->up3.b, w.b3p, 1, s));
+  // decoder.upscaler.3 rows to NHWC order (vector mode: Pf = 1, the identity), so its output is the first convT's NHWC input
+  DR_TRY(perm_rows(D.C0, D.Pf, D.dh, dec->up3.w, w.w3p, 1, s));
+  DR_TRY(perm_rows(D.C0, D.Pf, 1, dec->up3.b, w.b3p, 1, s));
   {
     TransposeJob tj[10] = {
         {L, D.ph2, L, wm->prior.l6.w, w.t_pl6},          {D.ph2, D.ph1, D.ph2, wm->prior.l3.w, w.t_pl3},
@@ -547,7 +562,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     DR_TRY(op_transpose_multi(tj2, 5, s));
   }
   // latent_mapper.0 feature rows (of its transpose) to NHWC: dL/d conv4-out comes out NHWC
-  DR_TRY(perm_rows(D.c4, D.P16, eh, w.t_map0, w.w0tp, 1, s));
+  DR_TRY(perm_rows(D.e[N], D.Pf, eh, w.t_map0, w.w0tp, 1, s));
 
   // ---- window data ----
   hipLaunchKernelGGL(k_wm_gather, dim3(blocks(M, 256)), dim3(256), 0, s, B, T, A, *bt, w.act_tm, w.rew_tm, w.cont_tm);
@@ -563,23 +578,23 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   DR_TRY(dr_check_launch("wm_coef"));
 
   // ---- encoder over all M frames (VAE.py:57-75), activations kept ----
-  if (vec) {  // MLP stand-in: pre1 = X W1^T + b1, a1 = SiLU, pre4 = a1 W2^T + b2, a4 = SiLU
+  float* aL = w.a[N - 1];  // the flattened features (NCHW; vector mode: the MLP's last activation)
+  if (vec) {  // MLP stand-in: pre[0] = X W1^T + b1, a[0] = SiLU, pre[N-1] = a[0] W2^T + b2, a[N-1] = SiLU
     DR_TRY(op_vec_gather(M, B, Dv, src, w.x0, s));
-    DR_TRY(run(G_NT, AM_PLAIN, lin(M, F, Dv, w.x0, Dv, wm->conv[0].w, Dv, wm->conv[0].b, w.pre1, F), s));
-    hipLaunchKernelGGL(k_silu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, w.pre1, w.a1);
+    DR_TRY(run(G_NT, AM_PLAIN, lin(M, F, Dv, w.x0, Dv, wm->conv[0].w, Dv, wm->conv[0].b, w.pre[0], F), s));
+    hipLaunchKernelGGL(k_silu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, w.pre[0], w.a[0]);
     DR_TRY(dr_check_launch("silu"));
-    DR_TRY(run(G_NT, AM_PLAIN, lin(M, F, F, w.a1, F, wm->conv[1].w, F, wm->conv[1].b, w.pre4, F), s));
-    hipLaunchKernelGGL(k_silu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, w.pre4, w.a4);
+    DR_TRY(run(G_NT, AM_PLAIN, lin(M, F, F, w.a[0], F, wm->conv[1].w, F, wm->conv[1].b, w.pre[N - 1], F), s));
+    hipLaunchKernelGGL(k_silu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, w.pre[N - 1], aL);
     DR_TRY(dr_check_launch("silu"));
   } else {
   DR_TRY(op_frames_nhwc4(M, B, IH, IW, src, w.x0, s));
-  DR_TRY(op_conv_nhwc_ex(M, 4, IH, IW, D.c1, w.x0, w.wr1, wm->conv[0].b, w.a1, 0, w.pre1, CONV_EPI_FWD, s));
-  DR_TRY(op_conv_nhwc_ex(M, D.c1, IH / 2, IW / 2, D.c2, w.a1, w.wr2, wm->conv[1].b, w.a2, 0, w.pre2, CONV_EPI_FWD, s));
-  DR_TRY(op_conv_nhwc_ex(M, D.c2, IH / 4, IW / 4, D.c3, w.a2, w.wr3, wm->conv[2].b, w.a3, 0, w.pre3, CONV_EPI_FWD, s));
-  DR_TRY(op_conv_nhwc_ex(M, D.c3, IH / 8, IW / 8, D.c4, w.a3, w.wr4, wm->conv[3].b, w.a4, 1, w.pre4, CONV_EPI_FWD, s));
+  for (int k = 0; k < N; ++k)
+    DR_TRY(op_conv_nhwc_ex(M, enc_cin_st(D, k), IH >> k, IW >> k, D.e[k + 1], k ? w.a[k - 1] : w.x0, w.wr[k],
+                           wm->conv[k].b, w.a[k], k == N - 1 ? 1 : 0, w.pre[k], CONV_EPI_FWD, s));
   }
   {
-    GemmArgs g = lin(M, eh, F, w.a4, F, wm->map0.w, F + Hd, wm->map0.b, w.feat, eh);
+    GemmArgs g = lin(M, eh, F, aL, F, wm->map0.w, F + Hd, wm->map0.b, w.feat, eh);
     splitk_all(&g, 1, w.sk, w.sk_n);
     DR_TRY(run(G_NT, AM_PLAIN, g, s));
   }
@@ -648,31 +663,28 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     const long long MF = (long long)M1 * D.Fd;
     hipLaunchKernelGGL(k_silu, dim3(blocks(MF, 256)), dim3(256), 0, s, MF, w.du2, w.du2p);
     DR_TRY(dr_check_launch("silu"));
-    DR_TRY(run(G_NT, AM_PLAIN, lin(M1, D.Fd, D.Fd, w.du2p, D.Fd, dec->convt[0].w, D.Fd, dec->convt[0].b, w.dq1, D.Fd), s));
-    hipLaunchKernelGGL(k_silu, dim3(blocks(MF, 256)), dim3(256), 0, s, MF, w.dq1, w.dq1p);
+    DR_TRY(run(G_NT, AM_PLAIN, lin(M1, D.Fd, D.Fd, w.du2p, D.Fd, dec->convt[0].w, D.Fd, dec->convt[0].b, w.dq[0], D.Fd), s));
+    hipLaunchKernelGGL(k_silu, dim3(blocks(MF, 256)), dim3(256), 0, s, MF, w.dq[0], w.dqp[0]);
     DR_TRY(dr_check_launch("silu"));
-    DR_TRY(run(G_NT, AM_PLAIN, lin(M1, Dv, D.Fd, w.dq1p, D.Fd, dec->convt[1].w, D.Fd, dec->convt[1].b, w.dq2, Dv), s));
-    hipLaunchKernelGGL(k_vec_mse, dim3(blocks(M1, 4)), dim3(256), 0, s, M1, Dv, w.dq2, w.x0 + (long long)B * Dv,
-                       w.coef_obs, w.dg4, w.obs_part);
+    DR_TRY(run(G_NT, AM_PLAIN, lin(M1, Dv, D.Fd, w.dqp[0], D.Fd, dec->convt[1].w, D.Fd, dec->convt[1].b, w.dq[1], Dv), s));
+    hipLaunchKernelGGL(k_vec_mse, dim3(blocks(M1, 4)), dim3(256), 0, s, M1, Dv, w.dq[1], w.x0 + (long long)B * Dv,
+                       w.coef_obs, w.dgout, w.obs_part);
     DR_TRY(dr_check_launch("vec_mse"));
   } else {
     hipLaunchKernelGGL(k_silu, dim3(blocks((long long)M1 * D.Fd, 256)), dim3(256), 0, s, (long long)M1 * D.Fd,
                        w.du2, w.du2p);
     DR_TRY(dr_check_launch("silu"));
-    const float* ins[4] = {w.du2p, w.dq1p, w.dq2p, w.dq3p};
-    float* outs[3] = {w.dq1, w.dq2, w.dq3};
-    float* posts[3] = {w.dq1p, w.dq2p, w.dq3p};
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < N; ++k) {
       ConvTArgs a = {};
-      a.n = M1; a.cin = cin_t[k]; a.h = IH >> (4 - k); a.w = IW >> (4 - k); a.cout = cout_t[k];
-      a.in = ins[k]; a.silu_in = 0; a.wq = w.wqd[k]; a.bias = dec->convt[k].b;
-      if (k < 3) {
-        a.out = outs[k]; a.out2 = posts[k]; a.ldc = cout_t[k];
+      a.n = M1; a.cin = cin_t[k]; a.h = IH >> (N - k); a.w = IW >> (N - k); a.cout = cout_t[k];
+      a.in = k ? w.dqp[k - 1] : w.du2p; a.silu_in = 0; a.wq = w.wqd[k]; a.bias = dec->convt[k].b;
+      if (k < N - 1) {
+        a.out = w.dq[k]; a.out2 = w.dqp[k]; a.ldc = cout_t[k];
         DR_TRY(op_convT_nhwc(CT_EPI_BIAS, a, s));
       } else {
         // Tanh + squared error against frames t >= 1 (WorldModel.py:129); writes dL/d(pre-tanh)
-        a.out = w.dg4; a.ldc = 4;
-        a.target = w.x0 + (long long)B * D.p0 * 4; a.tstride = 4;
+        a.out = w.dgout; a.ldc = 4;
+        a.target = w.x0 + (long long)B * D.pix[0] * 4; a.tstride = 4;
         a.coef = w.coef_obs; a.part = w.obs_part;
         DR_TRY(op_convT_nhwc(CT_EPI_TANH_MSE, a, s));
       }
@@ -726,7 +738,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
                   w.cp2, 1, hB, zB, gHB, gZB, w.bc, w.sk, w.sk_n, s));
   // decoder: image_builder.6 .. .0 (data grads as strided convs, weight grads, bias sums)
   if (vec) {
-    // image_builder stand-in backward: dg4 = dL/dmu -> Wd2 / bd2 grads, dL/dq = (dg4 Wd2) SiLU'(q)
+    // image_builder stand-in backward: dgout = dL/dmu -> Wd2 / bd2 grads, dL/dq = (dgout Wd2) SiLU'(q)
     // -> Wd1 / bd1 grads, dL/d du2 = (dL/dq Wd1) SiLU'(du2)  (NN products with the weights as stored)
     const long long MF = (long long)M1 * D.Fd;
     auto nn = [&](int N, int K, const float* A, const float* Wkn, float* Y) {
@@ -734,32 +746,32 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
       g.M = M1; g.N = N; g.K = K; g.A = A; g.lda = K; g.W = Wkn; g.ldb = N; g.Y = Y; g.ldy = N;
       return gemm_launch(G_NN, AM_PLAIN, &g, 1, s);
     };
-    DR_TRY(nn(D.Fd, Dv, w.dg4, dec->convt[1].w, w.dgq1));
-    hipLaunchKernelGGL(k_mul_dsilu, dim3(blocks(MF, 256)), dim3(256), 0, s, MF, w.dgq1, w.dq1);
+    DR_TRY(nn(D.Fd, Dv, w.dgout, dec->convt[1].w, w.dgq[0]));
+    hipLaunchKernelGGL(k_mul_dsilu, dim3(blocks(MF, 256)), dim3(256), 0, s, MF, w.dgq[0], w.dq[0]);
     DR_TRY(dr_check_launch("mul_dsilu"));
-    DR_TRY(nn(D.Fd, D.Fd, w.dgq1, dec->convt[0].w, w.dgu2));
+    DR_TRY(nn(D.Fd, D.Fd, w.dgq[0], dec->convt[0].w, w.dgu2));
     hipLaunchKernelGGL(k_mul_dsilu, dim3(blocks(MF, 256)), dim3(256), 0, s, MF, w.dgu2, w.du2);
     DR_TRY(dr_check_launch("mul_dsilu"));
     GemmArgs p[2];
-    p[0] = bwd_w(Dv, D.Fd, M1, w.dg4, Dv, w.dq1p, D.Fd, gd->convt[1].w);
-    p[1] = bwd_w(D.Fd, D.Fd, M1, w.dgq1, D.Fd, w.du2p, D.Fd, gd->convt[0].w);
+    p[0] = bwd_w(Dv, D.Fd, M1, w.dgout, Dv, w.dqp[0], D.Fd, gd->convt[1].w);
+    p[1] = bwd_w(D.Fd, D.Fd, M1, w.dgq[0], D.Fd, w.du2p, D.Fd, gd->convt[0].w);
     splitk_all(p, 2, w.sk, w.sk_n);
     DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 2, s));
-    ColsumJob cj[2] = {{Dv, w.dg4, Dv, nullptr, 0, gd->convt[1].b}, {D.Fd, w.dgq1, D.Fd, nullptr, 0, gd->convt[0].b}};
+    ColsumJob cj[2] = {{Dv, w.dgout, Dv, nullptr, 0, gd->convt[1].b}, {D.Fd, w.dgq[0], D.Fd, nullptr, 0, gd->convt[0].b}};
     DR_TRY(op_colsum_multi(M1, cj, 2, s));
   } else {
-    float* gins[4] = {w.dgu2, w.dgq1, w.dgq2, w.dgq3};   // dL/d(pre-activation) of each convT input
-    const float* pres[4] = {w.du2, w.dq1, w.dq2, w.dq3};
-    const float* posts[4] = {w.du2p, w.dq1p, w.dq2p, w.dq3p};
-    const float* gouts[4] = {w.dgq1, w.dgq2, w.dgq3, w.dg4};
-    for (int k = 3; k >= 0; --k) {
-      const int ih = IH >> (3 - k), iw = IW >> (3 - k);  // output (high-res) size of convT k
-      const int co = cout_t[k], co_st = (k == 3) ? 4 : co;
-      DR_TRY(op_conv_nhwc_ex(M1, co_st, ih, iw, cin_t[k], gouts[k], w.wrd[k], nullptr, gins[k], 0,
-                             const_cast<float*>(pres[k]), CONV_EPI_DSILU, s));
-      DR_TRY(op_conv_wgrad(M1, ih / 2, iw / 2, cin_t[k], co_st, posts[k], cin_t[k], 0, gouts[k], co_st, gd->convt[k].w,
-                           co, 1.0f, 0, w.cws, w.cws_n, s));
-      DR_TRY(op_chan_sum((long long)M1 * ih * iw, co, gouts[k], co_st, gd->convt[k].b, 0, w.cws, w.cws_n, s));
+    for (int k = N - 1; k >= 0; --k) {
+      const int ih = IH >> (N - 1 - k), iw = IW >> (N - 1 - k);  // output (high-res) size of convT k
+      const int co = cout_t[k], co_st = dec_cout_st(D, k);
+      float* gin = k ? w.dgq[k - 1] : w.dgu2;              // dL/d(pre-activation) of convT k's input
+      const float* pre = k ? w.dq[k - 1] : w.du2;
+      const float* post = k ? w.dqp[k - 1] : w.du2p;
+      const float* gout = k < N - 1 ? w.dgq[k] : w.dgout;  // dL/d(convT k's output pre-activation)
+      DR_TRY(op_conv_nhwc_ex(M1, co_st, ih, iw, cin_t[k], gout, w.wrd[k], nullptr, gin, 0, const_cast<float*>(pre),
+                             CONV_EPI_DSILU, s));
+      DR_TRY(op_conv_wgrad(M1, ih / 2, iw / 2, cin_t[k], co_st, post, cin_t[k], 0, gout, co_st, gd->convt[k].w, co, 1.0f,
+                           0, w.cws, w.cws_n, s));
+      DR_TRY(op_chan_sum((long long)M1 * ih * iw, co, gout, co_st, gd->convt[k].b, 0, w.cws, w.cws_n, s));
     }
   }
   // decoder.upscaler: .3 (permuted rows) then LN-SiLU(.1) and .0 into dL/d[h | z]
@@ -784,8 +796,8 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
         {D.dh, w.gyu, D.dh, nullptr, 0, gd->up1.b},
     };
     DR_TRY(op_colsum_multi(M1, cj, 4, s));
-    DR_TRY(perm_rows(D.C0, D.P16, D.dh, w.dw3p, gd->up3.w, 0, s));
-    DR_TRY(perm_rows(D.C0, D.P16, 1, w.db3p, gd->up3.b, 0, s));
+    DR_TRY(perm_rows(D.C0, D.Pf, D.dh, w.dw3p, gd->up3.w, 0, s));
+    DR_TRY(perm_rows(D.C0, D.Pf, 1, w.db3p, gd->up3.b, 0, s));
   }
   }  // bwd_heads
 
@@ -820,7 +832,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   {
     GemmArgs p[4];
     p[0] = bwd_w(L, eh, M, w.glog, L, w.x_m, eh, gw->map3.w);
-    p[1] = bwd_w(eh, F + Hd, M, w.gpre_m, eh, w.a4, F, gw->map0.w);
+    p[1] = bwd_w(eh, F + Hd, M, w.gpre_m, eh, w.a[N - 1], F, gw->map0.w);
     p[1].W2 = w.h_all; p[1].ldb2 = Hd; p[1].nsplitB = F;
     p[2] = bwd_w(3 * Hd, L + A, M1, w.ggi + (long long)B * 3 * Hd, 3 * Hd, w.z_all, L, gw->w_ih);
     p[2].W2 = w.act_tm; p[2].ldb2 = A; p[2].nsplitB = L;
@@ -838,40 +850,38 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
 
   if (bwd_enc) {
   // ---- backward through the encoder convolutions (all M frames) ----
-  DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M, F, eh, w.gpre_m, eh, w.w0tp, w.ga4, F, 0), s));
-  hipLaunchKernelGGL(k_mul_dsilu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, w.ga4,
-                     w.pre4);
+  float* gL = w.gp[N - 1];  // dL/d pre[N-1], NHWC (w0tp's rows are permuted to NHWC)
+  DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M, F, eh, w.gpre_m, eh, w.w0tp, gL, F, 0), s));
+  hipLaunchKernelGGL(k_mul_dsilu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, gL,
+                     w.pre[N - 1]);
   DR_TRY(dr_check_launch("mul_dsilu"));
   if (vec) {
-    // MLP stand-in backward: W2 / b2 grads from dL/d pre4, dL/d pre1 = (ga4 W2) SiLU'(pre1), W1 / b1 grads
+    // MLP stand-in backward: W2 / b2 grads from dL/d pre[N-1], dL/d pre[0] = (gL W2) SiLU'(pre[0]), W1 / b1 grads
     GemmArgs g = gemm_args();
-    g.M = M; g.N = F; g.K = F; g.A = w.ga4; g.lda = F; g.W = wm->conv[1].w; g.ldb = F; g.Y = w.gp1; g.ldy = F;
+    g.M = M; g.N = F; g.K = F; g.A = gL; g.lda = F; g.W = wm->conv[1].w; g.ldb = F; g.Y = w.gp[0]; g.ldy = F;
     DR_TRY(gemm_launch(G_NN, AM_PLAIN, &g, 1, s));
-    hipLaunchKernelGGL(k_mul_dsilu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, w.gp1,
-                       w.pre1);
+    hipLaunchKernelGGL(k_mul_dsilu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, w.gp[0],
+                       w.pre[0]);
     DR_TRY(dr_check_launch("mul_dsilu"));
     GemmArgs p[2];
-    p[0] = bwd_w(F, F, M, w.ga4, F, w.a1, F, gw->conv[1].w);
-    p[1] = bwd_w(F, Dv, M, w.gp1, F, w.x0, Dv, gw->conv[0].w);
+    p[0] = bwd_w(F, F, M, gL, F, w.a[0], F, gw->conv[1].w);
+    p[1] = bwd_w(F, Dv, M, w.gp[0], F, w.x0, Dv, gw->conv[0].w);
     splitk_all(p, 2, w.sk, w.sk_n);
     DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 2, s));
-    ColsumJob cj[2] = {{F, w.ga4, F, nullptr, 0, gw->conv[1].b}, {F, w.gp1, F, nullptr, 0, gw->conv[0].b}};
+    ColsumJob cj[2] = {{F, gL, F, nullptr, 0, gw->conv[1].b}, {F, w.gp[0], F, nullptr, 0, gw->conv[0].b}};
     DR_TRY(op_colsum_multi(M, cj, 2, s));
   } else {
-    float* go[4] = {w.gp1, w.gp2, w.gp3, w.ga4};           // dL/d pre-activation of conv k's output
-    const float* pr[3] = {w.pre1, w.pre2, w.pre3};
-    const float* hi[4] = {w.x0, w.a1, w.a2, w.a3};         // conv k's input
-    const float* wq[4] = {nullptr, w.wqe2, w.wqe3, w.wqe4};
-    const int cin[4] = {4, D.c1, D.c2, D.c3}, cout[4] = {D.c1, D.c2, D.c3, D.c4};
-    for (int k = 3; k >= 0; --k) {
+    for (int k = N - 1; k >= 0; --k) {
       const int oh = IH >> (k + 1), ow = IW >> (k + 1);
-      DR_TRY(op_conv_wgrad(M, oh, ow, cout[k], cin[k], go[k], cout[k], 0, hi[k], cin[k], gw->conv[k].w,
-                           k == 0 ? 3 : cin[k], 1.0f, 0, w.cws, w.cws_n, s));
-      DR_TRY(op_chan_sum((long long)M * oh * ow, cout[k], go[k], cout[k], gw->conv[k].b, 0, w.cws, w.cws_n, s));
+      const int cin = enc_cin_st(D, k), cout = D.e[k + 1];
+      const float* hi = k ? w.a[k - 1] : w.x0;  // conv k's input
+      DR_TRY(op_conv_wgrad(M, oh, ow, cout, cin, w.gp[k], cout, 0, hi, cin, gw->conv[k].w, D.e[k], 1.0f, 0, w.cws,
+                           w.cws_n, s));
+      DR_TRY(op_chan_sum((long long)M * oh * ow, cout, w.gp[k], cout, gw->conv[k].b, 0, w.cws, w.cws_n, s));
       if (k > 0) {
         ConvTArgs a = {};
-        a.n = M; a.cin = cout[k]; a.h = oh; a.w = ow; a.cout = cin[k];
-        a.in = go[k]; a.wq = wq[k]; a.out = go[k - 1]; a.ldc = cin[k]; a.pre = pr[k - 1];
+        a.n = M; a.cin = cout; a.h = oh; a.w = ow; a.cout = cin;
+        a.in = w.gp[k]; a.wq = w.wqe[k]; a.out = w.gp[k - 1]; a.ldc = cin; a.pre = w.pre[k - 1];
         DR_TRY(op_convT_nhwc(CT_EPI_DSILU, a, s));
       }
     }
@@ -909,19 +919,22 @@ extern "C" int dr_wm_train_grads(const dr_dims* d, const dr_world_model* wm, con
 // a20  Decoder.forward (VariationalAutoEncoder.py:139-161), inference
 // ===========================================================================
 struct DecWs {
-  float *u1, *u2, *q[3], *w3p, *b3p, *wq[4];
+  float *u1, *u2, *q[DR_MAX_DEPTH], *w3p, *b3p, *wq[DR_MAX_DEPTH];
 };
 static void dec_carve(Carve& c, const dr_dims* d, int M, DecWs& w) {
+  memset(&w, 0, sizeof(w));
   const WmDims D = wm_dims(d, 1, 2);
-  const int cin_t[4] = {D.C0, 2 * D.d2, D.d2, D.d1}, cout_t[4] = {2 * D.d2, D.d2, D.d1, 3};
+  const int N = D.N;
   w.u1 = c.f((long long)M * D.dh);
   w.u2 = c.f((long long)M * D.Fd);
-  w.q[0] = c.f(D.Dv ? (long long)M * D.Fd : (long long)M * D.p3 * cout_t[0]);
-  w.q[1] = c.f((long long)M * D.p2 * cout_t[1]);
-  w.q[2] = c.f((long long)M * D.p1 * cout_t[2]);
+  if (D.Dv) {
+    w.q[0] = c.f((long long)M * D.Fd);
+  } else {
+    for (int k = 0; k + 1 < N; ++k) w.q[k] = c.f((long long)M * D.pix[N - k - 1] * D.cd[k + 1]);
+  }
   w.w3p = c.f((long long)D.Fd * D.dh);
   w.b3p = c.f(D.Fd);
-  for (int k = 0; k < 4; ++k) w.wq[k] = c.f((long long)16 * cin_t[k] * cout_t[k]);
+  for (int k = 0; k < N; ++k) w.wq[k] = c.f((long long)16 * D.cd[k] * D.cd[k + 1]);
 }
 
 extern "C" size_t dr_decoder_workspace_bytes(const dr_dims* d, int M) {
@@ -935,15 +948,18 @@ extern "C" size_t dr_decoder_workspace_bytes(const dr_dims* d, int M) {
 extern "C" int dr_decoder_fwd(const dr_dims* d, const dr_decoder* dec, int M, const float* h, long long ldh,
                               const float* z, long long ldz, float* mu, void* ws, size_t ws_bytes, hipStream_t s) {
   DR_REQUIRE(d && dec && h && z && mu && M > 0, "null argument or empty batch");
-  DR_REQUIRE(d->obs_dim > 0 || (d->img_h % 16 == 0 && d->img_w % 16 == 0), "image size must be a multiple of 16");
+  DR_REQUIRE(vae_depth_ok(d), "enc_depth must be 0, 4 or 5");
+  DR_REQUIRE(d->obs_dim > 0 || (d->img_h % (1 << vae_depth(d)) == 0 && d->img_w % (1 << vae_depth(d)) == 0),
+             "image size must be a multiple of 2^depth (16, or 32 for the 5-layer VAE)");
   DR_REQUIRE(d->dec_f1 % 8 == 0 && d->dec_f2 % 8 == 0, "decoder filter counts must be multiples of 8");
   Carve c(ws);
   DecWs w;
   dec_carve(c, d, M, w);
   WS_CHECK(c, ws_bytes);
   const WmDims D = wm_dims(d, 1, 2);
-  const int cin_t[4] = {D.C0, 2 * D.d2, D.d2, D.d1}, cout_t[4] = {2 * D.d2, D.d2, D.d1, 3};
-  const int Hd = D.Hd, L = D.L;
+  const int* cin_t = D.cd;
+  const int* cout_t = D.cd + 1;
+  const int Hd = D.Hd, L = D.L, N = D.N;
   if (D.Dv) {  // vector observations: upscaler, then the image_builder MLP stand-in -> mu [M][D]
     DR_TRY(run(G_NT, AM_PLAIN, lin2(M, D.dh, h, ldh, Hd, z, ldz, L, dec->up0.w, dec->up0.b, w.u1, D.dh), s));
     GemmArgs g = lin_ln(M, D.Fd, D.dh, w.u1, D.dh, dec->up1, dec->up3.w, dec->up3.b, w.u2, D.Fd);
@@ -954,10 +970,10 @@ extern "C" int dr_decoder_fwd(const dr_dims* d, const dr_decoder* dec, int M, co
     DR_TRY(run(G_NT, AM_PLAIN, g1, s));
     return run(G_NT, AM_PLAIN, lin(M, D.Dv, D.Fd, w.q[0], D.Fd, dec->convt[1].w, D.Fd, dec->convt[1].b, mu, D.Dv), s);
   }
-  DR_TRY(perm_rows(D.C0, D.P16, D.dh, dec->up3.w, w.w3p, 1, s));
-  DR_TRY(perm_rows(D.C0, D.P16, 1, dec->up3.b, w.b3p, 1, s));
-  for (int k = 0; k < 3; ++k) DR_TRY(op_convT_repack(cin_t[k], cout_t[k], dec->convt[k].w, w.wq[k], s));
-  DR_TRY(op_convT_out3_repack(cin_t[3], dec->convt[3].w, w.wq[3], s));
+  DR_TRY(perm_rows(D.C0, D.Pf, D.dh, dec->up3.w, w.w3p, 1, s));
+  DR_TRY(perm_rows(D.C0, D.Pf, 1, dec->up3.b, w.b3p, 1, s));
+  for (int k = 0; k + 1 < N; ++k) DR_TRY(op_convT_repack(cin_t[k], cout_t[k], dec->convt[k].w, w.wq[k], s));
+  DR_TRY(op_convT_out3_repack(cin_t[N - 1], dec->convt[N - 1].w, w.wq[N - 1], s));
   // upscaler: cat(h, flatten z) -> Linear -> LN -> SiLU -> Linear (rows permuted to NHWC); its SiLU runs in convT1's loader
   DR_TRY(run(G_NT, AM_PLAIN, lin2(M, D.dh, h, ldh, Hd, z, ldz, L, dec->up0.w, dec->up0.b, w.u1, D.dh), s));
   {
@@ -965,12 +981,11 @@ extern "C" int dr_decoder_fwd(const dr_dims* d, const dr_decoder* dec, int M, co
     g.act = 1;  // upscaler.4 SiLU
     DR_TRY(run(G_NT, AM_LNSILU, g, s));
   }
-  const float* ins[4] = {w.u2, w.q[0], w.q[1], w.q[2]};
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < N; ++k) {
     ConvTArgs a = {};
-    a.n = M; a.cin = cin_t[k]; a.h = D.IH >> (4 - k); a.w = D.IW >> (4 - k); a.cout = cout_t[k];
-    a.in = ins[k]; a.silu_in = 0; a.wq = w.wq[k]; a.bias = dec->convt[k].b;
-    if (k < 3) {
+    a.n = M; a.cin = cin_t[k]; a.h = D.IH >> (N - k); a.w = D.IW >> (N - k); a.cout = cout_t[k];
+    a.in = k ? w.q[k - 1] : w.u2; a.silu_in = 0; a.wq = w.wq[k]; a.bias = dec->convt[k].b;
+    if (k < N - 1) {
       a.out = w.q[k]; a.silu_out = 1; a.ldc = cout_t[k];
       DR_TRY(op_convT_nhwc(CT_EPI_BIAS, a, s));
     } else {

@@ -77,7 +77,7 @@ class Dreamer(nn.Module):
             c["decoder_filter_num_2"], c["decoder_hidden_layer_nodes"], c["dyn_pred_hidden_num_nodes_1"],
             c["dyn_pred_hidden_num_nodes_2"], c["rew_pred_hidden_num_nodes_1"], c["rew_pred_hidden_num_nodes_2"],
             c["critic_reward_buckets"], c["cont_pred_hidden_num_nodes_1"], c["cont_pred_hidden_num_nodes_2"],
-            device=device)
+            device=device, encoder_depth=int(c.get("encoder_depth", 4)))
         self.agent = Agent(
             c["action_dims"], tuple(c["latent_state_dims"]), c["hidden_state_dims"], c["hidden_layer_actor_1_size"],
             c["hidden_layer_actor_2_size"], c["hidden_layer_critic_1_size"], c["hidden_layer_critic_2_size"],
@@ -333,9 +333,10 @@ class Dreamer(nn.Module):
                    L.ptr(z2), L.ptr(h2), L.ptr(a2), L.ptr(mu), L.ptr(sg), None, L.ptr(st["status"]),
                    L.ptr(st["ws"]), st["ws"].numel(), hip.stream())
         except RuntimeError as e:
-            if "co-resident" not in str(e):
+            if "co-resident" not in str(e) and "outside the batch-1 acting kernel" not in str(e):
                 raise
-            # the device cannot hold the one-launch grid: the unfused launches from now on
+            # the device cannot hold the one-launch grid, or the widths are not the ones the
+            # kernel's register batches are sized for (e.g. the 5-layer VAE): the unfused launches
             self._act_unfused = True
             return self._act_step_unfused(observation, z, h, a, deterministic)
         # the status word travels back with the step (4 bytes behind the kernel);

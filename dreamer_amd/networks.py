@@ -177,14 +177,24 @@ class ContinuePredictor(nn.Module):
         return prob
 
 
+def vae_channels(depth, f1, f2):
+    """Encoder channels 3, f1, f2, 2 f2, 4 f2 (VariationalAutoEncoder.py:33-42); depth 5 (BASELINE
+    configs[3]'s "deeper VAE", config key encoder_depth) adds one 4 f2 -> 4 f2 stride-2 layer
+    (include/dreamer_hip.h dr_dims.enc_depth)."""
+    if depth not in (4, 5):
+        raise ValueError(f"encoder_depth must be 4 (the reference) or 5 (the deeper VAE), got {depth}")
+    return [3, f1, f2, 2 * f2, 4 * f2] + ([4 * f2] if depth == 5 else [])
+
+
 class Encoder(nn.Module):
     """4x [Conv2d(k4,s2,p1)+SiLU] -> flatten -> cat(features, h) -> Linear-LN-SiLU
     -> Linear -> (R,C) logits; unimix categorical sample + STE
-    (VariationalAutoEncoder.py:4-99)."""
+    (VariationalAutoEncoder.py:4-99).  depth=5: one more stride-2 conv (configs[3])."""
 
     def __init__(self, observation_dims, hidden_state_dim, latent_num_rows, latent_num_columns, num_filters_1,
-                 num_filters_2, hidden_layer_nodes, device="cpu"):
+                 num_filters_2, hidden_layer_nodes, device="cpu", depth=4):
         super().__init__()
+        self.depth = int(depth)
         self.latent_size = latent_num_rows * latent_num_columns
         self.latent_num_rows, self.latent_num_columns = latent_num_rows, latent_num_columns
         self.observation_dims = tuple(observation_dims)
@@ -202,11 +212,11 @@ class Encoder(nn.Module):
                                                    nn.Linear(F, F, device=device), nn.SiLU())
             n_feat = F
         else:
-            self.final_height = observation_dims[0] // 16
-            self.final_width = observation_dims[1] // 16
+            chans = vae_channels(self.depth, num_filters_1, num_filters_2)
+            self.final_height = observation_dims[0] // 2 ** self.depth
+            self.final_width = observation_dims[1] // 2 ** self.depth
             if self.final_height < 1 or self.final_width < 1:
-                raise ValueError(f"Input image {observation_dims} is too small for 4 layers of downsampling.")
-            chans = [3, num_filters_1, num_filters_2, 2 * num_filters_2, 4 * num_filters_2]
+                raise ValueError(f"Input image {observation_dims} is too small for {self.depth} layers of downsampling.")
             layers = []
             for cin, cout in zip(chans[:-1], chans[1:]):
                 layers += [nn.Conv2d(cin, cout, kernel_size=4, stride=2, padding=1, device=device), nn.SiLU()]
@@ -230,14 +240,15 @@ class Encoder(nn.Module):
             d.obs_dim = 0
             d.enc_f1 = self.feature_extractor[0].out_channels
             d.enc_f2 = self.feature_extractor[2].out_channels
+            d.enc_depth = self.depth
         d.enc_hidden = self.latent_mapper[0].out_features
         d.hidden = self.hidden_state_dim
         d.rows, d.cols = self.latent_num_rows, self.latent_num_columns
 
     def fill(self, wm):
         fe = self.feature_extractor
-        for i, j in enumerate((0, 2, 4, 6)[:len(fe) // 2]):
-            wm.conv[i] = hip.linear(fe[j])
+        for i in range(len(fe) // 2):
+            wm.conv[i] = hip.linear(fe[2 * i])
         wm.map0, wm.map1, wm.map3 = (hip.linear(self.latent_mapper[j]) for j in (0, 1, 3))
 
     def forward(self, hidden, observation):
@@ -297,15 +308,16 @@ class Decoder(nn.Module):
     inside dr_wm_train_grads.  Autograd callers get the nn.Module forward."""
 
     def __init__(self, latent_num_rows, latent_num_columns, observation_dim, hidden_state_dim, num_filters_1,
-                 num_filters_2, hidden_layer_nodes, device="cpu"):
+                 num_filters_2, hidden_layer_nodes, device="cpu", depth=4):
         super().__init__()
         # observation_dim = [D]: vector observations (Encoder's note); the
         # image_builder stand-in is Linear(4 f2, 4 f2)-SiLU-Linear(4 f2, D), no Tanh
         self.vector = len(observation_dim) == 1
         self.observation_dim = tuple(observation_dim)
         self.num_filters_1, self.num_filters_2 = num_filters_1, num_filters_2
-        self.start_height = 1 if self.vector else observation_dim[0] // 16
-        self.start_width = 1 if self.vector else observation_dim[1] // 16
+        self.depth = int(depth)
+        self.start_height = 1 if self.vector else observation_dim[0] // 2 ** self.depth
+        self.start_width = 1 if self.vector else observation_dim[1] // 2 ** self.depth
         self.num_filters_start = num_filters_2 * 4
         self.hidden_dim = hidden_state_dim
         self.latent_row_dim, self.latent_col_dim = latent_num_rows, latent_num_columns
@@ -319,11 +331,13 @@ class Decoder(nn.Module):
             self.image_builder = nn.Sequential(nn.Linear(n_start, n_start, device=device), nn.SiLU(),
                                                nn.Linear(n_start, observation_dim[0], device=device))
             return
-        chans = [self.num_filters_start, 2 * num_filters_2, num_filters_2, num_filters_1, 3]
+        # the encoder's channels mirrored (VAE.py:128-137; depth 5: the deeper VAE's extra 4 f2 -> 4 f2 layer)
+        chans = [c for c in reversed(vae_channels(self.depth, num_filters_1, num_filters_2))]
+        chans[0] = self.num_filters_start
         layers = []
         for i, (cin, cout) in enumerate(zip(chans[:-1], chans[1:])):
             layers.append(nn.ConvTranspose2d(cin, cout, kernel_size=4, stride=2, padding=1, device=device))
-            layers.append(nn.Tanh() if i == 3 else nn.SiLU())
+            layers.append(nn.Tanh() if i == self.depth - 1 else nn.SiLU())
         self.image_builder = nn.Sequential(*layers)
 
     def fill_dims(self, d):
@@ -334,13 +348,14 @@ class Decoder(nn.Module):
             d.img_h = d.img_w = 0
         else:
             d.obs_dim = 0
-            d.img_h, d.img_w = 16 * self.start_height, 16 * self.start_width
+            d.enc_depth = self.depth
+            d.img_h, d.img_w = 2 ** self.depth * self.start_height, 2 ** self.depth * self.start_width
 
     def packed(self):
         ib = self.image_builder
         dec = L.dr_decoder(hip.linear(self.upscaler[0]), hip.linear(self.upscaler[1]), hip.linear(self.upscaler[3]))
-        for i, j in enumerate((0, 2, 4, 6)[:(len(ib) + 1) // 2]):
-            dec.convt[i] = hip.linear(ib[j])
+        for i in range((len(ib) + 1) // 2):
+            dec.convt[i] = hip.linear(ib[2 * i])
         return dec
 
     def forward(self, hidden, latent):

@@ -19,7 +19,7 @@ class WorldModel(nn.Module):
                  encoder_hidden_layer_nodes, num_decoder_filters_1, num_decoder_filters_2, decoder_hidden_layer_nodes,
                  dyn_pred_hidden_num_nodes_1, dyn_pred_hidden_num_nodes_2, rew_pred_hidden_num_nodes_1,
                  rew_pred_hidden_num_nodes_2, reward_buckets, cont_pred_hidden_num_nodes_1,
-                 cont_pred_hidden_num_nodes_2, device="cpu"):
+                 cont_pred_hidden_num_nodes_2, device="cpu", encoder_depth=4):
         super().__init__()
         self.latent_num_rows, self.latent_num_columns = latent_dims
         self.hidden_dims = hidden_dims
@@ -33,7 +33,7 @@ class WorldModel(nn.Module):
         self.batch_size = batch_size
         R, C = latent_dims
         self.encoder = Encoder(observation_dims, hidden_dims, R, C, num_encoder_filters_1, num_encoder_filters_2,
-                               encoder_hidden_layer_nodes, device=device)
+                               encoder_hidden_layer_nodes, device=device, depth=encoder_depth)
         self.sequence_model = SequenceModel(R, C, hidden_dims, action_dims, num_layers=1, device=device)
         self.dynamics_predictor = DynamicsPredictor(R, C, hidden_dims, dyn_pred_hidden_num_nodes_1,
                                                     dyn_pred_hidden_num_nodes_2, device)
@@ -42,7 +42,7 @@ class WorldModel(nn.Module):
         self.continue_predictor = ContinuePredictor(R, C, hidden_dims, cont_pred_hidden_num_nodes_1,
                                                     cont_pred_hidden_num_nodes_2, device=device)
         self.decoder = Decoder(R, C, observation_dims, hidden_dims, num_decoder_filters_1, num_decoder_filters_2,
-                               decoder_hidden_layer_nodes, device=device)
+                               decoder_hidden_layer_nodes, device=device, depth=encoder_depth)
         self.device = torch.device(device)
         self.optimiser = torch.optim.AdamW(self.parameters(), lr=WM_lr, betas=(WM_betas[0], WM_betas[1]), eps=WM_eps,
                                            weight_decay=1e-6)
@@ -87,8 +87,8 @@ class WorldModel(nn.Module):
     def _grad_structs(self):
         """C structs pointing at the parameters' .grad views (one flat buffer)."""
         e, g = self.encoder, L.dr_world_model()
-        for i, j in enumerate((0, 2, 4, 6)[:len(e.feature_extractor) // 2]):
-            g.conv[i] = hip.linear_grad(e.feature_extractor[j])
+        for i in range(len(e.feature_extractor) // 2):
+            g.conv[i] = hip.linear_grad(e.feature_extractor[2 * i])
         g.map0, g.map1, g.map3 = (hip.linear_grad(e.latent_mapper[j]) for j in (0, 1, 3))
         gru = self.sequence_model.GRU
         g.w_ih, g.w_hh, g.b_ih, g.b_hh = (L.ptr(t.grad) for t in (gru.weight_ih, gru.weight_hh, gru.bias_ih,
@@ -98,8 +98,8 @@ class WorldModel(nn.Module):
         g.cont = hip.mlp3_grad(self.continue_predictor.logit_generator)
         up, ib = self.decoder.upscaler, self.decoder.image_builder
         gd = L.dr_decoder(hip.linear_grad(up[0]), hip.linear_grad(up[1]), hip.linear_grad(up[3]))
-        for i, j in enumerate((0, 2, 4, 6)[:(len(ib) + 1) // 2]):
-            gd.convt[i] = hip.linear_grad(ib[j])
+        for i in range((len(ib) + 1) // 2):
+            gd.convt[i] = hip.linear_grad(ib[2 * i])
         return g, gd
 
     def _grad_buckets(self, f):

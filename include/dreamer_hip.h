@@ -68,13 +68,20 @@ typedef struct {
                           Linear(4*enc_f2, 4*enc_f2), each + SiLU (F = 4*enc_f2 features, conv[2..3]
                           unused); decoder upscaler.3 -> 4*dec_f2, convt[0] = Linear(4*dec_f2, 4*dec_f2)
                           + SiLU, convt[1] = Linear(4*dec_f2, D) (no Tanh; convt[2..3] unused). */
+  int enc_depth;       /* k4 s2 p1 convolutions of the encoder (and transposed convolutions of the decoder):
+                          0 or 4 = the reference's VAE (VAE.py:33-42, 128-137); 5 = the "deeper VAE" of BASELINE
+                          configs[3] (the extra config key encoder_depth; no reference definition -- one more
+                          stride-2 layer each way, so 128x128 frames reach the same 4x4 grid 64x64 frames reach
+                          in the reference): encoder channels 3, f1, f2, 2 f2, 4 f2, 4 f2 (conv[0..4]); decoder
+                          4 d2 (H/32 x W/32) -> 4 d2 -> 2 d2 -> d2 -> d1 -> 3 (convt[0..4]). */
 } dr_dims;
+#define DR_MAX_DEPTH 5
 #define DR_PREC_FP32 0
 #define DR_PREC_BF16 1
 
 /* WorldModel parameters (WorldModel.py:55-60). */
 typedef struct {
-  dr_linear conv[4];              /* encoder.feature_extractor.{0,2,4,6} */
+  dr_linear conv[DR_MAX_DEPTH];   /* encoder.feature_extractor.{0,2,4,6(,8)} (dr_dims.enc_depth layers) */
   dr_linear map0, map1, map3;     /* encoder.latent_mapper.{0, 1 (LN), 3} */
   float *w_ih, *w_hh, *b_ih, *b_hh; /* sequence_model.GRU */
   dr_mlp3 prior;                  /* dynamics_predictor.logit_net */
@@ -86,7 +93,7 @@ typedef struct {
 /* Decoder parameters (VariationalAutoEncoder.py:118-137). */
 typedef struct {
   dr_linear up0, up1, up3;        /* decoder.upscaler.{0, 1 (LN), 3} */
-  dr_linear convt[4];             /* decoder.image_builder.{0,2,4,6}: ConvTranspose2d w [in][out][4][4] */
+  dr_linear convt[DR_MAX_DEPTH];  /* decoder.image_builder.{0,2,4,6(,8)}: ConvTranspose2d w [in][out][4][4] */
 } dr_decoder;
 
 /* Actor (Agent.py:174-200): base_net.{0,1,3,4}, mu_head, log_sig_head. */

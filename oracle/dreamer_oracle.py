@@ -132,9 +132,14 @@ def encoder_logits(h, obs, P):
         return _lin(y, P, WM + "encoder.latent_mapper.3")
     B, S, C, Hh, Ww = obs.shape
     x = obs.reshape(B * S, C, Hh, Ww)
-    for i in (0, 2, 4, 6):
+    # 4 convs (VAE.py:33-42), or 5 for BASELINE configs[3]'s "deeper VAE" (the framework's
+    # encoder_depth key: one more k4 s2 p1 conv + SiLU; no reference definition -- parity of
+    # that depth is pinned only against this restatement)
+    i = 0
+    while WM + f"encoder.feature_extractor.{i}.weight" in P:
         x = F.silu(F.conv2d(x, P[WM + f"encoder.feature_extractor.{i}.weight"],
                             P[WM + f"encoder.feature_extractor.{i}.bias"], stride=2, padding=1))
+        i += 2
     feat = x.reshape(B, S, -1)
     inp = torch.cat((feat, h), dim=-1)
     y = F.silu(_ln(_lin(inp, P, WM + "encoder.latent_mapper.0"), P, WM + "encoder.latent_mapper.1"))
@@ -379,7 +384,8 @@ def replay_starts(size, capacity, next_idx, seq_len, batch, rng=None):
 def decoder_forward(h, z, P, img_hw):
     """Decoder.forward (VariationalAutoEncoder.py:139-161): cat(h, flatten z) ->
     Linear-LN-SiLU-Linear-SiLU -> view (C0, H/16, W/16) -> 4x ConvTranspose2d
-    (k4 s2 p1) with SiLU between and Tanh at the end."""
+    (k4 s2 p1) with SiLU between and Tanh at the end (the deeper VAE of
+    configs[3]: H/32, 5 transposed convs -- encoder_logits' note)."""
     B, S, Hd = h.shape
     x = torch.cat((h.reshape(B * S, Hd), z.reshape(B * S, -1)), dim=-1)
     D = WM + "decoder."
@@ -389,11 +395,13 @@ def decoder_forward(h, z, P, img_hw):
         x = F.silu(_lin(x, P, D + "image_builder.0"))
         return _lin(x, P, D + "image_builder.2").view(B, S, -1)
     c0 = P[D + "image_builder.0.weight"].shape[0]
-    x = x.view(-1, c0, img_hw[0] // 16, img_hw[1] // 16)
-    for j, i in enumerate((0, 2, 4, 6)):
+    depth = sum(1 for k in P if k.startswith(D + "image_builder.") and k.endswith(".weight"))  # 4, or 5 (configs[3])
+    x = x.view(-1, c0, img_hw[0] // 2 ** depth, img_hw[1] // 2 ** depth)
+    for j in range(depth):
+        i = 2 * j
         x = F.conv_transpose2d(x, P[D + f"image_builder.{i}.weight"], P[D + f"image_builder.{i}.bias"],
                                stride=2, padding=1)
-        x = torch.tanh(x) if j == 3 else F.silu(x)
+        x = torch.tanh(x) if j == depth - 1 else F.silu(x)
     _, C, Hh, Ww = x.shape
     return x.view(B, S, C, Hh, Ww)
 
