@@ -109,8 +109,11 @@ def test_train_agent_bf16_epoch_vs_oracle(B, gpu):
         normwise relative error <= 1e-2;
       critic loss: relative 1e-2; actor loss: |d| <= 1e-2 max(|ref|, 0.1);
       S: relative 1e-3;
-      clipped actor and critic gradients: normwise relative 5e-2 per buffer.
-    The measured values are printed."""
+      clipped actor and critic gradients: normwise relative 2e-2 per buffer.
+    The measured values are printed (first GPU run: B = 256 h0 5.0e-4, R 2.2e-3,
+    actor / critic gradients 2.9e-3 / 1.3e-3, no flips on 11,159 guarded of
+    385,024 draws; B = 64 is fp32 past the encoder, so only the sampled indices
+    could differ)."""
     import bench
     from baseline_case import TieGuard, oracle_epoch
     from test_gpu_baseline import CAR, run_gpu_epoch
@@ -164,7 +167,7 @@ def test_train_agent_bf16_epoch_vs_oracle(B, gpu):
     assert abs(pre["lc"] - lc_ref) <= 1e-2 * abs(lc_ref), m["loss_critic"]
     assert abs(pre["la"] - la_ref) <= 1e-2 * max(abs(la_ref), 0.1), m["loss_actor"]
     assert abs(pre["S"] - float(ref["ts"]["S"])) <= 1e-3 * abs(float(ref["ts"]["S"])), m["S"]
-    assert m["grad_actor"] <= 5e-2 and m["grad_critic"] <= 5e-2, m
+    assert m["grad_actor"] <= 2e-2 and m["grad_critic"] <= 2e-2, m
 
 
 @pytest.mark.parametrize("res", [64, 128])

@@ -125,7 +125,7 @@ def test_deep_wm_step_matches_oracle(gpu):
     assert n_flip == 0, f"{n_flip} posterior one-hot flips"
     ls = cpu(wm.last_losses)
     for i, k in ((0, "total"), (1, "loss_pred"), (2, "kl_dyn"), (3, "kl_rep")):
-        r = float(ref[k])
+        r = float(ref[k].detach())
         assert abs(float(ls[i]) - r) <= 1e-4 * max(1.0, abs(r)), (k, float(ls[i]), r)
     assert any(n == "encoder.feature_extractor.8.weight" for n in names)
     assert any(n == "decoder.image_builder.8.weight" for n in names)

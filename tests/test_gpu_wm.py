@@ -14,10 +14,11 @@ the AdamW step: against AdamW (the oracle's torch-order restatement) applied to
 the GPU's OWN clipped gradients at |d| <= 1e-7 + 1e-6 |p| (pins the fused
 optimiser), and against the reference's / oracle's post-step parameters at
 |d| <= 1e-6 + 1e-6 |p| on every element whose gradient is determined to
-better than its tolerance (|g_ref| > 4 x the gradient atol): there Adam's first
-step cannot change sign.  Elements below that are Adam's sign(g) * lr
-ambiguity (a near-zero gradient of either sign moves the weight by ~lr); they
-are counted and reported, not banded."""
+to 1 % by the two sides (|g_ref| > 100 |g_gpu - g_ref|): there Adam's first
+step, lr g / (|g| + eps), differs by at most lr / 400.  The rest are Adam's
+sign(g) * lr ambiguity (a gradient whose summation-order error rivals its size
+moves the weight by ~lr either way); they are counted and reported, not
+banded -- the AdamW-on-own-gradients check above covers every element."""
 import numpy as np
 import pytest
 import torch
@@ -100,10 +101,11 @@ def check_grads_and_params(named, keys, P0, g_ref_of, post_ref_of, sub, label, l
         pn, _, _ = O.adamw_step(p0, g_gpu, torch.zeros_like(p0), torch.zeros_like(p0), 1, lr)
         got = cpu(p)
         close(got, pn, 1e-6, 1e-7, f"{label} AdamW(step 1) on the GPU's grads {k}")
-        # the reference's post-step parameters, away from Adam's sign ambiguity
+        # the reference's post-step parameters, away from Adam's sign ambiguity: where the two
+        # gradients agree to 1 % the first Adam step, lr g / (|g| + eps), differs by <= lr / 400
         want = post_ref_of(k).reshape(-1)
         gs = g_ref.reshape(-1)
-        live = gs.abs() > 4 * atol
+        live = gs.abs() > 100 * (sub(g_gpu).reshape(-1) - gs).abs()
         n_amb += int((~live).sum())
         err = (sub(got).reshape(-1) - want).abs()
         bad = live & (err > 1e-6 + 1e-6 * want.abs())
