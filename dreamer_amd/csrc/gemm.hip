@@ -976,6 +976,173 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, int m, int n, 
 }
 
 // ---------------------------------------------------------------------------
+// The categorical-sampler head as its own kernel: logits = SiLU(LN(x)) W^T + b
+// (K <= 256), then per group of C = 32 classes softmax, 1 % unimix,
+// argmax(p_hat / Exp(1)) and the straight-through one-hot (VAE.py:77-99 on
+// latent_mapper.3; DynamicsPredictors.py:31-40 on logit_net.6).  It runs once
+// per warm-start / imagination step, 46 times per epoch, and the general
+// skinny kernel spent 15.3 us on it at 256 rows (8 waves splitting a K of only
+// 200, an 8-way LDS reduction, 512 workgroups in two dispatch rounds).  Here a
+// workgroup of 4 waves owns 16 rows x 64 columns (two groups): the 16 rows and
+// 64 weight rows are read once into LDS with every load issued before the
+// first wait, the LayerNorm-SiLU runs on the way (a wave per row, DPP
+// statistics), wave w then accumulates output columns 16w..16w+15 over the
+// whole K (two accumulators alternating per 16-k chunk: consecutive MFMAs are
+// independent), and the logits pass through LDS to the sampler, two (row,
+// group) pairs per wave instruction.  256 rows = 256 workgroups, one round.
+// ---------------------------------------------------------------------------
+#define LS_MT 16
+#define LS_NT 64
+#define LS_KMAX 256
+static size_t ln_sample_lds_bytes(int K) {
+  const int KP = ((K + 15) & ~15) + 8;  // 8 mod 16 dwords: conflict-free ds_read_b128 fragments
+  return sizeof(float) * ((size_t)(LS_MT + LS_NT) * KP + (size_t)LS_MT * (LS_NT + 1));
+}
+
+__global__ __launch_bounds__(256) void k_ln_gemm_sample(GemmArgs ga) {
+  __shared__ GemmArgs g;
+  dr_stage_args(ga, g, threadIdx.x);
+  const int M = dr_uni(g.M), N = dr_uni(g.N), K = dr_uni(g.K);
+  const int tiles_m = (M + LS_MT - 1) / LS_MT, tiles_n = N / LS_NT;
+  // row tiles reading one weight slice are adjacent (one XCD's L2)
+  const int lt = dr_xcd_tile(blockIdx.x, tiles_m * tiles_n);
+  if (lt < 0) return;
+  const int tn = lt / tiles_m, tm = lt - tn * tiles_m;
+  const int m0 = tm * LS_MT, n0 = tn * LS_NT;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
+  const int K4 = K >> 2, K16 = (K + 15) & ~15, KP = K16 + 8;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sA = smem;                  // [LS_MT][KP]   SiLU(LN(x)) rows
+  float* sB = smem + LS_MT * KP;     // [LS_NT][KP]   weight rows
+  float* sO = sB + LS_NT * KP;       // [LS_MT][LS_NT + 1] logits
+  const float* A = dr_uni(g.A);
+  const float* W = dr_uni(g.W);
+  const int lda = dr_uni((int)g.lda), ldb = dr_uni((int)g.ldb);
+  // Philox state of the sampler, fetched now (not after the K loop)
+  unsigned long long rng_seed = 0, rng_off = 0;
+  if (!g.noise.q && g.noise.rng) {
+    rng_seed = g.noise.rng[0];
+    rng_off = g.noise.rng[1];
+  }
+  // every global load of the tile, issued together: 4 LayerNorm rows, 16
+  // weight rows, gamma / beta (one float4 per lane each: K <= 256) and the
+  // bias of the column this lane finalises
+  const bool okk = lane < K4;
+  const unsigned ek = okk ? (unsigned)(4 * lane) : 0u;
+  float4 xa[4], xb[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wave + 4 * i;
+    const bool ok = okk && m < M;
+    xa[i] = dr_ld4(A, ok ? (unsigned)m * (unsigned)lda + 4u * lane : 0u);
+    if (!ok) xa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int n = n0 + 16 * wave + j;
+    xb[j] = dr_ld4(W, okk ? (unsigned)n * (unsigned)ldb + 4u * lane : 0u);
+    if (!okk) xb[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const float4 gv = dr_ld4(dr_uni(g.ln_g), ek), bv = dr_ld4(dr_uni(g.ln_b), ek);
+  const float* bias = dr_uni(g.bias);
+  const int ncol = n0 + 16 * wave + r;
+  const float bcol = bias ? dr_ld1(bias, (unsigned)ncol) : 0.f;
+  float* a_out = dr_uni(g.a_out);
+  const int ld_aout = dr_uni((int)g.ld_aout);
+  const bool store_a = a_out != nullptr && tn == 0;
+  // LayerNorm (eps 1e-5) + SiLU of this wave's 4 rows, as the skinny kernel's prologue
+  const bool in16 = lane < (K16 >> 2);  // lanes that write the zero-padded K16 row
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ml = wave + 4 * i, m = m0 + ml;
+    float4 x = xa[i];
+    const float mean = wave_sum(okk ? (x.x + x.y) + (x.z + x.w) : 0.f) / (float)K;
+    float sq = 0.f;
+    if (okk) {
+      const float dx = x.x - mean, dy = x.y - mean, dz = x.z - mean, dw = x.w - mean;
+      sq = (dx * dx + dy * dy) + (dz * dz + dw * dw);
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)K + 1e-5f);
+    float4 y;
+    y.x = dr_silu_fast((x.x - mean) * rstd * gv.x + bv.x);
+    y.y = dr_silu_fast((x.y - mean) * rstd * gv.y + bv.y);
+    y.z = dr_silu_fast((x.z - mean) * rstd * gv.z + bv.z);
+    y.w = dr_silu_fast((x.w - mean) * rstd * gv.w + bv.w);
+    if (!okk || m >= M) y = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (in16) *reinterpret_cast<float4*>(&sA[ml * KP + 4 * lane]) = y;
+    if (store_a && okk && m < M) dr_st4(a_out, (unsigned)m * (unsigned)ld_aout + 4u * lane, y);
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    if (in16) *reinterpret_cast<float4*>(&sB[(16 * wave + j) * KP + 4 * lane]) = xb[j];
+  __syncthreads();
+  // wave w: output columns 16w..16w+15 of the 16 rows, the whole K
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const float* pa = sA + r * KP + 4 * q;
+  const float* pb = sB + (16 * wave + r) * KP + 4 * q;
+  for (int k16 = 0; k16 < K16; k16 += 32) {
+    const float4 a0 = *reinterpret_cast<const float4*>(pa + k16);
+    const float4 b0 = *reinterpret_cast<const float4*>(pb + k16);
+    const bool two = k16 + 16 < K16;
+    const float4 a1 = *reinterpret_cast<const float4*>(pa + (two ? k16 + 16 : k16));
+    const float4 b1 = *reinterpret_cast<const float4*>(pb + (two ? k16 + 16 : k16));
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b0.x, acc0, 0, 0, 0);
+    if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b1.x, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b0.y, acc0, 0, 0, 0);
+    if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b1.y, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b0.z, acc0, 0, 0, 0);
+    if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, b1.z, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc0, 0, 0, 0);
+    if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b1.w, acc1, 0, 0, 0);
+  }
+  // logits: lane (r, q) holds rows 4q..4q+3 of column ncol
+  float* Y = dr_uni(g.Y);
+  const long long ldy = g.ldy;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int ml = 4 * q + e, m = m0 + ml;
+    const float v = (acc0[e] + acc1[e]) + bcol;
+    sO[ml * (LS_NT + 1) + 16 * wave + r] = v;
+    if (Y && m < M) dr_g(Y)[(long long)m * ldy + ncol] = v;
+  }
+  __syncthreads();
+  // sampler: 16 rows x 2 groups = 32 (row, group) pairs, 2 per wave instruction
+  const int C = 32, Rg = dr_uni(g.R);
+  const float unimix = g.unimix;
+  const int c = lane & 31;
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    const int pidx = wave * 8 + pass * 2 + (lane >> 5);
+    const int ml = pidx >> 1, gl = pidx & 1;
+    const int m = m0 + ml, grp = (n0 >> 5) + gl;
+    const bool act = m < M;
+    const float x = act ? sO[ml * (LS_NT + 1) + gl * C + c] : -INFINITY;
+    const float mx = group_max(x, C);
+    const float ex = act ? expf(x - mx) : 0.0f;
+    const float se = group_sum(ex, C);
+    const float p = ex / se;
+    const float pu = act ? (0.99f * p + unimix) : 0.0f;
+    const float sp = group_sum(pu, C);
+    const float ph = pu / sp;
+    float qv = 1.0f;
+    if (act) {
+      if (g.noise.q) qv = dr_g(g.noise.q)[((long long)g.step * M * Rg + (long long)m * Rg + grp) * C + c];
+      else qv = dr_exp1_k(rng_seed, rng_off, (uint32_t)(g.noise.stream + g.step), (uint32_t)(g.noise.row0 + m),
+                          (uint32_t)(grp * C + c));
+    }
+    float best = act ? ph / qv : -INFINITY;
+    int bi = act ? c : 0x7fffffff;
+    group_argmax(best, bi, C);
+    if (act) {
+      dr_g(g.z_out)[(long long)m * g.ldz + grp * C + c] = (c == bi) ? ((1.0f + pu) - pu) : 0.0f;
+      if (g.soft_out) dr_g(g.soft_out)[(long long)m * g.ld_soft + grp * C + c] = p;
+      if (g.idx_out && c == 0) dr_g(g.idx_out)[m * Rg + grp] = bi;
+      if (g.zval_out && c == bi) dr_g(g.zval_out)[m * Rg + grp] = (1.0f + pu) - pu;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Tile GEMM for the mid-size problems (M >= 256 rows or TN weight gradients):
 // BM x BN output tile, 4 waves (2 x 2), K in chunks of 32 double-buffered
 // through LDS (rows padded to 36 floats, fragments read as float4 along k).
@@ -1931,11 +2098,44 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
   else launch_tile<32, 32, AMODE, A_KM, B_KN>(gb, count, s);
 }
 
+// the sampler-head kernel's shape: one LN-SiLU NT problem, C = 32, K <= 256
+static bool ln_sample_ok(const GemmArgs& g) {
+  return g.epi == EPI_SAMPLE && g.C == 32 && g.R * g.C == g.N && g.N % LS_NT == 0 && g.K > 0 && g.K % 4 == 0 &&
+         g.K <= LS_KMAX && g.M > 0 && g.M <= 65536 && g.ln_g && g.ln_b && g.ksplitA >= g.K && !g.addend &&
+         g.alpha == 1.0f && g.act == 0 && !g.accumulate && !g.W2 && aligned16(g.A) && aligned16(g.W) &&
+         aligned16(g.ln_g) && aligned16(g.ln_b) && g.lda % 4 == 0 && g.ldb % 4 == 0 &&
+         (!g.a_out || (aligned16(g.a_out) && g.ld_aout % 4 == 0)) && skinny_offsets_ok(g, false) &&
+         (long long)g.M * g.ldz < (1LL << 31);
+}
+#ifdef DR_PHASE_TIMING
+static int g_ln_sample_off = 0;  // kbench A/B: 1 = the skinny kernel's sampler epilogue instead
+extern "C" void dr_debug_ln_sample_off(int v) { g_ln_sample_off = v; }
+#else
+static constexpr int g_ln_sample_off = 0;
+#endif
+
+static int launch_ln_sample(const GemmArgs& g, hipStream_t s) {
+  const size_t lds = ln_sample_lds_bytes(g.K);
+  if (lds > 64 * 1024) {
+    static const bool raised = [] {
+      (void)hipFuncSetAttribute((const void*)k_ln_gemm_sample, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)ln_sample_lds_bytes(LS_KMAX));
+      return true;
+    }();
+    (void)raised;
+  }
+  const int tiles = dr_cdiv(g.M, LS_MT) * (g.N / LS_NT);
+  hipLaunchKernelGGL(k_ln_gemm_sample, dim3(dr_xcd_grid(tiles)), dim3(256), lds, s, g);
+  return dr_check_launch("ln_gemm_sample");
+}
+
 int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hipStream_t s) {
   if (count < 1 || count > 4) {
     dr_set_error("gemm_launch: bad problem count %d", count);
     return DR_E_INVALID;
   }
+  if (lay == G_NT && amode == AM_LNSILU && count == 1 && !g_ln_sample_off && ln_sample_ok(probs[0]))
+    return launch_ln_sample(probs[0], s);
   for (int i = 0; i < count; ++i) {
     const GemmArgs& g = probs[i];
     if (g.epi == EPI_SAMPLE && (g.C < 1 || g.C > 32 || 32 % g.C != 0 || g.N != g.R * g.C)) {

@@ -22,6 +22,7 @@ extern "C" void dr_debug_tile_variant(int v);
 extern "C" void dr_debug_skinny_variant(int v);
 extern "C" void dr_debug_tile_wgs(int v);
 extern "C" void dr_debug_gates_batch(int v);
+extern "C" void dr_debug_ln_sample_off(int v);
 
 // one more launch, then the per-phase times of wave 0 of each workgroup
 // (relative to its own start) averaged over the workgroups that wrote them
@@ -462,8 +463,11 @@ int main(int argc, char** argv) {
     float* zo = frand((size_t)B * 1024);
     int* io;
     CK(hipMalloc(&io, (size_t)B * 32 * 8));
-    for (int var : {0, 5}) {
-      dr_debug_skinny_variant(var);
+    for (int var : {0, 1, 5}) {
+      // 0: the dedicated sampler-head kernel (k_ln_gemm_sample); 1 / 5: the skinny kernel's
+      // sampler epilogue with 16-row (default) / 64-row tiles
+      dr_debug_ln_sample_off(var != 0);
+      dr_debug_skinny_variant(var == 5 ? 5 : 0);
       GemmArgs g = nt_(B, 1024, 200);
       g.ln_g = lng; g.ln_b = lnb;
       g.epi = EPI_SAMPLE; g.R = 32; g.C = 32; g.unimix = 0.01f / 32;
@@ -480,6 +484,7 @@ int main(int argc, char** argv) {
       phases(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_LNSILU, &gn, 1, st); }, dr_debug_tbuf_gemm, s);
     }
     dr_debug_skinny_variant(0);
+    dr_debug_ln_sample_off(0);
   }
   // per-step shapes of the imagination / BPTT chain, both row-tile variants
   for (int var = 0; var < 5; ++var) {
