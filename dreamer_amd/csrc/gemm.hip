@@ -1010,6 +1010,7 @@ __global__ __launch_bounds__(256) void k_ln_gemm_sample(GemmArgs ga) {
   const int tn = lt / tiles_m, tm = lt - tn * tiles_m;
   const int m0 = tm * LS_MT, n0 = tn * LS_NT;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
+  DR_TS(dr_tbuf_gemm, 0);
   const int K4 = K >> 2, K16 = (K + 15) & ~15, KP = K16 + 8;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sA = smem;                  // [LS_MT][KP]   SiLU(LN(x)) rows
@@ -1050,6 +1051,7 @@ __global__ __launch_bounds__(256) void k_ln_gemm_sample(GemmArgs ga) {
   float* a_out = dr_uni(g.a_out);
   const int ld_aout = dr_uni((int)g.ld_aout);
   const bool store_a = a_out != nullptr && tn == 0;
+  DR_TS(dr_tbuf_gemm, 1);
   // LayerNorm (eps 1e-5) + SiLU of this wave's 4 rows, as the skinny kernel's prologue
   const bool in16 = lane < (K16 >> 2);  // lanes that write the zero-padded K16 row
 #pragma unroll
@@ -1075,7 +1077,9 @@ __global__ __launch_bounds__(256) void k_ln_gemm_sample(GemmArgs ga) {
 #pragma unroll
   for (int j = 0; j < 16; ++j)
     if (in16) *reinterpret_cast<float4*>(&sB[(16 * wave + j) * KP + 4 * lane]) = xb[j];
+  DR_TS(dr_tbuf_gemm, 2);
   __syncthreads();
+  DR_TS(dr_tbuf_gemm, 3);
   // wave w: output columns 16w..16w+15 of the 16 rows, the whole K
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   const float* pa = sA + r * KP + 4 * q;
@@ -1095,6 +1099,7 @@ __global__ __launch_bounds__(256) void k_ln_gemm_sample(GemmArgs ga) {
     acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc0, 0, 0, 0);
     if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b1.w, acc1, 0, 0, 0);
   }
+  DR_TS(dr_tbuf_gemm, 4);
   // logits: lane (r, q) holds rows 4q..4q+3 of column ncol
   float* Y = dr_uni(g.Y);
   const long long ldy = g.ldy;
@@ -1106,6 +1111,7 @@ __global__ __launch_bounds__(256) void k_ln_gemm_sample(GemmArgs ga) {
     if (Y && m < M) dr_g(Y)[(long long)m * ldy + ncol] = v;
   }
   __syncthreads();
+  DR_TS(dr_tbuf_gemm, 5);
   // sampler: 16 rows x 2 groups = 32 (row, group) pairs, 2 per wave instruction
   const int C = 32, Rg = dr_uni(g.R);
   const float unimix = g.unimix;
@@ -1140,6 +1146,7 @@ __global__ __launch_bounds__(256) void k_ln_gemm_sample(GemmArgs ga) {
       if (g.zval_out && c == bi) dr_g(g.zval_out)[m * Rg + grp] = (1.0f + pu) - pu;
     }
   }
+  DR_TS(dr_tbuf_gemm, 6);
 }
 
 // ---------------------------------------------------------------------------
@@ -2041,11 +2048,16 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
     if (!A_KM && !B_KN && maxM >= 128 && maxM <= 512) {
       int tiles32 = 0;
       for (int i = 0; i < count; ++i) tiles32 += dr_cdiv(gb.p[i].M, 32) * dr_cdiv(gb.p[i].N, 32);
-      if (g_tile_variant == 0 && maxM <= 512 && (minK >= 1024 || (minK >= 512 && tiles32 >= 256))) {
+      if ((g_tile_variant == 0 || g_tile_variant >= 8) && maxM <= 512 &&
+          (minK >= 1024 || (minK >= 512 && tiles32 >= 256))) {
         GemmBatch gt = gb;
         if (tiles32 >= 256)
           for (int i = 0; i < count; ++i) gt.p[i].splitk_ws = nullptr;
         if (b16_ok(gb, count)) launch_tile_b16<32, 32, 4>(gt, count, s);
+        else if (g_tile_variant == 8) launch_tile2<32, 64, 64, false, false, 4>(gt, count, s);
+        else if (g_tile_variant == 9) launch_tile2<64, 32, 64, false, false, 4>(gt, count, s);
+        else if (g_tile_variant == 10) launch_tile2<64, 64, 64, false, false, 4>(gt, count, s);
+        else if (g_tile_variant == 11) launch_tile2<32, 64, 32, false, false, 4>(gt, count, s);
         else launch_tile2<32, 32, 64, false, false, 4>(gt, count, s);
         return;
       }

@@ -409,10 +409,10 @@ int main(int argc, char** argv) {
   // tile variants, without and with split-K scratch
   {
     float* skw = frand((size_t)8 * 256 * 2048);
-    for (int var : {0, 4, 5, 6, 7}) {
+    for (int var : {0, 4, 5, 6, 7, 8, 9, 10, 11}) {
       dr_debug_tile_variant(var);
       for (int sk = 0; sk < 2; ++sk) {
-        if (var == 0 && sk) continue;
+        if ((var == 0 || var >= 8) && sk) continue;
         auto prep = [&](GemmArgs g) {
           if (sk) { g.splitk_ws = skw; g.splitk_floats = 8LL * 256 * 2048; }
           return g;
