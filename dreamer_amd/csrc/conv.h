@@ -39,6 +39,12 @@ int op_to_bf16_2d(int rows, int cols, const float* x, long long ld, void* y, hip
 int op_conv1_bf16(int n, int nb, int h, int w, int cout, const dr_frames* src, const void* wr, const float* bias,
                   void* out, hipStream_t s);
 // conv1 + conv2 fused (c1 = 32, c2 = 64, square 64 / 128 frames); DR_E_INVALID = shape not covered
+// conv1 + conv2 (32 -> 64 channels, 64 x 64 frames from the u8 ring), f32-accurate
+// (conv_split.hip); repacks both weights into wr1 (3 x cout1 x 64 bf16) and wr2
+// (op_conv_repack_split3); DR_E_INVALID (nothing launched) for other shapes/sources
+int op_enc12_split3(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
+                    const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, float* out,
+                    hipStream_t s);
 int op_enc12_bf16(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const void* wr1, const float* b1,
                   const void* wr2, const float* b2, void* out, hipStream_t s);
 // k4 s2 p1 conv + bias + SiLU, bf16 NHWC in -> bf16 NHWC (or NCHW) out

@@ -271,6 +271,254 @@ int op_conv_repack_split3(int cout, int cin, const float* w, void* wr, hipStream
   return dr_check_launch("conv_repack_split3");
 }
 
+// ---------------------------------------------------------------------------
+// conv1 + conv2 fused, f32-accurate (enc_f1 = 32 -> enc_f2 = 64, 64 x 64
+// frames from the u8 replay ring; VariationalAutoEncoder.py:33-42 first two
+// layers, input x/255 - 0.5 as Dreamer.py:251).  Removes the f32 conv1
+// activation round trip through HBM (8192 frames: 1.07 GB written, 1.5 GB
+// re-read by conv2).
+//
+// conv1 needs no split of its input: the centred pixel values x - 127.5 are
+// exact in bf16 (8 significant bits), so x/255 - 0.5 = (x - 127.5) / 255 enters
+// the MFMA as ONE bf16 term against the three split3 planes of the weights (3
+// MFMAs per block), and the 1/255 is applied to the f32 sum.  The padding of
+// the normalised input is 0 = x - 127.5 at x = 127.5: zero in the centred
+// space too.  conv1's output (+ bias, SiLU) is split3 once, into three bf16
+// planes in LDS, and conv2 runs the usual six split products from them.
+//
+// A workgroup (4 waves) owns R2 = 8 rows of conv2 output (128 pixels x 64
+// channels, half a frame): it stages the RI = 38 input rows (bf16 [row][x+1][4
+// ch], as k_enc12_bf16), computes the R1 = 18 conv1 rows they feed (2 rows
+// recomputed per frame), then conv2 tap by tap with the tap's weight planes
+// (12 KB) double-buffered through LDS.  Wave w: conv2 rows 4 (w & 1) .. + 3,
+// channels 32 (w >> 1) .. + 31.
+// LDS: conv1 planes [3][4 c8][PS] 16-byte units, PS = 18 * 32 + 1 (odd plane
+// stride: the ds_read_b128 lane groups of a stride-2 pixel fragment fall on
+// distinct bank quads, as in k_enc12_bf16), 110.8 KB; input rows 20 KB;
+// weight ring 2 x 12 KB.  One workgroup per CU.
+// ---------------------------------------------------------------------------
+#define E12_R2 8
+#define E12_R1 (2 * E12_R2 + 2)
+#define E12_RI (2 * E12_R1 + 2)
+#define E12_PS (E12_R1 * 32 + 1)
+#define E12_LWI 66
+static constexpr size_t e12_lds_bytes() {
+  return (size_t)3 * 4 * E12_PS * 16 + (size_t)E12_RI * E12_LWI * 8 + (size_t)2 * 3 * 64 * 4 * 16;
+}
+
+__global__ __launch_bounds__(256) void k_enc12_split3(int n, int nb, dr_frames src, const u16* __restrict__ wr1,
+                                                      const float* __restrict__ b1, const u16* __restrict__ wr2,
+                                                      const float* __restrict__ b2, float* __restrict__ out) {
+  constexpr int R2 = E12_R2, R1 = E12_R1, RI = E12_RI, PS = E12_PS, LWI = E12_LWI;
+  constexpr int OW1 = 32, OW2 = 16, W = 64, H = 64, C1 = 32, C2 = 64;
+  extern __shared__ __attribute__((aligned(16))) u32x4 e12_smem[];
+  u32x4* c1o = e12_smem;                                                       // [3][4][PS]
+  uint2* xin = reinterpret_cast<uint2*>(e12_smem + 3 * 4 * PS);               // [RI][LWI]
+  u32x4* wring = e12_smem + 3 * 4 * PS + (RI * LWI * 8) / 16;                  // [2][3][64][4]
+  const int f = blockIdx.x >> 1, ty = blockIdx.x & 1;
+  if (f >= n) return;
+  const int y2_0 = ty * R2, y1_0 = 2 * y2_0 - 1, iy0 = 2 * y1_0 - 1;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
+
+  // conv2 weight ring: tap t's three planes, [plane][cout][4 units], unit u of
+  // row n at u ^ swz(n); thread -> units tid, tid + 256, tid + 512
+  u32x4 rw[3];
+  auto wload = [&](int tap) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int e = tid + 256 * k, pl = e >> 8, row = (e >> 2) & 63, u = e & 3;
+      rw[k] = *reinterpret_cast<const u32x4*>(wr2 + (((long long)tap * 3 + pl) * C2 + row) * 32 + 8 * u);
+    }
+  };
+  auto wstore = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int e = tid + 256 * k, pl = e >> 8, row = (e >> 2) & 63, u = e & 3;
+      wring[((buf * 3 + pl) * C2 + row) * 4 + (u ^ swz(row))] = rw[k];
+    }
+  };
+  wload(0);
+
+  // conv1 weights (A operand: lane -> channel 16 j + r, k = 32 s + 8 q .. + 7), three planes
+  u32x4 wa1[3][2][2];
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        wa1[pl][s][j] = *reinterpret_cast<const u32x4*>(wr1 + ((long long)pl * C1 + 16 * j + r) * 64 + 32 * s + 8 * q);
+  float bb1[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bb1[j][e] = b1[16 * j + 4 * q + e];
+
+  // ---- stage the input rows: bf16 of the centred pixel values ----
+  for (int i = tid; i < RI * LWI; i += 256) xin[i] = make_uint2(0u, 0u);
+  constexpr int W4 = W / 4, PERC = RI * W4, MAXI = (3 * PERC + 255) / 256;
+  const unsigned hw = (unsigned)(H * W);
+  const int b = f % nb, t = f / nb + src.t0;
+  const unsigned char* fr8 = src.ring + ((src.starts[b] + t) % src.ring_cap) * 3 * (long long)hw;
+  unsigned uv[MAXI];
+#pragma unroll
+  for (int k = 0; k < MAXI; ++k) {
+    const int i = tid + 256 * k;
+    const int c = i / PERC, rem = i - c * PERC, rr = rem / W4, x4 = rem - rr * W4;
+    const int y = iy0 + rr;
+    const bool ok = i < 3 * PERC && y >= 0 && y < H;
+    uv[k] = *reinterpret_cast<const unsigned*>(fr8 + (ok ? (unsigned)c * hw + (unsigned)(y * W + 4 * x4) : 0u));
+  }
+  const float centre = src.raw255 ? 127.5f : 0.0f, scale = src.raw255 ? 1.0f / 255.0f : 1.0f;
+  __syncthreads();
+  u16* xs = reinterpret_cast<u16*>(xin);
+#pragma unroll
+  for (int k = 0; k < MAXI; ++k) {
+    const int i = tid + 256 * k;
+    const int c = i / PERC, rem = i - c * PERC, rr = rem / W4, x4 = rem - rr * W4;
+    const int y = iy0 + rr;
+    if (i >= 3 * PERC || y < 0 || y >= H) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      xs[(rr * LWI + 4 * x4 + e + 1) * 4 + c] = b16bits((__bf16)((float)((uv[k] >> (8 * e)) & 255u) - centre));
+  }
+  wstore(0);
+  __syncthreads();
+
+  // ---- conv1 over the R1 tile rows; rows outside the frame are conv2's zero padding ----
+  u16* c1h = reinterpret_cast<u16*>(c1o);
+  constexpr int F1 = R1 * OW1 / 16;
+  for (int i = wave; i < F1; i += 4) {
+    const int p0 = 16 * i, yl = p0 / OW1, x1 = p0 - yl * OW1 + r, p = p0 + r;
+    const int y1 = y1_0 + yl;
+    uint2 hv[2], mv[2], lv[2];
+    if (y1 < 0 || y1 >= H / 2) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) hv[j] = mv[j] = lv[j] = make_uint2(0u, 0u);
+    } else {
+      f32x4 acc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int t0 = 8 * s + 2 * q, ky = t0 >> 2, kx = t0 & 3;
+        const u32x4 pb = *reinterpret_cast<const u32x4*>(&xin[(2 * yl + ky) * LWI + 2 * x1 + kx]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[j] = mfma_b16(wa1[2][s][j], pb, acc[j]);
+          acc[j] = mfma_b16(wa1[1][s][j], pb, acc[j]);
+          acc[j] = mfma_b16(wa1[0][s][j], pb, acc[j]);
+        }
+      }
+      // lane: pixel p, channels 16 j + 4 q .. + 3
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(acc[j][e] * scale + bb1[j][e]);
+        split3_pair(v[0], v[1], hv[j].x, mv[j].x, lv[j].x);
+        split3_pair(v[2], v[3], hv[j].y, mv[j].y, lv[j].y);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c8 = 2 * j + (q >> 1);
+      const int o = (c8 * PS + p) * 8 + (q & 1) * 4;  // u16 offset inside a plane
+      *reinterpret_cast<uint2*>(c1h + o) = hv[j];
+      *reinterpret_cast<uint2*>(c1h + 4 * PS * 8 + o) = mv[j];
+      *reinterpret_cast<uint2*>(c1h + 2 * 4 * PS * 8 + o) = lv[j];
+    }
+  }
+  __syncthreads();
+
+  // ---- conv2: K = 16 taps x 32 channels, one MFMA k-step per tap ----
+  const int ph = wave & 1, ch = wave >> 1;
+  const int fu = q ^ swz(r);  // weight rows 32 ch + 16 jj + r: swz(row) = swz(r)
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int tap = 0; tap < 16; ++tap) {
+    const int buf = tap & 1, ky = tap >> 2, kx = tap & 3;
+    if (tap + 1 < 16) wload(tap + 1);
+    u32x4 wf[3][2], pf[3][4];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) wf[pl][jj] = wring[((buf * 3 + pl) * C2 + 32 * ch + 16 * jj + r) * 4 + fu];
+    const int x1 = 2 * r - 1 + kx;
+    const bool xok = x1 >= 0 && x1 < OW1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int yl = 2 * (4 * ph + i) + ky;
+      const int u = q * PS + yl * OW1 + (xok ? x1 : 0);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        const u32x4 v = c1o[pl * 4 * PS + u];
+        pf[pl][i] = xok ? v : (u32x4){0u, 0u, 0u, 0u};
+      }
+    }
+    // smallest terms first (weight plane x activation plane)
+#define E12_S3(PW, PA)                       \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int jj = 0; jj < 2; ++jj) acc[i][jj] = \
+      mfma_b16(wf[PW][jj], pf[PA][i], acc[i][jj]);
+    E12_S3(2, 0)
+    E12_S3(1, 1)
+    E12_S3(0, 2)
+    E12_S3(1, 0)
+    E12_S3(0, 1)
+    E12_S3(0, 0)
+#undef E12_S3
+    if (tap + 1 < 16) wstore(buf ^ 1);
+    dr_lds_barrier();
+  }
+  // lane (r, q) of acc[i][jj]: channels 32 ch + 16 jj + 4 q .. + 3 of conv2 pixel (row 4 ph + i, column r)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float* o = out + (((long long)f * OW2 + y2_0 + 4 * ph + i) * OW2 + r) * C2;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int co = 32 * ch + 16 * jj + 4 * q;
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(b2 + co);
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(acc[i][jj][e] + bv[e]);
+      *reinterpret_cast<f32x4*>(o + co) = v;
+    }
+  }
+}
+
+// conv1 weight [cout][3][4][4] f32 -> three bf16 planes [3][cout][64], k = tap * 4 + c (c = 3: zero)
+__global__ void k_conv1_repack_split3(int cout, const float* __restrict__ w, u16* __restrict__ wr) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cout * 64) return;
+  const int co = i >> 6, k = i & 63, tap = k >> 2, c = k & 3;
+  unsigned h, m, l;
+  split3(c < 3 ? w[((long long)co * 3 + c) * 16 + tap] : 0.f, h, m, l);
+  wr[i] = (u16)h;
+  wr[cout * 64 + i] = (u16)m;
+  wr[2 * cout * 64 + i] = (u16)l;
+}
+
+int op_enc12_split3(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
+                    const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, float* out,
+                    hipStream_t s) {
+  if (c1 != 32 || c2 != 64 || h != 64 || w != 64 || !src->ring || !src->starts || src->ring_cap <= 0 || n <= 0 ||
+      (long long)n * 2 >= (1LL << 31))
+    return DR_E_INVALID;
+  static const bool raised = [] {
+    (void)hipFuncSetAttribute((const void*)k_enc12_split3, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)e12_lds_bytes());
+    return true;
+  }();
+  (void)raised;
+  hipLaunchKernelGGL(k_conv1_repack_split3, dim3((c1 * 64 + 255) / 256), dim3(256), 0, s, c1, w1, (u16*)wr1);
+  DR_TRY(dr_check_launch("conv1_repack_split3"));
+  DR_TRY(op_conv_repack_split3(c2, c1, w2, wr2, s));
+  hipLaunchKernelGGL(k_enc12_split3, dim3((unsigned)(n * 2)), dim3(256), e12_lds_bytes(), s, n, nb, *src,
+                     (const u16*)wr1, b1, (const u16*)wr2, b2, out);
+  return dr_check_launch("enc12_split3");
+}
+
 template <int BM, int BN, int CIN, bool NCHW, int PIPE>
 static int launch_s3(int n, int ih, int iw, int cout, const float* in, const void* wr, const float* bias, float* out,
                      hipStream_t s) {

@@ -35,7 +35,8 @@ static void enc_carve(Carve& c, const dr_dims* d, int n, EncWs& w) {
   w.sk = bf ? nullptr : c.f(w.sk_n);
   w.x0 = bf ? nullptr : c.f((long long)n * p0 * 4);
   for (int k = 0; k < N; ++k) w.a[k] = act((long long)n * (p0 >> (2 * (k + 1))) * e[k + 1]);
-  w.wr[0] = act((long long)e[1] * 4 * 16);
+  // conv1 weights: f32 [cout][64] (k_conv1_frames) or three bf16 planes (k_enc12_split3)
+  w.wr[0] = bf ? act((long long)e[1] * 4 * 16) : (float*)c.raw((size_t)e[1] * 64 * 6);
   // fp32: conv2..N weights as three bf16 planes (op_conv_repack_split3, 6 bytes
   // per weight; the f32 repack of the fallback fits in the same slot)
   for (int k = 1; k < N; ++k) {
@@ -114,17 +115,27 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
   WS_CHECK(c, ws_bytes);
   if (d->precision == DR_PREC_BF16) return encoder_bf16(d, wm, src, B, n, feat, w, s);
   const int h0 = d->img_h, w0 = d->img_w;
-  DR_TRY(op_conv_repack_pad(e[1], 3, 4, wm->conv[0].w, w.wr[0], s));
-  // the first conv straight from the frames (u8 ring or f32); shapes it does
-  // not tile go through the normalised NHWC4 copy
-  if (op_conv1_frames(n, B, h0, w0, e[1], src, w.wr[0], wm->conv[0].b, w.a[0], s) != DR_OK) {
-    DR_TRY(op_frames_nhwc4(n, B, h0, w0, src, w.x0, s));
-    DR_TRY(op_conv_nhwc(n, 4, h0, w0, e[1], w.x0, w.wr[0], wm->conv[0].b, w.a[0], 0, s));
+  // conv1 + conv2 in one launch from the u8 ring (conv_split.hip) where the
+  // shape allows; else the first conv straight from the frames (u8 ring or
+  // f32), and shapes that does not tile through the normalised NHWC4 copy
+  int k0 = 1;
+  const int rc12 = N >= 2 ? op_enc12_split3(n, B, h0, w0, e[1], e[2], src, wm->conv[0].w, wm->conv[0].b,
+                                            wm->conv[1].w, wm->conv[1].b, w.wr[0], w.wr[1], w.a[1], s)
+                          : DR_E_INVALID;
+  if (rc12 == DR_OK) {
+    k0 = 2;
+  } else {
+    if (rc12 != DR_E_INVALID) return rc12;
+    DR_TRY(op_conv_repack_pad(e[1], 3, 4, wm->conv[0].w, w.wr[0], s));
+    if (op_conv1_frames(n, B, h0, w0, e[1], src, w.wr[0], wm->conv[0].b, w.a[0], s) != DR_OK) {
+      DR_TRY(op_frames_nhwc4(n, B, h0, w0, src, w.x0, s));
+      DR_TRY(op_conv_nhwc(n, 4, h0, w0, e[1], w.x0, w.wr[0], wm->conv[0].b, w.a[0], 0, s));
+    }
   }
   // conv2..N: NHWC implicit GEMMs, f32-accurate on the bf16 MFMA (3-term split,
   // conv_split.hip) where the shape tiles, else on the f32 MFMA; the last layer
   // in NCHW == nn.Flatten order of Encoder.forward (VAE.py:72)
-  for (int k = 1; k < N; ++k) {
+  for (int k = k0; k < N; ++k) {
     const int cin = e[k], cout = e[k + 1], hin = h0 >> k, win = w0 >> k, last = k == N - 1;
     const float* cw = wm->conv[k].w;
     const float* cb = wm->conv[k].b;

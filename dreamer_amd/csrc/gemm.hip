@@ -994,11 +994,19 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, int m, int n, 
 #define LS_MT 16
 #define LS_NT 64
 #define LS_KMAX 256
+#define LS_SO (LS_NT + 4)  // logit row stride: float4 rows, the 16 x 4 fragment writes hit 64 banks
 static size_t ln_sample_lds_bytes(int K) {
   const int KP = ((K + 15) & ~15) + 8;  // 8 mod 16 dwords: conflict-free ds_read_b128 fragments
-  return sizeof(float) * ((size_t)(LS_MT + LS_NT) * KP + (size_t)LS_MT * (LS_NT + 1));
+  return sizeof(float) * ((size_t)(LS_MT + LS_NT) * KP + (size_t)LS_MT * LS_SO);
 }
 
+// NK = K16 / 16 k-chunks, a compile-time count: the fragment reads of the
+// whole K are ds_read_b128s the compiler can issue ahead of the MFMA chain.
+// Nothing after the first barrier loads from global memory: the sampler noise
+// (explicit q, or the Philox draws computed while the tile loads are in
+// flight) is in registers before the LayerNorm, and every load is branch-free
+// (a load inside a branch is waited for at the join, one round trip each).
+template <int NK>
 __global__ __launch_bounds__(256) void k_ln_gemm_sample(GemmArgs ga) {
   __shared__ GemmArgs g;
   dr_stage_args(ga, g, threadIdx.x);
@@ -1011,23 +1019,23 @@ __global__ __launch_bounds__(256) void k_ln_gemm_sample(GemmArgs ga) {
   const int m0 = tm * LS_MT, n0 = tn * LS_NT;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
   DR_TS(dr_tbuf_gemm, 0);
-  const int K4 = K >> 2, K16 = (K + 15) & ~15, KP = K16 + 8;
+  constexpr int K16 = 16 * NK, KP = K16 + 8;
+  const int K4 = K >> 2;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sA = smem;                  // [LS_MT][KP]   SiLU(LN(x)) rows
   float* sB = smem + LS_MT * KP;     // [LS_NT][KP]   weight rows
-  float* sO = sB + LS_NT * KP;       // [LS_MT][LS_NT + 1] logits
+  float* sO = sB + LS_NT * KP;       // [LS_MT][LS_SO] logits
   const float* A = dr_uni(g.A);
   const float* W = dr_uni(g.W);
   const int lda = dr_uni((int)g.lda), ldb = dr_uni((int)g.ldb);
-  // Philox state of the sampler, fetched now (not after the K loop)
-  unsigned long long rng_seed = 0, rng_off = 0;
-  if (!g.noise.q && g.noise.rng) {
-    rng_seed = g.noise.rng[0];
-    rng_off = g.noise.rng[1];
-  }
   // every global load of the tile, issued together: 4 LayerNorm rows, 16
-  // weight rows, gamma / beta (one float4 per lane each: K <= 256) and the
-  // bias of the column this lane finalises
+  // weight rows, gamma / beta (one float4 per lane each: K <= 256), the bias
+  // of the column this lane finalises and the sampler noise / Philox state
+  // the Philox state through the scalar cache (lgkmcnt): the draws below do
+  // not wait for the tile loads
+  typedef const __attribute__((address_space(4))) unsigned long long* dr_cu64;
+  const unsigned long long* rngp = g.noise.rng ? g.noise.rng : reinterpret_cast<const unsigned long long*>(W);
+  const unsigned long long rng_seed = ((dr_cu64)rngp)[0], rng_off = ((dr_cu64)rngp)[1];
   const bool okk = lane < K4;
   const unsigned ek = okk ? (unsigned)(4 * lane) : 0u;
   float4 xa[4], xb[16];
@@ -1047,11 +1055,35 @@ __global__ __launch_bounds__(256) void k_ln_gemm_sample(GemmArgs ga) {
   const float4 gv = dr_ld4(dr_uni(g.ln_g), ek), bv = dr_ld4(dr_uni(g.ln_b), ek);
   const float* bias = dr_uni(g.bias);
   const int ncol = n0 + 16 * wave + r;
-  const float bcol = bias ? dr_ld1(bias, (unsigned)ncol) : 0.f;
+  const float bcol = dr_ld1(bias ? bias : W, bias ? (unsigned)ncol : 0u);
+  // sampler: 16 rows x 2 groups = 32 (row, group) pairs, 8 lanes per pair
+  // and 4 consecutive classes per lane: lane -> row 4 wave + lane / 16, group
+  // (lane / 8) % 2, classes 4 (lane % 8) .. + 3
+  constexpr int C = 32;
+  const int Rg = dr_uni(g.R), sub = lane & 7, ml_s = 4 * wave + (lane >> 4), gl_s = (lane >> 3) & 1;
+  const int m_s = m0 + ml_s, grp_s = (n0 >> 5) + gl_s, c_s = 4 * sub;
+  const bool act_s = m_s < M;
+  const float* qsrc = dr_uni(g.noise.q);
+  const bool explicit_q = qsrc != nullptr;
+  // explicit q: one float4 per lane, loaded branch-free (from W, unused, in
+  // Philox mode) into registers of its own -- a load in a branch, or one
+  // whose registers the Philox branch overwrites, is waited for right there
+  const float* qb = explicit_q ? qsrc + (long long)g.step * M * Rg * C : W;
+  const float4 qx = dr_ld4(qb, explicit_q ? (unsigned)(((act_s ? m_s : 0) * Rg + grp_s) * C + c_s) : 0u);
+  float4 qn = make_float4(1.f, 1.f, 1.f, 1.f);
   float* a_out = dr_uni(g.a_out);
   const int ld_aout = dr_uni((int)g.ld_aout);
   const bool store_a = a_out != nullptr && tn == 0;
   DR_TS(dr_tbuf_gemm, 1);
+  if (!explicit_q) {
+    // Philox Exp(1) draws (VALU only) while the tile loads are in flight
+    const uint32_t stream = (uint32_t)(g.noise.stream + g.step), row = (uint32_t)(g.noise.row0 + m_s);
+    const uint32_t e0 = (uint32_t)(grp_s * C + c_s);
+    qn.x = dr_exp1_k(rng_seed, rng_off, stream, row, e0);
+    qn.y = dr_exp1_k(rng_seed, rng_off, stream, row, e0 + 1);
+    qn.z = dr_exp1_k(rng_seed, rng_off, stream, row, e0 + 2);
+    qn.w = dr_exp1_k(rng_seed, rng_off, stream, row, e0 + 3);
+  }
   // LayerNorm (eps 1e-5) + SiLU of this wave's 4 rows, as the skinny kernel's prologue
   const bool in16 = lane < (K16 >> 2);  // lanes that write the zero-padded K16 row
 #pragma unroll
@@ -1080,24 +1112,20 @@ __global__ __launch_bounds__(256) void k_ln_gemm_sample(GemmArgs ga) {
   DR_TS(dr_tbuf_gemm, 2);
   __syncthreads();
   DR_TS(dr_tbuf_gemm, 3);
-  // wave w: output columns 16w..16w+15 of the 16 rows, the whole K
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  // wave w: output columns 16w..16w+15 of the 16 rows, the whole K; two
+  // accumulators alternating per 16-k chunk (consecutive MFMAs independent)
+  f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   const float* pa = sA + r * KP + 4 * q;
   const float* pb = sB + (16 * wave + r) * KP + 4 * q;
-  for (int k16 = 0; k16 < K16; k16 += 32) {
-    const float4 a0 = *reinterpret_cast<const float4*>(pa + k16);
-    const float4 b0 = *reinterpret_cast<const float4*>(pb + k16);
-    const bool two = k16 + 16 < K16;
-    const float4 a1 = *reinterpret_cast<const float4*>(pa + (two ? k16 + 16 : k16));
-    const float4 b1 = *reinterpret_cast<const float4*>(pb + (two ? k16 + 16 : k16));
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b0.x, acc0, 0, 0, 0);
-    if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b1.x, acc1, 0, 0, 0);
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b0.y, acc0, 0, 0, 0);
-    if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b1.y, acc1, 0, 0, 0);
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b0.z, acc0, 0, 0, 0);
-    if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, b1.z, acc1, 0, 0, 0);
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc0, 0, 0, 0);
-    if (two) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b1.w, acc1, 0, 0, 0);
+#pragma unroll
+  for (int kc = 0; kc < NK; ++kc) {
+    const float4 a = *reinterpret_cast<const float4*>(pa + 16 * kc);
+    const float4 b = *reinterpret_cast<const float4*>(pb + 16 * kc);
+    f32x4& t = acc[kc & 1];
+    t = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, t, 0, 0, 0);
   }
   DR_TS(dr_tbuf_gemm, 4);
   // logits: lane (r, q) holds rows 4q..4q+3 of column ncol
@@ -1106,44 +1134,61 @@ __global__ __launch_bounds__(256) void k_ln_gemm_sample(GemmArgs ga) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int ml = 4 * q + e, m = m0 + ml;
-    const float v = (acc0[e] + acc1[e]) + bcol;
-    sO[ml * (LS_NT + 1) + 16 * wave + r] = v;
+    const float v = (acc[0][e] + acc[1][e]) + bcol;
+    sO[ml * LS_SO + 16 * wave + r] = v;
     if (Y && m < M) dr_g(Y)[(long long)m * ldy + ncol] = v;
   }
   __syncthreads();
   DR_TS(dr_tbuf_gemm, 5);
-  // sampler: 16 rows x 2 groups = 32 (row, group) pairs, 2 per wave instruction
-  const int C = 32, Rg = dr_uni(g.R);
+  // the sampler (softmax, 1 % unimix, argmax(p_hat / q), straight-through
+  // one-hot): 8-lane DPP reductions, no loads, no LDS permutes
   const float unimix = g.unimix;
-  const int c = lane & 31;
+  float x[4];
+  {
+    const float4 xv = *reinterpret_cast<const float4*>(&sO[ml_s * LS_SO + gl_s * C + c_s]);
+    x[0] = xv.x, x[1] = xv.y, x[2] = xv.z, x[3] = xv.w;
+  }
+  if (explicit_q) qn = qx;
+  const float qv[4] = {qn.x, qn.y, qn.z, qn.w};
+  float mx = act_s ? fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])) : -INFINITY;
+  mx = group_max(mx, 8);
+  float ex[4], pu[4], p[4];
 #pragma unroll
-  for (int pass = 0; pass < 4; ++pass) {
-    const int pidx = wave * 8 + pass * 2 + (lane >> 5);
-    const int ml = pidx >> 1, gl = pidx & 1;
-    const int m = m0 + ml, grp = (n0 >> 5) + gl;
-    const bool act = m < M;
-    const float x = act ? sO[ml * (LS_NT + 1) + gl * C + c] : -INFINITY;
-    const float mx = group_max(x, C);
-    const float ex = act ? expf(x - mx) : 0.0f;
-    const float se = group_sum(ex, C);
-    const float p = ex / se;
-    const float pu = act ? (0.99f * p + unimix) : 0.0f;
-    const float sp = group_sum(pu, C);
-    const float ph = pu / sp;
-    float qv = 1.0f;
-    if (act) {
-      if (g.noise.q) qv = dr_g(g.noise.q)[((long long)g.step * M * Rg + (long long)m * Rg + grp) * C + c];
-      else qv = dr_exp1_k(rng_seed, rng_off, (uint32_t)(g.noise.stream + g.step), (uint32_t)(g.noise.row0 + m),
-                          (uint32_t)(grp * C + c));
+  for (int t = 0; t < 4; ++t) ex[t] = act_s ? expf(x[t] - mx) : 0.0f;
+  const float se = group_sum((ex[0] + ex[1]) + (ex[2] + ex[3]), 8);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    p[t] = ex[t] / se;
+    pu[t] = act_s ? (0.99f * p[t] + unimix) : 0.0f;
+  }
+  const float sp = group_sum((pu[0] + pu[1]) + (pu[2] + pu[3]), 8);
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  if (act_s) {
+    best = (pu[0] / sp) / qv[0];
+    bi = c_s;
+#pragma unroll
+    for (int t = 1; t < 4; ++t) {
+      const float v = (pu[t] / sp) / qv[t];
+      bi = v > best ? c_s + t : bi;  // ties keep the lower class
+      best = fmaxf(best, v);
     }
-    float best = act ? ph / qv : -INFINITY;
-    int bi = act ? c : 0x7fffffff;
-    group_argmax(best, bi, C);
-    if (act) {
-      dr_g(g.z_out)[(long long)m * g.ldz + grp * C + c] = (c == bi) ? ((1.0f + pu) - pu) : 0.0f;
-      if (g.soft_out) dr_g(g.soft_out)[(long long)m * g.ld_soft + grp * C + c] = p;
-      if (g.idx_out && c == 0) dr_g(g.idx_out)[m * Rg + grp] = bi;
-      if (g.zval_out && c == bi) dr_g(g.zval_out)[m * Rg + grp] = (1.0f + pu) - pu;
+  }
+  group_argmax(best, bi, 8);
+  if (act_s) {
+    float4 z;
+    z.x = (c_s + 0 == bi) ? ((1.0f + pu[0]) - pu[0]) : 0.0f;
+    z.y = (c_s + 1 == bi) ? ((1.0f + pu[1]) - pu[1]) : 0.0f;
+    z.z = (c_s + 2 == bi) ? ((1.0f + pu[2]) - pu[2]) : 0.0f;
+    z.w = (c_s + 3 == bi) ? ((1.0f + pu[3]) - pu[3]) : 0.0f;
+    *(DR_GLOBAL dr_f4*)(dr_g(g.z_out) + ((long long)m_s * g.ldz + grp_s * C + c_s)) = dr_f4{z.x, z.y, z.z, z.w};
+    if (g.soft_out)
+      *(DR_GLOBAL dr_f4*)(dr_g(g.soft_out) + ((long long)m_s * g.ld_soft + grp_s * C + c_s)) = dr_f4{p[0], p[1], p[2], p[3]};
+    if (g.idx_out && sub == 0) dr_g(g.idx_out)[m_s * Rg + grp_s] = bi;
+    if (g.zval_out && (unsigned)(bi - c_s) < 4u) {
+      const int t = bi - c_s;
+      const float pb = t == 0 ? pu[0] : t == 1 ? pu[1] : t == 2 ? pu[2] : pu[3];
+      dr_g(g.zval_out)[m_s * Rg + grp_s] = (1.0f + pb) - pb;
     }
   }
   DR_TS(dr_tbuf_gemm, 6);
@@ -2117,7 +2162,8 @@ static bool ln_sample_ok(const GemmArgs& g) {
          g.alpha == 1.0f && g.act == 0 && !g.accumulate && !g.W2 && aligned16(g.A) && aligned16(g.W) &&
          aligned16(g.ln_g) && aligned16(g.ln_b) && g.lda % 4 == 0 && g.ldb % 4 == 0 &&
          (!g.a_out || (aligned16(g.a_out) && g.ld_aout % 4 == 0)) && skinny_offsets_ok(g, false) &&
-         (long long)g.M * g.ldz < (1LL << 31);
+         (long long)g.M * g.ldz < (1LL << 31) && aligned16(g.z_out) && g.ldz % 4 == 0 &&
+         (!g.soft_out || (aligned16(g.soft_out) && g.ld_soft % 4 == 0)) && (!g.noise.q || aligned16(g.noise.q));
 }
 #ifdef DR_PHASE_TIMING
 static int g_ln_sample_off = 0;  // kbench A/B: 1 = the skinny kernel's sampler epilogue instead
@@ -2126,19 +2172,35 @@ extern "C" void dr_debug_ln_sample_off(int v) { g_ln_sample_off = v; }
 static constexpr int g_ln_sample_off = 0;
 #endif
 
-static int launch_ln_sample(const GemmArgs& g, hipStream_t s) {
+template <int NK>
+static int launch_ln_sample_nk(const GemmArgs& g, hipStream_t s) {
   const size_t lds = ln_sample_lds_bytes(g.K);
   if (lds > 64 * 1024) {
     static const bool raised = [] {
-      (void)hipFuncSetAttribute((const void*)k_ln_gemm_sample, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)ln_sample_lds_bytes(LS_KMAX));
+      (void)hipFuncSetAttribute((const void*)k_ln_gemm_sample<NK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)ln_sample_lds_bytes(16 * NK));
       return true;
     }();
     (void)raised;
   }
   const int tiles = dr_cdiv(g.M, LS_MT) * (g.N / LS_NT);
-  hipLaunchKernelGGL(k_ln_gemm_sample, dim3(dr_xcd_grid(tiles)), dim3(256), lds, s, g);
+  hipLaunchKernelGGL(k_ln_gemm_sample<NK>, dim3(dr_xcd_grid(tiles)), dim3(256), lds, s, g);
   return dr_check_launch("ln_gemm_sample");
+}
+
+static int launch_ln_sample(const GemmArgs& g, hipStream_t s) {
+  switch ((g.K + 15) >> 4) {  // ln_sample_ok: 0 < K <= LS_KMAX
+#define DR_LS_CASE(n) \
+  case n:             \
+    return launch_ln_sample_nk<n>(g, s);
+    DR_LS_CASE(1) DR_LS_CASE(2) DR_LS_CASE(3) DR_LS_CASE(4) DR_LS_CASE(5) DR_LS_CASE(6) DR_LS_CASE(7)
+    DR_LS_CASE(8) DR_LS_CASE(9) DR_LS_CASE(10) DR_LS_CASE(11) DR_LS_CASE(12) DR_LS_CASE(13) DR_LS_CASE(14)
+    DR_LS_CASE(15) DR_LS_CASE(16)
+#undef DR_LS_CASE
+    default:
+      dr_set_error("ln_gemm_sample: K %d out of range", g.K);
+      return DR_E_INVALID;
+  }
 }
 
 int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hipStream_t s) {
