@@ -267,7 +267,7 @@ extern "C" size_t dr_imagine_tape_bytes(const dr_dims* d, int B, int H) {
 }
 
 struct ImWs {
-  float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog, *wt, *wst, *bst;  // forward scratch
+  float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog, *rval, *wt, *wst, *bst;  // forward scratch
   int* idx[2];
   // backward
   float *gH, *gZ, *gA, *glog, *gx2, *gp2, *gx1, *gp1, *ggi, *ggh, *gheads, *gx2a, *gpre2a, *gy2a, *xh2a, *gx1a,
@@ -282,12 +282,14 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.gi = c.f(Bl * 3 * Hd);
   w.gh = c.f(Bl * 3 * Hd);
   w.plog = c.f(Bl * L);
-  w.p1r = c.f(Bl * d->rew_h1);
-  w.p1c = c.f(Bl * d->cont_h1);
-  w.p2r = c.f(Bl * d->rew_h2);
-  w.p2c = c.f(Bl * d->cont_h2);
-  w.rlog = c.f((long long)B * H * d->buckets);
-  w.clog = c.f(Bl);
+  // reward / continue heads, batched over all B (H + 1) imagined states after the unroll
+  w.p1r = c.f(B1 * d->rew_h1);
+  w.p1c = c.f(B1 * d->cont_h1);
+  w.p2r = c.f(B1 * d->rew_h2);
+  w.p2c = c.f(B1 * d->cont_h2);
+  w.rlog = c.f(B1 * d->buckets);
+  w.clog = c.f(B1);
+  w.rval = c.f(B1);
   w.wt = c.f((long long)(L + A) * 3 * Hd);
   w.wst = c.f((long long)2 * A * d->actor_h2);
   w.bst = c.f((long long)2 * A);
@@ -387,55 +389,68 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
     GemmArgs g = lin_ln(B, L, d->prior_h2, p2, d->prior_h2, wm->prior.n4, wm->prior.l6.w, wm->prior.l6.b, nullptr, 0);
     with_sampler(g, d, nq, t, z_n, ldL, w.idx[(t + 1) & 1], tp.soft + (long long)t * B * L, L);
     DR_TRY(run(G_NT, AM_LNSILU, g, s));
-    // reward / continue heads on (h', z') and the actor for step t+1, grouped
-    const bool nxt = (t + 1 < H);
-    {
-      GemmArgs p[3];
-      p[0] = lin2(B, d->rew_h1, h_n, ldH, Hd, z_n, ldL, L, wm->reward.l0.w, wm->reward.l0.b, w.p1r, d->rew_h1);
-      p[1] = lin2(B, d->cont_h1, h_n, ldH, Hd, z_n, ldL, L, wm->cont.l0.w, wm->cont.l0.b, w.p1c, d->cont_h1);
-      if (nxt)
-        p[2] = lin2(B, a1, h_n, ldH, Hd, z_n, ldL, L, ac->l0.w, ac->l0.b, tp.pre1a + (long long)(t + 1) * a1, lda1);
-      // split-K scratch (the actor weight-gradient region, idle until the backward)
-      float* sk = w.sk;
-      long long skn = w.sk_n;
-      for (int i = 0; i < (nxt ? 3 : 2); ++i) give_splitk(p[i], sk, skn);
-      DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, nxt ? 3 : 2, s));
-    }
-    {
-      GemmArgs p[3];
-      p[0] = lin_ln(B, d->rew_h2, d->rew_h1, w.p1r, d->rew_h1, wm->reward.n1, wm->reward.l3.w, wm->reward.l3.b, w.p2r,
-                    d->rew_h2);
-      p[1] = lin_ln(B, d->cont_h2, d->cont_h1, w.p1c, d->cont_h1, wm->cont.n1, wm->cont.l3.w, wm->cont.l3.b, w.p2c,
-                    d->cont_h2);
-      if (nxt) {
-        p[2] = lin_ln(B, a2, a1, tp.pre1a + (long long)(t + 1) * a1, lda1, ac->n1, ac->l3.w, ac->l3.b,
-                      tp.pre2a + (long long)(t + 1) * a2, lda2);
-        p[2].a_out = tp.x1a + (long long)(t + 1) * a1;
-        p[2].ld_aout = lda1;
-      }
-      DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, nxt ? 3 : 2, s));
-    }
-    {
-      // reward logits kept for one deferred bucket-value pass; continue
-      // probability via the sigmoid epilogue; actor head (next step) fused
-      GemmArgs p[3];
-      p[0] = lin_ln(B, d->buckets, d->rew_h2, w.p2r, d->rew_h2, wm->reward.n4, wm->reward.l6.w, wm->reward.l6.b,
-                    w.rlog + (long long)t * d->buckets, (long long)H * d->buckets);
-      p[1] = lin_ln(B, 1, d->cont_h2, w.p2c, d->cont_h2, wm->cont.n4, wm->cont.l6.w, wm->cont.l6.b, continues + t, H);
-      p[1].act = 2;
-      if (nxt) {
-        const long long o = (long long)(t + 1) * A;
-        p[2] = lin_ln(B, 2 * A, a2, tp.pre2a + (long long)(t + 1) * a2, lda2, ac->n4, w.wst, w.bst, nullptr, 0);
-        p[2].a_out = tp.x2a + (long long)(t + 1) * a2;
-        p[2].ld_aout = lda2;
-        with_actor_head(p[2], A, noise, t + 1, deterministic, actions + o, ldA, mus + o, ldA, sigmas + o, ldA,
-                        tp.eps + (long long)(t + 1) * B * A, tp.ls_raw + o, ldA);
-      }
-      DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, nxt ? 3 : 2, s));
+    // the actor for step t+1 (the reward / continue heads run once after the unroll)
+    if (t + 1 < H) {
+      const long long o1 = (long long)(t + 1) * a1, o2 = (long long)(t + 1) * a2, o = (long long)(t + 1) * A;
+      DR_TRY(run(G_NT, AM_PLAIN, lin2(B, a1, h_n, ldH, Hd, z_n, ldL, L, ac->l0.w, ac->l0.b, tp.pre1a + o1, lda1), s));
+      GemmArgs g3 = lin_ln(B, a2, a1, tp.pre1a + o1, lda1, ac->n1, ac->l3.w, ac->l3.b, tp.pre2a + o2, lda2);
+      g3.a_out = tp.x1a + o1;
+      g3.ld_aout = lda1;
+      DR_TRY(run(G_NT, AM_LNSILU, g3, s));
+      GemmArgs hd = lin_ln(B, 2 * A, a2, tp.pre2a + o2, lda2, ac->n4, w.wst, w.bst, nullptr, 0);
+      hd.a_out = tp.x2a + o2;
+      hd.ld_aout = lda2;
+      with_actor_head(hd, A, noise, t + 1, deterministic, actions + o, ldA, mus + o, ldA, sigmas + o, ldA,
+                      tp.eps + (long long)(t + 1) * B * A, tp.ls_raw + o, ldA);
+      DR_TRY(run(G_NT, AM_LNSILU, hd, s));
     }
   }
-  // RewardPredictor.predict for every imagined step at once (rows b*H + t)
-  DR_TRY(op_bucket_value(B * H, d->buckets, w.rlog, d->buckets, wm->buckets_rew, rewards, 1, s));
+  // RewardPredictor / ContinuePredictor (DynamicsPredictors.py:64-74, 95-105)
+  // on every imagined state (h_{t+1}, z_{t+1}) at once: rows m = b (H+1) + t'
+  // of the contiguous [B][H+1] hiddens / latents (t' = 0 rides along unused);
+  // forward only -- the actor loss takes no gradient through the heads
+  {
+    const int M1 = B * (H + 1);
+    GemmArgs p[2];
+    p[0] = lin2(M1, d->rew_h1, hiddens, Hd, Hd, latents, L, L, wm->reward.l0.w, wm->reward.l0.b, w.p1r, d->rew_h1);
+    p[1] = lin2(M1, d->cont_h1, hiddens, Hd, Hd, latents, L, L, wm->cont.l0.w, wm->cont.l0.b, w.p1c, d->cont_h1);
+    DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, 2, s));
+    p[0] = lin_ln(M1, d->buckets, d->rew_h2, w.p2r, d->rew_h2, wm->reward.n4, wm->reward.l6.w, wm->reward.l6.b, w.rlog,
+                  d->buckets);
+    p[1] = lin_ln(M1, 1, d->cont_h2, w.p2c, d->cont_h2, wm->cont.n4, wm->cont.l6.w, wm->cont.l6.b, w.clog, 1);
+    p[1].act = 2;  // sigmoid
+    if (std::max(std::max(d->rew_h1, d->rew_h2), std::max(d->cont_h1, d->cont_h2)) <= 208) {
+      // LN-SiLU, Linear, LN-SiLU, Linear of both heads in one launch (k_mlp2_tail:
+      // 16 rows per workgroup, the 200-wide middle layer recomputed per
+      // 128-column block); the two-launch form below is the general path
+      Mlp2Args m2[2];
+      const float* x1[2] = {w.p1r, w.p1c};
+      const dr_mlp3* hm[2] = {&wm->reward, &wm->cont};
+      const int k1[2] = {d->rew_h1, d->cont_h1}, k2[2] = {d->rew_h2, d->cont_h2};
+      for (int i = 0; i < 2; ++i) {
+        memset(&m2[i], 0, sizeof(Mlp2Args));
+        m2[i].M = M1; m2[i].K1 = k1[i]; m2[i].K2 = k2[i];
+        m2[i].X = x1[i]; m2[i].ldx = k1[i];
+        m2[i].ln1_g = hm[i]->n1.w; m2[i].ln1_b = hm[i]->n1.b;
+        m2[i].W3 = hm[i]->l3.w; m2[i].b3 = hm[i]->l3.b;
+        m2[i].ln4_g = hm[i]->n4.w; m2[i].ln4_b = hm[i]->n4.b;
+        m2[i].e = p[i];
+        m2[i].e.A = nullptr;
+      }
+      DR_TRY(mlp2_launch(m2, 2, s));
+    } else {
+      GemmArgs q[2];
+      q[0] = lin_ln(M1, d->rew_h2, d->rew_h1, w.p1r, d->rew_h1, wm->reward.n1, wm->reward.l3.w, wm->reward.l3.b, w.p2r,
+                    d->rew_h2);
+      q[1] = lin_ln(M1, d->cont_h2, d->cont_h1, w.p1c, d->cont_h1, wm->cont.n1, wm->cont.l3.w, wm->cont.l3.b, w.p2c,
+                    d->cont_h2);
+      DR_TRY(gemm_launch(G_NT, AM_LNSILU, q, 2, s));
+      DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, 2, s));
+    }
+    DR_TRY(op_bucket_value(M1, d->buckets, w.rlog, d->buckets, wm->buckets_rew, w.rval, 1, s));
+    DR_TRY(copy2d(rewards, H, w.rval + 1, H + 1, H, B, s));
+    DR_TRY(copy2d(continues, H, w.clog + 1, H + 1, H, B, s));
+  }
   return DR_OK;
 }
 

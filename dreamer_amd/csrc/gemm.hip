@@ -236,6 +236,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmBatch gb) {
         if (g.bias) v = v + g.bias[n];
         if (g.addend) v = v + g.addend[(long long)m * g.ld_add + n];
         if (g.act == 1) v = v / (1.0f + expf(-v));
+        else if (g.act == 2) v = 1.0f / (1.0f + expf(-v));
         float* dst;
         if (g.out_conv) {
           const int hw = g.oh * g.ow;
@@ -1568,6 +1569,160 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tile_b16(GemmBatch gb, int spl
       }
 }
 
+// ---------------------------------------------------------------------------
+// Per-step chain products at 128-512 rows (GRU hidden product, heads' first
+// layers, BPTT input gradients): NT, f32 MFMA, no LDS staging.  Every wave of
+// the workgroup computes the WHOLE BM x BN tile over its own run of 32-k
+// blocks (K split over the waves), so no operand fragment is shared between
+// waves: each lane loads its MFMA fragments straight from L2 into registers
+// (lane (r, q) reads 8 consecutive k of row r: a 16-row x 128-B coalesced
+// line per pair of float4 loads), D blocks ahead in a register ring, with no
+// barrier in the K loop.  The 8 k of a lane feed 8 consecutive MFMAs; A and B
+// use the same k order, so the sum is the product's.  The NW partial tiles
+// meet once in LDS at the end.  K % 8 == 0, ksplitA % 8 == 0 (a lane's 8-run
+// never straddles A / A2), 16-byte aligned rows (host-checked: wk_ok).
+// ---------------------------------------------------------------------------
+template <int BM, int BN, int NW, int D, int KMAP = 0>
+__global__ __launch_bounds__(64 * NW) void k_gemm_wk(GemmBatch gb, int splits) {
+  constexpr int NTH = 64 * NW, FM = BM / 16, FN = BN / 16, NT4 = FM * FN * 256;
+  static_assert(FM * FN >= 4, "at least 4 independent accumulators per wave (40-cycle MFMA latency)");
+  __shared__ GemmArgs s_args;
+  __shared__ __attribute__((aligned(16))) float red[NW][FM * FN * 4][64];
+  dr_stage_args(gb.p[blockIdx.z], s_args, threadIdx.x);
+  const GemmArgs& g = s_args;
+  const int M = dr_uni(g.M), N = dr_uni(g.N), K = dr_uni(g.K);
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const int lt = dr_xcd_tile(blockIdx.x, tiles_m * tiles_n);
+  if (lt < 0) return;
+  const int tn = lt / tiles_m, tm = lt - tn * tiles_m;  // m-tiles sharing a weight slice are adjacent
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const float* A = dr_uni(g.A);
+  const float* A2 = dr_uni(g.A2);
+  const float* W = dr_uni(g.W);
+  const int lda = dr_uni((int)g.lda), lda2 = dr_uni((int)g.lda2), ldb = dr_uni((int)g.ldb);
+  const int ksA = dr_uni(g.ksplitA);
+
+  // bias of the outputs this thread finalises: issued now, waited for at the end
+  constexpr int NEPI = (NT4 + NTH - 1) / NTH;
+  float ebias[NEPI];
+  {
+    const float* bias = dr_uni(g.bias);
+#pragma unroll
+    for (int i = 0; i < NEPI; ++i) {
+      const int x = tid + NTH * i, l = x & 63, tj = x >> 8;
+      const int n = n0 + (tj % FN) * 16 + (l & 15);
+      const bool ok = bias && splits == 1 && x < NT4 && n < N;
+      const float v = dr_ld1(ok ? bias : W, ok ? (unsigned)n : 0u);
+      ebias[i] = ok ? v : 0.f;
+    }
+  }
+
+  // this workgroup's 32-k blocks (split-K over blockIdx.y), then this wave's
+  const int nkb = (K + 31) >> 5;
+  const int per = (nkb + splits - 1) / splits;
+  const int kb0 = min(nkb, (int)blockIdx.y * per), kb1 = min(nkb, kb0 + per);
+  const int nbg = kb1 - kb0;
+  const int b0 = kb0 + (nbg * wave) / NW, b1 = kb0 + (nbg * (wave + 1)) / NW;
+  const int blast = max(min(b1, nkb) - 1, 0);  // loads past this wave's run re-read its last block (unused)
+
+  // per-lane row offsets (rows past M / N read row M-1 / N-1: valid addresses, outputs discarded)
+  unsigned oa[FM], oa2[FM], ob[FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = min(m0 + 16 * i + r, M - 1);
+    oa[i] = (unsigned)(m * lda);
+    oa2[i] = (unsigned)(m * lda2);
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j) ob[j] = (unsigned)(min(n0 + 16 * j + r, N - 1) * ldb);
+
+  f32x4 ra[D][FM][2], rb[D][FN][2];
+  // KMAP 0: lane q reads k = 8q..8q+7 of the block (two float4, one 32-B run);
+  // KMAP 1: k = 4q..4q+3 and 16+4q..16+4q+3 (each instruction a 64-B run per row)
+  constexpr int KL = KMAP == 0 ? 8 : 4, KH = KMAP == 0 ? 4 : 16;
+  auto load = [&](int b, int sl) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = 32 * b + KL * q + KH * h;
+      const int kk = k < K ? k : 0;  // lanes past K re-read k = 0 (zeroed before use)
+      const bool s1 = kk < ksA;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const float* base = s1 ? A : A2;
+        const unsigned e = s1 ? oa[i] + (unsigned)kk : oa2[i] + (unsigned)(kk - ksA);
+        ra[sl][i][h] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)base + (e << 2));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const unsigned e = ob[j] + (unsigned)kk;
+        rb[sl][j][h] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)W + (e << 2));
+      }
+    }
+  };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < D; ++u) load(min(b0 + u, blast), u);
+  const int nbw = b1 - b0;
+  const bool ktail = (K & 31) != 0;
+  for (int bb = 0; bb < nbw; bb += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      if (bb + u >= nbw) break;
+      const int b = b0 + bb + u;
+      if (ktail && b == nkb - 1) {  // the K tail: zero the runs past K
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if (32 * b + KL * q + KH * h < K) continue;
+#pragma unroll
+          for (int i = 0; i < FM; ++i) ra[u][i][h] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int j = 0; j < FN; ++j) rb[u][j][h] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[u][i][h][c], rb[u][j][h][c], acc[i][j], 0, 0, 0);
+      load(min(b + D, blast), u);  // unconditional: a load under a branch is waited for at once
+    }
+  }
+  // the NW partial tiles meet in LDS; element (t, e, l) of tile t = (i, j):
+  // D[row 4 (l >> 4) + e][col l & 15]
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[wave][(i * FN + j) * 4 + e][lane] = acc[i][j][e];
+  __syncthreads();
+  float* part = g.splitk_ws;
+#pragma unroll
+  for (int ii = 0; ii < NEPI; ++ii) {
+    const int x = tid + NTH * ii;
+    if (x >= NT4) break;
+    const int l = x & 63, e = (x >> 6) & 3, tj = x >> 8;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][tj * 4 + e][l];
+    const int t = tj / FN, j = tj - t * FN;
+    const int m = m0 + t * 16 + 4 * (l >> 4) + e, n = n0 + j * 16 + (l & 15);
+    if (m >= M || n >= N) continue;
+    if (splits == 1) epilogue_store_b(g, m, n, v, ebias[ii]);
+    else dr_g(part)[((long long)blockIdx.y * M + m) * N + n] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_splitk_finish(GemmBatch gb, int splits) {
   const GemmArgs& g = gb.p[blockIdx.z];
   const long long MN = (long long)g.M * g.N;
@@ -1678,7 +1833,9 @@ static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
     if (!skinny_offsets_ok(g, B_KN)) return false;
     vec = vec && skinny_vec_ok(g, B_KN);
   }
-  if (maxM > 4096) return false;
+  // fused row epilogues are validated for M <= 4096 (gemm_launch); plain
+  // epilogues take any M the 32-bit offsets allow (64-row tiles past 64 rows)
+  if (maxM > (epi == EPI_NONE ? (1 << 20) : 4096)) return false;
   if (g_skinny_variant == 1 && maxM > 16) maxM = 65;
   if (g_skinny_variant == 3) maxM = std::min(maxM, 64);  // 16-row tiles at any M
   // 16-row tiles past 64 rows while the grid stays within ~2.5 dispatch
@@ -2050,6 +2207,47 @@ static void launch_tile_b16(GemmBatch& gb, int count, hipStream_t s) {
     hipLaunchKernelGGL(k_splitk_finish, dim3((unsigned)((maxMN + 255) / 256), 1, count), dim3(256), 0, s, gb, splits);
 }
 
+// wave-K chain kernel: 8-wide k runs on 16-byte boundaries in every operand
+static bool wk_ok(const GemmBatch& gb, int count) {
+  for (int i = 0; i < count; ++i) {
+    const GemmArgs& g = gb.p[i];
+    if (g.K % 8 || g.K < 8 || g.lda % 4 || g.ldb % 4 || ((uintptr_t)g.A & 15) || ((uintptr_t)g.W & 15)) return false;
+    if (g.ksplitA < g.K && (g.ksplitA % 8 || g.lda2 % 4 || ((uintptr_t)g.A2 & 15))) return false;
+    if (g.W2 || g.epi != EPI_NONE || g.out_conv || g.M < 1 || g.N < 1) return false;
+  }
+  return true;
+}
+
+// split-K over workgroups only when the tile grid is under one workgroup per
+// CU and every problem brought scratch for it
+template <int BM, int BN, int NW, int D, int KMAP = 0>
+static void launch_wk(GemmBatch& gb, int count, hipStream_t s, int target = 256) {
+  int maxt = 0, tot = 0, nkb = 1 << 30;
+  long long maxMN = 0;
+  bool ws = true;
+  for (int i = 0; i < count; ++i) {
+    const GemmArgs& g = gb.p[i];
+    const int t = dr_cdiv(g.M, BM) * dr_cdiv(g.N, BN);
+    maxt = std::max(maxt, t);
+    tot += t;
+    nkb = std::min(nkb, dr_cdiv(g.K, 32));
+    maxMN = std::max(maxMN, (long long)g.M * g.N);
+    ws = ws && g.splitk_ws != nullptr;
+  }
+  if (maxt == 0) return;
+  int splits = 1;
+  if (ws && tot < target) {
+    splits = std::max(1, std::min(DR_TILE_SPLITS, dr_cdiv(target, tot)));
+    splits = std::min(splits, std::max(1, nkb / (2 * NW)));  // at least 2 blocks per wave
+    for (int i = 0; i < count; ++i)
+      while (splits > 1 && (long long)splits * gb.p[i].M * gb.p[i].N > gb.p[i].splitk_floats) --splits;
+  }
+  hipLaunchKernelGGL((k_gemm_wk<BM, BN, NW, D, KMAP>), dim3(dr_xcd_grid(maxt), splits, count), dim3(64 * NW), 0, s, gb,
+                     splits);
+  if (splits > 1)
+    hipLaunchKernelGGL(k_splitk_finish, dim3((unsigned)((maxMN + 255) / 256), 1, count), dim3(256), 0, s, gb, splits);
+}
+
 // every problem bf16 and 16-byte-aligned 8-wide k runs (ksplitA on an 8 boundary)
 static bool b16_ok(const GemmBatch& gb, int count) {
   for (int i = 0; i < count; ++i) {
@@ -2090,16 +2288,44 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
     // tiles, which re-read the weights per row tile and the activations per
     // 16 columns: 44 -> 32 us (BPTT, 2 problems), 23 -> 15 us (heads, 3
     // problems, split-K 4), profiles/r02h_kbench_tile_B256.txt
-    if (!A_KM && !B_KN && maxM >= 128 && maxM <= 512) {
+    if (!A_KM && !B_KN && maxM >= 128 && maxM <= 512 && g_tile_variant != 26) {
       int tiles32 = 0;
       for (int i = 0; i < count; ++i) tiles32 += dr_cdiv(gb.p[i].M, 32) * dr_cdiv(gb.p[i].N, 32);
+      // (f32 under ~112 tiles -- one per-step Linear of 200 outputs, K = 1624 --
+      // the 16-row skinny tiles spread wider: 8.4 against 13.0 us)
       if ((g_tile_variant == 0 || g_tile_variant >= 8) && maxM <= 512 &&
-          (minK >= 1024 || (minK >= 512 && tiles32 >= 256))) {
+          ((minK >= 1024 && (tiles32 >= 112 || g_tile_variant != 0 || b16_ok(gb, count))) ||
+           (minK >= 512 && tiles32 >= 256))) {
         GemmBatch gt = gb;
         if (tiles32 >= 256)
           for (int i = 0; i < count; ++i) gt.p[i].splitk_ws = nullptr;
+        // f32: the wave-K kernel (32 x 32 tiles, 4 waves, no split-K: heads
+        // 15.8 -> 13.0 us, BPTT 32.2 -> 25.7, GRU hidden product 13.3 -> 12.3,
+        // profiles/r03g_kbench_wk.txt); the LDS tile kernel stays for the
+        // shapes the wave-K kernel does not take (and as kbench variant 25)
         if (b16_ok(gb, count)) launch_tile_b16<32, 32, 4>(gt, count, s);
-        else if (g_tile_variant == 8) launch_tile2<32, 64, 64, false, false, 4>(gt, count, s);
+        else if (g_tile_variant == 0 && wk_ok(gb, count)) launch_wk<32, 32, 4, 2, 1>(gt, count, s, 0);
+        else if (g_tile_variant >= 12 && g_tile_variant < 25 && wk_ok(gb, count)) {
+          GemmBatch gw = gb;  // (split-K scratch kept: launch_wk splits only under 256 tiles)
+          switch (g_tile_variant) {
+            case 12: launch_wk<32, 32, 4, 4>(gw, count, s); break;
+            case 13: launch_wk<32, 32, 8, 4>(gw, count, s); break;
+            case 14: launch_wk<64, 32, 8, 3>(gw, count, s); break;
+            case 15: launch_wk<32, 64, 8, 3>(gw, count, s); break;
+            case 16: launch_wk<32, 32, 4, 4, 1>(gw, count, s); break;
+            case 18: launch_wk<32, 32, 4, 2>(gw, count, s); break;
+            case 19: launch_wk<32, 32, 4, 2, 1>(gw, count, s); break;
+            case 20: launch_wk<32, 32, 8, 2, 1>(gw, count, s); break;
+            case 21: launch_wk<64, 64, 4, 2, 1>(gw, count, s, g_tile_wgs); break;
+            case 22: launch_wk<64, 32, 4, 2, 1>(gw, count, s, g_tile_wgs); break;
+            case 23: launch_wk<32, 64, 4, 2, 1>(gw, count, s, g_tile_wgs); break;
+            case 24: launch_wk<64, 64, 8, 2, 1>(gw, count, s, g_tile_wgs); break;
+            default:
+              if (tiles32 >= 256) launch_wk<32, 32, 4, 4>(gw, count, s);
+              else launch_wk<32, 32, 8, 4>(gw, count, s);
+              break;
+          }
+        } else if (g_tile_variant == 8) launch_tile2<32, 64, 64, false, false, 4>(gt, count, s);
         else if (g_tile_variant == 9) launch_tile2<64, 32, 64, false, false, 4>(gt, count, s);
         else if (g_tile_variant == 10) launch_tile2<64, 64, 64, false, false, 4>(gt, count, s);
         else if (g_tile_variant == 11) launch_tile2<32, 64, 32, false, false, 4>(gt, count, s);
@@ -2110,7 +2336,8 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
     // weight gradients (TN) and tall, deep products go to the tile kernel --
     // when it can fill the chip: a per-step product at B = 256 (16 tiles of
     // 64 x 64, no split-K scratch) runs on 52+ skinny 64-row workgroups instead
-    if (A_KM || (maxM >= 256 && minK >= 512 && (ws || tiles >= 128)) || (g_tile_variant >= 4 && maxM >= 128)) {
+    if (A_KM || (maxM >= 256 && minK >= 512 && (ws || tiles >= 128) && g_tile_variant != 26) ||
+        (g_tile_variant >= 4 && g_tile_variant < 26 && maxM >= 128)) {
       GemmBatch gt = gb;
       // tall NT products with a deep K (the encoder feature projection, the
       // critic's first layer over B*(H+1) rows): 8 waves as 4 x 2 over 64 x 64

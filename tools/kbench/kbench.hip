@@ -409,10 +409,51 @@ int main(int argc, char** argv) {
   // tile variants, without and with split-K scratch
   {
     float* skw = frand((size_t)8 * 256 * 2048);
-    for (int var : {0, 4, 5, 6, 7, 8, 9, 10, 11}) {
+    // correctness of the wave-K variants against variant 0 (same inputs, own outputs)
+    if (!g_filter || strstr("tv check", g_filter) || strstr(g_filter, "tv")) {
+      float* Yc = frand((size_t)3 * B * 2048);
+      auto run_shapes = [&](int var, std::vector<float>& out) {
+        dr_debug_tile_variant(var);
+        CK(hipMemset(Yc, 0, (size_t)3 * B * 2048 * 4));
+        GemmArgs a = nt_(B, 1027, 1800), b = nt_(B, 600, 1800);
+        a.Y = Yc; a.ldy = 1027; b.Y = Yc + (size_t)B * 1027; b.ldy = 600;
+        GemmArgs p2[2] = {a, b};
+        gemm_launch(G_NT, AM_PLAIN, p2, 2, s);
+        GemmArgs h3[3];
+        for (int i = 0; i < 3; ++i) {
+          h3[i] = nt_(B, 200, 1624);
+          h3[i].A = X; h3[i].lda = 600; h3[i].ksplitA = 600; h3[i].A2 = X + 700000; h3[i].lda2 = 1024;
+          h3[i].W = W + 100 * i; h3[i].Y = Yc + (size_t)B * 1627 + (size_t)B * 200 * i; h3[i].ldy = 200;
+          h3[i].splitk_ws = skw + (size_t)i * 1024 * 1024; h3[i].splitk_floats = 1024LL * 1024;
+        }
+        gemm_launch(G_NT, AM_PLAIN, h3, 3, s);
+        GemmArgs gg = nt_(B, 1800, 600);
+        gg.Y = Yc + (size_t)B * 2227; gg.ldy = 1800;
+        gemm_launch(G_NT, AM_PLAIN, &gg, 1, s);
+        CK(hipStreamSynchronize(s));
+        out.resize((size_t)B * 4027);
+        CK(hipMemcpy(out.data(), Yc, out.size() * 4, hipMemcpyDeviceToHost));
+      };
+      std::vector<float> ref, got;
+      run_shapes(0, ref);
+      for (int var : {19, 25}) {
+        run_shapes(var, got);
+        const size_t cut[4] = {0, (size_t)B * 1627, (size_t)B * 2227, (size_t)B * 4027};
+        for (int rg = 0; rg < 3; ++rg) {
+          double md = 0, mr = 0;
+          for (size_t i = cut[rg]; i < cut[rg + 1]; ++i) {
+            md = std::max(md, (double)fabsf(got[i] - ref[i]));
+            mr = std::max(mr, (double)fabsf(ref[i]));
+          }
+          printf("tv%d check vs tv0 (%s): max|d| %.3e (max|ref| %.3e)\n", var, rg == 0 ? "BPTT" : rg == 1 ? "heads" : "GRU", md, mr);
+        }
+      }
+      dr_debug_tile_variant(0);
+    }
+    for (int var : {0, 13, 20, 25, 26}) {
       dr_debug_tile_variant(var);
       for (int sk = 0; sk < 2; ++sk) {
-        if ((var == 0 || var >= 8) && sk) continue;
+        if ((var >= 8 && var < 12) && sk) continue;
         auto prep = [&](GemmArgs g) {
           if (sk) { g.splitk_ws = skw; g.splitk_floats = 8LL * 256 * 2048; }
           return g;
@@ -426,6 +467,9 @@ int main(int argc, char** argv) {
         GemmArgs s3 = prep(nt_(B, 1800, 600));
         snprintf(buf, sizeof buf, "tv%d%s GRU gh N1800 K600", var, sk ? " sk" : "");
         timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, &s3, 1, st); }, s);
+        GemmArgs s5 = prep(nt_(B, 200, 1624));
+        snprintf(buf, sizeof buf, "tv%d%s actor L1 1x N200 K1624", var, sk ? " sk" : "");
+        timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, &s5, 1, st); }, s);
         GemmArgs s4 = prep(nt_(B, 200, 600));
         snprintf(buf, sizeof buf, "tv%d%s prior L1 N200 K600", var, sk ? " sk" : "");
         timeit(buf, [&](hipStream_t st) { gemm_launch(G_NT, AM_PLAIN, &s4, 1, st); }, s);
