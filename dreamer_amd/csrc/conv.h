@@ -30,6 +30,10 @@ bool op_conv_split3_supported(int n, int cin, int ih, int iw, int cout);
 // k4 s2 p1 conv + bias + SiLU, f32 NHWC in -> f32 NHWC (or NCHW) out, as op_conv_nhwc
 int op_conv_split3(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
                    float* out, int out_nchw, hipStream_t s);
+// with the world-model step's epilogues (as op_conv_nhwc_ex): CONV_EPI_FWD +
+// optional pre = acc + bias (NHWC), or CONV_EPI_DSILU: out = acc * SiLU'(pre)
+int op_conv_split3_ex(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
+                      float* out, int out_nchw, float* pre, int epi, hipStream_t s);
 
 // ---- conv_bf16.hip (bf16 perf mode; activations bf16, accumulation f32) ----
 // weights: Conv2d [co][ci][4][4] f32 -> bf16 [co][tap][cin_pad]; matrix slice -> bf16 [rows][cols]
@@ -87,6 +91,12 @@ int op_convT_mse_parts(int h, int w);  // partial sums per frame written by CT_E
 int op_convT_out3_repack(int cin, const float* wt, float* wq, hipStream_t s);
 // the same direct kernel; target == NULL: mu = tanh(acc + bias) written NCHW [n][3][2h][2w]
 int op_convT_out3(const ConvTArgs& a, hipStream_t s);
+// conv_split.hip: the same upsampling conv f32-accurate on the bf16 MFMA (3-term
+// split) for CT_EPI_BIAS / CT_EPI_DSILU, NHWC out with ldc == cout, no silu_in;
+// wr = op_convT_repack_split3(wt) scratch, 6 bytes per weight
+int op_convT_repack_split3(int cin, int cout, const float* wt, void* wr, hipStream_t s);
+bool op_convT_split3_supported(int n, int cin, int h, int w, int cout);
+int op_convT_split3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s);
 
 // Weight gradient of a k4 s2 p1 (transposed) convolution:
 //   dW[a][b][ky][kx] (+)= scale * sum_{f,y,x} lo[f][y][x][a] * hi[f][2y-1+ky][2x-1+kx][b]
@@ -95,6 +105,16 @@ int op_convT_out3(const ConvTArgs& a, hipStream_t s);
 // ConvTranspose2d: lo = input, hi = output gradient -> dW [cin][cout][4][4].
 // lo_silu: lo holds pre-activations, SiLU is applied on load.
 size_t op_conv_wgrad_ws_floats(int n, int h, int w, int ca, int cb);
+// the ordered partial-plane reduction of both weight-gradient kernels
+int op_wgrad_reduce(int ca, int cb, int cbo, int nsplit, const float* part, float* dw, float scale, int accumulate,
+                    hipStream_t s);
+// conv_split.hip: the same weight gradient f32-accurate on the bf16 MFMA (both
+// operands split3 while staged); ca in {64, 128, 256}, cb % 8 == 0, h and w
+// powers of two, lo without SiLU on load
+bool op_wgrad_split3_supported(int n, int h, int w, int ca, int cb);
+size_t op_wgrad_split3_ws_floats(int n, int h, int w, int ca, int cb);
+int op_wgrad_split3(int n, int h, int w, int ca, int cb, const float* lo, int lda, const float* hi, int ldb,
+                    float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s);
 // dW has cbo <= cb channels per row (cbo < cb when hi carries zero padding channels).
 int op_conv_wgrad(int n, int h, int w, int ca, int cb, const float* lo, int lda, int lo_silu, const float* hi, int ldb,
                   float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s);

@@ -59,10 +59,15 @@ __device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsign
 __device__ __forceinline__ int swz(int row) { return (0x1320 >> (((row >> 2) & 3) * 4)) & 3; }
 }  // namespace
 
-template <int BM, int BN, int CIN, bool OUT_NCHW, int PIPE>
+// EPI (conv.h): CONV_EPI_FWD: out = SiLU(acc + bias), optionally pre = acc + bias
+// (NHWC, for the world-model backward); CONV_EPI_DSILU (NHWC only, no bias):
+// out = acc * SiLU'(pre) -- the input gradient of a transposed conv followed by
+// the SiLU backward of the layer below (WorldModel.training_step's decoder)
+template <int BM, int BN, int CIN, bool OUT_NCHW, int PIPE, int EPI = CONV_EPI_FWD>
 __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, int iw, int cout,
                                                          const float* __restrict__ in, const u16* __restrict__ wr,
-                                                         const float* __restrict__ bias, float* __restrict__ out) {
+                                                         const float* __restrict__ bias, float* __restrict__ out,
+                                                         float* __restrict__ pre) {
   constexpr int NT = BM * 2;         // WM = BM / 64 waves over pixels x 2 waves over channels
   constexpr int K = CIN * 16;
   constexpr int NCH = K / 32;
@@ -230,6 +235,10 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
         if (m >= M) continue;
         const float bv = bias[co];
         f32x4 v = acc[i][j] + bv;
+        if (pre) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pre[(m + e) * cout + co] = v[e];
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(v[e]);
         const long long f = m / hw;
@@ -238,11 +247,18 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
         const long long m = m0 + wm0 + 16 * i + r;
         const int co = n0 + wn0 + 16 * j + 4 * q;
         if (m >= M) continue;
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + co);
         f32x4 v;
+        if (EPI == CONV_EPI_DSILU) {
+          const f32x4 pv = *reinterpret_cast<const f32x4*>(pre + m * cout + co);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = dr_silu_fast(acc[i][j][e] + bv[e]);
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * dr_dsilu(pv[e]);
+        } else {
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + co);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
+          if (pre) *reinterpret_cast<f32x4*>(pre + m * cout + co) = v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(v[e]);
         }
         *reinterpret_cast<f32x4*>(out + m * cout + co) = v;
       }
@@ -519,17 +535,17 @@ int op_enc12_split3(int n, int nb, int h, int w, int c1, int c2, const dr_frames
   return dr_check_launch("enc12_split3");
 }
 
-template <int BM, int BN, int CIN, bool NCHW, int PIPE>
+template <int BM, int BN, int CIN, bool NCHW, int PIPE, int EPI = CONV_EPI_FWD>
 static int launch_s3(int n, int ih, int iw, int cout, const float* in, const void* wr, const float* bias, float* out,
-                     hipStream_t s) {
+                     float* pre, hipStream_t s) {
   const long long M = (long long)n * (ih / 2) * (iw / 2);
   const long long tiles = ((M + BM - 1) / BM) * (cout / BN);
   if (tiles >= (1LL << 30)) {
     dr_set_error("conv_split3: too many tiles");
     return DR_E_INVALID;
   }
-  hipLaunchKernelGGL((k_conv_split3<BM, BN, CIN, NCHW, PIPE>), dim3((unsigned)dr_xcd_grid((int)tiles)), dim3(BM * 2), 0,
-                     s, n, ih, iw, cout, in, (const u16*)wr, bias, out);
+  hipLaunchKernelGGL((k_conv_split3<BM, BN, CIN, NCHW, PIPE, EPI>), dim3((unsigned)dr_xcd_grid((int)tiles)),
+                     dim3(BM * 2), 0, s, n, ih, iw, cout, in, (const u16*)wr, bias, out, pre);
   return dr_check_launch("conv_split3");
 }
 
@@ -539,28 +555,481 @@ bool op_conv_split3_supported(int n, int cin, int ih, int iw, int cout) {
          (long long)n * ih * iw * cin < (1LL << 31) - (1LL << 20);
 }
 
-int op_conv_split3(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
-                   float* out, int out_nchw, hipStream_t s) {
+int op_conv_split3_ex(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
+                      float* out, int out_nchw, float* pre, int epi, hipStream_t s) {
   if (!op_conv_split3_supported(n, cin, ih, iw, cout)) {
     dr_set_error("conv_split3: unsupported shape (cin=%d ih=%d iw=%d cout=%d)", cin, ih, iw, cout);
+    return DR_E_INVALID;
+  }
+  if (epi == CONV_EPI_DSILU && (out_nchw || !pre)) {
+    dr_set_error("conv_split3: the SiLU-backward epilogue needs NHWC output and a pre-activation tensor");
     return DR_E_INVALID;
   }
   // measured at 8192 frames (tools/conv_ab.py): 256 x 64 tiles
   // for 64 output channels (980 us; 128 x 64 at two workgroups per CU: 1004),
   // 256 x 128 for 128 / 256 channels (709 / 658 us; 128 x 128: ~1.1 ms): the
   // weights are re-read once per pixel tile, so taller tiles pay
+#define DR_S3E(BN, C, NCHW)                                                                                   \
+  (epi == CONV_EPI_DSILU ? launch_s3<256, BN, C, NCHW, 2, CONV_EPI_DSILU>(n, ih, iw, cout, in, wr, bias, out, pre, s) \
+                         : launch_s3<256, BN, C, NCHW, 2, CONV_EPI_FWD>(n, ih, iw, cout, in, wr, bias, out, pre, s))
 #define DR_S3L(C)                                                                                          \
   if (cin == C) {                                                                                          \
     if (cout % 128 == 0)                                                                                   \
-      return out_nchw ? launch_s3<256, 128, C, true, 2>(n, ih, iw, cout, in, wr, bias, out, s)            \
-                      : launch_s3<256, 128, C, false, 2>(n, ih, iw, cout, in, wr, bias, out, s);          \
-    return out_nchw ? launch_s3<256, 64, C, true, 2>(n, ih, iw, cout, in, wr, bias, out, s)               \
-                    : launch_s3<256, 64, C, false, 2>(n, ih, iw, cout, in, wr, bias, out, s);             \
+      return out_nchw ? launch_s3<256, 128, C, true, 2>(n, ih, iw, cout, in, wr, bias, out, pre, s)       \
+                      : DR_S3E(128, C, false);                                                             \
+    return out_nchw ? launch_s3<256, 64, C, true, 2>(n, ih, iw, cout, in, wr, bias, out, pre, s)          \
+                    : DR_S3E(64, C, false);                                                                \
   }
   DR_S3L(32)
   DR_S3L(64)
   DR_S3L(128)
   DR_S3L(256)
 #undef DR_S3L
+#undef DR_S3E
   return DR_E_INVALID;
+}
+
+int op_conv_split3(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
+                   float* out, int out_nchw, hipStream_t s) {
+  return op_conv_split3_ex(n, cin, ih, iw, cout, in, wr, bias, out, out_nchw, nullptr, CONV_EPI_FWD, s);
+}
+
+// ---------------------------------------------------------------------------
+// Upsampling k4 s2 p1 (ConvTranspose2d of the decoder, VAE.py:128-137, and the
+// data gradient of an encoder Conv2d), f32-accurate on the bf16 MFMA: the
+// implicit GEMM of wmconv.hip's k_convT_nhwc -- per output parity class
+// (py, px) a dense K = 4 taps x CIN, tap (dy, dx): input (y + py - dy,
+// x + px - dx), kernel (1 - py + 2 dy, 1 - px + 2 dx) -- with the operands of
+// k_conv_split3: activations split3 as they are staged (truncation split,
+// v_perm packing, swizzled 64-byte plane rows), weights split once per call
+// into [class][K/32][3 planes][cout][32].  Epilogues of the world-model step
+// (NHWC out, ldc == cout): CT_EPI_BIAS (out = acc + bias, out2 / silu_out =
+// SiLU) and CT_EPI_DSILU (out = acc * SiLU'(pre)).
+// ---------------------------------------------------------------------------
+template <int BM, int BN, int CIN, int EPI>
+__global__ __launch_bounds__(BM * 2) void k_convT_split3(ConvTArgs a, const u16* __restrict__ wr) {
+  constexpr int NT = BM * 2;
+  constexpr int K = CIN * 4;
+  constexpr int NCH = K / 32;
+  constexpr int WTN = BN / 2, FM = 4, FN = WTN / 16;
+  constexpr int APT = BM * 8 / NT;
+  constexpr int BU = 3 * BN * 4;
+  constexpr int BPT = (BU + NT - 1) / NT;
+  static_assert(CIN % 32 == 0 && APT == 4 && FN >= 1 && NCH % 2 == 0, "convT_split3 tile");
+  __shared__ __attribute__((aligned(16))) u32x4 As[2][3][BM][4];
+  __shared__ __attribute__((aligned(16))) u32x4 Bs[2][3][BN][4];
+
+  const int h = a.h, w = a.w, hw = h * w, cout = a.cout;
+  const long long M = (long long)a.n * hw;  // input-resolution pixels of one parity class
+  const int tiles_n = cout / BN;
+  const long long tiles_m = (M + BM - 1) / BM;
+  const int lt = dr_xcd_tile(blockIdx.x, (int)(4 * tiles_m * tiles_n));
+  if (lt < 0) return;
+  const int cls = (int)(lt / (tiles_m * tiles_n));
+  const long long rem = lt - (long long)cls * tiles_m * tiles_n;
+  const long long m0 = (rem / tiles_n) * BM;
+  const int n0 = (int)(rem % tiles_n) * BN;
+  const int py = cls >> 1, px = cls & 1;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
+  const int quad = tid & 7, prow = tid >> 3;
+  const float* __restrict__ in = a.in;
+  const u16* __restrict__ wc = wr + (long long)cls * NCH * 3 * cout * 32;
+
+  // per A row: element offset of input pixel (y, x) (32-bit: n h w CIN < 2^31,
+  // host-checked) and the valid taps (bit dy * 2 + dx); rows past M: none
+  int pb[APT];
+  unsigned vm[APT];
+#pragma unroll
+  for (int i = 0; i < APT; ++i) {
+    const long long m = m0 + prow + (NT / 8) * i;
+    const int mm = (int)(m < M ? m : 0);
+    const int f = mm / hw, p = mm - f * hw, y = p / w, x = p - y * w;
+    pb[i] = ((f * h + y) * w + x) * CIN;
+    unsigned v = 0u;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int iy = y + py - (t >> 1), ix = x + px - (t & 1);
+      v |= (iy >= 0 && iy < h && ix >= 0 && ix < w) ? (1u << t) : 0u;
+    }
+    vm[i] = m < M ? v : 0u;
+  }
+
+  f32x4 ra0[APT], ra1[APT];
+  u32x4 rb0[BPT], rb1[BPT];
+  unsigned ok0 = 0, ok1 = 0;
+  auto load = [&](int c, auto slot) __attribute__((always_inline)) {
+    f32x4* ra = decltype(slot)::value == 0 ? ra0 : ra1;
+    unsigned& okm = decltype(slot)::value == 0 ? ok0 : ok1;
+    u32x4* rb = decltype(slot)::value == 0 ? rb0 : rb1;
+    const int tap = (32 * c) / CIN, ci0 = 32 * c - tap * CIN;
+    const int toff = ((py - (tap >> 1)) * w + (px - (tap & 1))) * CIN + ci0 + 4 * quad;
+    unsigned om = 0u;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const bool ok = (vm[i] >> tap) & 1u;
+      ra[i] = *reinterpret_cast<const f32x4*>(in + (ok ? pb[i] + toff : 0));
+      om |= ok ? (1u << i) : 0u;
+    }
+    okm = om;
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      const int e = tid + NT * j;
+      if (BU % NT == 0 || e < BU) {
+        const int pl = e / (BN * 4), rm = e - pl * BN * 4, row = rm >> 2, u = rm & 3;
+        rb[j] = *reinterpret_cast<const u32x4*>(wc + (((long long)c * 3 + pl) * cout + n0 + row) * 32 + 8 * u);
+      }
+    }
+  };
+  auto store = [&](auto slot, int buf) __attribute__((always_inline)) {
+    const f32x4* ra = decltype(slot)::value == 0 ? ra0 : ra1;
+    const u32x4* rb = decltype(slot)::value == 0 ? rb0 : rb1;
+    const unsigned okm = decltype(slot)::value == 0 ? ok0 : ok1;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const int row = prow + (NT / 8) * i;
+      const f32x4 v = (okm >> i) & 1u ? ra[i] : (f32x4){0.f, 0.f, 0.f, 0.f};
+      unsigned h0, m0_, l0, h1, m1, l1;
+      split3_pair(v[0], v[1], h0, m0_, l0);
+      split3_pair(v[2], v[3], h1, m1, l1);
+      const int unit = (quad >> 1) ^ swz(row), half = quad & 1;
+      reinterpret_cast<u32x2*>(&As[buf][0][row][unit])[half] = (u32x2){h0, h1};
+      reinterpret_cast<u32x2*>(&As[buf][1][row][unit])[half] = (u32x2){m0_, m1};
+      reinterpret_cast<u32x2*>(&As[buf][2][row][unit])[half] = (u32x2){l0, l1};
+    }
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      const int e = tid + NT * j;
+      if (BU % NT == 0 || e < BU) {
+        const int pl = e / (BN * 4), rm = e - pl * BN * 4, row = rm >> 2, u = rm & 3;
+        Bs[buf][pl][row][u ^ swz(row)] = rb[j];
+      }
+    }
+  };
+
+  const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * WTN;
+  const int fu = q ^ swz(r);
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  load(0, S0{});
+  load(1, S1{});
+  store(S0{}, 0);
+  __syncthreads();
+  auto step = [&](int c, auto slot) __attribute__((always_inline)) {
+    constexpr int SL = decltype(slot)::value;
+    using Next = std::integral_constant<int, 1 - SL>;
+    const int buf = c & 1;
+    load(min(c + 2, NCH - 1), slot);
+    u32x4 av[3][FM], bv[3][FN];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) av[pl][i] = As[buf][pl][wm0 + 16 * i + r][fu];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bv[pl][j] = Bs[buf][pl][wn0 + 16 * j + r][fu];
+    }
+    // weights as the MFMA A operand (lane: 4 consecutive channels of one pixel)
+#define DR_T3(PA, PB)                                                                                   \
+  _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
+      mfma_b16(bv[PB][j], av[PA][i], acc[i][j]);
+    DR_T3(2, 0)
+    DR_T3(1, 1)
+    DR_T3(0, 2)
+    DR_T3(1, 0)
+    DR_T3(0, 1)
+    DR_T3(0, 0)
+#undef DR_T3
+    if (c + 1 < NCH) store(Next{}, buf ^ 1);
+    dr_lds_barrier();
+  };
+  for (int c = 0; c < NCH; c += 2) {
+    step(c, S0{});
+    step(c + 1, S1{});
+  }
+
+  const int OW = 2 * w, OH = 2 * h;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const long long m = m0 + wm0 + 16 * i + r;
+    if (m >= M) continue;
+    const int f = (int)(m / hw), p = (int)(m - (long long)f * hw), y = p / w, x = p - y * w;
+    const long long opix = ((long long)f * OH + 2 * y + py) * OW + 2 * x + px;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int co = n0 + wn0 + 16 * j + 4 * q;
+      f32x4 v = acc[i][j];
+      if (EPI == CT_EPI_BIAS) {
+        v += *reinterpret_cast<const f32x4*>(a.bias + co);
+        f32x4 sv = v;
+        if (a.out2 || a.silu_out) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sv[e] = dr_silu(v[e]);
+        }
+        *reinterpret_cast<f32x4*>(a.out + opix * cout + co) = a.silu_out ? sv : v;
+        if (a.out2) *reinterpret_cast<f32x4*>(a.out2 + opix * cout + co) = sv;
+      } else {
+        const f32x4 pv = *reinterpret_cast<const f32x4*>(a.pre + opix * cout + co);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] * dr_dsilu(pv[e]);
+        *reinterpret_cast<f32x4*>(a.out + opix * cout + co) = v;
+      }
+    }
+  }
+}
+
+// ConvTranspose2d weight [cin][cout][4][4] (or a Conv2d weight [co][ci][4][4]
+// read as [cin = co][cout = ci]) -> bf16 [class][K/32][3 planes][cout][32],
+// k = tap * cin + ci, tap = dy * 2 + dx
+__global__ void k_convT_repack_split3(int cin, int cout, const float* __restrict__ wt, u16* __restrict__ wr) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int K = 4 * cin;
+  if (i >= 4 * cout * K) return;
+  const int cls = i / (cout * K), rm = i - cls * cout * K, co = rm / K, k = rm - co * K;
+  const int tap = k / cin, ci = k - tap * cin;
+  const int py = cls >> 1, px = cls & 1, ky = 1 - py + 2 * (tap >> 1), kx = 1 - px + 2 * (tap & 1);
+  unsigned hh, mm, ll;
+  split3(wt[(((long long)ci * cout + co) * 4 + ky) * 4 + kx], hh, mm, ll);
+  const long long plane = (long long)cout * 32;
+  const long long base = (((long long)cls * (K / 32) + (k >> 5)) * 3 * cout + co) * 32 + (k & 31);
+  wr[base] = (u16)hh;
+  wr[base + plane] = (u16)mm;
+  wr[base + 2 * plane] = (u16)ll;
+}
+
+int op_convT_repack_split3(int cin, int cout, const float* wt, void* wr, hipStream_t s) {
+  const int total = 16 * cout * cin;
+  hipLaunchKernelGGL(k_convT_repack_split3, dim3((total + 255) / 256), dim3(256), 0, s, cin, cout, wt, (u16*)wr);
+  return dr_check_launch("convT_repack_split3");
+}
+
+// cout >= 64: at 32 output channels the 256 x 32 tile's split of the staged
+// activations outweighs its 24 MFMAs per wave and chunk (975 / 887 us against
+// 991 / 900 us on the f32 MFMA, WM step B = 256 T = 15, profiles/r03i_wm_step_kernels.txt)
+bool op_convT_split3_supported(int n, int cin, int h, int w, int cout) {
+  const bool cin_ok = cin == 32 || cin == 64 || cin == 128 || cin == 256;
+  return cin_ok && cout % 64 == 0 && (long long)n * h * w * cin < (1LL << 31) - (1LL << 20) &&
+         4LL * (((long long)n * h * w + 255) / 256) * (cout / 32) < (1LL << 30);
+}
+
+template <int BN, int C, int EPI>
+static int launch_t3(const ConvTArgs& a, const void* wr, hipStream_t s) {
+  const long long tiles = 4 * (((long long)a.n * a.h * a.w + 255) / 256) * (a.cout / BN);
+  hipLaunchKernelGGL((k_convT_split3<256, BN, C, EPI>), dim3((unsigned)dr_xcd_grid((int)tiles)), dim3(512), 0, s, a,
+                     (const u16*)wr);
+  return dr_check_launch("convT_split3");
+}
+
+int op_convT_split3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s) {
+  if (!op_convT_split3_supported(a.n, a.cin, a.h, a.w, a.cout) || a.silu_in || a.ldc != a.cout ||
+      (epi != CT_EPI_BIAS && epi != CT_EPI_DSILU) || (epi == CT_EPI_DSILU && !a.pre) ||
+      (epi == CT_EPI_BIAS && !a.bias)) {
+    dr_set_error("convT_split3: unsupported problem (cin=%d cout=%d h=%d w=%d epi=%d)", a.cin, a.cout, a.h, a.w, epi);
+    return DR_E_INVALID;
+  }
+#define DR_T3E(BN, C) \
+  (epi == CT_EPI_DSILU ? launch_t3<BN, C, CT_EPI_DSILU>(a, wr, s) : launch_t3<BN, C, CT_EPI_BIAS>(a, wr, s))
+#define DR_T3L(C)                                         \
+  if (a.cin == C) {                                       \
+    if (a.cout % 128 == 0) return DR_T3E(128, C);         \
+    return DR_T3E(64, C);                                 \
+  }
+  DR_T3L(32)
+  DR_T3L(64)
+  DR_T3L(128)
+  DR_T3L(256)
+#undef DR_T3L
+#undef DR_T3E
+  return DR_E_INVALID;
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradient of a k4 s2 p1 (transposed) convolution, f32-accurate on the
+// bf16 MFMA (the k_conv_wgrad GEMM of wmconv.hip: [ca] x [16 cb] over K = the
+// low-resolution pixels, column n = tap * cb + b).  Both operands are
+// activations, so both are split3 while they are staged: a thread stages one
+// unit of 8 consecutive pixels x 4 channels (8 float4 loads), splits the 4
+// pixel pairs of each channel and writes one 16-byte unit per channel and
+// plane -- the transpose to the [channel][pixel] rows the MFMA fragments read
+// happens in registers.  Rows of 64 pixels (8 units) are padded to 9 units:
+// the 16 rows of a fragment read fall on distinct bank quads.  One LDS buffer
+// (the next chunk's loads are in flight in registers meanwhile), 8 waves as
+// 2 (a) x 4 (n), partial planes per pixel split reduced by k_wgrad_reduce.
+// Low-resolution sizes are powers of two (shift addressing).
+// ---------------------------------------------------------------------------
+template <int BM>
+__global__ __launch_bounds__(512) void k_wgrad_split3(int n, int lh, int lw, int ca, int cb,
+                                                      const float* __restrict__ lo, int lda,
+                                                      const float* __restrict__ hi, int ldb, int chunk,
+                                                      float* __restrict__ part) {
+  constexpr int BN = 128, KC = 64, RP = KC / 8 + 1;
+  constexpr int FM = BM / 32, FN = 2;  // wave tile (BM / 2) x 32
+  __shared__ __attribute__((aligned(16))) u32x4 S[3][BM + BN][RP];
+  const int N = 16 * cb;
+  const int tiles_n = N / BN, tiles = (ca / BM) * tiles_n;
+  const int split = blockIdx.x / tiles, lt = blockIdx.x - split * tiles;
+  const int m0 = (lt / tiles_n) * BM, n0 = (lt % tiles_n) * BN;
+  const int h = 1 << lh, w = 1 << lw, H2 = 2 * h, W2 = 2 * w;
+  const long long K = (long long)n * h * w;
+  const long long k_begin = (long long)split * chunk;
+  const long long k_end = k_begin + chunk < K ? k_begin + chunk : K;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
+
+  // staging unit of this thread: channel quad cq, pixel octet oct (A: rows of
+  // ca channels m0 + 4 cq; B: columns n0 + 4 cq, one tap, 4 channels)
+  constexpr int AU = BM / 4 * 8, BUn = BN / 4 * 8;
+  const bool isA = tid < AU, active = tid < AU + BUn;
+  const int u = isA ? tid : tid - AU, cq = u >> 3, oct = u & 7;
+  const int row0 = isA ? 4 * cq : BM + 4 * cq;
+  const int bn = n0 + 4 * cq, btap = bn / cb, bch = bn - btap * cb, bky = btap >> 2, bkx = btap & 3;
+  const float* __restrict__ abase = lo + m0 + 4 * cq;
+  f32x4 v[8];
+  auto load = [&](long long p0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const long long p = p0 + i;
+      bool ok = active && p < k_end;
+      long long off;
+      if (isA) {
+        off = p * lda;
+      } else {
+        const long long f = p >> (lw + lh);
+        const int y = (int)(p >> lw) & (h - 1), x = (int)p & (w - 1);
+        const int Y = 2 * y - 1 + bky, X = 2 * x - 1 + bkx;
+        ok = ok && Y >= 0 && Y < H2 && X >= 0 && X < W2;
+        off = ((f * H2 + Y) * W2 + X) * ldb + bch;
+      }
+      const f32x4 t = *reinterpret_cast<const f32x4*>((isA ? abase : hi) + (ok ? off : 0));
+      v[i] = ok ? t : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store = [&]() __attribute__((always_inline)) {
+    if (!active) return;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      u32x4 ph, pm, pl;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        unsigned hh, mm, ll;
+        split3_pair(v[2 * i][c], v[2 * i + 1][c], hh, mm, ll);
+        ph[i] = hh;
+        pm[i] = mm;
+        pl[i] = ll;
+      }
+      S[0][row0 + c][oct] = ph;
+      S[1][row0 + c][oct] = pm;
+      S[2][row0 + c][oct] = pl;
+    }
+  };
+
+  const int wm0 = (wave >> 2) * (BM / 2), wn0 = (wave & 3) * 32;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const long long nch = k_end > k_begin ? (k_end - k_begin + KC - 1) / KC : 0;
+  if (nch > 0) {
+    load(k_begin + 8 * oct);
+    store();
+    __syncthreads();
+    for (long long c = 0; c < nch; ++c) {
+      // next chunk in flight (the last chunk reloads itself, unused)
+      load(k_begin + (c + 1 < nch ? c + 1 : c) * KC + 8 * oct);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        u32x4 av[3][FM], bv[3][FN];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) av[pl][i] = S[pl][wm0 + 16 * i + r][4 * ks + q];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) bv[pl][j] = S[pl][BM + wn0 + 16 * j + r][4 * ks + q];
+        }
+#define DR_W3(PA, PB)                                                                                   \
+  _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
+      mfma_b16(av[PA][i], bv[PB][j], acc[i][j]);
+        DR_W3(2, 0)
+        DR_W3(1, 1)
+        DR_W3(0, 2)
+        DR_W3(1, 0)
+        DR_W3(0, 1)
+        DR_W3(0, 0)
+#undef DR_W3
+      }
+      __syncthreads();
+      if (c + 1 < nch) {
+        store();
+        __syncthreads();
+      }
+    }
+  }
+  // lane (r, q) of acc[i][j]: a = 4 q + e of row block i, n = r of column block j
+  float* P = part + (long long)split * ca * N;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) P[(long long)(m0 + wm0 + 16 * i + 4 * q + e) * N + n0 + wn0 + 16 * j + r] = acc[i][j][e];
+}
+
+static int ilog2_exact(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return (1 << l) == v ? l : -1;
+}
+
+bool op_wgrad_split3_supported(int n, int h, int w, int ca, int cb) {
+  return (ca == 64 || ca == 128 || ca == 256) && cb % 8 == 0 && cb >= 8 && ilog2_exact(h) >= 0 && ilog2_exact(w) >= 0 &&
+         n > 0 && (long long)n * 4 * h * w * cb < (1LL << 31);
+}
+
+static void wgrad3_plan(int n, int h, int w, int ca, int cb, int& nsplit, int& chunk) {
+  const int bm = ca >= 128 ? 128 : 64;
+  const int tiles = (ca / bm) * (16 * cb / 128);
+  const long long K = (long long)n * h * w;
+  const long long kch = (K + 63) / 64;
+  long long ns = (512 + tiles - 1) / tiles;  // about 2 workgroups per CU
+  if (ns > (kch + 1) / 2) ns = (kch + 1) / 2;  // at least 2 chunks per split
+  if (ns < 1) ns = 1;
+  const long long ch = ((kch + ns - 1) / ns) * 64;
+  chunk = (int)ch;
+  nsplit = (int)((K + ch - 1) / ch);
+}
+
+size_t op_wgrad_split3_ws_floats(int n, int h, int w, int ca, int cb) {
+  int ns, ch;
+  wgrad3_plan(n, h, w, ca, cb, ns, ch);
+  return (size_t)ns * ca * 16 * cb;
+}
+
+int op_wgrad_split3(int n, int h, int w, int ca, int cb, const float* lo, int lda, const float* hi, int ldb,
+                    float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s) {
+  if (!op_wgrad_split3_supported(n, h, w, ca, cb) || lda % 4 || ldb % 4 || lda < ca || ldb < cb || cbo < 1 ||
+      cbo > cb || !lo || !hi || !dw || ((uintptr_t)lo & 15) || ((uintptr_t)hi & 15)) {
+    dr_set_error("wgrad_split3: unsupported problem (ca=%d cb=%d h=%d w=%d)", ca, cb, h, w);
+    return DR_E_INVALID;
+  }
+  int ns, ch;
+  wgrad3_plan(n, h, w, ca, cb, ns, ch);
+  if ((size_t)ns * ca * 16 * cb > ws_floats) {
+    dr_set_error("wgrad_split3: workspace too small");
+    return DR_E_WORKSPACE;
+  }
+  const int bm = ca >= 128 ? 128 : 64;
+  const int tiles = (ca / bm) * (16 * cb / 128);
+  const int lh = ilog2_exact(h), lw = ilog2_exact(w);
+  if (bm == 128)
+    hipLaunchKernelGGL(k_wgrad_split3<128>, dim3((unsigned)(tiles * ns)), dim3(512), 0, s, n, lh, lw, ca, cb, lo, lda,
+                       hi, ldb, ch, ws);
+  else
+    hipLaunchKernelGGL(k_wgrad_split3<64>, dim3((unsigned)(tiles * ns)), dim3(512), 0, s, n, lh, lw, ca, cb, lo, lda,
+                       hi, ldb, ch, ws);
+  DR_TRY(dr_check_launch("wgrad_split3"));
+  return op_wgrad_reduce(ca, cb, cbo, ns, ws, dw, scale, accumulate, s);
 }

@@ -296,6 +296,11 @@ struct WmWs {
   // vector mode: dq[0] = image_builder.0 pre, dq[1] = mu) and its SiLU dqp[k]; dgout = dL/d(pre-tanh output)
   float *du1, *dx1, *du2, *du2p, *dq[DR_MAX_DEPTH], *dqp[DR_MAX_DEPTH], *dgout, *w3p, *b3p;
   float *wqd[DR_MAX_DEPTH], *wrd[DR_MAX_DEPTH];
+  // split3 bf16 weight planes (conv_split.hip) of encoder conv k (forward) and
+  // of decoder convT k read as a Conv2d (its data gradient); NULL: f32 path
+  void *s3e[DR_MAX_DEPTH], *s3d[DR_MAX_DEPTH];
+  // ... and of decoder convT k (forward) / encoder conv k's data gradient as upsampling convs
+  void *t3d[DR_MAX_DEPTH], *t3e[DR_MAX_DEPTH];
   // loss
   float *coef_row, *coef_obs, *obs_part, *kl_grp, *rew_row, *cont_row, *scal, *stats;
   // backward
@@ -347,6 +352,42 @@ static WmDims wm_dims(const dr_dims* d, int B, int T) {
 static inline int enc_cin_st(const WmDims& D, int k) { return k == 0 ? 4 : D.e[k]; }
 static inline int dec_cout_st(const WmDims& D, int k) { return k == D.N - 1 ? 4 : D.cd[k + 1]; }
 
+// the convolutions that run f32-accurate on the bf16 MFMA (3-term split):
+// encoder conv k >= 1 (conv1's 4-channel input stays on the f32 MFMA) and the
+// data gradient of decoder convT k (a Conv2d from cout_t to cin_t channels)
+static inline bool enc_s3(const WmDims& D, int k) {
+  return !D.Dv && k >= 1 && op_conv_split3_supported(D.M, D.e[k], D.IH >> k, D.IW >> k, D.e[k + 1]);
+}
+static inline bool dec_s3(const WmDims& D, int k) {
+  const int lvl = D.N - 1 - k;  // convT k's output resolution level
+  return !D.Dv && dec_cout_st(D, k) == D.cd[k + 1] &&
+         op_conv_split3_supported(D.M1, D.cd[k + 1], D.IH >> lvl, D.IW >> lvl, D.cd[k]);
+}
+
+// upsampling convs on the split3 path: decoder convT k < N - 1 (forward;
+// the last, 3-channel layer runs k_convT_out3) and encoder conv k >= 1's data
+// gradient (an upsampling conv from e[k + 1] to e[k] channels)
+static inline bool dect_s3(const WmDims& D, int k) {
+  return !D.Dv && k < D.N - 1 && op_convT_split3_supported(D.M1, D.cd[k], D.IH >> (D.N - k), D.IW >> (D.N - k), D.cd[k + 1]);
+}
+static inline bool encg_s3(const WmDims& D, int k) {
+  return !D.Dv && k >= 1 && op_convT_split3_supported(D.M, D.e[k + 1], D.IH >> (k + 1), D.IW >> (k + 1), D.e[k]);
+}
+
+// conv / convT weight gradient: f32-accurate split3 kernel where the shape
+// allows (conv_split.hip), else the f32 MFMA kernel (wmconv.hip)
+static size_t wgrad_ws_floats(int n, int h, int w, int ca, int cb) {
+  size_t f = op_conv_wgrad_ws_floats(n, h, w, ca, cb);
+  if (op_wgrad_split3_supported(n, h, w, ca, cb)) f = std::max(f, op_wgrad_split3_ws_floats(n, h, w, ca, cb));
+  return f;
+}
+static int wgrad(int n, int h, int w, int ca, int cb, const float* lo, int lda, const float* hi, int ldb, float* dw,
+                 int cbo, float* ws, size_t ws_floats, hipStream_t s) {
+  if (op_wgrad_split3_supported(n, h, w, ca, cb))
+    return op_wgrad_split3(n, h, w, ca, cb, lo, lda, hi, ldb, dw, cbo, 1.0f, 0, ws, ws_floats, s);
+  return op_conv_wgrad(n, h, w, ca, cb, lo, lda, 0, hi, ldb, dw, cbo, 1.0f, 0, ws, ws_floats, s);
+}
+
 static void mlp_bwd_carve(Carve& c, long long M1, int w1, int w2, MlpBwd& b) {
   b.gx2 = c.f(M1 * w2); b.gp2 = c.f(M1 * w2); b.gy2 = c.f(M1 * w2); b.xh2 = c.f(M1 * w2);
   b.gx1 = c.f(M1 * w1); b.gp1 = c.f(M1 * w1); b.gy1 = c.f(M1 * w1); b.xh1 = c.f(M1 * w1);
@@ -359,10 +400,10 @@ static long long wm_conv_scratch(const WmDims& D) {
   auto mx = [&](long long v) { if (v > m) m = v; };
   for (int k = 0; k < N; ++k) {
     // encoder conv k: lo = output grad (res k + 1), hi = input; its bias sum
-    mx(op_conv_wgrad_ws_floats(n, D.IH >> (k + 1), D.IW >> (k + 1), D.e[k + 1], enc_cin_st(D, k)));
+    mx(wgrad_ws_floats(n, D.IH >> (k + 1), D.IW >> (k + 1), D.e[k + 1], enc_cin_st(D, k)));
     mx(op_chan_sum_ws_floats((long long)n * D.pix[k + 1], D.e[k + 1]));
     // decoder convT k: lo = input (res N - k), hi = output grad; its bias sum
-    mx(op_conv_wgrad_ws_floats(n1, D.IH >> (N - k), D.IW >> (N - k), D.cd[k], dec_cout_st(D, k)));
+    mx(wgrad_ws_floats(n1, D.IH >> (N - k), D.IW >> (N - k), D.cd[k], dec_cout_st(D, k)));
     mx(op_chan_sum_ws_floats((long long)n1 * D.pix[N - k - 1], D.cd[k + 1]));
   }
   return m;
@@ -417,6 +458,12 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
   for (int k = 0; k < N; ++k) {
     w.wqd[k] = c.f((long long)16 * D.cd[k] * D.cd[k + 1]);
     w.wrd[k] = c.f((long long)16 * D.cd[k] * dec_cout_st(D, k));
+  }
+  for (int k = 0; k < N; ++k) {  // 3 bf16 planes = 1.5 floats per weight
+    w.s3e[k] = enc_s3(D, k) ? c.f((3LL * 16 * D.e[k] * D.e[k + 1] + 1) / 2) : nullptr;
+    w.s3d[k] = dec_s3(D, k) ? c.f((3LL * 16 * D.cd[k] * D.cd[k + 1] + 1) / 2) : nullptr;
+    w.t3d[k] = dect_s3(D, k) ? c.f((3LL * 16 * D.cd[k] * D.cd[k + 1] + 1) / 2) : nullptr;
+    w.t3e[k] = encg_s3(D, k) ? c.f((3LL * 16 * D.e[k] * D.e[k + 1] + 1) / 2) : nullptr;
   }
   w.coef_row = c.f(M1); w.coef_obs = c.f(M1);
   w.obs_part = c.f(Dv ? M1 : M1 * op_convT_mse_parts(D.IH / 2, D.IW / 2));
@@ -541,6 +588,12 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     // ConvTranspose2d data gradient = strided Conv2d with the weight read as [out=ci][in=co]
     DR_TRY(op_conv_repack_pad(cin_t[k], cout_t[k], dec_cout_st(D, k), dec->convt[k].w, w.wrd[k], s));
   }
+  for (int k = 0; k < N; ++k) {
+    if (w.s3e[k]) DR_TRY(op_conv_repack_split3(D.e[k + 1], D.e[k], wm->conv[k].w, w.s3e[k], s));
+    if (w.s3d[k]) DR_TRY(op_conv_repack_split3(cin_t[k], cout_t[k], dec->convt[k].w, w.s3d[k], s));
+    if (w.t3d[k]) DR_TRY(op_convT_repack_split3(cin_t[k], cout_t[k], dec->convt[k].w, w.t3d[k], s));
+    if (w.t3e[k]) DR_TRY(op_convT_repack_split3(D.e[k + 1], D.e[k], wm->conv[k].w, w.t3e[k], s));
+  }
   }  // !vec
   // decoder.upscaler.3 rows to NHWC order (vector mode: Pf = 1, the identity), so its output is the first convT's NHWC input
   DR_TRY(perm_rows(D.C0, D.Pf, D.dh, dec->up3.w, w.w3p, 1, s));
@@ -589,9 +642,14 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     DR_TRY(dr_check_launch("silu"));
   } else {
   DR_TRY(op_frames_nhwc4(M, B, IH, IW, src, w.x0, s));
-  for (int k = 0; k < N; ++k)
-    DR_TRY(op_conv_nhwc_ex(M, enc_cin_st(D, k), IH >> k, IW >> k, D.e[k + 1], k ? w.a[k - 1] : w.x0, w.wr[k],
-                           wm->conv[k].b, w.a[k], k == N - 1 ? 1 : 0, w.pre[k], CONV_EPI_FWD, s));
+  for (int k = 0; k < N; ++k) {
+    if (w.s3e[k])
+      DR_TRY(op_conv_split3_ex(M, D.e[k], IH >> k, IW >> k, D.e[k + 1], w.a[k - 1], w.s3e[k], wm->conv[k].b, w.a[k],
+                               k == N - 1 ? 1 : 0, w.pre[k], CONV_EPI_FWD, s));
+    else
+      DR_TRY(op_conv_nhwc_ex(M, enc_cin_st(D, k), IH >> k, IW >> k, D.e[k + 1], k ? w.a[k - 1] : w.x0, w.wr[k],
+                             wm->conv[k].b, w.a[k], k == N - 1 ? 1 : 0, w.pre[k], CONV_EPI_FWD, s));
+  }
   }
   {
     GemmArgs g = lin(M, eh, F, aL, F, wm->map0.w, F + Hd, wm->map0.b, w.feat, eh);
@@ -680,7 +738,8 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
       a.in = k ? w.dqp[k - 1] : w.du2p; a.silu_in = 0; a.wq = w.wqd[k]; a.bias = dec->convt[k].b;
       if (k < N - 1) {
         a.out = w.dq[k]; a.out2 = w.dqp[k]; a.ldc = cout_t[k];
-        DR_TRY(op_convT_nhwc(CT_EPI_BIAS, a, s));
+        if (w.t3d[k]) DR_TRY(op_convT_split3(CT_EPI_BIAS, a, w.t3d[k], s));
+        else DR_TRY(op_convT_nhwc(CT_EPI_BIAS, a, s));
       } else {
         // Tanh + squared error against frames t >= 1 (WorldModel.py:129); writes dL/d(pre-tanh)
         a.out = w.dgout; a.ldc = 4;
@@ -767,10 +826,14 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
       const float* pre = k ? w.dq[k - 1] : w.du2;
       const float* post = k ? w.dqp[k - 1] : w.du2p;
       const float* gout = k < N - 1 ? w.dgq[k] : w.dgout;  // dL/d(convT k's output pre-activation)
-      DR_TRY(op_conv_nhwc_ex(M1, co_st, ih, iw, cin_t[k], gout, w.wrd[k], nullptr, gin, 0, const_cast<float*>(pre),
-                             CONV_EPI_DSILU, s));
-      DR_TRY(op_conv_wgrad(M1, ih / 2, iw / 2, cin_t[k], co_st, post, cin_t[k], 0, gout, co_st, gd->convt[k].w, co, 1.0f,
-                           0, w.cws, w.cws_n, s));
+      if (w.s3d[k])
+        DR_TRY(op_conv_split3_ex(M1, co_st, ih, iw, cin_t[k], gout, w.s3d[k], nullptr, gin, 0, const_cast<float*>(pre),
+                                 CONV_EPI_DSILU, s));
+      else
+        DR_TRY(op_conv_nhwc_ex(M1, co_st, ih, iw, cin_t[k], gout, w.wrd[k], nullptr, gin, 0, const_cast<float*>(pre),
+                               CONV_EPI_DSILU, s));
+      DR_TRY(wgrad(M1, ih / 2, iw / 2, cin_t[k], co_st, post, cin_t[k], gout, co_st, gd->convt[k].w, co, w.cws, w.cws_n,
+                   s));
       DR_TRY(op_chan_sum((long long)M1 * ih * iw, co, gout, co_st, gd->convt[k].b, 0, w.cws, w.cws_n, s));
     }
   }
@@ -875,14 +938,14 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
       const int oh = IH >> (k + 1), ow = IW >> (k + 1);
       const int cin = enc_cin_st(D, k), cout = D.e[k + 1];
       const float* hi = k ? w.a[k - 1] : w.x0;  // conv k's input
-      DR_TRY(op_conv_wgrad(M, oh, ow, cout, cin, w.gp[k], cout, 0, hi, cin, gw->conv[k].w, D.e[k], 1.0f, 0, w.cws,
-                           w.cws_n, s));
+      DR_TRY(wgrad(M, oh, ow, cout, cin, w.gp[k], cout, hi, cin, gw->conv[k].w, D.e[k], w.cws, w.cws_n, s));
       DR_TRY(op_chan_sum((long long)M * oh * ow, cout, w.gp[k], cout, gw->conv[k].b, 0, w.cws, w.cws_n, s));
       if (k > 0) {
         ConvTArgs a = {};
         a.n = M; a.cin = cout; a.h = oh; a.w = ow; a.cout = cin;
         a.in = w.gp[k]; a.wq = w.wqe[k]; a.out = w.gp[k - 1]; a.ldc = cin; a.pre = w.pre[k - 1];
-        DR_TRY(op_convT_nhwc(CT_EPI_DSILU, a, s));
+        if (w.t3e[k]) DR_TRY(op_convT_split3(CT_EPI_DSILU, a, w.t3e[k], s));
+        else DR_TRY(op_convT_nhwc(CT_EPI_DSILU, a, s));
       }
     }
   }

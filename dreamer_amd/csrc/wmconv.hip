@@ -655,6 +655,14 @@ static void wgrad_plan(int n, int h, int w, int ca, int cb, int& bm, int& nsplit
   nsplit = (int)((K + ch - 1) / ch);
 }
 
+int op_wgrad_reduce(int ca, int cb, int cbo, int nsplit, const float* part, float* dw, float scale, int accumulate,
+                    hipStream_t s) {
+  const int total = ca * 16 * cb;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((total + 63) / 64), dim3(1024), 0, s, ca, cb, cbo, nsplit, part, dw, scale,
+                     accumulate);
+  return dr_check_launch("wgrad_reduce");
+}
+
 size_t op_conv_wgrad_ws_floats(int n, int h, int w, int ca, int cb) {
   int bm, ns, ch;
   wgrad_plan(n, h, w, ca, cb, bm, ns, ch);
