@@ -35,6 +35,17 @@ int op_conv_split3(int n, int cin, int ih, int iw, int cout, const float* in, co
 int op_conv_split3_ex(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
                       float* out, int out_nchw, float* pre, int epi, hipStream_t s);
 
+// tall NT products f32-accurate on the bf16 MFMA (conv_split.hip):
+// Y = act(A W^T + bias), A [M][K] row-major with an optional second K segment
+// (A2 at k >= ksA, ksA % 4 == 0), W pre-split by op_nt_repack_split3 into a
+// scratch of op_nt_split3_ws_bytes(N, K); N % 4 == 0, K % 4 == 0, act 1 = SiLU
+size_t op_nt_split3_ws_bytes(int N, int K);
+int op_nt_repack_split3(int N, int K, const float* W, int ldw, void* wr, hipStream_t s);
+bool op_gemm_nt_split3_supported(int M, int N, int K, const float* A, int lda, const float* A2, int lda2, int ksA,
+                                 int ldy);
+int op_gemm_nt_split3(int M, int N, int K, const float* A, int lda, const float* A2, int lda2, int ksA, const void* wr,
+                      const float* bias, int act, float* Y, int ldy, hipStream_t s);
+
 // ---- conv_bf16.hip (bf16 perf mode; activations bf16, accumulation f32) ----
 // weights: Conv2d [co][ci][4][4] f32 -> bf16 [co][tap][cin_pad]; matrix slice -> bf16 [rows][cols]
 int op_conv_repack_bf16(int cout, int cin, int cin_pad, const float* w, void* wr, hipStream_t s);

@@ -1033,3 +1033,225 @@ int op_wgrad_split3(int n, int h, int w, int ca, int cb, const float* lo, int ld
   DR_TRY(dr_check_launch("wgrad_split3"));
   return op_wgrad_reduce(ca, cb, cbo, ns, ws, dw, scale, accumulate, s);
 }
+
+// ---------------------------------------------------------------------------
+// Tall NT products, f32-accurate on the bf16 MFMA: Y[m][n] = act(sum_k A[m][k]
+// W[n][k] + bias[n]) for M in the thousands (the encoder feature projection
+// over B S / 2 frames, K = 4096; the critic's and the reward / continue heads'
+// first layers over B (H + 1) imagined states, K = Hd + L).  The k_conv_split3
+// pipeline with a row-major A (optional second K segment at ksA, k % 4
+// aligned) in place of the im2col gather; W split once per call into planes
+// [K/32][3][Np][32] (Np = N rounded up to BN, zero rows past N).
+// ---------------------------------------------------------------------------
+struct GemmS3 {
+  int M, N, K, ksA, lda, lda2, ldy, act, Np;
+  const float* A;
+  const float* A2;
+  const u16* wr;
+  const float* bias;
+  float* Y;
+};
+
+template <int BM, int BN>
+__global__ __launch_bounds__(BM * 2) void k_gemm_split3(GemmS3 g) {
+  constexpr int NT = BM * 2;
+  constexpr int WTN = BN / 2, FM = 4, FN = WTN / 16;
+  constexpr int APT = BM * 8 / NT;
+  constexpr int BU = 3 * BN * 4;
+  constexpr int BPT = (BU + NT - 1) / NT;
+  static_assert(APT == 4 && FN >= 1 && BM % 64 == 0, "gemm_split3 tile");
+  __shared__ __attribute__((aligned(16))) u32x4 As[2][3][BM][4];
+  __shared__ __attribute__((aligned(16))) u32x4 Bs[2][3][BN][4];
+  const int M = g.M, N = g.N, K = g.K, ksA = g.ksA, Np = g.Np;
+  const int tiles_n = (N + BN - 1) / BN;
+  const int tiles = ((M + BM - 1) / BM) * tiles_n;
+  const int lt = dr_xcd_tile(blockIdx.x, tiles);
+  if (lt < 0) return;
+  const int m0 = (lt / tiles_n) * BM, n0 = (lt % tiles_n) * BN;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
+  const int quad = tid & 7, prow = tid >> 3;
+  const int NCH = (K + 31) / 32;
+  // per A row: element offsets of the row in both segments (rows past M read row M - 1)
+  unsigned oa[APT], oa2[APT];
+#pragma unroll
+  for (int i = 0; i < APT; ++i) {
+    const int m = min(m0 + prow + (NT / 8) * i, M - 1);
+    oa[i] = (unsigned)(m * g.lda);
+    oa2[i] = (unsigned)(m * g.lda2);
+  }
+  f32x4 ra0[APT], ra1[APT];
+  u32x4 rb0[BPT], rb1[BPT];
+  bool kv0 = true, kv1 = true;  // this thread's float4 lies below K
+  auto load = [&](int c, auto slot) __attribute__((always_inline)) {
+    f32x4* ra = decltype(slot)::value == 0 ? ra0 : ra1;
+    u32x4* rb = decltype(slot)::value == 0 ? rb0 : rb1;
+    bool& kv = decltype(slot)::value == 0 ? kv0 : kv1;
+    const int k = 32 * c + 4 * quad;
+    kv = k < K;
+    const int kk = kv ? k : 0;
+    const bool s1 = kk < ksA;
+    const float* base = s1 ? g.A : g.A2;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const unsigned e = s1 ? oa[i] + (unsigned)kk : oa2[i] + (unsigned)(kk - ksA);
+      ra[i] = *reinterpret_cast<const f32x4*>(base + e);
+    }
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      const int e = tid + NT * j;
+      if (BU % NT == 0 || e < BU) {
+        const int pl = e / (BN * 4), rm = e - pl * BN * 4, row = rm >> 2, u = rm & 3;
+        rb[j] = *reinterpret_cast<const u32x4*>(g.wr + (((long long)c * 3 + pl) * Np + n0 + row) * 32 + 8 * u);
+      }
+    }
+  };
+  auto store = [&](auto slot, int buf) __attribute__((always_inline)) {
+    const f32x4* ra = decltype(slot)::value == 0 ? ra0 : ra1;
+    const u32x4* rb = decltype(slot)::value == 0 ? rb0 : rb1;
+    const bool kv = decltype(slot)::value == 0 ? kv0 : kv1;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const int row = prow + (NT / 8) * i;
+      const f32x4 v = kv ? ra[i] : (f32x4){0.f, 0.f, 0.f, 0.f};
+      unsigned h0, m0_, l0, h1, m1, l1;
+      split3_pair(v[0], v[1], h0, m0_, l0);
+      split3_pair(v[2], v[3], h1, m1, l1);
+      const int unit = (quad >> 1) ^ swz(row), half = quad & 1;
+      reinterpret_cast<u32x2*>(&As[buf][0][row][unit])[half] = (u32x2){h0, h1};
+      reinterpret_cast<u32x2*>(&As[buf][1][row][unit])[half] = (u32x2){m0_, m1};
+      reinterpret_cast<u32x2*>(&As[buf][2][row][unit])[half] = (u32x2){l0, l1};
+    }
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      const int e = tid + NT * j;
+      if (BU % NT == 0 || e < BU) {
+        const int pl = e / (BN * 4), rm = e - pl * BN * 4, row = rm >> 2, u = rm & 3;
+        Bs[buf][pl][row][u ^ swz(row)] = rb[j];
+      }
+    }
+  };
+  const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * WTN;
+  const int fu = q ^ swz(r);
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  load(0, S0{});
+  load(min(1, NCH - 1), S1{});
+  store(S0{}, 0);
+  __syncthreads();
+  auto step = [&](int c, auto slot) __attribute__((always_inline)) {
+    constexpr int SL = decltype(slot)::value;
+    using Next = std::integral_constant<int, 1 - SL>;
+    const int buf = c & 1;
+    load(min(c + 2, NCH - 1), slot);
+    u32x4 av[3][FM], bv[3][FN];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) av[pl][i] = As[buf][pl][wm0 + 16 * i + r][fu];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bv[pl][j] = Bs[buf][pl][wn0 + 16 * j + r][fu];
+    }
+#define DR_G3(PA, PB)                                                                                   \
+  _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
+      mfma_b16(bv[PB][j], av[PA][i], acc[i][j]);
+    DR_G3(2, 0)
+    DR_G3(1, 1)
+    DR_G3(0, 2)
+    DR_G3(1, 0)
+    DR_G3(0, 1)
+    DR_G3(0, 0)
+#undef DR_G3
+    if (c + 1 < NCH) store(Next{}, buf ^ 1);
+    dr_lds_barrier();
+  };
+  int c = 0;
+  for (; c + 1 < NCH; c += 2) {
+    step(c, S0{});
+    step(c + 1, S1{});
+  }
+  if (c < NCH) step(c, S0{});
+  // lane (r, q) of acc[i][j]: row m0 + wm0 + 16 i + r, columns n0 + wn0 + 16 j + 4 q .. + 3
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wm0 + 16 * i + r;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn0 + 16 * j + 4 * q;
+      if (n >= N) continue;
+      f32x4 v = acc[i][j];
+      if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + n);
+      if (g.act == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] / (1.0f + expf(-v[e]));
+      }
+      *reinterpret_cast<f32x4*>(g.Y + (long long)m * g.ldy + n) = v;
+    }
+  }
+}
+
+// W [N][K] (row stride ldw) -> bf16 planes [K/32][3][Np][32], zero past N and K
+__global__ void k_nt_repack_split3(int N, int K, int Np, const float* __restrict__ W, int ldw, u16* __restrict__ wr) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int KC = (K + 31) / 32;
+  if (i >= (long long)KC * 32 * Np) return;
+  const int n = (int)(i / (KC * 32)), k = (int)(i - (long long)n * KC * 32);
+  unsigned hh = 0, mm = 0, ll = 0;
+  if (n < N && k < K) split3(W[(long long)n * ldw + k], hh, mm, ll);
+  const long long plane = (long long)Np * 32;
+  const long long base = ((long long)(k >> 5) * 3 * Np + n) * 32 + (k & 31);
+  wr[base] = (u16)hh;
+  wr[base + plane] = (u16)mm;
+  wr[base + 2 * plane] = (u16)ll;
+}
+
+// weight planes hold N rounded up to 128 rows (either column tile reads whole tiles)
+static int s3_np(int N) { return (N + 127) / 128 * 128; }
+size_t op_nt_split3_ws_bytes(int N, int K) {
+  return (size_t)((K + 31) / 32) * 32 * 3 * s3_np(N) * sizeof(u16);
+}
+int op_nt_repack_split3(int N, int K, const float* W, int ldw, void* wr, hipStream_t s) {
+  const int Np = s3_np(N);
+  const long long total = (long long)((K + 31) / 32) * 32 * Np;
+  hipLaunchKernelGGL(k_nt_repack_split3, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, N, K, Np, W, ldw,
+                     (u16*)wr);
+  return dr_check_launch("nt_repack_split3");
+}
+bool op_gemm_nt_split3_supported(int M, int N, int K, const float* A, int lda, const float* A2, int lda2, int ksA,
+                                 int ldy) {
+  const bool seg = ksA < K;
+  return M > 0 && N > 0 && N % 4 == 0 && ldy % 4 == 0 && K % 4 == 0 && lda % 4 == 0 && !((uintptr_t)A & 15) &&
+         (!seg || (ksA % 4 == 0 && lda2 % 4 == 0 && A2 && !((uintptr_t)A2 & 15))) &&
+         (long long)M * lda < (1LL << 31) && (!seg || (long long)M * lda2 < (1LL << 31));
+}
+int op_gemm_nt_split3(int M, int N, int K, const float* A, int lda, const float* A2, int lda2, int ksA, const void* wr,
+                      const float* bias, int act, float* Y, int ldy, hipStream_t s) {
+  if (!op_gemm_nt_split3_supported(M, N, K, A, lda, A2, lda2, ksA, ldy) || ((uintptr_t)Y & 15) ||
+      (bias && ((uintptr_t)bias & 15))) {
+    dr_set_error("gemm_nt_split3: unsupported problem (M=%d N=%d K=%d)", M, N, K);
+    return DR_E_INVALID;
+  }
+  GemmS3 g = {M, N, K, ksA < K ? ksA : K, lda, lda2, ldy, act, s3_np(N), A, A2, (const u16*)wr, bias, Y};
+  // the largest tile that still gives ~two waves per SIMD over the chip
+  // (256 x 128, 256 x 64, 128 x 128, 128 x 64, else 64 x 64): taller / wider
+  // tiles re-read less, but a half-empty chip costs more (M = 8192, N = 200:
+  // 128 x 64 tiles gave 256 single-wave-per-SIMD workgroups)
+  auto tl = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  auto waves = [&](int bm, int bn) { return (long long)tl(bm, bn) * (bm / 32); };
+  if (waves(256, 128) >= 2048)
+    hipLaunchKernelGGL((k_gemm_split3<256, 128>), dim3(dr_xcd_grid(tl(256, 128))), dim3(512), 0, s, g);
+  else if (waves(256, 64) >= 2048)
+    hipLaunchKernelGGL((k_gemm_split3<256, 64>), dim3(dr_xcd_grid(tl(256, 64))), dim3(512), 0, s, g);
+  else if (waves(128, 128) >= 2048)
+    hipLaunchKernelGGL((k_gemm_split3<128, 128>), dim3(dr_xcd_grid(tl(128, 128))), dim3(256), 0, s, g);
+  else if (waves(128, 64) >= 2048)
+    hipLaunchKernelGGL((k_gemm_split3<128, 64>), dim3(dr_xcd_grid(tl(128, 64))), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((k_gemm_split3<64, 64>), dim3(dr_xcd_grid(tl(64, 64))), dim3(128), 0, s, g);
+  return dr_check_launch("gemm_nt_split3");
+}

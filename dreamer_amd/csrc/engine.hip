@@ -4,6 +4,14 @@
 // no allocation) so a whole train_Agent epoch can be captured in a hipGraph.
 #include "engine_util.h"
 
+// fp32 mode, tall batches: the first Linear of a head over [h | z] on the
+// split3 bf16 MFMA (conv_split.hip) when the workspace holds its weight planes
+static bool s3_first_layer(const dr_dims* d, int M, int N, const float* h, long long ldh, const float* z,
+                           long long ldz) {
+  return d->precision != DR_PREC_BF16 && M >= 1024 && ldh < INT_MAX && ldz < INT_MAX &&
+         op_gemm_nt_split3_supported(M, N, d->hidden + latent(d), h, (int)ldh, z, (int)ldz, d->hidden, N);
+}
+
 // ===========================================================================
 // a3  encoder features
 // ===========================================================================
@@ -11,6 +19,7 @@ struct EncWs {
   float *x0, *a[DR_MAX_DEPTH], *wr[DR_MAX_DEPTH], *sk;  // a[k] / wr[k]: conv k's output / repacked weight
   long long sk_n;
   void* wproj;  // bf16 mode: latent_mapper.0 feature columns as bf16 [enc_hidden][F]
+  void* s3proj;  // fp32 mode: the same columns as split3 bf16 planes (op_nt_repack_split3)
 };
 
 // bf16 mode stores activations / repacked weights as bf16 (2 bytes): the same
@@ -44,6 +53,7 @@ static void enc_carve(Carve& c, const dr_dims* d, int n, EncWs& w) {
     w.wr[k] = bf ? (float*)c.raw(elems * 2) : (float*)c.raw(elems * 6);
   }
   w.wproj = bf ? c.raw((size_t)d->enc_hidden * enc_feat_dim(d) * 2) : nullptr;
+  w.s3proj = bf ? nullptr : c.raw(op_nt_split3_ws_bytes(d->enc_hidden, enc_feat_dim(d)));
 }
 
 extern "C" size_t dr_encoder_workspace_bytes(const dr_dims* d, int n_frames) {
@@ -148,6 +158,13 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
     }
   }
   const int F = enc_feat_dim(d);
+  if (w.s3proj && n >= 1024 &&
+      op_gemm_nt_split3_supported(n, d->enc_hidden, F, w.a[N - 1], F, nullptr, 0, F, d->enc_hidden)) {
+    // latent_mapper.0's feature columns (VAE.py:57-75 -> WorldModel.py) on the split3 bf16 MFMA
+    DR_TRY(op_nt_repack_split3(d->enc_hidden, F, wm->map0.w, F + d->hidden, w.s3proj, s));
+    return op_gemm_nt_split3(n, d->enc_hidden, F, w.a[N - 1], F, nullptr, 0, F, w.s3proj, wm->map0.b, 0, feat,
+                             d->enc_hidden, s);
+  }
   GemmArgs gp = lin(n, d->enc_hidden, F, w.a[N - 1], F, wm->map0.w, F + d->hidden, wm->map0.b, feat, d->enc_hidden);
   float* sk = w.sk;
   long long skn = w.sk_n;
@@ -268,6 +285,7 @@ extern "C" size_t dr_imagine_tape_bytes(const dr_dims* d, int B, int H) {
 
 struct ImWs {
   float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog, *rval, *wt, *wst, *bst;  // forward scratch
+  void *s3r, *s3c;  // split3 weight planes of the reward / continue heads' first Linear
   int* idx[2];
   // backward
   float *gH, *gZ, *gA, *glog, *gx2, *gp2, *gx1, *gp1, *ggi, *ggh, *gheads, *gx2a, *gpre2a, *gy2a, *xh2a, *gx1a,
@@ -290,6 +308,8 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.rlog = c.f(B1 * d->buckets);
   w.clog = c.f(B1);
   w.rval = c.f(B1);
+  w.s3r = c.raw(op_nt_split3_ws_bytes(d->rew_h1, d->hidden + L));
+  w.s3c = c.raw(op_nt_split3_ws_bytes(d->cont_h1, d->hidden + L));
   w.wt = c.f((long long)(L + A) * 3 * Hd);
   w.wst = c.f((long long)2 * A * d->actor_h2);
   w.bst = c.f((long long)2 * A);
@@ -412,9 +432,19 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
   {
     const int M1 = B * (H + 1);
     GemmArgs p[2];
-    p[0] = lin2(M1, d->rew_h1, hiddens, Hd, Hd, latents, L, L, wm->reward.l0.w, wm->reward.l0.b, w.p1r, d->rew_h1);
-    p[1] = lin2(M1, d->cont_h1, hiddens, Hd, Hd, latents, L, L, wm->cont.l0.w, wm->cont.l0.b, w.p1c, d->cont_h1);
-    DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, 2, s));
+    if (s3_first_layer(d, M1, d->rew_h1, hiddens, Hd, latents, L) &&
+        s3_first_layer(d, M1, d->cont_h1, hiddens, Hd, latents, L)) {
+      DR_TRY(op_nt_repack_split3(d->rew_h1, Hd + L, wm->reward.l0.w, Hd + L, w.s3r, s));
+      DR_TRY(op_nt_repack_split3(d->cont_h1, Hd + L, wm->cont.l0.w, Hd + L, w.s3c, s));
+      DR_TRY(op_gemm_nt_split3(M1, d->rew_h1, Hd + L, hiddens, Hd, latents, L, Hd, w.s3r, wm->reward.l0.b, 0, w.p1r,
+                               d->rew_h1, s));
+      DR_TRY(op_gemm_nt_split3(M1, d->cont_h1, Hd + L, hiddens, Hd, latents, L, Hd, w.s3c, wm->cont.l0.b, 0, w.p1c,
+                               d->cont_h1, s));
+    } else {
+      p[0] = lin2(M1, d->rew_h1, hiddens, Hd, Hd, latents, L, L, wm->reward.l0.w, wm->reward.l0.b, w.p1r, d->rew_h1);
+      p[1] = lin2(M1, d->cont_h1, hiddens, Hd, Hd, latents, L, L, wm->cont.l0.w, wm->cont.l0.b, w.p1c, d->cont_h1);
+      DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, 2, s));
+    }
     p[0] = lin_ln(M1, d->buckets, d->rew_h2, w.p2r, d->rew_h2, wm->reward.n4, wm->reward.l6.w, wm->reward.l6.b, w.rlog,
                   d->buckets);
     p[1] = lin_ln(M1, 1, d->cont_h2, w.p2c, d->cont_h2, wm->cont.n4, wm->cont.l6.w, wm->cont.l6.b, w.clog, 1);
@@ -655,8 +685,10 @@ static size_t critic_ws_bytes(const dr_dims* d, int M) {
   CTape t;
   ctape_carve(c, d, M, t);
   c.f(splitk_floats(M, d->critic_h1));
+  c.raw(op_nt_split3_ws_bytes(d->critic_h1, d->hidden + latent(d)));
   return c.off;
 }
+
 
 extern "C" int dr_critic_fwd(const dr_dims* d, const dr_critic* cr, int M, const float* h, long long ldh,
                              const float* z, long long ldz, float* logits, float* values, void* tape, void* ws,
@@ -666,6 +698,7 @@ extern "C" int dr_critic_fwd(const dr_dims* d, const dr_critic* cr, int M, const
   CTape t;
   float* sk = nullptr;
   long long skn = 0;
+  void* s3w = nullptr;  // split3 weight planes of value_net.0 (fp32 mode)
   if (tape) {
     Carve c(tape);
     ctape_carve(c, d, M, t);
@@ -682,11 +715,16 @@ extern "C" int dr_critic_fwd(const dr_dims* d, const dr_critic* cr, int M, const
     if (c.off + (size_t)want * sizeof(float) + 256 <= ws_bytes) {
       skn = want;
       sk = c.f(skn);
+      const size_t pb = op_nt_split3_ws_bytes(d->critic_h1, d->hidden + latent(d));
+      if (c.off + pb + 256 <= ws_bytes) s3w = c.raw(pb);
     }
   }
   DR_REQUIRE(tape || ws, "dr_critic_fwd needs a tape or a workspace");
   const int L = latent(d), Hd = d->hidden, c1 = d->critic_h1, c2 = d->critic_h2, nb = d->buckets;
-  {
+  if (s3w && s3_first_layer(d, M, c1, h, ldh, z, ldz)) {
+    DR_TRY(op_nt_repack_split3(c1, Hd + L, cr->net.l0.w, Hd + L, s3w, s));
+    DR_TRY(op_gemm_nt_split3(M, c1, Hd + L, h, (int)ldh, z, (int)ldz, Hd, s3w, cr->net.l0.b, 0, t.pre1, c1, s));
+  } else {
     GemmArgs g1 = lin2(M, c1, h, ldh, Hd, z, ldz, L, cr->net.l0.w, cr->net.l0.b, t.pre1, c1);
     give_splitk(g1, sk, skn);
     DR_TRY(run(G_NT, AM_PLAIN, g1, s));
