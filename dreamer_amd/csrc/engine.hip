@@ -221,6 +221,10 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
   }
   const float* h = h_init;  // current hidden (NULL = zeros)
   int hb = 0;
+  // B >= 128 (split GRU): the next step's hidden product h W_hh^T + b_hh rides
+  // in the same grouped launch as latent_mapper.0 (both read only h)
+  const bool split_gru = B >= 128;
+  bool gh_pre = false;
   if (z_init) {
     if (z_init != z_out) DR_TRY(copy2d(z_out, L, z_init, L, L, B, s));
     DR_TRY(op_onehot_index(B, d->rows, d->cols, z_out, L, w.idx, onehot_vals(w.idx, B, d->rows), s));
@@ -232,14 +236,20 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
       float* hn = w.hb[hb];
       hb ^= 1;
       DR_TRY(gru_onehot(d, wm, B, w.idx, actions + ai * act_st, act_sb, h, Hd, hn, Hd, w.wt, nullptr,
-                        nullptr, nullptr, nullptr, s, z_out, L, w.gh));
+                        nullptr, nullptr, nullptr, s, z_out, L, w.gh, gh_pre));
       h = hn;
     }
     // latent_mapper.0 on cat(features, h): feature part precomputed in feat[t]
-    GemmArgs g = lin(B, eh, h ? Hd : 0, h, Hd, wm->map0.w + F, F + Hd, nullptr, w.pre1, eh);
-    g.addend = feat + (long long)t * B * eh;
-    g.ld_add = eh;
-    DR_TRY(run(G_NT, AM_PLAIN, g, s));
+    GemmArgs g[2];
+    g[0] = lin(B, eh, h ? Hd : 0, h, Hd, wm->map0.w + F, F + Hd, nullptr, w.pre1, eh);
+    g[0].addend = feat + (long long)t * B * eh;
+    g[0].ld_add = eh;
+    gh_pre = split_gru && h && t + 1 < T;
+    if (gh_pre) {
+      g[1] = lin(B, 3 * Hd, Hd, h, Hd, wm->w_hh, Hd, wm->b_hh, w.gh, 3 * Hd);
+      g[0].bf16 = g[1].bf16 = 0;  // (bf16 mode: these products stay f32)
+    }
+    DR_TRY(gemm_launch(G_NT, AM_PLAIN, g, gh_pre ? 2 : 1, s));
     float* lg = (t == T - 1 && logits_out) ? logits_out : nullptr;
     GemmArgs gp = lin_ln(B, L, eh, w.pre1, eh, wm->map1, wm->map3.w, wm->map3.b, lg, L);
     with_sampler(gp, d, noise, t, z_out, L, w.idx, nullptr, 0);
@@ -285,6 +295,7 @@ extern "C" size_t dr_imagine_tape_bytes(const dr_dims* d, int B, int H) {
 
 struct ImWs {
   float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog, *rval, *wt, *wst, *bst;  // forward scratch
+  float *tl0f, *hpart;  // forward: actor Linear 0 transposed ([Hd+L][a1]), its h-part + bias [B][a1]
   void *s3r, *s3c;  // split3 weight planes of the reward / continue heads' first Linear
   int* idx[2];
   // backward
@@ -311,6 +322,8 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.s3r = c.raw(op_nt_split3_ws_bytes(d->rew_h1, d->hidden + L));
   w.s3c = c.raw(op_nt_split3_ws_bytes(d->cont_h1, d->hidden + L));
   w.wt = c.f((long long)(L + A) * 3 * Hd);
+  w.tl0f = c.f((long long)(Hd + L) * d->actor_h1);
+  w.hpart = c.f(Bl * d->actor_h1);
   w.wst = c.f((long long)2 * A * d->actor_h2);
   w.bst = c.f((long long)2 * A);
   w.idx[0] = c.i(2 * Bl * d->rows);
@@ -377,7 +390,17 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
   DR_TRY(copy2d(hiddens, ldH, h0, Hd, Hd, B, s));
   dr_noise nq = noise;  // Categorical draws: a Philox stream apart from the actor's
   nq.stream += 65536;
-  DR_TRY(op_transpose(3 * Hd, L + A, wm->w_ih, w.wt, s));
+  // per-step structure: the three products that read only
+  // h_{t+1} -- the prior's first Linear, the h-part of the next actor's first
+  // Linear and (B >= 128, split GRU) the next GRU step's hidden product --
+  // run as ONE grouped launch right after the GRU; the actor's latent part is
+  // then a gather of R rows of its transposed z-columns (z is one-hot)
+  const bool split_gru = B >= 128;
+  const bool zg = d->rows <= 32 && a1 % 4 == 0;
+  {
+    TransposeJob tj[2] = {{3 * Hd, L + A, 3 * Hd, wm->w_ih, w.wt}, {a1, Hd + L, a1, ac->l0.w, w.tl0f}};
+    DR_TRY(op_transpose_multi(tj, zg ? 2 : 1, s));
+  }
   DR_TRY(op_onehot_index(B, d->rows, d->cols, latents, ldL, w.idx[0], onehot_vals(w.idx[0], B, d->rows), s));
 
   // actor at step 0 (Agent.py:191-210)
@@ -400,10 +423,19 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
     float* z_n = latents + (long long)(t + 1) * L;
     // WorldModel.imagine_step (WorldModel.py:72-77)
     DR_TRY(gru_onehot(d, wm, B, w.idx[t & 1], actions + (long long)t * A, ldA, h_t, ldH, h_n, ldH, w.wt,
-                      tp.r + hb, tp.u + hb, tp.n + hb, tp.ghn + hb, s, z_t, ldL, w.gh));
+                      tp.r + hb, tp.u + hb, tp.n + hb, tp.ghn + hb, s, z_t, ldL, w.gh, split_gru && t > 0));
     float* p1 = tp.pre1p + (long long)t * B * d->prior_h1;
     float* p2 = tp.pre2p + (long long)t * B * d->prior_h2;
-    DR_TRY(run(G_NT, AM_PLAIN, lin(B, d->prior_h1, Hd, h_n, ldH, wm->prior.l0.w, Hd, wm->prior.l0.b, p1, d->prior_h1), s));
+    {
+      const bool more = t + 1 < H;
+      GemmArgs p[3];
+      int np = 0;
+      p[np++] = lin(B, d->prior_h1, Hd, h_n, ldH, wm->prior.l0.w, Hd, wm->prior.l0.b, p1, d->prior_h1);
+      if (more && zg) p[np++] = lin(B, a1, Hd, h_n, ldH, ac->l0.w, Hd + L, ac->l0.b, w.hpart, a1);
+      if (more && split_gru) p[np++] = lin(B, 3 * Hd, Hd, h_n, ldH, wm->w_hh, Hd, wm->b_hh, w.gh, 3 * Hd);
+      for (int i = 0; i < np; ++i) p[i].bf16 = 0;  // (bf16 mode: these products stay f32)
+      DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, np, s));
+    }
     DR_TRY(run(G_NT, AM_LNSILU, lin_ln(B, d->prior_h2, d->prior_h1, p1, d->prior_h1, wm->prior.n1, wm->prior.l3.w,
                                        wm->prior.l3.b, p2, d->prior_h2), s));
     GemmArgs g = lin_ln(B, L, d->prior_h2, p2, d->prior_h2, wm->prior.n4, wm->prior.l6.w, wm->prior.l6.b, nullptr, 0);
@@ -412,7 +444,13 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
     // the actor for step t+1 (the reward / continue heads run once after the unroll)
     if (t + 1 < H) {
       const long long o1 = (long long)(t + 1) * a1, o2 = (long long)(t + 1) * a2, o = (long long)(t + 1) * A;
-      DR_TRY(run(G_NT, AM_PLAIN, lin2(B, a1, h_n, ldH, Hd, z_n, ldL, L, ac->l0.w, ac->l0.b, tp.pre1a + o1, lda1), s));
+      if (zg) {
+        int* ix = w.idx[(t + 1) & 1];
+        DR_TRY(op_zgather_add(B, a1, d->rows, d->cols, ix, onehot_vals(ix, B, d->rows), z_n, ldL,
+                              w.tl0f + (long long)Hd * a1, a1, w.hpart, a1, tp.pre1a + o1, lda1, s));
+      } else {
+        DR_TRY(run(G_NT, AM_PLAIN, lin2(B, a1, h_n, ldH, Hd, z_n, ldL, L, ac->l0.w, ac->l0.b, tp.pre1a + o1, lda1), s));
+      }
       GemmArgs g3 = lin_ln(B, a2, a1, tp.pre1a + o1, lda1, ac->n1, ac->l3.w, ac->l3.b, tp.pre2a + o2, lda2);
       g3.a_out = tp.x1a + o1;
       g3.ld_aout = lda1;

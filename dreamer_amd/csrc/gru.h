@@ -20,9 +20,18 @@ struct alignas(16) GruArgs {
   long long ldo;
   float *sr, *su, *sn, *sghn;  // optional saves [B][Hd] for the backward
   float* gh_ws;                // optional [B][3*Hd] scratch: enables the split path at B >= 128
+  int gh_ready;                // split path: gh_ws already holds h W_hh^T + b_hh (computed by the
+                               //   caller's grouped launch of the previous step), skip the GEMM
 };
 
 int op_gru_fused(const GruArgs& g, hipStream_t s);
+// out[m][n] = base[m][n] + sum over the R latent groups of zval[m][u] * wt[u*C + idx[m][u]][n]
+// (groups with idx < 0: every class, z[m][u*C + c] * wt[u*C + c][n]).  The latent
+// part of a Linear on cat(h, z) with a one-hot z: wt = the z-columns of its weight,
+// transposed ([R*C][N], row stride ldw), base = the h-part plus bias.
+int op_zgather_add(int M, int N, int R, int C, const int* idx, const float* zval, const float* z, long long ldz,
+                   const float* wt, long long ldw, const float* base, long long ldb, float* out, long long ldo,
+                   hipStream_t s);
 int op_transpose(int rows, int cols, const float* in, float* out, hipStream_t s);
 // batched transposes in one launch: out[c * ldo + r] = in[r * cols + c]
 struct TransposeJob {

@@ -491,6 +491,83 @@ static int gates_batch() { return g_gates_batch; }
 static int gates_batch() { return 8; }
 #endif
 
+// ---------------------------------------------------------------------------
+// Latent part of a Linear on cat(h, z) with a one-hot z (the actor's first
+// layer inside the imagination unroll, Agent.py:191-210 on cat(h, z)):
+// out = base + sum_u zval[u] * wt[u*C + idx[u]] -- R gathered rows of the
+// transposed z-columns instead of a K = R*C dense product.  Thread = (row,
+// 4 outputs); every gathered float4 of a thread issued before the first FMA.
+// ---------------------------------------------------------------------------
+#define ZG_ROWS 4
+__global__ __launch_bounds__(256) void k_zgather_add(int M, int N, int R, int C, const int* __restrict__ idx,
+                                                     const float* __restrict__ zval, const float* __restrict__ z,
+                                                     long long ldz, const float* __restrict__ wt, long long ldw,
+                                                     const float* __restrict__ base, long long ldb,
+                                                     float* __restrict__ out, long long ldo) {
+  __shared__ int s_idx[ZG_ROWS][GRU_MAXR];
+  __shared__ float s_zv[ZG_ROWS][GRU_MAXR];
+  const int m0 = blockIdx.x * ZG_ROWS, tid = threadIdx.x;
+  for (int x = tid; x < ZG_ROWS * GRU_MAXR; x += 256) {
+    const int ml = x / GRU_MAXR, u = x - ml * GRU_MAXR, m = m0 + ml;
+    const bool ok = m < M && u < R;
+    s_idx[ml][u] = ok ? idx[m * R + u] : 0;
+    s_zv[ml][u] = ok ? zval[m * R + u] : 0.f;
+  }
+  const int ml = tid >> 6, m = m0 + ml, n = 4 * ((tid & 63) + 64 * (int)blockIdx.y);
+  const bool live = m < M && n < N;
+  const float4 b = dr_ld4(base, live ? (unsigned)(m * ldb + n) : 0u);
+  __syncthreads();
+  float4 w[GRU_MAXR];
+#pragma unroll
+  for (int u = 0; u < GRU_MAXR; ++u) {
+    const int iv = s_idx[ml][u];
+    const bool ok = live && u < R && iv >= 0;
+    w[u] = dr_ld4(wt, ok ? (unsigned)((u * C + iv) * ldw + n) : 0u);
+  }
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  bool dense = false;
+#pragma unroll
+  for (int u = 0; u < GRU_MAXR; ++u) {
+    if (u < R) {
+      const float zv = s_zv[ml][u];
+      dense = dense || s_idx[ml][u] < 0;
+      v.x = fmaf(w[u].x, zv, v.x);
+      v.y = fmaf(w[u].y, zv, v.y);
+      v.z = fmaf(w[u].z, zv, v.z);
+      v.w = fmaf(w[u].w, zv, v.w);
+    }
+  }
+  if (dense && live) {
+    const float* zr = z + (long long)m * ldz;
+    for (int u = 0; u < R; ++u) {
+      if (s_idx[ml][u] >= 0) continue;
+      for (int c = 0; c < C; ++c) {
+        const float zc = zr[u * C + c];
+        const float4 wc = dr_ld4(wt, (unsigned)((u * C + c) * ldw + n));
+        v.x = fmaf(wc.x, zc, v.x);
+        v.y = fmaf(wc.y, zc, v.y);
+        v.z = fmaf(wc.z, zc, v.z);
+        v.w = fmaf(wc.w, zc, v.w);
+      }
+    }
+  }
+  if (live) dr_st4(out, (unsigned)(m * ldo + n), make_float4(b.x + v.x, b.y + v.y, b.z + v.z, b.w + v.w));
+}
+
+int op_zgather_add(int M, int N, int R, int C, const int* idx, const float* zval, const float* z, long long ldz,
+                   const float* wt, long long ldw, const float* base, long long ldb, float* out, long long ldo,
+                   hipStream_t s) {
+  if (M <= 0 || N <= 0 || R < 1 || R > GRU_MAXR || C < 1 || N % 4 || ldw % 4 || ldb % 4 || ldo % 4 ||
+      (((uintptr_t)wt | (uintptr_t)base | (uintptr_t)out) & 15) || (long long)R * C * ldw >= (1LL << 31) ||
+      (long long)M * std::max(ldb, ldo) >= (1LL << 31)) {
+    dr_set_error("zgather_add: unsupported dims/alignment M=%d N=%d R=%d C=%d", M, N, R, C);
+    return DR_E_INVALID;
+  }
+  const dim3 grid((unsigned)((M + ZG_ROWS - 1) / ZG_ROWS), (unsigned)((N / 4 + 63) / 64));
+  hipLaunchKernelGGL(k_zgather_add, grid, dim3(256), 0, s, M, N, R, C, idx, zval, z, ldz, wt, ldw, base, ldb, out, ldo);
+  return dr_check_launch("zgather_add");
+}
+
 int op_gru_fused(const GruArgs& g, hipStream_t s) {
   if (g.R > GRU_MAXR || g.A > GRU_MAXA || g.B <= 0 || g.Hd <= 0 || g.Hd % 4 != 0 || g.ldh % 4 != 0 ||
       (((uintptr_t)g.h | (uintptr_t)g.w_hh | (uintptr_t)g.wt | (uintptr_t)g.b_ih | (uintptr_t)g.zval |
@@ -508,7 +585,7 @@ int op_gru_fused(const GruArgs& g, hipStream_t s) {
   if (g.gh_ws && g.B >= 128 && ((uintptr_t)g.gh_ws | (uintptr_t)g.hout | (uintptr_t)g.sr | (uintptr_t)g.su |
                                  (uintptr_t)g.sn | (uintptr_t)g.sghn) % 16 == 0 && g.ldo % 4 == 0) {
     // split path: hidden product on the tile GEMM, then gather + gates
-    if (g.h) {
+    if (g.h && !g.gh_ready) {
       GemmArgs p = gemm_args();
       p.M = g.B; p.N = 3 * g.Hd; p.K = g.Hd;
       p.A = g.h; p.lda = g.ldh; p.ksplitA = g.Hd;
