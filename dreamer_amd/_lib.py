@@ -10,6 +10,11 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdreamer_hip.so")
+# kernel A/B runs only (tools/build_variant.py): another build of the same
+# library, e.g. with a -D knob; never set on the product path
+if os.environ.get("DREAMER_LIB_VARIANT"):
+    LIB_PATH = os.path.join(os.path.dirname(_HERE), "tools", "variants",
+                            f"libdreamer_hip_{os.environ['DREAMER_LIB_VARIANT']}.so")
 
 fp = C.c_void_p  # device pointers
 

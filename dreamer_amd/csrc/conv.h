@@ -45,6 +45,12 @@ bool op_gemm_nt_split3_supported(int M, int N, int K, const float* A, int lda, c
                                  int ldy);
 int op_gemm_nt_split3(int M, int N, int K, const float* A, int lda, const float* A2, int lda2, int ksA, const void* wr,
                       const float* bias, int act, float* Y, int ldy, hipStream_t s);
+// the same with split-K partial sums in `part` (op_gemm_nt_split3_part_floats(M, N) floats,
+// 16-byte aligned) when the tile grid alone leaves the chip under-filled
+size_t op_gemm_nt_split3_part_floats(int M, int N);
+int op_gemm_nt_split3_sk(int M, int N, int K, const float* A, int lda, const float* A2, int lda2, int ksA,
+                         const void* wr, const float* bias, int act, float* Y, int ldy, float* part,
+                         size_t part_floats, hipStream_t s);
 
 // ---- conv_bf16.hip (bf16 perf mode; activations bf16, accumulation f32) ----
 // weights: Conv2d [co][ci][4][4] f32 -> bf16 [co][tap][cin_pad]; matrix slice -> bf16 [rows][cols]
@@ -133,3 +139,12 @@ int op_conv_wgrad(int n, int h, int w, int ca, int cb, const float* lo, int lda,
 size_t op_chan_sum_ws_floats(long long rows, int C);
 int op_chan_sum(long long rows, int C, const float* X, int ldx, float* out, int accumulate, float* ws, size_t ws_floats,
                 hipStream_t s);
+
+// TN products dW[m][n] = sum_k G[k][m] X[k][n] (Linear weight gradients over
+// K rows; X columns n >= nsplitB from X2[k][n - nsplitB]) f32-accurate on the
+// bf16 MFMA: both operands split3 once into planes, then a pre-split GEMM
+// (conv_split.hip).  Y (+)= dW with row stride ldy.
+size_t op_gemm_tn_split3_ws_bytes(int M, int N, int K);
+int op_gemm_tn_split3(int M, int N, int K, const float* G, long long ldg, const float* X, long long ldx,
+                      const float* X2, long long ldx2, int nsplitB, float* Y, long long ldy, int accumulate, void* ws,
+                      size_t ws_bytes, hipStream_t s);

@@ -25,6 +25,7 @@
 // read touches fall on 16 distinct 16-byte bank groups.
 #include "conv.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace {
@@ -313,193 +314,235 @@ int op_conv_repack_split3(int cout, int cin, const float* w, void* wr, hipStream
 // distinct bank quads, as in k_enc12_bf16), 110.8 KB; input rows 20 KB;
 // weight ring 2 x 12 KB.  One workgroup per CU.
 // ---------------------------------------------------------------------------
+#ifndef DR_E12_WAVES
+#define DR_E12_WAVES 8  // A/B knob (tools/build_variant.py): 4 = one wave per SIMD
+#endif
 #define E12_R2 8
 #define E12_R1 (2 * E12_R2 + 2)
 #define E12_RI (2 * E12_R1 + 2)
 #define E12_PS (E12_R1 * 32 + 1)
 #define E12_LWI 66
-static constexpr size_t e12_lds_bytes() {
-  return (size_t)3 * 4 * E12_PS * 16 + (size_t)E12_RI * E12_LWI * 8 + (size_t)2 * 3 * 64 * 4 * 16;
-}
+static constexpr size_t e12_lds_bytes() { return (size_t)3 * 4 * E12_PS * 16 + (size_t)E12_RI * E12_LWI * 8; }
 
-__global__ __launch_bounds__(256) void k_enc12_split3(int n, int nb, dr_frames src, const u16* __restrict__ wr1,
-                                                      const float* __restrict__ b1, const u16* __restrict__ wr2,
-                                                      const float* __restrict__ b2, float* __restrict__ out) {
+// NW = 8: two waves per SIMD -- waves 0-3 run conv2's taps 0-7 and waves 4-7
+// taps 8-15 over the same 64 x 32 output blocks, the two partial sums meet in
+// LDS (fixed order: taps 0-7 + taps 8-15) before the epilogue
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_enc12_split3(int n, int nb, dr_frames src, const u16* __restrict__ wr1,
+                                                          const float* __restrict__ b1, const u16* __restrict__ wr2,
+                                                          const float* __restrict__ b2, float* __restrict__ out) {
+  static_assert(NW == 4 || NW == 8, "enc12 waves");
+  constexpr int NTH = 64 * NW, TAPS = NW == 8 ? 8 : 16;
   constexpr int R2 = E12_R2, R1 = E12_R1, RI = E12_RI, PS = E12_PS, LWI = E12_LWI;
   constexpr int OW1 = 32, OW2 = 16, W = 64, H = 64, C1 = 32, C2 = 64;
   extern __shared__ __attribute__((aligned(16))) u32x4 e12_smem[];
   u32x4* c1o = e12_smem;                                                       // [3][4][PS]
   uint2* xin = reinterpret_cast<uint2*>(e12_smem + 3 * 4 * PS);               // [RI][LWI]
-  u32x4* wring = e12_smem + 3 * 4 * PS + (RI * LWI * 8) / 16;                  // [2][3][64][4]
-  const int f = blockIdx.x >> 1, ty = blockIdx.x & 1;
-  if (f >= n) return;
-  const int y2_0 = ty * R2, y1_0 = 2 * y2_0 - 1, iy0 = 2 * y1_0 - 1;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
-
-  // conv2 weight ring: tap t's three planes, [plane][cout][4 units], unit u of
-  // row n at u ^ swz(n); thread -> units tid, tid + 256, tid + 512
-  u32x4 rw[3];
-  auto wload = [&](int tap) __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int e = tid + 256 * k, pl = e >> 8, row = (e >> 2) & 63, u = e & 3;
-      rw[k] = *reinterpret_cast<const u32x4*>(wr2 + (((long long)tap * 3 + pl) * C2 + row) * 32 + 8 * u);
-    }
-  };
-  auto wstore = [&](int buf) __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int e = tid + 256 * k, pl = e >> 8, row = (e >> 2) & 63, u = e & 3;
-      wring[((buf * 3 + pl) * C2 + row) * 4 + (u ^ swz(row))] = rw[k];
-    }
-  };
-  wload(0);
-
-  // conv1 weights (A operand: lane -> channel 16 j + r, k = 32 s + 8 q .. + 7), three planes
-  u32x4 wa1[3][2][2];
-#pragma unroll
-  for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        wa1[pl][s][j] = *reinterpret_cast<const u32x4*>(wr1 + ((long long)pl * C1 + 16 * j + r) * 64 + 32 * s + 8 * q);
-  float bb1[2][4];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bb1[j][e] = b1[16 * j + 4 * q + e];
-
-  // ---- stage the input rows: bf16 of the centred pixel values ----
-  for (int i = tid; i < RI * LWI; i += 256) xin[i] = make_uint2(0u, 0u);
-  constexpr int W4 = W / 4, PERC = RI * W4, MAXI = (3 * PERC + 255) / 256;
-  const unsigned hw = (unsigned)(H * W);
-  const int b = f % nb, t = f / nb + src.t0;
-  const unsigned char* fr8 = src.ring + ((src.starts[b] + t) % src.ring_cap) * 3 * (long long)hw;
-  unsigned uv[MAXI];
-#pragma unroll
-  for (int k = 0; k < MAXI; ++k) {
-    const int i = tid + 256 * k;
-    const int c = i / PERC, rem = i - c * PERC, rr = rem / W4, x4 = rem - rr * W4;
-    const int y = iy0 + rr;
-    const bool ok = i < 3 * PERC && y >= 0 && y < H;
-    uv[k] = *reinterpret_cast<const unsigned*>(fr8 + (ok ? (unsigned)c * hw + (unsigned)(y * W + 4 * x4) : 0u));
-  }
-  const float centre = src.raw255 ? 127.5f : 0.0f, scale = src.raw255 ? 1.0f / 255.0f : 1.0f;
-  __syncthreads();
   u16* xs = reinterpret_cast<u16*>(xin);
-#pragma unroll
-  for (int k = 0; k < MAXI; ++k) {
-    const int i = tid + 256 * k;
-    const int c = i / PERC, rem = i - c * PERC, rr = rem / W4, x4 = rem - rr * W4;
-    const int y = iy0 + rr;
-    if (i >= 3 * PERC || y < 0 || y >= H) continue;
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      xs[(rr * LWI + 4 * x4 + e + 1) * 4 + c] = b16bits((__bf16)((float)((uv[k] >> (8 * e)) & 255u) - centre));
-  }
-  wstore(0);
-  __syncthreads();
-
-  // ---- conv1 over the R1 tile rows; rows outside the frame are conv2's zero padding ----
   u16* c1h = reinterpret_cast<u16*>(c1o);
-  constexpr int F1 = R1 * OW1 / 16;
-  for (int i = wave; i < F1; i += 4) {
-    const int p0 = 16 * i, yl = p0 / OW1, x1 = p0 - yl * OW1 + r, p = p0 + r;
-    const int y1 = y1_0 + yl;
-    uint2 hv[2], mv[2], lv[2];
-    if (y1 < 0 || y1 >= H / 2) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
+  const int ntiles = 2 * n;
+  int tile = blockIdx.x;
+  if (tile >= ntiles) return;
+
+  // ---- input rows: bf16 of the centred pixel values, [row][x + 1][4 ch] ----
+  // columns 0 / LWI - 1 and channel slot 3 are zero padding, written once here;
+  // every tile rewrites all other entries (zeros for rows outside the frame)
+  for (int i = tid; i < RI * LWI; i += NTH) xin[i] = make_uint2(0u, 0u);
+  constexpr int W4 = W / 4, PERC = RI * W4, MAXI = (3 * PERC + NTH - 1) / NTH;
+  const unsigned hw = (unsigned)(H * W);
+  const float centre = src.raw255 ? 127.5f : 0.0f, scale = src.raw255 ? 1.0f / 255.0f : 1.0f;
+  unsigned uv[MAXI];
+  auto in_load = [&](int tl) __attribute__((always_inline)) {
+    const int f = tl >> 1, iy0 = 2 * (2 * (tl & 1) * R2 - 1) - 1;
+    const int b = f % nb, t = f / nb + src.t0;
+    const unsigned char* fr8 = src.ring + ((src.starts[b] + t) % src.ring_cap) * 3 * (long long)hw;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) hv[j] = mv[j] = lv[j] = make_uint2(0u, 0u);
-    } else {
-      f32x4 acc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int t0 = 8 * s + 2 * q, ky = t0 >> 2, kx = t0 & 3;
-        const u32x4 pb = *reinterpret_cast<const u32x4*>(&xin[(2 * yl + ky) * LWI + 2 * x1 + kx]);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc[j] = mfma_b16(wa1[2][s][j], pb, acc[j]);
-          acc[j] = mfma_b16(wa1[1][s][j], pb, acc[j]);
-          acc[j] = mfma_b16(wa1[0][s][j], pb, acc[j]);
-        }
-      }
-      // lane: pixel p, channels 16 j + 4 q .. + 3
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(acc[j][e] * scale + bb1[j][e]);
-        split3_pair(v[0], v[1], hv[j].x, mv[j].x, lv[j].x);
-        split3_pair(v[2], v[3], hv[j].y, mv[j].y, lv[j].y);
-      }
+    for (int k = 0; k < MAXI; ++k) {
+      const int i = tid + NTH * k;
+      const int c = i / PERC, rem = i - c * PERC, rr = rem / W4, x4 = rem - rr * W4;
+      const int y = iy0 + rr;
+      const bool ok = i < 3 * PERC && y >= 0 && y < H;
+      uv[k] = *reinterpret_cast<const unsigned*>(fr8 + (ok ? (unsigned)c * hw + (unsigned)(y * W + 4 * x4) : 0u));
     }
+  };
+  auto in_store = [&](int tl) __attribute__((always_inline)) {
+    const int iy0 = 2 * (2 * (tl & 1) * R2 - 1) - 1;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int c8 = 2 * j + (q >> 1);
-      const int o = (c8 * PS + p) * 8 + (q & 1) * 4;  // u16 offset inside a plane
-      *reinterpret_cast<uint2*>(c1h + o) = hv[j];
-      *reinterpret_cast<uint2*>(c1h + 4 * PS * 8 + o) = mv[j];
-      *reinterpret_cast<uint2*>(c1h + 2 * 4 * PS * 8 + o) = lv[j];
+    for (int k = 0; k < MAXI; ++k) {
+      const int i = tid + NTH * k;
+      if (i >= 3 * PERC) continue;
+      const int c = i / PERC, rem = i - c * PERC, rr = rem / W4, x4 = rem - rr * W4;
+      const int y = iy0 + rr;
+      const bool ok = y >= 0 && y < H;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        xs[(rr * LWI + 4 * x4 + e + 1) * 4 + c] =
+            ok ? b16bits((__bf16)((float)((uv[k] >> (8 * e)) & 255u) - centre)) : (u16)0;
     }
-  }
+  };
+  in_load(tile);
+  __syncthreads();  // the zero fill before the stores of other threads
+  in_store(tile);
   __syncthreads();
 
-  // ---- conv2: K = 16 taps x 32 channels, one MFMA k-step per tap ----
-  const int ph = wave & 1, ch = wave >> 1;
-  const int fu = q ^ swz(r);  // weight rows 32 ch + 16 jj + r: swz(row) = swz(r)
-  f32x4 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int tap = 0; tap < 16; ++tap) {
-    const int buf = tap & 1, ky = tap >> 2, kx = tap & 3;
-    if (tap + 1 < 16) wload(tap + 1);
-    u32x4 wf[3][2], pf[3][4];
+  const int w4 = wave & 3, kh = wave >> 2, ph = w4 & 1, ch = w4 >> 1;
+  // conv2 weight fragments straight from L2 (the 196 KB of split planes stay
+  // resident): lane (r, q) of wf[pl][jj] = row 32 ch + 16 jj + r, k 8 q .. + 7
+  const u16* wbase = wr2 + ((long long)(32 * ch + r)) * 32 + 8 * q;
+  auto wld = [&](u32x4 (&wf)[3][2], int tap) __attribute__((always_inline)) {
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) wf[pl][jj] = wring[((buf * 3 + pl) * C2 + 32 * ch + 16 * jj + r) * 4 + fu];
-    const int x1 = 2 * r - 1 + kx;
-    const bool xok = x1 >= 0 && x1 < OW1;
+      for (int jj = 0; jj < 2; ++jj)
+        wf[pl][jj] = *reinterpret_cast<const u32x4*>(wbase + ((long long)(tap * 3 + pl) * C2 + 16 * jj) * 32);
+  };
+
+  for (;;) {
+    const int f = tile >> 1, y2_0 = (tile & 1) * R2, y1_0 = 2 * y2_0 - 1;
+    const int next = tile + (int)gridDim.x;
+    // conv1 weights (A operand: lane -> channel 16 j + r, k = 32 s + 8 q .. + 7), three
+    // planes: re-read per tile (L2) so that they hold no registers during conv2
+    u32x4 wa1[3][2][2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int yl = 2 * (4 * ph + i) + ky;
-      const int u = q * PS + yl * OW1 + (xok ? x1 : 0);
+    for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
-        const u32x4 v = c1o[pl * 4 * PS + u];
-        pf[pl][i] = xok ? v : (u32x4){0u, 0u, 0u, 0u};
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          wa1[pl][s][j] = *reinterpret_cast<const u32x4*>(wr1 + ((long long)pl * C1 + 16 * j + r) * 64 + 32 * s + 8 * q);
+    float bb1[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bb1[j][e] = b1[16 * j + 4 * q + e];
+    u32x4 wfa[3][2], wfb[3][2];
+    wld(wfa, TAPS * kh);
+    // ---- conv1 over the R1 tile rows; rows outside the frame are conv2's zero padding ----
+    constexpr int F1 = R1 * OW1 / 16;
+    for (int i = wave; i < F1; i += NW) {
+      const int p0 = 16 * i, yl = p0 / OW1, x1 = p0 - yl * OW1 + r, p = p0 + r;
+      const int y1 = y1_0 + yl;
+      uint2 hv[2], mv[2], lv[2];
+      if (y1 < 0 || y1 >= H / 2) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) hv[j] = mv[j] = lv[j] = make_uint2(0u, 0u);
+      } else {
+        f32x4 acc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int t0 = 8 * s + 2 * q, ky = t0 >> 2, kx = t0 & 3;
+          const u32x4 pb = *reinterpret_cast<const u32x4*>(&xin[(2 * yl + ky) * LWI + 2 * x1 + kx]);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            acc[j] = mfma_b16(wa1[2][s][j], pb, acc[j]);
+            acc[j] = mfma_b16(wa1[1][s][j], pb, acc[j]);
+            acc[j] = mfma_b16(wa1[0][s][j], pb, acc[j]);
+          }
+        }
+        // lane: pixel p, channels 16 j + 4 q .. + 3
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(acc[j][e] * scale + bb1[j][e]);
+          split3_pair(v[0], v[1], hv[j].x, mv[j].x, lv[j].x);
+          split3_pair(v[2], v[3], hv[j].y, mv[j].y, lv[j].y);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c8 = 2 * j + (q >> 1);
+        const int o = (c8 * PS + p) * 8 + (q & 1) * 4;  // u16 offset inside a plane
+        *reinterpret_cast<uint2*>(c1h + o) = hv[j];
+        *reinterpret_cast<uint2*>(c1h + 4 * PS * 8 + o) = mv[j];
+        *reinterpret_cast<uint2*>(c1h + 2 * 4 * PS * 8 + o) = lv[j];
       }
     }
-    // smallest terms first (weight plane x activation plane)
+    __syncthreads();
+    // the next tile's input rows: loads in flight under conv2 (xin is free now)
+    if (next < ntiles) in_load(next);
+
+    // ---- conv2: K = 16 taps x 32 channels, one MFMA k-step per tap; c1o is
+    // read-only here and the weights come from L2, so no barrier in the loop ----
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    auto tap_step = [&](int tap, u32x4 (&wf)[3][2], u32x4 (&wn)[3][2]) __attribute__((always_inline)) {
+      wld(wn, tap + 1 < TAPS * (kh + 1) ? tap + 1 : tap);  // one tap ahead (the last reload is unused)
+      const int ky = tap >> 2, kx = tap & 3;
+      const int x1 = 2 * r - 1 + kx;
+      const bool xok = x1 >= 0 && x1 < OW1;
+      u32x4 pf[3][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int yl = 2 * (4 * ph + i) + ky;
+        const int u = q * PS + yl * OW1 + (xok ? x1 : 0);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          const u32x4 v = c1o[pl * 4 * PS + u];
+          pf[pl][i] = xok ? v : (u32x4){0u, 0u, 0u, 0u};
+        }
+      }
+      // smallest terms first (weight plane x activation plane)
 #define E12_S3(PW, PA)                       \
   _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int jj = 0; jj < 2; ++jj) acc[i][jj] = \
       mfma_b16(wf[PW][jj], pf[PA][i], acc[i][jj]);
-    E12_S3(2, 0)
-    E12_S3(1, 1)
-    E12_S3(0, 2)
-    E12_S3(1, 0)
-    E12_S3(0, 1)
-    E12_S3(0, 0)
+      E12_S3(2, 0)
+      E12_S3(1, 1)
+      E12_S3(0, 2)
+      E12_S3(1, 0)
+      E12_S3(0, 1)
+      E12_S3(0, 0)
 #undef E12_S3
-    if (tap + 1 < 16) wstore(buf ^ 1);
-    dr_lds_barrier();
-  }
-  // lane (r, q) of acc[i][jj]: channels 32 ch + 16 jj + 4 q .. + 3 of conv2 pixel (row 4 ph + i, column r)
+    };
+#pragma unroll 1
+    for (int tap = TAPS * kh; tap < TAPS * (kh + 1); ++tap) {
+      tap_step(tap, wfa, wfb);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float* o = out + (((long long)f * OW2 + y2_0 + 4 * ph + i) * OW2 + r) * C2;
+      for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int co = 32 * ch + 16 * jj + 4 * q;
-      const f32x4 bv = *reinterpret_cast<const f32x4*>(b2 + co);
-      f32x4 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(acc[i][jj][e] + bv[e]);
-      *reinterpret_cast<f32x4*>(o + co) = v;
+        for (int jj = 0; jj < 2; ++jj) wfa[pl][jj] = wfb[pl][jj];
     }
+    if (NW == 8) {
+      // taps 8-15 partials through LDS (c1o is free once every wave is past conv2)
+      f32x4* red = reinterpret_cast<f32x4*>(e12_smem);  // [4 waves][8 blocks][64 lanes]
+      __syncthreads();
+      if (kh == 1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) red[(w4 * 8 + i * 2 + jj) * 64 + lane] = acc[i][jj];
+      }
+      __syncthreads();
+      if (kh == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) acc[i][jj] += red[(w4 * 8 + i * 2 + jj) * 64 + lane];
+      }
+    }
+    // lane (r, q) of acc[i][jj]: channels 32 ch + 16 jj + 4 q .. + 3 of conv2 pixel (row 4 ph + i, column r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (kh) break;
+      float* o = out + (((long long)f * OW2 + y2_0 + 4 * ph + i) * OW2 + r) * C2;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int co = 32 * ch + 16 * jj + 4 * q;
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(b2 + co);
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(acc[i][jj][e] + bv[e]);
+        *reinterpret_cast<f32x4*>(o + co) = v;
+      }
+    }
+    if (next >= ntiles) break;  // uniform over the workgroup: every wave leaves here
+    in_store(next);
+    __syncthreads();  // next input staged; every wave is past its conv2 reads of c1o
+    tile = next;
   }
 }
 
@@ -522,7 +565,9 @@ int op_enc12_split3(int n, int nb, int h, int w, int c1, int c2, const dr_frames
       (long long)n * 2 >= (1LL << 31))
     return DR_E_INVALID;
   static const bool raised = [] {
-    (void)hipFuncSetAttribute((const void*)k_enc12_split3, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_enc12_split3<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)e12_lds_bytes());
+    (void)hipFuncSetAttribute((const void*)k_enc12_split3<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)e12_lds_bytes());
     return true;
   }();
@@ -530,8 +575,21 @@ int op_enc12_split3(int n, int nb, int h, int w, int c1, int c2, const dr_frames
   hipLaunchKernelGGL(k_conv1_repack_split3, dim3((c1 * 64 + 255) / 256), dim3(256), 0, s, c1, w1, (u16*)wr1);
   DR_TRY(dr_check_launch("conv1_repack_split3"));
   DR_TRY(op_conv_repack_split3(c2, c1, w2, wr2, s));
-  hipLaunchKernelGGL(k_enc12_split3, dim3((unsigned)(n * 2)), dim3(256), e12_lds_bytes(), s, n, nb, *src,
-                     (const u16*)wr1, b1, (const u16*)wr2, b2, out);
+  // persistent: one workgroup per CU (the LDS allows no second), each walks
+  // tiles blockIdx.x, + gridDim.x, ... so that its next tile's input loads
+  // run under the current tile's conv2
+  static int cus[64];
+  int dev = 0;
+  DR_TRY_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return DR_E_INVALID;
+  if (cus[dev] == 0) DR_TRY_HIP(hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev));
+  const int grid = std::min(n * 2, std::max(1, cus[dev]));
+  if (DR_E12_WAVES == 8)
+    hipLaunchKernelGGL(k_enc12_split3<8>, dim3((unsigned)grid), dim3(512), e12_lds_bytes(), s, n, nb, *src,
+                       (const u16*)wr1, b1, (const u16*)wr2, b2, out);
+  else
+    hipLaunchKernelGGL(k_enc12_split3<4>, dim3((unsigned)grid), dim3(256), e12_lds_bytes(), s, n, nb, *src,
+                       (const u16*)wr1, b1, (const u16*)wr2, b2, out);
   return dr_check_launch("enc12_split3");
 }
 
@@ -1043,6 +1101,7 @@ int op_wgrad_split3(int n, int h, int w, int ca, int cb, const float* lo, int ld
 // aligned) in place of the im2col gather; W split once per call into planes
 // [K/32][3][Np][32] (Np = N rounded up to BN, zero rows past N).
 // ---------------------------------------------------------------------------
+#define DR_S3_SPLITS 8
 struct GemmS3 {
   int M, N, K, ksA, lda, lda2, ldy, act, Np;
   const float* A;
@@ -1050,6 +1109,8 @@ struct GemmS3 {
   const u16* wr;
   const float* bias;
   float* Y;
+  int splits;   // split-K over blockIdx.y (> 1: raw partial sums to part, k_s3_finish applies the epilogue)
+  float* part;  // [splits][M][N]
 };
 
 template <int BM, int BN>
@@ -1070,7 +1131,9 @@ __global__ __launch_bounds__(BM * 2) void k_gemm_split3(GemmS3 g) {
   const int m0 = (lt / tiles_n) * BM, n0 = (lt % tiles_n) * BN;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
   const int quad = tid & 7, prow = tid >> 3;
-  const int NCH = (K + 31) / 32;
+  const int NCH_ALL = (K + 31) / 32;
+  const int per = (NCH_ALL + g.splits - 1) / g.splits;
+  const int cb = min(NCH_ALL, (int)blockIdx.y * per), NCH = min(NCH_ALL, cb + per);  // chunks [cb, NCH)
   // per A row: element offsets of the row in both segments (rows past M read row M - 1)
   unsigned oa[APT], oa2[APT];
 #pragma unroll
@@ -1139,14 +1202,15 @@ __global__ __launch_bounds__(BM * 2) void k_gemm_split3(GemmS3 g) {
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
-  load(0, S0{});
-  load(min(1, NCH - 1), S1{});
+  if (cb < NCH) {
+  load(cb, S0{});
+  load(min(cb + 1, NCH - 1), S1{});
   store(S0{}, 0);
   __syncthreads();
   auto step = [&](int c, auto slot) __attribute__((always_inline)) {
     constexpr int SL = decltype(slot)::value;
     using Next = std::integral_constant<int, 1 - SL>;
-    const int buf = c & 1;
+    const int buf = (c - cb) & 1;
     load(min(c + 2, NCH - 1), slot);
     u32x4 av[3][FM], bv[3][FN];
 #pragma unroll
@@ -1169,12 +1233,13 @@ __global__ __launch_bounds__(BM * 2) void k_gemm_split3(GemmS3 g) {
     if (c + 1 < NCH) store(Next{}, buf ^ 1);
     dr_lds_barrier();
   };
-  int c = 0;
+  int c = cb;
   for (; c + 1 < NCH; c += 2) {
     step(c, S0{});
     step(c + 1, S1{});
   }
   if (c < NCH) step(c, S0{});
+  }
   // lane (r, q) of acc[i][j]: row m0 + wm0 + 16 i + r, columns n0 + wn0 + 16 j + 4 q .. + 3
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
@@ -1185,6 +1250,10 @@ __global__ __launch_bounds__(BM * 2) void k_gemm_split3(GemmS3 g) {
       const int n = n0 + wn0 + 16 * j + 4 * q;
       if (n >= N) continue;
       f32x4 v = acc[i][j];
+      if (g.splits > 1) {
+        *reinterpret_cast<f32x4*>(g.part + ((long long)blockIdx.y * M + m) * N + n) = v;
+        continue;
+      }
       if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + n);
       if (g.act == 1) {
 #pragma unroll
@@ -1193,6 +1262,22 @@ __global__ __launch_bounds__(BM * 2) void k_gemm_split3(GemmS3 g) {
       *reinterpret_cast<f32x4*>(g.Y + (long long)m * g.ldy + n) = v;
     }
   }
+}
+
+// split-K partial planes of k_gemm_split3 -> Y (fixed order over the splits), bias, activation
+__global__ void k_s3_finish(GemmS3 g) {
+  const long long i4 = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int N4 = g.N / 4;
+  if (i4 >= (long long)g.M * N4) return;
+  const int m = (int)(i4 / N4), n = 4 * (int)(i4 - (long long)m * N4);
+  f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int sp = 0; sp < g.splits; ++sp) v += *reinterpret_cast<const f32x4*>(g.part + ((long long)sp * g.M + m) * g.N + n);
+  if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + n);
+  if (g.act == 1) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = v[e] / (1.0f + expf(-v[e]));
+  }
+  *reinterpret_cast<f32x4*>(g.Y + (long long)m * g.ldy + n) = v;
 }
 
 // W [N][K] (row stride ldw) -> bf16 planes [K/32][3][Np][32], zero past N and K
@@ -1229,20 +1314,41 @@ bool op_gemm_nt_split3_supported(int M, int N, int K, const float* A, int lda, c
          (!seg || (ksA % 4 == 0 && lda2 % 4 == 0 && A2 && !((uintptr_t)A2 & 15))) &&
          (long long)M * lda < (1LL << 31) && (!seg || (long long)M * lda2 < (1LL << 31));
 }
+size_t op_gemm_nt_split3_part_floats(int M, int N) { return (size_t)DR_S3_SPLITS * M * N; }
+
 int op_gemm_nt_split3(int M, int N, int K, const float* A, int lda, const float* A2, int lda2, int ksA, const void* wr,
                       const float* bias, int act, float* Y, int ldy, hipStream_t s) {
+  return op_gemm_nt_split3_sk(M, N, K, A, lda, A2, lda2, ksA, wr, bias, act, Y, ldy, nullptr, 0, s);
+}
+
+int op_gemm_nt_split3_sk(int M, int N, int K, const float* A, int lda, const float* A2, int lda2, int ksA,
+                         const void* wr, const float* bias, int act, float* Y, int ldy, float* part,
+                         size_t part_floats, hipStream_t s) {
   if (!op_gemm_nt_split3_supported(M, N, K, A, lda, A2, lda2, ksA, ldy) || ((uintptr_t)Y & 15) ||
-      (bias && ((uintptr_t)bias & 15))) {
+      (bias && ((uintptr_t)bias & 15)) || ((uintptr_t)part & 15)) {
     dr_set_error("gemm_nt_split3: unsupported problem (M=%d N=%d K=%d)", M, N, K);
     return DR_E_INVALID;
   }
-  GemmS3 g = {M, N, K, ksA < K ? ksA : K, lda, lda2, ldy, act, s3_np(N), A, A2, (const u16*)wr, bias, Y};
+  GemmS3 g = {M, N, K, ksA < K ? ksA : K, lda, lda2, ldy, act, s3_np(N), A, A2, (const u16*)wr, bias, Y, 1, part};
   // the largest tile that still gives ~two waves per SIMD over the chip
   // (256 x 128, 256 x 64, 128 x 128, 128 x 64, else 64 x 64): taller / wider
   // tiles re-read less, but a half-empty chip costs more (M = 8192, N = 200:
   // 128 x 64 tiles gave 256 single-wave-per-SIMD workgroups)
   auto tl = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   auto waves = [&](int bm, int bn) { return (long long)tl(bm, bn) * (bm / 32); };
+  // split K while even the 64 x 64 grid is under ~2 waves per SIMD (N = 200
+  // products: the critic's / heads' first layers over 4096 rows, 512 waves),
+  // >= 8 chunks per split, when the caller brought partial-sum scratch
+  const int nch = (K + 31) / 32;
+  const bool small = waves(256, 128) < 2048 && waves(256, 64) < 2048 && waves(128, 128) < 2048 && waves(128, 64) < 2048;
+  if (part && small) {
+    int sp = 1;
+    while (sp < DR_S3_SPLITS && waves(64, 64) * sp * 2 <= 2048 && nch / (2 * sp) >= 8 &&
+           (size_t)(2 * sp) * M * N <= part_floats)
+      sp *= 2;
+    g.splits = sp;
+  }
+  const dim3 gy(1, (unsigned)g.splits);
   if (waves(256, 128) >= 2048)
     hipLaunchKernelGGL((k_gemm_split3<256, 128>), dim3(dr_xcd_grid(tl(256, 128))), dim3(512), 0, s, g);
   else if (waves(256, 64) >= 2048)
@@ -1252,6 +1358,256 @@ int op_gemm_nt_split3(int M, int N, int K, const float* A, int lda, const float*
   else if (waves(128, 64) >= 2048)
     hipLaunchKernelGGL((k_gemm_split3<128, 64>), dim3(dr_xcd_grid(tl(128, 64))), dim3(256), 0, s, g);
   else
-    hipLaunchKernelGGL((k_gemm_split3<64, 64>), dim3(dr_xcd_grid(tl(64, 64))), dim3(128), 0, s, g);
-  return dr_check_launch("gemm_nt_split3");
+    hipLaunchKernelGGL((k_gemm_split3<64, 64>), dim3(dr_xcd_grid(tl(64, 64)), g.splits), dim3(128), 0, s, g);
+  DR_TRY(dr_check_launch("gemm_nt_split3"));
+  if (g.splits > 1) {
+    hipLaunchKernelGGL(k_s3_finish, dim3((unsigned)(((long long)M * (N / 4) + 255) / 256)), dim3(256), 0, s, g);
+    DR_TRY(dr_check_launch("s3_finish"));
+  }
+  return DR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// TN products (the weight gradients of the Linears over many rows:
+// dW[m][n] = sum_k G[k][m] X[k][n], k = rows, WorldModel.training_step's
+// heads / decoder / posterior-scan layers, Agent.train_step's actor and
+// critic), f32-accurate on the bf16 MFMA.  Both operands are activations in
+// row-major [K][.] layout: each is split3 (truncation split) ONCE by a repack
+// pass into chunk-major planes [K/32][3][P][32] (P = M or N rounded up to
+// 128, zero past the edge and past K), so the GEMM loop stages both operands
+// as whole 16-byte units (no split VALU, no transpose in the loop), with the
+// k_gemm_split3 tile, swizzle and six-product order; split-K over workgroups
+// while the tile grid is under two workgroups per CU, partial planes reduced
+// in a fixed order.
+// ---------------------------------------------------------------------------
+static int s3_pad(int n) { return (n + 127) / 128 * 128; }
+
+// thread = (column n, 32-row chunk kc): 32 rows of one column (coalesced over
+// the threads of a row), split and written as three 64-byte plane runs
+__global__ __launch_bounds__(256) void k_kn_repack_split3(int K, int N, int P, const float* __restrict__ X, long long ldx,
+                                                          const float* __restrict__ X2, long long ldx2, int nsplit,
+                                                          u16* __restrict__ wr) {
+  const int n = blockIdx.x * 256 + threadIdx.x, kc = blockIdx.y;
+  if (n >= P) return;
+  const bool seg2 = n >= nsplit;
+  const float* src = seg2 ? X2 : X;
+  const long long ld = seg2 ? ldx2 : ldx;
+  const int nn = seg2 ? n - nsplit : n;
+  float v[32];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    const int kk = 32 * kc + k;
+    v[k] = (n < N && kk < K) ? src[(long long)kk * ld + nn] : 0.f;
+  }
+  u32x4 h[4], m[4], l[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      unsigned hh, mm, ll;
+      split3_pair(v[8 * u + 2 * e], v[8 * u + 2 * e + 1], hh, mm, ll);
+      h[u][e] = hh;
+      m[u][e] = mm;
+      l[u][e] = ll;
+    }
+  u32x4* o = reinterpret_cast<u32x4*>(wr + (((long long)kc * 3) * P + n) * 32);
+  const long long pl = (long long)P * 32 / 8;  // plane stride in u32x4 units
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    o[u] = h[u];
+    o[pl + u] = m[u];
+    o[2 * pl + u] = l[u];
+  }
+}
+
+struct GemmPP {
+  int M, N, K, Mp, Np, splits, accumulate;
+  long long ldy;
+  const u16* wa;  // planes of the A side (rows m), [K/32][3][Mp][32]
+  const u16* wb;  // planes of the B side (rows n), [K/32][3][Np][32]
+  float* Y;
+  float* part;    // splits > 1: [splits][M][N] partial sums
+};
+
+template <int BM, int BN>
+__global__ __launch_bounds__(BM * 2) void k_gemm_pp_split3(GemmPP g) {
+  constexpr int NT = BM * 2;
+  constexpr int WTN = BN / 2, FM = 4, FN = WTN / 16;
+  constexpr int AU = 3 * BM * 4, BU = 3 * BN * 4;
+  constexpr int APT = (AU + NT - 1) / NT, BPT = (BU + NT - 1) / NT;
+  static_assert(FN >= 1 && BM % 64 == 0, "gemm_pp tile");
+  __shared__ __attribute__((aligned(16))) u32x4 As[2][3][BM][4];
+  __shared__ __attribute__((aligned(16))) u32x4 Bs[2][3][BN][4];
+  const int M = g.M, N = g.N, Mp = g.Mp, Np = g.Np;
+  const int tiles_n = (N + BN - 1) / BN;
+  const int tiles = ((M + BM - 1) / BM) * tiles_n;
+  const int lt = dr_xcd_tile(blockIdx.x, tiles);
+  if (lt < 0) return;
+  const int m0 = (lt / tiles_n) * BM, n0 = (lt % tiles_n) * BN;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
+  const int NCH = (g.K + 31) / 32;
+  const int per = (NCH + g.splits - 1) / g.splits;
+  const int c0 = min(NCH, (int)blockIdx.y * per), c1 = min(NCH, c0 + per);
+  u32x4 ra0[APT], ra1[APT], rb0[BPT], rb1[BPT];
+  auto load = [&](int c, auto slot) __attribute__((always_inline)) {
+    u32x4* ra = decltype(slot)::value == 0 ? ra0 : ra1;
+    u32x4* rb = decltype(slot)::value == 0 ? rb0 : rb1;
+#pragma unroll
+    for (int j = 0; j < APT; ++j) {
+      const int e = tid + NT * j;
+      if (AU % NT == 0 || e < AU) {
+        const int pl = e / (BM * 4), rm = e - pl * BM * 4, row = rm >> 2, u = rm & 3;
+        ra[j] = *reinterpret_cast<const u32x4*>(g.wa + (((long long)c * 3 + pl) * Mp + m0 + row) * 32 + 8 * u);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      const int e = tid + NT * j;
+      if (BU % NT == 0 || e < BU) {
+        const int pl = e / (BN * 4), rm = e - pl * BN * 4, row = rm >> 2, u = rm & 3;
+        rb[j] = *reinterpret_cast<const u32x4*>(g.wb + (((long long)c * 3 + pl) * Np + n0 + row) * 32 + 8 * u);
+      }
+    }
+  };
+  auto store = [&](auto slot, int buf) __attribute__((always_inline)) {
+    const u32x4* ra = decltype(slot)::value == 0 ? ra0 : ra1;
+    const u32x4* rb = decltype(slot)::value == 0 ? rb0 : rb1;
+#pragma unroll
+    for (int j = 0; j < APT; ++j) {
+      const int e = tid + NT * j;
+      if (AU % NT == 0 || e < AU) {
+        const int pl = e / (BM * 4), rm = e - pl * BM * 4, row = rm >> 2, u = rm & 3;
+        As[buf][pl][row][u ^ swz(row)] = ra[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      const int e = tid + NT * j;
+      if (BU % NT == 0 || e < BU) {
+        const int pl = e / (BN * 4), rm = e - pl * BN * 4, row = rm >> 2, u = rm & 3;
+        Bs[buf][pl][row][u ^ swz(row)] = rb[j];
+      }
+    }
+  };
+  const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * WTN;
+  const int fu = q ^ swz(r);
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  if (c0 < c1) {
+    load(c0, S0{});
+    load(min(c0 + 1, c1 - 1), S1{});
+    store(S0{}, 0);
+    __syncthreads();
+    auto step = [&](int c, auto slot) __attribute__((always_inline)) {
+      constexpr int SL = decltype(slot)::value;
+      using Next = std::integral_constant<int, 1 - SL>;
+      const int buf = (c - c0) & 1;
+      load(min(c + 2, c1 - 1), slot);
+      u32x4 av[3][FM], bv[3][FN];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) av[pl][i] = As[buf][pl][wm0 + 16 * i + r][fu];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bv[pl][j] = Bs[buf][pl][wn0 + 16 * j + r][fu];
+      }
+#define DR_P3(PA, PB)                                                                                   \
+  _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
+      mfma_b16(bv[PB][j], av[PA][i], acc[i][j]);
+      DR_P3(2, 0)
+      DR_P3(1, 1)
+      DR_P3(0, 2)
+      DR_P3(1, 0)
+      DR_P3(0, 1)
+      DR_P3(0, 0)
+#undef DR_P3
+      if (c + 1 < c1) store(Next{}, buf ^ 1);
+      dr_lds_barrier();
+    };
+    int c = c0;
+    for (; c + 1 < c1; c += 2) {
+      step(c, S0{});
+      step(c + 1, S1{});
+    }
+    if (c < c1) step(c, S0{});
+  }
+  // lane (r, q) of acc[i][j]: row m0 + wm0 + 16 i + r, columns n0 + wn0 + 16 j + 4 q .. + 3
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wm0 + 16 * i + r;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + wn0 + 16 * j + 4 * q + e;
+        if (n >= N) continue;
+        if (g.splits > 1) {
+          g.part[((long long)blockIdx.y * M + m) * N + n] = acc[i][j][e];
+        } else {
+          float* y = g.Y + (long long)m * g.ldy + n;
+          *y = g.accumulate ? *y + acc[i][j][e] : acc[i][j][e];
+        }
+      }
+    }
+  }
+}
+
+__global__ void k_pp_finish(GemmPP g) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)g.M * g.N) return;
+  const int m = (int)(i / g.N), n = (int)(i - (long long)m * g.N);
+  float v = 0.f;
+  for (int sp = 0; sp < g.splits; ++sp) v += g.part[(long long)sp * g.M * g.N + i];
+  float* y = g.Y + (long long)m * g.ldy + n;
+  *y = g.accumulate ? *y + v : v;
+}
+
+#define DR_PP_SPLITS 8
+size_t op_gemm_tn_split3_ws_bytes(int M, int N, int K) {
+  const size_t kc = (size_t)((K + 31) / 32);
+  const size_t planes = kc * 32 * 3 * (size_t)(s3_pad(M) + s3_pad(N)) * sizeof(u16);
+  return planes + 256 + (size_t)DR_PP_SPLITS * M * N * sizeof(float);
+}
+
+int op_gemm_tn_split3(int M, int N, int K, const float* G, long long ldg, const float* X, long long ldx,
+                      const float* X2, long long ldx2, int nsplitB, float* Y, long long ldy, int accumulate, void* ws,
+                      size_t ws_bytes, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0 || !G || !X || !Y || (nsplitB < N && !X2) ||
+      ws_bytes < op_gemm_tn_split3_ws_bytes(M, N, K) || (long long)s3_pad(std::max(M, N)) * K * 3 >= (1LL << 31)) {
+    dr_set_error("gemm_tn_split3: unsupported problem (M=%d N=%d K=%d) or workspace too small", M, N, K);
+    return DR_E_INVALID;
+  }
+  const int KC = (K + 31) / 32, Mp = s3_pad(M), Np = s3_pad(N);
+  u16* wa = reinterpret_cast<u16*>(ws);
+  u16* wb = wa + (size_t)KC * 32 * 3 * Mp;
+  float* part = reinterpret_cast<float*>(((uintptr_t)(wb + (size_t)KC * 32 * 3 * Np) + 255) & ~(uintptr_t)255);
+  hipLaunchKernelGGL(k_kn_repack_split3, dim3((unsigned)((Mp + 255) / 256), (unsigned)KC), dim3(256), 0, s, K, M, Mp,
+                     G, ldg, G, ldg, M, wa);
+  DR_TRY(dr_check_launch("kn_repack_split3"));
+  hipLaunchKernelGGL(k_kn_repack_split3, dim3((unsigned)((Np + 255) / 256), (unsigned)KC), dim3(256), 0, s, K, N, Np,
+                     X, ldx, X2 ? X2 : X, ldx2, nsplitB < N ? nsplitB : N, wb);
+  DR_TRY(dr_check_launch("kn_repack_split3"));
+  auto tl = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  const bool big = tl(128, 64) >= 512;
+  const int tiles = big ? tl(128, 64) : tl(64, 64);
+  // split K while the grid is under two workgroups per CU, >= 8 chunks per split
+  int splits = 1;
+  while (splits < DR_PP_SPLITS && tiles * splits < 512 && KC / (2 * splits) >= 8) splits *= 2;
+  GemmPP g = {M, N, K, Mp, Np, splits, accumulate, ldy, wa, wb, Y, part};
+  if (big)
+    hipLaunchKernelGGL((k_gemm_pp_split3<128, 64>), dim3(dr_xcd_grid(tiles), splits), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((k_gemm_pp_split3<64, 64>), dim3(dr_xcd_grid(tiles), splits), dim3(128), 0, s, g);
+  DR_TRY(dr_check_launch("gemm_pp_split3"));
+  if (splits > 1) {
+    hipLaunchKernelGGL(k_pp_finish, dim3((unsigned)(((long long)M * N + 255) / 256)), dim3(256), 0, s, g);
+    DR_TRY(dr_check_launch("pp_finish"));
+  }
+  return DR_OK;
 }

@@ -20,6 +20,8 @@ struct EncWs {
   long long sk_n;
   void* wproj;  // bf16 mode: latent_mapper.0 feature columns as bf16 [enc_hidden][F]
   void* s3proj;  // fp32 mode: the same columns as split3 bf16 planes (op_nt_repack_split3)
+  float* s3part;  // fp32 mode: split-K partial sums of the projection
+  size_t s3part_n;
 };
 
 // bf16 mode stores activations / repacked weights as bf16 (2 bytes): the same
@@ -54,6 +56,8 @@ static void enc_carve(Carve& c, const dr_dims* d, int n, EncWs& w) {
   }
   w.wproj = bf ? c.raw((size_t)d->enc_hidden * enc_feat_dim(d) * 2) : nullptr;
   w.s3proj = bf ? nullptr : c.raw(op_nt_split3_ws_bytes(d->enc_hidden, enc_feat_dim(d)));
+  w.s3part_n = bf ? 0 : op_gemm_nt_split3_part_floats(n, d->enc_hidden);
+  w.s3part = bf ? nullptr : c.f((long long)w.s3part_n);
 }
 
 extern "C" size_t dr_encoder_workspace_bytes(const dr_dims* d, int n_frames) {
@@ -162,8 +166,8 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
       op_gemm_nt_split3_supported(n, d->enc_hidden, F, w.a[N - 1], F, nullptr, 0, F, d->enc_hidden)) {
     // latent_mapper.0's feature columns (VAE.py:57-75 -> WorldModel.py) on the split3 bf16 MFMA
     DR_TRY(op_nt_repack_split3(d->enc_hidden, F, wm->map0.w, F + d->hidden, w.s3proj, s));
-    return op_gemm_nt_split3(n, d->enc_hidden, F, w.a[N - 1], F, nullptr, 0, F, w.s3proj, wm->map0.b, 0, feat,
-                             d->enc_hidden, s);
+    return op_gemm_nt_split3_sk(n, d->enc_hidden, F, w.a[N - 1], F, nullptr, 0, F, w.s3proj, wm->map0.b, 0, feat,
+                                d->enc_hidden, w.s3part, w.s3part_n, s);
   }
   GemmArgs gp = lin(n, d->enc_hidden, F, w.a[N - 1], F, wm->map0.w, F + d->hidden, wm->map0.b, feat, d->enc_hidden);
   float* sk = w.sk;
@@ -297,6 +301,8 @@ struct ImWs {
   float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog, *rval, *wt, *wst, *bst;  // forward scratch
   float *tl0f, *hpart;  // forward: actor Linear 0 transposed ([Hd+L][a1]), its h-part + bias [B][a1]
   void *s3r, *s3c;  // split3 weight planes of the reward / continue heads' first Linear
+  float* s3part;    // their split-K partial sums
+  size_t s3part_n;
   int* idx[2];
   // backward
   float *gH, *gZ, *gA, *glog, *gx2, *gp2, *gx1, *gp1, *ggi, *ggh, *gheads, *gx2a, *gpre2a, *gy2a, *xh2a, *gx1a,
@@ -304,6 +310,8 @@ struct ImWs {
   long long sk_n;
   // transposed weights for the input-gradient GEMMs (NT with float4 loads)
   float *tl6p, *tl3p, *tl0p, *twhh, *thead, *tl3a, *tl0a;
+  void* tn;  // split3 TN scratch of the actor weight gradients (tn_launch)
+  size_t tn_bytes;
 };
 static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   const long long Bl = B, BH = (long long)B * H, B1 = (long long)B * (H + 1);
@@ -321,6 +329,8 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.rval = c.f(B1);
   w.s3r = c.raw(op_nt_split3_ws_bytes(d->rew_h1, d->hidden + L));
   w.s3c = c.raw(op_nt_split3_ws_bytes(d->cont_h1, d->hidden + L));
+  w.s3part_n = op_gemm_nt_split3_part_floats((int)B1, std::max(d->rew_h1, d->cont_h1));
+  w.s3part = c.f((long long)w.s3part_n);
   w.wt = c.f((long long)(L + A) * 3 * Hd);
   w.tl0f = c.f((long long)(Hd + L) * d->actor_h1);
   w.hpart = c.f(Bl * d->actor_h1);
@@ -359,6 +369,11 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.sk_n = splitk_floats(d->actor_h1, Hd + L) + splitk_floats(d->actor_h2, d->actor_h1) +
            2 * splitk_floats(A, d->actor_h2);
   w.sk = c.f(w.sk_n);
+  const int BHi = (int)BH;
+  w.tn_bytes = std::max(std::max(op_gemm_tn_split3_ws_bytes(d->actor_h1, Hd + L, BHi),
+                                 op_gemm_tn_split3_ws_bytes(d->actor_h2, d->actor_h1, BHi)),
+                        op_gemm_tn_split3_ws_bytes(A, d->actor_h2, BHi));
+  w.tn = c.raw(w.tn_bytes);
 }
 
 extern "C" size_t dr_imagine_workspace_bytes(const dr_dims* d, int B, int H) {
@@ -474,10 +489,10 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
         s3_first_layer(d, M1, d->cont_h1, hiddens, Hd, latents, L)) {
       DR_TRY(op_nt_repack_split3(d->rew_h1, Hd + L, wm->reward.l0.w, Hd + L, w.s3r, s));
       DR_TRY(op_nt_repack_split3(d->cont_h1, Hd + L, wm->cont.l0.w, Hd + L, w.s3c, s));
-      DR_TRY(op_gemm_nt_split3(M1, d->rew_h1, Hd + L, hiddens, Hd, latents, L, Hd, w.s3r, wm->reward.l0.b, 0, w.p1r,
-                               d->rew_h1, s));
-      DR_TRY(op_gemm_nt_split3(M1, d->cont_h1, Hd + L, hiddens, Hd, latents, L, Hd, w.s3c, wm->cont.l0.b, 0, w.p1c,
-                               d->cont_h1, s));
+      DR_TRY(op_gemm_nt_split3_sk(M1, d->rew_h1, Hd + L, hiddens, Hd, latents, L, Hd, w.s3r, wm->reward.l0.b, 0,
+                                  w.p1r, d->rew_h1, w.s3part, w.s3part_n, s));
+      DR_TRY(op_gemm_nt_split3_sk(M1, d->cont_h1, Hd + L, hiddens, Hd, latents, L, Hd, w.s3c, wm->cont.l0.b, 0,
+                                  w.p1c, d->cont_h1, w.s3part, w.s3part_n, s));
     } else {
       p[0] = lin2(M1, d->rew_h1, hiddens, Hd, Hd, latents, L, L, wm->reward.l0.w, wm->reward.l0.b, w.p1r, d->rew_h1);
       p[1] = lin2(M1, d->cont_h1, hiddens, Hd, Hd, latents, L, L, wm->cont.l0.w, wm->cont.l0.b, w.p1c, d->cont_h1);
@@ -683,7 +698,7 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
     float* sk = w.sk;
     long long skn = w.sk_n;
     for (int i = 0; i < 4; ++i) give_splitk(p[i], sk, skn);
-    DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 4, s));
+    DR_TRY(tn_launch(p, 4, w.tn, w.tn_bytes, s));
   }
   {
     ColsumJob cj[8] = {
@@ -724,7 +739,8 @@ static size_t critic_ws_bytes(const dr_dims* d, int M) {
   ctape_carve(c, d, M, t);
   c.f(splitk_floats(M, d->critic_h1));
   c.raw(op_nt_split3_ws_bytes(d->critic_h1, d->hidden + latent(d)));
-  return c.off;
+  c.f((long long)op_gemm_nt_split3_part_floats(M, d->critic_h1));
+  return c.off + 256;
 }
 
 
@@ -737,6 +753,8 @@ extern "C" int dr_critic_fwd(const dr_dims* d, const dr_critic* cr, int M, const
   float* sk = nullptr;
   long long skn = 0;
   void* s3w = nullptr;  // split3 weight planes of value_net.0 (fp32 mode)
+  float* s3part = nullptr;  // and their split-K partial sums, when the workspace holds them
+  size_t s3part_n = 0;
   if (tape) {
     Carve c(tape);
     ctape_carve(c, d, M, t);
@@ -755,13 +773,19 @@ extern "C" int dr_critic_fwd(const dr_dims* d, const dr_critic* cr, int M, const
       sk = c.f(skn);
       const size_t pb = op_nt_split3_ws_bytes(d->critic_h1, d->hidden + latent(d));
       if (c.off + pb + 256 <= ws_bytes) s3w = c.raw(pb);
+      const size_t pn = op_gemm_nt_split3_part_floats(M, d->critic_h1);
+      if (s3w && c.off + pn * sizeof(float) + 256 <= ws_bytes) {
+        s3part = c.f((long long)pn);
+        s3part_n = pn;
+      }
     }
   }
   DR_REQUIRE(tape || ws, "dr_critic_fwd needs a tape or a workspace");
   const int L = latent(d), Hd = d->hidden, c1 = d->critic_h1, c2 = d->critic_h2, nb = d->buckets;
   if (s3w && s3_first_layer(d, M, c1, h, ldh, z, ldz)) {
     DR_TRY(op_nt_repack_split3(c1, Hd + L, cr->net.l0.w, Hd + L, s3w, s));
-    DR_TRY(op_gemm_nt_split3(M, c1, Hd + L, h, (int)ldh, z, (int)ldz, Hd, s3w, cr->net.l0.b, 0, t.pre1, c1, s));
+    DR_TRY(op_gemm_nt_split3_sk(M, c1, Hd + L, h, (int)ldh, z, (int)ldz, Hd, s3w, cr->net.l0.b, 0, t.pre1, c1,
+                                s3part, s3part_n, s));
   } else {
     GemmArgs g1 = lin2(M, c1, h, ldh, Hd, z, ldz, L, cr->net.l0.w, cr->net.l0.b, t.pre1, c1);
     give_splitk(g1, sk, skn);
@@ -784,9 +808,15 @@ struct CBws {
   float *tl6, *tl3;  // transposed value_net.6 / .3 weights
   float* sk;         // split-K partials of the weight-gradient GEMMs
   long long sk_n;
+  void* tn;          // split3 TN scratch (tn_launch)
+  size_t tn_bytes;
 };
 static void cbws_carve(Carve& c, const dr_dims* d, int B, int H, CBws& w) {
   const long long M = (long long)B * (H + 1);
+  w.tn_bytes = std::max(std::max(op_gemm_tn_split3_ws_bytes(d->buckets, d->critic_h2, (int)M),
+                                 op_gemm_tn_split3_ws_bytes(d->critic_h2, d->critic_h1, (int)M)),
+                        op_gemm_tn_split3_ws_bytes(d->critic_h1, d->hidden + latent(d), (int)M));
+  w.tn = c.raw(w.tn_bytes);
   w.row_loss = c.f((long long)B * H);
   w.sk_n = splitk_floats(d->buckets, d->critic_h2) + splitk_floats(d->critic_h2, d->critic_h1) +
            splitk_floats(d->critic_h1, d->hidden + latent(d));
@@ -846,7 +876,7 @@ extern "C" int dr_critic_loss_bwd(const dr_dims* d, const dr_critic* cr, int B, 
     float* sk = w.sk;
     long long skn = w.sk_n;
     for (int i = 0; i < 3; ++i) give_splitk(p[i], sk, skn);
-    DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 3, s));
+    DR_TRY(tn_launch(p, 3, w.tn, w.tn_bytes, s));
   }
   {
     ColsumJob cj[7] = {

@@ -170,6 +170,24 @@ static inline GemmArgs bwd_w(int out, int in, int R, const float* G, long long l
   return g;
 }
 
+// weight-gradient (TN) problems built by bwd_w: on the split3 bf16 MFMA
+// (op_gemm_tn_split3, one problem after another through the same scratch)
+// when `ws` holds every problem's planes, else one grouped f32 tile launch
+static inline bool tn_split3_ok(const GemmArgs& g) {
+  return g.alpha == 1.0f && !g.act && !g.bias && !g.addend && g.ksplitB >= g.K && g.nsplitY >= g.N && !g.out_conv &&
+         g.ksplitA >= g.K && g.epi == EPI_NONE && g.M > 0 && g.N > 0 && g.K > 0;
+}
+static inline int tn_launch(const GemmArgs* p, int n, void* ws, size_t ws_bytes, hipStream_t s) {
+  bool ok = ws != nullptr;
+  for (int i = 0; i < n && ok; ++i) ok = tn_split3_ok(p[i]) && op_gemm_tn_split3_ws_bytes(p[i].M, p[i].N, p[i].K) <= ws_bytes;
+  if (!ok) return gemm_launch(G_TN, AM_PLAIN, p, n, s);
+  for (int i = 0; i < n; ++i) {
+    const GemmArgs& g = p[i];
+    DR_TRY(op_gemm_tn_split3(g.M, g.N, g.K, g.A, g.lda, g.W, g.ldb, g.W2, g.ldb2, g.nsplitB < g.N ? g.nsplitB : g.N,
+                             g.Y, g.ldy, g.accumulate, ws, ws_bytes, s));
+  }
+  return DR_OK;
+}
 
 // one-hot index buffers hold [B][R] class indices followed by the [B][R]
 // straight-through values at those indices (what the fused GRU gathers)

@@ -283,6 +283,8 @@ struct MlpBwd {  // backward scratch of one 3-layer head (and its LayerNorm save
   float *gx2, *gp2, *gy2, *xh2, *gx1, *gp1, *gy1, *xh1;
 };
 struct WmWs {
+  void* tn;         // split3 TN scratch (tn_launch)
+  size_t tn_bytes;
   // encoder (all M frames): conv k's pre-activation (NHWC) and output (NHWC; the last NCHW = the flatten order)
   float *x0, *pre[DR_MAX_DEPTH], *a[DR_MAX_DEPTH], *feat;
   float *wr[DR_MAX_DEPTH], *wqe[DR_MAX_DEPTH];  // conv k repacked (forward) / as a convT (data gradient, k >= 1)
@@ -502,6 +504,19 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
     w.sk_n = mx;
     w.sk = c.f(w.sk_n);
   }
+  {
+    // split3 TN scratch: the largest weight-gradient problem over K = M rows
+    const int hd = D.Hd, L = D.L, eh = D.eh;
+    const int mn[][2] = {{D.nb, D.rh2}, {D.rh2, D.rh1}, {D.rh1, hd + L}, {1, D.ch2}, {D.ch2, D.ch1}, {D.ch1, hd + L},
+                         {L, D.ph2}, {D.ph2, D.ph1}, {D.ph1, hd + L}, {D.Fd, D.dh}, {D.dh, hd + L}, {L, eh},
+                         {eh, D.F + hd}, {3 * hd, L + D.A}, {3 * hd, hd}, {D.Dv, D.Fd}, {D.Fd, D.Fd}, {D.F, D.F},
+                         {D.F, D.Dv}};
+    size_t mx = 0;
+    for (const auto& q : mn)
+      if (q[0] > 0 && q[1] > 0) mx = std::max(mx, op_gemm_tn_split3_ws_bytes(q[0], q[1], M));
+    w.tn_bytes = mx;
+    w.tn = c.raw(mx);
+  }
 }
 
 extern "C" size_t dr_wm_train_workspace_bytes(const dr_dims* d, int B, int T) {
@@ -518,7 +533,7 @@ extern "C" size_t dr_wm_train_workspace_bytes(const dr_dims* d, int B, int T) {
 static int head_bwd(const WmDims& D, const dr_mlp3& m, const dr_mlp3& g, int w1, int w2, int nout, const float* glog,
                     const float* t6, const float* t3, const float* t0, const float* x1, const float* x2,
                     const float* pre1, const float* pre2, int in_z, const float* hB, const float* zB, float* gHB,
-                    float* gZB, MlpBwd& b, float* sk, long long sk_n, hipStream_t s) {
+                    float* gZB, MlpBwd& b, float* sk, long long sk_n, void* tn, size_t tn_bytes, hipStream_t s) {
   const int M1 = D.M1, Hd = D.Hd, L = D.L;
   DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M1, w2, nout, glog, nout, t6, b.gx2, w2, 0), s));
   DR_TRY(lnbwd_nt(M1, w1, w2, b.gx2, w2, pre2, w2, m.n4, t3, b.gx1, w1, 0, b.gp2, w2, b.gy2, b.xh2, nullptr, 0,
@@ -533,7 +548,7 @@ static int head_bwd(const WmDims& D, const dr_mlp3& m, const dr_mlp3& g, int w1,
     p[2].W2 = zB; p[2].ldb2 = L; p[2].nsplitB = Hd;
   }
   splitk_all(p, 3, sk, sk_n);
-  DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 3, s));
+  DR_TRY(tn_launch(p, 3, tn, tn_bytes, s));
   ColsumJob cj[7] = {
       {nout, glog, nout, nullptr, 0, g.l6.b}, {w2, b.gp2, w2, nullptr, 0, g.l3.b},
       {w2, b.gy2, w2, b.xh2, w2, g.n4.w},     {w2, b.gy2, w2, nullptr, 0, g.n4.b},
@@ -659,6 +674,9 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
 
   // ---- posterior scan (unroll_model, WorldModel.py:97-107) ----
   const long long idx_stride = 2LL * B * R;
+  // B >= 128 (split GRU): the next step's hidden product h W_hh^T + b_hh rides
+  // in the same grouped launch as latent_mapper.0 (both read only h_t)
+  bool gh_pre = false;
   for (int t = 0; t < T; ++t) {
     const long long rb = (long long)t * B;
     float* h_t = w.h_all + rb * Hd;
@@ -668,12 +686,16 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
                       Hd, w.gi, w.gh, w.sr, w.su, w.sn, w.sghn, s));
     } else {
       DR_TRY(gru_onehot(d, wm, B, w.idx + (t - 1) * idx_stride, w.act_tm + (rb - B) * A, A, h_t - (long long)B * Hd,
-                        Hd, h_t, Hd, w.wt, w.sr + rb * Hd, w.su + rb * Hd, w.sn + rb * Hd, w.sghn + rb * Hd, s));
+                        Hd, h_t, Hd, w.wt, w.sr + rb * Hd, w.su + rb * Hd, w.sn + rb * Hd, w.sghn + rb * Hd, s,
+                        nullptr, 0, w.gh, gh_pre));
     }
-    GemmArgs g = lin(B, eh, Hd, h_t, Hd, wm->map0.w + F, F + Hd, nullptr, w.pre_m + rb * eh, eh);
-    g.addend = w.feat + rb * eh;
-    g.ld_add = eh;
-    DR_TRY(run(G_NT, AM_PLAIN, g, s));
+    GemmArgs g[2];
+    g[0] = lin(B, eh, Hd, h_t, Hd, wm->map0.w + F, F + Hd, nullptr, w.pre_m + rb * eh, eh);
+    g[0].addend = w.feat + rb * eh;
+    g[0].ld_add = eh;
+    gh_pre = B >= 128 && t + 1 < T;
+    if (gh_pre) g[1] = lin(B, 3 * Hd, Hd, h_t, Hd, wm->w_hh, Hd, wm->b_hh, w.gh, 3 * Hd);
+    DR_TRY(gemm_launch(G_NT, AM_PLAIN, g, gh_pre ? 2 : 1, s));
     GemmArgs gp = lin_ln(B, L, eh, w.pre_m + rb * eh, eh, wm->map1, wm->map3.w, wm->map3.b, w.plog + rb * L, L);
     gp.a_out = w.x_m + rb * eh;
     gp.ld_aout = eh;
@@ -790,11 +812,11 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   DR_TRY(zero(w.gH, (long long)M * Hd, s));
   DR_TRY(zero(w.gZ, (long long)M * L, s));
   DR_TRY(head_bwd(D, wm->prior, gw->prior, D.ph1, D.ph2, L, w.g_prior, w.t_pl6, w.t_pl3, w.t_pl0, w.px1, w.px2, w.pp1,
-                  w.pp2, 0, hB, zB, gHB, gZB, w.bp, w.sk, w.sk_n, s));
+                  w.pp2, 0, hB, zB, gHB, gZB, w.bp, w.sk, w.sk_n, w.tn, w.tn_bytes, s));
   DR_TRY(head_bwd(D, wm->reward, gw->reward, D.rh1, D.rh2, nb, w.g_rew, w.t_rl6, w.t_rl3, w.t_rl0, w.rx1, w.rx2, w.rp1,
-                  w.rp2, 1, hB, zB, gHB, gZB, w.br, w.sk, w.sk_n, s));
+                  w.rp2, 1, hB, zB, gHB, gZB, w.br, w.sk, w.sk_n, w.tn, w.tn_bytes, s));
   DR_TRY(head_bwd(D, wm->cont, gw->cont, D.ch1, D.ch2, 1, w.g_cont, w.t_cl6, w.t_cl3, w.t_cl0, w.cx1, w.cx2, w.cp1,
-                  w.cp2, 1, hB, zB, gHB, gZB, w.bc, w.sk, w.sk_n, s));
+                  w.cp2, 1, hB, zB, gHB, gZB, w.bc, w.sk, w.sk_n, w.tn, w.tn_bytes, s));
   // decoder: image_builder.6 .. .0 (data grads as strided convs, weight grads, bias sums)
   if (vec) {
     // image_builder stand-in backward: dgout = dL/dmu -> Wd2 / bd2 grads, dL/dq = (dgout Wd2) SiLU'(q)
@@ -815,7 +837,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     p[0] = bwd_w(Dv, D.Fd, M1, w.dgout, Dv, w.dqp[0], D.Fd, gd->convt[1].w);
     p[1] = bwd_w(D.Fd, D.Fd, M1, w.dgq[0], D.Fd, w.du2p, D.Fd, gd->convt[0].w);
     splitk_all(p, 2, w.sk, w.sk_n);
-    DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 2, s));
+    DR_TRY(tn_launch(p, 2, w.tn, w.tn_bytes, s));
     ColsumJob cj[2] = {{Dv, w.dgout, Dv, nullptr, 0, gd->convt[1].b}, {D.Fd, w.dgq[0], D.Fd, nullptr, 0, gd->convt[0].b}};
     DR_TRY(op_colsum_multi(M1, cj, 2, s));
   } else {
@@ -851,7 +873,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     p[1] = bwd_w(D.dh, Hd + L, M1, w.gpu, D.dh, hB, Hd, gd->up0.w);
     p[1].W2 = zB; p[1].ldb2 = L; p[1].nsplitB = Hd;
     splitk_all(p, 2, w.sk, w.sk_n);
-    DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 2, s));
+    DR_TRY(tn_launch(p, 2, w.tn, w.tn_bytes, s));
     ColsumJob cj[4] = {
         {D.Fd, w.dgu2, D.Fd, nullptr, 0, w.db3p},
         {D.dh, w.gpu, D.dh, nullptr, 0, gd->up0.b},
@@ -901,7 +923,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     p[2].W2 = w.act_tm; p[2].ldb2 = A; p[2].nsplitB = L;
     p[3] = bwd_w(3 * Hd, Hd, M1, w.ggh + (long long)B * 3 * Hd, 3 * Hd, w.h_all, Hd, gw->w_hh);
     splitk_all(p, 4, w.sk, w.sk_n);
-    DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 4, s));
+    DR_TRY(tn_launch(p, 4, w.tn, w.tn_bytes, s));
     ColsumJob cj[6] = {
         {L, w.glog, L, nullptr, 0, gw->map3.b},       {eh, w.gpre_m, eh, nullptr, 0, gw->map0.b},
         {eh, w.gy_m, eh, w.xh_m, eh, gw->map1.w},     {eh, w.gy_m, eh, nullptr, 0, gw->map1.b},
@@ -930,7 +952,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     p[0] = bwd_w(F, F, M, gL, F, w.a[0], F, gw->conv[1].w);
     p[1] = bwd_w(F, Dv, M, w.gp[0], F, w.x0, Dv, gw->conv[0].w);
     splitk_all(p, 2, w.sk, w.sk_n);
-    DR_TRY(gemm_launch(G_TN, AM_PLAIN, p, 2, s));
+    DR_TRY(tn_launch(p, 2, w.tn, w.tn_bytes, s));
     ColsumJob cj[2] = {{F, gL, F, nullptr, 0, gw->conv[1].b}, {F, w.gp[0], F, nullptr, 0, gw->conv[0].b}};
     DR_TRY(op_colsum_multi(M, cj, 2, s));
   } else {

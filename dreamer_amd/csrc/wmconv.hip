@@ -730,6 +730,57 @@ __global__ __launch_bounds__(256) void k_chan_sum_part(long long rows, int C, in
   }
 }
 
+// the same partial sums with 16-byte loads: thread = (row lane, 4 channels),
+// eight rows in flight per thread (independent accumulators, fixed order).
+// Needs ldx % 4 == 0, a 16-byte aligned X and the padded channel quads inside
+// the row (rows of the world-model gradient tensors: C = 3 at stride 4, 32..256)
+__global__ __launch_bounds__(256) void k_chan_sum_part4(long long rows, int C, int Cp, const float* __restrict__ X,
+                                                        int ldx, long long chunk, float* __restrict__ part) {
+  constexpr int U = 8;
+  __shared__ float4 red[256];
+  const int tid = threadIdx.x, tpr = Cp >> 2, rpi = 256 / tpr;
+  const int c0 = 4 * (tid % tpr), rl = tid / tpr;
+  const long long r0 = (long long)blockIdx.x * chunk;
+  const long long r1 = r0 + chunk < rows ? r0 + chunk : rows;
+  float4 acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c0 < C) {
+    long long rr = r0 + rl;
+    for (; rr + (long long)(U - 1) * rpi < r1; rr += (long long)U * rpi) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const float4*>(X + (rr + (long long)u * rpi) * ldx + c0);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
+      }
+    }
+    for (; rr < r1; rr += rpi) {
+      const float4 v = *reinterpret_cast<const float4*>(X + rr * ldx + c0);
+      acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
+    }
+  }
+  float4 t = acc[0];
+#pragma unroll
+  for (int u = 1; u < U; ++u) {
+    t.x += acc[u].x; t.y += acc[u].y; t.z += acc[u].z; t.w += acc[u].w;
+  }
+  red[tid] = t;
+  __syncthreads();
+  if (tid < tpr) {
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < rpi; ++k) {
+      const float4 v = red[k * tpr + tid];
+      q.x += v.x; q.y += v.y; q.z += v.z; q.w += v.w;
+    }
+    const float qs[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (c0 + e < C) part[(long long)blockIdx.x * C + c0 + e] = qs[e];
+  }
+}
+
 // one workgroup per channel: strided partial sums, then a fixed-order tree
 __global__ __launch_bounds__(256) void k_chan_sum_final(int nb, int C, const float* __restrict__ part,
                                                         float* __restrict__ out, int accumulate) {
@@ -760,7 +811,11 @@ int op_chan_sum(long long rows, int C, const float* X, int ldx, float* out, int 
     return DR_E_WORKSPACE;
   }
   const long long chunk = (rows + nb - 1) / nb;
-  hipLaunchKernelGGL(k_chan_sum_part, dim3(nb), dim3(256), 0, s, rows, C, chan_pow2(C), X, ldx, chunk, ws);
+  const int cp4 = chan_pow2(C < 4 ? 4 : C);
+  if (ldx % 4 == 0 && ((uintptr_t)X & 15) == 0 && ldx >= ((C + 3) & ~3))
+    hipLaunchKernelGGL(k_chan_sum_part4, dim3(nb), dim3(256), 0, s, rows, C, cp4, X, ldx, chunk, ws);
+  else
+    hipLaunchKernelGGL(k_chan_sum_part, dim3(nb), dim3(256), 0, s, rows, C, chan_pow2(C), X, ldx, chunk, ws);
   DR_TRY(dr_check_launch("chan_sum_part"));
   hipLaunchKernelGGL(k_chan_sum_final, dim3(C), dim3(256), 0, s, nb, C, ws, out, accumulate);
   return dr_check_launch("chan_sum_final");
