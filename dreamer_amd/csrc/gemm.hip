@@ -2336,7 +2336,12 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
     // weight gradients (TN) and tall, deep products go to the tile kernel --
     // when it can fill the chip: a per-step product at B = 256 (16 tiles of
     // 64 x 64, no split-K scratch) runs on 52+ skinny 64-row workgroups instead
-    if (A_KM || (maxM >= 256 && minK >= 512 && (ws || tiles >= 128) && g_tile_variant != 26) ||
+    // tall products with a small K (M >= 1024: the world-model heads' and
+    // decoder's layers over B (T - 1) rows, the critic's over B (H + 1)): the
+    // 64-row skinny tiles re-read the weights per row tile and run 16 columns
+    // per workgroup (480 us for the decoder's 3584 x 4096 x 200 product)
+    const bool tall = !A_KM && !B_KN && maxM >= 1024 && tiles >= 256 && g_tile_variant == 0;
+    if (A_KM || (maxM >= 256 && minK >= 512 && (ws || tiles >= 128) && g_tile_variant != 26) || tall ||
         (g_tile_variant >= 4 && g_tile_variant < 26 && maxM >= 128)) {
       GemmBatch gt = gb;
       // tall NT products with a deep K (the encoder feature projection, the
@@ -2430,10 +2435,92 @@ static int launch_ln_sample(const GemmArgs& g, hipStream_t s) {
   }
 }
 
+// SiLU(LayerNorm(x)) of whole rows, one wave per row: the staged prologue of
+// k_gemm_skinny (same lane -> k mapping and summation order, so the same
+// values) as its own pass for tall products, whose consumers then run a plain
+// tile GEMM on the result instead of re-normalising the rows per column tile
+template <int LNV>
+__global__ __launch_bounds__(256) void k_ln_silu_rows(int M, int K, const float* __restrict__ X, int ldx,
+                                                      const float* __restrict__ gam, const float* __restrict__ bet,
+                                                      float* __restrict__ Y, int ldy) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + wave;
+  if (m >= M) return;  // whole waves: wave_sum stays within a live wave
+  const int K4 = K >> 2;
+  float4 xv[LNV], gv[LNV], bv[LNV];
+#pragma unroll
+  for (int i = 0; i < LNV; ++i) {
+    const int k4 = lane + 64 * i;
+    const bool ok = k4 < K4;
+    xv[i] = ok ? *reinterpret_cast<const float4*>(X + (long long)m * ldx + 4 * k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gv[i] = ok ? *reinterpret_cast<const float4*>(gam + 4 * k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bv[i] = ok ? *reinterpret_cast<const float4*>(bet + 4 * k4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float sm = 0.f;
+#pragma unroll
+  for (int i = 0; i < LNV; ++i) sm += (xv[i].x + xv[i].y) + (xv[i].z + xv[i].w);
+  const float mean = wave_sum(sm) / (float)K;
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < LNV; ++i) {
+    if (lane + 64 * i < K4) {
+      const float dx = xv[i].x - mean, dy = xv[i].y - mean, dz = xv[i].z - mean, dw = xv[i].w - mean;
+      sq += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+    }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)K + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < LNV; ++i) {
+    const int k4 = lane + 64 * i;
+    if (k4 < K4) {
+      float4 y;
+      y.x = dr_silu_fast((xv[i].x - mean) * rstd * gv[i].x + bv[i].x);
+      y.y = dr_silu_fast((xv[i].y - mean) * rstd * gv[i].y + bv[i].y);
+      y.z = dr_silu_fast((xv[i].z - mean) * rstd * gv[i].z + bv[i].z);
+      y.w = dr_silu_fast((xv[i].w - mean) * rstd * gv[i].w + bv[i].w);
+      *reinterpret_cast<float4*>(Y + (long long)m * ldy + 4 * k4) = y;
+    }
+  }
+}
+
+// tall LN-SiLU products (M >= 1024 rows: the world-model heads / decoder over
+// B (T - 1) rows, the critic over B (H + 1)) whose transformed rows are saved
+// anyway (a_out): normalise once, then the plain GEMM on the saved rows
+static bool tall_ln_ok(const GemmArgs* probs, int count) {
+  for (int i = 0; i < count; ++i) {
+    const GemmArgs& g = probs[i];
+    if (g.M < 1024 || g.epi != EPI_NONE || !g.a_out || g.K % 4 || g.K > 1024 || g.K < 4 || g.ksplitA < g.K ||
+        g.lda % 4 || g.ld_aout % 4 || ((uintptr_t)g.A | (uintptr_t)g.a_out | (uintptr_t)g.ln_g | (uintptr_t)g.ln_b) & 15 ||
+        (long long)g.M * std::max(g.lda, g.ld_aout) >= (1LL << 31))
+      return false;
+  }
+  return true;
+}
+
 int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hipStream_t s) {
   if (count < 1 || count > 4) {
     dr_set_error("gemm_launch: bad problem count %d", count);
     return DR_E_INVALID;
+  }
+  if (lay == G_NT && amode == AM_LNSILU && tall_ln_ok(probs, count)) {
+    GemmArgs pp[4];
+    for (int i = 0; i < count; ++i) {
+      const GemmArgs& g = probs[i];
+      const dim3 grid((unsigned)((g.M + 3) / 4));
+      if (g.K <= 256)
+        hipLaunchKernelGGL(k_ln_silu_rows<1>, grid, dim3(256), 0, s, g.M, g.K, g.A, (int)g.lda, g.ln_g, g.ln_b, g.a_out,
+                           (int)g.ld_aout);
+      else
+        hipLaunchKernelGGL(k_ln_silu_rows<4>, grid, dim3(256), 0, s, g.M, g.K, g.A, (int)g.lda, g.ln_g, g.ln_b, g.a_out,
+                           (int)g.ld_aout);
+      DR_TRY(dr_check_launch("ln_silu_rows"));
+      pp[i] = g;
+      pp[i].A = g.a_out;
+      pp[i].lda = g.ld_aout;
+      pp[i].ln_g = pp[i].ln_b = nullptr;
+      pp[i].a_out = nullptr;
+    }
+    return gemm_launch(G_NT, AM_PLAIN, pp, count, s);
   }
   if (lay == G_NT && amode == AM_LNSILU && count == 1 && !g_ln_sample_off && ln_sample_ok(probs[0]))
     return launch_ln_sample(probs[0], s);

@@ -26,7 +26,7 @@ fi
 for v in ${VARIANTS:-}; do
   for lib in base $v; do
     if [ $lib = base ]; then unset DREAMER_LIB_VARIANT; else export DREAMER_LIB_VARIANT=$lib; fi
-    timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-secondary --wm-steps ${AB_WM:-0} > gpurun_out/ab_${TAG}_$lib.json 2> gpurun_out/ab_${TAG}_$lib.err || { tail -10 gpurun_out/ab_${TAG}_$lib.err; exit 1; }
+    timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-secondary --wm-steps ${AB_WM:-0} ${AB_ARGS:-} > gpurun_out/ab_${TAG}_$lib.json 2> gpurun_out/ab_${TAG}_$lib.err || { tail -10 gpurun_out/ab_${TAG}_$lib.err; exit 1; }
     python -c "import json;d=json.load(open('gpurun_out/ab_${TAG}_$lib.json'));print('ab $lib', d['value'], 'encoder_ms', d['roofline']['encoder_ms'])"
   done
 done
