@@ -22,6 +22,8 @@
 // (NCHW, the flatten order that feeds the projection).
 #include "conv.h"
 
+#include <algorithm>
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
@@ -144,6 +146,9 @@ __global__ __launch_bounds__(256) void k_conv1_bf16(int n, int nb, int h, int w,
     }
 }
 
+#ifndef DR_E12B_WAVES
+#define DR_E12B_WAVES 4  // A/B knob (tools/build_variant.py): 8 waves measured slower (172 VGPRs, one workgroup per CU)
+#endif
 // ---------------------------------------------------------------------------
 // conv1 + conv2 fused (enc_f1 = 32 -> enc_f2 = 64): a workgroup owns R2 rows of
 // conv2 output (128 pixels); it stages the u8 input rows they depend on, runs
@@ -155,22 +160,26 @@ __global__ __launch_bounds__(256) void k_conv1_bf16(int n, int nb, int h, int w,
 // group of a conv2 B fragment (16 pixels at stride 2, two 8-channel chunks)
 // land on 16 distinct bank quads.
 // ---------------------------------------------------------------------------
-template <int R2, int OW1>  // conv2 rows per workgroup, conv1 output width (= w / 2)
-__global__ __launch_bounds__(256) void k_enc12_bf16(int n, int nb, int h, int w, dr_frames src,
-                                                    const u16* __restrict__ wr1, const float* __restrict__ b1,
-                                                    const u16* __restrict__ wr2, const float* __restrict__ b2,
-                                                    u16* __restrict__ out) {
+// Persistent (round 3): each workgroup walks tiles blockIdx.x, + gridDim.x, ...
+// and loads its next tile's input rows into registers under the current
+// tile's conv2; NW = 8 waves, wave w owning 128 / 16 / NW pixel fragments x 64
+// channels of conv2 (two workgroups per CU by LDS: four waves per SIMD).
+template <int R2, int OW1, int NW>  // conv2 rows per workgroup, conv1 output width (= w / 2), waves
+__global__ __launch_bounds__(64 * NW) void k_enc12_bf16(int n, int nb, int h, int w, dr_frames src,
+                                                        const u16* __restrict__ wr1, const float* __restrict__ b1,
+                                                        const u16* __restrict__ wr2, const float* __restrict__ b2,
+                                                        u16* __restrict__ out) {
   constexpr int R1 = 2 * R2 + 2, RI = 2 * R1 + 2, OW2 = OW1 / 2, W = 2 * OW1;
   constexpr int NP = R1 * OW1, PS = NP + 1;  // conv1 pixels in the tile, unit plane stride
   constexpr int LWI = W + 2;
-  static_assert(R2 * OW2 == 128, "128 conv2 pixels per workgroup");
+  constexpr int NTH = 64 * NW, FPW = 8 / NW;  // conv2 pixel fragments per wave
+  static_assert(R2 * OW2 == 128 && (NW == 4 || NW == 8), "128 conv2 pixels per workgroup");
   __shared__ __attribute__((aligned(16))) uint2 xin[RI][LWI];  // input [row][x + 1][4 ch] bf16
   __shared__ __attribute__((aligned(16))) uint4 c1o[4 * PS];   // conv1 output, 8-channel units
   const int oh1 = h / 2, oh2 = h / 4;
-  const int tiles_y = oh2 / R2;
-  const int f = blockIdx.x / tiles_y, ty = blockIdx.x - f * tiles_y;
-  if (f >= n) return;
-  const int y2_0 = ty * R2, y1_0 = 2 * y2_0 - 1, iy0 = 2 * y1_0 - 1;
+  const int tiles_y = oh2 / R2, ntiles = n * tiles_y;
+  int tile = blockIdx.x;
+  if (tile >= ntiles) return;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
   // conv1 weights (A fragments, both k-steps, both channel tiles) and biases
   uint4 wa1[2][2];
@@ -183,135 +192,160 @@ __global__ __launch_bounds__(256) void k_enc12_bf16(int n, int nb, int h, int w,
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) bb1[j][e] = b1[16 * j + 4 * q + e];
-  // ---- stage the input rows (u8 ring or f32 frames) ----
-  for (int i = tid; i < RI * LWI; i += 256) {
+  // ---- input rows (u8 ring or f32 frames): padding columns / channel slot 3
+  // zeroed once; every tile rewrites all other entries (zeros outside the frame)
+  for (int i = tid; i < RI * LWI; i += NTH) {
     const int rr = i / LWI;
     xin[rr][i - rr * LWI] = make_uint2(0u, 0u);
   }
   const unsigned hw = (unsigned)(h * w);
-  const int b = f % nb, t = f / nb + src.t0;
-  const unsigned char* fr8 = nullptr;
-  const float* fr32 = nullptr;
-  if (src.ring) fr8 = src.ring + ((src.starts[b] + t) % src.ring_cap) * 3 * (long long)hw;
-  else fr32 = src.obs + (long long)b * src.stride_b + (long long)t * src.stride_t;
-  constexpr int W4 = W / 4, PERC = RI * W4, MAXI = (3 * PERC + 255) / 256;
+  constexpr int W4 = W / 4, PERC = RI * W4, MAXI = (3 * PERC + NTH - 1) / NTH;
   float v[MAXI][4];
+  auto in_load = [&](int tl) __attribute__((always_inline)) {
+    const int f = tl / tiles_y, ty = tl - f * tiles_y;
+    const int iy0 = 2 * (2 * (ty * R2) - 1) - 1;
+    const int b = f % nb, t = f / nb + src.t0;
+    const unsigned char* fr8 = nullptr;
+    const float* fr32 = nullptr;
+    if (src.ring) fr8 = src.ring + ((src.starts[b] + t) % src.ring_cap) * 3 * (long long)hw;
+    else fr32 = src.obs + (long long)b * src.stride_b + (long long)t * src.stride_t;
 #pragma unroll
-  for (int k = 0; k < MAXI; ++k) {
-    const int i = tid + 256 * k;
-    const int c = i / PERC, rem = i - c * PERC, rr = rem / W4, x4 = rem - rr * W4;
-    const int y = iy0 + rr;
-    const bool ok = i < 3 * PERC && y >= 0 && y < h;
-    const unsigned off = ok ? (unsigned)c * hw + (unsigned)(y * w + 4 * x4) : 0u;
-    if (fr8) {
-      const unsigned u = ok ? *reinterpret_cast<const unsigned*>(fr8 + off) : 0u;
+    for (int k = 0; k < MAXI; ++k) {
+      const int i = tid + NTH * k;
+      const int c = i / PERC, rem = i - c * PERC, rr = rem / W4, x4 = rem - rr * W4;
+      const int y = iy0 + rr;
+      const bool ok = i < 3 * PERC && y >= 0 && y < h;
+      const unsigned off = ok ? (unsigned)c * hw + (unsigned)(y * w + 4 * x4) : 0u;
+      if (fr8) {
+        const unsigned u = ok ? *reinterpret_cast<const unsigned*>(fr8 + off) : 0u;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[k][e] = (float)((u >> (8 * e)) & 255u);
-    } else {
-      const float4 qv = ok ? *reinterpret_cast<const float4*>(fr32 + off) : make_float4(0.f, 0.f, 0.f, 0.f);
-      v[k][0] = qv.x; v[k][1] = qv.y; v[k][2] = qv.z; v[k][3] = qv.w;
-    }
-  }
-  __syncthreads();
-  u16* xs = reinterpret_cast<u16*>(&xin[0][0]);
-#pragma unroll
-  for (int k = 0; k < MAXI; ++k) {
-    const int i = tid + 256 * k;
-    const int c = i / PERC, rem = i - c * PERC, rr = rem / W4, x4 = rem - rr * W4;
-    const int y = iy0 + rr;
-    if (i >= 3 * PERC || y < 0 || y >= h) continue;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float x = src.raw255 ? v[k][e] / 255.0f - 0.5f : v[k][e];  // Dreamer.py:251
-      xs[(rr * LWI + 4 * x4 + e + 1) * 4 + c] = dr_bf16(x);
-    }
-  }
-  __syncthreads();
-  // ---- conv1 over the tile's R1 rows (rows outside the frame are conv2 padding: zeros) ----
-  constexpr int F1 = NP / 16;  // conv1 pixel fragments
-  for (int i = wave; i < F1; i += 4) {
-    const int p0 = 16 * i, yl = p0 / OW1, x1 = p0 - yl * OW1 + r;
-    const int y1 = y1_0 + yl;
-    const int p = p0 + r;
-    u16* dst0 = reinterpret_cast<u16*>(c1o);
-    if (y1 < 0 || y1 >= oh1) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int c8 = 2 * j + (q >> 1);
-        *reinterpret_cast<uint2*>(dst0 + (c8 * PS + p) * 8 + (q & 1) * 4) = make_uint2(0u, 0u);
+        for (int e = 0; e < 4; ++e) v[k][e] = (float)((u >> (8 * e)) & 255u);
+      } else {
+        const float4 qv = ok ? *reinterpret_cast<const float4*>(fr32 + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[k][0] = qv.x; v[k][1] = qv.y; v[k][2] = qv.z; v[k][3] = qv.w;
       }
-      continue;
     }
-    f32x4 acc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+  };
+  u16* xs = reinterpret_cast<u16*>(&xin[0][0]);
+  auto in_store = [&](int tl) __attribute__((always_inline)) {
+    const int ty = tl % tiles_y;
+    const int iy0 = 2 * (2 * (ty * R2) - 1) - 1;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int t0 = 8 * s + 2 * q, ky = t0 >> 2, kx = t0 & 3;
-      const uint4 pb = *reinterpret_cast<const uint4*>(&xin[2 * yl + ky][2 * x1 + kx]);
+    for (int k = 0; k < MAXI; ++k) {
+      const int i = tid + NTH * k;
+      if (i >= 3 * PERC) continue;
+      const int c = i / PERC, rem = i - c * PERC, rr = rem / W4, x4 = rem - rr * W4;
+      const int y = iy0 + rr;
+      const bool ok = y >= 0 && y < h;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[j] = dr_mfma_bf16(wa1[s][j], pb, acc[j]);
+      for (int e = 0; e < 4; ++e) {
+        const float x = src.raw255 ? v[k][e] / 255.0f - 0.5f : v[k][e];  // Dreamer.py:251
+        xs[(rr * LWI + 4 * x4 + e + 1) * 4 + c] = ok ? dr_bf16(x) : (u16)0;
+      }
     }
-    // lane: pixel p, channels 16 j + 4 q .. +3 = half (q & 1) of 8-channel unit 2 j + (q >> 1)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int c8 = 2 * j + (q >> 1);
-      *reinterpret_cast<uint2*>(dst0 + (c8 * PS + p) * 8 + (q & 1) * 4) =
-          dr_pack_bf16x4(dr_silu_fast(acc[j][0] + bb1[j][0]), dr_silu_fast(acc[j][1] + bb1[j][1]),
-                         dr_silu_fast(acc[j][2] + bb1[j][2]), dr_silu_fast(acc[j][3] + bb1[j][3]));
-    }
-  }
+  };
+  in_load(tile);
+  __syncthreads();  // the zero fill before other threads' stores
+  in_store(tile);
   __syncthreads();
-  // ---- conv2: wave w owns pixel fragments 2w, 2w + 1 (16 pixels each) x all 64 channels ----
-  // weights as the A operand (lane -> 4 channels of one pixel); K = 16 taps x 32 channels
-  f32x4 acc[2][4];
+  int py[FPW], px[FPW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  int py[2], px[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int pl = 16 * (2 * wave + i) + r;  // tile pixel
+  for (int i = 0; i < FPW; ++i) {
+    const int pl = 16 * (FPW * wave + i) + r;  // tile pixel
     py[i] = pl / OW2;
     px[i] = pl - py[i] * OW2;
-  }
-  constexpr int WP = 3;  // weight fragments in flight (k-steps ahead)
-  uint4 wa[WP][4];
-  auto wload = [&](int tap, int sl) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) wa[sl][j] = *reinterpret_cast<const uint4*>(wr2 + (16 * j + r) * 512 + 32 * tap + 8 * q);
-  };
-#pragma unroll
-  for (int s = 0; s < WP; ++s) wload(s, s);
-#pragma unroll
-  for (int tap = 0; tap < 16; ++tap) {
-    const int ky = tap >> 2, kx = tap & 3, sl = tap % WP;
-    uint4 pb[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      // conv1 pixel (2 y2 - 1 + ky, 2 x2 - 1 + kx) in tile coordinates
-      const int yl = 2 * py[i] + ky, x1 = 2 * px[i] - 1 + kx;
-      const bool ok = x1 >= 0 && x1 < OW1;
-      pb[i] = ok ? c1o[q * PS + yl * OW1 + x1] : make_uint4(0u, 0u, 0u, 0u);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = dr_mfma_bf16(wa[sl][j], pb[i], acc[i][j]);
-    if (tap + WP < 16) wload(tap + WP, sl);
   }
   float bb2[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) bb2[j][e] = b2[16 * j + 4 * q + e];
+  for (;;) {
+    const int f = tile / tiles_y, ty = tile - f * tiles_y;
+    const int y2_0 = ty * R2, y1_0 = 2 * y2_0 - 1;
+    const int next = tile + (int)gridDim.x;
+    // ---- conv1 over the tile's R1 rows (rows outside the frame are conv2 padding: zeros) ----
+    constexpr int F1 = NP / 16;  // conv1 pixel fragments
+    for (int i = wave; i < F1; i += NW) {
+      const int p0 = 16 * i, yl = p0 / OW1, x1 = p0 - yl * OW1 + r;
+      const int y1 = y1_0 + yl;
+      const int p = p0 + r;
+      u16* dst0 = reinterpret_cast<u16*>(c1o);
+      if (y1 < 0 || y1 >= oh1) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    u16* o = out + (((long long)f * oh2 + y2_0 + py[i]) * OW2 + px[i]) * 64;
+        for (int j = 0; j < 2; ++j) {
+          const int c8 = 2 * j + (q >> 1);
+          *reinterpret_cast<uint2*>(dst0 + (c8 * PS + p) * 8 + (q & 1) * 4) = make_uint2(0u, 0u);
+        }
+        continue;
+      }
+      f32x4 acc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      *reinterpret_cast<uint2*>(o + 16 * j + 4 * q) =
-          dr_pack_bf16x4(dr_silu_fast(acc[i][j][0] + bb2[j][0]), dr_silu_fast(acc[i][j][1] + bb2[j][1]),
-                         dr_silu_fast(acc[i][j][2] + bb2[j][2]), dr_silu_fast(acc[i][j][3] + bb2[j][3]));
+      for (int s = 0; s < 2; ++s) {
+        const int t0 = 8 * s + 2 * q, ky = t0 >> 2, kx = t0 & 3;
+        const uint4 pb = *reinterpret_cast<const uint4*>(&xin[2 * yl + ky][2 * x1 + kx]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[j] = dr_mfma_bf16(wa1[s][j], pb, acc[j]);
+      }
+      // lane: pixel p, channels 16 j + 4 q .. +3 = half (q & 1) of 8-channel unit 2 j + (q >> 1)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c8 = 2 * j + (q >> 1);
+        *reinterpret_cast<uint2*>(dst0 + (c8 * PS + p) * 8 + (q & 1) * 4) =
+            dr_pack_bf16x4(dr_silu_fast(acc[j][0] + bb1[j][0]), dr_silu_fast(acc[j][1] + bb1[j][1]),
+                           dr_silu_fast(acc[j][2] + bb1[j][2]), dr_silu_fast(acc[j][3] + bb1[j][3]));
+      }
+    }
+    __syncthreads();
+    if (next < ntiles) in_load(next);  // under conv2 (xin is free now)
+    // ---- conv2: weights as the A operand (lane -> 4 channels of one pixel); K = 16 taps x 32 channels ----
+    f32x4 acc[FPW][4];
+#pragma unroll
+    for (int i = 0; i < FPW; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    // weight fragments one tap ahead in a two-slot register ring (compile-time
+    // slots: two taps per loop iteration, the loop itself not unrolled)
+    uint4 wa0[4], wa1r[4];
+    auto wload = [&](uint4 (&wa)[4], int tap) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wa[j] = *reinterpret_cast<const uint4*>(wr2 + (16 * j + r) * 512 + 32 * tap + 8 * q);
+    };
+    auto tap_step = [&](int tap, uint4 (&wa)[4], uint4 (&wn)[4]) __attribute__((always_inline)) {
+      wload(wn, tap + 1 < 16 ? tap + 1 : 15);
+      const int ky = tap >> 2, kx = tap & 3;
+      uint4 pb[FPW];
+#pragma unroll
+      for (int i = 0; i < FPW; ++i) {
+        // conv1 pixel (2 y2 - 1 + ky, 2 x2 - 1 + kx) in tile coordinates
+        const int yl = 2 * py[i] + ky, x1 = 2 * px[i] - 1 + kx;
+        const bool ok = x1 >= 0 && x1 < OW1;
+        pb[i] = ok ? c1o[q * PS + yl * OW1 + x1] : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int i = 0; i < FPW; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = dr_mfma_bf16(wa[j], pb[i], acc[i][j]);
+    };
+    wload(wa0, 0);
+#pragma unroll 1
+    for (int tap = 0; tap < 16; tap += 2) {
+      tap_step(tap, wa0, wa1r);
+      tap_step(tap + 1, wa1r, wa0);
+    }
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) {
+      u16* o = out + (((long long)f * oh2 + y2_0 + py[i]) * OW2 + px[i]) * 64;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<uint2*>(o + 16 * j + 4 * q) =
+            dr_pack_bf16x4(dr_silu_fast(acc[i][j][0] + bb2[j][0]), dr_silu_fast(acc[i][j][1] + bb2[j][1]),
+                           dr_silu_fast(acc[i][j][2] + bb2[j][2]), dr_silu_fast(acc[i][j][3] + bb2[j][3]));
+    }
+    if (next >= ntiles) break;  // uniform over the workgroup
+    in_store(next);
+    __syncthreads();  // next input staged; every wave is past its conv2 reads of c1o
+    tile = next;
   }
 }
 
@@ -542,12 +576,30 @@ int op_enc12_bf16(int n, int nb, int h, int w, int c1, int c2, const dr_frames* 
     return DR_E_INVALID;
   const long long blocks = (long long)n * (h == 64 ? 2 : 8);
   if (blocks >= (1LL << 31)) return DR_E_INVALID;
+  // persistent: as many workgroups as are resident at once (occupancy API x CUs)
+  static int slots[64][2];
+  int dev = 0;
+  DR_TRY_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return DR_E_INVALID;
+  const int vi = h == 64 ? 0 : 1;
+  if (slots[dev][vi] == 0) {
+    int cus = 0, per = 0;
+    DR_TRY_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (h == 64)
+      DR_TRY_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_enc12_bf16<8, 32, DR_E12B_WAVES>,
+                                                              64 * DR_E12B_WAVES, 0));
+    else
+      DR_TRY_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_enc12_bf16<4, 64, DR_E12B_WAVES>,
+                                                              64 * DR_E12B_WAVES, 0));
+    slots[dev][vi] = std::max(1, per) * std::max(1, cus);
+  }
+  const unsigned grid = (unsigned)std::min(blocks, (long long)slots[dev][vi]);
   if (h == 64)
-    hipLaunchKernelGGL((k_enc12_bf16<8, 32>), dim3((unsigned)blocks), dim3(256), 0, s, n, nb, h, w, *src, (const u16*)wr1,
-                       b1, (const u16*)wr2, b2, (u16*)out);
+    hipLaunchKernelGGL((k_enc12_bf16<8, 32, DR_E12B_WAVES>), dim3(grid), dim3(64 * DR_E12B_WAVES), 0, s, n, nb, h, w,
+                       *src, (const u16*)wr1, b1, (const u16*)wr2, b2, (u16*)out);
   else
-    hipLaunchKernelGGL((k_enc12_bf16<4, 64>), dim3((unsigned)blocks), dim3(256), 0, s, n, nb, h, w, *src, (const u16*)wr1,
-                       b1, (const u16*)wr2, b2, (u16*)out);
+    hipLaunchKernelGGL((k_enc12_bf16<4, 64, DR_E12B_WAVES>), dim3(grid), dim3(64 * DR_E12B_WAVES), 0, s, n, nb, h, w,
+                       *src, (const u16*)wr1, b1, (const u16*)wr2, b2, (u16*)out);
   return dr_check_launch("enc12_bf16");
 }
 

@@ -1330,35 +1330,39 @@ int op_gemm_nt_split3_sk(int M, int N, int K, const float* A, int lda, const flo
     return DR_E_INVALID;
   }
   GemmS3 g = {M, N, K, ksA < K ? ksA : K, lda, lda2, ldy, act, s3_np(N), A, A2, (const u16*)wr, bias, Y, 1, part};
-  // the largest tile that still gives ~two waves per SIMD over the chip
-  // (256 x 128, 256 x 64, 128 x 128, 128 x 64, else 64 x 64): taller / wider
-  // tiles re-read less, but a half-empty chip costs more (M = 8192, N = 200:
-  // 128 x 64 tiles gave 256 single-wave-per-SIMD workgroups)
   auto tl = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   auto waves = [&](int bm, int bn) { return (long long)tl(bm, bn) * (bm / 32); };
-  // split K while even the 64 x 64 grid is under ~2 waves per SIMD (N = 200
-  // products: the critic's / heads' first layers over 4096 rows, 512 waves),
-  // >= 8 chunks per split, when the caller brought partial-sum scratch
+  // the largest tile (256 x 128, 256 x 64, 128 x 128, 128 x 64, else 64 x 64)
+  // that gives ~two waves per SIMD over the chip (2048 waves), splitting K
+  // (>= 8 chunks per split, when the caller brought partial-sum scratch) to
+  // get there: taller / wider tiles re-read less.  The N = 200 products over
+  // 4096-8192 rows (projection, critic / heads' first layers) otherwise ran
+  // 64 x 64 tiles at 75 TF/s.
   const int nch = (K + 31) / 32;
-  const bool small = waves(256, 128) < 2048 && waves(256, 64) < 2048 && waves(128, 128) < 2048 && waves(128, 64) < 2048;
-  if (part && small) {
+  auto splits_for = [&](int bm, int bn) {
     int sp = 1;
-    while (sp < DR_S3_SPLITS && waves(64, 64) * sp * 2 <= 2048 && nch / (2 * sp) >= 8 &&
+    while (part && sp < DR_S3_SPLITS && waves(bm, bn) * sp < 2048 && nch / (2 * sp) >= 8 &&
            (size_t)(2 * sp) * M * N <= part_floats)
       sp *= 2;
-    g.splits = sp;
+    return sp;
+  };
+  const int shapes[5][2] = {{256, 128}, {256, 64}, {128, 128}, {128, 64}, {64, 64}};
+  int pick = 4;
+  for (int c = 0; c < 5; ++c) {
+    if (waves(shapes[c][0], shapes[c][1]) * splits_for(shapes[c][0], shapes[c][1]) >= 2048) {
+      pick = c;
+      break;
+    }
   }
-  const dim3 gy(1, (unsigned)g.splits);
-  if (waves(256, 128) >= 2048)
-    hipLaunchKernelGGL((k_gemm_split3<256, 128>), dim3(dr_xcd_grid(tl(256, 128))), dim3(512), 0, s, g);
-  else if (waves(256, 64) >= 2048)
-    hipLaunchKernelGGL((k_gemm_split3<256, 64>), dim3(dr_xcd_grid(tl(256, 64))), dim3(512), 0, s, g);
-  else if (waves(128, 128) >= 2048)
-    hipLaunchKernelGGL((k_gemm_split3<128, 128>), dim3(dr_xcd_grid(tl(128, 128))), dim3(256), 0, s, g);
-  else if (waves(128, 64) >= 2048)
-    hipLaunchKernelGGL((k_gemm_split3<128, 64>), dim3(dr_xcd_grid(tl(128, 64))), dim3(256), 0, s, g);
-  else
-    hipLaunchKernelGGL((k_gemm_split3<64, 64>), dim3(dr_xcd_grid(tl(64, 64)), g.splits), dim3(128), 0, s, g);
+  g.splits = splits_for(shapes[pick][0], shapes[pick][1]);
+  const unsigned gy = (unsigned)g.splits;
+  switch (pick) {
+    case 0: hipLaunchKernelGGL((k_gemm_split3<256, 128>), dim3(dr_xcd_grid(tl(256, 128)), gy), dim3(512), 0, s, g); break;
+    case 1: hipLaunchKernelGGL((k_gemm_split3<256, 64>), dim3(dr_xcd_grid(tl(256, 64)), gy), dim3(512), 0, s, g); break;
+    case 2: hipLaunchKernelGGL((k_gemm_split3<128, 128>), dim3(dr_xcd_grid(tl(128, 128)), gy), dim3(256), 0, s, g); break;
+    case 3: hipLaunchKernelGGL((k_gemm_split3<128, 64>), dim3(dr_xcd_grid(tl(128, 64)), gy), dim3(256), 0, s, g); break;
+    default: hipLaunchKernelGGL((k_gemm_split3<64, 64>), dim3(dr_xcd_grid(tl(64, 64)), gy), dim3(128), 0, s, g); break;
+  }
   DR_TRY(dr_check_launch("gemm_nt_split3"));
   if (g.splits > 1) {
     hipLaunchKernelGGL(k_s3_finish, dim3((unsigned)(((long long)M * (N / 4) + 255) / 256)), dim3(256), 0, s, g);
