@@ -23,6 +23,35 @@ struct GemmBatch {
   GemmArgs p[4];
 };
 
+// Grouped launches pack their problems' tiles into one linear grid (npack > 0):
+// block b -> XCD-ordered logical tile over the concatenated tile lists, then
+// (problem z, tile within z).  Without packing a blockIdx.z slice is sized for
+// the largest problem and the smaller problems' surplus workgroups idle in it.
+// Returns -1 for padding blocks; npack == 0 keeps blockIdx.z (lt = -2: the
+// caller computes its tile from its own problem).
+template <int BM, int BN>
+__device__ __forceinline__ int dr_pack_tile(const GemmBatch& gb, int npack, int& z) {
+  z = blockIdx.z;
+  if (npack <= 0) return -2;
+  int tot = 0;
+  for (int i = 0; i < npack; ++i) tot += ((gb.p[i].M + BM - 1) / BM) * ((gb.p[i].N + BN - 1) / BN);
+  int lt = dr_xcd_tile(blockIdx.x, tot);
+  if (lt < 0) return -1;
+  z = 0;
+  for (int i = 0; i + 1 < npack; ++i) {
+    const int ti = ((gb.p[i].M + BM - 1) / BM) * ((gb.p[i].N + BN - 1) / BN);
+    if (lt < ti) break;
+    lt -= ti;
+    z = i + 1;
+  }
+  return lt;
+}
+static int pack_tiles(const GemmBatch& gb, int count, int bm, int bn) {
+  int tot = 0;
+  for (int i = 0; i < count; ++i) tot += ((gb.p[i].M + bm - 1) / bm) * ((gb.p[i].N + bn - 1) / bn);
+  return tot;
+}
+
 static thread_local int g_gemm_bf16 = 0;
 GemmBf16Scope::GemmBf16Scope(bool on) : prev(g_gemm_bf16) { g_gemm_bf16 = on ? 1 : 0; }
 GemmBf16Scope::~GemmBf16Scope() { g_gemm_bf16 = prev; }
@@ -366,10 +395,13 @@ __device__ __forceinline__ void epilogue_store_b(const GemmArgs& g, int m, int n
 #define DR_SKW 8  // waves per skinny-GEMM workgroup (K split over them)
 #endif
 template <int MT, int NT, int AMODE, bool B_KN, bool VEC, int EPI>
-__global__ __launch_bounds__(64 * DR_SKW) void k_gemm_skinny(GemmBatch gb) {
+__global__ __launch_bounds__(64 * DR_SKW) void k_gemm_skinny(GemmBatch gb, int npack) {
   constexpr int NWAVE = DR_SKW, NTH = 64 * DR_SKW, FT = MT / 16, FN = NT / 16;
   __shared__ GemmArgs s_args;
-  dr_stage_args(gb.p[blockIdx.z], s_args, threadIdx.x);
+  int pz;
+  const int plt = dr_pack_tile<MT, NT>(gb, npack, pz);
+  if (plt == -1) return;
+  dr_stage_args(gb.p[pz], s_args, threadIdx.x);
   const GemmArgs& g = s_args;
   SkOps o;
   o.M = dr_uni(g.M); o.N = dr_uni(g.N); o.K = dr_uni(g.K);
@@ -381,7 +413,7 @@ __global__ __launch_bounds__(64 * DR_SKW) void k_gemm_skinny(GemmBatch gb) {
   const int tiles_m = (M + MT - 1) / MT;
   // logical tiles column-major: the row tiles reading one weight slice are
   // adjacent and share an XCD's L2
-  const int lt = dr_xcd_tile(blockIdx.x, tiles_m * tiles_n);
+  const int lt = plt >= 0 ? plt : dr_xcd_tile(blockIdx.x, tiles_m * tiles_n);
   if (lt < 0) return;
   const int tn = lt / tiles_m, tm = lt - tn * tiles_m;
   const int m0 = tm * MT, n0 = tn * NT;
@@ -1228,16 +1260,19 @@ __device__ __forceinline__ float tile_b_kn_ld(const GemmArgs& g, const float* W,
 // wave tiles at 64 x 32: two waves per SIMD hide the per-chunk barrier and
 // LDS latency that one wave per SIMD exposes at these short K ranges)
 template <int BM, int BN, int KC, bool A_KM, bool B_KN, bool VEC, int NW = 4>
-__global__ __launch_bounds__(64 * NW) void k_gemm_tile(GemmBatch gb, int splits) {
+__global__ __launch_bounds__(64 * NW) void k_gemm_tile(GemmBatch gb, int splits, int npack) {
   constexpr int NTH = 64 * NW;
   constexpr int TLDS = KC + 8;  // = 8 mod 16 dwords: conflict-free ds_read_b128 fragments
   constexpr int KQ = KC / 4;  // float4 per row piece
   __shared__ GemmArgs s_args;
-  dr_stage_args(gb.p[blockIdx.z], s_args, threadIdx.x);
+  int pz;
+  const int plt = dr_pack_tile<BM, BN>(gb, npack, pz);
+  if (plt == -1) return;
+  dr_stage_args(gb.p[pz], s_args, threadIdx.x);
   const GemmArgs& g = s_args;
   const int M = dr_uni(g.M), N = dr_uni(g.N), K = dr_uni(g.K);
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
-  const int lt = dr_xcd_tile(blockIdx.x, tiles_m * tiles_n);
+  const int lt = plt >= 0 ? plt : dr_xcd_tile(blockIdx.x, tiles_m * tiles_n);
   if (lt < 0) return;
   const int tn = lt / tiles_m, tm = lt - tn * tiles_m;  // m-tiles sharing a weight slice are adjacent
   const int m0 = tm * BM, n0 = tn * BN;
@@ -1828,12 +1863,12 @@ static void launch_skinny(const GemmBatch& gb, int count, bool vec, hipStream_t 
     }();
     (void)raised;
   }
+  const int npack = count > 1 ? count : 0;
+  const dim3 grid(dr_xcd_grid(npack ? pack_tiles(gb, count, MT, NT) : maxt), 1, npack ? 1 : count);
   if (vec)
-    hipLaunchKernelGGL((k_gemm_skinny<MT, NT, AMODE, B_KN, true, EPI>), dim3(dr_xcd_grid(maxt), 1, count), dim3(64 * DR_SKW),
-                       lds, s, gb);
+    hipLaunchKernelGGL((k_gemm_skinny<MT, NT, AMODE, B_KN, true, EPI>), grid, dim3(64 * DR_SKW), lds, s, gb, npack);
   else
-    hipLaunchKernelGGL((k_gemm_skinny<MT, NT, AMODE, B_KN, false, EPI>), dim3(dr_xcd_grid(maxt), 1, count), dim3(64 * DR_SKW),
-                       lds, s, gb);
+    hipLaunchKernelGGL((k_gemm_skinny<MT, NT, AMODE, B_KN, false, EPI>), grid, dim3(64 * DR_SKW), lds, s, gb, npack);
 }
 
 
@@ -2188,9 +2223,10 @@ static void launch_tile2(GemmBatch& gb, int count, hipStream_t s) {
     for (int i = 0; i < count; ++i)
       while (splits > 1 && (long long)splits * gb.p[i].M * gb.p[i].N > gb.p[i].splitk_floats) --splits;
   }
-  dim3 grid(dr_xcd_grid(maxt), splits, count);
-  if (vec) hipLaunchKernelGGL((k_gemm_tile<BM, BN, KC, A_KM, B_KN, true, NW>), grid, dim3(64 * NW), 0, s, gb, splits);
-  else hipLaunchKernelGGL((k_gemm_tile<BM, BN, KC, A_KM, B_KN, false, NW>), grid, dim3(64 * NW), 0, s, gb, splits);
+  const int npack = count > 1 ? count : 0;
+  dim3 grid(dr_xcd_grid(npack ? tot : maxt), splits, npack ? 1 : count);
+  if (vec) hipLaunchKernelGGL((k_gemm_tile<BM, BN, KC, A_KM, B_KN, true, NW>), grid, dim3(64 * NW), 0, s, gb, splits, npack);
+  else hipLaunchKernelGGL((k_gemm_tile<BM, BN, KC, A_KM, B_KN, false, NW>), grid, dim3(64 * NW), 0, s, gb, splits, npack);
   if (splits > 1)
     hipLaunchKernelGGL(k_splitk_finish, dim3((unsigned)((maxMN + 255) / 256), 1, count), dim3(256), 0, s, gb, splits);
 }
