@@ -66,6 +66,11 @@ int op_conv1_bf16(int n, int nb, int h, int w, int cout, const dr_frames* src, c
 int op_enc12_split3(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
                     const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, float* out,
                     hipStream_t s);
+// the same with the world-model step's saves (NHWC f32, pre0 / a0 together or
+// neither): conv1's pre-activation and output, conv2's pre-activation
+int op_enc12_split3_ex(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
+                       const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, float* out,
+                       float* pre0, float* a0, float* pre1, hipStream_t s);
 int op_enc12_bf16(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const void* wr1, const float* b1,
                   const void* wr2, const float* b2, void* out, hipStream_t s);
 // k4 s2 p1 conv + bias + SiLU, bf16 NHWC in -> bf16 NHWC (or NCHW) out

@@ -328,9 +328,14 @@ static constexpr size_t e12_lds_bytes() { return (size_t)3 * 4 * E12_PS * 16 + (
 // taps 8-15 over the same 64 x 32 output blocks, the two partial sums meet in
 // LDS (fixed order: taps 0-7 + taps 8-15) before the epilogue
 template <int NW>
+// Optional saves for the world-model backward (NHWC f32, NULL = none): pre0 /
+// a0 = conv1's pre-activation / output (the tile's own 16 conv1 rows), pre1 =
+// conv2's pre-activation (out receives conv2's output as always).
 __global__ __launch_bounds__(64 * NW) void k_enc12_split3(int n, int nb, dr_frames src, const u16* __restrict__ wr1,
                                                           const float* __restrict__ b1, const u16* __restrict__ wr2,
-                                                          const float* __restrict__ b2, float* __restrict__ out) {
+                                                          const float* __restrict__ b2, float* __restrict__ out,
+                                                          float* __restrict__ pre0, float* __restrict__ a0,
+                                                          float* __restrict__ pre1) {
   static_assert(NW == 4 || NW == 8, "enc12 waves");
   constexpr int NTH = 64 * NW, TAPS = NW == 8 ? 8 : 16;
   constexpr int R2 = E12_R2, R1 = E12_R1, RI = E12_RI, PS = E12_PS, LWI = E12_LWI;
@@ -441,11 +446,20 @@ __global__ __launch_bounds__(64 * NW) void k_enc12_split3(int n, int nb, dr_fram
           }
         }
         // lane: pixel p, channels 16 j + 4 q .. + 3
+        const bool own = pre0 && yl >= 1 && yl <= 2 * R2;  // this tile's own conv1 rows
+        const long long o1 = (((long long)f * (H / 2) + y1) * OW1 + x1) * C1;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          float v[4];
+          float v[4], pv[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(acc[j][e] * scale + bb1[j][e]);
+          for (int e = 0; e < 4; ++e) {
+            pv[e] = acc[j][e] * scale + bb1[j][e];
+            v[e] = dr_silu_fast(pv[e]);
+          }
+          if (own) {
+            *reinterpret_cast<f32x4*>(pre0 + o1 + 16 * j + 4 * q) = (f32x4){pv[0], pv[1], pv[2], pv[3]};
+            *reinterpret_cast<f32x4*>(a0 + o1 + 16 * j + 4 * q) = (f32x4){v[0], v[1], v[2], v[3]};
+          }
           split3_pair(v[0], v[1], hv[j].x, mv[j].x, lv[j].x);
           split3_pair(v[2], v[3], hv[j].y, mv[j].y, lv[j].y);
         }
@@ -534,9 +548,11 @@ __global__ __launch_bounds__(64 * NW) void k_enc12_split3(int n, int nb, dr_fram
         const int co = 32 * ch + 16 * jj + 4 * q;
         const f32x4 bv = *reinterpret_cast<const f32x4*>(b2 + co);
         f32x4 v;
+        const f32x4 pv = acc[i][jj] + bv;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(acc[i][jj][e] + bv[e]);
+        for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(pv[e]);
         *reinterpret_cast<f32x4*>(o + co) = v;
+        if (pre1) *reinterpret_cast<f32x4*>(pre1 + (o - out) + co) = pv;
       }
     }
     if (next >= ntiles) break;  // uniform over the workgroup: every wave leaves here
@@ -561,6 +577,14 @@ __global__ void k_conv1_repack_split3(int cout, const float* __restrict__ w, u16
 int op_enc12_split3(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
                     const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, float* out,
                     hipStream_t s) {
+  return op_enc12_split3_ex(n, nb, h, w, c1, c2, src, w1, b1, w2, b2, wr1, wr2, out, nullptr, nullptr, nullptr, s);
+}
+
+int op_enc12_split3_ex(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
+                       const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, float* out,
+                       float* pre0, float* a0, float* pre1, hipStream_t s) {
+  if ((pre0 != nullptr) != (a0 != nullptr) || ((uintptr_t)pre0 | (uintptr_t)a0 | (uintptr_t)pre1) & 15)
+    return DR_E_INVALID;
   if (c1 != 32 || c2 != 64 || h != 64 || w != 64 || !src->ring || !src->starts || src->ring_cap <= 0 || n <= 0 ||
       (long long)n * 2 >= (1LL << 31))
     return DR_E_INVALID;
@@ -586,10 +610,10 @@ int op_enc12_split3(int n, int nb, int h, int w, int c1, int c2, const dr_frames
   const int grid = std::min(n * 2, std::max(1, cus[dev]));
   if (DR_E12_WAVES == 8)
     hipLaunchKernelGGL(k_enc12_split3<8>, dim3((unsigned)grid), dim3(512), e12_lds_bytes(), s, n, nb, *src,
-                       (const u16*)wr1, b1, (const u16*)wr2, b2, out);
+                       (const u16*)wr1, b1, (const u16*)wr2, b2, out, pre0, a0, pre1);
   else
     hipLaunchKernelGGL(k_enc12_split3<4>, dim3((unsigned)grid), dim3(256), e12_lds_bytes(), s, n, nb, *src,
-                       (const u16*)wr1, b1, (const u16*)wr2, b2, out);
+                       (const u16*)wr1, b1, (const u16*)wr2, b2, out, pre0, a0, pre1);
   return dr_check_launch("enc12_split3");
 }
 

@@ -303,6 +303,7 @@ struct WmWs {
   void *s3e[DR_MAX_DEPTH], *s3d[DR_MAX_DEPTH];
   // ... and of decoder convT k (forward) / encoder conv k's data gradient as upsampling convs
   void *t3d[DR_MAX_DEPTH], *t3e[DR_MAX_DEPTH];
+  void* e12w1;  // conv1's split3 weight planes for k_enc12_split3
   // loss
   float *coef_row, *coef_obs, *obs_part, *kl_grp, *rew_row, *cont_row, *scal, *stats;
   // backward
@@ -493,6 +494,7 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
   w.t_up3 = c.f((long long)D.Fd * D.dh); w.t_up0 = c.f((long long)D.dh * (Hd + L));
   w.t_map3 = c.f((long long)L * eh); w.t_map0 = c.f((long long)eh * (D.F + Hd));
   w.t_whh = c.f((long long)3 * Hd * Hd); w.w0tp = c.f((long long)D.F * eh);
+  w.e12w1 = D.Dv ? nullptr : c.raw((size_t)D.e[1] * 64 * 6);
   w.cws_n = wm_conv_scratch(D);
   w.cws = c.f(w.cws_n);
   {
@@ -656,8 +658,15 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     hipLaunchKernelGGL(k_silu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, w.pre[N - 1], aL);
     DR_TRY(dr_check_launch("silu"));
   } else {
-  DR_TRY(op_frames_nhwc4(M, B, IH, IW, src, w.x0, s));
-  for (int k = 0; k < N; ++k) {
+  DR_TRY(op_frames_nhwc4(M, B, IH, IW, src, w.x0, s));  // (conv1's weight gradient reads it)
+  // conv1 + conv2 in one kernel from the u8 ring (k_enc12_split3) with the
+  // backward's saves; other shapes / sources take the per-layer kernels
+  int k0 = 0;
+  if (N >= 2 && w.e12w1 && w.s3e[1] &&
+      op_enc12_split3_ex(M, B, IH, IW, D.e[1], D.e[2], src, wm->conv[0].w, wm->conv[0].b, wm->conv[1].w,
+                         wm->conv[1].b, w.e12w1, w.s3e[1], w.a[1], w.pre[0], w.a[0], w.pre[1], s) == DR_OK)
+    k0 = 2;
+  for (int k = k0; k < N; ++k) {
     if (w.s3e[k])
       DR_TRY(op_conv_split3_ex(M, D.e[k], IH >> k, IW >> k, D.e[k + 1], w.a[k - 1], w.s3e[k], wm->conv[k].b, w.a[k],
                                k == N - 1 ? 1 : 0, w.pre[k], CONV_EPI_FWD, s));
