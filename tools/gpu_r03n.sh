@@ -27,8 +27,15 @@ for v in ${VARIANTS:-}; do
   for lib in base $v; do
     if [ $lib = base ]; then unset DREAMER_LIB_VARIANT; else export DREAMER_LIB_VARIANT=$lib; fi
     timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-secondary --wm-steps ${AB_WM:-0} ${AB_ARGS:-} > gpurun_out/ab_${TAG}_$lib.json 2> gpurun_out/ab_${TAG}_$lib.err || { tail -10 gpurun_out/ab_${TAG}_$lib.err; exit 1; }
-    python -c "import json;d=json.load(open('gpurun_out/ab_${TAG}_$lib.json'));print('ab $lib', d['value'], 'encoder_ms', d['roofline']['encoder_ms'])"
+    python -c "import json;d=json.load(open('gpurun_out/ab_${TAG}_$lib.json'));print('ab $lib', d['value'], 'encoder_ms', d['roofline']['encoder_ms'], 'wm_ms', d.get('secondary', {}).get('wm_step', {}).get('ms_per_step'))"
   done
 done
 unset DREAMER_LIB_VARIANT
+if [ "${DPPROBE:-0}" = 1 ]; then
+  timeout -k 10 200 python tools/dp_probe.py 256 > gpurun_out/dpp1_$TAG.txt 2>&1 || { tail -20 gpurun_out/dpp1_$TAG.txt; exit 1; }
+  grep epoch gpurun_out/dpp1_$TAG.txt
+  DREAMER_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29519 tools/dp_probe.py 256 > gpurun_out/dpp2_$TAG.txt 2>&1 || { tail -20 gpurun_out/dpp2_$TAG.txt; exit 1; }
+  grep epoch gpurun_out/dpp2_$TAG.txt
+fi
 echo "gpu_$TAG done"
