@@ -1071,120 +1071,6 @@ bool op_wgrad_split3_supported(int n, int h, int w, int ca, int cb) {
          n > 0 && (long long)n * 4 * h * w * cb < (1LL << 31);
 }
 
-// Double-buffered form (chunks of 32 pixels, two LDS buffers): the split and
-// LDS store of chunk c + 1 go to the other buffer, so they need no barrier
-// after chunk c's MFMAs and the compiler can interleave them (one barrier per
-// chunk).  Staging threads: (channel quad, pixel octet 0..3), BM + 128 of 512.
-template <int BM>
-__global__ __launch_bounds__(512) void k_wgrad_split3_db(int n, int lh, int lw, int ca, int cb,
-                                                         const float* __restrict__ lo, int lda,
-                                                         const float* __restrict__ hi, int ldb, int chunk,
-                                                         float* __restrict__ part) {
-  constexpr int BN = 128, KC = 32, RP = KC / 8 + 1;
-  constexpr int FM = BM / 32, FN = 2;  // wave tile (BM / 2) x 32
-  __shared__ __attribute__((aligned(16))) u32x4 S[2][3][BM + BN][RP];
-  const int N = 16 * cb;
-  const int tiles_n = N / BN, tiles = (ca / BM) * tiles_n;
-  const int split = blockIdx.x / tiles, lt = blockIdx.x - split * tiles;
-  const int m0 = (lt / tiles_n) * BM, n0 = (lt % tiles_n) * BN;
-  const int h = 1 << lh, w = 1 << lw, H2 = 2 * h, W2 = 2 * w;
-  const long long K = (long long)n * h * w;
-  const long long k_begin = (long long)split * chunk;
-  const long long k_end = k_begin + chunk < K ? k_begin + chunk : K;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
-  constexpr int AU = BM / 4 * 4, BUn = BN / 4 * 4;
-  const bool isA = tid < AU, active = tid < AU + BUn;
-  const int u = isA ? tid : tid - AU, cq = u >> 2, oct = u & 3;
-  const int row0 = isA ? 4 * cq : BM + 4 * cq;
-  const int bn = n0 + 4 * cq, btap = bn / cb, bch = bn - btap * cb, bky = btap >> 2, bkx = btap & 3;
-  const float* __restrict__ abase = lo + m0 + 4 * cq;
-  f32x4 v[8];
-  auto load = [&](long long p0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const long long p = p0 + i;
-      bool ok = active && p < k_end;
-      long long off;
-      if (isA) {
-        off = p * lda;
-      } else {
-        const long long f = p >> (lw + lh);
-        const int y = (int)(p >> lw) & (h - 1), x = (int)p & (w - 1);
-        const int Y = 2 * y - 1 + bky, X = 2 * x - 1 + bkx;
-        ok = ok && Y >= 0 && Y < H2 && X >= 0 && X < W2;
-        off = ((f * H2 + Y) * W2 + X) * ldb + bch;
-      }
-      const f32x4 t = *reinterpret_cast<const f32x4*>((isA ? abase : hi) + (ok ? off : 0));
-      v[i] = ok ? t : (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-  };
-  auto store = [&](int buf) __attribute__((always_inline)) {
-    if (!active) return;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      u32x4 ph, pm, pl;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        unsigned hh, mm, ll;
-        split3_pair(v[2 * i][c], v[2 * i + 1][c], hh, mm, ll);
-        ph[i] = hh;
-        pm[i] = mm;
-        pl[i] = ll;
-      }
-      S[buf][0][row0 + c][oct] = ph;
-      S[buf][1][row0 + c][oct] = pm;
-      S[buf][2][row0 + c][oct] = pl;
-    }
-  };
-  const int wm0 = (wave >> 2) * (BM / 2), wn0 = (wave & 3) * 32;
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const long long nch = k_end > k_begin ? (k_end - k_begin + KC - 1) / KC : 0;
-  if (nch > 0) {
-    load(k_begin + 8 * oct);
-    store(0);
-    __syncthreads();
-    for (long long c = 0; c < nch; ++c) {
-      const int buf = (int)(c & 1);
-      load(k_begin + (c + 1 < nch ? c + 1 : c) * KC + 8 * oct);  // (the last chunk reloads itself, unused)
-      u32x4 av[3][FM], bv[3][FN];
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i) av[pl][i] = S[buf][pl][wm0 + 16 * i + r][q];
-#pragma unroll
-        for (int j = 0; j < FN; ++j) bv[pl][j] = S[buf][pl][BM + wn0 + 16 * j + r][q];
-      }
-#define DR_W3(PA, PB)                                                                                   \
-  _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
-      mfma_b16(av[PA][i], bv[PB][j], acc[i][j]);
-      DR_W3(2, 0)
-      DR_W3(1, 1)
-      DR_W3(0, 2)
-      DR_W3(1, 0)
-      DR_W3(0, 1)
-      DR_W3(0, 0)
-#undef DR_W3
-      if (c + 1 < nch) store(buf ^ 1);
-      __syncthreads();
-    }
-  }
-  float* P = part + (long long)split * ca * N;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) P[(long long)(m0 + wm0 + 16 * i + 4 * q + e) * N + n0 + wn0 + 16 * j + r] = acc[i][j][e];
-}
-
-#ifndef DR_WGRAD_DB
-#define DR_WGRAD_DB 0  // A/B knob (tools/build_variant.py): 1 = the double-buffered 32-pixel-chunk kernel
-#endif
-
 static void wgrad3_plan(int n, int h, int w, int ca, int cb, int& nsplit, int& chunk) {
   const int bm = ca >= 128 ? 128 : 64;
   const int tiles = (ca / bm) * (16 * cb / 128);
@@ -1220,13 +1106,7 @@ int op_wgrad_split3(int n, int h, int w, int ca, int cb, const float* lo, int ld
   const int bm = ca >= 128 ? 128 : 64;
   const int tiles = (ca / bm) * (16 * cb / 128);
   const int lh = ilog2_exact(h), lw = ilog2_exact(w);
-  if (DR_WGRAD_DB && bm == 128)
-    hipLaunchKernelGGL(k_wgrad_split3_db<128>, dim3((unsigned)(tiles * ns)), dim3(512), 0, s, n, lh, lw, ca, cb, lo,
-                       lda, hi, ldb, ch, ws);
-  else if (DR_WGRAD_DB)
-    hipLaunchKernelGGL(k_wgrad_split3_db<64>, dim3((unsigned)(tiles * ns)), dim3(512), 0, s, n, lh, lw, ca, cb, lo,
-                       lda, hi, ldb, ch, ws);
-  else if (bm == 128)
+  if (bm == 128)
     hipLaunchKernelGGL(k_wgrad_split3<128>, dim3((unsigned)(tiles * ns)), dim3(512), 0, s, n, lh, lw, ca, cb, lo, lda,
                        hi, ldb, ch, ws);
   else

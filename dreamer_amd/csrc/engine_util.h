@@ -147,6 +147,8 @@ static inline int lnbwd_nt(int M, int N, int K, const float* gx, long long ldgx,
   // at 128+ rows the staged prologue (recomputed by every column tile, 64-row
   // tiles) costs more than one elementwise pass + a plain GEMM: B = 256,
   // N = 1624: 26.5 us fused vs the two launches below
+  // (also for the 200-wide layers: 16.5 us fused against 5.0 + 6.3 split at
+  // B = 256, profiles/r03x_epoch_kernel_table.txt)
   const bool split = gpre != nullptr && M >= 128;
   if (ok && !split) {
     g.pre = pre; g.ld_pre = ld_pre; g.ln_g = ln.w; g.ln_b = ln.b;
