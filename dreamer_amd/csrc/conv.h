@@ -27,6 +27,10 @@ int op_conv_repack_pad(int cout, int cin, int cin_pad, const float* w, float* wr
 // weights: Conv2d [co][ci][4][4] f32 -> 3 bf16 planes [3][co][16][cin] (6 bytes per weight)
 int op_conv_repack_split3(int cout, int cin, const float* w, void* wr, hipStream_t s);
 bool op_conv_split3_supported(int n, int cin, int ih, int iw, int cout);
+// bf16 perf mode's conv3..: the split-conv tiling with one bf16 term (bf16 NHWC in,
+// bf16 NHWC / NCHW out, weights in op_conv_repack_split3 planes)
+int op_conv_s1_bf16(int n, int cin, int ih, int iw, int cout, const void* in, const void* wr, const float* bias,
+                    void* out, int out_nchw, hipStream_t s);
 // k4 s2 p1 conv + bias + SiLU, f32 NHWC in -> f32 NHWC (or NCHW) out, as op_conv_nhwc
 int op_conv_split3(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
                    float* out, int out_nchw, hipStream_t s);

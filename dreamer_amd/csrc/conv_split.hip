@@ -58,27 +58,40 @@ __device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsign
 // group's 16 lanes hit 16 distinct 16-byte bank quads (the plain (r >> 2) & 3
 // swizzle left 2-way conflicts)
 __device__ __forceinline__ int swz(int row) { return (0x1320 >> (((row >> 2) & 3) * 4)) & 3; }
+// four f32 -> four bf16 (RNE), packed
+__device__ __forceinline__ u32x2 pack_bf16x4(f32x4 v) {
+  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+  const bf16x4_t b = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  return __builtin_bit_cast(u32x2, b);
+}
 }  // namespace
 
 // EPI (conv.h): CONV_EPI_FWD: out = SiLU(acc + bias), optionally pre = acc + bias
 // (NHWC, for the world-model backward); CONV_EPI_DSILU (NHWC only, no bias):
 // out = acc * SiLU'(pre) -- the input gradient of a transposed conv followed by
 // the SiLU backward of the layer below (WorldModel.training_step's decoder)
-template <int BM, int BN, int CIN, bool OUT_NCHW, int PIPE, int EPI = CONV_EPI_FWD>
+// NT3 = 1: the bf16 perf mode's form of the same tile -- bf16 NHWC activations
+// staged as they are (one plane), the weights' first split plane (= their RNE
+// bf16), one MFMA per block, bf16 output (RNE after bias + SiLU); `in` / `out`
+// then point at u16 data
+template <int BM, int BN, int CIN, bool OUT_NCHW, int PIPE, int EPI = CONV_EPI_FWD, int NT3 = 3>
 __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, int iw, int cout,
                                                          const float* __restrict__ in, const u16* __restrict__ wr,
                                                          const float* __restrict__ bias, float* __restrict__ out,
                                                          float* __restrict__ pre) {
+  static_assert(NT3 == 3 || (NT3 == 1 && EPI == CONV_EPI_FWD), "conv_split3 terms");
+  const u16* __restrict__ in16 = reinterpret_cast<const u16*>(in);
+  u16* __restrict__ out16 = reinterpret_cast<u16*>(out);
   constexpr int NT = BM * 2;         // WM = BM / 64 waves over pixels x 2 waves over channels
   constexpr int K = CIN * 16;
   constexpr int NCH = K / 32;
   constexpr int WTN = BN / 2, FM = 4, FN = WTN / 16;
   constexpr int APT = BM * 8 / NT;   // float4 of A per thread per chunk (= 4)
-  constexpr int BU = 3 * BN * 4;     // 16-byte B units per chunk (3 planes x BN rows x 4)
+  constexpr int BU = NT3 * BN * 4;   // 16-byte B units per chunk (NT3 planes x BN rows x 4)
   constexpr int BPT = (BU + NT - 1) / NT;
   static_assert(CIN % 32 == 0 && APT == 4 && FN >= 1, "conv_split3 tile");
-  __shared__ __attribute__((aligned(16))) u32x4 As[2][3][BM][4];
-  __shared__ __attribute__((aligned(16))) u32x4 Bs[2][3][BN][4];
+  __shared__ __attribute__((aligned(16))) u32x4 As[2][NT3][BM][4];
+  __shared__ __attribute__((aligned(16))) u32x4 Bs[2][NT3][BN][4];
 
   const int oh = ih / 2, ow = iw / 2, hw = oh * ow;
   const long long M = (long long)n_frames * hw;
@@ -115,10 +128,12 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
   // two ring slots as separate arrays picked at compile time (one 2-D ring
   // array indexed by slot was left in scratch memory by the compiler)
   f32x4 ra0[APT], ra1[APT];
+  u32x2 rh0[APT], rh1[APT];  // NT3 = 1: 4 bf16 channels
   u32x4 rb0[BPT], rb1[BPT];
   unsigned ok0 = 0, ok1 = 0;  // per slot: bit i = A row i's tap is inside the frame
   auto load = [&](int c, auto slot) __attribute__((always_inline)) {
     f32x4* ra = decltype(slot)::value == 0 ? ra0 : ra1;
+    u32x2* rh = decltype(slot)::value == 0 ? rh0 : rh1;
     unsigned& okm = decltype(slot)::value == 0 ? ok0 : ok1;
     u32x4* rb = decltype(slot)::value == 0 ? rb0 : rb1;
     // CIN % 32 == 0: a chunk is 32 channels of one tap (uniform over the workgroup)
@@ -132,7 +147,8 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
       // LDS store: a conditional load compiled to a branch that waited for
       // each load before issuing the next
       const bool ok = (vm[i] >> ky) & (vm[i] >> (4 + kx)) & 1u;
-      ra[i] = *reinterpret_cast<const f32x4*>(in + (ok ? pb[i] + toff : 0));
+      if constexpr (NT3 == 1) rh[i] = *reinterpret_cast<const u32x2*>(in16 + (ok ? pb[i] + toff : 0));
+      else ra[i] = *reinterpret_cast<const f32x4*>(in + (ok ? pb[i] + toff : 0));
       om |= ok ? (1u << i) : 0u;
     }
     okm = om;
@@ -147,19 +163,24 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
   };
   auto store = [&](auto slot, int buf) __attribute__((always_inline)) {
     const f32x4* ra = decltype(slot)::value == 0 ? ra0 : ra1;
+    const u32x2* rh = decltype(slot)::value == 0 ? rh0 : rh1;
     const u32x4* rb = decltype(slot)::value == 0 ? rb0 : rb1;
     const unsigned okm = decltype(slot)::value == 0 ? ok0 : ok1;
 #pragma unroll
     for (int i = 0; i < APT; ++i) {
       const int row = prow + (NT / 8) * i;
-      const f32x4 v = (okm >> i) & 1u ? ra[i] : (f32x4){0.f, 0.f, 0.f, 0.f};
-      unsigned h0, m0_, l0, h1, m1, l1;
-      split3_pair(v[0], v[1], h0, m0_, l0);
-      split3_pair(v[2], v[3], h1, m1, l1);
       const int unit = (quad >> 1) ^ swz(row), half = quad & 1;
-      reinterpret_cast<u32x2*>(&As[buf][0][row][unit])[half] = (u32x2){h0, h1};
-      reinterpret_cast<u32x2*>(&As[buf][1][row][unit])[half] = (u32x2){m0_, m1};
-      reinterpret_cast<u32x2*>(&As[buf][2][row][unit])[half] = (u32x2){l0, l1};
+      if constexpr (NT3 == 1) {
+        reinterpret_cast<u32x2*>(&As[buf][0][row][unit])[half] = (okm >> i) & 1u ? rh[i] : (u32x2){0u, 0u};
+      } else {
+        const f32x4 v = (okm >> i) & 1u ? ra[i] : (f32x4){0.f, 0.f, 0.f, 0.f};
+        unsigned h0, m0_, l0, h1, m1, l1;
+        split3_pair(v[0], v[1], h0, m0_, l0);
+        split3_pair(v[2], v[3], h1, m1, l1);
+        reinterpret_cast<u32x2*>(&As[buf][0][row][unit])[half] = (u32x2){h0, h1};
+        reinterpret_cast<u32x2*>(&As[buf][1][row][unit])[half] = (u32x2){m0_, m1};
+        reinterpret_cast<u32x2*>(&As[buf][2][row][unit])[half] = (u32x2){l0, l1};
+      }
     }
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
@@ -196,9 +217,9 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
     // conditional refill made the compiler wait for every outstanding load
     // before the next LDS store, a one-deep pipeline
     load(min(c + PIPE, NCH - 1), slot);
-    u32x4 a[3][FM], b[3][FN];
+    u32x4 a[NT3][FM], b[NT3][FN];
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) {
+    for (int pl = 0; pl < NT3; ++pl) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) a[pl][i] = As[buf][pl][wm0 + 16 * i + r][fu];
 #pragma unroll
@@ -208,11 +229,13 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
 #define DR_S3(PA, PB)                                                                                   \
   _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
       OUT_NCHW ? mfma_b16(a[PA][i], b[PB][j], acc[i][j]) : mfma_b16(b[PB][j], a[PA][i], acc[i][j]);
-    DR_S3(2, 0)
-    DR_S3(1, 1)
-    DR_S3(0, 2)
-    DR_S3(1, 0)
-    DR_S3(0, 1)
+    if constexpr (NT3 == 3) {
+      DR_S3(2, 0)
+      DR_S3(1, 1)
+      DR_S3(0, 2)
+      DR_S3(1, 0)
+      DR_S3(0, 1)
+    }
     DR_S3(0, 0)
 #undef DR_S3
     if (c + 1 < NCH) store(Next{}, buf ^ 1);
@@ -236,6 +259,13 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
         if (m >= M) continue;
         const float bv = bias[co];
         f32x4 v = acc[i][j] + bv;
+        if constexpr (NT3 == 1) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(v[e]);
+          const long long f = m / hw;
+          *reinterpret_cast<u32x2*>(out16 + (f * cout + co) * hw + (m - f * hw)) = pack_bf16x4(v);
+          continue;
+        }
         if (pre) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) pre[(m + e) * cout + co] = v[e];
@@ -260,6 +290,10 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
           if (pre) *reinterpret_cast<f32x4*>(pre + m * cout + co) = v;
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(v[e]);
+        }
+        if constexpr (NT3 == 1) {
+          *reinterpret_cast<u32x2*>(out16 + m * cout + co) = pack_bf16x4(v);
+          continue;
         }
         *reinterpret_cast<f32x4*>(out + m * cout + co) = v;
       }
@@ -674,6 +708,46 @@ int op_conv_split3_ex(int n, int cin, int ih, int iw, int cout, const float* in,
 int op_conv_split3(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
                    float* out, int out_nchw, hipStream_t s) {
   return op_conv_split3_ex(n, cin, ih, iw, cout, in, wr, bias, out, out_nchw, nullptr, CONV_EPI_FWD, s);
+}
+
+// bf16 perf mode: the same tiling with one term (k_conv_split3<..., NT3 = 1>):
+// bf16 NHWC in, bf16 NHWC / NCHW out, weights as op_conv_repack_split3 planes
+// (plane 0 read).  Replaces k_conv_bf16 for conv3.. (its 128 x 128 tiles ran
+// at 0.16 of the bf16 peak).
+template <int BN, int C, bool NCHW>
+static int launch_s1(int n, int ih, int iw, int cout, const void* in, const void* wr, const float* bias, void* out,
+                     hipStream_t s) {
+  const long long M = (long long)n * (ih / 2) * (iw / 2);
+  const long long tiles = ((M + 255) / 256) * (cout / BN);
+  if (tiles >= (1LL << 30)) {
+    dr_set_error("conv_s1_bf16: too many tiles");
+    return DR_E_INVALID;
+  }
+  hipLaunchKernelGGL((k_conv_split3<256, BN, C, NCHW, 2, CONV_EPI_FWD, 1>), dim3((unsigned)dr_xcd_grid((int)tiles)),
+                     dim3(512), 0, s, n, ih, iw, cout, (const float*)in, (const u16*)wr, bias, (float*)out, nullptr);
+  return dr_check_launch("conv_s1_bf16");
+}
+
+int op_conv_s1_bf16(int n, int cin, int ih, int iw, int cout, const void* in, const void* wr, const float* bias,
+                    void* out, int out_nchw, hipStream_t s) {
+  if (!op_conv_split3_supported(n, cin, ih, iw, cout) || (((uintptr_t)in | (uintptr_t)out | (uintptr_t)bias) & 15)) {
+    dr_set_error("conv_s1_bf16: unsupported shape (cin=%d ih=%d iw=%d cout=%d)", cin, ih, iw, cout);
+    return DR_E_INVALID;
+  }
+#define DR_S1L(C)                                                                              \
+  if (cin == C) {                                                                              \
+    if (cout % 128 == 0)                                                                       \
+      return out_nchw ? launch_s1<128, C, true>(n, ih, iw, cout, in, wr, bias, out, s)         \
+                      : launch_s1<128, C, false>(n, ih, iw, cout, in, wr, bias, out, s);       \
+    return out_nchw ? launch_s1<64, C, true>(n, ih, iw, cout, in, wr, bias, out, s)            \
+                    : launch_s1<64, C, false>(n, ih, iw, cout, in, wr, bias, out, s);          \
+  }
+  DR_S1L(32)
+  DR_S1L(64)
+  DR_S1L(128)
+  DR_S1L(256)
+#undef DR_S1L
+  return DR_E_INVALID;
 }
 
 // ---------------------------------------------------------------------------
