@@ -29,6 +29,11 @@ int op_conv_repack_split3(int cout, int cin, const float* w, void* wr, hipStream
 bool op_conv_split3_supported(int n, int cin, int ih, int iw, int cout);
 // bf16 perf mode's conv3..: the split-conv tiling with one bf16 term (bf16 NHWC in,
 // bf16 NHWC / NCHW out, weights in op_conv_repack_split3 planes)
+// bf16 perf mode's conv1 + conv2: k_enc12_split3 with one bf16 term (64 x 64,
+// 32 -> 64 channels, u8 ring only; DR_E_INVALID, nothing launched, otherwise)
+int op_enc12_s1_bf16(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
+                     const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, void* out,
+                     hipStream_t s);
 int op_conv_s1_bf16(int n, int cin, int ih, int iw, int cout, const void* in, const void* wr, const float* bias,
                     void* out, int out_nchw, hipStream_t s);
 // k4 s2 p1 conv + bias + SiLU, f32 NHWC in -> f32 NHWC (or NCHW) out, as op_conv_nhwc

@@ -356,27 +356,43 @@ int op_conv_repack_split3(int cout, int cin, const float* w, void* wr, hipStream
 #define E12_RI (2 * E12_R1 + 2)
 #define E12_PS (E12_R1 * 32 + 1)
 #define E12_LWI 66
-static constexpr size_t e12_lds_bytes() { return (size_t)3 * 4 * E12_PS * 16 + (size_t)E12_RI * E12_LWI * 8; }
+static constexpr size_t e12_lds_bytes(int terms = 3) {
+  return (size_t)terms * 4 * E12_PS * 16 + (size_t)E12_RI * E12_LWI * 8;
+}
 
 // NW = 8: two waves per SIMD -- waves 0-3 run conv2's taps 0-7 and waves 4-7
 // taps 8-15 over the same 64 x 32 output blocks, the two partial sums meet in
 // LDS (fixed order: taps 0-7 + taps 8-15) before the epilogue
-template <int NW>
 // Optional saves for the world-model backward (NHWC f32, NULL = none): pre0 /
 // a0 = conv1's pre-activation / output (the tile's own 16 conv1 rows), pre1 =
 // conv2's pre-activation (out receives conv2's output as always).
-__global__ __launch_bounds__(64 * NW) void k_enc12_split3(int n, int nb, dr_frames src, const u16* __restrict__ wr1,
+// NTM = 1: the bf16 perf mode's form -- the weights' first plane (their RNE
+// bf16) only, conv1's output rounded (RNE) to ONE bf16 plane in LDS, one MFMA
+// per block, conv2's output written as bf16 NHWC (`out` then points at u16
+// data); no saves.  One third of the LDS, so two workgroups fit per CU.
+// one-term form (bf16 mode), measured at B = 256 (profiles/r03za_ab_enc12_s1.txt):
+// 4 waves, two workgroups per CU (57 KB of LDS each; 164 VGPRs, no spill):
+// encoder 0.936 ms; 8 waves at two workgroups per CU (128 VGPRs, 104 B spilled)
+// 1.01-1.02 ms; 8 waves at one (165 VGPRs) 0.962 ms
+#ifndef DR_E12S1_WAVES
+#define DR_E12S1_WAVES 4  // A/B knob: waves per workgroup of the one-term form
+#endif
+#ifndef DR_E12S1_OCC
+#define DR_E12S1_OCC 2  // A/B knob: min waves per SIMD of the one-term form
+#endif
+template <int NW, int NTM = 3>
+__global__ __launch_bounds__(64 * NW, NTM == 1 ? DR_E12S1_OCC : 1) void k_enc12_split3(int n, int nb, dr_frames src, const u16* __restrict__ wr1,
                                                           const float* __restrict__ b1, const u16* __restrict__ wr2,
                                                           const float* __restrict__ b2, float* __restrict__ out,
                                                           float* __restrict__ pre0, float* __restrict__ a0,
                                                           float* __restrict__ pre1) {
-  static_assert(NW == 4 || NW == 8, "enc12 waves");
+  static_assert((NW == 4 || NW == 8) && (NTM == 1 || NTM == 3), "enc12 waves / terms");
   constexpr int NTH = 64 * NW, TAPS = NW == 8 ? 8 : 16;
   constexpr int R2 = E12_R2, R1 = E12_R1, RI = E12_RI, PS = E12_PS, LWI = E12_LWI;
   constexpr int OW1 = 32, OW2 = 16, W = 64, H = 64, C1 = 32, C2 = 64;
   extern __shared__ __attribute__((aligned(16))) u32x4 e12_smem[];
   u32x4* c1o = e12_smem;                                                       // [3][4][PS]
-  uint2* xin = reinterpret_cast<uint2*>(e12_smem + 3 * 4 * PS);               // [RI][LWI]
+  uint2* xin = reinterpret_cast<uint2*>(e12_smem + NTM * 4 * PS);             // [RI][LWI]
   u16* xs = reinterpret_cast<u16*>(xin);
   u16* c1h = reinterpret_cast<u16*>(c1o);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
@@ -429,9 +445,9 @@ __global__ __launch_bounds__(64 * NW) void k_enc12_split3(int n, int nb, dr_fram
   // conv2 weight fragments straight from L2 (the 196 KB of split planes stay
   // resident): lane (r, q) of wf[pl][jj] = row 32 ch + 16 jj + r, k 8 q .. + 7
   const u16* wbase = wr2 + ((long long)(32 * ch + r)) * 32 + 8 * q;
-  auto wld = [&](u32x4 (&wf)[3][2], int tap) __attribute__((always_inline)) {
+  auto wld = [&](u32x4 (&wf)[NTM][2], int tap) __attribute__((always_inline)) {
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
+    for (int pl = 0; pl < NTM; ++pl)
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj)
         wf[pl][jj] = *reinterpret_cast<const u32x4*>(wbase + ((long long)(tap * 3 + pl) * C2 + 16 * jj) * 32);
@@ -442,9 +458,9 @@ __global__ __launch_bounds__(64 * NW) void k_enc12_split3(int n, int nb, dr_fram
     const int next = tile + (int)gridDim.x;
     // conv1 weights (A operand: lane -> channel 16 j + r, k = 32 s + 8 q .. + 7), three
     // planes: re-read per tile (L2) so that they hold no registers during conv2
-    u32x4 wa1[3][2][2];
+    u32x4 wa1[NTM][2][2];
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
+    for (int pl = 0; pl < NTM; ++pl)
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -455,7 +471,7 @@ __global__ __launch_bounds__(64 * NW) void k_enc12_split3(int n, int nb, dr_fram
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) bb1[j][e] = b1[16 * j + 4 * q + e];
-    u32x4 wfa[3][2], wfb[3][2];
+    u32x4 wfa[NTM][2], wfb[NTM][2];
     wld(wfa, TAPS * kh);
     // ---- conv1 over the R1 tile rows; rows outside the frame are conv2's zero padding ----
     constexpr int F1 = R1 * OW1 / 16;
@@ -474,13 +490,12 @@ __global__ __launch_bounds__(64 * NW) void k_enc12_split3(int n, int nb, dr_fram
           const u32x4 pb = *reinterpret_cast<const u32x4*>(&xin[(2 * yl + ky) * LWI + 2 * x1 + kx]);
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            acc[j] = mfma_b16(wa1[2][s][j], pb, acc[j]);
-            acc[j] = mfma_b16(wa1[1][s][j], pb, acc[j]);
-            acc[j] = mfma_b16(wa1[0][s][j], pb, acc[j]);
+#pragma unroll
+            for (int pl = NTM - 1; pl >= 0; --pl) acc[j] = mfma_b16(wa1[pl][s][j], pb, acc[j]);
           }
         }
         // lane: pixel p, channels 16 j + 4 q .. + 3
-        const bool own = pre0 && yl >= 1 && yl <= 2 * R2;  // this tile's own conv1 rows
+        const bool own = NTM == 3 && pre0 && yl >= 1 && yl <= 2 * R2;  // this tile's own conv1 rows
         const long long o1 = (((long long)f * (H / 2) + y1) * OW1 + x1) * C1;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -494,8 +509,13 @@ __global__ __launch_bounds__(64 * NW) void k_enc12_split3(int n, int nb, dr_fram
             *reinterpret_cast<f32x4*>(pre0 + o1 + 16 * j + 4 * q) = (f32x4){pv[0], pv[1], pv[2], pv[3]};
             *reinterpret_cast<f32x4*>(a0 + o1 + 16 * j + 4 * q) = (f32x4){v[0], v[1], v[2], v[3]};
           }
-          split3_pair(v[0], v[1], hv[j].x, mv[j].x, lv[j].x);
-          split3_pair(v[2], v[3], hv[j].y, mv[j].y, lv[j].y);
+          if constexpr (NTM == 1) {
+            const u32x2 pk = pack_bf16x4((f32x4){v[0], v[1], v[2], v[3]});
+            hv[j] = make_uint2(pk[0], pk[1]);
+          } else {
+            split3_pair(v[0], v[1], hv[j].x, mv[j].x, lv[j].x);
+            split3_pair(v[2], v[3], hv[j].y, mv[j].y, lv[j].y);
+          }
         }
       }
 #pragma unroll
@@ -503,8 +523,10 @@ __global__ __launch_bounds__(64 * NW) void k_enc12_split3(int n, int nb, dr_fram
         const int c8 = 2 * j + (q >> 1);
         const int o = (c8 * PS + p) * 8 + (q & 1) * 4;  // u16 offset inside a plane
         *reinterpret_cast<uint2*>(c1h + o) = hv[j];
-        *reinterpret_cast<uint2*>(c1h + 4 * PS * 8 + o) = mv[j];
-        *reinterpret_cast<uint2*>(c1h + 2 * 4 * PS * 8 + o) = lv[j];
+        if constexpr (NTM == 3) {
+          *reinterpret_cast<uint2*>(c1h + 4 * PS * 8 + o) = mv[j];
+          *reinterpret_cast<uint2*>(c1h + 2 * 4 * PS * 8 + o) = lv[j];
+        }
       }
     }
     __syncthreads();
@@ -518,18 +540,18 @@ __global__ __launch_bounds__(64 * NW) void k_enc12_split3(int n, int nb, dr_fram
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) acc[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    auto tap_step = [&](int tap, u32x4 (&wf)[3][2], u32x4 (&wn)[3][2]) __attribute__((always_inline)) {
+    auto tap_step = [&](int tap, u32x4 (&wf)[NTM][2], u32x4 (&wn)[NTM][2]) __attribute__((always_inline)) {
       wld(wn, tap + 1 < TAPS * (kh + 1) ? tap + 1 : tap);  // one tap ahead (the last reload is unused)
       const int ky = tap >> 2, kx = tap & 3;
       const int x1 = 2 * r - 1 + kx;
       const bool xok = x1 >= 0 && x1 < OW1;
-      u32x4 pf[3][4];
+      u32x4 pf[NTM][4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int yl = 2 * (4 * ph + i) + ky;
         const int u = q * PS + yl * OW1 + (xok ? x1 : 0);
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
+        for (int pl = 0; pl < NTM; ++pl) {
           const u32x4 v = c1o[pl * 4 * PS + u];
           pf[pl][i] = xok ? v : (u32x4){0u, 0u, 0u, 0u};
         }
@@ -538,11 +560,13 @@ __global__ __launch_bounds__(64 * NW) void k_enc12_split3(int n, int nb, dr_fram
 #define E12_S3(PW, PA)                       \
   _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int jj = 0; jj < 2; ++jj) acc[i][jj] = \
       mfma_b16(wf[PW][jj], pf[PA][i], acc[i][jj]);
-      E12_S3(2, 0)
-      E12_S3(1, 1)
-      E12_S3(0, 2)
-      E12_S3(1, 0)
-      E12_S3(0, 1)
+      if constexpr (NTM == 3) {
+        E12_S3(2, 0)
+        E12_S3(1, 1)
+        E12_S3(0, 2)
+        E12_S3(1, 0)
+        E12_S3(0, 1)
+      }
       E12_S3(0, 0)
 #undef E12_S3
     };
@@ -550,7 +574,7 @@ __global__ __launch_bounds__(64 * NW) void k_enc12_split3(int n, int nb, dr_fram
     for (int tap = TAPS * kh; tap < TAPS * (kh + 1); ++tap) {
       tap_step(tap, wfa, wfb);
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
+      for (int pl = 0; pl < NTM; ++pl)
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) wfa[pl][jj] = wfb[pl][jj];
     }
@@ -585,6 +609,10 @@ __global__ __launch_bounds__(64 * NW) void k_enc12_split3(int n, int nb, dr_fram
         const f32x4 pv = acc[i][jj] + bv;
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(pv[e]);
+        if constexpr (NTM == 1) {
+          *reinterpret_cast<u32x2*>(reinterpret_cast<u16*>(out) + (o - out) + co) = pack_bf16x4(v);
+          continue;
+        }
         *reinterpret_cast<f32x4*>(o + co) = v;
         if (pre1) *reinterpret_cast<f32x4*>(pre1 + (o - out) + co) = pv;
       }
@@ -649,6 +677,39 @@ int op_enc12_split3_ex(int n, int nb, int h, int w, int c1, int c2, const dr_fra
     hipLaunchKernelGGL(k_enc12_split3<4>, dim3((unsigned)grid), dim3(256), e12_lds_bytes(), s, n, nb, *src,
                        (const u16*)wr1, b1, (const u16*)wr2, b2, out, pre0, a0, pre1);
   return dr_check_launch("enc12_split3");
+}
+
+// bf16 perf mode: k_enc12_split3<DR_E12S1_WAVES, 1> (one bf16 term; out = bf16 NHWC).
+// wr1 / wr2 are the split3 repack slots (c1 * 64 * 6 and c2 * c1 * 16 * 6
+// bytes; plane 0 is read).  DR_E_INVALID (nothing launched) for other shapes.
+int op_enc12_s1_bf16(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
+                     const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, void* out,
+                     hipStream_t s) {
+  if (c1 != 32 || c2 != 64 || h != 64 || w != 64 || !src->ring || !src->starts || src->ring_cap <= 0 || n <= 0 ||
+      (long long)n * 2 >= (1LL << 31) || ((uintptr_t)out & 15))
+    return DR_E_INVALID;
+  // persistent: as many workgroups as are resident at once (occupancy x CUs)
+  static int slots[64];
+  int dev = 0;
+  DR_TRY_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return DR_E_INVALID;
+  if (slots[dev] == 0) {
+    (void)hipFuncSetAttribute((const void*)k_enc12_split3<DR_E12S1_WAVES, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)e12_lds_bytes(1));
+    int cus = 0, per = 0;
+    DR_TRY_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    DR_TRY_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_enc12_split3<DR_E12S1_WAVES, 1>,
+                                                            64 * DR_E12S1_WAVES, e12_lds_bytes(1)));
+    slots[dev] = std::max(1, per) * std::max(1, cus);
+  }
+  hipLaunchKernelGGL(k_conv1_repack_split3, dim3((c1 * 64 + 255) / 256), dim3(256), 0, s, c1, w1, (u16*)wr1);
+  DR_TRY(dr_check_launch("conv1_repack_split3"));
+  DR_TRY(op_conv_repack_split3(c2, c1, w2, wr2, s));
+  const int grid = std::min(n * 2, slots[dev]);
+  hipLaunchKernelGGL((k_enc12_split3<DR_E12S1_WAVES, 1>), dim3((unsigned)grid), dim3(64 * DR_E12S1_WAVES),
+                     e12_lds_bytes(1), s, n, nb, *src,
+                     (const u16*)wr1, b1, (const u16*)wr2, b2, (float*)out, nullptr, nullptr, nullptr);
+  return dr_check_launch("enc12_s1_bf16");
 }
 
 template <int BM, int BN, int CIN, bool NCHW, int PIPE, int EPI = CONV_EPI_FWD>

@@ -46,14 +46,12 @@ static void enc_carve(Carve& c, const dr_dims* d, int n, EncWs& w) {
   w.sk = bf ? nullptr : c.f(w.sk_n);
   w.x0 = bf ? nullptr : c.f((long long)n * p0 * 4);
   for (int k = 0; k < N; ++k) w.a[k] = act((long long)n * (p0 >> (2 * (k + 1))) * e[k + 1]);
-  // conv1 weights: f32 [cout][64] (k_conv1_frames) or three bf16 planes (k_enc12_split3)
-  w.wr[0] = bf ? act((long long)e[1] * 4 * 16) : (float*)c.raw((size_t)e[1] * 64 * 6);
-  // fp32: conv2..N weights as three bf16 planes (op_conv_repack_split3, 6 bytes
-  // per weight; the f32 repack of the fallback fits in the same slot)
-  for (int k = 1; k < N; ++k) {  // (bf16 mode, k >= 2: the split planes of op_conv_s1_bf16 too)
-    const long long elems = (long long)e[k + 1] * e[k] * 16;
-    w.wr[k] = bf && k == 1 ? (float*)c.raw(elems * 2) : (float*)c.raw(elems * 6);
-  }
+  // conv1 weights: f32 [cout][64] (k_conv1_frames) or three bf16 planes
+  // (k_enc12_split3, both modes; the bf16 repack of k_enc12_bf16 fits in it)
+  w.wr[0] = (float*)c.raw((size_t)e[1] * 64 * 6);
+  // conv2..N weights as three bf16 planes (op_conv_repack_split3, 6 bytes per
+  // weight; the f32 / bf16 repacks of the fallbacks fit in the same slot)
+  for (int k = 1; k < N; ++k) w.wr[k] = (float*)c.raw((long long)e[k + 1] * e[k] * 16 * 6);
   w.wproj = bf ? c.raw((size_t)d->enc_hidden * enc_feat_dim(d) * 2) : nullptr;
   w.s3proj = bf ? nullptr : c.raw(op_nt_split3_ws_bytes(d->enc_hidden, enc_feat_dim(d)));
   w.s3part_n = bf ? 0 : op_gemm_nt_split3_part_floats(n, d->enc_hidden);
@@ -76,15 +74,21 @@ static int encoder_bf16(const dr_dims* d, const dr_world_model* wm, const dr_fra
   const int N = enc_chans(d, e);
   const int h0 = d->img_h, w0 = d->img_w;
   const int F = enc_feat_dim(d);
-  DR_TRY(op_conv_repack_bf16(e[1], 3, 4, wm->conv[0].w, w.wr[0], s));
-  for (int k = 1; k < N; ++k)
-    if (k == 1 || !op_conv_split3_supported(n, e[k], h0 >> k, w0 >> k, e[k + 1]))
+  for (int k = 2; k < N; ++k)
+    if (!op_conv_split3_supported(n, e[k], h0 >> k, w0 >> k, e[k + 1]))
       DR_TRY(op_conv_repack_bf16(e[k + 1], e[k], e[k], wm->conv[k].w, w.wr[k], s));
   DR_TRY(op_to_bf16_2d(d->enc_hidden, F, wm->map0.w, F + d->hidden, w.wproj, s));
-  if (op_enc12_bf16(n, B, h0, w0, e[1], e[2], src, w.wr[0], wm->conv[0].b, w.wr[1], wm->conv[1].b, w.a[1], s) !=
-      DR_OK) {
-    DR_TRY(op_conv1_bf16(n, B, h0, w0, e[1], src, w.wr[0], wm->conv[0].b, w.a[0], s));
-    DR_TRY(op_conv_bf16(n, e[1], h0 / 2, w0 / 2, e[2], w.a[0], w.wr[1], wm->conv[1].b, w.a[1], 0, s));
+  // conv1 + conv2: k_enc12_split3 with one term (64 x 64 from the u8 ring), else
+  // k_enc12_bf16, else two launches
+  if (op_enc12_s1_bf16(n, B, h0, w0, e[1], e[2], src, wm->conv[0].w, wm->conv[0].b, wm->conv[1].w, wm->conv[1].b,
+                       w.wr[0], w.wr[1], w.a[1], s) != DR_OK) {
+    DR_TRY(op_conv_repack_bf16(e[1], 3, 4, wm->conv[0].w, w.wr[0], s));
+    DR_TRY(op_conv_repack_bf16(e[2], e[1], e[1], wm->conv[1].w, w.wr[1], s));
+    if (op_enc12_bf16(n, B, h0, w0, e[1], e[2], src, w.wr[0], wm->conv[0].b, w.wr[1], wm->conv[1].b, w.a[1], s) !=
+        DR_OK) {
+      DR_TRY(op_conv1_bf16(n, B, h0, w0, e[1], src, w.wr[0], wm->conv[0].b, w.a[0], s));
+      DR_TRY(op_conv_bf16(n, e[1], h0 / 2, w0 / 2, e[2], w.a[0], w.wr[1], wm->conv[1].b, w.a[1], 0, s));
+    }
   }
   for (int k = 2; k < N; ++k) {
     // the split-conv tiling with one bf16 term where the shape allows, else k_conv_bf16
