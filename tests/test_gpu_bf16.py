@@ -200,6 +200,44 @@ def test_encoder_fp32_from_frames_matches_torch(gpu, res):
     assert err <= 1e-5
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_encoder_persistent_tiles_match_reference(gpu, precision):
+    """The persistent conv1 + conv2 kernels (k_enc12_split3: one workgroup per
+    CU in fp32; the one-term form, two per CU, in bf16) walk several tiles per
+    workgroup only when the frames outnumber the resident grid: 1536 frames =
+    3072 half-frame tiles, against 256 / 512 resident workgroups.  Every frame
+    is checked on its own (a wrong tile in a later loop iteration must not hide
+    in a normwise average): fp32 against torch's f32 stack at 1e-5, bf16 against
+    the bf16 emulation at 4e-3 per frame (2e-3 normwise).  Measured: fp32 worst
+    frame 2.7e-7, bf16 worst frame 1.0e-3 (normwise 8.7e-4)."""
+    from dreamer_amd import Dreamer
+    from formula import FULL
+    cfg = dict(FULL)
+    cfg.update(precision=precision)
+    torch.manual_seed(0)
+    d = Dreamer(cfg, gpu)
+    wm = d.world_model
+    g = torch.Generator().manual_seed(7)
+    frames = torch.randint(0, 256, (1536, 3, 64, 64), generator=g, dtype=torch.uint8)
+    got = _features(wm.packed(), wm.dims(d.agent), frames, gpu)
+    P = {k: v.detach().cpu() for k, v in wm.encoder.state_dict().items()}
+    if precision == "bf16":
+        ref = _emulate(frames, P)
+        tol_frame, tol_all = 4e-3, 2e-3
+    else:
+        x = frames.float() / 255.0 - 0.5
+        for i in range(4):
+            x = F.silu(F.conv2d(x, P[f"feature_extractor.{2 * i}.weight"], P[f"feature_extractor.{2 * i}.bias"],
+                                stride=2, padding=1))
+        flat = x.flatten(1)
+        ref = flat @ P["latent_mapper.0.weight"][:, :flat.shape[1]].t() + P["latent_mapper.0.bias"]
+        tol_frame, tol_all = 1e-5, 1e-5
+    per_frame = ((got - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
+    err = float((got - ref).norm() / ref.norm())
+    print(f"{precision}: 1536 frames, normwise {err:.2e}, worst frame {per_frame:.2e}")
+    assert err <= tol_all and per_frame <= tol_frame, (err, per_frame)
+
+
 def test_encoder_fp32_split_is_f32_accurate(gpu):
     """The fp32 encoder's conv2..4 run on the bf16 MFMA with a 3-term split
     (conv_split.hip): its error against a float64 conv stack must be of the
