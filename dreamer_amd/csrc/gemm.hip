@@ -2328,6 +2328,11 @@ static bool tile_offsets_ok(const GemmBatch& gb, int count) {
   return true;
 }
 
+#ifndef DR_B16_CHAIN_TILE
+// bf16 mode's chain products on k_gemm_tile_b16 (0: the f32 wave-K kernel):
+// bf16 headline 730.5 k against 723.3 k (profiles/r03zf_ab_bf16_chain_route.txt)
+#define DR_B16_CHAIN_TILE 1  // A/B knob
+#endif
 template <int AMODE, bool A_KM, bool B_KN>
 static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
   if (AMODE == AM_PLAIN && tile_offsets_ok(gb, count)) {
@@ -2361,7 +2366,7 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
         // 15.8 -> 13.0 us, BPTT 32.2 -> 25.7, GRU hidden product 13.3 -> 12.3,
         // profiles/r03g_kbench_wk.txt); the LDS tile kernel stays for the
         // shapes the wave-K kernel does not take (and as kbench variant 25)
-        if (b16_ok(gb, count)) launch_tile_b16<32, 32, 4>(gt, count, s);
+        if (DR_B16_CHAIN_TILE && b16_ok(gb, count)) launch_tile_b16<32, 32, 4>(gt, count, s);
         else if (g_tile_variant == 0 && wk_ok(gb, count)) launch_wk<32, 32, 4, 2, 1>(gt, count, s, 0);
         else if (g_tile_variant >= 12 && g_tile_variant < 25 && wk_ok(gb, count)) {
           GemmBatch gw = gb;  // (split-K scratch kept: launch_wk splits only under 256 tiles)
