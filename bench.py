@@ -343,6 +343,34 @@ def traffic_for(B, res, precision):
     return t.get("encoder_bytes_per_epoch"), os.path.relpath(path, REPO)
 
 
+def profile_encoder_ms(precision):
+    """Encoder-group kernel time per epoch from the latest committed rocprofv3
+    --kernel-trace --stats summary of the headline bench command
+    (profiles/r*_kernel_stats*.txt; tools/prof_summary.py format): the sum of
+    the average durations of every kernel launched as often as the fused conv1 +
+    conv2 kernel (one launch per encode: the convs, their weight repacks, the
+    projection).  Returns (ms, kernels, source) or (None, None, None)."""
+    import glob
+    import re
+    tag = "_bf16" if precision == "bf16" else ""
+    paths = [p for p in sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_kernel_stats{tag}.txt")))
+             if precision == "bf16" or "_bf16" not in p]
+    if not paths:
+        return None, None, None
+    path = paths[-1]
+    rows = []
+    for line in open(path):
+        m = re.match(r"\s*([\d.]+)\s+(\d+)\s+([\d.]+)\s+(.*)", line)
+        if m:
+            rows.append((int(m.group(2)), float(m.group(3)), m.group(4)))
+    enc = [r for r in rows if "k_enc12" in r[2]]
+    if not enc:
+        return None, None, None
+    n = enc[0][0]
+    grp = [r for r in rows if r[0] == n]
+    return sum(r[1] for r in grp) / 1e3, [r[2].split("(")[0][:60] for r in grp], os.path.relpath(path, REPO)
+
+
 def make_dreamer(cfg, dev, B, S, H, res, ac_epochs, world, rank, group, precision, depth=4):
     from dreamer_amd import Dreamer
     from dreamer_amd.engine import ImaginationEngine
@@ -584,6 +612,13 @@ def main():
     if args.precision != "bf16":
         out["roofline"]["frac_vs_f32_mfma_peak"] = round(achieved / FP32_MFMA_PEAK_TFLOPS, 4)
         out["roofline"]["frac_vs_bf16_pipe"] = round(6 * achieved / BF16_MFMA_PEAK_TFLOPS, 4)
+    if (B, S, H, res) == (256, 64, 15, 64):
+        # the same group from the committed kernel trace (per-kernel averages under the profiler)
+        pms, pk, psrc = profile_encoder_ms(args.precision)
+        if pms:
+            out["roofline"]["profile"] = {"encoder_ms": round(pms, 4), "frac": round(enc_flops / (pms / 1e3) / 1e12 / peak, 4),
+                                          "live_over_profile": round(enc_s * 1e3 / pms, 4), "kernels": pk,
+                                          "source": psrc}
     mf = PATH_MFLOP_PER_STEP.get((S, H, res))
     if mf is not None:
         tf = value * mf * 1e6 / 1e12
@@ -591,6 +626,16 @@ def main():
                                 "unit": "TFLOP/s", "frac": round(tf / path_peak, 4),
                                 "mflop_per_imagined_step": mf,
                                 "note": "whole train_Agent epoch, SURVEY §8d necessary FLOPs x imagined steps/s"}
+        # the chain: everything but the encoder group (warm-start scan, dream, update) per epoch
+        chain_fl = mf * 1e6 * B * H - enc_flops
+        chain_s = el / args.steps - enc_s
+        if chain_s > 0:
+            ctf = chain_fl / chain_s / 1e12
+            out["chain_roofline"] = {"bound": "mfma", "achieved": round(ctf, 2), "peak": path_peak, "unit": "TFLOP/s",
+                                     "frac": round(ctf / path_peak, 4), "gflop_per_epoch": round(chain_fl / 1e9, 2),
+                                     "ms_per_epoch": round(chain_s * 1e3, 4),
+                                     "note": "non-encoder FLOPs of the epoch (SURVEY §8d total - encoder group) over "
+                                             "the epoch time minus the live encoder time"}
     if wm is not None:
         wm_s, wm_gpu_s, wm_loss = wm
         fl = wm_step_flops(cfg, B, H)

@@ -159,13 +159,25 @@ def load():
     return lib
 
 
+# include/dreamer_hip.h error codes
+DR_E_INVALID, DR_E_HIP, DR_E_WORKSPACE, DR_E_UNSUPPORTED = 1001, 1002, 1003, 1004
+
+
+class HipError(RuntimeError):
+    """A libdreamer_hip entry point returned a non-zero code (``.code``)."""
+
+    def __init__(self, name, code, msg):
+        super().__init__(f"{name} failed ({code}): {msg}")
+        self.code = code
+
+
 def call(name, *args):
-    """Call an int-returning entry point; raise on a non-zero code."""
+    """Call an int-returning entry point; raise HipError on a non-zero code."""
     lib = load()
     rc = getattr(lib, name)(*args)
     if rc != 0:
         msg = lib.dr_last_error().decode(errors="replace")
-        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+        raise HipError(name, rc, msg)
 
 
 def query(name, *args):

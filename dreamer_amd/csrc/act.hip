@@ -45,6 +45,7 @@ struct alignas(16) ActArgs {
   unsigned* bar;
   float *c1, *c2, *c3, *c4, *gi, *gh, *hn, *pre1, *prea;
   int* fail;
+  int spin_limit;  // polls before a grid barrier gives up (ACT_SPIN_LIMIT; 0 under DREAMER_ACT_FORCE=timeout)
   long long* ts;  // workgroup 0's stage timestamps (100 MHz wall clock), for profiling
 };
 
@@ -56,7 +57,7 @@ struct alignas(16) ActArgs {
 // poll.  Arrivals are agent-scope releases, every exit an agent-scope acquire.
 // bar: [0..8) group counters, [16] top counter, [32..40) generations (128-B apart).
 #define ACT_GROUPS 8
-__device__ __forceinline__ bool act_sync(unsigned* bar, unsigned& round, int* s_ok) {
+__device__ __forceinline__ bool act_sync(unsigned* bar, unsigned& round, int* s_ok, int spin_limit) {
   __syncthreads();
   if (threadIdx.x == 0) {
     ++round;
@@ -71,7 +72,7 @@ __device__ __forceinline__ bool act_sync(unsigned* bar, unsigned& round, int* s_
       __hip_atomic_fetch_add(top, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       while (__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < round * ACT_GROUPS) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > ACT_SPIN_LIMIT) {
+        if (++spins > spin_limit) {
           ok = 0;
           break;
         }
@@ -81,7 +82,7 @@ __device__ __forceinline__ bool act_sync(unsigned* bar, unsigned& round, int* s_
     } else {
       while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < round) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > ACT_SPIN_LIMIT) {
+        if (++spins > spin_limit) {
           ok = 0;
           break;
         }
@@ -308,7 +309,7 @@ __global__ __launch_bounds__(ACT_NT) void k_act_step(ActArgs ga) {
     act_dense<10>(3 * Hd, Hd, a.wm.w_hh, Hd, a.wm.b_hh, xs + off + 2048, a.gh, gw, nw);
   }
   act_conv<1, true, false>(H0, W0, 3, c1, nullptr, a.frame, a.wm.conv[0].w, a.wm.conv[0].b, a.c1, xs);
-  ok = act_sync(a.bar, round, &s_ok);
+  ok = act_sync(a.bar, round, &s_ok, a.spin_limit);
   ACT_TS(a, 1);
   // ---- stage 2: conv2  ||  GRU gates (torch gru_cell order r, z, n) ----
   if (ok) {
@@ -327,13 +328,13 @@ __global__ __launch_bounds__(ACT_NT) void k_act_step(ActArgs ga) {
     }
     act_conv<8, false, false>(H0 / 2, W0 / 2, c1, c2, a.c1, nullptr, a.wm.conv[1].w, a.wm.conv[1].b, a.c2, xs);
   }
-  if (ok) ok = act_sync(a.bar, round, &s_ok);
+  if (ok) ok = act_sync(a.bar, round, &s_ok, a.spin_limit);
   ACT_TS(a, 2);
   if (ok) act_conv<16, false, false>(H0 / 4, W0 / 4, c2, c3, a.c2, nullptr, a.wm.conv[2].w, a.wm.conv[2].b, a.c3, xs);
-  if (ok) ok = act_sync(a.bar, round, &s_ok);
+  if (ok) ok = act_sync(a.bar, round, &s_ok, a.spin_limit);
   ACT_TS(a, 3);
   if (ok) act_conv<32, false, true>(H0 / 8, W0 / 8, c3, c4, a.c3, nullptr, a.wm.conv[3].w, a.wm.conv[3].b, a.c4, xs);
-  if (ok) ok = act_sync(a.bar, round, &s_ok);
+  if (ok) ok = act_sync(a.bar, round, &s_ok, a.spin_limit);
   ACT_TS(a, 4);
   // ---- stage 5: latent_mapper.0 on cat(features, h') (VAE.py:73) ----
   if (ok) {
@@ -341,7 +342,7 @@ __global__ __launch_bounds__(ACT_NT) void k_act_step(ActArgs ga) {
     __syncthreads();
     act_dense<25>(d.enc_hidden, F + Hd, a.wm.map0.w, F + Hd, a.wm.map0.b, xs, a.pre1, gw, nw);
   }
-  if (ok) ok = act_sync(a.bar, round, &s_ok);
+  if (ok) ok = act_sync(a.bar, round, &s_ok, a.spin_limit);
   ACT_TS(a, 5);
   // ---- stage 6: LN-SiLU, latent_mapper.3 and the categorical sampler: one wave per latent group ----
   if (ok && gw < R) {
@@ -403,7 +404,7 @@ __global__ __launch_bounds__(ACT_NT) void k_act_step(ActArgs ga) {
     }
     if (act) a.z_out[grp * C + lane] = (lane == bi) ? ((1.0f + pu) - pu) : 0.0f;
   }
-  if (ok) ok = act_sync(a.bar, round, &s_ok);
+  if (ok) ok = act_sync(a.bar, round, &s_ok, a.spin_limit);
   ACT_TS(a, 6);
   // ---- stage 7: actor base_net.0 on cat(h', z') (Agent.py:191-200) ----
   if (ok) {
@@ -411,16 +412,26 @@ __global__ __launch_bounds__(ACT_NT) void k_act_step(ActArgs ga) {
     __syncthreads();
     act_dense<26>(d.actor_h1, Hd + L, a.ac.l0.w, Hd + L, a.ac.l0.b, xs, a.prea, gw, nw);
   }
-  if (ok) ok = act_sync(a.bar, round, &s_ok);
+  if (ok) ok = act_sync(a.bar, round, &s_ok, a.spin_limit);
   ACT_TS(a, 7);
   // A barrier that timed out (a workgroup never arrived: the grid was not
   // co-resident) is reported, never silent: every workgroup that saw it raises
   // the status word the host checks after the step, and workgroup 0 writes NaN
   // to every output (action, mu, sigma, z', h') so nothing downstream can
   // mistake them for a state.
+  // Workgroup 0 also re-reads the shared fail flag after the last barrier: a
+  // workgroup that timed out there raised it after arriving (its stage data is
+  // complete), but the outputs are poisoned all the same.  `status` stays the
+  // authoritative signal (a flag raised after this read is seen only there).
+  if (blockIdx.x == 0) {  // (uniform over the workgroup: every wave takes both barriers)
+    __shared__ int s_fail;
+    if (threadIdx.x == 0) s_fail = __hip_atomic_load(a.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_fail) ok = false;
+  }
   if (!ok) {
     if (threadIdx.x == 0) {
-      *a.fail = 1;
+      __hip_atomic_store(a.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.status) __hip_atomic_store(a.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (blockIdx.x == 0) {
@@ -521,11 +532,17 @@ extern "C" int dr_act_step(const dr_dims* d, const dr_world_model* wm, const dr_
   const int F = 4 * d->enc_f2 * (d->img_h / 16) * (d->img_w / 16), L = d->rows * d->cols;
   // the stage helpers' register batches (KJ) and the LDS staging are sized for the
   // CarRacing encoder (Dreamer.py:20-64 config); other shapes use the unfused calls
-  DR_REQUIRE((d->enc_depth == 0 || d->enc_depth == 4) && d->img_h == 64 && d->img_w == 64 && d->enc_f1 == 32 && d->enc_f2 == 64 && F + d->hidden <= 64 * 74 &&
-                 L + d->action <= 64 * 17 && d->hidden <= 64 * 10 && d->hidden + L <= 64 * 26 && d->cols <= 64 &&
-                 d->rows <= ACT_NB * (ACT_NT / 64) && d->enc_hidden <= 256 && d->actor_h1 <= 256 &&
-                 d->actor_h2 <= 1024 && d->action <= 64,
-             "dims outside the batch-1 acting kernel (64x64 frames, encoder 32/64 filters, widths <= the staging)");
+  if (!((d->enc_depth == 0 || d->enc_depth == 4) && d->img_h == 64 && d->img_w == 64 && d->enc_f1 == 32 &&
+        d->enc_f2 == 64 && F + d->hidden <= 64 * 74 && L + d->action <= 64 * 17 && d->hidden <= 64 * 10 &&
+        d->hidden + L <= 64 * 26 && d->cols <= 64 && d->rows <= ACT_NB * (ACT_NT / 64) && d->enc_hidden <= 256 &&
+        d->actor_h1 <= 256 && d->actor_h2 <= 1024 && d->action <= 64)) {
+    dr_set_error("dr_act_step: dims outside the batch-1 acting kernel (64x64 frames, encoder 32/64 filters, widths "
+                 "<= the staging)");
+    return DR_E_UNSUPPORTED;
+  }
+  const char* force = getenv("DREAMER_ACT_FORCE");  // test hook (include/dreamer_hip.h)
+  const bool force_timeout = force && strcmp(force, "timeout") == 0;
+  const bool force_nonres = force && strcmp(force, "nonresident") == 0;
   ActArgs a;
   memset(&a, 0, sizeof(a));
   a.d = *d;
@@ -570,7 +587,11 @@ extern "C" int dr_act_step(const dr_dims* d, const dr_world_model* wm, const dr_
     DR_TRY_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     resident_ok[dev] = (long long)(per_cu - 1 > 0 ? per_cu - 1 : per_cu) * cus >= ACT_NB ? 1 : -1;
   }
-  DR_REQUIRE(resident_ok[dev] == 1, "dr_act_step: the device cannot hold the acting grid co-resident");
+  if (resident_ok[dev] != 1 || force_nonres) {
+    dr_set_error("dr_act_step: the device cannot hold the acting grid co-resident");
+    return DR_E_UNSUPPORTED;
+  }
+  a.spin_limit = force_timeout ? 0 : ACT_SPIN_LIMIT;
   hipLaunchKernelGGL(k_act_step, dim3(ACT_NB), dim3(ACT_NT), ACT_LDS * 4, s, a);
   return dr_check_launch("act_step");
 }

@@ -254,8 +254,12 @@ __device__ __forceinline__ dr_u4 philox4x32(dr_u4 c, uint32_t k0, uint32_t k1) {
   }
   return c;
 }
-// uniform in (0, 1]
-__device__ __forceinline__ float dr_u01(uint32_t x) { return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f); }
+// uniform on the 2^23-point grid (k + 1/2) 2^-23 in [2^-24, 1 - 2^-24]: never 0
+// and never 1, so an Exp(1) variate -log(u) is > 0 (p_hat / q stays finite; a
+// u of exactly 1 once gave q = 0 with probability 2^-24 per draw) and
+// Box-Muller's log(u1) is finite (torch's exponential_ avoids a zero variate
+// likewise)
+__device__ __forceinline__ float dr_u01(uint32_t x) { return ((float)(x >> 9) + 0.5f) * (1.0f / 8388608.0f); }
 
 __device__ __forceinline__ dr_u4 dr_rand4(const unsigned long long* so, uint32_t stream, uint32_t row,
                                           uint32_t elem) {

@@ -159,6 +159,9 @@ int op_chan_sum(long long rows, int C, const float* X, int ldx, float* out, int 
 // bf16 MFMA: both operands split3 once into planes, then a pre-split GEMM
 // (conv_split.hip).  Y (+)= dW with row stride ldy.
 size_t op_gemm_tn_split3_ws_bytes(int M, int N, int K);
+// shape / size limits of op_gemm_tn_split3 (32-bit plane offsets): callers
+// route problems it rejects to the f32 tile GEMM instead
+bool op_gemm_tn_split3_supported(int M, int N, int K);
 int op_gemm_tn_split3(int M, int N, int K, const float* G, long long ldg, const float* X, long long ldx,
                       const float* X2, long long ldx2, int nsplitB, float* Y, long long ldy, int accumulate, void* ws,
                       size_t ws_bytes, hipStream_t s);

@@ -1738,11 +1738,21 @@ size_t op_gemm_tn_split3_ws_bytes(int M, int N, int K) {
   return planes + 256 + (size_t)DR_PP_SPLITS * M * N * sizeof(float);
 }
 
+bool op_gemm_tn_split3_supported(int M, int N, int K) {
+  // the planes [K/32][3][P][32] are addressed with 32-bit element offsets,
+  // the split-K partials with 32-bit row offsets
+  return M > 0 && N > 0 && K > 0 && (long long)s3_pad(std::max(M, N)) * (((long long)K + 31) & ~31LL) * 3 < (1LL << 31) &&
+         (long long)DR_PP_SPLITS * M * N < (1LL << 31);
+}
+
+// host-side probe of the predicate (tests/test_host.py; not part of include/dreamer_hip.h)
+extern "C" int dr_internal_tn_split3_supported(int M, int N, int K) { return op_gemm_tn_split3_supported(M, N, K); }
+
 int op_gemm_tn_split3(int M, int N, int K, const float* G, long long ldg, const float* X, long long ldx,
                       const float* X2, long long ldx2, int nsplitB, float* Y, long long ldy, int accumulate, void* ws,
                       size_t ws_bytes, hipStream_t s) {
-  if (M <= 0 || N <= 0 || K <= 0 || !G || !X || !Y || (nsplitB < N && !X2) ||
-      ws_bytes < op_gemm_tn_split3_ws_bytes(M, N, K) || (long long)s3_pad(std::max(M, N)) * K * 3 >= (1LL << 31)) {
+  if (!op_gemm_tn_split3_supported(M, N, K) || !G || !X || !Y || (nsplitB < N && !X2) ||
+      ws_bytes < op_gemm_tn_split3_ws_bytes(M, N, K)) {
     dr_set_error("gemm_tn_split3: unsupported problem (M=%d N=%d K=%d) or workspace too small", M, N, K);
     return DR_E_INVALID;
   }

@@ -80,12 +80,17 @@ static int encoder_bf16(const dr_dims* d, const dr_world_model* wm, const dr_fra
   DR_TRY(op_to_bf16_2d(d->enc_hidden, F, wm->map0.w, F + d->hidden, w.wproj, s));
   // conv1 + conv2: k_enc12_split3 with one term (64 x 64 from the u8 ring), else
   // k_enc12_bf16, else two launches
-  if (op_enc12_s1_bf16(n, B, h0, w0, e[1], e[2], src, wm->conv[0].w, wm->conv[0].b, wm->conv[1].w, wm->conv[1].b,
-                       w.wr[0], w.wr[1], w.a[1], s) != DR_OK) {
+  // (DR_E_INVALID = shape / source not covered: next form; any other failure is returned)
+  const int rc_s1 = op_enc12_s1_bf16(n, B, h0, w0, e[1], e[2], src, wm->conv[0].w, wm->conv[0].b, wm->conv[1].w,
+                                     wm->conv[1].b, w.wr[0], w.wr[1], w.a[1], s);
+  if (rc_s1 != DR_OK) {
+    if (rc_s1 != DR_E_INVALID) return rc_s1;
     DR_TRY(op_conv_repack_bf16(e[1], 3, 4, wm->conv[0].w, w.wr[0], s));
     DR_TRY(op_conv_repack_bf16(e[2], e[1], e[1], wm->conv[1].w, w.wr[1], s));
-    if (op_enc12_bf16(n, B, h0, w0, e[1], e[2], src, w.wr[0], wm->conv[0].b, w.wr[1], wm->conv[1].b, w.a[1], s) !=
-        DR_OK) {
+    const int rc_b = op_enc12_bf16(n, B, h0, w0, e[1], e[2], src, w.wr[0], wm->conv[0].b, w.wr[1], wm->conv[1].b,
+                                   w.a[1], s);
+    if (rc_b != DR_OK) {
+      if (rc_b != DR_E_INVALID) return rc_b;
       DR_TRY(op_conv1_bf16(n, B, h0, w0, e[1], src, w.wr[0], wm->conv[0].b, w.a[0], s));
       DR_TRY(op_conv_bf16(n, e[1], h0 / 2, w0 / 2, e[2], w.a[0], w.wr[1], wm->conv[1].b, w.a[1], 0, s));
     }

@@ -177,7 +177,7 @@ static inline GemmArgs bwd_w(int out, int in, int R, const float* G, long long l
 // when `ws` holds every problem's planes, else one grouped f32 tile launch
 static inline bool tn_split3_ok(const GemmArgs& g) {
   return g.alpha == 1.0f && !g.act && !g.bias && !g.addend && g.ksplitB >= g.K && g.nsplitY >= g.N && !g.out_conv &&
-         g.ksplitA >= g.K && g.epi == EPI_NONE && g.M > 0 && g.N > 0 && g.K > 0;
+         g.ksplitA >= g.K && g.epi == EPI_NONE && op_gemm_tn_split3_supported(g.M, g.N, g.K);
 }
 static inline int tn_launch(const GemmArgs* p, int n, void* ws, size_t ws_bytes, hipStream_t s) {
   bool ok = ws != nullptr;

@@ -662,10 +662,15 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   // conv1 + conv2 in one kernel from the u8 ring (k_enc12_split3) with the
   // backward's saves; other shapes / sources take the per-layer kernels
   int k0 = 0;
-  if (N >= 2 && w.e12w1 && w.s3e[1] &&
-      op_enc12_split3_ex(M, B, IH, IW, D.e[1], D.e[2], src, wm->conv[0].w, wm->conv[0].b, wm->conv[1].w,
-                         wm->conv[1].b, w.e12w1, w.s3e[1], w.a[1], w.pre[0], w.a[0], w.pre[1], s) == DR_OK)
-    k0 = 2;
+  if (N >= 2 && w.e12w1 && w.s3e[1]) {
+    // DR_E_INVALID: shape / source not covered (per-layer kernels below); any
+    // other failure (a launch or occupancy query) is returned
+    const int rc12 = op_enc12_split3_ex(M, B, IH, IW, D.e[1], D.e[2], src, wm->conv[0].w, wm->conv[0].b,
+                                        wm->conv[1].w, wm->conv[1].b, w.e12w1, w.s3e[1], w.a[1], w.pre[0], w.a[0],
+                                        w.pre[1], s);
+    if (rc12 == DR_OK) k0 = 2;
+    else if (rc12 != DR_E_INVALID) return rc12;
+  }
   for (int k = k0; k < N; ++k) {
     if (w.s3e[k])
       DR_TRY(op_conv_split3_ex(M, D.e[k], IH >> k, IW >> k, D.e[k + 1], w.a[k - 1], w.s3e[k], wm->conv[k].b, w.a[k],

@@ -332,8 +332,8 @@ class Dreamer(nn.Module):
                    int(has_prev), L.ptr(zp), L.ptr(hp), L.ptr(ap), hip.adhoc(dev).noise(), int(deterministic),
                    L.ptr(z2), L.ptr(h2), L.ptr(a2), L.ptr(mu), L.ptr(sg), None, L.ptr(st["status"]),
                    L.ptr(st["ws"]), st["ws"].numel(), hip.stream())
-        except RuntimeError as e:
-            if "co-resident" not in str(e) and "outside the batch-1 acting kernel" not in str(e):
+        except L.HipError as e:
+            if e.code != L.DR_E_UNSUPPORTED:
                 raise
             # the device cannot hold the one-launch grid, or the widths are not the ones the
             # kernel's register batches are sized for (e.g. the 5-layer VAE): the unfused launches

@@ -38,6 +38,8 @@ extern "C" {
 #define DR_E_INVALID 1001   /* bad dims / pointers */
 #define DR_E_HIP 1002       /* a HIP launch failed */
 #define DR_E_WORKSPACE 1003 /* workspace too small */
+#define DR_E_UNSUPPORTED 1004 /* valid call outside what this entry point covers (dims / device):
+                                 use the unfused entry points (dr_act_step) */
 
 /* Linear (or LayerNorm) parameters: w [out][in] (LN: gamma [n]), b [out]. */
 typedef struct { float* w; float* b; } dr_linear;
@@ -204,10 +206,14 @@ int dr_actor_act(const dr_dims* d, const dr_actor* actor, int B, const float* h,
  * eps [A] when given).  logits_out may be NULL.  Inputs and outputs may alias
  * (h / h_out, z_prev / z_out, a_prev / a_out).
  * Co-residency of the grid is checked once per device (occupancy query); the
- * call returns DR_E_INVALID when the device cannot hold it (callers then use
- * the unfused entry points).  status (device int, may be NULL; the caller
- * zeroes it): set to 1 if a grid barrier timed out at run time, in which case
- * every output holds NaN -- callers must check it before using the outputs. */
+ * call returns DR_E_UNSUPPORTED when the device cannot hold it, or for dims
+ * outside the kernel's staging (callers then use the unfused entry points).
+ * status (device int, may be NULL; the caller zeroes it): set to 1 if a grid
+ * barrier timed out at run time; it is the authoritative signal -- the outputs
+ * then hold NaN whenever workgroup 0 saw the failure, and must not be used.
+ * Test hook: the environment variable DREAMER_ACT_FORCE=timeout (every grid
+ * barrier times out at once) or =nonresident (the co-residency check fails),
+ * read at each call. */
 size_t dr_act_step_workspace_bytes(const dr_dims* d);
 int dr_act_step(const dr_dims* d, const dr_world_model* wm, const dr_actor* actor, const unsigned char* frame,
                 int has_prev, const float* z_prev, const float* h, const float* a_prev, dr_noise noise,

@@ -407,3 +407,47 @@ def test_act_step_matches_unfused(gpu):
     marks = [0, 1, 2, 3, 4, 5, 6, 7, 15]
     print("dr_act_step stage ends (us after kernel start):",
           [round(float(ts[m] - ts[0]) / 100.0, 2) for m in marks[1:]])
+
+
+def test_act_step_failure_paths(gpu, monkeypatch):
+    """dr_act_step's failure paths, forced through its test hook
+    (include/dreamer_hip.h: DREAMER_ACT_FORCE).  =timeout: every grid barrier
+    gives up at once -> the status word is raised, act_check() raises, the
+    outputs are NaN, and the next step runs normally.  =nonresident: the
+    co-residency check fails -> DR_E_UNSUPPORTED -> Dreamer.act_step runs the
+    unfused launches, which match the CPU oracle (O.encode at an episode start,
+    O.actor_act; tie-guarded explicit noise, indices exact)."""
+    from dreamer_amd import hip
+    d, P = _dreamer(gpu)
+    g = torch.Generator().manual_seed(44)
+    frame = torch.randint(0, 256, (64, 64, 3), generator=g, dtype=torch.uint8).numpy()
+    with torch.no_grad():
+        monkeypatch.setenv("DREAMER_ACT_FORCE", "timeout")
+        a, mu, sg, z, h = d.act_step(frame)
+        with pytest.raises(RuntimeError, match="grid barrier timed out"):
+            d.act_check()
+        for t, name in ((a, "a"), (mu, "mu"), (sg, "sigma"), (z, "z"), (h, "h")):
+            assert bool(torch.isnan(t).all()), f"{name} must be NaN after a barrier timeout"
+        monkeypatch.delenv("DREAMER_ACT_FORCE")
+        a, mu, sg, z, h = d.act_step(frame)
+        d.act_check()
+        assert all(bool(torch.isfinite(t).all()) for t in (a, mu, sg, z, h))
+        assert int(d._act_bufs["status"].item()) == 0
+        assert not getattr(d, "_act_unfused", False)
+        # co-residency check failing: the unfused path, against the oracle
+        monkeypatch.setenv("DREAMER_ACT_FORCE", "nonresident")
+        obs = torch.tensor(frame.transpose(2, 0, 1), dtype=torch.float32).view(1, 1, 3, 64, 64) / 255.0 - 0.5
+        q = torch.empty(1, R, C).exponential_(generator=g)
+        eps = torch.randn(1, 1, A, generator=g)
+        with TieGuard():
+            h_o = torch.zeros(1, 1, HD)
+            z_o, _ = O.encode(h_o, obs, P, q[0], R, C)
+        a_o, mu_o, sg_o = O.actor_act(h_o, z_o, P, eps.view(1, 1, A))
+        with hip.noise_override(q=q.to(gpu), eps=eps.to(gpu)):
+            a_f, mu_f, sg_f, z_f, h_f = d.act_step(frame)
+        assert getattr(d, "_act_unfused", False), "DR_E_UNSUPPORTED must switch Dreamer to the unfused path"
+        assert torch.equal(_idx(z_f), z_o.reshape(-1, C).argmax(-1))
+        close(h_f, h_o, 0, 0, "h' at an episode start")
+        close(mu_f, mu_o, 1e-4, 1e-6, "mu (unfused fallback)")
+        close(sg_f, sg_o, 1e-4, 1e-6, "sigma (unfused fallback)")
+        close(a_f, a_o, 1e-4, 1e-6, "action (unfused fallback)")

@@ -231,3 +231,19 @@ def test_deep_vae_state_layout():
     assert tuple(O.encoder_logits(h, obs, P).shape) == (1, 2, 1024)
     z = torch.nn.functional.one_hot(torch.randint(0, 32, (1, 2, 32), generator=g), 32).float()
     assert tuple(O.decoder_forward(h, z, P, (128, 128)).shape) == (1, 2, 3, 128, 128)
+
+
+def test_tn_split3_predicate_covers_its_limits():
+    """tn_launch routes a TN weight-gradient problem to the split3 kernel only
+    when op_gemm_tn_split3 accepts it: the 4736-wide encoder
+    projection gradient at K = B*T rows beyond ~151k exceeds the 32-bit plane
+    offsets and must fall back to the f32 tile GEMM instead of failing."""
+    import ctypes
+    from dreamer_amd import _lib
+    f = _lib.load().dr_internal_tn_split3_supported
+    f.restype, f.argtypes = ctypes.c_int, [ctypes.c_int] * 3
+    assert f(200, 4736, 3840) == 1        # the WM step's projection gradient at B = 256, T = 15
+    assert f(200, 4736, 16384) == 1
+    assert f(200, 4736, 160000) == 0      # > 2^31 plane elements
+    assert f(200, 1624, 61440) == 1       # the critic's first layer at B = 4096, H + 1 = 16 (configs[4])
+    assert f(0, 10, 10) == 0 and f(10, 10, 0) == 0

@@ -1,0 +1,21 @@
+#!/bin/bash
+# round-4 iteration check: B = 256 parity + determinism + natural-noise flips,
+# headline bench, kernel-trace epoch table.  Stops at the first failure.
+cd "$(dirname "$0")/.." || exit 1
+export PYTHONUNBUFFERED=1
+TAG=${1:-r04b}
+TESTS=${TESTS:-"tests/test_gpu_baseline.py tests/test_gpu_determinism.py tests/test_gpu_flips.py tests/test_gpu_parity.py"}
+R=$(pwd)
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest $TESTS -m gpu -v -s --timeout 300 --timeout-method thread -p no:cacheprovider \
+  > gpurun_out/tests_$TAG.log 2>&1 || { grep -E "FAILED|Error|assert" gpurun_out/tests_$TAG.log | head -30; tail -30 gpurun_out/tests_$TAG.log; exit 1; }
+grep -E "PASSED|FAILED|passed|failed|flip|guarded|NATURAL" gpurun_out/tests_$TAG.log | cut -c1-400 | head -60
+timeout -k 10 300 python bench.py --no-secondary --wm-steps 0 --no-cpu-baseline > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -30 gpurun_out/bench_$TAG.err; exit 1; }
+cut -c1-200 gpurun_out/bench_$TAG.json
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o p -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-secondary --wm-steps 0 > $R/gpurun_out/prof_$TAG.log 2>&1 || { tail -20 $R/gpurun_out/prof_$TAG.log; exit 1; }
+cd $R
+python tools/epoch_table.py gpurun_out/prof_$TAG/p_results.db 7 13 40 > gpurun_out/epoch_table_$TAG.txt && head -30 gpurun_out/epoch_table_$TAG.txt
+python tools/prof_summary.py gpurun_out/prof_$TAG/p_results.db 40 > gpurun_out/kernel_stats_$TAG.txt
+rm -rf gpurun_out/prof_$TAG
+echo "gpu_$TAG done"
