@@ -3,6 +3,14 @@
 // Each is a fixed sequence of kernel launches on one stream (no host sync,
 // no allocation) so a whole train_Agent epoch can be captured in a hipGraph.
 #include "engine_util.h"
+#include "chain.h"
+
+#ifndef DR_GRU_BWD_EPI
+#define DR_GRU_BWD_EPI 1  // A/B knob: 0 = the GRU backward as its own elementwise launch
+#endif
+#ifndef DR_ACTOR_TAIL
+#define DR_ACTOR_TAIL 1  // A/B knob (tools/build_variant.py): 0 = z-gather + two skinny launches
+#endif
 
 // fp32 mode, tall batches: the first Linear of a head over [h | z] on the
 // split3 bf16 MFMA (conv_split.hip) when the workspace holds its weight planes
@@ -437,13 +445,43 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
   }
   DR_TRY(op_onehot_index(B, d->rows, d->cols, latents, ldL, w.idx[0], onehot_vals(w.idx[0], B, d->rows), s));
 
+  // the actor of step `st` after its latents are sampled (Agent.py:191-210): ONE
+  // launch from the h-part (+ bias) of base_net.0 in w.hpart and the sampled
+  // indices (chain.hip k_actor_tail)
+  auto actor_tail = [&](int st, int* ix, const float* z_rows) -> ActorTailArgs {
+    const long long o1 = (long long)st * a1, o2 = (long long)st * a2, o = (long long)st * A;
+    ActorTailArgs at;
+    memset(&at, 0, sizeof(at));
+    at.M = B; at.A = A; at.a1 = a1; at.a2 = a2; at.R = d->rows; at.C = d->cols;
+    at.step = st; at.det = deterministic;
+    at.idx = ix; at.zval = onehot_vals(ix, B, d->rows); at.z = z_rows; at.ldz = ldL;
+    at.wzt = w.tl0f + (long long)Hd * a1; at.ldw = a1;
+    at.hpart = w.hpart; at.ldh = a1;
+    at.n1g = ac->n1.w; at.n1b = ac->n1.b; at.w3 = ac->l3.w; at.b3 = ac->l3.b; at.n4g = ac->n4.w; at.n4b = ac->n4.b;
+    at.wmu = ac->mu.w; at.bmu = ac->mu.b; at.wls = ac->ls.w; at.bls = ac->ls.b;
+    at.pre1 = tp.pre1a + o1; at.x1 = tp.x1a + o1; at.ld1 = lda1;
+    at.pre2 = tp.pre2a + o2; at.x2 = tp.x2a + o2; at.ld2 = lda2;
+    at.noise = noise;
+    at.act = actions + o; at.mu = mus + o; at.sig = sigmas + o; at.ldA = ldA;
+    at.eps_save = tp.eps + (long long)st * B * A; at.ls_save = tp.ls_raw + o;
+    return at;
+  };
+  const bool fused_actor = zg && DR_ACTOR_TAIL && op_actor_tail_ok(actor_tail(0, w.idx[0], latents));
+
   // actor at step 0 (Agent.py:191-210)
-  DR_TRY(run(G_NT, AM_PLAIN, lin2(B, a1, hiddens, ldH, Hd, latents, ldL, L, ac->l0.w, ac->l0.b, tp.pre1a, lda1), s));
-  {
+  if (fused_actor) {
+    DR_TRY(run(G_NT, AM_PLAIN, lin(B, a1, Hd, hiddens, ldH, ac->l0.w, Hd + L, ac->l0.b, w.hpart, a1), s));
+    DR_TRY(op_actor_tail(actor_tail(0, w.idx[0], latents), s));
+  } else {
+    DR_TRY(run(G_NT, AM_PLAIN, lin2(B, a1, hiddens, ldH, Hd, latents, ldL, L, ac->l0.w, ac->l0.b, tp.pre1a, lda1), s));
     GemmArgs g = lin_ln(B, a2, a1, tp.pre1a, lda1, ac->n1, ac->l3.w, ac->l3.b, tp.pre2a, lda2);
     g.a_out = tp.x1a; g.ld_aout = lda1;
     DR_TRY(run(G_NT, AM_LNSILU, g, s));
+  }
+  if (!fused_actor || !zg) {
     DR_TRY(stack_heads(ac, A, a2, w.wst, w.bst, s));
+  }
+  if (!fused_actor) {
     GemmArgs h = lin_ln(B, 2 * A, a2, tp.pre2a, lda2, ac->n4, w.wst, w.bst, nullptr, 0);
     h.a_out = tp.x2a; h.ld_aout = lda2;
     with_actor_head(h, A, noise, 0, deterministic, actions, ldA, mus, ldA, sigmas, ldA, tp.eps, tp.ls_raw, ldA);
@@ -478,6 +516,11 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
     // the actor for step t+1 (the reward / continue heads run once after the unroll)
     if (t + 1 < H) {
       const long long o1 = (long long)(t + 1) * a1, o2 = (long long)(t + 1) * a2, o = (long long)(t + 1) * A;
+      if (fused_actor) {
+        // z-gather + LN-SiLU + base_net.3 + LN-SiLU + heads + rsample in one launch (chain.hip)
+        DR_TRY(op_actor_tail(actor_tail(t + 1, w.idx[(t + 1) & 1], z_n), s));
+        continue;
+      }
       if (zg) {
         int* ix = w.idx[(t + 1) & 1];
         DR_TRY(op_zgather_add(B, a1, d->rows, d->cols, ix, onehot_vals(ix, B, d->rows), z_n, ldL,
@@ -652,7 +695,8 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
       // z_{t+1} = STE(prior(h_{t+1}))   (DynamicsPredictors.py:31-40)
       const int h1 = d->prior_h1, h2 = d->prior_h2;
       const int gl = d->cols / 4;
-      if (B <= 64 && L <= 1024 && d->cols % 4 == 0 && gl <= 64 && (gl & (gl - 1)) == 0) {
+      GemmArgs gs = bwd_nt(B, h2, L, gZ_n, ldL, w.tl6p, w.gx2, h2, 0);
+      if (L <= 1024 && d->cols % 4 == 0 && gl <= 64 && (gl & (gl - 1)) == 0 && gemm_bwd_rows16(&gs, 1)) {
         // straight-through softmax backward fused into the prior head's
         // input-gradient GEMM (its A-operand prologue)
         GemmArgs g = bwd_nt(B, h2, L, gZ_n, ldL, w.tl6p, w.gx2, h2, 0);
@@ -667,11 +711,18 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
       // dynamic_predictor.4/.3 and .1/.0: LN-SiLU backward fused into the next input-gradient GEMM
       DR_TRY(lnbwd_nt(B, h1, h2, w.gx2, h2, tp.pre2p + (long long)t * B * h2, h2, wm->prior.n4, w.tl3p, w.gx1, h1, 0,
                       w.gp2, h2, nullptr, nullptr, nullptr, 0, INT_MAX, s));
+      // ... whose epilogue (the last addend of dL/dh_{t+1}) also runs the GRU
+      // backward of h_{t+1} = GRU(z_t, a_t, h_t) (SequenceModel.py:19-24)
+      GruBwdEpi ge;
+      memset(&ge, 0, sizeof(ge));
+      ge.h = hiddens + (long long)t * Hd; ge.ldh = ldH;
+      ge.r = tp.r + hb; ge.u = tp.u + hb; ge.n = tp.n + hb; ge.ghn = tp.ghn + hb;
+      ge.gi = w.ggi; ge.gh = w.ggh; ge.ho = gH_t; ge.ldo = ldH; ge.Hd = Hd;
       DR_TRY(lnbwd_nt(B, Hd, h1, w.gx1, h1, tp.pre1p + (long long)t * B * h1, h1, wm->prior.n1, w.tl0p, gH_n, ldH, 1,
-                      w.gp1, h1, nullptr, nullptr, nullptr, 0, INT_MAX, s));
-      // h_{t+1} = GRU(z_t, a_t, h_t)   (SequenceModel.py:19-24)
-      DR_TRY(op_gru_bwd(B, Hd, gH_n, ldH, hiddens + (long long)t * Hd, ldH, tp.r + hb, tp.u + hb, tp.n + hb,
-                        tp.ghn + hb, w.ggi, w.ggh, gH_t, ldH, 1, s));
+                      w.gp1, h1, nullptr, nullptr, nullptr, 0, INT_MAX, s, DR_GRU_BWD_EPI ? &ge : nullptr));
+      if (!DR_GRU_BWD_EPI)
+        DR_TRY(op_gru_bwd(B, Hd, gH_n, ldH, hiddens + (long long)t * Hd, ldH, tp.r + hb, tp.u + hb, tp.n + hb,
+                          tp.ghn + hb, w.ggi, w.ggh, gH_t, ldH, 1, s));
       if (t > 0) {
         GemmArgs p[2];
         p[0] = bwd_nt(B, L + A, 3 * Hd, w.ggi, 3 * Hd, w.wt, gZ_t, ldL, 1);

@@ -139,17 +139,20 @@ static inline long long splitk_floats(long long M, long long N) { return DR_SPLI
 // k_ln_silu_bwd + NT GEMM where the fused path does not apply.
 static inline int lnbwd_nt(int M, int N, int K, const float* gx, long long ldgx, const float* pre, long long ld_pre,
                     const dr_linear& ln, const float* WT, float* Y, long long ldy, int accumulate, float* gpre,
-                    long long ld_gpre, float* gy, float* xh, float* Y2, long long ldy2, int nsplitY, hipStream_t s) {
+                    long long ld_gpre, float* gy, float* xh, float* Y2, long long ldy2, int nsplitY, hipStream_t s,
+                    const GruBwdEpi* gru_epi = nullptr) {
   GemmArgs g = bwd_nt(M, N, K, gx, ldgx, WT, Y, ldy, accumulate);
   g.Y2 = Y2; g.ldy2 = ldy2; g.nsplitY = nsplitY;
-  const bool ok = K % 4 == 0 && K <= (M <= 64 ? 1024 : 256) && M <= 4096 && ldgx % 4 == 0 && ld_pre % 4 == 0 &&
+  if (gru_epi) g.gb = *gru_epi;
+  const bool r16 = gemm_bwd_rows16(&g, 1);
+  const bool ok = K % 4 == 0 && K <= (r16 ? 1024 : 256) && M <= 4096 && ldgx % 4 == 0 && ld_pre % 4 == 0 &&
                   ((((uintptr_t)gx | (uintptr_t)pre | (uintptr_t)WT | (uintptr_t)ln.w | (uintptr_t)ln.b) & 15) == 0);
-  // at 128+ rows the staged prologue (recomputed by every column tile, 64-row
-  // tiles) costs more than one elementwise pass + a plain GEMM: B = 256,
-  // N = 1624: 26.5 us fused vs the two launches below
-  // (also for the 200-wide layers: 16.5 us fused against 5.0 + 6.3 split at
-  // B = 256, profiles/r03x_epoch_kernel_table.txt)
-  const bool split = gpre != nullptr && M >= 128;
+  // on 64-row tiles (tall problems) the staged prologue, recomputed by every
+  // column tile, costs more than one elementwise pass + a plain GEMM (B = 256,
+  // N = 1624: 26.5 us fused vs the two launches; the 200-wide layers 16.5 us
+  // against 5.0 + 6.3, profiles/r03x_epoch_kernel_table.txt); on 16-row tiles
+  // (per-step products up to ~2.5 dispatch rounds) the prologue is fused
+  const bool split = gpre != nullptr && M >= 128 && !r16;
   if (ok && !split) {
     g.pre = pre; g.ld_pre = ld_pre; g.ln_g = ln.w; g.ln_b = ln.b;
     g.a_out = gpre; g.ld_aout = ld_gpre;

@@ -17,6 +17,19 @@ enum { AM_PLAIN = 0, AM_LNSILU = 1, AM_CONV = 2, AM_CONV_SRC = 3, AM_LNBWD = 4, 
 // (ln_g/ln_b) come from the fields below.  a_out receives g_pre, sv_gy /
 // sv_xh the SiLU-input gradient and x_hat (for the LayerNorm parameter grads).
 
+// Fused GRU backward (SequenceModel.py:19-24 -> torch gru_cell) on the FINAL
+// value of an accumulated hidden-state gradient g = dL/dh' (the last GEMM that
+// adds into it, engine.hip's BPTT): for output (m, j < Hd) the epilogue writes
+// gi[m][{r,u,n}] / gh[m][{r,u,n}] and adds dL/dh through h' = (h - n) u + n to
+// ho[m][j] -- ops.hip k_gru_bwd's arithmetic, one launch fewer per BPTT step.
+struct GruBwdEpi {
+  const float* h; long long ldh;        // h (NULL = zeros)
+  const float *r, *u, *n, *ghn;          // forward saves [M][Hd]
+  float *gi, *gh;                        // [M][3 Hd]
+  float* ho; long long ldo;              // dL/dh (+=)
+  int Hd, pad_;
+};
+
 struct alignas(16) GemmArgs {
   int M, N, K;
   // A
@@ -55,6 +68,7 @@ struct alignas(16) GemmArgs {
   // run on v_mfma_f32_16x16x32_bf16 with operands rounded to bf16 as they are
   // staged (f32 accumulation, f32 in / out); set by the engine per call
   int bf16;
+  GruBwdEpi gb;  // gb.Hd > 0: fused GRU backward on the stored values (see GruBwdEpi)
 };
 
 enum { EPI_NONE = 0, EPI_SAMPLE = 1, EPI_ACTOR = 2 };
@@ -71,6 +85,11 @@ struct GemmBf16Scope {
 };
 // Launch up to 4 problems sharing layout/A-mode in one dispatch.
 int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hipStream_t s);
+#ifndef DR_BWD_ROWS16
+#define DR_BWD_ROWS16 1  // A/B knob: the staged backward prologues on 16-row tiles past 64 rows
+#endif
+// true when AM_LNBWD / AM_STEBWD problems run on 16-row skinny tiles (K <= 1024)
+bool gemm_bwd_rows16(const GemmArgs* p, int count);
 
 // The tail of the reference's 3-layer heads (Linear, LN, SiLU, Linear, LN,
 // SiLU, Linear -- DynamicsPredictors.py:15-23, Agent.py:180-190) from the

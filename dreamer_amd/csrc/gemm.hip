@@ -379,6 +379,34 @@ __device__ __forceinline__ float epi_act(const GemmArgs& g, float v) {
   return v;
 }
 
+// GruBwdEpi: the gru_cell backward of one (row, unit) from the final dL/dh'
+__device__ __noinline__ void gru_bwd_elem(const GruBwdEpi& e, int m, int j, float g) {
+  const int Hd = e.Hd;
+  const long long i = (long long)m * Hd + j;
+  const float r = dr_g(e.r)[i], u = dr_g(e.u)[i], n = dr_g(e.n)[i], hn = dr_g(e.ghn)[i];
+  const float hv = e.h ? dr_g(e.h)[(long long)m * e.ldh + j] : 0.0f;
+  // h' = (h - n)*u + n
+  const float g_hmn = g * u;
+  const float g_u = g * (hv - n);
+  const float g_n = g + (-g_hmn);
+  // n = tanh(in + hn*r)
+  const float g_pn = g_n * (1.0f - n * n);
+  const float g_r = g_pn * hn;
+  const float g_hn = g_pn * r;
+  const float g_pr = g_r * (1.0f - r) * r;
+  const float g_pu = g_u * (1.0f - u) * u;
+  DR_GLOBAL float* gib = dr_g(e.gi) + (long long)m * 3 * Hd;
+  DR_GLOBAL float* ghb = dr_g(e.gh) + (long long)m * 3 * Hd;
+  gib[j] = g_pr;
+  gib[Hd + j] = g_pu;
+  gib[2 * Hd + j] = g_pn;
+  ghb[j] = g_pr;
+  ghb[Hd + j] = g_pu;
+  ghb[2 * Hd + j] = g_hn;
+  DR_GLOBAL float* o = dr_g(e.ho) + (long long)m * e.ldo + j;
+  *o = *o + g_hmn;
+}
+
 __device__ __forceinline__ void epilogue_store_b(const GemmArgs& g, int m, int n, float acc, float bias) {
   float v = (g.alpha == 1.0f) ? acc : g.alpha * acc;
   if (g.bias) v = v + bias;
@@ -387,8 +415,9 @@ __device__ __forceinline__ void epilogue_store_b(const GemmArgs& g, int m, int n
   DR_GLOBAL float* dst;
   if (n < g.nsplitY) dst = dr_g(g.Y) + (long long)m * g.ldy + n;
   else dst = dr_g(g.Y2) + (long long)m * g.ldy2 + (n - g.nsplitY);
-  if (g.accumulate) *dst = *dst + v;
-  else *dst = v;
+  const float fin = g.accumulate ? *dst + v : v;
+  *dst = fin;
+  if (g.gb.Hd > 0 && n < g.gb.Hd) gru_bwd_elem(g.gb, m, n, fin);
 }
 
 #ifndef DR_SKW
@@ -1873,6 +1902,18 @@ static void launch_skinny(const GemmBatch& gb, int count, bool vec, hipStream_t 
 
 
 
+// The staged backward prologues (AM_LNBWD, AM_STEBWD) run on 16-row tiles
+// (K <= 1024) when the problem has at most 64 rows or its 16 x 16 grid stays
+// within ~2.5 dispatch rounds (try_skinny), else on 64-row tiles (K <= 256).
+bool gemm_bwd_rows16(const GemmArgs* p, int count) {
+  int maxM = 0, t16 = 0;
+  for (int i = 0; i < count; ++i) {
+    maxM = std::max(maxM, p[i].M);
+    t16 += dr_cdiv(p[i].M, 16) * dr_cdiv(p[i].N, 16);
+  }
+  return maxM <= 64 || (DR_BWD_ROWS16 && g_skinny_variant == 0 && maxM <= 4096 && t16 <= 640);
+}
+
 template <int AMODE, bool B_KN>
 static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
   int maxM = 0, epi = EPI_NONE;
@@ -1894,7 +1935,10 @@ static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
   // 16-row tiles past 64 rows while the grid stays within ~2.5 dispatch
   // rounds: a B = 256 per-step product (N = 200) then spreads over 208
   // workgroups instead of 52 (K = 1624: 19.3 -> 8.4 us, profiles/r02_kbench_B256.txt)
-  if ((g_skinny_variant == 0 || g_skinny_variant == 5) && maxM > 64 && (AMODE == AM_PLAIN || AMODE == AM_LNSILU) &&
+  // (also the staged LayerNorm- and softmax-STE-backward prologues, DR_BWD_ROWS16:
+  // at 64-row tiles a B = 256 LN-backward product ran on 52 workgroups, 16.5 us)
+  if ((g_skinny_variant == 0 || g_skinny_variant == 5) && maxM > 64 &&
+      (AMODE == AM_PLAIN || AMODE == AM_LNSILU || (DR_BWD_ROWS16 && (AMODE == AM_LNBWD || AMODE == AM_STEBWD))) &&
       !(g_skinny_variant == 5 && epi == EPI_SAMPLE)) {
     int t16 = 0;
     for (int i = 0; i < count; ++i) t16 += dr_cdiv(gb.p[i].M, 16) * dr_cdiv(gb.p[i].N, epi == EPI_SAMPLE ? 32 : 16);
@@ -2619,9 +2663,10 @@ int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hip
         case AM_CONV: launch_pick<AM_CONV, false, false>(gb, count, s); break;
         case AM_CONV_SRC: launch_pick<AM_CONV_SRC, false, false>(gb, count, s); break;
         case AM_LNBWD: {
+          const bool r16 = gemm_bwd_rows16(probs, count);
           for (int i = 0; i < count; ++i) {
             const GemmArgs& g = probs[i];
-            const int lim = (g.M <= 64) ? 1024 : 256;  // staged rows per lane: SV = 4 (MT 16) / 1 (MT 64)
+            const int lim = r16 ? 1024 : 256;  // staged rows per lane: SV = 4 (MT 16) / 1 (MT 64)
             if (g.K % 4 || g.K > lim || g.lda % 4 || g.ld_pre % 4 || g.ldb % 4 ||
                 ((uintptr_t)g.A | (uintptr_t)g.pre | (uintptr_t)g.W | (uintptr_t)g.ln_g | (uintptr_t)g.ln_b) & 15) {
               dr_set_error("gemm_launch: AM_LNBWD needs K %% 4 == 0, K <= %d, 16-byte aligned rows (K=%d)", lim, g.K);
@@ -2632,15 +2677,16 @@ int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hip
           break;
         }
         case AM_STEBWD: {
+          const bool r16 = gemm_bwd_rows16(probs, count);
           for (int i = 0; i < count; ++i) {
             const GemmArgs& g = probs[i];
-            const int lim = (g.M <= 64) ? 1024 : 256;
+            const int lim = r16 ? 1024 : 256;
             const int gl = g.C / 4;
             if (g.K % 4 || g.K > lim || g.lda % 4 || g.ld_pre % 4 || g.ldb % 4 || g.C < 4 || g.C % 4 ||
-                (gl & (gl - 1)) || gl > 64 || g.K % g.C || g.M > 64 ||
+                (gl & (gl - 1)) || gl > 64 || g.K % g.C || !r16 ||
                 ((uintptr_t)g.A | (uintptr_t)g.pre | (uintptr_t)g.W) & 15) {
-              dr_set_error("gemm_launch: AM_STEBWD needs M <= 64, K %% C == 0, C/4 a power of two, K <= %d, "
-                           "16-byte aligned rows (K=%d C=%d)", lim, g.K, g.C);
+              dr_set_error("gemm_launch: AM_STEBWD needs 16-row tiles (gemm_bwd_rows16), K %% C == 0, C/4 a power "
+                           "of two, K <= %d, 16-byte aligned rows (K=%d C=%d)", lim, g.K, g.C);
               return DR_E_INVALID;
             }
           }

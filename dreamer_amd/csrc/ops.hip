@@ -762,6 +762,95 @@ __global__ __launch_bounds__(1024) void k_update_S_select(int n, const float* R,
   }
 }
 
+// The same exact radix select with the returns held in registers (n <= 1024
+// VPT): the bitonic sort of k_update_S ran 78 barrier-separated LDS stages
+// (48 us at n = 3840); here one load, then per 8-bit pass one LDS histogram
+// (atomics) and a wave-parallel prefix search per target rank.
+template <int VPT>
+__global__ __launch_bounds__(1024) void k_update_S_reg(int n, const float* R, float* S, float* norm_out) {
+  __shared__ unsigned hist[4][256];
+  __shared__ unsigned prefix[4], want[4];
+  __shared__ int bad;
+  const float r95 = 0.95f * (float)(n - 1), r05 = 0.05f * (float)(n - 1);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (tid == 0) {
+    bad = 0;
+    want[0] = (unsigned)(int)r95;
+    want[1] = (unsigned)(int)ceilf(r95);
+    want[2] = (unsigned)(int)r05;
+    want[3] = (unsigned)(int)ceilf(r05);
+  }
+  if (tid < 4) prefix[tid] = 0u;
+  unsigned key[VPT];
+  bool nonfinite = false;
+#pragma unroll
+  for (int v = 0; v < VPT; ++v) {
+    const int i = tid + 1024 * v;
+    const float x = R[i < n ? i : 0];
+    nonfinite = nonfinite || (i < n && !isfinite(x));
+    key[v] = f2key(x);
+  }
+  __syncthreads();
+  if (nonfinite) bad = 1;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    const unsigned hi_mask = pass == 0 ? 0u : (0xffffffffu << (shift + 8));
+    (&hist[0][0])[tid] = 0u;  // 1024 threads, 4 x 256 bins
+    __syncthreads();
+    unsigned pf[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) pf[t] = prefix[t];
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+      if (tid + 1024 * v < n) {
+        const unsigned k = key[v], bin = (k >> shift) & 255u;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if ((k & hi_mask) == pf[t]) atomicAdd(&hist[t][bin], 1u);
+      }
+    }
+    __syncthreads();
+    if (wave < 4) {  // wave t: the bin holding rank want[t]; lane l sums bins 4l .. 4l+3
+      const int t = wave;
+      const unsigned w = want[t];
+      const unsigned c0 = hist[t][4 * lane], c1 = hist[t][4 * lane + 1], c2 = hist[t][4 * lane + 2],
+                     c3 = hist[t][4 * lane + 3];
+      const unsigned sum = c0 + c1 + c2 + c3;
+      unsigned inc = sum;  // inclusive prefix over lanes
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned up = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += up;
+      }
+      const unsigned ex = inc - sum;
+      if (ex <= w && w < inc) {  // exactly one lane
+        unsigned below = ex, b = 4 * lane;
+        if (below + c0 <= w) { below += c0; ++b;
+          if (below + c1 <= w) { below += c1; ++b;
+            if (below + c2 <= w) { below += c2; ++b; } } }
+        prefix[t] = pf[t] | (b << shift);
+        want[t] = w - below;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    float s = *S;
+    if (!bad) {
+      const float q95 = torch_lerp(key2f(prefix[0]), key2f(prefix[1]), r95 - (float)(int)r95);
+      const float q05 = torch_lerp(key2f(prefix[2]), key2f(prefix[3]), r05 - (float)(int)r05);
+      const float range = fmaxf(q95 - q05, 1.0f);
+      s = 0.99f * s + 0.01f * range;
+      *S = s;
+    }
+    if (norm_out) *norm_out = fmaxf(s, 1.0f);
+  }
+}
+
+#ifndef DR_UPDATE_S_REG
+#define DR_UPDATE_S_REG 1  // A/B knob: 0 = the LDS bitonic sort for n <= DR_SORT_MAX
+#endif
+
 extern "C" int dr_update_S(int n, const float* R, float* S, float* norm_out, void* ws, size_t ws_bytes,
                            hipStream_t stream) {
   (void)ws;
@@ -769,6 +858,14 @@ extern "C" int dr_update_S(int n, const float* R, float* S, float* norm_out, voi
   if (n <= 0 || !R || !S) {
     dr_set_error("update_S: n=%d or null pointer", n);
     return DR_E_INVALID;
+  }
+  if (DR_UPDATE_S_REG && n <= 4096) {
+    hipLaunchKernelGGL(k_update_S_reg<4>, dim3(1), dim3(1024), 0, stream, n, R, S, norm_out);
+    return dr_check_launch("update_S_reg");
+  }
+  if (DR_UPDATE_S_REG && n <= 16384) {
+    hipLaunchKernelGGL(k_update_S_reg<16>, dim3(1), dim3(1024), 0, stream, n, R, S, norm_out);
+    return dr_check_launch("update_S_reg");
   }
   if (n > DR_SORT_MAX) {
     hipLaunchKernelGGL(k_update_S_select, dim3(1), dim3(1024), 0, stream, n, R, S, norm_out);

@@ -40,6 +40,9 @@ class ImaginationEngine:
         self.world = world  # (rank, size, group) or None
         self.rank = world[0] if world else 0
         self.wsize = world[1] if world else 1
+        # the collectives run whenever a process group is given, also at size 1
+        # (tests/test_gpu_rccl.py exercises the RCCL path on one GPU)
+        self.dp = world is not None
         self.use_graph = use_graph
         self.graph = None
         self.graph_key = None
@@ -89,7 +92,7 @@ class ImaginationEngine:
         self.rewards, self.continues = f(B, H), f(B, H)
         self.V_t, self.V_c = f(B, H + 1), f(B, H + 1)
         self.R = f(B, H)
-        self.R_all = f(self.wsize * B, H) if self.wsize > 1 else self.R
+        self.R_all = f(self.wsize * B, H) if self.dp else self.R
         self.norm = f(1)
         self.loss_a = f(1 + B * H)
         self.g_mu, self.g_sig = f(B, H, d.action), f(B, H, d.action)
@@ -289,8 +292,8 @@ class ImaginationEngine:
     def phases(self):
         """(name, body, collective-after) in execution order."""
         ph = [("encwarm", self._ph_encwarm, None), ("imagine", self.imagine, None),
-              ("returns", self.returns, self._allgather_R if self.wsize > 1 else None),
-              ("update", self._ph_update, self._allreduce_grads if self.wsize > 1 else None),
+              ("returns", self.returns, self._allgather_R if self.dp else None),
+              ("update", self._ph_update, self._allreduce_grads if self.dp else None),
               ("optim", self._ph_optim, None)]
         return ph
 
@@ -466,7 +469,7 @@ class ImaginationEngine:
                 G["xfwd"].replay()
             ev_x1 = record(s1)
             G["returns"].replay()
-            if self.wsize > 1:
+            if self.dp:
                 self._allgather_R()
             ev_r = record(main)
             main.wait_event(ev_x1)
@@ -478,7 +481,7 @@ class ImaginationEngine:
             ev_x2 = record(s2)
             G["bptt"].replay()
             main.wait_event(ev_x2)
-            if self.wsize > 1:
+            if self.dp:
                 self._allreduce_grads()
             G["optim"].replay()
             losses[e].copy_(ag.loss_buffer[0:2])

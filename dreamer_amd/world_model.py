@@ -142,12 +142,14 @@ class WorldModel(nn.Module):
         self.optimiser = FlatAdamW(self._flat, g["lr"], g["betas"], g["eps"], g["weight_decay"])
         return self._flat
 
-    def set_data_parallel(self, rank, world, group=None):
+    def set_data_parallel(self, rank, world, group=None, force=False):
         """Shard training_step's batch over `world` ranks (one per GPU): the
         mask sum and the loss sums are all-reduced between the step's phases,
         so losses, free-bit clamps and gradients are the global ones, and the
-        flat gradient is all-reduced (sum) before clip_grad_norm_."""
-        self._dp = (rank, world, group) if world > 1 else None
+        flat gradient is all-reduced (sum) before clip_grad_norm_.  force=True
+        keeps the collective path at world == 1 (tests/test_gpu_rccl.py runs
+        it over RCCL on one GPU)."""
+        self._dp = (rank, world, group) if (world > 1 or force) else None
 
     def params_key(self):
         return tuple(p.data_ptr() for p in self.parameters())

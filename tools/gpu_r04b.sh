@@ -4,7 +4,8 @@
 cd "$(dirname "$0")/.." || exit 1
 export PYTHONUNBUFFERED=1
 TAG=${1:-r04b}
-TESTS=${TESTS:-"tests/test_gpu_baseline.py tests/test_gpu_determinism.py tests/test_gpu_flips.py tests/test_gpu_parity.py"}
+TESTS=${TESTS:-"tests/test_gpu_baseline.py tests/test_gpu_determinism.py tests/test_gpu_flips.py tests/test_gpu_parity.py tests/test_gpu_rccl.py"}
+VARIANTS=${VARIANTS:-""}
 R=$(pwd)
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest $TESTS -m gpu -v -s --timeout 300 --timeout-method thread -p no:cacheprovider \
@@ -12,6 +13,11 @@ timeout -k 10 900 python -u -m pytest $TESTS -m gpu -v -s --timeout 300 --timeou
 grep -E "PASSED|FAILED|passed|failed|flip|guarded|NATURAL" gpurun_out/tests_$TAG.log | cut -c1-400 | head -60
 timeout -k 10 300 python bench.py --no-secondary --wm-steps 0 --no-cpu-baseline > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -30 gpurun_out/bench_$TAG.err; exit 1; }
 cut -c1-200 gpurun_out/bench_$TAG.json
+for v in $VARIANTS; do
+  DREAMER_LIB_VARIANT=$v timeout -k 10 300 python bench.py --no-secondary --wm-steps 0 --no-cpu-baseline > gpurun_out/bench_${TAG}_$v.json 2> gpurun_out/bench_${TAG}_$v.err || { tail -30 gpurun_out/bench_${TAG}_$v.err; exit 1; }
+  echo "variant $v: $(cut -c1-160 gpurun_out/bench_${TAG}_$v.json)"
+done
+timeout -k 10 300 python bench.py --no-secondary --wm-steps 0 --no-cpu-baseline > gpurun_out/bench_${TAG}_again.json 2>> gpurun_out/bench_$TAG.err && echo "again: $(cut -c1-160 gpurun_out/bench_${TAG}_again.json)"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o p -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-secondary --wm-steps 0 > $R/gpurun_out/prof_$TAG.log 2>&1 || { tail -20 $R/gpurun_out/prof_$TAG.log; exit 1; }
 cd $R
