@@ -31,3 +31,29 @@ struct alignas(16) ActorTailArgs {
 };
 bool op_actor_tail_ok(const ActorTailArgs& a);
 int op_actor_tail(const ActorTailArgs& a, hipStream_t s);
+
+// The actor's backward for one imagined step (Agent.py:191-210, backward), in
+// ONE launch up to the input gradient of base_net.0:
+//   heads: g_mu = dL/dmu + g_a (1 - a^2), g_ls through clamp + softplus      (saved: gheads)
+//   gx2 = [g_mu | g_ls] [W_mu; W_ls];  g_pre2 = LN-SiLU backward (pre2, n4)     (saved: gpre2, gy2, xh2)
+//   gx1 = g_pre2 W3;                   g_pre1 = LN-SiLU backward (pre1, n1)     (saved: gpre1, gy1, xh1)
+// The caller then runs the input-gradient GEMM of base_net.0 on g_pre1.
+struct alignas(16) ActorTailBwdArgs {
+  int M, A, a1, a2;
+  const float* g_a; long long ldga;        // dL/da through the GRU (may be NULL)
+  const float *g_mu, *g_sig; long long ldgl;  // direct dL/dmu, dL/dsigma (may be NULL)
+  const float* act; long long ldact;       // the actions (tanh outputs)
+  const float* ls_raw; long long ldl;      // raw log_sig head outputs
+  const float* eps;                        // [M][A] rsample noise
+  const float *wmu, *wls;                  // mu_head / log_sig_head weights [A][a2]
+  float* gheads; long long ldh;            // [M] x 2A save
+  const float* pre2; long long ld2;        // base_net.3 output rows (LN4 input)
+  const float *n4g, *n4b;
+  float *gpre2, *gy2, *xh2;                // saves, row stride ld2
+  const float* w3t;                        // base_net.3 weight transposed [a1][a2]
+  const float* pre1; long long ld1;        // base_net.0 output rows (LN1 input)
+  const float *n1g, *n1b;
+  float *gpre1, *gy1, *xh1;                // saves, row stride ld1
+};
+bool op_actor_tail_bwd_ok(const ActorTailBwdArgs& a);
+int op_actor_tail_bwd(const ActorTailBwdArgs& a, hipStream_t s);

@@ -256,3 +256,199 @@ int op_actor_tail(const ActorTailArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_actor_tail, dim3((unsigned)((a.M + AT_ROWS - 1) / AT_ROWS)), dim3(AT_NT), 0, s, a);
   return dr_check_launch("actor_tail");
 }
+
+// ---------------------------------------------------------------------------
+// k_actor_tail_bwd: the backward of k_actor_tail's layers (chain.h).  It
+// replaces the head backward (k_actor_head_bwd_x), the fused LN-backward +
+// base_net.3 input-gradient product, and base_net.1's LN-SiLU backward pass:
+// three launches per BPTT step.  Same row-block layout as the forward: a
+// workgroup owns AT_ROWS batch rows, wave r row r for the LayerNorms, thread
+// (k, half) one column of W3 over half of its rows in registers.
+// LayerNorm-SiLU backward (k_ln_silu_bwd's arithmetic): x_hat, y = x_hat g + b,
+// s = sigmoid(y), dy = gx s (1 + y (1 - s)), dx_hat = dy g,
+// g_pre = rstd (dx_hat - mean(dx_hat) - x_hat mean(dx_hat x_hat)).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float4 at_ln_silu_bwd(float4 gx, float4 p, bool ok, int K, float4 gm, float4 bt,
+                                                 float4& gy, float4& xh) {
+  const float mean = wave_sum(ok ? (p.x + p.y) + (p.z + p.w) : 0.f) / (float)K;
+  float sq = 0.f;
+  if (ok) {
+    const float dx = p.x - mean, dy = p.y - mean, dz = p.z - mean, dw = p.w - mean;
+    sq = (dx * dx + dy * dy) + (dz * dz + dw * dw);
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)K + 1e-5f);
+  const float pv[4] = {p.x, p.y, p.z, p.w}, gv[4] = {gx.x, gx.y, gx.z, gx.w};
+  const float gmv[4] = {gm.x, gm.y, gm.z, gm.w}, btv[4] = {bt.x, bt.y, bt.z, bt.w};
+  float xhv[4], gyv[4], gxh[4];
+  float c1 = 0.f, c2 = 0.f;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    xhv[c] = (pv[c] - mean) * rstd;
+    const float y = xhv[c] * gmv[c] + btv[c];
+    const float sg = 1.0f / (1.0f + expf(-y));
+    gyv[c] = gv[c] * (sg * (1.0f + y * (1.0f - sg)));
+    gxh[c] = gyv[c] * gmv[c];
+    if (ok) {
+      c1 += gxh[c];
+      c2 += gxh[c] * xhv[c];
+    }
+  }
+  c1 = wave_sum(c1) / (float)K;
+  c2 = wave_sum(c2) / (float)K;
+  gy = make_float4(gyv[0], gyv[1], gyv[2], gyv[3]);
+  xh = make_float4(xhv[0], xhv[1], xhv[2], xhv[3]);
+  return make_float4(rstd * (gxh[0] - c1 - xhv[0] * c2), rstd * (gxh[1] - c1 - xhv[1] * c2),
+                     rstd * (gxh[2] - c1 - xhv[2] * c2), rstd * (gxh[3] - c1 - xhv[3] * c2));
+}
+
+__global__ __launch_bounds__(AT_NT) void k_actor_tail_bwd(ActorTailBwdArgs aa) {
+  __shared__ ActorTailBwdArgs a;
+  dr_stage_args(aa, a, threadIdx.x);
+  __shared__ float s_gh[AT_ROWS][AT_MAXH];
+  __shared__ __attribute__((aligned(16))) float s_w[AT_MAXH][AT_MAXW];  // head weights
+  __shared__ __attribute__((aligned(16))) float s_g2[AT_ROWS][AT_MAXW];  // g_pre2
+  __shared__ __attribute__((aligned(16))) float s_g1[AT_ROWS][AT_MAXW];  // gx1
+  const int M = dr_uni(a.M), A = dr_uni(a.A), a1 = dr_uni(a.a1), a2 = dr_uni(a.a2);
+  const int m0 = blockIdx.x * AT_ROWS;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int m = m0 + wave;  // this wave's row in the LayerNorm phases
+  // ---- P1: head weights -> LDS, head backward of the rows -> LDS (+ save) ----
+  for (int x = tid; x < 2 * A * (a2 >> 2); x += AT_NT) {
+    const int o = x / (a2 >> 2), k4 = x - o * (a2 >> 2);
+    const float* src = o < A ? dr_uni(a.wmu) : dr_uni(a.wls);
+    const int oo = o < A ? o : o - A;
+    *reinterpret_cast<float4*>(&s_w[o][4 * k4]) = dr_ld4(src, (unsigned)(oo * a2 + 4 * k4));
+  }
+  // the LN rows of the first phase and their parameters, issued with the above
+  const bool ok2 = lane < (a2 >> 2);
+  const unsigned k2 = ok2 ? 4u * lane : 0u;
+  const bool live = m < M;
+  const float4 p2 = dr_ld4(dr_uni(a.pre2), live && ok2 ? (unsigned)(m * (int)a.ld2) + k2 : 0u);
+  const float4 g4 = dr_ld4(dr_uni(a.n4g), k2), b4 = dr_ld4(dr_uni(a.n4b), k2);
+  if (tid < AT_ROWS * A) {
+    const int ml = tid / A, k = tid - ml * A, mm = m0 + ml;
+    float gmu = 0.f, gls = 0.f;
+    if (mm < M) {
+      gmu = a.g_mu ? dr_g(a.g_mu)[(long long)mm * a.ldgl + k] : 0.0f;
+      float gsg = a.g_sig ? dr_g(a.g_sig)[(long long)mm * a.ldgl + k] : 0.0f;
+      if (a.g_a) {
+        const float av = dr_g(a.act)[(long long)mm * a.ldact + k];
+        const float gp = dr_g(a.g_a)[(long long)mm * a.ldga + k] * (1.0f - av * av);
+        gmu = gmu + gp;
+        gsg = gsg + gp * dr_g(a.eps)[(long long)mm * A + k];
+      }
+      const float lr = dr_g(a.ls_raw)[(long long)mm * a.ldl + k];
+      const float lc = fminf(fmaxf(lr, -5.0f), 2.0f);
+      if (lr >= -5.0f && lr <= 2.0f) {
+        const float ez = expf(lc);
+        gls = (lc > 20.0f) ? gsg : gsg * ez / (ez + 1.0f);
+      }
+      dr_g(a.gheads)[(long long)mm * a.ldh + k] = gmu;
+      dr_g(a.gheads)[(long long)mm * a.ldh + A + k] = gls;
+    }
+    s_gh[ml][k] = gmu;
+    s_gh[ml][A + k] = gls;
+  }
+  __syncthreads();
+  // ---- P2: wave r: gx2 = gheads [W_mu; W_ls], g_pre2 = LN4-SiLU backward; W3^T half rows requested ----
+  const int j = tid >> 1, hf = tid & 1, kh = a2 >> 1;  // thread: column j of W3 (row j of W3^T), half hf
+  const bool wthr = j < a1;
+  float4 w3[AT_KH4];
+  {
+    const float* W = dr_uni(a.w3t);
+#pragma unroll
+    for (int i = 0; i < AT_KH4; ++i) {
+      const bool ok = wthr && 4 * i < kh;
+      w3[i] = dr_ld4(W, ok ? (unsigned)(j * a2 + hf * kh + 4 * i) : 0u);
+    }
+  }
+  {
+    float4 gx = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok2) {
+#pragma unroll
+      for (int o = 0; o < AT_MAXH; ++o) {
+        if (o < 2 * A) {
+          const float gh = s_gh[wave][o];
+          const float4 wv = *reinterpret_cast<const float4*>(&s_w[o][4 * lane]);
+          gx.x = fmaf(gh, wv.x, gx.x);
+          gx.y = fmaf(gh, wv.y, gx.y);
+          gx.z = fmaf(gh, wv.z, gx.z);
+          gx.w = fmaf(gh, wv.w, gx.w);
+        }
+      }
+    }
+    float4 gy, xh;
+    const float4 gp = at_ln_silu_bwd(gx, p2, ok2, a2, g4, b4, gy, xh);
+    if (ok2) {
+      *reinterpret_cast<float4*>(&s_g2[wave][4 * lane]) = gp;
+      if (live) {
+        const unsigned e = (unsigned)(m * (int)a.ld2) + k2;
+        dr_st4(a.gpre2, e, gp);
+        dr_st4(a.gy2, e, gy);
+        dr_st4(a.xh2, e, xh);
+      }
+    }
+  }
+  __syncthreads();
+  // ---- P3: gx1 = g_pre2 W3 (thread (j, half): 2 x AT_ROWS partial dots over its half of a2) ----
+  {
+    float acc[AT_ROWS];
+#pragma unroll
+    for (int r = 0; r < AT_ROWS; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < AT_KH4; ++i) {
+      if (4 * i < kh) {
+        const int k = hf * kh + 4 * i;
+#pragma unroll
+        for (int r = 0; r < AT_ROWS; ++r) {
+          const float4 gv = *reinterpret_cast<const float4*>(&s_g2[r][k]);
+          acc[r] = fmaf(gv.x, w3[i].x, acc[r]);
+          acc[r] = fmaf(gv.y, w3[i].y, acc[r]);
+          acc[r] = fmaf(gv.z, w3[i].z, acc[r]);
+          acc[r] = fmaf(gv.w, w3[i].w, acc[r]);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < AT_ROWS; ++r) {
+      const float o = __shfl_xor(acc[r], 1, 64);
+      if (wthr && hf == 0) s_g1[r][j] = acc[r] + o;
+    }
+  }
+  __syncthreads();
+  // ---- P4: wave r: g_pre1 = LN1-SiLU backward of gx1 ----
+  {
+    const bool ok1 = lane < (a1 >> 2);
+    const unsigned k1 = ok1 ? 4u * lane : 0u;
+    const float4 p1 = dr_ld4(dr_uni(a.pre1), live && ok1 ? (unsigned)(m * (int)a.ld1) + k1 : 0u);
+    const float4 g1 = dr_ld4(dr_uni(a.n1g), k1), b1 = dr_ld4(dr_uni(a.n1b), k1);
+    const float4 gx = ok1 ? *reinterpret_cast<const float4*>(&s_g1[wave][4 * lane]) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 gy, xh;
+    const float4 gp = at_ln_silu_bwd(gx, p1, ok1, a1, g1, b1, gy, xh);
+    if (ok1 && live) {
+      const unsigned e = (unsigned)(m * (int)a.ld1) + k1;
+      dr_st4(a.gpre1, e, gp);
+      dr_st4(a.gy1, e, gy);
+      dr_st4(a.xh1, e, xh);
+    }
+  }
+}
+
+bool op_actor_tail_bwd_ok(const ActorTailBwdArgs& a) {
+  const uintptr_t al = (uintptr_t)a.wmu | (uintptr_t)a.wls | (uintptr_t)a.pre2 | (uintptr_t)a.n4g | (uintptr_t)a.n4b |
+                       (uintptr_t)a.gpre2 | (uintptr_t)a.gy2 | (uintptr_t)a.xh2 | (uintptr_t)a.w3t | (uintptr_t)a.pre1 |
+                       (uintptr_t)a.n1g | (uintptr_t)a.n1b | (uintptr_t)a.gpre1 | (uintptr_t)a.gy1 | (uintptr_t)a.xh1;
+  return a.M > 0 && a.A >= 1 && 2 * a.A <= AT_MAXH && a.a2 % 8 == 0 && a.a2 / 2 <= 4 * AT_KH4 && a.a2 <= AT_MAXW &&
+         a.a1 % 4 == 0 && a.a1 <= AT_MAXW && 2 * a.a1 <= AT_NT && (al & 15) == 0 && a.ld1 % 4 == 0 && a.ld2 % 4 == 0 &&
+         (long long)a.M * std::max(a.ld1, a.ld2) < (1LL << 31) && a.act && a.ls_raw && a.eps && a.gheads &&
+         (!a.g_a || a.act);
+}
+
+int op_actor_tail_bwd(const ActorTailBwdArgs& a, hipStream_t s) {
+  if (!op_actor_tail_bwd_ok(a)) {
+    dr_set_error("actor_tail_bwd: unsupported dims / alignment (a2 %% 8 == 0, a2 <= 200, a1 <= 256, 2A <= 16)");
+    return DR_E_INVALID;
+  }
+  hipLaunchKernelGGL(k_actor_tail_bwd, dim3((unsigned)((a.M + AT_ROWS - 1) / AT_ROWS)), dim3(AT_NT), 0, s, a);
+  return dr_check_launch("actor_tail_bwd");
+}

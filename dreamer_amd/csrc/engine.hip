@@ -5,8 +5,14 @@
 #include "engine_util.h"
 #include "chain.h"
 
+#ifndef DR_B16_CHAIN_WKS
+#define DR_B16_CHAIN_WKS 1  // A/B knob: bf16 mode's per-step grouped products on bf16 weight planes
+#endif
 #ifndef DR_GRU_BWD_EPI
 #define DR_GRU_BWD_EPI 1  // A/B knob: 0 = the GRU backward as its own elementwise launch
+#endif
+#ifndef DR_ACTOR_TAIL_BWD
+#define DR_ACTOR_TAIL_BWD 1  // A/B knob: 0 = head backward + two LN-backward launches + the fused product
 #endif
 #ifndef DR_ACTOR_TAIL
 #define DR_ACTOR_TAIL 1  // A/B knob (tools/build_variant.py): 0 = z-gather + two skinny launches
@@ -209,8 +215,11 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
 struct ObsWs {
   float *gi, *gh, *pre1, *logits, *wt, *hb[2];
   int* idx;
+  void *s3m0, *s3whh;  // bf16 planes of latent_mapper.0's h-columns and W_hh (k_gemm_wks3)
 };
 static void obs_carve(Carve& c, const dr_dims* d, int B, ObsWs& w) {
+  w.s3m0 = c.raw(op_nt_split3_ws_bytes(d->enc_hidden, d->hidden));
+  w.s3whh = c.raw(op_nt_split3_ws_bytes(3 * d->hidden, d->hidden));
   w.gi = c.f((long long)B * 3 * d->hidden);
   w.gh = c.f((long long)B * 3 * d->hidden);
   w.pre1 = c.f((long long)B * d->enc_hidden);
@@ -250,6 +259,11 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
     DR_REQUIRE(wm->w_ih && wm->w_hh && wm->b_ih && wm->b_hh, "GRU weights required");
     DR_TRY(op_transpose(3 * Hd, L + d->action, wm->w_ih, w.wt, s));
   }
+  const bool planes = B >= 128 && T > 1 && Hd % 8 == 0;
+  if (planes) {
+    DR_TRY(split_planes(eh, Hd, wm->map0.w + F, F + Hd, w.s3m0, s));
+    DR_TRY(split_planes(3 * Hd, Hd, wm->w_hh, Hd, w.s3whh, s));
+  }
   const float* h = h_init;  // current hidden (NULL = zeros)
   int hb = 0;
   // B >= 128 (split GRU): the next step's hidden product h W_hh^T + b_hh rides
@@ -278,7 +292,14 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
     gh_pre = split_gru && h && t + 1 < T;
     if (gh_pre) {
       g[1] = lin(B, 3 * Hd, Hd, h, Hd, wm->w_hh, Hd, wm->b_hh, w.gh, 3 * Hd);
-      g[0].bf16 = g[1].bf16 = 0;  // (bf16 mode: these products stay f32)
+      if (planes) {
+        // bf16 mode: plane 0 times bf16-rounded h (k_gemm_wks3<1>); fp32 mode: the 3-term split
+        wplanes(g[0], w.s3m0);
+        wplanes(g[1], w.s3whh);
+        if (!DR_B16_CHAIN_WKS) g[0].bf16 = g[1].bf16 = 0;
+      } else {
+        g[0].bf16 = g[1].bf16 = 0;  // (bf16 mode: these products stay f32)
+      }
     }
     DR_TRY(gemm_launch(G_NT, AM_PLAIN, g, gh_pre ? 2 : 1, s));
     float* lg = (t == T - 1 && logits_out) ? logits_out : nullptr;
@@ -328,6 +349,7 @@ struct ImWs {
   float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog, *rval, *wt, *wst, *bst;  // forward scratch
   float *tl0f, *hpart;  // forward: actor Linear 0 transposed ([Hd+L][a1]), its h-part + bias [B][a1]
   void *s3r, *s3c;  // split3 weight planes of the reward / continue heads' first Linear
+  void *s3p0, *s3a0, *s3whh, *s3wt, *s3twhh;  // bf16 planes of the per-step chain weights (k_gemm_wks3)
   float* s3part;    // their split-K partial sums
   size_t s3part_n;
   int* idx[2];
@@ -354,6 +376,11 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.rlog = c.f(B1 * d->buckets);
   w.clog = c.f(B1);
   w.rval = c.f(B1);
+  w.s3p0 = c.raw(op_nt_split3_ws_bytes(d->prior_h1, Hd));
+  w.s3a0 = c.raw(op_nt_split3_ws_bytes(d->actor_h1, Hd));
+  w.s3whh = c.raw(op_nt_split3_ws_bytes(3 * Hd, Hd));
+  w.s3wt = c.raw(op_nt_split3_ws_bytes(L + A, 3 * Hd));
+  w.s3twhh = c.raw(op_nt_split3_ws_bytes(Hd, 3 * Hd));
   w.s3r = c.raw(op_nt_split3_ws_bytes(d->rew_h1, d->hidden + L));
   w.s3c = c.raw(op_nt_split3_ws_bytes(d->cont_h1, d->hidden + L));
   w.s3part_n = op_gemm_nt_split3_part_floats((int)B1, std::max(d->rew_h1, d->cont_h1));
@@ -467,6 +494,12 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
     return at;
   };
   const bool fused_actor = zg && DR_ACTOR_TAIL && op_actor_tail_ok(actor_tail(0, w.idx[0], latents));
+  const bool planes = split_gru && H > 1 && Hd % 8 == 0;
+  if (planes) {
+    DR_TRY(split_planes(d->prior_h1, Hd, wm->prior.l0.w, Hd, w.s3p0, s));
+    if (zg) DR_TRY(split_planes(a1, Hd, ac->l0.w, Hd + L, w.s3a0, s));
+    DR_TRY(split_planes(3 * Hd, Hd, wm->w_hh, Hd, w.s3whh, s));
+  }
 
   // actor at step 0 (Agent.py:191-210)
   if (fused_actor) {
@@ -502,10 +535,23 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
       const bool more = t + 1 < H;
       GemmArgs p[3];
       int np = 0;
-      p[np++] = lin(B, d->prior_h1, Hd, h_n, ldH, wm->prior.l0.w, Hd, wm->prior.l0.b, p1, d->prior_h1);
-      if (more && zg) p[np++] = lin(B, a1, Hd, h_n, ldH, ac->l0.w, Hd + L, ac->l0.b, w.hpart, a1);
-      if (more && split_gru) p[np++] = lin(B, 3 * Hd, Hd, h_n, ldH, wm->w_hh, Hd, wm->b_hh, w.gh, 3 * Hd);
-      for (int i = 0; i < np; ++i) p[i].bf16 = 0;  // (bf16 mode: these products stay f32)
+      p[np] = lin(B, d->prior_h1, Hd, h_n, ldH, wm->prior.l0.w, Hd, wm->prior.l0.b, p1, d->prior_h1);
+      if (planes) wplanes(p[np], w.s3p0);
+      ++np;
+      if (more && zg) {
+        p[np] = lin(B, a1, Hd, h_n, ldH, ac->l0.w, Hd + L, ac->l0.b, w.hpart, a1);
+        if (planes) wplanes(p[np], w.s3a0);
+        ++np;
+      }
+      if (more && split_gru) {
+        p[np] = lin(B, 3 * Hd, Hd, h_n, ldH, wm->w_hh, Hd, wm->b_hh, w.gh, 3 * Hd);
+        if (planes) wplanes(p[np], w.s3whh);
+        ++np;
+      }
+      // bf16 mode: on the weight planes the products run in bf16 (k_gemm_wks3<1>),
+      // else they stay f32
+      for (int i = 0; i < np; ++i)
+        if (!planes || !DR_B16_CHAIN_WKS) p[i].bf16 = 0;
       DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, np, s));
     }
     DR_TRY(run(G_NT, AM_LNSILU, lin_ln(B, d->prior_h2, d->prior_h1, p1, d->prior_h1, wm->prior.n1, wm->prior.l3.w,
@@ -680,8 +726,13 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
         {a1, Hd + L, a1, ac->l0.w, w.tl0a},
     };
     DR_TRY(op_transpose_multi(tj, 9, s));
+    if (B >= 128 && (3 * Hd) % 8 == 0) {
+      DR_TRY(split_planes(L + A, 3 * Hd, w.wt, 3 * Hd, w.s3wt, s));
+      DR_TRY(split_planes(Hd, 3 * Hd, w.twhh, 3 * Hd, w.s3twhh, s));
+    }
   }
   }  // do_prep
+  const bool planes = B >= 128 && (3 * Hd) % 8 == 0;
   if (!do_main) return DR_OK;
 
   for (int t = H - 1; t >= 0; --t) {
@@ -728,6 +779,10 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
         p[0] = bwd_nt(B, L + A, 3 * Hd, w.ggi, 3 * Hd, w.wt, gZ_t, ldL, 1);
         p[0].Y2 = w.gA + (long long)t * A; p[0].ldy2 = ldA; p[0].nsplitY = L;
         p[1] = bwd_nt(B, Hd, 3 * Hd, w.ggh, 3 * Hd, w.twhh, gH_t, ldH, 1);
+        if (planes) {
+          wplanes(p[0], w.s3wt);
+          wplanes(p[1], w.s3twhh);
+        }
         DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, 2, s));
       } else {
         // only the action gradient is consumed at t = 0
@@ -737,11 +792,36 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
     // actor at step t: heads, then base_net (Agent.py:191-210)
     const long long ot = (long long)t * A;
     float* gh_t = w.gheads + (long long)t * 2 * A;
+    const long long o2 = (long long)t * a2, o1 = (long long)t * a1;
+    ActorTailBwdArgs tb;
+    memset(&tb, 0, sizeof(tb));
+    tb.M = B; tb.A = A; tb.a1 = a1; tb.a2 = a2;
+    tb.g_a = w.gA + ot; tb.ldga = ldA;
+    tb.g_mu = g_mus ? g_mus + ot : nullptr; tb.g_sig = g_sigmas ? g_sigmas + ot : nullptr; tb.ldgl = ldA;
+    tb.act = actions + ot; tb.ldact = ldA; tb.ls_raw = tp.ls_raw + ot; tb.ldl = ldA;
+    tb.eps = tp.eps + (long long)t * B * A;
+    tb.wmu = ac->mu.w; tb.wls = ac->ls.w;
+    tb.gheads = gh_t; tb.ldh = (long long)H * 2 * A;
+    tb.pre2 = tp.pre2a + o2; tb.ld2 = lda2; tb.n4g = ac->n4.w; tb.n4b = ac->n4.b;
+    tb.gpre2 = w.gpre2a + o2; tb.gy2 = w.gy2a + o2; tb.xh2 = w.xh2a + o2;
+    tb.w3t = w.tl3a;
+    tb.pre1 = tp.pre1a + o1; tb.ld1 = lda1; tb.n1g = ac->n1.w; tb.n1b = ac->n1.b;
+    tb.gpre1 = w.gpre1a + o1; tb.gy1 = w.gy1a + o1; tb.xh1 = w.xh1a + o1;
+    if (DR_ACTOR_TAIL_BWD && op_actor_tail_bwd_ok(tb)) {
+      // heads + both LN-SiLU backwards + base_net.3's input gradient in one
+      // launch (chain.hip), then base_net.0's input gradient into [gH_t | gZ_t]
+      DR_TRY(op_actor_tail_bwd(tb, s));
+      if (t > 0) {
+        GemmArgs g0 = bwd_nt(B, Hd + L, a1, w.gpre1a + o1, lda1, w.tl0a, gH_t, ldH, 1);
+        g0.Y2 = gZ_t; g0.ldy2 = ldL; g0.nsplitY = Hd;
+        DR_TRY(run(G_NT, AM_PLAIN, g0, s));
+      }
+      continue;
+    }
     // head backward + its input gradient (K = 2A) in one launch
     DR_TRY(op_actor_head_bwd_x(B, A, a2, w.gA + ot, ldA, g_mus ? g_mus + ot : nullptr,
                                g_sigmas ? g_sigmas + ot : nullptr, ldA, actions + ot, ldA, tp.ls_raw + ot, ldA,
                                tp.eps + (long long)t * B * A, gh_t, (long long)H * 2 * A, w.thead, w.gx2a, a2, s));
-    const long long o2 = (long long)t * a2, o1 = (long long)t * a1;
     // base_net.4/.3: LN-SiLU backward fused into the .3 input-gradient GEMM; the
     // prologue also writes g_pre and the LN-parameter saves for the weight grads
     DR_TRY(lnbwd_nt(B, a1, a2, w.gx2a, a2, tp.pre2a + o2, lda2, ac->n4, w.tl3a, w.gx1a, a1, 0, w.gpre2a + o2, lda2,

@@ -69,6 +69,10 @@ struct alignas(16) GemmArgs {
   // staged (f32 accumulation, f32 in / out); set by the engine per call
   int bf16;
   GruBwdEpi gb;  // gb.Hd > 0: fused GRU backward on the stored values (see GruBwdEpi)
+  // NT B operand also given as bf16 planes [K/32][3][wsplit_np][32] (conv.h
+  // op_nt_repack_split3 of W): per-step chain products then run on the bf16
+  // MFMA -- f32-accurate 3-term split (fp32 mode) or plane 0 alone (bf16 mode)
+  const unsigned short* wsplit; int wsplit_np, pad2_;
 };
 
 enum { EPI_NONE = 0, EPI_SAMPLE = 1, EPI_ACTOR = 2 };

@@ -1805,6 +1805,163 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wk(GemmBatch gb, int splits, i
   }
 }
 
+// ---------------------------------------------------------------------------
+// The wave-K chain kernel on the bf16 MFMA (v_mfma_f32_16x16x32_bf16).  Same
+// work split as k_gemm_wk<32, 32, 4> -- every wave computes the whole 32 x 32
+// tile over its own run of 32-k chunks, fragments straight from L2 into a
+// register ring, the partial tiles met once in LDS -- but the products run on
+// bf16 planes: W pre-split once per call into [K/32][3][Np][32]
+// (op_nt_repack_split3, RNE), the A rows split in registers as they arrive
+// (split3_pair: truncation, exact residuals).  NTP = 3: the six products of
+// order >= 2^-16 (conv_split.hip's f32-accurate scheme, 2.67x the f32 MFMA
+// rate); NTP = 1: A rounded to bf16 (RNE) times plane 0 (bf16 perf mode).
+// Lane (r, q) loads k = 8q .. 8q + 7 of its rows -- the MFMA fragment -- and
+// the accumulator holds row r, columns 4q .. 4q + 3 (B fragment first).
+// ---------------------------------------------------------------------------
+typedef unsigned wk_u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 wk_bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4 wk_mfma(wk_u32x4 a, wk_u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(wk_bf16x8, a), __builtin_bit_cast(wk_bf16x8, b),
+                                                  c, 0, 0, 0);
+}
+__device__ __forceinline__ unsigned wk_pack_rne(float x0, float x1) {
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  const b2 v = {(__bf16)x0, (__bf16)x1};
+  return __builtin_bit_cast(unsigned, v);
+}
+
+template <int NTP, int D>
+__global__ __launch_bounds__(256) void k_gemm_wks3(GemmBatch gb, int npack) {
+  constexpr int NW = 4, FM = 2, FN = 2, NTH = 256, NT4 = FM * FN * 256;
+  __shared__ GemmArgs s_args;
+  __shared__ __attribute__((aligned(16))) float red[NW][FM * FN * 4][64];
+  int z = 0;
+  const int plt = dr_pack_tile<32, 32>(gb, npack, z);
+  if (plt == -1) return;
+  dr_stage_args(gb.p[z], s_args, threadIdx.x);
+  const GemmArgs& g = s_args;
+  const int M = dr_uni(g.M), N = dr_uni(g.N), K = dr_uni(g.K);
+  const int tiles_m = (M + 31) / 32, tiles_n = (N + 31) / 32;
+  const int lt = plt >= 0 ? plt : dr_xcd_tile(blockIdx.x, tiles_m * tiles_n);
+  if (lt < 0) return;
+  const int tn = lt / tiles_m, tm = lt - tn * tiles_m;  // row tiles of one weight slice adjacent
+  const int m0 = tm * 32, n0 = tn * 32;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
+  const float* A = dr_uni(g.A);
+  const int lda = dr_uni((int)g.lda);
+  const unsigned short* wr = dr_uni(g.wsplit);
+  const int Np = dr_uni(g.wsplit_np);
+  // bias of the outputs this thread finalises (waited for at the end)
+  constexpr int NEPI = (NT4 + NTH - 1) / NTH;
+  float ebias[NEPI];
+  {
+    const float* bias = dr_uni(g.bias);
+#pragma unroll
+    for (int i = 0; i < NEPI; ++i) {
+      const int x = tid + NTH * i, l = x & 63, e = (x >> 6) & 3, tj = x >> 8;
+      const int n = n0 + (tj % FN) * 16 + 4 * (l >> 4) + e;
+      const bool ok = bias && x < NT4 && n < N;
+      ebias[i] = ok ? dr_ld1(bias, (unsigned)n) : 0.f;
+    }
+  }
+  const int nkc = (K + 31) >> 5;
+  const int c0 = (nkc * wave) / NW, c1 = (nkc * (wave + 1)) / NW;
+  const int clast = max(c1 - 1, 0);
+  unsigned oa[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) oa[i] = (unsigned)(min(m0 + 16 * i + r, M - 1) * lda);
+  unsigned ob[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) ob[j] = (unsigned)(n0 + 16 * j + r) * 32u + 8u * q;  // within a plane (Np >= n rows)
+  f32x4 ra[D][FM][2];
+  wk_u32x4 rb[D][NTP][FN];
+  auto load = [&](int c, int sl) {
+    const int k = 32 * c + 8 * q;
+    const unsigned kk = k < K ? (unsigned)k : 0u;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      ra[sl][i][0] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)A + ((oa[i] + kk) << 2));
+      ra[sl][i][1] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)A + ((oa[i] + kk + 4) << 2));
+    }
+#pragma unroll
+    for (int p = 0; p < NTP; ++p)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const unsigned e = (unsigned)((c * 3 + p) * Np) * 32u + ob[j];
+        rb[sl][p][j] = *(const DR_GLOBAL wk_u32x4*)((const DR_GLOBAL char*)wr + (e << 1));
+      }
+  };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < D; ++u) load(min(c0 + u, clast), u);
+  const int ncw = c1 - c0;
+  for (int cc = 0; cc < ncw; cc += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      if (cc + u >= ncw) break;
+      const int c = c0 + cc + u;
+      const bool kin = 32 * c + 8 * q < K;  // K % 8 == 0: a lane's 8-run is all in or all out
+      wk_u32x4 a[NTP][FM];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        f32x4 x0 = ra[u][i][0], x1 = ra[u][i][1];
+        if (!kin) x0 = x1 = (f32x4){0.f, 0.f, 0.f, 0.f};
+        if constexpr (NTP == 3) {
+          unsigned h[4], m[4], l[4];
+          split3_pair(x0[0], x0[1], h[0], m[0], l[0]);
+          split3_pair(x0[2], x0[3], h[1], m[1], l[1]);
+          split3_pair(x1[0], x1[1], h[2], m[2], l[2]);
+          split3_pair(x1[2], x1[3], h[3], m[3], l[3]);
+          a[0][i] = (wk_u32x4){h[0], h[1], h[2], h[3]};
+          a[1 % NTP][i] = (wk_u32x4){m[0], m[1], m[2], m[3]};
+          a[2 % NTP][i] = (wk_u32x4){l[0], l[1], l[2], l[3]};
+        } else {
+          a[0][i] = (wk_u32x4){wk_pack_rne(x0[0], x0[1]), wk_pack_rne(x0[2], x0[3]), wk_pack_rne(x1[0], x1[1]),
+                               wk_pack_rne(x1[2], x1[3])};
+        }
+      }
+#define DR_WK3(PA, PB)                        \
+  _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
+      wk_mfma(rb[u][PB][j], a[PA][i], acc[i][j]);
+      if constexpr (NTP == 3) {
+        DR_WK3(2 % NTP, 0)
+        DR_WK3(1 % NTP, 1 % NTP)
+        DR_WK3(0, 2 % NTP)
+        DR_WK3(1 % NTP, 0)
+        DR_WK3(0, 1 % NTP)
+      }
+      DR_WK3(0, 0)
+#undef DR_WK3
+      load(min(c + D, clast), u);  // unconditional: a load under a branch is waited for at once
+    }
+  }
+  // partial tiles meet in LDS; element (t, e, l) of tile t = (i, j): row 16 i + (l & 15), column 16 j + 4 (l >> 4) + e
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[wave][(i * FN + j) * 4 + e][lane] = acc[i][j][e];
+  __syncthreads();
+#pragma unroll
+  for (int ii = 0; ii < NEPI; ++ii) {
+    const int x = tid + NTH * ii;
+    if (x >= NT4) break;
+    const int l = x & 63, e = (x >> 6) & 3, tj = x >> 8;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += red[w][tj * 4 + e][l];
+    const int t = tj / FN, j = tj - t * FN;
+    const int m = m0 + t * 16 + (l & 15), n = n0 + j * 16 + 4 * (l >> 4) + e;
+    if (m >= M || n >= N) continue;
+    epilogue_store_b(g, m, n, v, ebias[ii]);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_splitk_finish(GemmBatch gb, int splits) {
   const GemmArgs& g = gb.p[blockIdx.z];
   const long long MN = (long long)g.M * g.N;
@@ -2316,6 +2473,31 @@ static bool wk_ok(const GemmBatch& gb, int count) {
   return true;
 }
 
+// every problem with pre-split weight planes and the wave-K shape (NT, no second
+// A segment or B segment, K % 8 == 0, 16-byte aligned rows, 32-bit offsets)
+static bool wks3_ok(const GemmBatch& gb, int count) {
+  for (int i = 0; i < count; ++i) {
+    const GemmArgs& g = gb.p[i];
+    if (!g.wsplit || g.wsplit_np < ((g.N + 31) & ~31) || g.K % 8 || g.K < 8 || g.lda % 4 || ((uintptr_t)g.A & 15) ||
+        ((uintptr_t)g.wsplit & 15) || g.ksplitA < g.K || g.W2 || g.epi != EPI_NONE || g.out_conv || g.M < 1 || g.N < 1 ||
+        (long long)g.M * g.lda >= (1LL << 30) || (long long)((g.K + 31) / 32) * 3 * g.wsplit_np * 32 >= (1LL << 30))
+      return false;
+  }
+  return true;
+}
+static void launch_wks3(const GemmBatch& gb, int count, hipStream_t s, bool bf16) {
+  int tot = 0, maxt = 0;
+  for (int i = 0; i < count; ++i) {
+    const int t = dr_cdiv(gb.p[i].M, 32) * dr_cdiv(gb.p[i].N, 32);
+    tot += t;
+    maxt = std::max(maxt, t);
+  }
+  const int npack = count > 1 ? count : 0;
+  const dim3 grid(dr_xcd_grid(npack ? tot : maxt));
+  if (bf16) hipLaunchKernelGGL((k_gemm_wks3<1, 2>), grid, dim3(256), 0, s, gb, npack);
+  else hipLaunchKernelGGL((k_gemm_wks3<3, 2>), grid, dim3(256), 0, s, gb, npack);
+}
+
 // split-K over workgroups only when the tile grid is under one workgroup per
 // CU and every problem brought scratch for it
 template <int BM, int BN, int NW, int D, int KMAP = 0>
@@ -2372,6 +2554,9 @@ static bool tile_offsets_ok(const GemmBatch& gb, int count) {
   return true;
 }
 
+#ifndef DR_WKS3
+#define DR_WKS3 1  // A/B knob: 0 = chain products with weight planes keep the f32 wave-K / bf16 tile kernels
+#endif
 #ifndef DR_B16_CHAIN_TILE
 // bf16 mode's chain products on k_gemm_tile_b16 (0: the f32 wave-K kernel):
 // bf16 headline 730.5 k against 723.3 k (profiles/r03zf_ab_bf16_chain_route.txt)
@@ -2410,7 +2595,8 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
         // 15.8 -> 13.0 us, BPTT 32.2 -> 25.7, GRU hidden product 13.3 -> 12.3,
         // profiles/r03g_kbench_wk.txt); the LDS tile kernel stays for the
         // shapes the wave-K kernel does not take (and as kbench variant 25)
-        if (DR_B16_CHAIN_TILE && b16_ok(gb, count)) launch_tile_b16<32, 32, 4>(gt, count, s);
+        if (DR_WKS3 && wks3_ok(gb, count)) launch_wks3(gt, count, s, b16_ok(gb, count));
+        else if (DR_B16_CHAIN_TILE && b16_ok(gb, count)) launch_tile_b16<32, 32, 4>(gt, count, s);
         else if (g_tile_variant == 0 && wk_ok(gb, count)) launch_wk<32, 32, 4, 2, 1>(gt, count, s, 0);
         else if (g_tile_variant >= 12 && g_tile_variant < 25 && wk_ok(gb, count)) {
           GemmBatch gw = gb;  // (split-K scratch kept: launch_wk splits only under 256 tiles)

@@ -9,7 +9,21 @@ VARIANTS=${VARIANTS:-""}
 R=$(pwd)
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest $TESTS -m gpu -v -s --timeout 300 --timeout-method thread -p no:cacheprovider \
-  > gpurun_out/tests_$TAG.log 2>&1 || { grep -E "FAILED|Error|assert" gpurun_out/tests_$TAG.log | head -30; tail -30 gpurun_out/tests_$TAG.log; exit 1; }
+  > gpurun_out/tests_$TAG.log 2>&1
+rc=$?
+if [ $rc -ne 0 ]; then
+  grep -E "FAILED|Error|assert" gpurun_out/tests_$TAG.log | head -30; tail -30 gpurun_out/tests_$TAG.log
+  # assertion failures only (pytest rc 1): localise with the single-knob-off variants; anything else ends the call
+  if [ $rc -eq 1 ] && [ -n "$BISECT" ]; then
+    for v in $BISECT; do
+      DREAMER_LIB_VARIANT=$v timeout -k 10 300 python -u -m pytest "$BISECT_TEST" -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/bisect_${TAG}_$v.log 2>&1
+      brc=$?
+      echo "bisect $v: rc $brc $(tail -1 gpurun_out/bisect_${TAG}_$v.log)"
+      [ $brc -gt 1 ] && exit 1
+    done
+  fi
+  exit 1
+fi
 grep -E "PASSED|FAILED|passed|failed|flip|guarded|NATURAL" gpurun_out/tests_$TAG.log | cut -c1-400 | head -60
 timeout -k 10 300 python bench.py --no-secondary --wm-steps 0 --no-cpu-baseline > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -30 gpurun_out/bench_$TAG.err; exit 1; }
 cut -c1-200 gpurun_out/bench_$TAG.json
