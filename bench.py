@@ -524,6 +524,14 @@ def main():
                                         "achieved": round(ach, 2), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                                         "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4),
                                         "encoder_ms": round(enc_b * 1e3, 4)}}
+                if tag == "north_star_B256" and args.wm_steps > 0:
+                    # WorldModel.training_step in bf16 mode: the convolutions (encoder, decoder, their data and
+                    # weight gradients) as one-term bf16 implicit GEMMs (tests/test_gpu_wm.py states the bounds)
+                    wb_s, wb_gpu_s, wb_loss = bench_wm(db, bb, args.wm_steps, 2)
+                    wb_s, wb_gpu_s = max_over_ranks(wb_s), max_over_ranks(wb_gpu_s)
+                    bf[tag]["wm_step"] = {"value": round(world * bb / wb_s, 1), "unit": "sequences/s",
+                                          "ms_per_step": round(wb_s * 1e3, 3),
+                                          "gpu_ms_per_step": round(wb_gpu_s * 1e3, 3), "loss": wb_loss, "T": H}
                 del db
             bf["note"] = ("Dreamer(config with precision='bf16'): conv1+conv2 fused from the u8 ring, conv3/conv4 "
                           "and the projection as bf16 implicit GEMMs (f32 accumulate); the imagination / update "
@@ -552,7 +560,9 @@ def main():
             del dc
         c3["note"] = ("BASELINE configs[3] (128x128 frames, deeper VAE, S=64, H=20; global B=256 on 8 GPUs = 32 per "
                       "GPU): Dreamer.train_Agent() AC_epochs=1 with encoder_depth=5 (one more k4 s2 conv each way, "
-                      "the framework's definition: the reference has no deeper VAE); fp32 parity mode")
+                      "the framework's definition: the reference has no deeper VAE); fp32 mode")
+        c3["parity"] = ("unpinned against the reference (framework-defined architecture): checked only against the "
+                        "oracle's restatement of the same definition (tests/test_gpu_deep_vae.py)")
         secondary["configs3_deep_vae_128px_H20"] = c3
         # BASELINE configs[4]: vector observations, B = 4096 H = 15 (S = 64 assumed)
         _, dv = make_vector_dreamer(CAR_RACER, dev, 4096, 64, 15, world, rank, group)
@@ -563,7 +573,9 @@ def main():
             "ms_per_epoch": round(elv / kv * 1e3, 4), "dtype": "f32", "obs_dim": VEC_OBS_DIM,
             "losses": {"actor": lav, "critic": lcv},
             "note": "BASELINE configs[4] (B=4096/GPU, H=15, S=64): observation_dims=[24], MLP encoder instead of "
-                    "the conv stack (no reference counterpart), Dreamer.train_Agent() AC_epochs=1"}
+                    "the conv stack (no reference counterpart), Dreamer.train_Agent() AC_epochs=1",
+            "parity": "unpinned against the reference (framework-defined MLP encoder): checked only against the "
+                      "oracle's restatement (tests/test_gpu_vector.py)"}
         del dv
     wm = None
     if args.wm_steps > 0:

@@ -40,9 +40,12 @@ int op_conv_s1_bf16(int n, int cin, int ih, int iw, int cout, const void* in, co
 int op_conv_split3(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
                    float* out, int out_nchw, hipStream_t s);
 // with the world-model step's epilogues (as op_conv_nhwc_ex): CONV_EPI_FWD +
-// optional pre = acc + bias (NHWC), or CONV_EPI_DSILU: out = acc * SiLU'(pre)
+// optional pre = acc + bias (NHWC), or CONV_EPI_DSILU: out = acc * SiLU'(pre).
+// terms = 1: the bf16 world-model step's form (activations RNE-rounded to one
+// bf16 term as they are staged, the weights' first plane = their RNE bf16, one
+// MFMA per block; f32 in / out and the same epilogues)
 int op_conv_split3_ex(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
-                      float* out, int out_nchw, float* pre, int epi, hipStream_t s);
+                      float* out, int out_nchw, float* pre, int epi, hipStream_t s, int terms = 3);
 
 // tall NT products f32-accurate on the bf16 MFMA (conv_split.hip):
 // Y = act(A W^T + bias), A [M][K] row-major with an optional second K segment
@@ -79,7 +82,7 @@ int op_enc12_split3(int n, int nb, int h, int w, int c1, int c2, const dr_frames
 // neither): conv1's pre-activation and output, conv2's pre-activation
 int op_enc12_split3_ex(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
                        const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, float* out,
-                       float* pre0, float* a0, float* pre1, hipStream_t s);
+                       float* pre0, float* a0, float* pre1, hipStream_t s, int terms = 3);
 int op_enc12_bf16(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const void* wr1, const float* b1,
                   const void* wr2, const float* b2, void* out, hipStream_t s);
 // k4 s2 p1 conv + bias + SiLU, bf16 NHWC in -> bf16 NHWC (or NCHW) out
@@ -126,8 +129,10 @@ int op_convT_out3(const ConvTArgs& a, hipStream_t s);
 // split) for CT_EPI_BIAS / CT_EPI_DSILU, NHWC out with ldc == cout, no silu_in;
 // wr = op_convT_repack_split3(wt) scratch, 6 bytes per weight
 int op_convT_repack_split3(int cin, int cout, const float* wt, void* wr, hipStream_t s);
-bool op_convT_split3_supported(int n, int cin, int h, int w, int cout);
-int op_convT_split3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s);
+// terms = 1: the bf16 world-model step's one-term form (as op_conv_split3_ex),
+// which also covers cout = 32
+bool op_convT_split3_supported(int n, int cin, int h, int w, int cout, int terms = 3);
+int op_convT_split3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s, int terms = 3);
 
 // Weight gradient of a k4 s2 p1 (transposed) convolution:
 //   dW[a][b][ky][kx] (+)= scale * sum_{f,y,x} lo[f][y][x][a] * hi[f][2y-1+ky][2x-1+kx][b]
@@ -144,8 +149,10 @@ int op_wgrad_reduce(int ca, int cb, int cbo, int nsplit, const float* part, floa
 // powers of two, lo without SiLU on load
 bool op_wgrad_split3_supported(int n, int h, int w, int ca, int cb);
 size_t op_wgrad_split3_ws_floats(int n, int h, int w, int ca, int cb);
+// terms = 1: both operands RNE-rounded to one bf16 term (bf16 world-model step)
 int op_wgrad_split3(int n, int h, int w, int ca, int cb, const float* lo, int lda, const float* hi, int ldb,
-                    float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s);
+                    float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s,
+                    int terms = 3);
 // dW has cbo <= cb channels per row (cbo < cb when hi carries zero padding channels).
 int op_conv_wgrad(int n, int h, int w, int ca, int cb, const float* lo, int lda, int lo_silu, const float* hi, int ldb,
                   float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s);

@@ -64,6 +64,8 @@ __device__ __forceinline__ u32x2 pack_bf16x4(f32x4 v) {
   const bf16x4_t b = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
   return __builtin_bit_cast(u32x2, b);
 }
+// two f32 -> two bf16 (RNE), x0 in the low half (split3_pair's packing)
+__device__ __forceinline__ unsigned pack_bf16x2(float x0, float x1) { return b16bits((__bf16)x0) | (b16bits((__bf16)x1) << 16); }
 }  // namespace
 
 // EPI (conv.h): CONV_EPI_FWD: out = SiLU(acc + bias), optionally pre = acc + bias
@@ -73,13 +75,16 @@ __device__ __forceinline__ u32x2 pack_bf16x4(f32x4 v) {
 // NT3 = 1: the bf16 perf mode's form of the same tile -- bf16 NHWC activations
 // staged as they are (one plane), the weights' first split plane (= their RNE
 // bf16), one MFMA per block, bf16 output (RNE after bias + SiLU); `in` / `out`
-// then point at u16 data
-template <int BM, int BN, int CIN, bool OUT_NCHW, int PIPE, int EPI = CONV_EPI_FWD, int NT3 = 3>
+// then point at u16 data.  NT3 = 1 with IO16 = false: the bf16 world-model
+// step's form -- f32 activations rounded (RNE) to one bf16 plane as they are
+// staged, f32 outputs and every epilogue of the three-term form
+template <int BM, int BN, int CIN, bool OUT_NCHW, int PIPE, int EPI = CONV_EPI_FWD, int NT3 = 3, bool IO16 = (NT3 == 1)>
 __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, int iw, int cout,
                                                          const float* __restrict__ in, const u16* __restrict__ wr,
                                                          const float* __restrict__ bias, float* __restrict__ out,
                                                          float* __restrict__ pre) {
-  static_assert(NT3 == 3 || (NT3 == 1 && EPI == CONV_EPI_FWD), "conv_split3 terms");
+  static_assert(NT3 == 3 || (NT3 == 1 && (EPI == CONV_EPI_FWD || !IO16)), "conv_split3 terms");
+  static_assert(!IO16 || NT3 == 1, "bf16 storage is the one-term form's");
   const u16* __restrict__ in16 = reinterpret_cast<const u16*>(in);
   u16* __restrict__ out16 = reinterpret_cast<u16*>(out);
   constexpr int NT = BM * 2;         // WM = BM / 64 waves over pixels x 2 waves over channels
@@ -147,7 +152,7 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
       // LDS store: a conditional load compiled to a branch that waited for
       // each load before issuing the next
       const bool ok = (vm[i] >> ky) & (vm[i] >> (4 + kx)) & 1u;
-      if constexpr (NT3 == 1) rh[i] = *reinterpret_cast<const u32x2*>(in16 + (ok ? pb[i] + toff : 0));
+      if constexpr (IO16) rh[i] = *reinterpret_cast<const u32x2*>(in16 + (ok ? pb[i] + toff : 0));
       else ra[i] = *reinterpret_cast<const f32x4*>(in + (ok ? pb[i] + toff : 0));
       om |= ok ? (1u << i) : 0u;
     }
@@ -170,8 +175,11 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
     for (int i = 0; i < APT; ++i) {
       const int row = prow + (NT / 8) * i;
       const int unit = (quad >> 1) ^ swz(row), half = quad & 1;
-      if constexpr (NT3 == 1) {
+      if constexpr (IO16) {
         reinterpret_cast<u32x2*>(&As[buf][0][row][unit])[half] = (okm >> i) & 1u ? rh[i] : (u32x2){0u, 0u};
+      } else if constexpr (NT3 == 1) {
+        const f32x4 v = (okm >> i) & 1u ? ra[i] : (f32x4){0.f, 0.f, 0.f, 0.f};
+        reinterpret_cast<u32x2*>(&As[buf][0][row][unit])[half] = pack_bf16x4(v);
       } else {
         const f32x4 v = (okm >> i) & 1u ? ra[i] : (f32x4){0.f, 0.f, 0.f, 0.f};
         unsigned h0, m0_, l0, h1, m1, l1;
@@ -259,7 +267,7 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
         if (m >= M) continue;
         const float bv = bias[co];
         f32x4 v = acc[i][j] + bv;
-        if constexpr (NT3 == 1) {
+        if constexpr (IO16) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(v[e]);
           const long long f = m / hw;
@@ -291,7 +299,7 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(v[e]);
         }
-        if constexpr (NT3 == 1) {
+        if constexpr (IO16) {
           *reinterpret_cast<u32x2*>(out16 + m * cout + co) = pack_bf16x4(v);
           continue;
         }
@@ -380,13 +388,15 @@ static constexpr size_t e12_lds_bytes(int terms = 3) {
 #ifndef DR_E12S1_OCC
 #define DR_E12S1_OCC 2  // A/B knob: min waves per SIMD of the one-term form
 #endif
-template <int NW, int NTM = 3>
+// O16 = false with NTM = 1: the bf16 world-model step's form -- one term, f32
+// output and the saves
+template <int NW, int NTM = 3, bool O16 = (NTM == 1)>
 __global__ __launch_bounds__(64 * NW, NTM == 1 ? DR_E12S1_OCC : 1) void k_enc12_split3(int n, int nb, dr_frames src, const u16* __restrict__ wr1,
                                                           const float* __restrict__ b1, const u16* __restrict__ wr2,
                                                           const float* __restrict__ b2, float* __restrict__ out,
                                                           float* __restrict__ pre0, float* __restrict__ a0,
                                                           float* __restrict__ pre1) {
-  static_assert((NW == 4 || NW == 8) && (NTM == 1 || NTM == 3), "enc12 waves / terms");
+  static_assert((NW == 4 || NW == 8) && (NTM == 1 || NTM == 3) && (!O16 || NTM == 1), "enc12 waves / terms");
   constexpr int NTH = 64 * NW, TAPS = NW == 8 ? 8 : 16;
   constexpr int R2 = E12_R2, R1 = E12_R1, RI = E12_RI, PS = E12_PS, LWI = E12_LWI;
   constexpr int OW1 = 32, OW2 = 16, W = 64, H = 64, C1 = 32, C2 = 64;
@@ -495,7 +505,7 @@ __global__ __launch_bounds__(64 * NW, NTM == 1 ? DR_E12S1_OCC : 1) void k_enc12_
           }
         }
         // lane: pixel p, channels 16 j + 4 q .. + 3
-        const bool own = NTM == 3 && pre0 && yl >= 1 && yl <= 2 * R2;  // this tile's own conv1 rows
+        const bool own = !O16 && pre0 && yl >= 1 && yl <= 2 * R2;  // this tile's own conv1 rows
         const long long o1 = (((long long)f * (H / 2) + y1) * OW1 + x1) * C1;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -609,7 +619,7 @@ __global__ __launch_bounds__(64 * NW, NTM == 1 ? DR_E12S1_OCC : 1) void k_enc12_
         const f32x4 pv = acc[i][jj] + bv;
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(pv[e]);
-        if constexpr (NTM == 1) {
+        if constexpr (O16) {
           *reinterpret_cast<u32x2*>(reinterpret_cast<u16*>(out) + (o - out) + co) = pack_bf16x4(v);
           continue;
         }
@@ -644,8 +654,9 @@ int op_enc12_split3(int n, int nb, int h, int w, int c1, int c2, const dr_frames
 
 int op_enc12_split3_ex(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
                        const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, float* out,
-                       float* pre0, float* a0, float* pre1, hipStream_t s) {
-  if ((pre0 != nullptr) != (a0 != nullptr) || ((uintptr_t)pre0 | (uintptr_t)a0 | (uintptr_t)pre1) & 15)
+                       float* pre0, float* a0, float* pre1, hipStream_t s, int terms) {
+  if ((pre0 != nullptr) != (a0 != nullptr) || ((uintptr_t)pre0 | (uintptr_t)a0 | (uintptr_t)pre1) & 15 ||
+      (terms != 1 && terms != 3))
     return DR_E_INVALID;
   if (c1 != 32 || c2 != 64 || h != 64 || w != 64 || !src->ring || !src->starts || src->ring_cap <= 0 || n <= 0 ||
       (long long)n * 2 >= (1LL << 31))
@@ -661,6 +672,24 @@ int op_enc12_split3_ex(int n, int nb, int h, int w, int c1, int c2, const dr_fra
   hipLaunchKernelGGL(k_conv1_repack_split3, dim3((c1 * 64 + 255) / 256), dim3(256), 0, s, c1, w1, (u16*)wr1);
   DR_TRY(dr_check_launch("conv1_repack_split3"));
   DR_TRY(op_conv_repack_split3(c2, c1, w2, wr2, s));
+  if (terms == 1) {  // one term, f32 out + saves: the one-term form's occupancy (op_enc12_s1_bf16)
+    static int slots1[64];
+    int dev = 0;
+    DR_TRY_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return DR_E_INVALID;
+    auto kf = k_enc12_split3<DR_E12S1_WAVES, 1, false>;
+    if (slots1[dev] == 0) {
+      (void)hipFuncSetAttribute((const void*)kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e12_lds_bytes(1));
+      int cus = 0, per = 0;
+      DR_TRY_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      DR_TRY_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kf, 64 * DR_E12S1_WAVES, e12_lds_bytes(1)));
+      slots1[dev] = std::max(1, per) * std::max(1, cus);
+    }
+    const int grid = std::min(n * 2, slots1[dev]);
+    hipLaunchKernelGGL(kf, dim3((unsigned)grid), dim3(64 * DR_E12S1_WAVES), e12_lds_bytes(1), s, n, nb, *src,
+                       (const u16*)wr1, b1, (const u16*)wr2, b2, out, pre0, a0, pre1);
+    return dr_check_launch("enc12_split3 (one term)");
+  }
   // persistent: one workgroup per CU (the LDS allows no second), each walks
   // tiles blockIdx.x, + gridDim.x, ... so that its next tile's input loads
   // run under the current tile's conv2
@@ -712,7 +741,7 @@ int op_enc12_s1_bf16(int n, int nb, int h, int w, int c1, int c2, const dr_frame
   return dr_check_launch("enc12_s1_bf16");
 }
 
-template <int BM, int BN, int CIN, bool NCHW, int PIPE, int EPI = CONV_EPI_FWD>
+template <int BM, int BN, int CIN, bool NCHW, int PIPE, int EPI = CONV_EPI_FWD, int TERMS = 3>
 static int launch_s3(int n, int ih, int iw, int cout, const float* in, const void* wr, const float* bias, float* out,
                      float* pre, hipStream_t s) {
   const long long M = (long long)n * (ih / 2) * (iw / 2);
@@ -721,7 +750,7 @@ static int launch_s3(int n, int ih, int iw, int cout, const float* in, const voi
     dr_set_error("conv_split3: too many tiles");
     return DR_E_INVALID;
   }
-  hipLaunchKernelGGL((k_conv_split3<BM, BN, CIN, NCHW, PIPE, EPI>), dim3((unsigned)dr_xcd_grid((int)tiles)),
+  hipLaunchKernelGGL((k_conv_split3<BM, BN, CIN, NCHW, PIPE, EPI, TERMS, false>), dim3((unsigned)dr_xcd_grid((int)tiles)),
                      dim3(BM * 2), 0, s, n, ih, iw, cout, in, (const u16*)wr, bias, out, pre);
   return dr_check_launch("conv_split3");
 }
@@ -733,8 +762,8 @@ bool op_conv_split3_supported(int n, int cin, int ih, int iw, int cout) {
 }
 
 int op_conv_split3_ex(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
-                      float* out, int out_nchw, float* pre, int epi, hipStream_t s) {
-  if (!op_conv_split3_supported(n, cin, ih, iw, cout)) {
+                      float* out, int out_nchw, float* pre, int epi, hipStream_t s, int terms) {
+  if (!op_conv_split3_supported(n, cin, ih, iw, cout) || (terms != 1 && terms != 3)) {
     dr_set_error("conv_split3: unsupported shape (cin=%d ih=%d iw=%d cout=%d)", cin, ih, iw, cout);
     return DR_E_INVALID;
   }
@@ -746,21 +775,28 @@ int op_conv_split3_ex(int n, int cin, int ih, int iw, int cout, const float* in,
   // for 64 output channels (980 us; 128 x 64 at two workgroups per CU: 1004),
   // 256 x 128 for 128 / 256 channels (709 / 658 us; 128 x 128: ~1.1 ms): the
   // weights are re-read once per pixel tile, so taller tiles pay
-#define DR_S3E(BN, C, NCHW)                                                                                   \
-  (epi == CONV_EPI_DSILU ? launch_s3<256, BN, C, NCHW, 2, CONV_EPI_DSILU>(n, ih, iw, cout, in, wr, bias, out, pre, s) \
-                         : launch_s3<256, BN, C, NCHW, 2, CONV_EPI_FWD>(n, ih, iw, cout, in, wr, bias, out, pre, s))
-#define DR_S3L(C)                                                                                          \
-  if (cin == C) {                                                                                          \
-    if (cout % 128 == 0)                                                                                   \
-      return out_nchw ? launch_s3<256, 128, C, true, 2>(n, ih, iw, cout, in, wr, bias, out, pre, s)       \
-                      : DR_S3E(128, C, false);                                                             \
-    return out_nchw ? launch_s3<256, 64, C, true, 2>(n, ih, iw, cout, in, wr, bias, out, pre, s)          \
-                    : DR_S3E(64, C, false);                                                                \
+#define DR_S3E(BN, C, NCHW, T)                                                                                         \
+  (epi == CONV_EPI_DSILU ? launch_s3<256, BN, C, NCHW, 2, CONV_EPI_DSILU, T>(n, ih, iw, cout, in, wr, bias, out, pre, s) \
+                         : launch_s3<256, BN, C, NCHW, 2, CONV_EPI_FWD, T>(n, ih, iw, cout, in, wr, bias, out, pre, s))
+#define DR_S3L(C, T)                                                                                                 \
+  if (cin == C) {                                                                                                    \
+    if (cout % 128 == 0)                                                                                             \
+      return out_nchw ? launch_s3<256, 128, C, true, 2, CONV_EPI_FWD, T>(n, ih, iw, cout, in, wr, bias, out, pre, s) \
+                      : DR_S3E(128, C, false, T);                                                                    \
+    return out_nchw ? launch_s3<256, 64, C, true, 2, CONV_EPI_FWD, T>(n, ih, iw, cout, in, wr, bias, out, pre, s)    \
+                    : DR_S3E(64, C, false, T);                                                                       \
   }
-  DR_S3L(32)
-  DR_S3L(64)
-  DR_S3L(128)
-  DR_S3L(256)
+  if (terms == 1) {
+    DR_S3L(32, 1)
+    DR_S3L(64, 1)
+    DR_S3L(128, 1)
+    DR_S3L(256, 1)
+  } else {
+    DR_S3L(32, 3)
+    DR_S3L(64, 3)
+    DR_S3L(128, 3)
+    DR_S3L(256, 3)
+  }
 #undef DR_S3L
 #undef DR_S3E
   return DR_E_INVALID;
@@ -821,20 +857,23 @@ int op_conv_s1_bf16(int n, int cin, int ih, int iw, int cout, const void* in, co
 // v_perm packing, swizzled 64-byte plane rows), weights split once per call
 // into [class][K/32][3 planes][cout][32].  Epilogues of the world-model step
 // (NHWC out, ldc == cout): CT_EPI_BIAS (out = acc + bias, out2 / silu_out =
-// SiLU) and CT_EPI_DSILU (out = acc * SiLU'(pre)).
+// SiLU) and CT_EPI_DSILU (out = acc * SiLU'(pre)).  TERMS = 1: the bf16
+// world-model step's form (activations RNE-rounded to one bf16 plane while
+// staged, weight plane 0, one MFMA per block).
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int CIN, int EPI>
+template <int BM, int BN, int CIN, int EPI, int TERMS = 3>
 __global__ __launch_bounds__(BM * 2) void k_convT_split3(ConvTArgs a, const u16* __restrict__ wr) {
   constexpr int NT = BM * 2;
   constexpr int K = CIN * 4;
   constexpr int NCH = K / 32;
   constexpr int WTN = BN / 2, FM = 4, FN = WTN / 16;
   constexpr int APT = BM * 8 / NT;
-  constexpr int BU = 3 * BN * 4;
+  constexpr int BU = TERMS * BN * 4;
   constexpr int BPT = (BU + NT - 1) / NT;
-  static_assert(CIN % 32 == 0 && APT == 4 && FN >= 1 && NCH % 2 == 0, "convT_split3 tile");
-  __shared__ __attribute__((aligned(16))) u32x4 As[2][3][BM][4];
-  __shared__ __attribute__((aligned(16))) u32x4 Bs[2][3][BN][4];
+  static_assert(CIN % 32 == 0 && APT == 4 && FN >= 1 && NCH % 2 == 0 && (TERMS == 1 || TERMS == 3),
+                "convT_split3 tile");
+  __shared__ __attribute__((aligned(16))) u32x4 As[2][TERMS][BM][4];
+  __shared__ __attribute__((aligned(16))) u32x4 Bs[2][TERMS][BN][4];
 
   const int h = a.h, w = a.w, hw = h * w, cout = a.cout;
   const long long M = (long long)a.n * hw;  // input-resolution pixels of one parity class
@@ -905,13 +944,17 @@ __global__ __launch_bounds__(BM * 2) void k_convT_split3(ConvTArgs a, const u16*
     for (int i = 0; i < APT; ++i) {
       const int row = prow + (NT / 8) * i;
       const f32x4 v = (okm >> i) & 1u ? ra[i] : (f32x4){0.f, 0.f, 0.f, 0.f};
-      unsigned h0, m0_, l0, h1, m1, l1;
-      split3_pair(v[0], v[1], h0, m0_, l0);
-      split3_pair(v[2], v[3], h1, m1, l1);
       const int unit = (quad >> 1) ^ swz(row), half = quad & 1;
-      reinterpret_cast<u32x2*>(&As[buf][0][row][unit])[half] = (u32x2){h0, h1};
-      reinterpret_cast<u32x2*>(&As[buf][1][row][unit])[half] = (u32x2){m0_, m1};
-      reinterpret_cast<u32x2*>(&As[buf][2][row][unit])[half] = (u32x2){l0, l1};
+      if constexpr (TERMS == 1) {
+        reinterpret_cast<u32x2*>(&As[buf][0][row][unit])[half] = pack_bf16x4(v);
+      } else {
+        unsigned h0, m0_, l0, h1, m1, l1;
+        split3_pair(v[0], v[1], h0, m0_, l0);
+        split3_pair(v[2], v[3], h1, m1, l1);
+        reinterpret_cast<u32x2*>(&As[buf][0][row][unit])[half] = (u32x2){h0, h1};
+        reinterpret_cast<u32x2*>(&As[buf][1][row][unit])[half] = (u32x2){m0_, m1};
+        reinterpret_cast<u32x2*>(&As[buf][2][row][unit])[half] = (u32x2){l0, l1};
+      }
     }
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
@@ -942,9 +985,9 @@ __global__ __launch_bounds__(BM * 2) void k_convT_split3(ConvTArgs a, const u16*
     using Next = std::integral_constant<int, 1 - SL>;
     const int buf = c & 1;
     load(min(c + 2, NCH - 1), slot);
-    u32x4 av[3][FM], bv[3][FN];
+    u32x4 av[TERMS][FM], bv[TERMS][FN];
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) {
+    for (int pl = 0; pl < TERMS; ++pl) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) av[pl][i] = As[buf][pl][wm0 + 16 * i + r][fu];
 #pragma unroll
@@ -954,11 +997,13 @@ __global__ __launch_bounds__(BM * 2) void k_convT_split3(ConvTArgs a, const u16*
 #define DR_T3(PA, PB)                                                                                   \
   _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
       mfma_b16(bv[PB][j], av[PA][i], acc[i][j]);
-    DR_T3(2, 0)
-    DR_T3(1, 1)
-    DR_T3(0, 2)
-    DR_T3(1, 0)
-    DR_T3(0, 1)
+    if constexpr (TERMS == 3) {
+      DR_T3(2, 0)
+      DR_T3(1, 1)
+      DR_T3(0, 2)
+      DR_T3(1, 0)
+      DR_T3(0, 1)
+    }
     DR_T3(0, 0)
 #undef DR_T3
     if (c + 1 < NCH) store(Next{}, buf ^ 1);
@@ -1027,33 +1072,40 @@ int op_convT_repack_split3(int cin, int cout, const float* wt, void* wr, hipStre
 // cout >= 64: at 32 output channels the 256 x 32 tile's split of the staged
 // activations outweighs its 24 MFMAs per wave and chunk (975 / 887 us against
 // 991 / 900 us on the f32 MFMA, WM step B = 256 T = 15, profiles/r03i_wm_step_kernels.txt)
-bool op_convT_split3_supported(int n, int cin, int h, int w, int cout) {
+// (one term: the split's cost is gone, so cout = 32 takes the 256 x 32 tile)
+bool op_convT_split3_supported(int n, int cin, int h, int w, int cout, int terms) {
   const bool cin_ok = cin == 32 || cin == 64 || cin == 128 || cin == 256;
-  return cin_ok && cout % 64 == 0 && (long long)n * h * w * cin < (1LL << 31) - (1LL << 20) &&
+  return cin_ok && (terms == 1 || terms == 3) && cout % (terms == 1 ? 32 : 64) == 0 && cout > 0 &&
+         (long long)n * h * w * cin < (1LL << 31) - (1LL << 20) &&
          4LL * (((long long)n * h * w + 255) / 256) * (cout / 32) < (1LL << 30);
 }
 
-template <int BN, int C, int EPI>
+template <int BN, int C, int EPI, int T>
 static int launch_t3(const ConvTArgs& a, const void* wr, hipStream_t s) {
   const long long tiles = 4 * (((long long)a.n * a.h * a.w + 255) / 256) * (a.cout / BN);
-  hipLaunchKernelGGL((k_convT_split3<256, BN, C, EPI>), dim3((unsigned)dr_xcd_grid((int)tiles)), dim3(512), 0, s, a,
-                     (const u16*)wr);
+  hipLaunchKernelGGL((k_convT_split3<256, BN, C, EPI, T>), dim3((unsigned)dr_xcd_grid((int)tiles)), dim3(512), 0, s,
+                     a, (const u16*)wr);
   return dr_check_launch("convT_split3");
 }
 
-int op_convT_split3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s) {
-  if (!op_convT_split3_supported(a.n, a.cin, a.h, a.w, a.cout) || a.silu_in || a.ldc != a.cout ||
+int op_convT_split3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s, int terms) {
+  if (!op_convT_split3_supported(a.n, a.cin, a.h, a.w, a.cout, terms) || a.silu_in || a.ldc != a.cout ||
       (epi != CT_EPI_BIAS && epi != CT_EPI_DSILU) || (epi == CT_EPI_DSILU && !a.pre) ||
       (epi == CT_EPI_BIAS && !a.bias)) {
     dr_set_error("convT_split3: unsupported problem (cin=%d cout=%d h=%d w=%d epi=%d)", a.cin, a.cout, a.h, a.w, epi);
     return DR_E_INVALID;
   }
-#define DR_T3E(BN, C) \
-  (epi == CT_EPI_DSILU ? launch_t3<BN, C, CT_EPI_DSILU>(a, wr, s) : launch_t3<BN, C, CT_EPI_BIAS>(a, wr, s))
-#define DR_T3L(C)                                         \
-  if (a.cin == C) {                                       \
-    if (a.cout % 128 == 0) return DR_T3E(128, C);         \
-    return DR_T3E(64, C);                                 \
+#define DR_T3E(BN, C, T) \
+  (epi == CT_EPI_DSILU ? launch_t3<BN, C, CT_EPI_DSILU, T>(a, wr, s) : launch_t3<BN, C, CT_EPI_BIAS, T>(a, wr, s))
+#define DR_T3L(C)                                                                          \
+  if (a.cin == C) {                                                                        \
+    if (terms == 1) {                                                                      \
+      if (a.cout % 128 == 0) return DR_T3E(128, C, 1);                                     \
+      if (a.cout % 64 == 0) return DR_T3E(64, C, 1);                                       \
+      return DR_T3E(32, C, 1);                                                             \
+    }                                                                                      \
+    if (a.cout % 128 == 0) return DR_T3E(128, C, 3);                                       \
+    return DR_T3E(64, C, 3);                                                               \
   }
   DR_T3L(32)
   DR_T3L(64)
@@ -1078,14 +1130,16 @@ int op_convT_split3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s) 
 // 2 (a) x 4 (n), partial planes per pixel split reduced by k_wgrad_reduce.
 // Low-resolution sizes are powers of two (shift addressing).
 // ---------------------------------------------------------------------------
-template <int BM>
+// TERMS = 1: both operands RNE-rounded to one bf16 plane (bf16 world-model step)
+template <int BM, int TERMS = 3>
 __global__ __launch_bounds__(512) void k_wgrad_split3(int n, int lh, int lw, int ca, int cb,
                                                       const float* __restrict__ lo, int lda,
                                                       const float* __restrict__ hi, int ldb, int chunk,
                                                       float* __restrict__ part) {
   constexpr int BN = 128, KC = 64, RP = KC / 8 + 1;
   constexpr int FM = BM / 32, FN = 2;  // wave tile (BM / 2) x 32
-  __shared__ __attribute__((aligned(16))) u32x4 S[3][BM + BN][RP];
+  static_assert(TERMS == 1 || TERMS == 3, "wgrad_split3 terms");
+  __shared__ __attribute__((aligned(16))) u32x4 S[TERMS][BM + BN][RP];
   const int N = 16 * cb;
   const int tiles_n = N / BN, tiles = (ca / BM) * tiles_n;
   const int split = blockIdx.x / tiles, lt = blockIdx.x - split * tiles;
@@ -1128,18 +1182,25 @@ __global__ __launch_bounds__(512) void k_wgrad_split3(int n, int lh, int lw, int
     if (!active) return;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      u32x4 ph, pm, pl;
+      if constexpr (TERMS == 1) {
+        u32x4 ph;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        unsigned hh, mm, ll;
-        split3_pair(v[2 * i][c], v[2 * i + 1][c], hh, mm, ll);
-        ph[i] = hh;
-        pm[i] = mm;
-        pl[i] = ll;
+        for (int i = 0; i < 4; ++i) ph[i] = pack_bf16x2(v[2 * i][c], v[2 * i + 1][c]);
+        S[0][row0 + c][oct] = ph;
+      } else {
+        u32x4 ph, pm, pl;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          unsigned hh, mm, ll;
+          split3_pair(v[2 * i][c], v[2 * i + 1][c], hh, mm, ll);
+          ph[i] = hh;
+          pm[i] = mm;
+          pl[i] = ll;
+        }
+        S[0][row0 + c][oct] = ph;
+        S[1][row0 + c][oct] = pm;
+        S[2][row0 + c][oct] = pl;
       }
-      S[0][row0 + c][oct] = ph;
-      S[1][row0 + c][oct] = pm;
-      S[2][row0 + c][oct] = pl;
     }
   };
 
@@ -1159,9 +1220,9 @@ __global__ __launch_bounds__(512) void k_wgrad_split3(int n, int lh, int lw, int
       load(k_begin + (c + 1 < nch ? c + 1 : c) * KC + 8 * oct);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        u32x4 av[3][FM], bv[3][FN];
+        u32x4 av[TERMS][FM], bv[TERMS][FN];
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
+        for (int pl = 0; pl < TERMS; ++pl) {
 #pragma unroll
           for (int i = 0; i < FM; ++i) av[pl][i] = S[pl][wm0 + 16 * i + r][4 * ks + q];
 #pragma unroll
@@ -1170,11 +1231,13 @@ __global__ __launch_bounds__(512) void k_wgrad_split3(int n, int lh, int lw, int
 #define DR_W3(PA, PB)                                                                                   \
   _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
       mfma_b16(av[PA][i], bv[PB][j], acc[i][j]);
-        DR_W3(2, 0)
-        DR_W3(1, 1)
-        DR_W3(0, 2)
-        DR_W3(1, 0)
-        DR_W3(0, 1)
+        if constexpr (TERMS == 3) {
+          DR_W3(2, 0)
+          DR_W3(1, 1)
+          DR_W3(0, 2)
+          DR_W3(1, 0)
+          DR_W3(0, 1)
+        }
         DR_W3(0, 0)
 #undef DR_W3
       }
@@ -1226,8 +1289,9 @@ size_t op_wgrad_split3_ws_floats(int n, int h, int w, int ca, int cb) {
 }
 
 int op_wgrad_split3(int n, int h, int w, int ca, int cb, const float* lo, int lda, const float* hi, int ldb,
-                    float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s) {
-  if (!op_wgrad_split3_supported(n, h, w, ca, cb) || lda % 4 || ldb % 4 || lda < ca || ldb < cb || cbo < 1 ||
+                    float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s,
+                    int terms) {
+  if (!op_wgrad_split3_supported(n, h, w, ca, cb) || (terms != 1 && terms != 3) || lda % 4 || ldb % 4 || lda < ca || ldb < cb || cbo < 1 ||
       cbo > cb || !lo || !hi || !dw || ((uintptr_t)lo & 15) || ((uintptr_t)hi & 15)) {
     dr_set_error("wgrad_split3: unsupported problem (ca=%d cb=%d h=%d w=%d)", ca, cb, h, w);
     return DR_E_INVALID;
@@ -1241,12 +1305,17 @@ int op_wgrad_split3(int n, int h, int w, int ca, int cb, const float* lo, int ld
   const int bm = ca >= 128 ? 128 : 64;
   const int tiles = (ca / bm) * (16 * cb / 128);
   const int lh = ilog2_exact(h), lw = ilog2_exact(w);
-  if (bm == 128)
-    hipLaunchKernelGGL(k_wgrad_split3<128>, dim3((unsigned)(tiles * ns)), dim3(512), 0, s, n, lh, lw, ca, cb, lo, lda,
-                       hi, ldb, ch, ws);
-  else
-    hipLaunchKernelGGL(k_wgrad_split3<64>, dim3((unsigned)(tiles * ns)), dim3(512), 0, s, n, lh, lw, ca, cb, lo, lda,
-                       hi, ldb, ch, ws);
+#define DR_W3L(BM, T)                                                                                             \
+  hipLaunchKernelGGL((k_wgrad_split3<BM, T>), dim3((unsigned)(tiles * ns)), dim3(512), 0, s, n, lh, lw, ca, cb, lo, \
+                     lda, hi, ldb, ch, ws)
+  if (terms == 1) {
+    if (bm == 128) DR_W3L(128, 1);
+    else DR_W3L(64, 1);
+  } else {
+    if (bm == 128) DR_W3L(128, 3);
+    else DR_W3L(64, 3);
+  }
+#undef DR_W3L
   DR_TRY(dr_check_launch("wgrad_split3"));
   return op_wgrad_reduce(ca, cb, cbo, ns, ws, dw, scale, accumulate, s);
 }

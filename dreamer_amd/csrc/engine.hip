@@ -5,6 +5,9 @@
 #include "engine_util.h"
 #include "chain.h"
 
+#ifndef DR_GATES_BLOCKED
+#define DR_GATES_BLOCKED 0  // A/B knob: 1 = unit-blocked W_ih copy for k_gru_gates_lds (r04d: 552.6k vs 560.1k with k_gru_gates)
+#endif
 #ifndef DR_B16_CHAIN_WKS
 #define DR_B16_CHAIN_WKS 1  // A/B knob: bf16 mode's per-step grouped products on bf16 weight planes
 #endif
@@ -15,7 +18,7 @@
 #define DR_ACTOR_TAIL_BWD 1  // A/B knob: 0 = head backward + two LN-backward launches + the fused product
 #endif
 #ifndef DR_ACTOR_TAIL
-#define DR_ACTOR_TAIL 1  // A/B knob (tools/build_variant.py): 0 = z-gather + two skinny launches
+#define DR_ACTOR_TAIL 0  // A/B knob (tools/build_variant.py): 0 = z-gather + two skinny launches
 #endif
 
 // fp32 mode, tall batches: the first Linear of a head over [h | z] on the
@@ -216,8 +219,10 @@ struct ObsWs {
   float *gi, *gh, *pre1, *logits, *wt, *hb[2];
   int* idx;
   void *s3m0, *s3whh;  // bf16 planes of latent_mapper.0's h-columns and W_hh (k_gemm_wks3)
+  float* wtb;          // W_ih in unit blocks (k_gru_gates_lds)
 };
 static void obs_carve(Carve& c, const dr_dims* d, int B, ObsWs& w) {
+  w.wtb = c.f((long long)(latent(d) + d->action) * 3 * d->hidden);
   w.s3m0 = c.raw(op_nt_split3_ws_bytes(d->enc_hidden, d->hidden));
   w.s3whh = c.raw(op_nt_split3_ws_bytes(3 * d->hidden, d->hidden));
   w.gi = c.f((long long)B * 3 * d->hidden);
@@ -258,6 +263,7 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
   if (any_gru) {
     DR_REQUIRE(wm->w_ih && wm->w_hh && wm->b_ih && wm->b_hh, "GRU weights required");
     DR_TRY(op_transpose(3 * Hd, L + d->action, wm->w_ih, w.wt, s));
+    if (DR_GATES_BLOCKED && B >= 128 && Hd % 4 == 0) DR_TRY(op_wih_block(Hd, L + d->action, wm->w_ih, w.wtb, s));
   }
   const bool planes = B >= 128 && T > 1 && Hd % 8 == 0;
   if (planes) {
@@ -281,7 +287,8 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
       float* hn = w.hb[hb];
       hb ^= 1;
       DR_TRY(gru_onehot(d, wm, B, w.idx, actions + ai * act_st, act_sb, h, Hd, hn, Hd, w.wt, nullptr,
-                        nullptr, nullptr, nullptr, s, z_out, L, w.gh, gh_pre));
+                        nullptr, nullptr, nullptr, s, z_out, L, w.gh, gh_pre,
+                        DR_GATES_BLOCKED && B >= 128 && Hd % 4 == 0 ? w.wtb : nullptr));
       h = hn;
     }
     // latent_mapper.0 on cat(features, h): feature part precomputed in feat[t]
@@ -348,6 +355,7 @@ extern "C" size_t dr_imagine_tape_bytes(const dr_dims* d, int B, int H) {
 struct ImWs {
   float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog, *rval, *wt, *wst, *bst;  // forward scratch
   float *tl0f, *hpart;  // forward: actor Linear 0 transposed ([Hd+L][a1]), its h-part + bias [B][a1]
+  float* wtb;           // forward: W_ih in unit blocks (k_gru_gates_lds)
   void *s3r, *s3c;  // split3 weight planes of the reward / continue heads' first Linear
   void *s3p0, *s3a0, *s3whh, *s3wt, *s3twhh;  // bf16 planes of the per-step chain weights (k_gemm_wks3)
   float* s3part;    // their split-K partial sums
@@ -386,6 +394,7 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.s3part_n = op_gemm_nt_split3_part_floats((int)B1, std::max(d->rew_h1, d->cont_h1));
   w.s3part = c.f((long long)w.s3part_n);
   w.wt = c.f((long long)(L + A) * 3 * Hd);
+  w.wtb = c.f((long long)(L + A) * 3 * Hd);
   w.tl0f = c.f((long long)(Hd + L) * d->actor_h1);
   w.hpart = c.f(Bl * d->actor_h1);
   w.wst = c.f((long long)2 * A * d->actor_h2);
@@ -469,6 +478,7 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
   {
     TransposeJob tj[2] = {{3 * Hd, L + A, 3 * Hd, wm->w_ih, w.wt}, {a1, Hd + L, a1, ac->l0.w, w.tl0f}};
     DR_TRY(op_transpose_multi(tj, zg ? 2 : 1, s));
+    if (DR_GATES_BLOCKED && split_gru && Hd % 4 == 0) DR_TRY(op_wih_block(Hd, L + A, wm->w_ih, w.wtb, s));
   }
   DR_TRY(op_onehot_index(B, d->rows, d->cols, latents, ldL, w.idx[0], onehot_vals(w.idx[0], B, d->rows), s));
 
@@ -528,7 +538,8 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
     float* z_n = latents + (long long)(t + 1) * L;
     // WorldModel.imagine_step (WorldModel.py:72-77)
     DR_TRY(gru_onehot(d, wm, B, w.idx[t & 1], actions + (long long)t * A, ldA, h_t, ldH, h_n, ldH, w.wt,
-                      tp.r + hb, tp.u + hb, tp.n + hb, tp.ghn + hb, s, z_t, ldL, w.gh, split_gru && t > 0));
+                      tp.r + hb, tp.u + hb, tp.n + hb, tp.ghn + hb, s, z_t, ldL, w.gh, split_gru && t > 0,
+                      DR_GATES_BLOCKED && split_gru && Hd % 4 == 0 ? w.wtb : nullptr));
     float* p1 = tp.pre1p + (long long)t * B * d->prior_h1;
     float* p2 = tp.pre2p + (long long)t * B * d->prior_h2;
     {

@@ -271,8 +271,11 @@ static inline int stack_heads(const dr_actor* ac, int A, int in, float* w, float
 // where idx always comes from the sampler)
 static inline int gru_onehot(const dr_dims* d, const dr_world_model* wm, int B, int* idx, const float* a, long long lda, const float* h, long long ldh, float* hout,
                       long long ldo, const float* wt, float* sr, float* su, float* sn, float* sghn, hipStream_t s,
-                      const float* z = nullptr, long long ldz = 0, float* gh_ws = nullptr, int gh_ready = 0) {
+                      const float* z = nullptr, long long ldz = 0, float* gh_ws = nullptr, int gh_ready = 0,
+                      const float* wtb = nullptr) {
   GruArgs g;
+  memset(&g, 0, sizeof(g));
+  g.wtb = wtb;
   g.gh_ws = gh_ws;
   g.gh_ready = gh_ready;
   g.z = z; g.ldz = ldz;

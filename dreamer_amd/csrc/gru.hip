@@ -516,16 +516,15 @@ __global__ __launch_bounds__(GL_NT) void k_gru_gates_lds(GruArgs ga) {
   const int tid = threadIdx.x, ml = tid >> 1, hh = tid & 1;
   const int m = m0 + ml, jj = j0 + 2 * hh;
   const bool live = m < B;
-  const unsigned ldw = 3u * (unsigned)Hd;
-  // every global load of the workgroup, issued together: the W_ih^T slice ...
-  const float* wt = dr_uni(g.wt);
+  // every global load of the workgroup, issued together: the W_ih^T slice (one
+  // contiguous 49 KB block of the unit-blocked copy: float4 x = (row x / 3, gate x % 3)) ...
   const int nw4 = (L + A) * 3;
+  const float* wtb = dr_uni(g.wtb) + (long long)tj * nw4 * 4;
   float4 wv[GL_WMAX];
 #pragma unroll
   for (int i = 0; i < GL_WMAX; ++i) {
     const int x = tid + GL_NT * i;
-    const int r = x / 3, t = x - 3 * (x / 3);
-    wv[i] = dr_ld4(wt, x < nw4 ? (unsigned)r * ldw + (unsigned)(t * Hd + j0) : 0u);
+    wv[i] = dr_ld4(wtb, x < nw4 ? 4u * (unsigned)x : 0u);
   }
   // ... and this thread's row: indices / values of the R groups, actions, gh, h, b_ih
   int iv[GRU_MAXR];
@@ -644,7 +643,7 @@ __global__ __launch_bounds__(GL_NT) void k_gru_gates_lds(GruArgs ga) {
 
 static bool gates_lds_ok(const GruArgs& g) {
   const int L = g.R * g.C;
-  return g.Hd % GL_UNITS == 0 && g.R % 4 == 0 && (L + g.A) * 3 <= GL_WMAX * GL_NT && g.ldo % 2 == 0 &&
+  return g.wtb && ((uintptr_t)g.wtb & 15) == 0 && g.Hd % GL_UNITS == 0 && g.R % 4 == 0 && (L + g.A) * 3 <= GL_WMAX * GL_NT && g.ldo % 2 == 0 &&
          (!g.h || g.ldh % 2 == 0) && (g.lda >= g.A) && gates_lds_bytes(L, g.A) <= 64 * 1024 &&
          (((uintptr_t)g.idx | (uintptr_t)g.zval) & 15) == 0 &&
          (((uintptr_t)g.gh_ws | (uintptr_t)g.h | (uintptr_t)g.hout | (uintptr_t)g.b_ih | (uintptr_t)g.b_hh) & 7) == 0;
@@ -653,6 +652,28 @@ static bool gates_lds_ok(const GruArgs& g) {
 #ifndef DR_GATES_LDS
 #define DR_GATES_LDS 1  // A/B knob (tools/build_variant.py): 0 = k_gru_gates
 #endif
+
+__global__ void k_wih_block(int Hd, int LA, const float* __restrict__ w_ih, float* __restrict__ wtb) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // output element
+  const long long n = (long long)Hd * LA * 3;
+  if (i >= n) return;
+  const int u = (int)(i & 3);
+  const long long rest = i >> 2;  // (tj, r, gate)
+  const int t = (int)(rest % 3);
+  const long long rr = rest / 3;
+  const int r = (int)(rr % LA), tj = (int)(rr / LA);
+  wtb[i] = w_ih[(long long)(t * Hd + 4 * tj + u) * LA + r];
+}
+
+int op_wih_block(int Hd, int LA, const float* w_ih, float* wtb, hipStream_t s) {
+  if (Hd % 4 || LA <= 0) {
+    dr_set_error("wih_block: Hd %% 4 == 0 required");
+    return DR_E_INVALID;
+  }
+  const long long n = (long long)Hd * LA * 3;
+  hipLaunchKernelGGL(k_wih_block, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, Hd, LA, w_ih, wtb);
+  return dr_check_launch("wih_block");
+}
 
 #ifdef DR_PHASE_TIMING  // microbenchmark knob (tools/kbench), not in the product library
 static int g_gates_batch = 8;

@@ -327,6 +327,9 @@ struct WmDims {
   int e[DR_MAX_DEPTH + 1], cd[DR_MAX_DEPTH + 1];  // encoder / decoder channels (engine_util.h enc_chans / dec_chans)
   long long pix[DR_MAX_DEPTH + 1];              // pixels per frame at resolution level k: (IH >> k) (IW >> k)
   int Dv;  // vector observations (dr_dims.obs_dim): MLP encoder / decoder, no conv planes
+  // bf16 operand terms of the split-conv kernels: 3 = f32-accurate (parity
+  // mode), 1 = bf16 perf mode (dr_dims.precision)
+  int terms;
 };
 static WmDims wm_dims(const dr_dims* d, int B, int T) {
   WmDims w;
@@ -342,6 +345,7 @@ static WmDims wm_dims(const dr_dims* d, int B, int T) {
   w.d1 = d->dec_f1; w.d2 = d->dec_f2; w.C0 = 4 * d->dec_f2; w.dh = d->dec_hidden; w.Fd = w.C0 * w.Pf;
   w.ph1 = d->prior_h1; w.ph2 = d->prior_h2; w.rh1 = d->rew_h1; w.rh2 = d->rew_h2; w.ch1 = d->cont_h1; w.ch2 = d->cont_h2;
   w.Dv = d->obs_dim > 0 ? d->obs_dim : 0;
+  w.terms = d->precision == DR_PREC_BF16 ? 1 : 3;
   if (w.Dv) {  // widths of the MLP stand-ins (include/dreamer_hip.h, dr_dims.obs_dim)
     w.IH = w.IW = 0;
     w.Pf = 1;
@@ -371,10 +375,12 @@ static inline bool dec_s3(const WmDims& D, int k) {
 // the last, 3-channel layer runs k_convT_out3) and encoder conv k >= 1's data
 // gradient (an upsampling conv from e[k + 1] to e[k] channels)
 static inline bool dect_s3(const WmDims& D, int k) {
-  return !D.Dv && k < D.N - 1 && op_convT_split3_supported(D.M1, D.cd[k], D.IH >> (D.N - k), D.IW >> (D.N - k), D.cd[k + 1]);
+  return !D.Dv && k < D.N - 1 &&
+         op_convT_split3_supported(D.M1, D.cd[k], D.IH >> (D.N - k), D.IW >> (D.N - k), D.cd[k + 1], D.terms);
 }
 static inline bool encg_s3(const WmDims& D, int k) {
-  return !D.Dv && k >= 1 && op_convT_split3_supported(D.M, D.e[k + 1], D.IH >> (k + 1), D.IW >> (k + 1), D.e[k]);
+  return !D.Dv && k >= 1 &&
+         op_convT_split3_supported(D.M, D.e[k + 1], D.IH >> (k + 1), D.IW >> (k + 1), D.e[k], D.terms);
 }
 
 // conv / convT weight gradient: f32-accurate split3 kernel where the shape
@@ -385,9 +391,9 @@ static size_t wgrad_ws_floats(int n, int h, int w, int ca, int cb) {
   return f;
 }
 static int wgrad(int n, int h, int w, int ca, int cb, const float* lo, int lda, const float* hi, int ldb, float* dw,
-                 int cbo, float* ws, size_t ws_floats, hipStream_t s) {
+                 int cbo, float* ws, size_t ws_floats, hipStream_t s, int terms) {
   if (op_wgrad_split3_supported(n, h, w, ca, cb))
-    return op_wgrad_split3(n, h, w, ca, cb, lo, lda, hi, ldb, dw, cbo, 1.0f, 0, ws, ws_floats, s);
+    return op_wgrad_split3(n, h, w, ca, cb, lo, lda, hi, ldb, dw, cbo, 1.0f, 0, ws, ws_floats, s, terms);
   return op_conv_wgrad(n, h, w, ca, cb, lo, lda, 0, hi, ldb, dw, cbo, 1.0f, 0, ws, ws_floats, s);
 }
 
@@ -667,14 +673,14 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     // other failure (a launch or occupancy query) is returned
     const int rc12 = op_enc12_split3_ex(M, B, IH, IW, D.e[1], D.e[2], src, wm->conv[0].w, wm->conv[0].b,
                                         wm->conv[1].w, wm->conv[1].b, w.e12w1, w.s3e[1], w.a[1], w.pre[0], w.a[0],
-                                        w.pre[1], s);
+                                        w.pre[1], s, D.terms);
     if (rc12 == DR_OK) k0 = 2;
     else if (rc12 != DR_E_INVALID) return rc12;
   }
   for (int k = k0; k < N; ++k) {
     if (w.s3e[k])
       DR_TRY(op_conv_split3_ex(M, D.e[k], IH >> k, IW >> k, D.e[k + 1], w.a[k - 1], w.s3e[k], wm->conv[k].b, w.a[k],
-                               k == N - 1 ? 1 : 0, w.pre[k], CONV_EPI_FWD, s));
+                               k == N - 1 ? 1 : 0, w.pre[k], CONV_EPI_FWD, s, D.terms));
     else
       DR_TRY(op_conv_nhwc_ex(M, enc_cin_st(D, k), IH >> k, IW >> k, D.e[k + 1], k ? w.a[k - 1] : w.x0, w.wr[k],
                              wm->conv[k].b, w.a[k], k == N - 1 ? 1 : 0, w.pre[k], CONV_EPI_FWD, s));
@@ -774,7 +780,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
       a.in = k ? w.dqp[k - 1] : w.du2p; a.silu_in = 0; a.wq = w.wqd[k]; a.bias = dec->convt[k].b;
       if (k < N - 1) {
         a.out = w.dq[k]; a.out2 = w.dqp[k]; a.ldc = cout_t[k];
-        if (w.t3d[k]) DR_TRY(op_convT_split3(CT_EPI_BIAS, a, w.t3d[k], s));
+        if (w.t3d[k]) DR_TRY(op_convT_split3(CT_EPI_BIAS, a, w.t3d[k], s, D.terms));
         else DR_TRY(op_convT_nhwc(CT_EPI_BIAS, a, s));
       } else {
         // Tanh + squared error against frames t >= 1 (WorldModel.py:129); writes dL/d(pre-tanh)
@@ -864,12 +870,12 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
       const float* gout = k < N - 1 ? w.dgq[k] : w.dgout;  // dL/d(convT k's output pre-activation)
       if (w.s3d[k])
         DR_TRY(op_conv_split3_ex(M1, co_st, ih, iw, cin_t[k], gout, w.s3d[k], nullptr, gin, 0, const_cast<float*>(pre),
-                                 CONV_EPI_DSILU, s));
+                                 CONV_EPI_DSILU, s, D.terms));
       else
         DR_TRY(op_conv_nhwc_ex(M1, co_st, ih, iw, cin_t[k], gout, w.wrd[k], nullptr, gin, 0, const_cast<float*>(pre),
                                CONV_EPI_DSILU, s));
       DR_TRY(wgrad(M1, ih / 2, iw / 2, cin_t[k], co_st, post, cin_t[k], gout, co_st, gd->convt[k].w, co, w.cws, w.cws_n,
-                   s));
+                   s, D.terms));
       DR_TRY(op_chan_sum((long long)M1 * ih * iw, co, gout, co_st, gd->convt[k].b, 0, w.cws, w.cws_n, s));
     }
   }
@@ -974,13 +980,13 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
       const int oh = IH >> (k + 1), ow = IW >> (k + 1);
       const int cin = enc_cin_st(D, k), cout = D.e[k + 1];
       const float* hi = k ? w.a[k - 1] : w.x0;  // conv k's input
-      DR_TRY(wgrad(M, oh, ow, cout, cin, w.gp[k], cout, hi, cin, gw->conv[k].w, D.e[k], w.cws, w.cws_n, s));
+      DR_TRY(wgrad(M, oh, ow, cout, cin, w.gp[k], cout, hi, cin, gw->conv[k].w, D.e[k], w.cws, w.cws_n, s, D.terms));
       DR_TRY(op_chan_sum((long long)M * oh * ow, cout, w.gp[k], cout, gw->conv[k].b, 0, w.cws, w.cws_n, s));
       if (k > 0) {
         ConvTArgs a = {};
         a.n = M; a.cin = cout; a.h = oh; a.w = ow; a.cout = cin;
         a.in = w.gp[k]; a.wq = w.wqe[k]; a.out = w.gp[k - 1]; a.ldc = cin; a.pre = w.pre[k - 1];
-        if (w.t3e[k]) DR_TRY(op_convT_split3(CT_EPI_DSILU, a, w.t3e[k], s));
+        if (w.t3e[k]) DR_TRY(op_convT_split3(CT_EPI_DSILU, a, w.t3e[k], s, D.terms));
         else DR_TRY(op_convT_nhwc(CT_EPI_DSILU, a, s));
       }
     }
