@@ -125,6 +125,9 @@ _SIGS = {
     "dr_nonfinite": (_i, [_ll, fp, fp, fp]),
     "dr_replay_gather": (_i, [_ll, _i, _i, _i, _i, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp]),
     "dr_rng_advance": (_i, [fp, C.c_ulonglong, fp]),
+    "dr_stream_create_cumask": (_i, [_i, _P(C.c_uint), _P(fp)]),
+    "dr_stream_destroy": (_i, [fp]),
+    "dr_device_cus": (_i, [_P(_i)]),
     "dr_wm_train_workspace_bytes": (_sz, [_P(dr_dims), _i, _i]),
     "dr_decoder_workspace_bytes": (_sz, [_P(dr_dims), _i]),
     "dr_decoder_fwd": (_i, [_P(dr_dims), _P(dr_decoder), _i, fp, _ll, fp, _ll, fp, fp, _sz, fp]),

@@ -1830,9 +1830,11 @@ __device__ __forceinline__ unsigned wk_pack_rne(float x0, float x1) {
   return __builtin_bit_cast(unsigned, v);
 }
 
-template <int NTP, int D>
-__global__ __launch_bounds__(256) void k_gemm_wks3(GemmBatch gb, int npack) {
-  constexpr int NW = 4, FM = 2, FN = 2, NTH = 256, NT4 = FM * FN * 256;
+// FULL: D >= every wave's chunk count -- all of a wave's fragments are loaded
+// up front (one memory latency per tile instead of one per D chunks), no refill
+template <int NTP, int D, int NW = 4, bool FULL = false>
+__global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) {
+  constexpr int FM = 2, FN = 2, NTH = 64 * NW, NT4 = FM * FN * 256;
   __shared__ GemmArgs s_args;
   __shared__ __attribute__((aligned(16))) float red[NW][FM * FN * 4][64];
   int z = 0;
@@ -1936,7 +1938,8 @@ __global__ __launch_bounds__(256) void k_gemm_wks3(GemmBatch gb, int npack) {
       }
       DR_WK3(0, 0)
 #undef DR_WK3
-      load(min(c + D, clast), u);  // unconditional: a load under a branch is waited for at once
+      // unconditional: a load under a branch is waited for at once
+      if constexpr (!FULL) load(min(c + D, clast), u);
     }
   }
   // partial tiles meet in LDS; element (t, e, l) of tile t = (i, j): row 16 i + (l & 15), column 16 j + 4 (l >> 4) + e
@@ -1963,7 +1966,12 @@ __global__ __launch_bounds__(256) void k_gemm_wks3(GemmBatch gb, int npack) {
 }
 
 __global__ __launch_bounds__(256) void k_splitk_finish(GemmBatch gb, int splits) {
-  const GemmArgs& g = gb.p[blockIdx.z];
+  // the problem's arguments staged in LDS: read straight from the by-value
+  // batch at a run-time index, the 624-byte GemmArgs was copied to scratch
+  // per thread (2.6 KB per lane, ~370 us per WM-step finish, r04g)
+  __shared__ GemmArgs s_args;
+  dr_stage_args(gb.p[blockIdx.z], s_args, threadIdx.x);
+  const GemmArgs& g = s_args;
   const long long MN = (long long)g.M * g.N;
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= MN) return;
@@ -2485,17 +2493,43 @@ static bool wks3_ok(const GemmBatch& gb, int count) {
   }
   return true;
 }
+#ifndef DR_WKS3_NW
+#define DR_WKS3_NW 4  // A/B knob: waves per 32 x 32 tile (each runs its own k-chunks)
+#endif
+#ifndef DR_WKS3_FULL
+#define DR_WKS3_FULL 0  // A/B knob: 1 = whole-wave prefetch when a wave has <= 5 k-chunks
+#endif
 static void launch_wks3(const GemmBatch& gb, int count, hipStream_t s, bool bf16) {
-  int tot = 0, maxt = 0;
+  int tot = 0, maxt = 0, nkc = 0;
   for (int i = 0; i < count; ++i) {
     const int t = dr_cdiv(gb.p[i].M, 32) * dr_cdiv(gb.p[i].N, 32);
     tot += t;
     maxt = std::max(maxt, t);
+    nkc = std::max(nkc, dr_cdiv(gb.p[i].K, 32));
   }
   const int npack = count > 1 ? count : 0;
   const dim3 grid(dr_xcd_grid(npack ? tot : maxt));
-  if (bf16) hipLaunchKernelGGL((k_gemm_wks3<1, 2>), grid, dim3(256), 0, s, gb, npack);
-  else hipLaunchKernelGGL((k_gemm_wks3<3, 2>), grid, dim3(256), 0, s, gb, npack);
+  constexpr int NW = DR_WKS3_NW;
+  const int per = dr_cdiv(nkc, NW);  // chunks of the busiest wave
+#define DR_WKS3_L(T, D, F) hipLaunchKernelGGL((k_gemm_wks3<T, D, NW, F>), grid, dim3(64 * NW), 0, s, gb, npack)
+  if (DR_WKS3_FULL && per <= 5) {
+    if (bf16) {
+      if (per <= 2) DR_WKS3_L(1, 2, true);
+      else if (per == 3) DR_WKS3_L(1, 3, true);
+      else if (per == 4) DR_WKS3_L(1, 4, true);
+      else DR_WKS3_L(1, 5, true);
+    } else {
+      if (per <= 2) DR_WKS3_L(3, 2, true);
+      else if (per == 3) DR_WKS3_L(3, 3, true);
+      else if (per == 4) DR_WKS3_L(3, 4, true);
+      else DR_WKS3_L(3, 5, true);
+    }
+  } else if (bf16) {
+    DR_WKS3_L(1, 2, false);
+  } else {
+    DR_WKS3_L(3, 2, false);
+  }
+#undef DR_WKS3_L
 }
 
 // split-K over workgroups only when the tile grid is under one workgroup per

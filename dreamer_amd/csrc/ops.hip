@@ -1353,6 +1353,29 @@ extern "C" int dr_rng_advance(unsigned long long* rng, unsigned long long delta,
   return dr_check_launch("rng_advance");
 }
 
+// CU-masked streams (include/dreamer_hip.h): the warm stream of the pipelined
+// epochs (engine.py run_many)
+extern "C" int dr_stream_create_cumask(int n_words, const unsigned* mask, hipStream_t* out) {
+  DR_REQUIRE(n_words > 0 && n_words <= 64 && mask && out, "cu mask: 1..64 words and an output slot required");
+  unsigned any = 0;
+  for (int i = 0; i < n_words; ++i) any |= mask[i];
+  DR_REQUIRE(any != 0, "cu mask: no CU selected");
+  DR_TRY_HIP(hipExtStreamCreateWithCUMask(out, (uint32_t)n_words, mask));
+  return DR_OK;
+}
+extern "C" int dr_stream_destroy(hipStream_t s) {
+  DR_REQUIRE(s != nullptr, "null stream");
+  DR_TRY_HIP(hipStreamDestroy(s));
+  return DR_OK;
+}
+extern "C" int dr_device_cus(int* out) {
+  DR_REQUIRE(out, "null output");
+  int dev = 0;
+  DR_TRY_HIP(hipGetDevice(&dev));
+  DR_TRY_HIP(hipDeviceGetAttribute(out, hipDeviceAttributeMultiprocessorCount, dev));
+  return DR_OK;
+}
+
 // ---------------------------------------------------------------------------
 // vector observations (BASELINE configs[4]): gather the window rows of the
 // f32 ring (Buffer.sample_sequences for D-float observations) time-major

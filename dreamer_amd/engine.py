@@ -363,11 +363,35 @@ class ImaginationEngine:
     # epoch e.  The results are those of the sequential epochs bit for bit:
     # the warm start keeps its own copy of the Philox state, advanced once per
     # epoch like the main one, and (z0, h0) are double-buffered.
+    def warm_stream(self, cu_fraction=None):
+        """The stream of the pipelined warm start: a plain torch stream, or with
+        cu_fraction in (0, 1) a HIP stream restricted to that share of the CUs
+        (dr_stream_create_cumask) so that the imagination / update chain keeps
+        CUs of its own.  DREAMER_WARM_CUS sets the default fraction."""
+        import ctypes
+        import os
+        if cu_fraction is None:
+            cu_fraction = float(os.environ.get("DREAMER_WARM_CUS", "1"))
+        if not 0.0 < cu_fraction < 1.0:
+            return torch.cuda.Stream(self.dev)
+        n = ctypes.c_int(0)
+        with torch.cuda.device(self.dev):
+            L.call("dr_device_cus", ctypes.byref(n))
+            keep = max(1, min(n.value, int(round(n.value * cu_fraction))))
+            words = (n.value + 31) // 32
+            mask = (ctypes.c_uint * words)()
+            for i in range(keep):
+                mask[i // 32] |= 1 << (i % 32)
+            h = ctypes.c_void_p()
+            L.call("dr_stream_create_cumask", words, mask, ctypes.byref(h))
+        self._masked_streams = getattr(self, "_masked_streams", []) + [h]
+        return torch.cuda.ExternalStream(h.value, device=self.dev)
+
     def _pipe_capture(self, key):
         dev, B, H = self.dev, self.B, self.H
         if getattr(self, "_pipe", None) is None:
             self._pipe = dict(
-                stream=torch.cuda.Stream(dev), side=torch.cuda.Stream(dev),
+                stream=self.warm_stream(), side=torch.cuda.Stream(dev),
                 rng=torch.zeros(2, dtype=torch.int64, device=dev),
                 z0=[self.z0, torch.zeros_like(self.z0)],
                 h0=[self.h0, torch.zeros_like(self.h0)],
@@ -412,12 +436,29 @@ class ImaginationEngine:
     def run_many(self, starts_list):
         """len(starts_list) consecutive train_Agent epochs, pipelined (see
         above).  Returns a [K, 2] device tensor of (actor, critic) losses."""
-        K = len(starts_list)
         ag = self.dr.agent
         key = (ag.params_key(), self.dr.world_model.params_key(), self.dr.buffer.device_key())
         P = self._pipe_capture(key)
         G = P["graphs"]
-        main = torch.cuda.current_stream(self.dev)
+        outer = torch.cuda.current_stream(self.dev)
+        # DREAMER_CHAIN_PRIORITY (torch stream priority, -1 = high): the
+        # imagination / update chain on a stream of that priority, so that its
+        # latency-bound launches win CU slots over the warm start's convolutions
+        import os
+        prio = int(os.environ.get("DREAMER_CHAIN_PRIORITY", "0"))
+        if prio != 0:
+            if P.get("chain") is None or P.get("chain_prio") != prio:
+                P["chain"], P["chain_prio"] = torch.cuda.Stream(self.dev, priority=prio), prio
+            P["chain"].wait_stream(outer)
+            with torch.cuda.stream(P["chain"]):
+                losses = self._run_many(P, G, starts_list, P["chain"])
+            outer.wait_stream(P["chain"])
+            return losses
+        return self._run_many(P, G, starts_list, outer)
+
+    def _run_many(self, P, G, starts_list, main):
+        K = len(starts_list)
+        ag = self.dr.agent
         ws = P["stream"]
         host = torch.from_numpy(np.stack([np.asarray(x, dtype=np.int64) for x in starts_list])).pin_memory()
         losses = torch.empty(K, 2, device=self.dev)

@@ -131,6 +131,17 @@ typedef struct {
 const char* dr_last_error(void);
 int dr_version(void);
 
+/* A HIP stream whose kernels run only on the CUs set in mask (n_words 32-bit
+ * words, bit i = CU i of the device's CU-mask order; hipExtStreamCreateWithCUMask).
+ * The pipelined AC_epochs > 1 schedule (dreamer_amd/engine.py run_many) fences
+ * the next epoch's warm start (conv encoder + posterior scan) off part of the
+ * chip so that the latency-bound imagination / update chain keeps free CUs.
+ * No Dreamer.py counterpart: a scheduling aid of this implementation. */
+int dr_stream_create_cumask(int n_words, const unsigned* mask, hipStream_t* out);
+int dr_stream_destroy(hipStream_t s);
+/* the device's CU count (hipDeviceAttributeMultiprocessorCount) */
+int dr_device_cus(int* out);
+
 /* ---- a3  Encoder conv stack + latent_mapper.0 feature columns ---------------
  * feat[f][enc_hidden] = flatten(SiLU(conv4(...SiLU(conv1(frame f)))))
  *                       . map0.w[:, :F]^T + map0.b            (VAE.py:57-75)

@@ -204,13 +204,19 @@ def test_graph_replay_matches_eager(gpu):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("which", ["small", "full"])
-def test_pipelined_epochs_match_sequential(which, gpu):
+@pytest.mark.parametrize("which,sched", [("small", None), ("full", None), ("full", "0.875:-1")])
+def test_pipelined_epochs_match_sequential(which, sched, gpu, monkeypatch):
     """run_many (warm start of epoch e+1 on a second stream beside epoch e's
     actor-critic chain) == the same epochs run one after another, bit for
-    bit: losses of every epoch, actor / critic / target parameters, S."""
+    bit: losses of every epoch, actor / critic / target parameters, S.
+    sched "f:p": the warm stream restricted to a share f of the CUs
+    (dr_stream_create_cumask) and the chain on a stream of priority p."""
     from dreamer_amd.engine import ImaginationEngine
     from formula import replay_data
+    if sched:
+        frac, prio = sched.split(":")
+        monkeypatch.setenv("DREAMER_WARM_CUS", frac)
+        monkeypatch.setenv("DREAMER_CHAIN_PRIORITY", prio)
     fx = load_fixture("small_epoch")
     hw = (32, 32) if which == "small" else (64, 64)
     B, S, H, K = (8, 8, 5, 5) if which == "small" else (16, 16, 6, 4)

@@ -1,13 +1,16 @@
-"""Probe: AC_epochs = 2 with the pipelined epochs (engine.run_many) -- why the
-side-stream warm start of epoch e+1 gains so little beside epoch e's chain.
+"""Probe: AC_epochs = 2 with the pipelined epochs (engine.run_many) -- how much
+of the warm start of epoch e+1 hides beside epoch e's imagination / update.
 
-Times K-epoch runs of run_many against K sequential engine.run epochs at
-B = 256 under stream-priority settings of the warm stream and the main stream
-(torch stream priorities; lower number = higher priority), and reports the
-warm start's and the chain's own durations for reference.
+One case per process (streams and HW queues of earlier cases would otherwise
+share the device's few hardware queues and skew later ones):
 
-  python tools/pipe_probe.py [K]
-"""
+  python tools/pipe_probe.py K CASE
+
+CASE: "seq" (K sequential engine.run epochs), "pipe" (run_many as shipped),
+or "pipe:<warm CU fraction>:<chain priority>" -- the warm stream restricted
+to that share of the CUs (engine.warm_stream; 1 = no mask) and the chain on a
+stream of the given torch priority (0 = normal, -1 = high).  Prints one JSON
+line: ms per epoch (best of 3 timed K-epoch runs at B = 256)."""
 import json
 import os
 import sys
@@ -23,6 +26,12 @@ import bench  # noqa: E402
 
 def main():
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    case = sys.argv[2] if len(sys.argv) > 2 else "pipe"
+    parts = case.split(":")
+    if len(parts) > 1:
+        os.environ["DREAMER_WARM_CUS"] = parts[1]
+    if len(parts) > 2:
+        os.environ["DREAMER_CHAIN_PRIORITY"] = parts[2]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     B = 256
@@ -30,8 +39,6 @@ def main():
     eng = d._engine
     rng = np.random.RandomState(3)
     starts = [rng.randint(0, 4096 - 64, size=B) for _ in range(K)]
-    lo, hi = torch.cuda.Stream.priority_range()
-    res = {"priority_range": [lo, hi]}
 
     def timed(fn, reps=3):
         fn()
@@ -44,32 +51,19 @@ def main():
             best = min(best, time.perf_counter() - t0)
         return best * 1e3 / K
 
-    def seq():
-        for s in starts:
-            eng.run(s)
-
-    res["sequential_ms_per_epoch"] = round(timed(seq), 4)
-    # phases of one sequential epoch
-    eng.run(starts[0], timing=True)
-    torch.cuda.synchronize()
-    res["phase_ms"] = {k: round(v, 4) for k, v in eng.phase_ms().items()}
-    for name, wp, mp in (("default", None, None), ("warm_low", lo, None), ("warm_low_main_high", lo, hi),
-                         ("main_high", None, hi)):
-        eng._pipe = None  # recapture with fresh streams
-        orig = torch.cuda.Stream
-
-        def mk(device=None, priority=0, **kw):
-            return orig(device=device, priority=priority, **kw)
-        P = eng._pipe_capture((d.agent.params_key(), d.world_model.params_key(), d.buffer.device_key()))
-        if wp is not None:
-            P["stream"] = orig(device=dev, priority=wp)
-        main = orig(device=dev, priority=mp) if mp is not None else torch.cuda.current_stream(dev)
-
-        def pipe():
-            with torch.cuda.stream(main):
-                eng.run_many(starts)
-        res[f"pipelined_{name}_ms_per_epoch"] = round(timed(pipe), 4)
-        print(name, res[f"pipelined_{name}_ms_per_epoch"], flush=True)
+    res = {"case": case, "K": K}
+    if case == "seq":
+        def seq():
+            for s in starts:
+                eng.run(s)
+        res["ms_per_epoch"] = round(timed(seq), 4)
+        eng.run(starts[0], timing=True)
+        torch.cuda.synchronize()
+        res["phase_ms"] = {k: round(v, 4) for k, v in eng.phase_ms().items()}
+    else:
+        res["ms_per_epoch"] = round(timed(lambda: eng.run_many(starts)), 4)
+        res["warm_cus"] = os.environ.get("DREAMER_WARM_CUS")
+        res["chain_priority"] = os.environ.get("DREAMER_CHAIN_PRIORITY")
     print(json.dumps(res), flush=True)
 
 

@@ -15,7 +15,7 @@ from dreamer_amd import Dreamer  # noqa: E402
 def main(steps=int(os.environ.get("WM_STEPS", "6")), B=int(os.environ.get("WM_B", "64"))):
     dev = torch.device("cuda", 0)
     cfg = dict(bench.CAR_RACER)
-    cfg.update(batch_size=B)
+    cfg.update(batch_size=B, precision=os.environ.get("WM_PREC", "fp32"))
     torch.manual_seed(0)
     d = Dreamer(cfg, dev)
     fr, ac, rw, ct = bench.synthetic_replay(4096, cfg["observation_dims"], cfg["action_dims"], seed=0)
@@ -24,7 +24,7 @@ def main(steps=int(os.environ.get("WM_STEPS", "6")), B=int(os.environ.get("WM_B"
     s, g, loss = bench.bench_wm(d, B, steps, 2)
     fl = bench.wm_step_flops(cfg, B, cfg["horizon"])
     print(f"WM step B={B} T={cfg['horizon']}: {s * 1e3:.3f} ms wall, {g * 1e3:.3f} ms GPU, "
-          f"{fl / s / 1e12:.1f} TFLOP/s, loss {loss:.3f}")
+          f"{fl / s / 1e12:.1f} TFLOP/s, loss {loss:.3f}, precision {cfg['precision']}")
 
 
 if __name__ == "__main__":
