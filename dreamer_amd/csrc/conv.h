@@ -60,9 +60,11 @@ int op_gemm_nt_split3(int M, int N, int K, const float* A, int lda, const float*
 // the same with split-K partial sums in `part` (op_gemm_nt_split3_part_floats(M, N) floats,
 // 16-byte aligned) when the tile grid alone leaves the chip under-filled
 size_t op_gemm_nt_split3_part_floats(int M, int N);
+// splits_fixed > 0: that many K splits whatever M is (the sums then do not
+// depend on M: the time-chunked encoder equals the whole-window one bit for bit)
 int op_gemm_nt_split3_sk(int M, int N, int K, const float* A, int lda, const float* A2, int lda2, int ksA,
                          const void* wr, const float* bias, int act, float* Y, int ldy, float* part,
-                         size_t part_floats, hipStream_t s);
+                         size_t part_floats, hipStream_t s, int splits_fixed = 0);
 
 // ---- conv_bf16.hip (bf16 perf mode; activations bf16, accumulation f32) ----
 // weights: Conv2d [co][ci][4][4] f32 -> bf16 [co][tap][cin_pad]; matrix slice -> bf16 [rows][cols]
@@ -171,4 +173,4 @@ size_t op_gemm_tn_split3_ws_bytes(int M, int N, int K);
 bool op_gemm_tn_split3_supported(int M, int N, int K);
 int op_gemm_tn_split3(int M, int N, int K, const float* G, long long ldg, const float* X, long long ldx,
                       const float* X2, long long ldx2, int nsplitB, float* Y, long long ldy, int accumulate, void* ws,
-                      size_t ws_bytes, hipStream_t s);
+                      size_t ws_bytes, hipStream_t s, int terms = 3);  // terms = 1: RNE bf16 operands (bf16 WM step)

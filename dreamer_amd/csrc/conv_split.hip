@@ -1551,9 +1551,10 @@ int op_gemm_nt_split3(int M, int N, int K, const float* A, int lda, const float*
 
 int op_gemm_nt_split3_sk(int M, int N, int K, const float* A, int lda, const float* A2, int lda2, int ksA,
                          const void* wr, const float* bias, int act, float* Y, int ldy, float* part,
-                         size_t part_floats, hipStream_t s) {
+                         size_t part_floats, hipStream_t s, int splits_fixed) {
   if (!op_gemm_nt_split3_supported(M, N, K, A, lda, A2, lda2, ksA, ldy) || ((uintptr_t)Y & 15) ||
-      (bias && ((uintptr_t)bias & 15)) || ((uintptr_t)part & 15)) {
+      (bias && ((uintptr_t)bias & 15)) || ((uintptr_t)part & 15) || splits_fixed < 0 ||
+      splits_fixed > DR_S3_SPLITS || (splits_fixed > 1 && (!part || (size_t)splits_fixed * M * N > part_floats))) {
     dr_set_error("gemm_nt_split3: unsupported problem (M=%d N=%d K=%d)", M, N, K);
     return DR_E_INVALID;
   }
@@ -1568,6 +1569,7 @@ int op_gemm_nt_split3_sk(int M, int N, int K, const float* A, int lda, const flo
   // 64 x 64 tiles at 75 TF/s.
   const int nch = (K + 31) / 32;
   auto splits_for = [&](int bm, int bn) {
+    if (splits_fixed > 0) return splits_fixed;  // the caller's K partition (summation order independent of M)
     int sp = 1;
     while (part && sp < DR_S3_SPLITS && waves(bm, bn) * sp < 2048 && nch / (2 * sp) >= 8 &&
            (size_t)(2 * sp) * M * N <= part_floats)
@@ -1616,6 +1618,8 @@ static int s3_pad(int n) { return (n + 127) / 128 * 128; }
 
 // thread = (column n, 32-row chunk kc): 32 rows of one column (coalesced over
 // the threads of a row), split and written as three 64-byte plane runs
+// (TERMS = 1: plane 0 only, RNE -- the bf16 world-model step)
+template <int TERMS>
 __global__ __launch_bounds__(256) void k_kn_repack_split3(int K, int N, int P, const float* __restrict__ X, long long ldx,
                                                           const float* __restrict__ X2, long long ldx2, int nsplit,
                                                           u16* __restrict__ wr) {
@@ -1631,6 +1635,17 @@ __global__ __launch_bounds__(256) void k_kn_repack_split3(int K, int N, int P, c
     const int kk = 32 * kc + k;
     v[k] = (n < N && kk < K) ? src[(long long)kk * ld + nn] : 0.f;
   }
+  u32x4* o = reinterpret_cast<u32x4*>(wr + (((long long)kc * 3) * P + n) * 32);
+  if constexpr (TERMS == 1) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      u32x4 h;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) h[e] = pack_bf16x2(v[8 * u + 2 * e], v[8 * u + 2 * e + 1]);
+      o[u] = h;
+    }
+    return;
+  }
   u32x4 h[4], m[4], l[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u)
@@ -1642,7 +1657,6 @@ __global__ __launch_bounds__(256) void k_kn_repack_split3(int K, int N, int P, c
       m[u][e] = mm;
       l[u][e] = ll;
     }
-  u32x4* o = reinterpret_cast<u32x4*>(wr + (((long long)kc * 3) * P + n) * 32);
   const long long pl = (long long)P * 32 / 8;  // plane stride in u32x4 units
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -1661,15 +1675,15 @@ struct GemmPP {
   float* part;    // splits > 1: [splits][M][N] partial sums
 };
 
-template <int BM, int BN>
+template <int BM, int BN, int TERMS = 3>
 __global__ __launch_bounds__(BM * 2) void k_gemm_pp_split3(GemmPP g) {
   constexpr int NT = BM * 2;
   constexpr int WTN = BN / 2, FM = 4, FN = WTN / 16;
-  constexpr int AU = 3 * BM * 4, BU = 3 * BN * 4;
+  constexpr int AU = TERMS * BM * 4, BU = TERMS * BN * 4;
   constexpr int APT = (AU + NT - 1) / NT, BPT = (BU + NT - 1) / NT;
-  static_assert(FN >= 1 && BM % 64 == 0, "gemm_pp tile");
-  __shared__ __attribute__((aligned(16))) u32x4 As[2][3][BM][4];
-  __shared__ __attribute__((aligned(16))) u32x4 Bs[2][3][BN][4];
+  static_assert(FN >= 1 && BM % 64 == 0 && (TERMS == 1 || TERMS == 3), "gemm_pp tile");
+  __shared__ __attribute__((aligned(16))) u32x4 As[2][TERMS][BM][4];
+  __shared__ __attribute__((aligned(16))) u32x4 Bs[2][TERMS][BN][4];
   const int M = g.M, N = g.N, Mp = g.Mp, Np = g.Np;
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles = ((M + BM - 1) / BM) * tiles_n;
@@ -1740,9 +1754,9 @@ __global__ __launch_bounds__(BM * 2) void k_gemm_pp_split3(GemmPP g) {
       using Next = std::integral_constant<int, 1 - SL>;
       const int buf = (c - c0) & 1;
       load(min(c + 2, c1 - 1), slot);
-      u32x4 av[3][FM], bv[3][FN];
+      u32x4 av[TERMS][FM], bv[TERMS][FN];
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
+      for (int pl = 0; pl < TERMS; ++pl) {
 #pragma unroll
         for (int i = 0; i < FM; ++i) av[pl][i] = As[buf][pl][wm0 + 16 * i + r][fu];
 #pragma unroll
@@ -1751,11 +1765,13 @@ __global__ __launch_bounds__(BM * 2) void k_gemm_pp_split3(GemmPP g) {
 #define DR_P3(PA, PB)                                                                                   \
   _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
       mfma_b16(bv[PB][j], av[PA][i], acc[i][j]);
-      DR_P3(2, 0)
-      DR_P3(1, 1)
-      DR_P3(0, 2)
-      DR_P3(1, 0)
-      DR_P3(0, 1)
+      if constexpr (TERMS == 3) {
+        DR_P3(2, 0)
+        DR_P3(1, 1)
+        DR_P3(0, 2)
+        DR_P3(1, 0)
+        DR_P3(0, 1)
+      }
       DR_P3(0, 0)
 #undef DR_P3
       if (c + 1 < c1) store(Next{}, buf ^ 1);
@@ -1819,8 +1835,8 @@ extern "C" int dr_internal_tn_split3_supported(int M, int N, int K) { return op_
 
 int op_gemm_tn_split3(int M, int N, int K, const float* G, long long ldg, const float* X, long long ldx,
                       const float* X2, long long ldx2, int nsplitB, float* Y, long long ldy, int accumulate, void* ws,
-                      size_t ws_bytes, hipStream_t s) {
-  if (!op_gemm_tn_split3_supported(M, N, K) || !G || !X || !Y || (nsplitB < N && !X2) ||
+                      size_t ws_bytes, hipStream_t s, int terms) {
+  if (!op_gemm_tn_split3_supported(M, N, K) || !G || !X || !Y || (nsplitB < N && !X2) || (terms != 1 && terms != 3) ||
       ws_bytes < op_gemm_tn_split3_ws_bytes(M, N, K)) {
     dr_set_error("gemm_tn_split3: unsupported problem (M=%d N=%d K=%d) or workspace too small", M, N, K);
     return DR_E_INVALID;
@@ -1829,10 +1845,11 @@ int op_gemm_tn_split3(int M, int N, int K, const float* G, long long ldg, const 
   u16* wa = reinterpret_cast<u16*>(ws);
   u16* wb = wa + (size_t)KC * 32 * 3 * Mp;
   float* part = reinterpret_cast<float*>(((uintptr_t)(wb + (size_t)KC * 32 * 3 * Np) + 255) & ~(uintptr_t)255);
-  hipLaunchKernelGGL(k_kn_repack_split3, dim3((unsigned)((Mp + 255) / 256), (unsigned)KC), dim3(256), 0, s, K, M, Mp,
+  auto repack = terms == 1 ? k_kn_repack_split3<1> : k_kn_repack_split3<3>;
+  hipLaunchKernelGGL(repack, dim3((unsigned)((Mp + 255) / 256), (unsigned)KC), dim3(256), 0, s, K, M, Mp,
                      G, ldg, G, ldg, M, wa);
   DR_TRY(dr_check_launch("kn_repack_split3"));
-  hipLaunchKernelGGL(k_kn_repack_split3, dim3((unsigned)((Np + 255) / 256), (unsigned)KC), dim3(256), 0, s, K, N, Np,
+  hipLaunchKernelGGL(repack, dim3((unsigned)((Np + 255) / 256), (unsigned)KC), dim3(256), 0, s, K, N, Np,
                      X, ldx, X2 ? X2 : X, ldx2, nsplitB < N ? nsplitB : N, wb);
   DR_TRY(dr_check_launch("kn_repack_split3"));
   auto tl = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
@@ -1842,10 +1859,16 @@ int op_gemm_tn_split3(int M, int N, int K, const float* G, long long ldg, const 
   int splits = 1;
   while (splits < DR_PP_SPLITS && tiles * splits < 512 && KC / (2 * splits) >= 8) splits *= 2;
   GemmPP g = {M, N, K, Mp, Np, splits, accumulate, ldy, wa, wb, Y, part};
-  if (big)
+  if (terms == 1) {
+    if (big)
+      hipLaunchKernelGGL((k_gemm_pp_split3<128, 64, 1>), dim3(dr_xcd_grid(tiles), splits), dim3(256), 0, s, g);
+    else
+      hipLaunchKernelGGL((k_gemm_pp_split3<64, 64, 1>), dim3(dr_xcd_grid(tiles), splits), dim3(128), 0, s, g);
+  } else if (big) {
     hipLaunchKernelGGL((k_gemm_pp_split3<128, 64>), dim3(dr_xcd_grid(tiles), splits), dim3(256), 0, s, g);
-  else
+  } else {
     hipLaunchKernelGGL((k_gemm_pp_split3<64, 64>), dim3(dr_xcd_grid(tiles), splits), dim3(128), 0, s, g);
+  }
   DR_TRY(dr_check_launch("gemm_pp_split3"));
   if (splits > 1) {
     hipLaunchKernelGGL(k_pp_finish, dim3((unsigned)(((long long)M * N + 255) / 256)), dim3(256), 0, s, g);

@@ -202,8 +202,12 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
       op_gemm_nt_split3_supported(n, d->enc_hidden, F, w.a[N - 1], F, nullptr, 0, F, d->enc_hidden)) {
     // latent_mapper.0's feature columns (VAE.py:57-75 -> WorldModel.py) on the split3 bf16 MFMA
     DR_TRY(op_nt_repack_split3(d->enc_hidden, F, wm->map0.w, F + d->hidden, w.s3proj, s));
+    // K split by K alone (32 chunks of 32 per split, at most 8): the frames
+    // of a window step get the same sums whether the window is encoded whole
+    // or in time chunks (engine.py's overlapped warm start)
+    const int ksplits = std::max(1, std::min(8, (F + 1023) / 1024));
     return op_gemm_nt_split3_sk(n, d->enc_hidden, F, w.a[N - 1], F, nullptr, 0, F, w.s3proj, wm->map0.b, 0, feat,
-                                d->enc_hidden, w.s3part, w.s3part_n, s);
+                                d->enc_hidden, w.s3part, w.s3part_n, s, ksplits);
   }
   GemmArgs gp = lin(n, d->enc_hidden, F, w.a[N - 1], F, wm->map0.w, F + d->hidden, wm->map0.b, feat, d->enc_hidden);
   float* sk = w.sk;
@@ -279,6 +283,16 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
   if (z_init) {
     if (z_init != z_out) DR_TRY(copy2d(z_out, L, z_init, L, L, B, s));
     DR_TRY(op_onehot_index(B, d->rows, d->cols, z_out, L, w.idx, onehot_vals(w.idx, B, d->rows), s));
+    if (split_gru && planes && h_init) {
+      // a continuing chunk: the first GRU's hidden product on the same kernel
+      // and planes as the grouped launch that computes it inside one call, so
+      // a time-chunked scan equals the whole-window scan bit for bit
+      GemmArgs gh = lin(B, 3 * Hd, Hd, h_init, Hd, wm->w_hh, Hd, wm->b_hh, w.gh, 3 * Hd);
+      wplanes(gh, w.s3whh);
+      if (!DR_B16_CHAIN_WKS) gh.bf16 = 0;
+      DR_TRY(gemm_launch(G_NT, AM_PLAIN, &gh, 1, s));
+      gh_pre = true;
+    }
   }
   for (int t = 0; t < T; ++t) {
     const bool do_gru = (z_init != nullptr) || t > 0;

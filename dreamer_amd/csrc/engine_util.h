@@ -182,14 +182,14 @@ static inline bool tn_split3_ok(const GemmArgs& g) {
   return g.alpha == 1.0f && !g.act && !g.bias && !g.addend && g.ksplitB >= g.K && g.nsplitY >= g.N && !g.out_conv &&
          g.ksplitA >= g.K && g.epi == EPI_NONE && op_gemm_tn_split3_supported(g.M, g.N, g.K);
 }
-static inline int tn_launch(const GemmArgs* p, int n, void* ws, size_t ws_bytes, hipStream_t s) {
+static inline int tn_launch(const GemmArgs* p, int n, void* ws, size_t ws_bytes, hipStream_t s, int terms = 3) {
   bool ok = ws != nullptr;
   for (int i = 0; i < n && ok; ++i) ok = tn_split3_ok(p[i]) && op_gemm_tn_split3_ws_bytes(p[i].M, p[i].N, p[i].K) <= ws_bytes;
   if (!ok) return gemm_launch(G_TN, AM_PLAIN, p, n, s);
   for (int i = 0; i < n; ++i) {
     const GemmArgs& g = p[i];
     DR_TRY(op_gemm_tn_split3(g.M, g.N, g.K, g.A, g.lda, g.W, g.ldb, g.W2, g.ldb2, g.nsplitB < g.N ? g.nsplitB : g.N,
-                             g.Y, g.ldy, g.accumulate, ws, ws_bytes, s));
+                             g.Y, g.ldy, g.accumulate, ws, ws_bytes, s, terms));
   }
   return DR_OK;
 }

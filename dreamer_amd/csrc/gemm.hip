@@ -1650,6 +1650,9 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tile_b16(GemmBatch gb, int spl
 // workgroups of a smaller problem idle in a blockIdx.z slice sized for the
 // largest: a grouped launch of the GRU hidden product (456 tiles) with a
 // 56-tile Linear ran 21.7 us against 12.3 for the product alone)
+#ifndef DR_WK_ACC2
+#define DR_WK_ACC2 0  // A/B knob: 1 = the two 16-k halves on separate accumulators (r04n: no gain)
+#endif
 template <int BM, int BN, int NW, int D, int KMAP = 0>
 __global__ __launch_bounds__(64 * NW) void k_gemm_wk(GemmBatch gb, int splits, int npack) {
   constexpr int NTH = 64 * NW, FM = BM / 16, FN = BN / 16, NT4 = FM * FN * 256;
@@ -1743,11 +1746,18 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wk(GemmBatch gb, int splits, i
       }
     }
   };
-  f32x4 acc[FM][FN];
+  // NA = 2 (DR_WK_ACC2): the two 16-k halves of a block on separate
+  // accumulators, summed at the end -- twice the independent MFMA chains
+  // per wave (issue-stalled on MFMA read-after-write at four,
+  // profiles/r04a_pmc_sq_tcc_chain_kernels.txt)
+  constexpr int NA = DR_WK_ACC2 ? 2 : 1;
+  f32x4 acc[NA][FM][FN];
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+  for (int a2 = 0; a2 < NA; ++a2)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[a2][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < D; ++u) load(min(b0 + u, blast), u);
   const int nbw = b1 - b0;
@@ -1767,15 +1777,29 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wk(GemmBatch gb, int splits, i
           for (int j = 0; j < FN; ++j) rb[u][j][h] = (f32x4){0.f, 0.f, 0.f, 0.f};
         }
       }
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
+      if constexpr (NA == 2) {  // the halves interleaved: 2 x FM x FN independent chains
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
-          for (int i = 0; i < FM; ++i)
+          for (int h = 0; h < 2; ++h)
 #pragma unroll
-            for (int j = 0; j < FN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[u][i][h][c], rb[u][j][h][c], acc[i][j], 0, 0, 0);
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+              for (int j = 0; j < FN; ++j)
+                acc[h][i][j] =
+                    __builtin_amdgcn_mfma_f32_16x16x4f32(ra[u][i][h][c], rb[u][j][h][c], acc[h][i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+              for (int j = 0; j < FN; ++j)
+                acc[0][i][j] =
+                    __builtin_amdgcn_mfma_f32_16x16x4f32(ra[u][i][h][c], rb[u][j][h][c], acc[0][i][j], 0, 0, 0);
+      }
       load(min(b + D, blast), u);  // unconditional: a load under a branch is waited for at once
     }
   }
@@ -1784,9 +1808,12 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wk(GemmBatch gb, int splits, i
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
+    for (int j = 0; j < FN; ++j) {
+      f32x4 v = acc[0][i][j];
+      if constexpr (NA == 2) v = acc[0][i][j] + acc[1][i][j];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) red[wave][(i * FN + j) * 4 + e][lane] = acc[i][j][e];
+      for (int e = 0; e < 4; ++e) red[wave][(i * FN + j) * 4 + e][lane] = v[e];
+    }
   __syncthreads();
   float* part = g.splitk_ws;
 #pragma unroll
@@ -1830,6 +1857,9 @@ __device__ __forceinline__ unsigned wk_pack_rne(float x0, float x1) {
   return __builtin_bit_cast(unsigned, v);
 }
 
+#ifndef DR_WKS3_ACC3
+#define DR_WKS3_ACC3 0  // A/B knob: 1 = per-order accumulators (r04n: 554.3k vs 558.2k off)
+#endif
 // FULL: D >= every wave's chunk count -- all of a wave's fragments are loaded
 // up front (one memory latency per tile instead of one per D chunks), no refill
 template <int NTP, int D, int NW = 4, bool FULL = false>
@@ -1893,11 +1923,20 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) 
         rb[sl][p][j] = *(const DR_GLOBAL wk_u32x4*)((const DR_GLOBAL char*)wr + (e << 1));
       }
   };
-  f32x4 acc[FM][FN];
+  // NA = 3 (DR_WKS3_ACC3, 3-term form): the products accumulate by order --
+  // acc[0] hi*hi, acc[1] the two 2^-8 cross terms, acc[2] the three 2^-16
+  // terms -- summed smallest first at the end: three independent MFMA chains
+  // per block instead of six dependent MFMAs in a row on one accumulator
+  // (the wave-K kernels were issue-stalled on MFMA read-after-write,
+  // profiles/r04a_pmc_sq_tcc_chain_kernels.txt)
+  constexpr int NA = (NTP == 3 && DR_WKS3_ACC3) ? 3 : 1;
+  f32x4 acc[NA][FM][FN];
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+  for (int a3 = 0; a3 < NA; ++a3)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[a3][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < D; ++u) load(min(c0 + u, clast), u);
   const int ncw = c1 - c0;
@@ -1926,17 +1965,26 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) 
                                wk_pack_rne(x1[2], x1[3])};
         }
       }
-#define DR_WK3(PA, PB)                        \
-  _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
-      wk_mfma(rb[u][PB][j], a[PA][i], acc[i][j]);
-      if constexpr (NTP == 3) {
-        DR_WK3(2 % NTP, 0)
-        DR_WK3(1 % NTP, 1 % NTP)
-        DR_WK3(0, 2 % NTP)
-        DR_WK3(1 % NTP, 0)
-        DR_WK3(0, 1 % NTP)
+#define DR_WK3(PA, PB, X)                        \
+  _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[X][i][j] = \
+      wk_mfma(rb[u][PB][j], a[PA][i], acc[X][i][j]);
+      if constexpr (NA == 3) {  // independent chains interleaved
+        DR_WK3(2 % NTP, 0, 2)
+        DR_WK3(1 % NTP, 0, 1)
+        DR_WK3(0, 0, 0)
+        DR_WK3(1 % NTP, 1 % NTP, 2)
+        DR_WK3(0, 1 % NTP, 1)
+        DR_WK3(0, 2 % NTP, 2)
+      } else {
+        if constexpr (NTP == 3) {
+          DR_WK3(2 % NTP, 0, 0)
+          DR_WK3(1 % NTP, 1 % NTP, 0)
+          DR_WK3(0, 2 % NTP, 0)
+          DR_WK3(1 % NTP, 0, 0)
+          DR_WK3(0, 1 % NTP, 0)
+        }
+        DR_WK3(0, 0, 0)
       }
-      DR_WK3(0, 0)
 #undef DR_WK3
       // unconditional: a load under a branch is waited for at once
       if constexpr (!FULL) load(min(c + D, clast), u);
@@ -1946,9 +1994,12 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) 
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
+    for (int j = 0; j < FN; ++j) {
+      f32x4 v = acc[0][i][j];
+      if constexpr (NA == 3) v = acc[2][i][j] + acc[1][i][j] + acc[0][i][j];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) red[wave][(i * FN + j) * 4 + e][lane] = acc[i][j][e];
+      for (int e = 0; e < 4; ++e) red[wave][(i * FN + j) * 4 + e][lane] = v[e];
+    }
   __syncthreads();
 #pragma unroll
   for (int ii = 0; ii < NEPI; ++ii) {

@@ -362,6 +362,9 @@ static inline int dec_cout_st(const WmDims& D, int k) { return k == D.N - 1 ? 4 
 // the convolutions that run f32-accurate on the bf16 MFMA (3-term split):
 // encoder conv k >= 1 (conv1's 4-channel input stays on the f32 MFMA) and the
 // data gradient of decoder convT k (a Conv2d from cout_t to cin_t channels)
+#ifndef DR_WM_BF16_GEMM
+#define DR_WM_BF16_GEMM 1  // A/B knob: 0 = the bf16 WM step's Linears stay on the f32 MFMA
+#endif
 static inline bool enc_s3(const WmDims& D, int k) {
   return !D.Dv && k >= 1 && op_conv_split3_supported(D.M, D.e[k], D.IH >> k, D.IW >> k, D.e[k + 1]);
 }
@@ -390,11 +393,12 @@ static size_t wgrad_ws_floats(int n, int h, int w, int ca, int cb) {
   if (op_wgrad_split3_supported(n, h, w, ca, cb)) f = std::max(f, op_wgrad_split3_ws_floats(n, h, w, ca, cb));
   return f;
 }
+// lo_silu: lo holds pre-activations, SiLU applied on load (the f32 kernel only)
 static int wgrad(int n, int h, int w, int ca, int cb, const float* lo, int lda, const float* hi, int ldb, float* dw,
-                 int cbo, float* ws, size_t ws_floats, hipStream_t s, int terms) {
-  if (op_wgrad_split3_supported(n, h, w, ca, cb))
+                 int cbo, float* ws, size_t ws_floats, hipStream_t s, int terms, int lo_silu = 0) {
+  if (!lo_silu && op_wgrad_split3_supported(n, h, w, ca, cb))
     return op_wgrad_split3(n, h, w, ca, cb, lo, lda, hi, ldb, dw, cbo, 1.0f, 0, ws, ws_floats, s, terms);
-  return op_conv_wgrad(n, h, w, ca, cb, lo, lda, 0, hi, ldb, dw, cbo, 1.0f, 0, ws, ws_floats, s);
+  return op_conv_wgrad(n, h, w, ca, cb, lo, lda, lo_silu, hi, ldb, dw, cbo, 1.0f, 0, ws, ws_floats, s);
 }
 
 static void mlp_bwd_carve(Carve& c, long long M1, int w1, int w2, MlpBwd& b) {
@@ -459,7 +463,10 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
   } else {
     for (int k = 0; k + 1 < N; ++k) {  // convT k output at resolution level N - k - 1
       const long long sz = M1 * D.pix[N - k - 1] * D.cd[k + 1];
-      w.dq[k] = c.f(sz); w.dqp[k] = c.f(sz); w.dgq[k] = c.f(sz);
+      // the last layer's input is never stored post-SiLU: its two readers (the
+      // fused tanh-MSE layer, its weight gradient) apply SiLU on load -- the
+      // largest activation of the step (B = 256: 1.9 GB) written once less
+      w.dq[k] = c.f(sz); w.dqp[k] = k == N - 2 ? nullptr : c.f(sz); w.dgq[k] = c.f(sz);
     }
   }
   w.dgout = c.f(Dv ? M1 * Dv : M1 * D.pix[0] * 4);
@@ -542,6 +549,7 @@ static int head_bwd(const WmDims& D, const dr_mlp3& m, const dr_mlp3& g, int w1,
                     const float* t6, const float* t3, const float* t0, const float* x1, const float* x2,
                     const float* pre1, const float* pre2, int in_z, const float* hB, const float* zB, float* gHB,
                     float* gZB, MlpBwd& b, float* sk, long long sk_n, void* tn, size_t tn_bytes, hipStream_t s) {
+  const int terms = D.terms;
   const int M1 = D.M1, Hd = D.Hd, L = D.L;
   DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M1, w2, nout, glog, nout, t6, b.gx2, w2, 0), s));
   DR_TRY(lnbwd_nt(M1, w1, w2, b.gx2, w2, pre2, w2, m.n4, t3, b.gx1, w1, 0, b.gp2, w2, b.gy2, b.xh2, nullptr, 0,
@@ -556,7 +564,7 @@ static int head_bwd(const WmDims& D, const dr_mlp3& m, const dr_mlp3& g, int w1,
     p[2].W2 = zB; p[2].ldb2 = L; p[2].nsplitB = Hd;
   }
   splitk_all(p, 3, sk, sk_n);
-  DR_TRY(tn_launch(p, 3, tn, tn_bytes, s));
+  DR_TRY(tn_launch(p, 3, tn, tn_bytes, s, terms));
   ColsumJob cj[7] = {
       {nout, glog, nout, nullptr, 0, g.l6.b}, {w2, b.gp2, w2, nullptr, 0, g.l3.b},
       {w2, b.gy2, w2, b.xh2, w2, g.n4.w},     {w2, b.gy2, w2, nullptr, 0, g.n4.b},
@@ -581,6 +589,9 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   DR_REQUIRE(d->cols <= 64, "latent classes must be <= 64");
   DR_REQUIRE(d->obs_dim == 0 || d->obs_dim % 4 == 0, "vector observations: obs_dim % 4 == 0 required");
   const WmDims D = wm_dims(d, B, T);
+  // bf16 mode: the NT products that take the tile route run on the bf16 tile
+  // GEMM (operands rounded as staged, f32 accumulation), as in the epoch
+  GemmBf16Scope bf16_scope(DR_WM_BF16_GEMM && D.terms == 1);
   const bool vec = D.Dv > 0;
   const int Dv = D.Dv;
   Carve c(ws);
@@ -778,6 +789,10 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
       ConvTArgs a = {};
       a.n = M1; a.cin = cin_t[k]; a.h = IH >> (N - k); a.w = IW >> (N - k); a.cout = cout_t[k];
       a.in = k ? w.dqp[k - 1] : w.du2p; a.silu_in = 0; a.wq = w.wqd[k]; a.bias = dec->convt[k].b;
+      if (k == N - 1 && k > 0) {  // SiLU of the pre-activations on load (dqp[N - 2] is not stored)
+        a.in = w.dq[k - 1];
+        a.silu_in = 1;
+      }
       if (k < N - 1) {
         a.out = w.dq[k]; a.out2 = w.dqp[k]; a.ldc = cout_t[k];
         if (w.t3d[k]) DR_TRY(op_convT_split3(CT_EPI_BIAS, a, w.t3d[k], s, D.terms));
@@ -857,7 +872,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     p[0] = bwd_w(Dv, D.Fd, M1, w.dgout, Dv, w.dqp[0], D.Fd, gd->convt[1].w);
     p[1] = bwd_w(D.Fd, D.Fd, M1, w.dgq[0], D.Fd, w.du2p, D.Fd, gd->convt[0].w);
     splitk_all(p, 2, w.sk, w.sk_n);
-    DR_TRY(tn_launch(p, 2, w.tn, w.tn_bytes, s));
+    DR_TRY(tn_launch(p, 2, w.tn, w.tn_bytes, s, D.terms));
     ColsumJob cj[2] = {{Dv, w.dgout, Dv, nullptr, 0, gd->convt[1].b}, {D.Fd, w.dgq[0], D.Fd, nullptr, 0, gd->convt[0].b}};
     DR_TRY(op_colsum_multi(M1, cj, 2, s));
   } else {
@@ -866,7 +881,9 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
       const int co = cout_t[k], co_st = dec_cout_st(D, k);
       float* gin = k ? w.dgq[k - 1] : w.dgu2;              // dL/d(pre-activation) of convT k's input
       const float* pre = k ? w.dq[k - 1] : w.du2;
-      const float* post = k ? w.dqp[k - 1] : w.du2p;
+      // input of convT k after SiLU; the last layer's is recomputed from dq (not stored)
+      const bool post_silu = k == N - 1 && k > 0;
+      const float* post = post_silu ? w.dq[k - 1] : k ? w.dqp[k - 1] : w.du2p;
       const float* gout = k < N - 1 ? w.dgq[k] : w.dgout;  // dL/d(convT k's output pre-activation)
       if (w.s3d[k])
         DR_TRY(op_conv_split3_ex(M1, co_st, ih, iw, cin_t[k], gout, w.s3d[k], nullptr, gin, 0, const_cast<float*>(pre),
@@ -875,7 +892,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
         DR_TRY(op_conv_nhwc_ex(M1, co_st, ih, iw, cin_t[k], gout, w.wrd[k], nullptr, gin, 0, const_cast<float*>(pre),
                                CONV_EPI_DSILU, s));
       DR_TRY(wgrad(M1, ih / 2, iw / 2, cin_t[k], co_st, post, cin_t[k], gout, co_st, gd->convt[k].w, co, w.cws, w.cws_n,
-                   s, D.terms));
+                   s, D.terms, post_silu ? 1 : 0));
       DR_TRY(op_chan_sum((long long)M1 * ih * iw, co, gout, co_st, gd->convt[k].b, 0, w.cws, w.cws_n, s));
     }
   }
@@ -893,7 +910,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     p[1] = bwd_w(D.dh, Hd + L, M1, w.gpu, D.dh, hB, Hd, gd->up0.w);
     p[1].W2 = zB; p[1].ldb2 = L; p[1].nsplitB = Hd;
     splitk_all(p, 2, w.sk, w.sk_n);
-    DR_TRY(tn_launch(p, 2, w.tn, w.tn_bytes, s));
+    DR_TRY(tn_launch(p, 2, w.tn, w.tn_bytes, s, D.terms));
     ColsumJob cj[4] = {
         {D.Fd, w.dgu2, D.Fd, nullptr, 0, w.db3p},
         {D.dh, w.gpu, D.dh, nullptr, 0, gd->up0.b},
@@ -943,7 +960,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     p[2].W2 = w.act_tm; p[2].ldb2 = A; p[2].nsplitB = L;
     p[3] = bwd_w(3 * Hd, Hd, M1, w.ggh + (long long)B * 3 * Hd, 3 * Hd, w.h_all, Hd, gw->w_hh);
     splitk_all(p, 4, w.sk, w.sk_n);
-    DR_TRY(tn_launch(p, 4, w.tn, w.tn_bytes, s));
+    DR_TRY(tn_launch(p, 4, w.tn, w.tn_bytes, s, D.terms));
     ColsumJob cj[6] = {
         {L, w.glog, L, nullptr, 0, gw->map3.b},       {eh, w.gpre_m, eh, nullptr, 0, gw->map0.b},
         {eh, w.gy_m, eh, w.xh_m, eh, gw->map1.w},     {eh, w.gy_m, eh, nullptr, 0, gw->map1.b},
@@ -972,7 +989,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     p[0] = bwd_w(F, F, M, gL, F, w.a[0], F, gw->conv[1].w);
     p[1] = bwd_w(F, Dv, M, w.gp[0], F, w.x0, Dv, gw->conv[0].w);
     splitk_all(p, 2, w.sk, w.sk_n);
-    DR_TRY(tn_launch(p, 2, w.tn, w.tn_bytes, s));
+    DR_TRY(tn_launch(p, 2, w.tn, w.tn_bytes, s, D.terms));
     ColsumJob cj[2] = {{F, gL, F, nullptr, 0, gw->conv[1].b}, {F, w.gp[0], F, nullptr, 0, gw->conv[0].b}};
     DR_TRY(op_colsum_multi(M, cj, 2, s));
   } else {

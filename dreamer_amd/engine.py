@@ -54,6 +54,11 @@ class ImaginationEngine:
         # and a forked branch slowed every later graph replay by ~6 %.  Both
         # stay available behind DREAMER_WARM_CHUNK / DREAMER_FORK for
         # re-measurement; the defaults run one stream, one encoder chunk.
+        # Round 4 re-tried the chunked encoder on a CU-masked stream beside a
+        # high-priority scan (the fence that pays for the pipelined epochs,
+        # warm_stream): 8-step chunks unfenced 7.56 ms per epoch against 6.92
+        # one-chunk, fenced to 7/8 of the CUs 17.9-18.9 ms -- every later phase
+        # of the epoch slowed 3-4x (profiles/r04l_overlap_phase_probe.txt).
         self.side = torch.cuda.Stream(self.dev)
         import os
         self.chunks = self.warm_chunks(self.T, int(os.environ.get("DREAMER_WARM_CHUNK", str(self.T))))
@@ -367,11 +372,15 @@ class ImaginationEngine:
         """The stream of the pipelined warm start: a plain torch stream, or with
         cu_fraction in (0, 1) a HIP stream restricted to that share of the CUs
         (dr_stream_create_cumask) so that the imagination / update chain keeps
-        CUs of its own.  DREAMER_WARM_CUS sets the default fraction."""
+        CUs of its own.  DREAMER_WARM_CUS sets the default fraction (0.875:
+        B = 256, K = 10 epochs, warm start fenced to 7/8 of the CUs with the
+        chain at high priority 5.86 ms per epoch against 6.33 unfenced and
+        6.87 sequential; fenced at normal priority 8.58, tools/pipe_probe.py,
+        profiles/r04i_pipe_probe.txt)"""
         import ctypes
         import os
         if cu_fraction is None:
-            cu_fraction = float(os.environ.get("DREAMER_WARM_CUS", "1"))
+            cu_fraction = float(os.environ.get("DREAMER_WARM_CUS", "0.875"))
         if not 0.0 < cu_fraction < 1.0:
             return torch.cuda.Stream(self.dev)
         n = ctypes.c_int(0)
@@ -444,8 +453,13 @@ class ImaginationEngine:
         # DREAMER_CHAIN_PRIORITY (torch stream priority, -1 = high): the
         # imagination / update chain on a stream of that priority, so that its
         # latency-bound launches win CU slots over the warm start's convolutions
+        # (default -1 with the fenced warm stream, 0 without: a high-priority
+        # chain beside an unfenced warm stream measured 13.1 ms per epoch
+        # against 6.9 sequential after sequential epochs in the same process,
+        # profiles/r04n_pipe_after.txt)
         import os
-        prio = int(os.environ.get("DREAMER_CHAIN_PRIORITY", "0"))
+        fenced = 0.0 < float(os.environ.get("DREAMER_WARM_CUS", "0.875")) < 1.0
+        prio = int(os.environ.get("DREAMER_CHAIN_PRIORITY", "-1" if fenced else "0"))
         if prio != 0:
             if P.get("chain") is None or P.get("chain_prio") != prio:
                 P["chain"], P["chain_prio"] = torch.cuda.Stream(self.dev, priority=prio), prio

@@ -7,6 +7,7 @@ share the device's few hardware queues and skew later ones):
   python tools/pipe_probe.py K CASE
 
 CASE: "seq" (K sequential engine.run epochs), "pipe" (run_many as shipped),
+"after:<fraction>" (sequential epochs timed before and after a pipelined run),
 or "pipe:<warm CU fraction>:<chain priority>" -- the warm stream restricted
 to that share of the CUs (engine.warm_stream; 1 = no mask) and the chain on a
 stream of the given torch priority (0 = normal, -1 = high).  Prints one JSON
@@ -52,6 +53,18 @@ def main():
         return best * 1e3 / K
 
     res = {"case": case, "K": K}
+    if case.startswith("after"):
+        # sequential epochs before and after a pipelined run in the same process:
+        # does a CU-masked warm stream leave later work on the device slower?
+        def seq():
+            for s in starts:
+                eng.run(s)
+        res["seq_before_ms"] = round(timed(seq), 4)
+        res["pipe_ms"] = round(timed(lambda: eng.run_many(starts)), 4)
+        res["seq_after_ms"] = round(timed(seq), 4)
+        res["warm_cus"] = os.environ.get("DREAMER_WARM_CUS")
+        print(json.dumps(res), flush=True)
+        return
     if case == "seq":
         def seq():
             for s in starts:
