@@ -149,7 +149,7 @@ int op_wgrad_reduce(int ca, int cb, int cbo, int nsplit, const float* part, floa
 // conv_split.hip: the same weight gradient f32-accurate on the bf16 MFMA (both
 // operands split3 while staged); ca in {64, 128, 256}, cb % 8 == 0, h and w
 // powers of two, lo without SiLU on load
-bool op_wgrad_split3_supported(int n, int h, int w, int ca, int cb);
+bool op_wgrad_split3_supported(int n, int h, int w, int ca, int cb, int terms = 3);  // terms 1: also ca = 32
 size_t op_wgrad_split3_ws_floats(int n, int h, int w, int ca, int cb);
 // terms = 1: both operands RNE-rounded to one bf16 term (bf16 world-model step)
 int op_wgrad_split3(int n, int h, int w, int ca, int cb, const float* lo, int lda, const float* hi, int ldb,

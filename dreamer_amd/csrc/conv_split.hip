@@ -1130,15 +1130,21 @@ int op_convT_split3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s, 
 // 2 (a) x 4 (n), partial planes per pixel split reduced by k_wgrad_reduce.
 // Low-resolution sizes are powers of two (shift addressing).
 // ---------------------------------------------------------------------------
-// TERMS = 1: both operands RNE-rounded to one bf16 plane (bf16 world-model step)
-template <int BM, int TERMS = 3>
+// TERMS = 1: both operands RNE-rounded to one bf16 plane (bf16 world-model
+// step); that form also takes BN = 256 column tiles (the output-gradient rows
+// re-read half as often: 255 -> 209 us for the 128-channel layers, r04r) and
+// BM = 32.  (The 32 x 4-channel layers next to the frames stay on the f32
+// kernel: a BN = 64 one-term form measured 314 us against 311, and with
+// SiLU on load 752 us.)
+template <int BM, int TERMS = 3, int BN = 128>
 __global__ __launch_bounds__(512) void k_wgrad_split3(int n, int lh, int lw, int ca, int cb,
                                                       const float* __restrict__ lo, int lda,
                                                       const float* __restrict__ hi, int ldb, int chunk,
                                                       float* __restrict__ part) {
-  constexpr int BN = 128, KC = 64, RP = KC / 8 + 1;
-  constexpr int FM = BM / 32, FN = 2;  // wave tile (BM / 2) x 32
-  static_assert(TERMS == 1 || TERMS == 3, "wgrad_split3 terms");
+  constexpr int KC = 64, RP = KC / 8 + 1;
+  constexpr int FM = BM / 32, FN = BN / 64;  // wave tile (BM / 2) x (BN / 4)
+  static_assert((TERMS == 1 || TERMS == 3) && FM >= 1 && (BN == 128 || (BN == 256 && TERMS == 1)),
+                "wgrad_split3 tile");
   __shared__ __attribute__((aligned(16))) u32x4 S[TERMS][BM + BN][RP];
   const int N = 16 * cb;
   const int tiles_n = N / BN, tiles = (ca / BM) * tiles_n;
@@ -1150,61 +1156,78 @@ __global__ __launch_bounds__(512) void k_wgrad_split3(int n, int lh, int lw, int
   const long long k_end = k_begin + chunk < K ? k_begin + chunk : K;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
 
-  // staging unit of this thread: channel quad cq, pixel octet oct (A: rows of
-  // ca channels m0 + 4 cq; B: columns n0 + 4 cq, one tap, 4 channels)
-  constexpr int AU = BM / 4 * 8, BUn = BN / 4 * 8;
-  const bool isA = tid < AU, active = tid < AU + BUn;
-  const int u = isA ? tid : tid - AU, cq = u >> 3, oct = u & 7;
-  const int row0 = isA ? 4 * cq : BM + 4 * cq;
-  const int bn = n0 + 4 * cq, btap = bn / cb, bch = bn - btap * cb, bky = btap >> 2, bkx = btap & 3;
-  const float* __restrict__ abase = lo + m0 + 4 * cq;
-  f32x4 v[8];
-  auto load = [&](long long p0) __attribute__((always_inline)) {
+  // staging units of this thread (UPT of them): channel quad cq, pixel octet
+  // oct (A: rows of ca channels m0 + 4 cq; B: columns n0 + 4 cq, one tap, 4 channels)
+  constexpr int AU = BM / 4 * 8, BUn = BN / 4 * 8, UPT = (AU + BUn + 511) / 512;
+  bool isA[UPT], active[UPT];
+  int oct[UPT], row0[UPT], bch[UPT], bky[UPT], bkx[UPT];
+  const float* src[UPT];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const long long p = p0 + i;
-      bool ok = active && p < k_end;
-      long long off;
-      if (isA) {
-        off = p * lda;
-      } else {
-        const long long f = p >> (lw + lh);
-        const int y = (int)(p >> lw) & (h - 1), x = (int)p & (w - 1);
-        const int Y = 2 * y - 1 + bky, X = 2 * x - 1 + bkx;
-        ok = ok && Y >= 0 && Y < H2 && X >= 0 && X < W2;
-        off = ((f * H2 + Y) * W2 + X) * ldb + bch;
+  for (int j = 0; j < UPT; ++j) {
+    const int id = tid + 512 * j;
+    isA[j] = id < AU;
+    active[j] = id < AU + BUn;
+    const int u = isA[j] ? id : id - AU, cq = u >> 3;
+    oct[j] = u & 7;
+    row0[j] = isA[j] ? 4 * cq : BM + 4 * cq;
+    const int bn = n0 + 4 * cq, btap = bn / cb;
+    bch[j] = bn - btap * cb;
+    bky[j] = btap >> 2;
+    bkx[j] = btap & 3;
+    src[j] = isA[j] ? lo + m0 + 4 * cq : hi;
+  }
+  f32x4 v[UPT][8];
+  auto load = [&](long long p0c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < UPT; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const long long p = p0c + 8 * oct[j] + i;
+        bool ok = active[j] && p < k_end;
+        long long off;
+        if (isA[j]) {
+          off = p * lda;
+        } else {
+          const long long f = p >> (lw + lh);
+          const int y = (int)(p >> lw) & (h - 1), x = (int)p & (w - 1);
+          const int Y = 2 * y - 1 + bky[j], X = 2 * x - 1 + bkx[j];
+          ok = ok && Y >= 0 && Y < H2 && X >= 0 && X < W2;
+          off = ((f * H2 + Y) * W2 + X) * ldb + bch[j];
+        }
+        const f32x4 t = *reinterpret_cast<const f32x4*>(src[j] + (ok ? off : 0));
+        v[j][i] = ok ? t : (f32x4){0.f, 0.f, 0.f, 0.f};
       }
-      const f32x4 t = *reinterpret_cast<const f32x4*>((isA ? abase : hi) + (ok ? off : 0));
-      v[i] = ok ? t : (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
   };
   auto store = [&]() __attribute__((always_inline)) {
-    if (!active) return;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if constexpr (TERMS == 1) {
-        u32x4 ph;
+    for (int j = 0; j < UPT; ++j) {
+      if (!active[j]) continue;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ph[i] = pack_bf16x2(v[2 * i][c], v[2 * i + 1][c]);
-        S[0][row0 + c][oct] = ph;
-      } else {
-        u32x4 ph, pm, pl;
+      for (int c = 0; c < 4; ++c) {
+        if constexpr (TERMS == 1) {
+          u32x4 ph;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          unsigned hh, mm, ll;
-          split3_pair(v[2 * i][c], v[2 * i + 1][c], hh, mm, ll);
-          ph[i] = hh;
-          pm[i] = mm;
-          pl[i] = ll;
+          for (int i = 0; i < 4; ++i) ph[i] = pack_bf16x2(v[j][2 * i][c], v[j][2 * i + 1][c]);
+          S[0][row0[j] + c][oct[j]] = ph;
+        } else {
+          u32x4 ph, pm, pl;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            unsigned hh, mm, ll;
+            split3_pair(v[j][2 * i][c], v[j][2 * i + 1][c], hh, mm, ll);
+            ph[i] = hh;
+            pm[i] = mm;
+            pl[i] = ll;
+          }
+          S[0][row0[j] + c][oct[j]] = ph;
+          S[1][row0[j] + c][oct[j]] = pm;
+          S[2][row0[j] + c][oct[j]] = pl;
         }
-        S[0][row0 + c][oct] = ph;
-        S[1][row0 + c][oct] = pm;
-        S[2][row0 + c][oct] = pl;
       }
     }
   };
 
-  const int wm0 = (wave >> 2) * (BM / 2), wn0 = (wave & 3) * 32;
+  const int wm0 = (wave >> 2) * (BM / 2), wn0 = (wave & 3) * (BN / 4);
   f32x4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -1212,12 +1235,12 @@ __global__ __launch_bounds__(512) void k_wgrad_split3(int n, int lh, int lw, int
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const long long nch = k_end > k_begin ? (k_end - k_begin + KC - 1) / KC : 0;
   if (nch > 0) {
-    load(k_begin + 8 * oct);
+    load(k_begin);
     store();
     __syncthreads();
     for (long long c = 0; c < nch; ++c) {
       // next chunk in flight (the last chunk reloads itself, unused)
-      load(k_begin + (c + 1 < nch ? c + 1 : c) * KC + 8 * oct);
+      load(k_begin + (c + 1 < nch ? c + 1 : c) * KC);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         u32x4 av[TERMS][FM], bv[TERMS][FN];
@@ -1264,14 +1287,21 @@ static int ilog2_exact(int v) {
   return (1 << l) == v ? l : -1;
 }
 
-bool op_wgrad_split3_supported(int n, int h, int w, int ca, int cb) {
-  return (ca == 64 || ca == 128 || ca == 256) && cb % 8 == 0 && cb >= 8 && ilog2_exact(h) >= 0 && ilog2_exact(w) >= 0 &&
-         n > 0 && (long long)n * 4 * h * w * cb < (1LL << 31);
+bool op_wgrad_split3_supported(int n, int h, int w, int ca, int cb, int terms) {
+  const bool cb_ok = cb % 8 == 0 && cb >= 8;
+  return (ca == 64 || ca == 128 || ca == 256 || (terms == 1 && ca == 32)) && cb_ok && ilog2_exact(h) >= 0 &&
+         ilog2_exact(w) >= 0 && n > 0 && (long long)n * 4 * h * w * cb < (1LL << 31);
 }
 
-static void wgrad3_plan(int n, int h, int w, int ca, int cb, int& nsplit, int& chunk) {
-  const int bm = ca >= 128 ? 128 : 64;
-  const int tiles = (ca / bm) * (16 * cb / 128);
+// tile of a problem: BM by the a-channels; the one-term form takes BN = 256
+// where N = 16 cb allows it
+static void wgrad3_tile(int ca, int cb, int terms, int& bm, int& bn) {
+  bm = ca >= 128 ? 128 : ca >= 64 ? 64 : 32;
+  bn = terms == 1 && (16 * cb) % 256 == 0 ? 256 : 128;
+}
+
+static void wgrad3_plan(int n, int h, int w, int ca, int cb, int bm, int bn, int& nsplit, int& chunk) {
+  const int tiles = (ca / bm) * (16 * cb / bn);
   const long long K = (long long)n * h * w;
   const long long kch = (K + 63) / 64;
   long long ns = (512 + tiles - 1) / tiles;  // about 2 workgroups per CU
@@ -1283,34 +1313,46 @@ static void wgrad3_plan(int n, int h, int w, int ca, int cb, int& nsplit, int& c
 }
 
 size_t op_wgrad_split3_ws_floats(int n, int h, int w, int ca, int cb) {
-  int ns, ch;
-  wgrad3_plan(n, h, w, ca, cb, ns, ch);
-  return (size_t)ns * ca * 16 * cb;
+  size_t f = 0;
+  for (int terms : {1, 3}) {  // either form's partial planes
+    int bm, bn, ns, ch;
+    wgrad3_tile(ca, cb, terms, bm, bn);
+    wgrad3_plan(n, h, w, ca, cb, bm, bn, ns, ch);
+    f = std::max(f, (size_t)ns * ca * 16 * cb);
+  }
+  return f;
 }
 
 int op_wgrad_split3(int n, int h, int w, int ca, int cb, const float* lo, int lda, const float* hi, int ldb,
                     float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s,
                     int terms) {
-  if (!op_wgrad_split3_supported(n, h, w, ca, cb) || (terms != 1 && terms != 3) || lda % 4 || ldb % 4 || lda < ca || ldb < cb || cbo < 1 ||
+  if (!op_wgrad_split3_supported(n, h, w, ca, cb, terms) || (terms != 1 && terms != 3) || lda % 4 || ldb % 4 || lda < ca || ldb < cb || cbo < 1 ||
       cbo > cb || !lo || !hi || !dw || ((uintptr_t)lo & 15) || ((uintptr_t)hi & 15)) {
     dr_set_error("wgrad_split3: unsupported problem (ca=%d cb=%d h=%d w=%d)", ca, cb, h, w);
     return DR_E_INVALID;
   }
-  int ns, ch;
-  wgrad3_plan(n, h, w, ca, cb, ns, ch);
+  int bm, bn, ns, ch;
+  wgrad3_tile(ca, cb, terms, bm, bn);
+  wgrad3_plan(n, h, w, ca, cb, bm, bn, ns, ch);
   if ((size_t)ns * ca * 16 * cb > ws_floats) {
     dr_set_error("wgrad_split3: workspace too small");
     return DR_E_WORKSPACE;
   }
-  const int bm = ca >= 128 ? 128 : 64;
-  const int tiles = (ca / bm) * (16 * cb / 128);
+  const int tiles = (ca / bm) * (16 * cb / bn);
   const int lh = ilog2_exact(h), lw = ilog2_exact(w);
-#define DR_W3L(BM, T)                                                                                             \
-  hipLaunchKernelGGL((k_wgrad_split3<BM, T>), dim3((unsigned)(tiles * ns)), dim3(512), 0, s, n, lh, lw, ca, cb, lo, \
-                     lda, hi, ldb, ch, ws)
+#define DR_W3L(BM, T, ...)                                                                                     \
+  hipLaunchKernelGGL((k_wgrad_split3<BM, T, ##__VA_ARGS__>), dim3((unsigned)(tiles * ns)), dim3(512), 0, s, n, lh, lw, \
+                     ca, cb, lo, lda, hi, ldb, ch, ws)
   if (terms == 1) {
-    if (bm == 128) DR_W3L(128, 1);
-    else DR_W3L(64, 1);
+    if (bn == 256) {
+      if (bm == 128) DR_W3L(128, 1, 256);
+      else if (bm == 64) DR_W3L(64, 1, 256);
+      else DR_W3L(32, 1, 256);
+    } else {
+      if (bm == 128) DR_W3L(128, 1);
+      else if (bm == 64) DR_W3L(64, 1);
+      else DR_W3L(32, 1);
+    }
   } else {
     if (bm == 128) DR_W3L(128, 3);
     else DR_W3L(64, 3);

@@ -363,7 +363,7 @@ static inline int dec_cout_st(const WmDims& D, int k) { return k == D.N - 1 ? 4 
 // encoder conv k >= 1 (conv1's 4-channel input stays on the f32 MFMA) and the
 // data gradient of decoder convT k (a Conv2d from cout_t to cin_t channels)
 #ifndef DR_WM_BF16_GEMM
-#define DR_WM_BF16_GEMM 1  // A/B knob: 0 = the bf16 WM step's Linears stay on the f32 MFMA
+#define DR_WM_BF16_GEMM 0  // A/B knob: 1 = the bf16 WM step's tile-routed Linears in bf16 (r04p: -0.1 ms, posterior flips 1.7e-4 -> 1.7e-3)
 #endif
 static inline bool enc_s3(const WmDims& D, int k) {
   return !D.Dv && k >= 1 && op_conv_split3_supported(D.M, D.e[k], D.IH >> k, D.IW >> k, D.e[k + 1]);
@@ -390,13 +390,13 @@ static inline bool encg_s3(const WmDims& D, int k) {
 // allows (conv_split.hip), else the f32 MFMA kernel (wmconv.hip)
 static size_t wgrad_ws_floats(int n, int h, int w, int ca, int cb) {
   size_t f = op_conv_wgrad_ws_floats(n, h, w, ca, cb);
-  if (op_wgrad_split3_supported(n, h, w, ca, cb)) f = std::max(f, op_wgrad_split3_ws_floats(n, h, w, ca, cb));
+  if (op_wgrad_split3_supported(n, h, w, ca, cb, 1)) f = std::max(f, op_wgrad_split3_ws_floats(n, h, w, ca, cb));
   return f;
 }
 // lo_silu: lo holds pre-activations, SiLU applied on load (the f32 kernel only)
 static int wgrad(int n, int h, int w, int ca, int cb, const float* lo, int lda, const float* hi, int ldb, float* dw,
                  int cbo, float* ws, size_t ws_floats, hipStream_t s, int terms, int lo_silu = 0) {
-  if (!lo_silu && op_wgrad_split3_supported(n, h, w, ca, cb))
+  if (!lo_silu && op_wgrad_split3_supported(n, h, w, ca, cb, terms))
     return op_wgrad_split3(n, h, w, ca, cb, lo, lda, hi, ldb, dw, cbo, 1.0f, 0, ws, ws_floats, s, terms);
   return op_conv_wgrad(n, h, w, ca, cb, lo, lda, lo_silu, hi, ldb, dw, cbo, 1.0f, 0, ws, ws_floats, s);
 }

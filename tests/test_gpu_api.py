@@ -242,14 +242,18 @@ class FakeCarRacing:
         pass
 
 
-def test_train_dreamer_with_fake_env(gpu, tmp_path, monkeypatch):
+@pytest.mark.parametrize("formula", [True, False])
+def test_train_dreamer_with_fake_env(formula, gpu, tmp_path, monkeypatch):
     """Dreamer.train_dreamer(env, eval_env) end to end (train_car_racer.py:38):
     random kick-start, world-model and agent training iterations, evaluation,
     checkpoint + training-log files; then Run() and a reference-format reload."""
     monkeypatch.chdir(tmp_path)
-    # default init: the closed-form parity weights drive this tiny training
-    # run into non-finite updates on some noise draws (sequential epochs too)
-    d, _ = _dreamer(gpu, formula=False, batch_size=4, sequence_length=16, horizon=5, buffer_size=256,
+    # the closed-form parity weights (formula=True) and the default init: in
+    # rounds 2-3 the formula-weight run went non-finite on some Philox draws;
+    # on the round-4 tree both run finite (profiles/r04o_fake_env_tests.txt)
+    # and the failing draws no longer occur, so no single change is pinned
+    # as the fix (DESIGN.md section 3)
+    d, _ = _dreamer(gpu, formula=formula, batch_size=4, sequence_length=16, horizon=5, buffer_size=256,
                     random_iterations=2, training_iterations=2, AC_epochs=2)
     env, eval_env = FakeCarRacing(seed=1), FakeCarRacing(seed=2)
     wm, al, cl, ev = d.train_dreamer(env, eval_env)
