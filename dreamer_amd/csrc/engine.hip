@@ -224,6 +224,7 @@ struct ObsWs {
   int* idx;
   void *s3m0, *s3whh;  // bf16 planes of latent_mapper.0's h-columns and W_hh (k_gemm_wks3)
   float* wtb;          // W_ih in unit blocks (k_gru_gates_lds)
+  unsigned short* hpl; // split3 planes of the GRU output [3][B][aplane_ld(Hd)] (k_gemm_wks3's A)
 };
 static void obs_carve(Carve& c, const dr_dims* d, int B, ObsWs& w) {
   w.wtb = c.f((long long)(latent(d) + d->action) * 3 * d->hidden);
@@ -237,6 +238,7 @@ static void obs_carve(Carve& c, const dr_dims* d, int B, ObsWs& w) {
   w.hb[0] = c.f((long long)B * d->hidden);
   w.hb[1] = c.f((long long)B * d->hidden);
   w.idx = c.i(2LL * B * d->rows);
+  w.hpl = reinterpret_cast<unsigned short*>(c.raw((size_t)3 * B * aplane_ld(d->hidden) * sizeof(unsigned short)));
 }
 
 extern "C" size_t dr_observe_workspace_bytes(const dr_dims* d, int B) {
@@ -270,6 +272,8 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
     if (DR_GATES_BLOCKED && B >= 128 && Hd % 4 == 0) DR_TRY(op_wih_block(Hd, L + d->action, wm->w_ih, w.wtb, s));
   }
   const bool planes = B >= 128 && T > 1 && Hd % 8 == 0;
+  // fp32 mode on the split GRU path: the gates kernel also writes h's split3 planes
+  const bool hpl_on = DR_APLANES && planes && d->precision == DR_PREC_FP32;
   if (planes) {
     DR_TRY(split_planes(eh, Hd, wm->map0.w + F, F + Hd, w.s3m0, s));
     DR_TRY(split_planes(3 * Hd, Hd, wm->w_hh, Hd, w.s3whh, s));
@@ -302,7 +306,8 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
       hb ^= 1;
       DR_TRY(gru_onehot(d, wm, B, w.idx, actions + ai * act_st, act_sb, h, Hd, hn, Hd, w.wt, nullptr,
                         nullptr, nullptr, nullptr, s, z_out, L, w.gh, gh_pre,
-                        DR_GATES_BLOCKED && B >= 128 && Hd % 4 == 0 ? w.wtb : nullptr));
+                        DR_GATES_BLOCKED && B >= 128 && Hd % 4 == 0 ? w.wtb : nullptr,
+                        hpl_on ? w.hpl : nullptr, aplane_ld(Hd)));
       h = hn;
     }
     // latent_mapper.0 on cat(features, h): feature part precomputed in feat[t]
@@ -317,6 +322,10 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
         // bf16 mode: plane 0 times bf16-rounded h (k_gemm_wks3<1>); fp32 mode: the 3-term split
         wplanes(g[0], w.s3m0);
         wplanes(g[1], w.s3whh);
+        if (hpl_on && do_gru) {  // h's split3 planes from this step's gates kernel
+          aplanes(g[0], w.hpl, B);
+          aplanes(g[1], w.hpl, B);
+        }
         if (!DR_B16_CHAIN_WKS) g[0].bf16 = g[1].bf16 = 0;
       } else {
         g[0].bf16 = g[1].bf16 = 0;  // (bf16 mode: these products stay f32)
@@ -370,6 +379,7 @@ struct ImWs {
   float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog, *rval, *wt, *wst, *bst;  // forward scratch
   float *tl0f, *hpart;  // forward: actor Linear 0 transposed ([Hd+L][a1]), its h-part + bias [B][a1]
   float* wtb;           // forward: W_ih in unit blocks (k_gru_gates_lds)
+  unsigned short* hpl;  // forward: split3 planes of h_{t+1} [3][B][aplane_ld(Hd)] (k_gemm_wks3's A)
   void *s3r, *s3c;  // split3 weight planes of the reward / continue heads' first Linear
   void *s3p0, *s3a0, *s3whh, *s3wt, *s3twhh;  // bf16 planes of the per-step chain weights (k_gemm_wks3)
   float* s3part;    // their split-K partial sums
@@ -409,6 +419,7 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.s3part = c.f((long long)w.s3part_n);
   w.wt = c.f((long long)(L + A) * 3 * Hd);
   w.wtb = c.f((long long)(L + A) * 3 * Hd);
+  w.hpl = reinterpret_cast<unsigned short*>(c.raw((size_t)3 * B * aplane_ld(Hd) * sizeof(unsigned short)));
   w.tl0f = c.f((long long)(Hd + L) * d->actor_h1);
   w.hpart = c.f(Bl * d->actor_h1);
   w.wst = c.f((long long)2 * A * d->actor_h2);
@@ -519,6 +530,7 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
   };
   const bool fused_actor = zg && DR_ACTOR_TAIL && op_actor_tail_ok(actor_tail(0, w.idx[0], latents));
   const bool planes = split_gru && H > 1 && Hd % 8 == 0;
+  const bool hpl_on = DR_APLANES && planes && d->precision == DR_PREC_FP32;
   if (planes) {
     DR_TRY(split_planes(d->prior_h1, Hd, wm->prior.l0.w, Hd, w.s3p0, s));
     if (zg) DR_TRY(split_planes(a1, Hd, ac->l0.w, Hd + L, w.s3a0, s));
@@ -553,7 +565,8 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
     // WorldModel.imagine_step (WorldModel.py:72-77)
     DR_TRY(gru_onehot(d, wm, B, w.idx[t & 1], actions + (long long)t * A, ldA, h_t, ldH, h_n, ldH, w.wt,
                       tp.r + hb, tp.u + hb, tp.n + hb, tp.ghn + hb, s, z_t, ldL, w.gh, split_gru && t > 0,
-                      DR_GATES_BLOCKED && split_gru && Hd % 4 == 0 ? w.wtb : nullptr));
+                      DR_GATES_BLOCKED && split_gru && Hd % 4 == 0 ? w.wtb : nullptr,
+                      hpl_on ? w.hpl : nullptr, aplane_ld(Hd)));
     float* p1 = tp.pre1p + (long long)t * B * d->prior_h1;
     float* p2 = tp.pre2p + (long long)t * B * d->prior_h2;
     {
@@ -574,9 +587,11 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
         ++np;
       }
       // bf16 mode: on the weight planes the products run in bf16 (k_gemm_wks3<1>),
-      // else they stay f32
-      for (int i = 0; i < np; ++i)
+      // else they stay f32; fp32 mode: h_{t+1}'s split3 planes from the gates kernel
+      for (int i = 0; i < np; ++i) {
         if (!planes || !DR_B16_CHAIN_WKS) p[i].bf16 = 0;
+        if (hpl_on) aplanes(p[i], w.hpl, B);
+      }
       DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, np, s));
     }
     DR_TRY(run(G_NT, AM_LNSILU, lin_ln(B, d->prior_h2, d->prior_h1, p1, d->prior_h1, wm->prior.n1, wm->prior.l3.w,

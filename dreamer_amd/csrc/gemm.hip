@@ -1862,8 +1862,10 @@ __device__ __forceinline__ unsigned wk_pack_rne(float x0, float x1) {
 #endif
 // FULL: D >= every wave's chunk count -- all of a wave's fragments are loaded
 // up front (one memory latency per tile instead of one per D chunks), no refill
-template <int NTP, int D, int NW = 4, bool FULL = false>
+// APL: A given as split3 planes (GemmArgs.asplit, 3-term form only)
+template <int NTP, int D, int NW = 4, bool FULL = false, bool APL = false>
 __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) {
+  static_assert(!APL || NTP == 3, "A planes: 3-term form");
   constexpr int FM = 2, FN = 2, NTH = 64 * NW, NT4 = FM * FN * 256;
   __shared__ GemmArgs s_args;
   __shared__ __attribute__((aligned(16))) float red[NW][FM * FN * 4][64];
@@ -1900,20 +1902,32 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) 
   const int c0 = (nkc * wave) / NW, c1 = (nkc * (wave + 1)) / NW;
   const int clast = max(c1 - 1, 0);
   unsigned oa[FM];
+  const unsigned short* asp = APL ? dr_uni(g.asplit) : nullptr;
+  const unsigned aps = APL ? (unsigned)dr_uni((int)g.asplit_ps) : 0u;
+  const int ald = APL ? dr_uni(g.asplit_ld) : 0;
 #pragma unroll
-  for (int i = 0; i < FM; ++i) oa[i] = (unsigned)(min(m0 + 16 * i + r, M - 1) * lda);
+  for (int i = 0; i < FM; ++i) oa[i] = (unsigned)(min(m0 + 16 * i + r, M - 1) * (APL ? ald : lda));
   unsigned ob[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) ob[j] = (unsigned)(n0 + 16 * j + r) * 32u + 8u * q;  // within a plane (Np >= n rows)
-  f32x4 ra[D][FM][2];
+  f32x4 ra[APL ? 1 : D][FM][2];
+  wk_u32x4 rap[APL ? D : 1][3][FM];
   wk_u32x4 rb[D][NTP][FN];
   auto load = [&](int c, int sl) {
     const int k = 32 * c + 8 * q;
     const unsigned kk = k < K ? (unsigned)k : 0u;
+    if constexpr (APL) {
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      ra[sl][i][0] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)A + ((oa[i] + kk) << 2));
-      ra[sl][i][1] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)A + ((oa[i] + kk + 4) << 2));
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          rap[sl][p][i] = *(const DR_GLOBAL wk_u32x4*)((const DR_GLOBAL char*)asp + ((p * aps + oa[i] + kk) << 1));
+    } else {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        ra[sl][i][0] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)A + ((oa[i] + kk) << 2));
+        ra[sl][i][1] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)A + ((oa[i] + kk + 4) << 2));
+      }
     }
 #pragma unroll
     for (int p = 0; p < NTP; ++p)
@@ -1949,7 +1963,12 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) 
       wk_u32x4 a[NTP][FM];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        f32x4 x0 = ra[u][i][0], x1 = ra[u][i][1];
+        if constexpr (APL) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) a[p % NTP][i] = kin ? rap[u][p][i] : (wk_u32x4){0u, 0u, 0u, 0u};
+          continue;
+        }
+        f32x4 x0 = ra[APL ? 0 : u][i][0], x1 = ra[APL ? 0 : u][i][1];
         if (!kin) x0 = x1 = (f32x4){0.f, 0.f, 0.f, 0.f};
         if constexpr (NTP == 3) {
           unsigned h[4], m[4], l[4];
@@ -2552,11 +2571,17 @@ static bool wks3_ok(const GemmBatch& gb, int count) {
 #endif
 static void launch_wks3(const GemmBatch& gb, int count, hipStream_t s, bool bf16) {
   int tot = 0, maxt = 0, nkc = 0;
+  bool apl = !bf16;
   for (int i = 0; i < count; ++i) {
-    const int t = dr_cdiv(gb.p[i].M, 32) * dr_cdiv(gb.p[i].N, 32);
+    const GemmArgs& g = gb.p[i];
+    const int t = dr_cdiv(g.M, 32) * dr_cdiv(g.N, 32);
     tot += t;
     maxt = std::max(maxt, t);
-    nkc = std::max(nkc, dr_cdiv(gb.p[i].K, 32));
+    nkc = std::max(nkc, dr_cdiv(g.K, 32));
+    // A planes: every problem's, 16-byte rows covering K rounded up to 32
+    apl = apl && g.asplit && ((uintptr_t)g.asplit & 15) == 0 && g.asplit_ld % 8 == 0 &&
+          g.asplit_ld >= (g.K + 31) / 32 * 32 && g.asplit_ps >= (long long)g.M * g.asplit_ld &&
+          3 * g.asplit_ps < (1LL << 30);
   }
   const int npack = count > 1 ? count : 0;
   const dim3 grid(dr_xcd_grid(npack ? tot : maxt));
@@ -2577,6 +2602,8 @@ static void launch_wks3(const GemmBatch& gb, int count, hipStream_t s, bool bf16
     }
   } else if (bf16) {
     DR_WKS3_L(1, 2, false);
+  } else if (apl) {
+    hipLaunchKernelGGL((k_gemm_wks3<3, 2, NW, false, true>), grid, dim3(64 * NW), 0, s, gb, npack);
   } else {
     DR_WKS3_L(3, 2, false);
   }

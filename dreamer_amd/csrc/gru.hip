@@ -473,6 +473,16 @@ __global__ __launch_bounds__(GG_NT) void k_gru_gates(GruArgs ga) {
       no[e] = nn;
     }
     dr_st4(g.hout, (unsigned)(gm * (int)g.ldo + gj), make_float4(ho[0], ho[1], ho[2], ho[3]));
+    if (g.hplanes) {  // split3 planes of h' for the next grouped product (k_gemm_wks3's A)
+      unsigned h0, m0_, l0, h1, m1, l1;
+      split3_pair(ho[0], ho[1], h0, m0_, l0);
+      split3_pair(ho[2], ho[3], h1, m1, l1);
+      const long long ps = (long long)B * g.hp_ld, o = (long long)gm * g.hp_ld + gj;
+      typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<u32x2_t*>(g.hplanes + o) = (u32x2_t){h0, h1};
+      *reinterpret_cast<u32x2_t*>(g.hplanes + ps + o) = (u32x2_t){m0_, m1};
+      *reinterpret_cast<u32x2_t*>(g.hplanes + 2 * ps + o) = (u32x2_t){l0, l1};
+    }
     if (g.sr) {
       const unsigned o = (unsigned)(gm * Hd + gj);
       dr_st4(g.sr, o, make_float4(ro[0], ro[1], ro[2], ro[3]));
@@ -643,7 +653,7 @@ __global__ __launch_bounds__(GL_NT) void k_gru_gates_lds(GruArgs ga) {
 
 static bool gates_lds_ok(const GruArgs& g) {
   const int L = g.R * g.C;
-  return g.wtb && ((uintptr_t)g.wtb & 15) == 0 && g.Hd % GL_UNITS == 0 && g.R % 4 == 0 && (L + g.A) * 3 <= GL_WMAX * GL_NT && g.ldo % 2 == 0 &&
+  return g.wtb && !g.hplanes && ((uintptr_t)g.wtb & 15) == 0 && g.Hd % GL_UNITS == 0 && g.R % 4 == 0 && (L + g.A) * 3 <= GL_WMAX * GL_NT && g.ldo % 2 == 0 &&
          (!g.h || g.ldh % 2 == 0) && (g.lda >= g.A) && gates_lds_bytes(L, g.A) <= 64 * 1024 &&
          (((uintptr_t)g.idx | (uintptr_t)g.zval) & 15) == 0 &&
          (((uintptr_t)g.gh_ws | (uintptr_t)g.h | (uintptr_t)g.hout | (uintptr_t)g.b_ih | (uintptr_t)g.b_hh) & 7) == 0;
@@ -774,6 +784,10 @@ int op_gru_fused(const GruArgs& g, hipStream_t s) {
     dr_set_error("gru_fused: operands exceed 32-bit offsets");
     return DR_E_INVALID;
   }
+  if (g.hplanes && (g.hp_ld % 4 != 0 || g.hp_ld < g.Hd || ((uintptr_t)g.hplanes & 15))) {
+    dr_set_error("gru_fused: h planes need a 16-byte aligned buffer and a row stride >= Hd, % 4 == 0");
+    return DR_E_INVALID;
+  }
   if (g.gh_ws && g.B >= 128 && ((uintptr_t)g.gh_ws | (uintptr_t)g.hout | (uintptr_t)g.sr | (uintptr_t)g.su |
                                  (uintptr_t)g.sn | (uintptr_t)g.sghn) % 16 == 0 && g.ldo % 4 == 0) {
     // split path: hidden product on the tile GEMM, then gather + gates
@@ -799,6 +813,10 @@ int op_gru_fused(const GruArgs& g, hipStream_t s) {
       default: hipLaunchKernelGGL(k_gru_gates<8>, dim3(dr_xcd_grid(tiles)), dim3(GG_NT), 0, s, g); break;
     }
     return dr_check_launch("gru_gates");
+  }
+  if (g.hplanes) {
+    dr_set_error("gru_fused: h planes are written by the split path only (B >= 128 with gh scratch)");
+    return DR_E_INVALID;
   }
   const int tiles = ((g.Hd + 15) / 16) * ((g.B + 15) / 16);
   hipLaunchKernelGGL(k_gru_fused, dim3(dr_xcd_grid(tiles)), dim3(512), 0, s, g);
