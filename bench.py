@@ -490,13 +490,21 @@ def main():
         # AC_epochs = 2 (car_racer_config.yaml): the warm start of epoch e+1 overlaps epoch e's update
         d.AC_epochs, d.pipeline_epochs = 2, True
         el2, _ = time_train_agent(d, max(2, args.steps // 2), 2)
+        # the same schedule over 10 epochs per call (one warm start exposed per call instead of one in two)
+        d.AC_epochs = 10
+        el10, _ = time_train_agent(d, 2, 1)
         d.AC_epochs, d.pipeline_epochs = 1, False
         secondary["ac_epochs2_pipelined"] = {
             "value": round(world * B * H * 2 * max(2, args.steps // 2) / el2, 1), "unit": "imagined latent-steps/s",
             "ms_per_epoch": round(el2 / (2 * max(2, args.steps // 2)) * 1e3, 4),
-            "note": "Dreamer.train_Agent() with AC_epochs=2 and the opt-in pipeline_epochs config key: the warm "
-                    "start of epoch e+1 on a second stream beside epoch e's update (equal to the sequential epochs "
-                    "in tests/test_gpu_parity.py; off by default, DESIGN.md 5a)"}
+            "vs_sequential": round((el / args.steps) / (el2 / (2 * max(2, args.steps // 2))), 4),
+            "ac_epochs10": {"value": round(world * B * H * 10 * 2 / el10, 1),
+                            "ms_per_epoch": round(el10 / 20 * 1e3, 4),
+                            "vs_sequential": round((el / args.steps) / (el10 / 20), 4)},
+            "note": "Dreamer.train_Agent() with AC_epochs=2 (and 10) and the opt-in pipeline_epochs config key: the "
+                    "warm start of epoch e+1 on a stream fenced to 7/8 of the CUs beside epoch e's update on a "
+                    "high-priority stream (equal to the sequential epochs in tests/test_gpu_parity.py; off by "
+                    "default, DESIGN.md 5a)"}
         if (B, S, H, res) != (64, 64, 15, 64):
             _, d64 = make_dreamer(CAR_RACER, dev, 64, 64, 15, 64, 1, world, rank, group, args.precision)
             el64, _ = time_train_agent(d64, args.steps, args.warmup)

@@ -68,6 +68,12 @@ __device__ __forceinline__ u32x2 pack_bf16x4(f32x4 v) {
 __device__ __forceinline__ unsigned pack_bf16x2(float x0, float x1) { return b16bits((__bf16)x0) | (b16bits((__bf16)x1) << 16); }
 }  // namespace
 
+// A/B knobs (MI355X guide T5): DR_CONV_PRIO 1 = s_setprio(1) around each
+// chunk's MFMA cluster; 2 = the static form, priority 1 for the younger half
+// of the workgroup's waves before the main loop
+#ifndef DR_CONV_PRIO
+#define DR_CONV_PRIO 0
+#endif
 // EPI (conv.h): CONV_EPI_FWD: out = SiLU(acc + bias), optionally pre = acc + bias
 // (NHWC, for the world-model backward); CONV_EPI_DSILU (NHWC only, no bias):
 // out = acc * SiLU'(pre) -- the input gradient of a transposed conv followed by
@@ -237,6 +243,7 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
 #define DR_S3(PA, PB)                                                                                   \
   _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
       OUT_NCHW ? mfma_b16(a[PA][i], b[PB][j], acc[i][j]) : mfma_b16(b[PB][j], a[PA][i], acc[i][j]);
+    if (DR_CONV_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     if constexpr (NT3 == 3) {
       DR_S3(2, 0)
       DR_S3(1, 1)
@@ -245,11 +252,13 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
       DR_S3(0, 1)
     }
     DR_S3(0, 0)
+    if (DR_CONV_PRIO == 1) __builtin_amdgcn_s_setprio(0);
 #undef DR_S3
     if (c + 1 < NCH) store(Next{}, buf ^ 1);
     dr_lds_barrier();
   };
   static_assert(PIPE == 2 && NCH % 2 == 0, "conv_split3 ring");
+  if (DR_CONV_PRIO == 2 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= NT / 2) __builtin_amdgcn_s_setprio(1);
   for (int c = 0; c < NCH; c += 2) {
     step(c, S0{});
     step(c + 1, S1{});
@@ -570,6 +579,7 @@ __global__ __launch_bounds__(64 * NW, NTM == 1 ? DR_E12S1_OCC : 1) void k_enc12_
 #define E12_S3(PW, PA)                       \
   _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int jj = 0; jj < 2; ++jj) acc[i][jj] = \
       mfma_b16(wf[PW][jj], pf[PA][i], acc[i][jj]);
+      if (DR_CONV_PRIO == 1) __builtin_amdgcn_s_setprio(1);
       if constexpr (NTM == 3) {
         E12_S3(2, 0)
         E12_S3(1, 1)
@@ -578,8 +588,10 @@ __global__ __launch_bounds__(64 * NW, NTM == 1 ? DR_E12S1_OCC : 1) void k_enc12_
         E12_S3(0, 1)
       }
       E12_S3(0, 0)
+      if (DR_CONV_PRIO == 1) __builtin_amdgcn_s_setprio(0);
 #undef E12_S3
     };
+    if (DR_CONV_PRIO == 2 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= NTH / 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll 1
     for (int tap = TAPS * kh; tap < TAPS * (kh + 1); ++tap) {
       tap_step(tap, wfa, wfb);

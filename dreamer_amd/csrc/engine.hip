@@ -15,7 +15,7 @@
 #define DR_GRU_BWD_EPI 1  // A/B knob: 0 = the GRU backward as its own elementwise launch
 #endif
 #ifndef DR_ACTOR_TAIL_BWD
-#define DR_ACTOR_TAIL_BWD 1  // A/B knob: 0 = head backward + two LN-backward launches + the fused product
+#define DR_ACTOR_TAIL_BWD 0  // A/B knob: 1 = k_actor_tail_bwd (perf-neutral, r04d; its B = 4096 / B = 512 actor gradients disagreed with the oracle / 8-rank runs, r04v -- off)
 #endif
 #ifndef DR_ACTOR_TAIL
 #define DR_ACTOR_TAIL 0  // A/B knob (tools/build_variant.py): 0 = z-gather + two skinny launches

@@ -465,7 +465,7 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
       const long long sz = M1 * D.pix[N - k - 1] * D.cd[k + 1];
       // the last layer's input is never stored post-SiLU: its two readers (the
       // fused tanh-MSE layer, its weight gradient) apply SiLU on load -- the
-      // largest activation of the step (B = 256: 1.9 GB) written once less
+      // 32-channel activation (B = 256: 470 MB) written once less
       w.dq[k] = c.f(sz); w.dqp[k] = k == N - 2 ? nullptr : c.f(sz); w.dgq[k] = c.f(sz);
     }
   }

@@ -29,6 +29,16 @@ WARM_STREAM = 1 << 24
 DREAM_STREAM = 2 << 24
 
 
+def cu_mask_words(n_cus, fraction):
+    """The 32-bit words of a CU mask keeping the first round(n_cus * fraction)
+    CUs (at least one, at most all) of the device's CU-mask order."""
+    keep = max(1, min(n_cus, int(round(n_cus * fraction))))
+    words = [0] * ((n_cus + 31) // 32)
+    for i in range(keep):
+        words[i // 32] |= 1 << (i % 32)
+    return words
+
+
 class ImaginationEngine:
     def __init__(self, dreamer, B=None, world=None, use_graph=True):
         self.dr = dreamer
@@ -386,13 +396,10 @@ class ImaginationEngine:
         n = ctypes.c_int(0)
         with torch.cuda.device(self.dev):
             L.call("dr_device_cus", ctypes.byref(n))
-            keep = max(1, min(n.value, int(round(n.value * cu_fraction))))
-            words = (n.value + 31) // 32
-            mask = (ctypes.c_uint * words)()
-            for i in range(keep):
-                mask[i // 32] |= 1 << (i % 32)
+            words = cu_mask_words(n.value, cu_fraction)
+            mask = (ctypes.c_uint * len(words))(*words)
             h = ctypes.c_void_p()
-            L.call("dr_stream_create_cumask", words, mask, ctypes.byref(h))
+            L.call("dr_stream_create_cumask", len(words), mask, ctypes.byref(h))
         self._masked_streams = getattr(self, "_masked_streams", []) + [h]
         return torch.cuda.ExternalStream(h.value, device=self.dev)
 

@@ -247,3 +247,17 @@ def test_tn_split3_predicate_covers_its_limits():
     assert f(200, 4736, 160000) == 0      # > 2^31 plane elements
     assert f(200, 1624, 61440) == 1       # the critic's first layer at B = 4096, H + 1 = 16 (configs[4])
     assert f(0, 10, 10) == 0 and f(10, 10, 0) == 0
+
+
+def test_cu_mask_words():
+    """The fenced warm stream's CU mask (engine.cu_mask_words): 7/8 of 256 CUs
+    keeps CUs 0-223 (words 0-6 full, word 7 empty); a fraction never keeps zero
+    CUs or more than the device has; a partial word sets its low bits."""
+    from dreamer_amd.engine import cu_mask_words
+    w = cu_mask_words(256, 0.875)
+    assert len(w) == 8 and w[:7] == [0xFFFFFFFF] * 7 and w[7] == 0
+    assert sum(bin(x).count("1") for x in cu_mask_words(256, 0.75)) == 192
+    assert cu_mask_words(256, 0.0001) == [1] + [0] * 7
+    assert sum(bin(x).count("1") for x in cu_mask_words(304, 1.5)) == 304
+    w = cu_mask_words(40, 0.5)
+    assert w == [0xFFFFF, 0]
