@@ -2185,7 +2185,22 @@ static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
   int tiles16 = 0;
   for (int i = 0; i < count; ++i)
     tiles16 += dr_cdiv(gb.p[i].M, maxM > 64 ? 64 : 16) * dr_cdiv(gb.p[i].N, 16);
-  const bool wide = g_skinny_variant != 2 && maxM <= 64 && tiles16 > 256;
+  bool wide = g_skinny_variant != 2 && maxM <= 64 && tiles16 > 256;
+  // the backward prologues exist only on the staged path (A and weight rows of
+  // the tile in LDS, k_gemm_skinny `staged`): a tile whose rows do not fit
+  // would read the raw operand.  At K = 1024 (the STE backward of a 32 x 32
+  // latent) the 32-column tile does not fit (48 x 1032 floats), so a B = 512
+  // grid (416 16-column tiles) stays on 16 columns
+  if (AMODE == AM_LNBWD || AMODE == AM_STEBWD) {
+    const int mt = maxM > 64 ? 64 : 16;
+    for (int i = 0; i < count; ++i) {
+      const int K = gb.p[i].K, KP = K + ((8 - (K & 15)) & 15);
+      const int nt = (epi == EPI_SAMPLE || wide) ? 32 : 16;
+      if ((mt + nt) * KP > SK_LN_MAXF && nt == 32 && epi != EPI_SAMPLE) wide = false;
+      if ((mt + (wide || epi == EPI_SAMPLE ? 32 : 16)) * KP > SK_LN_MAXF || K / 4 > 64 * (mt == 16 ? 4 : 1) || !vec)
+        return false;
+    }
+  }
   if (epi == EPI_SAMPLE) {
     if (maxM > 64) launch_skinny<64, 32, AMODE, B_KN, EPI_SAMPLE>(gb, count, vec, s);
     else launch_skinny<16, 32, AMODE, B_KN, EPI_SAMPLE>(gb, count, vec, s);

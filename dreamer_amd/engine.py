@@ -478,6 +478,7 @@ class ImaginationEngine:
         return self._run_many(P, G, starts_list, outer)
 
     def _run_many(self, P, G, starts_list, main):
+        import os
         K = len(starts_list)
         ag = self.dr.agent
         ws = P["stream"]
@@ -488,15 +489,24 @@ class ImaginationEngine:
             dst = host.to(self.dev, non_blocking=True)
             P["rng"].copy_(self.rng.state)
         ev_w, ev_i = [None] * K, [None] * K
+        # DREAMER_WARM0_MAIN: the first warm start has nothing to overlap with,
+        # so it runs on the chain's stream over all CUs (the fenced stream
+        # would only slow it); the later ones follow it on the fenced stream
+        warm0_main = os.environ.get("DREAMER_WARM0_MAIN", "1") == "1"
 
         def issue_warm(e):
-            with torch.cuda.stream(ws):
+            s = main if (e == 0 and warm0_main) else ws
+            if s is main:
+                main.wait_stream(ws)  # the window starts / Philox copies above
+            elif e == 1 and warm0_main:
+                ws.wait_event(ev_w[0])  # warm starts share their staging buffers
+            with torch.cuda.stream(s):
                 if e >= 2:
-                    ws.wait_event(ev_i[e - 2])
+                    s.wait_event(ev_i[e - 2])
                 self.starts.copy_(dst[e])
                 G[("warm", e & 1)].replay()
                 ev_w[e] = torch.cuda.Event()
-                ev_w[e].record(ws)
+                ev_w[e].record(s)
 
         xs = P["side"]
         import os

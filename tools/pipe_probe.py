@@ -10,7 +10,9 @@ CASE: "seq" (K sequential engine.run epochs), "pipe" (run_many as shipped),
 "after:<fraction>" (sequential epochs timed before and after a pipelined run),
 or "pipe:<warm CU fraction>:<chain priority>" -- the warm stream restricted
 to that share of the CUs (engine.warm_stream; 1 = no mask) and the chain on a
-stream of the given torch priority (0 = normal, -1 = high).  Prints one JSON
+stream of the given torch priority (0 = normal, -1 = high); an optional 4th
+field sets DREAMER_WARM0_MAIN (1: the first warm start of a call on the chain's
+stream over all CUs).  Prints one JSON
 line: ms per epoch (best of 3 timed K-epoch runs at B = 256)."""
 import json
 import os
@@ -33,6 +35,8 @@ def main():
         os.environ["DREAMER_WARM_CUS"] = parts[1]
     if len(parts) > 2:
         os.environ["DREAMER_CHAIN_PRIORITY"] = parts[2]
+    if len(parts) > 3:
+        os.environ["DREAMER_WARM0_MAIN"] = parts[3]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     B = 256
@@ -41,7 +45,7 @@ def main():
     rng = np.random.RandomState(3)
     starts = [rng.randint(0, 4096 - 64, size=B) for _ in range(K)]
 
-    def timed(fn, reps=3):
+    def timed(fn, reps=max(3, 30 // K)):
         fn()
         torch.cuda.synchronize()
         best = 1e9
@@ -77,6 +81,7 @@ def main():
         res["ms_per_epoch"] = round(timed(lambda: eng.run_many(starts)), 4)
         res["warm_cus"] = os.environ.get("DREAMER_WARM_CUS")
         res["chain_priority"] = os.environ.get("DREAMER_CHAIN_PRIORITY")
+        res["warm0_main"] = os.environ.get("DREAMER_WARM0_MAIN")
     print(json.dumps(res), flush=True)
 
 
