@@ -147,6 +147,16 @@ __device__ __forceinline__ void dr_st4(float* base, unsigned e, float4 v) {
 __device__ __forceinline__ float dr_silu_fast(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
 }
+// tanh on the hardware exp2 / rcp: 1 - 2 / (e^{2x} + 1) (saturates to +-1)
+__device__ __forceinline__ float dr_tanh_fast(float x) {
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(x * 2.8853900817779268f) + 1.0f);
+}
+// d SiLU / dx on the hardware exp2 / rcp (the conv epilogues over 10^8
+// elements: the IEEE expf + division cost ~30 VALU per element there)
+__device__ __forceinline__ float dr_dsilu_fast(float x) {
+  const float s = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+  return s * (1.0f + x * (1.0f - s));
+}
 
 // XCD-aware tile order.  Workgroups are dealt to the 8 XCDs round-robin
 // (block b runs on XCD b % 8, each XCD has its own L2).  Mapping block b to

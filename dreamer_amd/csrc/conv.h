@@ -11,10 +11,12 @@ int op_conv_nhwc(int n, int cin, int ih, int iw, int cout, const float* in, cons
                  float* out, int out_nchw, hipStream_t s);
 enum { CONV_EPI_FWD = 0, CONV_EPI_DSILU = 1 };
 // as op_conv_nhwc, plus: pre (optional with CONV_EPI_FWD) receives acc + bias
-// in NHWC; CONV_EPI_DSILU writes acc * SiLU'(pre) (no bias, NHWC out).
+// in NHWC; CONV_EPI_DSILU writes acc * SiLU'(pre) (no bias, NHWC out) and, with
+// csum, each 128-pixel tile's per-channel sums of that output:
+// csum[tile][cout], tiles = ceil(n * oh * ow / 128) (op_chan_sum_final reduces them).
 int op_conv_nhwc_ex(int n, int cin, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
-                    float* out, int out_nchw, float* pre, int epi, hipStream_t s);
-int op_frames_nhwc4(int n, int nb, int h, int w, const dr_frames* src, float* out, hipStream_t s);
+                    float* out, int out_nchw, float* pre, int epi, hipStream_t s, float* csum = nullptr);
+int op_frames_nhwc4(int n, int nb, int h, int w, const dr_frames* src, float* out, hipStream_t s, float pad = 0.0f);
 // first conv straight from the frames (u8 ring or f32 tensor): the frame rows
 // a tile reads are normalised into LDS once, no NHWC4 f32 copy in HBM.  Same
 // fragments and MFMA order as op_frames_nhwc4 + k_conv1_direct: bitwise equal.
@@ -118,6 +120,7 @@ struct ConvTArgs {
   int tstride;
   const float* coef;    // [n]
   float* part;          // [n][parts_per_frame()]
+  float* bpart;         // CT_EPI_TANH_MSE, optional: [n][parts_per_frame()][3] sums of out (bias-gradient partials)
 };
 int op_convT_repack(int cin, int cout, const float* wt, float* wq, hipStream_t s);
 int op_convT_nhwc(int epi, const ConvTArgs& a, hipStream_t s);
@@ -156,12 +159,17 @@ int op_wgrad_split3(int n, int h, int w, int ca, int cb, const float* lo, int ld
                     float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s,
                     int terms = 3);
 // dW has cbo <= cb channels per row (cbo < cb when hi carries zero padding channels).
+// bias_out (optional): hi's channel cbo is a pad of ones (op_frames_nhwc4 pad = 1),
+// so its tap-(1, 1) column is sum_k lo[k][a]: bias_out[a] (+)= scale * that.
 int op_conv_wgrad(int n, int h, int w, int ca, int cb, const float* lo, int lda, int lo_silu, const float* hi, int ldb,
-                  float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s);
+                  float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s,
+                  float* bias_out = nullptr);
 // out[c] (+)= sum_r X[r][c] for c < C (row stride ldx); two deterministic passes
 size_t op_chan_sum_ws_floats(long long rows, int C);
 int op_chan_sum(long long rows, int C, const float* X, int ldx, float* out, int accumulate, float* ws, size_t ws_floats,
                 hipStream_t s);
+// out[c] (+)= sum_b part[b][c] over nb partial rows (fixed order)
+int op_chan_sum_final(int nb, int C, const float* part, float* out, int accumulate, hipStream_t s);
 
 // TN products dW[m][n] = sum_k G[k][m] X[k][n] (Linear weight gradients over
 // K rows; X columns n >= nsplitB from X2[k][n - nsplitB]) f32-accurate on the

@@ -28,7 +28,7 @@ template <int BM, int BN, int CIN, bool OUT_NCHW, int EPI>
 __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw, int cout,
                                                    const float* __restrict__ in, const float* __restrict__ wr,
                                                    const float* __restrict__ bias, float* __restrict__ out,
-                                                   float* __restrict__ pre) {
+                                                   float* __restrict__ pre, float* __restrict__ csum) {
   constexpr int K = CIN * 16;
   constexpr int APT = BM / 32;  // pixel rows loaded per thread (8 float4 per 32-k row)
   constexpr int BPT = BN >= 32 ? BN / 32 : 1;
@@ -174,6 +174,11 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
   // holds channels 4q..4q+3 of pixel r and stores float4s along c.  NCHW
   // output: pixels are the A operand, so the lane holds 4 consecutive pixels
   // of channel r, one float4 along the plane (hw % 4 == 0, checked on the host).
+  float cs[FN][4];  // CONV_EPI_DSILU with csum: this lane's channel sums
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cs[j][e] = 0.f;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -200,7 +205,9 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
         if (EPI == CONV_EPI_DSILU) {
           const f32x4 pv = *reinterpret_cast<const f32x4*>(pre + m * cout + co);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * dr_dsilu(pv[e]);
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * dr_dsilu_fast(pv[e]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) cs[j][e] += v[e];
         } else {
           const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + co);
 #pragma unroll
@@ -212,6 +219,31 @@ __global__ __launch_bounds__(256) void k_conv_nhwc(int n_frames, int ih, int iw,
         *reinterpret_cast<f32x4*>(out + m * cout + co) = v;
       }
     }
+  // CONV_EPI_DSILU with csum: the tile's per-channel sums of its output (the
+  // next layer's bias-gradient partials), fixed order: lanes of one channel
+  // (xor over r), then the WM waves of one column block in LDS
+  if (EPI == CONV_EPI_DSILU && !OUT_NCHW && csum) {
+    float* s_cs = &As[0][0][0];  // the staging buffers are free after the K loop
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = cs[j][e];
+        t += __shfl_xor(t, 1, 64);
+        t += __shfl_xor(t, 2, 64);
+        t += __shfl_xor(t, 4, 64);
+        t += __shfl_xor(t, 8, 64);
+        if (r == 0) s_cs[(wave / WN) * BN + wn0 + 16 * j + 4 * q + e] = t;
+      }
+    __syncthreads();
+    if (tid < BN && n0 + tid < cout) {
+      float t = 0.f;
+#pragma unroll
+      for (int wm = 0; wm < WM; ++wm) t += s_cs[wm * BN + tid];
+      csum[(m0 / BM) * cout + n0 + tid] = t;
+    }
+  }
 }
 
 // First layer (CIN = 4, K = 64): no LDS.  Every MFMA fragment piece is one
@@ -508,7 +540,7 @@ int op_conv1_frames(int n, int nb, int ih, int iw, int cout, const dr_frames* sr
 
 template <int BM, int BN, int CIN, bool OUT_NCHW, int EPI>
 static int launch_conv(int n, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
-                       float* out, float* pre, hipStream_t s) {
+                       float* out, float* pre, hipStream_t s, float* csum = nullptr) {
   if (cout % 4 != 0 || (OUT_NCHW && ((ih / 2) * (iw / 2)) % 4 != 0)) {
     dr_set_error("conv: float4 epilogue needs cout %% 4 == 0 (and oh*ow %% 4 == 0 for NCHW output)");
     return DR_E_INVALID;
@@ -527,12 +559,16 @@ static int launch_conv(int n, int ih, int iw, int cout, const float* in, const f
   }();
   (void)raised;
   hipLaunchKernelGGL((k_conv_nhwc<BM, BN, CIN, OUT_NCHW, EPI>), grid, dim3(256), 0, s, n, ih, iw, cout,
-                     in, wr, bias, out, pre);
+                     in, wr, bias, out, pre, csum);
   return dr_check_launch("conv");
 }
 
 int op_conv_nhwc_ex(int n, int cin, int ih, int iw, int cout, const float* in, const float* wr, const float* bias,
-                    float* out, int out_nchw, float* pre, int epi, hipStream_t s) {
+                    float* out, int out_nchw, float* pre, int epi, hipStream_t s, float* csum) {
+  if (csum && (epi != CONV_EPI_DSILU || out_nchw)) {
+    dr_set_error("conv: channel sums only with the NHWC SiLU-backward epilogue");
+    return DR_E_INVALID;
+  }
   if (cin == 4 && epi == CONV_EPI_FWD && !out_nchw && cout % 32 == 0) {
     const long long tiles = (((long long)n * (ih / 2) * (iw / 2) + 127) / 128) * (cout / 32);
     if (tiles >= (1LL << 30)) {
@@ -549,7 +585,7 @@ int op_conv_nhwc_ex(int n, int cin, int ih, int iw, int cout, const float* in, c
   }
 #define DR_CONV_L(BM, BN, C, NCHW)                                                                \
   (epi == CONV_EPI_DSILU                                                                          \
-       ? launch_conv<BM, BN, C, NCHW, CONV_EPI_DSILU>(n, ih, iw, cout, in, wr, bias, out, pre, s) \
+       ? launch_conv<BM, BN, C, NCHW, CONV_EPI_DSILU>(n, ih, iw, cout, in, wr, bias, out, pre, s, csum) \
        : launch_conv<BM, BN, C, NCHW, CONV_EPI_FWD>(n, ih, iw, cout, in, wr, bias, out, pre, s))
 #define DR_CONV_CASE(C)                                                                                     \
   if (cin == C) {                                                                                           \
@@ -580,9 +616,12 @@ int op_conv_nhwc(int n, int cin, int ih, int iw, int cout, const float* in, cons
 }
 
 // frames (u8 replay ring or f32 tensor, NCHW 3 channels) -> normalised f32
-// NHWC with 4 channels (channel 3 = 0), frame f = t*nb + b.  x/255 - 0.5 is
+// NHWC with 4 channels (channel 3 = pad, 0 or 1), frame f = t*nb + b.  x/255 - 0.5 is
 // evaluated exactly as the reference does (IEEE div, then sub; Dreamer.py:251).
-__global__ void k_frames_nhwc4(int n, int nb, int h, int w, dr_frames src, float* out) {
+// pad = 1 (the world-model step): conv1's weight gradient then also yields its
+// bias gradient in the pad column (op_conv_wgrad's bias_out); the pad channel
+// meets only zero weights in the forward convs.
+__global__ void k_frames_nhwc4(int n, int nb, int h, int w, dr_frames src, float* out, float pad) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // (f, y, x)
   const long long hw = (long long)h * w;
   if (i >= (long long)n * hw) return;
@@ -603,12 +642,13 @@ __global__ void k_frames_nhwc4(int n, int nb, int h, int w, dr_frames src, float
 #pragma unroll
     for (int c = 0; c < 3; ++c) v[c] = v[c] / 255.0f - 0.5f;
   }
-  reinterpret_cast<float4*>(out)[i] = make_float4(v[0], v[1], v[2], 0.0f);
+  reinterpret_cast<float4*>(out)[i] = make_float4(v[0], v[1], v[2], pad);
 }
 
-int op_frames_nhwc4(int n, int nb, int h, int w, const dr_frames* src, float* out, hipStream_t s) {
+int op_frames_nhwc4(int n, int nb, int h, int w, const dr_frames* src, float* out, hipStream_t s, float pad) {
   const long long total = (long long)n * h * w;
-  hipLaunchKernelGGL(k_frames_nhwc4, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, n, nb, h, w, *src, out);
+  hipLaunchKernelGGL(k_frames_nhwc4, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, n, nb, h, w, *src, out,
+                     pad);
   return dr_check_launch("frames_nhwc4");
 }
 

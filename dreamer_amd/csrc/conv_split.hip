@@ -299,7 +299,7 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
         if (EPI == CONV_EPI_DSILU) {
           const f32x4 pv = *reinterpret_cast<const f32x4*>(pre + m * cout + co);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * dr_dsilu(pv[e]);
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * dr_dsilu_fast(pv[e]);
         } else {
           const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + co);
 #pragma unroll
@@ -1042,14 +1042,14 @@ __global__ __launch_bounds__(BM * 2) void k_convT_split3(ConvTArgs a, const u16*
         f32x4 sv = v;
         if (a.out2 || a.silu_out) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) sv[e] = dr_silu(v[e]);
+          for (int e = 0; e < 4; ++e) sv[e] = dr_silu_fast(v[e]);
         }
         *reinterpret_cast<f32x4*>(a.out + opix * cout + co) = a.silu_out ? sv : v;
         if (a.out2) *reinterpret_cast<f32x4*>(a.out2 + opix * cout + co) = sv;
       } else {
         const f32x4 pv = *reinterpret_cast<const f32x4*>(a.pre + opix * cout + co);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = v[e] * dr_dsilu(pv[e]);
+        for (int e = 0; e < 4; ++e) v[e] = v[e] * dr_dsilu_fast(pv[e]);
         *reinterpret_cast<f32x4*>(a.out + opix * cout + co) = v;
       }
     }
@@ -1673,21 +1673,36 @@ static int s3_pad(int n) { return (n + 127) / 128 * 128; }
 // thread = (column n, 32-row chunk kc): 32 rows of one column (coalesced over
 // the threads of a row), split and written as three 64-byte plane runs
 // (TERMS = 1: plane 0 only, RNE -- the bf16 world-model step)
+struct KnRepack {
+  int K, N, P, nsplit;
+  const float* X;
+  const float* X2;
+  long long ldx, ldx2;
+  u16* wr;
+};
+
 template <int TERMS>
-__global__ __launch_bounds__(256) void k_kn_repack_split3(int K, int N, int P, const float* __restrict__ X, long long ldx,
-                                                          const float* __restrict__ X2, long long ldx2, int nsplit,
-                                                          u16* __restrict__ wr) {
+__device__ __forceinline__ void kn_repack_body(int K, int N, int P, const float* __restrict__ X, long long ldx,
+                                               const float* __restrict__ X2, long long ldx2, int nsplit,
+                                               u16* __restrict__ wr) {
   const int n = blockIdx.x * 256 + threadIdx.x, kc = blockIdx.y;
   if (n >= P) return;
   const bool seg2 = n >= nsplit;
   const float* src = seg2 ? X2 : X;
   const long long ld = seg2 ? ldx2 : ldx;
   const int nn = seg2 ? n - nsplit : n;
+  // unconditional loads (clamped address, zeroed after): a bounds-checked
+  // load compiled to a branch that waited for each of the 32 loads in turn
+  // (16 us per world-model weight-gradient repack, r04zc)
   float v[32];
+  const bool nok = n < N;
+  const float* col = src + (nok ? nn : 0);
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
     const int kk = 32 * kc + k;
-    v[k] = (n < N && kk < K) ? src[(long long)kk * ld + nn] : 0.f;
+    const bool ok = nok && kk < K;
+    const float t = col[ok ? (long long)kk * ld : 0LL];
+    v[k] = ok ? t : 0.f;
   }
   u32x4* o = reinterpret_cast<u32x4*>(wr + (((long long)kc * 3) * P + n) * 32);
   if constexpr (TERMS == 1) {
@@ -1718,6 +1733,20 @@ __global__ __launch_bounds__(256) void k_kn_repack_split3(int K, int N, int P, c
     o[pl + u] = m[u];
     o[2 * pl + u] = l[u];
   }
+}
+
+// both operands of a TN product in one launch (blockIdx.z): the world-model
+// step's ~15 weight-gradient products per step are small enough that the
+// second launch was a visible share of each
+template <int TERMS>
+__global__ __launch_bounds__(256) void k_kn_repack2_split3(KnRepack a, KnRepack b) {
+  // (field-wise selects: a select of the whole by-value struct can be
+  // materialised in scratch)
+  const bool z = blockIdx.z != 0;
+  const int P = z ? b.P : a.P;
+  if ((int)blockIdx.x * 256 >= P) return;
+  kn_repack_body<TERMS>(z ? b.K : a.K, z ? b.N : a.N, P, z ? b.X : a.X, z ? b.ldx : a.ldx, z ? b.X2 : a.X2,
+                        z ? b.ldx2 : a.ldx2, z ? b.nsplit : a.nsplit, z ? b.wr : a.wr);
 }
 
 struct GemmPP {
@@ -1899,12 +1928,13 @@ int op_gemm_tn_split3(int M, int N, int K, const float* G, long long ldg, const 
   u16* wa = reinterpret_cast<u16*>(ws);
   u16* wb = wa + (size_t)KC * 32 * 3 * Mp;
   float* part = reinterpret_cast<float*>(((uintptr_t)(wb + (size_t)KC * 32 * 3 * Np) + 255) & ~(uintptr_t)255);
-  auto repack = terms == 1 ? k_kn_repack_split3<1> : k_kn_repack_split3<3>;
-  hipLaunchKernelGGL(repack, dim3((unsigned)((Mp + 255) / 256), (unsigned)KC), dim3(256), 0, s, K, M, Mp,
-                     G, ldg, G, ldg, M, wa);
-  DR_TRY(dr_check_launch("kn_repack_split3"));
-  hipLaunchKernelGGL(repack, dim3((unsigned)((Np + 255) / 256), (unsigned)KC), dim3(256), 0, s, K, N, Np,
-                     X, ldx, X2 ? X2 : X, ldx2, nsplitB < N ? nsplitB : N, wb);
+  const KnRepack ra = {K, M, Mp, M, G, G, ldg, ldg, wa};
+  const KnRepack rb = {K, N, Np, nsplitB < N ? nsplitB : N, X, X2 ? X2 : X, ldx, X2 ? ldx2 : ldx, wb};
+  const dim3 rgrid((unsigned)((std::max(Mp, Np) + 255) / 256), (unsigned)KC, 2);
+  if (terms == 1)
+    hipLaunchKernelGGL(k_kn_repack2_split3<1>, rgrid, dim3(256), 0, s, ra, rb);
+  else
+    hipLaunchKernelGGL(k_kn_repack2_split3<3>, rgrid, dim3(256), 0, s, ra, rb);
   DR_TRY(dr_check_launch("kn_repack_split3"));
   auto tl = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   const bool big = tl(128, 64) >= 512;

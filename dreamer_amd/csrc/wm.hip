@@ -305,7 +305,8 @@ struct WmWs {
   void *t3d[DR_MAX_DEPTH], *t3e[DR_MAX_DEPTH];
   void* e12w1;  // conv1's split3 weight planes for k_enc12_split3
   // loss
-  float *coef_row, *coef_obs, *obs_part, *kl_grp, *rew_row, *cont_row, *scal, *stats;
+  float *coef_row, *coef_obs, *obs_part, *obs_bpart, *kl_grp, *rew_row, *cont_row, *scal, *stats;
+  float* csp;  // per-tile channel sums of the last decoder layer's input gradient (k_conv_nhwc csum)
   // backward
   float *gH, *gZ, *glog, *gpost, *g_prior, *g_rew, *g_cont;
   MlpBwd bp, br, bc;
@@ -483,6 +484,9 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
   }
   w.coef_row = c.f(M1); w.coef_obs = c.f(M1);
   w.obs_part = c.f(Dv ? M1 : M1 * op_convT_mse_parts(D.IH / 2, D.IW / 2));
+  // the last decoder layer's bias-gradient partials (k_convT_out3), 3 per tile
+  w.obs_bpart = Dv ? nullptr : c.f(3LL * M1 * op_convT_mse_parts(D.IH / 2, D.IW / 2));
+  w.csp = Dv ? nullptr : c.f(((long long)M1 * (D.IH / 2) * (D.IW / 2) + 127) / 128 * D.cd[N - 1]);
   w.kl_grp = c.f(M1 * d->rows); w.rew_row = c.f(M1); w.cont_row = c.f(M1); w.scal = c.f(8); w.stats = c.f(8);
   w.gH = c.f(M * Hd); w.gZ = c.f(M * L); w.glog = c.f(M * L); w.gpost = c.f(M1 * L);
   w.g_prior = c.f(M1 * L); w.g_rew = c.f(M1 * D.nb); w.g_cont = c.f(M1);
@@ -611,16 +615,21 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   if (phases & DR_WM_PREP) {
   // ---- weights: repacks, transposes, permutations (fixed for the call) ----
   if (!vec) {
+  // (the f32 layouts only for the layers without split planes: each repack is
+  // a ~5 us launch, 13 of them per step unused, r04zd)
   for (int k = 0; k < N; ++k) {
-    DR_TRY(op_conv_repack_pad(D.e[k + 1], D.e[k], enc_cin_st(D, k), wm->conv[k].w, w.wr[k], s));
+    if (!w.s3e[k]) DR_TRY(op_conv_repack_pad(D.e[k + 1], D.e[k], enc_cin_st(D, k), wm->conv[k].w, w.wr[k], s));
     // Conv2d data gradient = upsampling conv with the weight read as [cin=co][cout=ci]
-    if (k > 0) DR_TRY(op_convT_repack(D.e[k + 1], D.e[k], wm->conv[k].w, w.wqe[k], s));
+    if (k > 0 && !w.t3e[k]) DR_TRY(op_convT_repack(D.e[k + 1], D.e[k], wm->conv[k].w, w.wqe[k], s));
   }
   for (int k = 0; k < N; ++k) {
-    if (k < N - 1) DR_TRY(op_convT_repack(cin_t[k], cout_t[k], dec->convt[k].w, w.wqd[k], s));
-    else DR_TRY(op_convT_out3_repack(cin_t[k], dec->convt[k].w, w.wqd[k], s));
+    if (k < N - 1) {
+      if (!w.t3d[k]) DR_TRY(op_convT_repack(cin_t[k], cout_t[k], dec->convt[k].w, w.wqd[k], s));
+    } else {
+      DR_TRY(op_convT_out3_repack(cin_t[k], dec->convt[k].w, w.wqd[k], s));
+    }
     // ConvTranspose2d data gradient = strided Conv2d with the weight read as [out=ci][in=co]
-    DR_TRY(op_conv_repack_pad(cin_t[k], cout_t[k], dec_cout_st(D, k), dec->convt[k].w, w.wrd[k], s));
+    if (!w.s3d[k]) DR_TRY(op_conv_repack_pad(cin_t[k], cout_t[k], dec_cout_st(D, k), dec->convt[k].w, w.wrd[k], s));
   }
   for (int k = 0; k < N; ++k) {
     if (w.s3e[k]) DR_TRY(op_conv_repack_split3(D.e[k + 1], D.e[k], wm->conv[k].w, w.s3e[k], s));
@@ -675,7 +684,9 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     hipLaunchKernelGGL(k_silu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, w.pre[N - 1], aL);
     DR_TRY(dr_check_launch("silu"));
   } else {
-  DR_TRY(op_frames_nhwc4(M, B, IH, IW, src, w.x0, s));  // (conv1's weight gradient reads it)
+  // (conv1's weight gradient reads it; pad channel = 1: its bias gradient comes
+  // out of the same product, enc_bias_fused below)
+  DR_TRY(op_frames_nhwc4(M, B, IH, IW, src, w.x0, s, 1.0f));
   // conv1 + conv2 in one kernel from the u8 ring (k_enc12_split3) with the
   // backward's saves; other shapes / sources take the per-layer kernels
   int k0 = 0;
@@ -801,7 +812,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
         // Tanh + squared error against frames t >= 1 (WorldModel.py:129); writes dL/d(pre-tanh)
         a.out = w.dgout; a.ldc = 4;
         a.target = w.x0 + (long long)B * D.pix[0] * 4; a.tstride = 4;
-        a.coef = w.coef_obs; a.part = w.obs_part;
+        a.coef = w.coef_obs; a.part = w.obs_part; a.bpart = w.obs_bpart;
         DR_TRY(op_convT_nhwc(CT_EPI_TANH_MSE, a, s));
       }
     }
@@ -876,6 +887,7 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     ColsumJob cj[2] = {{Dv, w.dgout, Dv, nullptr, 0, gd->convt[1].b}, {D.Fd, w.dgq[0], D.Fd, nullptr, 0, gd->convt[0].b}};
     DR_TRY(op_colsum_multi(M1, cj, 2, s));
   } else {
+    bool csum_next = false;  // gout of this layer was summed per tile by the layer above's input-gradient conv
     for (int k = N - 1; k >= 0; --k) {
       const int ih = IH >> (N - 1 - k), iw = IW >> (N - 1 - k);  // output (high-res) size of convT k
       const int co = cout_t[k], co_st = dec_cout_st(D, k);
@@ -885,15 +897,28 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
       const bool post_silu = k == N - 1 && k > 0;
       const float* post = post_silu ? w.dq[k - 1] : k ? w.dqp[k - 1] : w.du2p;
       const float* gout = k < N - 1 ? w.dgq[k] : w.dgout;  // dL/d(convT k's output pre-activation)
+      // the f32 4-channel input-gradient conv of the last layer also sums its
+      // output per tile: the bias gradient of convT k - 1 without re-reading
+      // that 0.5 GB gradient (csum_next below)
+      const bool csum_here = !w.s3d[k] && k == N - 1 && k > 0;
       if (w.s3d[k])
         DR_TRY(op_conv_split3_ex(M1, co_st, ih, iw, cin_t[k], gout, w.s3d[k], nullptr, gin, 0, const_cast<float*>(pre),
                                  CONV_EPI_DSILU, s, D.terms));
       else
         DR_TRY(op_conv_nhwc_ex(M1, co_st, ih, iw, cin_t[k], gout, w.wrd[k], nullptr, gin, 0, const_cast<float*>(pre),
-                               CONV_EPI_DSILU, s));
+                               CONV_EPI_DSILU, s, csum_here ? w.csp : nullptr));
       DR_TRY(wgrad(M1, ih / 2, iw / 2, cin_t[k], co_st, post, cin_t[k], gout, co_st, gd->convt[k].w, co, w.cws, w.cws_n,
                    s, D.terms, post_silu ? 1 : 0));
-      DR_TRY(op_chan_sum((long long)M1 * ih * iw, co, gout, co_st, gd->convt[k].b, 0, w.cws, w.cws_n, s));
+      // (the per-tile partials -- 1.5e4 / 2.9e4 rows -- go through the same
+      // two-pass channel sum: one workgroup per channel over them took 40-70 us)
+      if (k == N - 1 && co == 3)  // the tanh-MSE layer summed its gradient per tile (k_convT_out3)
+        DR_TRY(op_chan_sum((long long)M1 * op_convT_mse_parts(ih / 2, iw / 2), 3, w.obs_bpart, 3, gd->convt[k].b, 0,
+                           w.cws, w.cws_n, s));
+      else if (csum_next)
+        DR_TRY(op_chan_sum(((long long)M1 * ih * iw + 127) / 128, co, w.csp, co, gd->convt[k].b, 0, w.cws, w.cws_n, s));
+      else
+        DR_TRY(op_chan_sum((long long)M1 * ih * iw, co, gout, co_st, gd->convt[k].b, 0, w.cws, w.cws_n, s));
+      csum_next = csum_here;
     }
   }
   // decoder.upscaler: .3 (permuted rows) then LN-SiLU(.1) and .0 into dL/d[h | z]
@@ -997,6 +1022,14 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
       const int oh = IH >> (k + 1), ow = IW >> (k + 1);
       const int cin = enc_cin_st(D, k), cout = D.e[k + 1];
       const float* hi = k ? w.a[k - 1] : w.x0;  // conv k's input
+      if (k == 0 && cin > D.e[0]) {
+        // conv1: x0's pad channel holds 1, so the weight-gradient product's
+        // pad column is the bias gradient -- the 0.5 GB gradient gp[0] is not
+        // re-read by a channel-sum pass (op_conv_wgrad bias_out)
+        DR_TRY(op_conv_wgrad(M, oh, ow, cout, cin, w.gp[0], cout, 0, hi, cin, gw->conv[0].w, D.e[0], 1.0f, 0, w.cws,
+                             w.cws_n, s, gw->conv[0].b));
+        continue;
+      }
       DR_TRY(wgrad(M, oh, ow, cout, cin, w.gp[k], cout, hi, cin, gw->conv[k].w, D.e[k], w.cws, w.cws_n, s, D.terms));
       DR_TRY(op_chan_sum((long long)M * oh * ow, cout, w.gp[k], cout, gw->conv[k].b, 0, w.cws, w.cws_n, s));
       if (k > 0) {

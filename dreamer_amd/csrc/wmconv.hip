@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256) void k_convT_nhwc(ConvTArgs a) {
 #pragma unroll
     for (int i = 0; i < APT; ++i) {
       float4 v = (mka >> i) & 1u ? ra[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-      if (SILU_IN) v = make_float4(dr_silu(v.x), dr_silu(v.y), dr_silu(v.z), dr_silu(v.w));
+      if (SILU_IN) v = make_float4(dr_silu_fast(v.x), dr_silu_fast(v.y), dr_silu_fast(v.z), dr_silu_fast(v.w));
       *reinterpret_cast<float4*>(&As[buf][prow + 32 * i][4 * quad]) = v;
     }
 #pragma unroll
@@ -196,14 +196,14 @@ __global__ __launch_bounds__(256) void k_convT_nhwc(ConvTArgs a) {
             f32x4 sv = v;
             if (a.out2 || a.silu_out) {
 #pragma unroll
-              for (int e = 0; e < 4; ++e) sv[e] = dr_silu(v[e]);
+              for (int e = 0; e < 4; ++e) sv[e] = dr_silu_fast(v[e]);
             }
             *reinterpret_cast<f32x4*>(a.out + opix * ldc + co0) = a.silu_out ? sv : v;
             if (a.out2) *reinterpret_cast<f32x4*>(a.out2 + opix * ldc + co0) = sv;
           } else {
             const f32x4 pv = *reinterpret_cast<const f32x4*>(a.pre + opix * cout + co0);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = v[e] * dr_dsilu(pv[e]);
+            for (int e = 0; e < 4; ++e) v[e] = v[e] * dr_dsilu_fast(pv[e]);
             *reinterpret_cast<f32x4*>(a.out + opix * ldc + co0) = v;
           }
           continue;
@@ -219,11 +219,11 @@ __global__ __launch_bounds__(256) void k_convT_nhwc(ConvTArgs a) {
           const float v = acc[i][j][e];
           if (EPI == CT_EPI_BIAS) {
             const float pv = v + a.bias[co];
-            const float sv = (a.out2 || a.silu_out) ? dr_silu(pv) : 0.0f;
+            const float sv = (a.out2 || a.silu_out) ? dr_silu_fast(pv) : 0.0f;
             a.out[opix * ldc + co] = a.silu_out ? sv : pv;
             if (a.out2) a.out2[opix * ldc + co] = sv;
           } else {
-            a.out[opix * ldc + co] = v * dr_dsilu(a.pre[opix * cout + co]);
+            a.out[opix * ldc + co] = v * dr_dsilu_fast(a.pre[opix * cout + co]);
           }
         }
       }
@@ -250,11 +250,11 @@ __global__ __launch_bounds__(256) void k_convT_nhwc(ConvTArgs a) {
         const float v = acc[i][j][e];
         if (EPI == CT_EPI_BIAS) {
           const float pv = v + a.bias[co];
-          const float sv = (a.out2 || a.silu_out) ? dr_silu(pv) : 0.0f;
+          const float sv = (a.out2 || a.silu_out) ? dr_silu_fast(pv) : 0.0f;
           a.out[opix * ldc + co] = a.silu_out ? sv : pv;
           if (a.out2) a.out2[opix * ldc + co] = sv;
         } else if (EPI == CT_EPI_DSILU) {
-          a.out[opix * ldc + co] = v * dr_dsilu(a.pre[opix * cout + co]);
+          a.out[opix * ldc + co] = v * dr_dsilu_fast(a.pre[opix * cout + co]);
         } else {  // CT_EPI_TANH_MSE (VAE.py:136 Tanh; WorldModel.py:129 squared error)
           const float mu = tanhf(v + a.bias[co]);
           const float err = mu - a.target[opix * a.tstride + co];
@@ -309,9 +309,13 @@ static int launch_convT(const ConvTArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------------------
 template <int CIN, bool LOSS>
 __global__ __launch_bounds__(256) void k_convT_out3(ConvTArgs a) {
-  constexpr int PW = O3_TX + 2, PH = O3_TY + 2, PITCH = CIN + 1;
+  // the input channels pass through LDS CH at a time: a 16-channel patch
+  // (23 KB) lets ~5 workgroups share a CU where the whole 32-channel patch
+  // (45 KB) held 3, too few waves to cover the staging and LDS latency
+  constexpr int CH = CIN > 16 ? 16 : CIN;
+  constexpr int PW = O3_TX + 2, PH = O3_TY + 2, PITCH = CH + 1;
   __shared__ float patch[PH * PW * PITCH];
-  __shared__ float red[4];
+  __shared__ float red[4], redb[4][3];
   const int h = a.h, w = a.w;
   const int tiles_x = (w + O3_TX - 1) / O3_TX, tiles_y = h / O3_TY;
   const int per_frame = tiles_x * tiles_y;
@@ -320,44 +324,47 @@ __global__ __launch_bounds__(256) void k_convT_out3(ConvTArgs a) {
   const int y0 = (tile / tiles_x) * O3_TY, x0 = (tile % tiles_x) * O3_TX;
   const int tid = threadIdx.x;
   const float* __restrict__ in = a.in + f * h * w * CIN;
-  // stage the halo patch (SiLU of the pre-activations; zero outside the image)
-  for (int e = tid; e < PH * PW * (CIN / 4); e += 256) {
-    const int c4 = e % (CIN / 4), pix = e / (CIN / 4);
-    const int py = pix / PW, px = pix - py * PW;
-    const int y = y0 - 1 + py, x = x0 - 1 + px;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (y >= 0 && y < h && x >= 0 && x < w) {
-      v = *reinterpret_cast<const float4*>(in + ((long long)y * w + x) * CIN + 4 * c4);
-      if (a.silu_in) v = make_float4(dr_silu(v.x), dr_silu(v.y), dr_silu(v.z), dr_silu(v.w));
-    }
-    float* d = patch + pix * PITCH + 4 * c4;
-    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-  }
-  __syncthreads();
   const int ty = tid / O3_TX, tx = tid - ty * O3_TX;
   float acc[4][3];
 #pragma unroll
   for (int c = 0; c < 4; ++c)
 #pragma unroll
     for (int o = 0; o < 3; ++o) acc[c][o] = 0.0f;
-  const float* __restrict__ wo = a.wq;  // [ci][cls][tap][co]
   const float* pb = patch + (ty * PW + tx) * PITCH;
-  for (int ci = 0; ci < CIN; ++ci) {
-    float xv[3][3];
+  for (int c0 = 0; c0 < CIN; c0 += CH) {
+    if (c0) __syncthreads();  // the previous pass's reads are done
+    // stage the halo patch (SiLU of the pre-activations; zero outside the image)
+    for (int e = tid; e < PH * PW * (CH / 4); e += 256) {
+      const int c4 = e % (CH / 4), pix = e / (CH / 4);
+      const int py = pix / PW, px = pix - py * PW;
+      const int y = y0 - 1 + py, x = x0 - 1 + px;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (y >= 0 && y < h && x >= 0 && x < w) {
+        v = *reinterpret_cast<const float4*>(in + ((long long)y * w + x) * CIN + c0 + 4 * c4);
+        if (a.silu_in) v = make_float4(dr_silu_fast(v.x), dr_silu_fast(v.y), dr_silu_fast(v.z), dr_silu_fast(v.w));
+      }
+      float* d = patch + pix * PITCH + 4 * c4;
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+    __syncthreads();
+    const float* __restrict__ wo = a.wq + c0 * 48;  // [ci][cls][tap][co]
+    for (int ci = 0; ci < CH; ++ci) {
+      float xv[3][3];
 #pragma unroll
-    for (int r = 0; r < 3; ++r)
+      for (int r = 0; r < 3; ++r)
 #pragma unroll
-      for (int c = 0; c < 3; ++c) xv[r][c] = pb[(r * PW + c) * PITCH + ci];
-    const float* wc = wo + ci * 48;
+        for (int c = 0; c < 3; ++c) xv[r][c] = pb[(r * PW + c) * PITCH + ci];
+      const float* wc = wo + ci * 48;
 #pragma unroll
-    for (int cls = 0; cls < 4; ++cls) {
-      const int py = cls >> 1, px = cls & 1;
+      for (int cls = 0; cls < 4; ++cls) {
+        const int py = cls >> 1, px = cls & 1;
 #pragma unroll
-      for (int tap = 0; tap < 4; ++tap) {
-        const int dy = tap >> 1, dx = tap & 1;
-        const float x = xv[1 + py - dy][1 + px - dx];
+        for (int tap = 0; tap < 4; ++tap) {
+          const int dy = tap >> 1, dx = tap & 1;
+          const float x = xv[1 + py - dy][1 + px - dx];
 #pragma unroll
-        for (int o = 0; o < 3; ++o) acc[cls][o] = fmaf(x, wc[(cls * 4 + tap) * 3 + o], acc[cls][o]);
+          for (int o = 0; o < 3; ++o) acc[cls][o] = fmaf(x, wc[(cls * 4 + tap) * 3 + o], acc[cls][o]);
+        }
       }
     }
   }
@@ -376,7 +383,9 @@ __global__ __launch_bounds__(256) void k_convT_out3(ConvTArgs a) {
     return;
   }
   // epilogue: tanh, squared error vs the target frame, dL/d(pre-tanh)
-  float sq = 0.0f;
+  // (+ the tile's per-channel sums of dL/d(pre-tanh): the bias gradient's
+  // partials, so that 250 MB gradient is not re-read by a channel-sum pass)
+  float sq = 0.0f, gs0 = 0.0f, gs1 = 0.0f, gs2 = 0.0f;
   if (y < h && x < w) {
     const int OW = 2 * w;
     const float cf = a.coef[f];
@@ -384,22 +393,44 @@ __global__ __launch_bounds__(256) void k_convT_out3(ConvTArgs a) {
     for (int cls = 0; cls < 4; ++cls) {
       const int py = cls >> 1, px = cls & 1;
       const long long opix = (f * 2 * h + 2 * y + py) * OW + 2 * x + px;
-      const float* tg = a.target + opix * a.tstride;
+      float tg[3];
+      if (a.tstride == 4) {  // NHWC4 frames: one 16-byte load
+        const float4 t4 = *reinterpret_cast<const float4*>(a.target + opix * 4);
+        tg[0] = t4.x; tg[1] = t4.y; tg[2] = t4.z;
+      } else {
+#pragma unroll
+        for (int o = 0; o < 3; ++o) tg[o] = a.target[opix * a.tstride + o];
+      }
       float g[3];
 #pragma unroll
       for (int o = 0; o < 3; ++o) {
-        const float mu = tanhf(acc[cls][o] + a.bias[o]);
+        const float mu = dr_tanh_fast(acc[cls][o] + a.bias[o]);
         const float err = mu - tg[o];
         sq += err * err;
         g[o] = cf * err * (1.0f - mu * mu);
       }
+      gs0 += g[0];
+      gs1 += g[1];
+      gs2 += g[2];
       *reinterpret_cast<float4*>(a.out + opix * 4) = make_float4(g[0], g[1], g[2], 0.0f);
     }
   }
   sq = wave_sum(sq);
   if ((tid & 63) == 0) red[tid >> 6] = sq;
+  float* bpart = a.bpart;
+  if (bpart) {
+    gs0 = wave_sum(gs0);
+    gs1 = wave_sum(gs1);
+    gs2 = wave_sum(gs2);
+    if ((tid & 63) == 0) {
+      redb[tid >> 6][0] = gs0;
+      redb[tid >> 6][1] = gs1;
+      redb[tid >> 6][2] = gs2;
+    }
+  }
   __syncthreads();
   if (tid == 0) a.part[f * per_frame + tile] = ((red[0] + red[1]) + red[2]) + red[3];
+  if (bpart && tid < 3) bpart[(f * per_frame + tile) * 3 + tid] = ((redb[0][tid] + redb[1][tid]) + redb[2][tid]) + redb[3][tid];
 }
 
 // [cin][3][4][4] -> [ci][cls][tap][co] (48 weights per input channel)
@@ -527,9 +558,37 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(int n, int h, int w, int ca,
   const int bky = btap >> 2, bkx = btap & 3;
   const int am = m0 + 4 * acol;
 
-  // unconditional loads, masked (and activated) at the LDS store: see k_convT_nhwc
+  // unconditional loads, masked (and activated) at the LDS store: see k_convT_nhwc.
+  // The hi pixel (frame, y, x) of each of this thread's B rows is decomposed
+  // once and then advanced by WBK pixels per chunk: a 64-bit division per
+  // load per chunk made this kernel VALU-bound (311 us for the 32-channel
+  // layers at 3840 frames, r04o; the host checks n*h*w < 2^31)
   float4 ra[APT], rb[BPT];
   unsigned mka = 0u, mkb = 0u;
+  int bk[BPT], bf[BPT], by[BPT], bx[BPT];
+#pragma unroll
+  for (int i = 0; i < BPT; ++i) {
+    const int k = (int)k_begin + brow + BROWS * i;
+    bk[i] = k;
+    bf[i] = k / hw;
+    const int p = k - bf[i] * hw;
+    by[i] = p / w;
+    bx[i] = p - by[i] * w;
+  }
+  auto advance = [&]() {
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      bk[i] += WBK;
+      bx[i] += WBK;
+      while (bx[i] >= w) {
+        bx[i] -= w;
+        if (++by[i] == h) {
+          by[i] = 0;
+          ++bf[i];
+        }
+      }
+    }
+  };
   auto load = [&](long long k0) {
     mka = mkb = 0u;
 #pragma unroll
@@ -541,13 +600,9 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(int n, int h, int w, int ca,
     }
 #pragma unroll
     for (int i = 0; i < BPT; ++i) {
-      const long long k = k0 + brow + BROWS * i;
-      const long long f = k / hw;
-      const int p = (int)(k - f * hw);
-      const int y = p / w, x = p - y * w;
-      const int Y = 2 * y - 1 + bky, X = 2 * x - 1 + bkx;
-      const bool ok = k < k_end && Y >= 0 && Y < H2 && X >= 0 && X < W2;
-      rb[i] = *reinterpret_cast<const float4*>(hi + (ok ? ((f * H2 + Y) * W2 + X) * ldb + bch : 0));
+      const int Y = 2 * by[i] - 1 + bky, X = 2 * bx[i] - 1 + bkx;
+      const bool ok = bk[i] < k_end && Y >= 0 && Y < H2 && X >= 0 && X < W2;
+      rb[i] = *reinterpret_cast<const float4*>(hi + (ok ? (((long long)bf[i] * H2 + Y) * W2 + X) * ldb + bch : 0));
       mkb |= ok ? (1u << i) : 0u;
     }
   };
@@ -555,7 +610,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(int n, int h, int w, int ca,
 #pragma unroll
     for (int i = 0; i < APT; ++i) {
       float4 v = (mka >> i) & 1u ? ra[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-      if (lo_silu) v = make_float4(dr_silu(v.x), dr_silu(v.y), dr_silu(v.z), dr_silu(v.w));
+      if (lo_silu) v = make_float4(dr_silu_fast(v.x), dr_silu_fast(v.y), dr_silu_fast(v.z), dr_silu_fast(v.w));
       *reinterpret_cast<float4*>(&As[buf][arow + AROWS * i][4 * acol]) = v;
     }
 #pragma unroll
@@ -579,7 +634,10 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(int n, int h, int w, int ca,
     const int nch = (int)((k_end - k_begin + WBK - 1) / WBK);
     for (int c = 0; c < nch; ++c) {
       const int buf = c & 1;
-      load(k_begin + (long long)min(c + 1, nch - 1) * WBK);  // (the last chunk reloads itself, unused)
+      if (c + 1 < nch) {
+        advance();
+        load(k_begin + (long long)(c + 1) * WBK);
+      }
 #pragma unroll
       for (int s = 0; s < WBK; s += 16) {
 #pragma unroll
@@ -617,7 +675,7 @@ __global__ __launch_bounds__(256) void k_conv_wgrad(int n, int h, int w, int ca,
 // 256-byte partial rows), fixed-order combine in LDS
 __global__ __launch_bounds__(1024) void k_wgrad_reduce(int ca, int cb, int cbo, int nsplit,
                                                        const float* __restrict__ part, float* __restrict__ dw,
-                                                       float scale, int accumulate) {
+                                                       float scale, int accumulate, float* __restrict__ bias_out) {
   __shared__ float red[16][65];
   const int N = 16 * cb;
   const long long total = (long long)ca * N;
@@ -637,6 +695,11 @@ __global__ __launch_bounds__(1024) void k_wgrad_reduce(int ca, int cb, int cbo, 
     if (b < cbo) {
       float* o = dw + ((long long)a * cbo + b) * 16 + tap;
       *o = accumulate ? *o + scale * t : scale * t;
+    } else if (bias_out && b == cbo && tap == 5) {
+      // pad channel cbo of the hi operand holds 1 (op_frames_nhwc4 pad = 1):
+      // tap (1, 1) reads pixel (2y, 2x), inside the image for every low-res
+      // pixel, so this column is sum_k lo[k][a] -- the bias gradient
+      bias_out[a] = accumulate ? bias_out[a] + scale * t : scale * t;
     }
   }
 }
@@ -659,7 +722,7 @@ int op_wgrad_reduce(int ca, int cb, int cbo, int nsplit, const float* part, floa
                     hipStream_t s) {
   const int total = ca * 16 * cb;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3((total + 63) / 64), dim3(1024), 0, s, ca, cb, cbo, nsplit, part, dw, scale,
-                     accumulate);
+                     accumulate, nullptr);
   return dr_check_launch("wgrad_reduce");
 }
 
@@ -670,10 +733,15 @@ size_t op_conv_wgrad_ws_floats(int n, int h, int w, int ca, int cb) {
 }
 
 int op_conv_wgrad(int n, int h, int w, int ca, int cb, const float* lo, int lda, int lo_silu, const float* hi, int ldb,
-                  float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s) {
+                  float* dw, int cbo, float scale, int accumulate, float* ws, size_t ws_floats, hipStream_t s,
+                  float* bias_out) {
+  if (bias_out && cbo >= cb) {
+    dr_set_error("conv_wgrad: bias_out needs a pad channel (cbo < cb)");
+    return DR_E_INVALID;
+  }
   if (n <= 0 || ca % 4 || cb % 4 || lda % 4 || ldb % 4 || lda < ca || ldb < cb || cbo < 1 || cbo > cb || !lo || !hi ||
-      !dw) {
-    dr_set_error("conv_wgrad: bad arguments (channels and strides must be multiples of 4)");
+      !dw || (long long)n * h * w + 2 * WBK >= (1LL << 31)) {
+    dr_set_error("conv_wgrad: bad arguments (channels and strides must be multiples of 4, n*h*w < 2^31)");
     return DR_E_INVALID;
   }
   int bm, ns, ch;
@@ -693,7 +761,7 @@ int op_conv_wgrad(int n, int h, int w, int ca, int cb, const float* lo, int lda,
   DR_TRY(dr_check_launch("conv_wgrad"));
   const int total = ca * 16 * cb;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3((total + 63) / 64), dim3(1024), 0, s, ca, cb, cbo, ns, ws, dw, scale,
-                     accumulate);
+                     accumulate, bias_out);
   return dr_check_launch("wgrad_reduce");
 }
 
@@ -798,6 +866,15 @@ __global__ __launch_bounds__(256) void k_chan_sum_final(int nb, int C, const flo
 }
 
 size_t op_chan_sum_ws_floats(long long rows, int C) { return (size_t)chan_blocks(rows, C) * C; }
+
+int op_chan_sum_final(int nb, int C, const float* part, float* out, int accumulate, hipStream_t s) {
+  if (nb <= 0 || C <= 0 || !part || !out) {
+    dr_set_error("chan_sum_final: bad arguments");
+    return DR_E_INVALID;
+  }
+  hipLaunchKernelGGL(k_chan_sum_final, dim3(C), dim3(256), 0, s, nb, C, part, out, accumulate);
+  return dr_check_launch("chan_sum_final");
+}
 
 int op_chan_sum(long long rows, int C, const float* X, int ldx, float* out, int accumulate, float* ws,
                 size_t ws_floats, hipStream_t s) {
