@@ -95,7 +95,11 @@ class Dreamer(nn.Module):
         self.seed = c["seed"]
         # extra config key: "fp32" parity mode (default) or "bf16" perf mode
         self.precision = c.get("precision", "fp32")
-        self.pipeline_epochs = bool(c.get("pipeline_epochs", False))
+        # on by default from round 4: bit-equal to sequential epochs
+        # (test_pipelined_epochs_match_sequential), 1.04x at AC_epochs = 2 and
+        # 1.16x at 10; pipeline_epochs: false restores
+        # the sequential loop
+        self.pipeline_epochs = bool(c.get("pipeline_epochs", True))
         self.world_model.precision = self.precision  # encoder kernels: bf16 MFMA in perf mode
         if self.precision not in ("fp32", "bf16"):
             raise ValueError(f"precision must be 'fp32' or 'bf16', got {self.precision!r}")
@@ -177,12 +181,12 @@ class Dreamer(nn.Module):
     def train_Agent(self):
         """Dreamer.train_Agent (Dreamer.py:264-287): AC_epochs fused epochs."""
         if self.AC_epochs > 1 and self.pipeline_epochs:
-            # opt-in (config key pipeline_epochs): the epochs' window starts
-            # are drawn up front (same np.random order); the warm start of
-            # epoch e+1 then overlaps epoch e's update (engine.run_many).  Off
-            # by default: inside the fake-env train_dreamer flow its epoch-2
-            # results were seen to differ from the sequential epochs on some
-            # runs (tools/diag/pipe_stress.py, DESIGN.md section 5a)
+            # config key pipeline_epochs (default on): the epochs' window
+            # starts are drawn up front (same np.random order); the warm start
+            # of epoch e+1 then overlaps epoch e's update (engine.run_many).
+            # (Round 2 kept it off after epoch-2 mismatches inside the fake-env
+            # train_dreamer flow; the cause -- memset / memcpy2D nodes not
+            # re-executing on graph replay -- was fixed in round 3, DESIGN.md 5a)
             B = self.batch_size if self.world is None else self.engine.B
             starts = [self.buffer.sample_start_indices(B) for _ in range(self.AC_epochs)]
             losses = self.engine.run_many(starts)
