@@ -84,6 +84,25 @@ __device__ __forceinline__ unsigned pack_bf16x2(float x0, float x1) { return b16
 // then point at u16 data.  NT3 = 1 with IO16 = false: the bf16 world-model
 // step's form -- f32 activations rounded (RNE) to one bf16 plane as they are
 // staged, f32 outputs and every epilogue of the three-term form
+// K-loop position c -> (tap, first channel, chunk index of the natural
+// tap-major order).  Channel chunks outer; within one, the 16 taps in four
+// parity groups {ky, ky + 2} x {kx, kx + 2}: the four taps of a group read the
+// same input pixels (output row oy + 1 at ky reads oy's ky + 2 row), so a
+// workgroup's input is reused within 4 consecutive chunks.  In tap-major order
+// a pixel came back 4-16 chunks later, after 128-512 KB of other traffic per
+// workgroup, and the XCD's 4 MB L2 had dropped it: fp32 conv3 fetched 1.23 GB
+// for a 0.54 GB input (profiles/r04zf_traffic_B256_r64_fp32.json).
+template <int CIN>
+__device__ __forceinline__ void conv_chunk(int c, int& tap, int& ci0, int& kc) {
+  constexpr int CPT = CIN / 32;
+  const int cc = c >> 4, t = c & 15;
+  const int g = t >> 2, j = t & 3;
+  const int ky = (g >> 1) + 2 * (j >> 1), kx = (g & 1) + 2 * (j & 1);
+  tap = ky * 4 + kx;
+  ci0 = 32 * cc;
+  kc = tap * CPT + cc;
+}
+
 template <int BM, int BN, int CIN, bool OUT_NCHW, int PIPE, int EPI = CONV_EPI_FWD, int NT3 = 3, bool IO16 = (NT3 == 1)>
 __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, int iw, int cout,
                                                          const float* __restrict__ in, const u16* __restrict__ wr,
@@ -148,7 +167,8 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
     unsigned& okm = decltype(slot)::value == 0 ? ok0 : ok1;
     u32x4* rb = decltype(slot)::value == 0 ? rb0 : rb1;
     // CIN % 32 == 0: a chunk is 32 channels of one tap (uniform over the workgroup)
-    const int tap = (32 * c) / CIN, ci0 = 32 * c - tap * CIN;
+    int tap, ci0, kc;
+    conv_chunk<CIN>(c, tap, ci0, kc);
     const int ky = tap >> 2, kx = tap & 3;
     const int toff = (ky * iw + kx) * CIN + ci0 + 4 * quad;
     unsigned om = 0u;
@@ -168,7 +188,7 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
       const int e = tid + NT * j;  // (plane, row, unit)
       if (BU % NT == 0 || e < BU) {
         const int pl = e / (BN * 4), rem = e - pl * BN * 4, row = rem >> 2, u = rem & 3;
-        rb[j] = *reinterpret_cast<const u32x4*>(wr + (((long long)c * 3 + pl) * cout + n0 + row) * 32 + 8 * u);
+        rb[j] = *reinterpret_cast<const u32x4*>(wr + (((long long)kc * 3 + pl) * cout + n0 + row) * 32 + 8 * u);
       }
     }
   };
@@ -893,8 +913,12 @@ __global__ __launch_bounds__(BM * 2) void k_convT_split3(ConvTArgs a, const u16*
   const long long tiles_m = (M + BM - 1) / BM;
   const int lt = dr_xcd_tile(blockIdx.x, (int)(4 * tiles_m * tiles_n));
   if (lt < 0) return;
-  const int cls = (int)(lt / (tiles_m * tiles_n));
-  const long long rem = lt - (long long)cls * tiles_m * tiles_n;
+  // parity class fastest: the four classes of one pixel tile read the same
+  // input, and adjacent logical tiles share an XCD (dr_xcd_tile), so that
+  // input comes from HBM about once (class-major order sent each class to
+  // other XCDs: four HBM reads, one per L2)
+  const int cls = lt & 3;
+  const long long rem = lt >> 2;
   const long long m0 = (rem / tiles_n) * BM;
   const int n0 = (int)(rem % tiles_n) * BN;
   const int py = cls >> 1, px = cls & 1;
@@ -1160,10 +1184,16 @@ __global__ __launch_bounds__(512) void k_wgrad_split3(int n, int lh, int lw, int
   __shared__ __attribute__((aligned(16))) u32x4 S[TERMS][BM + BN][RP];
   const int N = 16 * cb;
   const int tiles_n = N / BN, tiles = (ca / BM) * tiles_n;
-  const int split = blockIdx.x / tiles, lt = blockIdx.x - split * tiles;
-  const int m0 = (lt / tiles_n) * BM, n0 = (lt % tiles_n) * BN;
+  // XCD-contiguous logical order (dr_xcd_tile), tiles of one pixel split
+  // adjacent: the tiles that read the same pixels share an XCD's L2 instead of
+  // each fetching them from HBM through its own
   const int h = 1 << lh, w = 1 << lw, H2 = 2 * h, W2 = 2 * w;
   const long long K = (long long)n * h * w;
+  const int nsplit = (int)((K + chunk - 1) / chunk);
+  const int lb = dr_xcd_tile(blockIdx.x, tiles * nsplit);
+  if (lb < 0) return;
+  const int split = lb / tiles, lt = lb - split * tiles;
+  const int m0 = (lt / tiles_n) * BM, n0 = (lt % tiles_n) * BN;
   const long long k_begin = (long long)split * chunk;
   const long long k_end = k_begin + chunk < K ? k_begin + chunk : K;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
@@ -1353,7 +1383,7 @@ int op_wgrad_split3(int n, int h, int w, int ca, int cb, const float* lo, int ld
   const int tiles = (ca / bm) * (16 * cb / bn);
   const int lh = ilog2_exact(h), lw = ilog2_exact(w);
 #define DR_W3L(BM, T, ...)                                                                                     \
-  hipLaunchKernelGGL((k_wgrad_split3<BM, T, ##__VA_ARGS__>), dim3((unsigned)(tiles * ns)), dim3(512), 0, s, n, lh, lw, \
+  hipLaunchKernelGGL((k_wgrad_split3<BM, T, ##__VA_ARGS__>), dim3((unsigned)dr_xcd_grid(tiles * ns)), dim3(512), 0, s, n, lh, lw, \
                      ca, cb, lo, lda, hi, ldb, ch, ws)
   if (terms == 1) {
     if (bn == 256) {

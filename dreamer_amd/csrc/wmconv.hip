@@ -60,8 +60,10 @@ __global__ __launch_bounds__(256) void k_convT_nhwc(ConvTArgs a) {
   const long long tiles_m = (M + BM - 1) / BM;
   const int lt = dr_xcd_tile(blockIdx.x, (int)(4 * tiles_m * tiles_n));
   if (lt < 0) return;
-  const int cls = (int)(lt / (tiles_m * tiles_n));
-  const long long rem = lt - (long long)cls * tiles_m * tiles_n;
+  // parity class fastest (as k_convT_split3): the four classes of a pixel
+  // tile share an XCD's L2 and read their common input from HBM about once
+  const int cls = lt & 3;
+  const long long rem = lt >> 2;
   const long long m0 = (rem / tiles_n) * BM;
   const int n0 = (int)(rem % tiles_n) * BN;
   const int py = cls >> 1, px = cls & 1;
