@@ -1,0 +1,17 @@
+#!/bin/bash
+# round-4: k_conv_wgrad without per-chunk 64-bit division -- WM-step parity, then bf16 / fp32 WM-step kernels
+cd "$(dirname "$0")/../.." || exit 1
+export PYTHONUNBUFFERED=1
+TAG=${1:-r04zb}
+R=$(pwd)
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests/test_gpu_wm.py tests/test_gpu_deep_vae.py -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/tests_$TAG.log 2>&1 || { grep -E "FAIL|Error|assert" gpurun_out/tests_$TAG.log | head; tail -20 gpurun_out/tests_$TAG.log; exit 1; }
+tail -1 gpurun_out/tests_$TAG.log
+cd /tmp && export TMPDIR=/tmp
+for P in bf16 fp32; do
+  WM_B=256 WM_PREC=$P timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/wmprof_$TAG$P -o p -- python3 $R/tools/wm_prof.py > $R/gpurun_out/wmprof_$TAG$P.log 2>&1 || { tail -20 $R/gpurun_out/wmprof_$TAG$P.log; exit 1; }
+  grep "WM step" $R/gpurun_out/wmprof_$TAG$P.log
+  python3 $R/tools/prof_summary.py $R/gpurun_out/wmprof_$TAG$P/p_results.db 50 > $R/gpurun_out/wm_kernels_$TAG$P.txt && head -24 $R/gpurun_out/wm_kernels_$TAG$P.txt
+  rm -rf $R/gpurun_out/wmprof_$TAG$P
+done
+echo "gpu_$TAG done"
