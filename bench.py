@@ -501,10 +501,10 @@ def main():
             "ac_epochs10": {"value": round(world * B * H * 10 * 2 / el10, 1),
                             "ms_per_epoch": round(el10 / 20 * 1e3, 4),
                             "vs_sequential": round((el / args.steps) / (el10 / 20), 4)},
-            "note": "Dreamer.train_Agent() with AC_epochs=2 (and 10) and the opt-in pipeline_epochs config key: the "
-                    "warm start of epoch e+1 on a stream fenced to 7/8 of the CUs beside epoch e's update on a "
-                    "high-priority stream (equal to the sequential epochs in tests/test_gpu_parity.py; off by "
-                    "default, DESIGN.md 5a)"}
+            "note": "Dreamer.train_Agent() with AC_epochs=2 (and 10) and the pipeline_epochs config key (on by "
+                    "default): the warm start of epoch e+1 on a stream fenced to 7/8 of the CUs beside epoch e's "
+                    "update on a high-priority stream, the first warm start of a call on the chain stream (equal "
+                    "to the sequential epochs in tests/test_gpu_parity.py; DESIGN.md 5a)"}
         if (B, S, H, res) != (64, 64, 15, 64):
             _, d64 = make_dreamer(CAR_RACER, dev, 64, 64, 15, 64, 1, world, rank, group, args.precision)
             el64, _ = time_train_agent(d64, args.steps, args.warmup)
