@@ -191,6 +191,15 @@ class Dreamer(nn.Module):
             starts = [self.buffer.sample_start_indices(B) for _ in range(self.AC_epochs)]
             losses = self.engine.run_many(starts)
             return losses[:, 0].mean(dim=0), losses[:, 1].mean(dim=0)
+        if self.AC_epochs == 1:
+            # one epoch: one copy of the two loss slots (the loop below costs
+            # clone + cat + mean per loss, six small launches outside the
+            # captured graphs, each behind a dispatch gap); the mean of one
+            # value is that value, bit for bit
+            starts = self.buffer.sample_start_indices(self.batch_size if self.world is None else self.engine.B)
+            self.engine.run(starts)
+            losses = self.agent.loss_buffer[0:2].clone()
+            return losses[0], losses[1]
         la, lc = [], []
         for _ in tqdm(range(self.AC_epochs), desc="Training Agent in Dreams", leave=False):
             starts = self.buffer.sample_start_indices(self.batch_size if self.world is None else self.engine.B)
