@@ -2191,6 +2191,7 @@ static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
   // would read the raw operand.  At K = 1024 (the STE backward of a 32 x 32
   // latent) the 32-column tile does not fit (48 x 1032 floats), so a B = 512
   // grid (416 16-column tiles) stays on 16 columns
+  if (!DR_BWD_WIDE && (AMODE == AM_LNBWD || AMODE == AM_STEBWD)) wide = false;
   if (AMODE == AM_LNBWD || AMODE == AM_STEBWD) {
     const int mt = maxM > 64 ? 64 : 16;
     for (int i = 0; i < count; ++i) {
