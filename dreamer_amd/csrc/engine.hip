@@ -3,22 +3,16 @@
 // Each is a fixed sequence of kernel launches on one stream (no host sync,
 // no allocation) so a whole train_Agent epoch can be captured in a hipGraph.
 #include "engine_util.h"
-#include "chain.h"
+#include "scan.h"
 
-#ifndef DR_GATES_BLOCKED
-#define DR_GATES_BLOCKED 0  // A/B knob: 1 = unit-blocked W_ih copy for k_gru_gates_lds (r04d: 552.6k vs 560.1k with k_gru_gates)
-#endif
 #ifndef DR_B16_CHAIN_WKS
 #define DR_B16_CHAIN_WKS 1  // A/B knob: bf16 mode's per-step grouped products on bf16 weight planes
 #endif
 #ifndef DR_GRU_BWD_EPI
 #define DR_GRU_BWD_EPI 1  // A/B knob: 0 = the GRU backward as its own elementwise launch
 #endif
-#ifndef DR_ACTOR_TAIL_BWD
-#define DR_ACTOR_TAIL_BWD 0  // A/B knob: 1 = k_actor_tail_bwd (perf-neutral, r04d; its B = 4096 / B = 512 actor gradients disagreed with the oracle / 8-rank runs, r04v -- off)
-#endif
-#ifndef DR_ACTOR_TAIL
-#define DR_ACTOR_TAIL 0  // A/B knob (tools/build_variant.py): 0 = z-gather + two skinny launches
+#ifndef DR_PSCAN
+#define DR_PSCAN 1  // A/B knob: 0 = the warm start's posterior scan as three launches per step
 #endif
 
 // fp32 mode, tall batches: the first Linear of a head over [h | z] on the
@@ -223,11 +217,12 @@ struct ObsWs {
   float *gi, *gh, *pre1, *logits, *wt, *hb[2];
   int* idx;
   void *s3m0, *s3whh;  // bf16 planes of latent_mapper.0's h-columns and W_hh (k_gemm_wks3)
-  float* wtb;          // W_ih in unit blocks (k_gru_gates_lds)
-  unsigned short* hpl; // split3 planes of the GRU output [3][B][aplane_ld(Hd)] (k_gemm_wks3's A)
+  void* s3m3;          // split3 planes of latent_mapper.3 (persistent scan)
+  void* ring;          // persistent scan: ring buffers + counters (scan.hip)
 };
 static void obs_carve(Carve& c, const dr_dims* d, int B, ObsWs& w) {
-  w.wtb = c.f((long long)(latent(d) + d->action) * 3 * d->hidden);
+  w.s3m3 = c.raw(op_nt_split3_ws_bytes(latent(d), d->enc_hidden));
+  w.ring = c.raw(op_pscan_ring_bytes(B));
   w.s3m0 = c.raw(op_nt_split3_ws_bytes(d->enc_hidden, d->hidden));
   w.s3whh = c.raw(op_nt_split3_ws_bytes(3 * d->hidden, d->hidden));
   w.gi = c.f((long long)B * 3 * d->hidden);
@@ -238,7 +233,6 @@ static void obs_carve(Carve& c, const dr_dims* d, int B, ObsWs& w) {
   w.hb[0] = c.f((long long)B * d->hidden);
   w.hb[1] = c.f((long long)B * d->hidden);
   w.idx = c.i(2LL * B * d->rows);
-  w.hpl = reinterpret_cast<unsigned short*>(c.raw((size_t)3 * B * aplane_ld(d->hidden) * sizeof(unsigned short)));
 }
 
 extern "C" size_t dr_observe_workspace_bytes(const dr_dims* d, int B) {
@@ -269,11 +263,17 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
   if (any_gru) {
     DR_REQUIRE(wm->w_ih && wm->w_hh && wm->b_ih && wm->b_hh, "GRU weights required");
     DR_TRY(op_transpose(3 * Hd, L + d->action, wm->w_ih, w.wt, s));
-    if (DR_GATES_BLOCKED && B >= 128 && Hd % 4 == 0) DR_TRY(op_wih_block(Hd, L + d->action, wm->w_ih, w.wtb, s));
+  }
+  // the warm start (no z_init / h_init) as ONE persistent launch (scan.hip)
+  if (DR_PSCAN && z_init == nullptr && h_init == nullptr && op_pscan_supported(d, B, T, d->action)) {
+    DR_TRY(op_nt_repack_split3(3 * Hd, Hd, wm->w_hh, Hd, w.s3whh, s));
+    DR_TRY(op_nt_repack_split3(eh, Hd, wm->map0.w + F, F + Hd, w.s3m0, s));
+    DR_TRY(op_nt_repack_split3(L, eh, wm->map3.w, eh, w.s3m3, s));
+    const int rc = op_pscan(d, wm, B, T, d->action, feat, actions, act_sb, act_st, w.wt, w.s3whh, w.s3m0, w.s3m3,
+                            noise, 0, z_out, h_out, logits_out, w.ring, s);
+    if (rc != DR_E_UNSUPPORTED) return rc;
   }
   const bool planes = B >= 128 && T > 1 && Hd % 8 == 0;
-  // fp32 mode on the split GRU path: the gates kernel also writes h's split3 planes
-  const bool hpl_on = DR_APLANES && planes && d->precision == DR_PREC_FP32;
   if (planes) {
     DR_TRY(split_planes(eh, Hd, wm->map0.w + F, F + Hd, w.s3m0, s));
     DR_TRY(split_planes(3 * Hd, Hd, wm->w_hh, Hd, w.s3whh, s));
@@ -305,9 +305,7 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
       float* hn = w.hb[hb];
       hb ^= 1;
       DR_TRY(gru_onehot(d, wm, B, w.idx, actions + ai * act_st, act_sb, h, Hd, hn, Hd, w.wt, nullptr,
-                        nullptr, nullptr, nullptr, s, z_out, L, w.gh, gh_pre,
-                        DR_GATES_BLOCKED && B >= 128 && Hd % 4 == 0 ? w.wtb : nullptr,
-                        hpl_on ? w.hpl : nullptr, aplane_ld(Hd)));
+                        nullptr, nullptr, nullptr, s, z_out, L, w.gh, gh_pre));
       h = hn;
     }
     // latent_mapper.0 on cat(features, h): feature part precomputed in feat[t]
@@ -322,10 +320,6 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
         // bf16 mode: plane 0 times bf16-rounded h (k_gemm_wks3<1>); fp32 mode: the 3-term split
         wplanes(g[0], w.s3m0);
         wplanes(g[1], w.s3whh);
-        if (hpl_on && do_gru) {  // h's split3 planes from this step's gates kernel
-          aplanes(g[0], w.hpl, B);
-          aplanes(g[1], w.hpl, B);
-        }
         if (!DR_B16_CHAIN_WKS) g[0].bf16 = g[1].bf16 = 0;
       } else {
         g[0].bf16 = g[1].bf16 = 0;  // (bf16 mode: these products stay f32)
@@ -378,8 +372,6 @@ extern "C" size_t dr_imagine_tape_bytes(const dr_dims* d, int B, int H) {
 struct ImWs {
   float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog, *rval, *wt, *wst, *bst;  // forward scratch
   float *tl0f, *hpart;  // forward: actor Linear 0 transposed ([Hd+L][a1]), its h-part + bias [B][a1]
-  float* wtb;           // forward: W_ih in unit blocks (k_gru_gates_lds)
-  unsigned short* hpl;  // forward: split3 planes of h_{t+1} [3][B][aplane_ld(Hd)] (k_gemm_wks3's A)
   void *s3r, *s3c;  // split3 weight planes of the reward / continue heads' first Linear
   void *s3p0, *s3a0, *s3whh, *s3wt, *s3twhh;  // bf16 planes of the per-step chain weights (k_gemm_wks3)
   float* s3part;    // their split-K partial sums
@@ -418,8 +410,6 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.s3part_n = op_gemm_nt_split3_part_floats((int)B1, std::max(d->rew_h1, d->cont_h1));
   w.s3part = c.f((long long)w.s3part_n);
   w.wt = c.f((long long)(L + A) * 3 * Hd);
-  w.wtb = c.f((long long)(L + A) * 3 * Hd);
-  w.hpl = reinterpret_cast<unsigned short*>(c.raw((size_t)3 * B * aplane_ld(Hd) * sizeof(unsigned short)));
   w.tl0f = c.f((long long)(Hd + L) * d->actor_h1);
   w.hpart = c.f(Bl * d->actor_h1);
   w.wst = c.f((long long)2 * A * d->actor_h2);
@@ -503,34 +493,10 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
   {
     TransposeJob tj[2] = {{3 * Hd, L + A, 3 * Hd, wm->w_ih, w.wt}, {a1, Hd + L, a1, ac->l0.w, w.tl0f}};
     DR_TRY(op_transpose_multi(tj, zg ? 2 : 1, s));
-    if (DR_GATES_BLOCKED && split_gru && Hd % 4 == 0) DR_TRY(op_wih_block(Hd, L + A, wm->w_ih, w.wtb, s));
   }
   DR_TRY(op_onehot_index(B, d->rows, d->cols, latents, ldL, w.idx[0], onehot_vals(w.idx[0], B, d->rows), s));
 
-  // the actor of step `st` after its latents are sampled (Agent.py:191-210): ONE
-  // launch from the h-part (+ bias) of base_net.0 in w.hpart and the sampled
-  // indices (chain.hip k_actor_tail)
-  auto actor_tail = [&](int st, int* ix, const float* z_rows) -> ActorTailArgs {
-    const long long o1 = (long long)st * a1, o2 = (long long)st * a2, o = (long long)st * A;
-    ActorTailArgs at;
-    memset(&at, 0, sizeof(at));
-    at.M = B; at.A = A; at.a1 = a1; at.a2 = a2; at.R = d->rows; at.C = d->cols;
-    at.step = st; at.det = deterministic;
-    at.idx = ix; at.zval = onehot_vals(ix, B, d->rows); at.z = z_rows; at.ldz = ldL;
-    at.wzt = w.tl0f + (long long)Hd * a1; at.ldw = a1;
-    at.hpart = w.hpart; at.ldh = a1;
-    at.n1g = ac->n1.w; at.n1b = ac->n1.b; at.w3 = ac->l3.w; at.b3 = ac->l3.b; at.n4g = ac->n4.w; at.n4b = ac->n4.b;
-    at.wmu = ac->mu.w; at.bmu = ac->mu.b; at.wls = ac->ls.w; at.bls = ac->ls.b;
-    at.pre1 = tp.pre1a + o1; at.x1 = tp.x1a + o1; at.ld1 = lda1;
-    at.pre2 = tp.pre2a + o2; at.x2 = tp.x2a + o2; at.ld2 = lda2;
-    at.noise = noise;
-    at.act = actions + o; at.mu = mus + o; at.sig = sigmas + o; at.ldA = ldA;
-    at.eps_save = tp.eps + (long long)st * B * A; at.ls_save = tp.ls_raw + o;
-    return at;
-  };
-  const bool fused_actor = zg && DR_ACTOR_TAIL && op_actor_tail_ok(actor_tail(0, w.idx[0], latents));
   const bool planes = split_gru && H > 1 && Hd % 8 == 0;
-  const bool hpl_on = DR_APLANES && planes && d->precision == DR_PREC_FP32;
   if (planes) {
     DR_TRY(split_planes(d->prior_h1, Hd, wm->prior.l0.w, Hd, w.s3p0, s));
     if (zg) DR_TRY(split_planes(a1, Hd, ac->l0.w, Hd + L, w.s3a0, s));
@@ -538,19 +504,14 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
   }
 
   // actor at step 0 (Agent.py:191-210)
-  if (fused_actor) {
-    DR_TRY(run(G_NT, AM_PLAIN, lin(B, a1, Hd, hiddens, ldH, ac->l0.w, Hd + L, ac->l0.b, w.hpart, a1), s));
-    DR_TRY(op_actor_tail(actor_tail(0, w.idx[0], latents), s));
-  } else {
+  {
     DR_TRY(run(G_NT, AM_PLAIN, lin2(B, a1, hiddens, ldH, Hd, latents, ldL, L, ac->l0.w, ac->l0.b, tp.pre1a, lda1), s));
     GemmArgs g = lin_ln(B, a2, a1, tp.pre1a, lda1, ac->n1, ac->l3.w, ac->l3.b, tp.pre2a, lda2);
     g.a_out = tp.x1a; g.ld_aout = lda1;
     DR_TRY(run(G_NT, AM_LNSILU, g, s));
   }
-  if (!fused_actor || !zg) {
-    DR_TRY(stack_heads(ac, A, a2, w.wst, w.bst, s));
-  }
-  if (!fused_actor) {
+  DR_TRY(stack_heads(ac, A, a2, w.wst, w.bst, s));
+  {
     GemmArgs h = lin_ln(B, 2 * A, a2, tp.pre2a, lda2, ac->n4, w.wst, w.bst, nullptr, 0);
     h.a_out = tp.x2a; h.ld_aout = lda2;
     with_actor_head(h, A, noise, 0, deterministic, actions, ldA, mus, ldA, sigmas, ldA, tp.eps, tp.ls_raw, ldA);
@@ -564,9 +525,7 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
     float* z_n = latents + (long long)(t + 1) * L;
     // WorldModel.imagine_step (WorldModel.py:72-77)
     DR_TRY(gru_onehot(d, wm, B, w.idx[t & 1], actions + (long long)t * A, ldA, h_t, ldH, h_n, ldH, w.wt,
-                      tp.r + hb, tp.u + hb, tp.n + hb, tp.ghn + hb, s, z_t, ldL, w.gh, split_gru && t > 0,
-                      DR_GATES_BLOCKED && split_gru && Hd % 4 == 0 ? w.wtb : nullptr,
-                      hpl_on ? w.hpl : nullptr, aplane_ld(Hd)));
+                      tp.r + hb, tp.u + hb, tp.n + hb, tp.ghn + hb, s, z_t, ldL, w.gh, split_gru && t > 0));
     float* p1 = tp.pre1p + (long long)t * B * d->prior_h1;
     float* p2 = tp.pre2p + (long long)t * B * d->prior_h2;
     {
@@ -590,7 +549,6 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
       // else they stay f32; fp32 mode: h_{t+1}'s split3 planes from the gates kernel
       for (int i = 0; i < np; ++i) {
         if (!planes || !DR_B16_CHAIN_WKS) p[i].bf16 = 0;
-        if (hpl_on) aplanes(p[i], w.hpl, B);
       }
       DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, np, s));
     }
@@ -602,11 +560,6 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
     // the actor for step t+1 (the reward / continue heads run once after the unroll)
     if (t + 1 < H) {
       const long long o1 = (long long)(t + 1) * a1, o2 = (long long)(t + 1) * a2, o = (long long)(t + 1) * A;
-      if (fused_actor) {
-        // z-gather + LN-SiLU + base_net.3 + LN-SiLU + heads + rsample in one launch (chain.hip)
-        DR_TRY(op_actor_tail(actor_tail(t + 1, w.idx[(t + 1) & 1], z_n), s));
-        continue;
-      }
       if (zg) {
         int* ix = w.idx[(t + 1) & 1];
         DR_TRY(op_zgather_add(B, a1, d->rows, d->cols, ix, onehot_vals(ix, B, d->rows), z_n, ldL,
@@ -833,31 +786,6 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
     const long long ot = (long long)t * A;
     float* gh_t = w.gheads + (long long)t * 2 * A;
     const long long o2 = (long long)t * a2, o1 = (long long)t * a1;
-    ActorTailBwdArgs tb;
-    memset(&tb, 0, sizeof(tb));
-    tb.M = B; tb.A = A; tb.a1 = a1; tb.a2 = a2;
-    tb.g_a = w.gA + ot; tb.ldga = ldA;
-    tb.g_mu = g_mus ? g_mus + ot : nullptr; tb.g_sig = g_sigmas ? g_sigmas + ot : nullptr; tb.ldgl = ldA;
-    tb.act = actions + ot; tb.ldact = ldA; tb.ls_raw = tp.ls_raw + ot; tb.ldl = ldA;
-    tb.eps = tp.eps + (long long)t * B * A;
-    tb.wmu = ac->mu.w; tb.wls = ac->ls.w;
-    tb.gheads = gh_t; tb.ldh = (long long)H * 2 * A;
-    tb.pre2 = tp.pre2a + o2; tb.ld2 = lda2; tb.n4g = ac->n4.w; tb.n4b = ac->n4.b;
-    tb.gpre2 = w.gpre2a + o2; tb.gy2 = w.gy2a + o2; tb.xh2 = w.xh2a + o2;
-    tb.w3t = w.tl3a;
-    tb.pre1 = tp.pre1a + o1; tb.ld1 = lda1; tb.n1g = ac->n1.w; tb.n1b = ac->n1.b;
-    tb.gpre1 = w.gpre1a + o1; tb.gy1 = w.gy1a + o1; tb.xh1 = w.xh1a + o1;
-    if (DR_ACTOR_TAIL_BWD && op_actor_tail_bwd_ok(tb)) {
-      // heads + both LN-SiLU backwards + base_net.3's input gradient in one
-      // launch (chain.hip), then base_net.0's input gradient into [gH_t | gZ_t]
-      DR_TRY(op_actor_tail_bwd(tb, s));
-      if (t > 0) {
-        GemmArgs g0 = bwd_nt(B, Hd + L, a1, w.gpre1a + o1, lda1, w.tl0a, gH_t, ldH, 1);
-        g0.Y2 = gZ_t; g0.ldy2 = ldL; g0.nsplitY = Hd;
-        DR_TRY(run(G_NT, AM_PLAIN, g0, s));
-      }
-      continue;
-    }
     // head backward + its input gradient (K = 2A) in one launch
     DR_TRY(op_actor_head_bwd_x(B, A, a2, w.gA + ot, ldA, g_mus ? g_mus + ot : nullptr,
                                g_sigmas ? g_sigmas + ot : nullptr, ldA, actions + ot, ldA, tp.ls_raw + ot, ldA,

@@ -209,20 +209,6 @@ static inline void wplanes(GemmArgs& g, const void* planes) {
   g.wsplit = reinterpret_cast<const unsigned short*>(planes);
   g.wsplit_np = (g.N + 127) / 128 * 128;  // op_nt_split3_ws_bytes' row padding
 }
-// the A operand's split3 planes [3][M][ld] written by the GRU gates kernel
-// (GruArgs.hplanes): the fp32-mode wave-K product loads them instead of
-// splitting A in registers (bitwise the same); DR_APLANES A/B knob
-#ifndef DR_APLANES
-#define DR_APLANES 0  // r04t: 550.7k / 547.8k with the planes vs 555.4k / 556.2k without
-#endif
-static inline long long aplane_ld(int K) { return (K + 31) / 32 * 32; }
-static inline void aplanes(GemmArgs& g, const unsigned short* planes, int rows) {
-  if (!DR_APLANES || !planes || !g.wsplit) return;
-  g.asplit = planes;
-  g.asplit_ld = (int)aplane_ld(g.K);
-  g.asplit_ps = (long long)rows * g.asplit_ld;
-}
-static inline unsigned short* hplanes_if(unsigned short* p) { return DR_APLANES ? p : nullptr; }
 
 // one-hot index buffers hold [B][R] class indices followed by the [B][R]
 // straight-through values at those indices (what the fused GRU gathers)
@@ -285,12 +271,9 @@ static inline int stack_heads(const dr_actor* ac, int A, int in, float* w, float
 // where idx always comes from the sampler)
 static inline int gru_onehot(const dr_dims* d, const dr_world_model* wm, int B, int* idx, const float* a, long long lda, const float* h, long long ldh, float* hout,
                       long long ldo, const float* wt, float* sr, float* su, float* sn, float* sghn, hipStream_t s,
-                      const float* z = nullptr, long long ldz = 0, float* gh_ws = nullptr, int gh_ready = 0,
-                      const float* wtb = nullptr, unsigned short* hplanes = nullptr, long long hp_ld = 0) {
+                      const float* z = nullptr, long long ldz = 0, float* gh_ws = nullptr, int gh_ready = 0) {
   GruArgs g;
   memset(&g, 0, sizeof(g));
-  g.wtb = wtb;
-  g.hplanes = hplanes; g.hp_ld = hp_ld;
   g.gh_ws = gh_ws;
   g.gh_ready = gh_ready;
   g.z = z; g.ldz = ldz;

@@ -1860,12 +1860,9 @@ __device__ __forceinline__ unsigned wk_pack_rne(float x0, float x1) {
 #ifndef DR_WKS3_ACC3
 #define DR_WKS3_ACC3 0  // A/B knob: 1 = per-order accumulators (r04n: 554.3k vs 558.2k off)
 #endif
-// FULL: D >= every wave's chunk count -- all of a wave's fragments are loaded
-// up front (one memory latency per tile instead of one per D chunks), no refill
-// APL: A given as split3 planes (GemmArgs.asplit, 3-term form only)
-template <int NTP, int D, int NW = 4, bool FULL = false, bool APL = false>
+template <int NTP, int D, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) {
-  static_assert(!APL || NTP == 3, "A planes: 3-term form");
+  constexpr bool FULL = false, APL = false;
   constexpr int FM = 2, FN = 2, NTH = 64 * NW, NT4 = FM * FN * 256;
   __shared__ GemmArgs s_args;
   __shared__ __attribute__((aligned(16))) float red[NW][FM * FN * 4][64];
@@ -2579,51 +2576,21 @@ static bool wks3_ok(const GemmBatch& gb, int count) {
   }
   return true;
 }
-#ifndef DR_WKS3_NW
-#define DR_WKS3_NW 4  // A/B knob: waves per 32 x 32 tile (each runs its own k-chunks)
-#endif
-#ifndef DR_WKS3_FULL
-#define DR_WKS3_FULL 0  // A/B knob: 1 = whole-wave prefetch when a wave has <= 5 k-chunks
-#endif
+// 4 waves per 32 x 32 tile, each over its own run of k-chunks, a 2-deep
+// register ring (r04g: 8 waves, whole-wave prefetch and A planes measured
+// slower, profiles/r04g_ab_wks3.txt, r04t_ab_aplanes.txt)
 static void launch_wks3(const GemmBatch& gb, int count, hipStream_t s, bool bf16) {
-  int tot = 0, maxt = 0, nkc = 0;
-  bool apl = !bf16;
+  int tot = 0, maxt = 0;
   for (int i = 0; i < count; ++i) {
     const GemmArgs& g = gb.p[i];
     const int t = dr_cdiv(g.M, 32) * dr_cdiv(g.N, 32);
     tot += t;
     maxt = std::max(maxt, t);
-    nkc = std::max(nkc, dr_cdiv(g.K, 32));
-    // A planes: every problem's, 16-byte rows covering K rounded up to 32
-    apl = apl && g.asplit && ((uintptr_t)g.asplit & 15) == 0 && g.asplit_ld % 8 == 0 &&
-          g.asplit_ld >= (g.K + 31) / 32 * 32 && g.asplit_ps >= (long long)g.M * g.asplit_ld &&
-          3 * g.asplit_ps < (1LL << 30);
   }
   const int npack = count > 1 ? count : 0;
   const dim3 grid(dr_xcd_grid(npack ? tot : maxt));
-  constexpr int NW = DR_WKS3_NW;
-  const int per = dr_cdiv(nkc, NW);  // chunks of the busiest wave
-#define DR_WKS3_L(T, D, F) hipLaunchKernelGGL((k_gemm_wks3<T, D, NW, F>), grid, dim3(64 * NW), 0, s, gb, npack)
-  if (DR_WKS3_FULL && per <= 5) {
-    if (bf16) {
-      if (per <= 2) DR_WKS3_L(1, 2, true);
-      else if (per == 3) DR_WKS3_L(1, 3, true);
-      else if (per == 4) DR_WKS3_L(1, 4, true);
-      else DR_WKS3_L(1, 5, true);
-    } else {
-      if (per <= 2) DR_WKS3_L(3, 2, true);
-      else if (per == 3) DR_WKS3_L(3, 3, true);
-      else if (per == 4) DR_WKS3_L(3, 4, true);
-      else DR_WKS3_L(3, 5, true);
-    }
-  } else if (bf16) {
-    DR_WKS3_L(1, 2, false);
-  } else if (apl) {
-    hipLaunchKernelGGL((k_gemm_wks3<3, 2, NW, false, true>), grid, dim3(64 * NW), 0, s, gb, npack);
-  } else {
-    DR_WKS3_L(3, 2, false);
-  }
-#undef DR_WKS3_L
+  if (bf16) hipLaunchKernelGGL((k_gemm_wks3<1, 2>), grid, dim3(256), 0, s, gb, npack);
+  else hipLaunchKernelGGL((k_gemm_wks3<3, 2>), grid, dim3(256), 0, s, gb, npack);
 }
 
 // split-K over workgroups only when the tile grid is under one workgroup per
@@ -2691,7 +2658,7 @@ static bool tile_offsets_ok(const GemmBatch& gb, int count) {
 #define DR_B16_CHAIN_TILE 1  // A/B knob
 #endif
 template <int AMODE, bool A_KM, bool B_KN>
-static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
+static int launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
   if (AMODE == AM_PLAIN && tile_offsets_ok(gb, count)) {
     int maxM = 0, minK = 1 << 30, tiles = 0;
     bool ws = true;
@@ -2751,7 +2718,7 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
         else if (g_tile_variant == 10) launch_tile2<64, 64, 64, false, false, 4>(gt, count, s);
         else if (g_tile_variant == 11) launch_tile2<32, 64, 32, false, false, 4>(gt, count, s);
         else launch_tile2<32, 32, 64, false, false, 4>(gt, count, s);
-        return;
+        return DR_OK;
       }
     }
     // weight gradients (TN) and tall, deep products go to the tile kernel --
@@ -2772,7 +2739,7 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
       if (g_tile_variant == 0 && !A_KM && !B_KN && minK >= 1024) {
         if (b16_ok(gb, count)) launch_tile_b16<64, 64, 8>(gt, count, s);
         else launch_tile2<64, 64, 64, false, false, 8>(gt, count, s);
-        return;
+        return DR_OK;
       }
       switch (g_tile_variant) {
         case 1: launch_tile2<64, 64, 64, A_KM, B_KN>(gt, count, s); break;
@@ -2784,21 +2751,21 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
         case 7: launch_tile2<32, 32, 64, A_KM, B_KN, 4>(gt, count, s); break;
         default: launch_tile2<64, 64, 32, A_KM, B_KN>(gt, count, s); break;
       }
-      return;
+      return DR_OK;
     }
   }
   if (AMODE == AM_LNBWD) {
-    if (!A_KM && !B_KN && try_skinny<AM_LNBWD, false>(gb, count, s)) return;
+    if (!A_KM && !B_KN && try_skinny<AM_LNBWD, false>(gb, count, s)) return DR_OK;
     dr_set_error("gemm: LayerNorm-backward prologue needs the staged NT skinny path");
-    return;
+    return DR_E_INVALID;
   }
   if (AMODE == AM_STEBWD) {
-    if (!A_KM && !B_KN && try_skinny<AM_STEBWD, false>(gb, count, s)) return;
+    if (!A_KM && !B_KN && try_skinny<AM_STEBWD, false>(gb, count, s)) return DR_OK;
     dr_set_error("gemm: softmax-STE-backward prologue needs the staged NT skinny path");
-    return;
+    return DR_E_INVALID;
   }
   if (!A_KM && (AMODE == AM_PLAIN || AMODE == AM_LNSILU)) {
-    if (try_skinny<(AMODE == AM_LNSILU ? AM_LNSILU : AM_PLAIN), B_KN>(gb, count, s)) return;
+    if (try_skinny<(AMODE == AM_LNSILU ? AM_LNSILU : AM_PLAIN), B_KN>(gb, count, s)) return DR_OK;
   }
   long long work = 0;
   for (int i = 0; i < count; ++i) work += (long long)gb.p[i].M * gb.p[i].N;
@@ -2806,6 +2773,7 @@ static void launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
   // so that the launch spreads over more CUs.
   if (work >= 256LL * 1024) launch_tile<64, 64, AMODE, A_KM, B_KN>(gb, count, s);
   else launch_tile<32, 32, AMODE, A_KM, B_KN>(gb, count, s);
+  return DR_OK;
 }
 
 // the sampler-head kernel's shape: one LN-SiLU NT problem, C = 32, K <= 256
@@ -2972,10 +2940,10 @@ int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hip
   switch (lay) {
     case G_NT:
       switch (amode) {
-        case AM_PLAIN: launch_pick<AM_PLAIN, false, false>(gb, count, s); break;
-        case AM_LNSILU: launch_pick<AM_LNSILU, false, false>(gb, count, s); break;
-        case AM_CONV: launch_pick<AM_CONV, false, false>(gb, count, s); break;
-        case AM_CONV_SRC: launch_pick<AM_CONV_SRC, false, false>(gb, count, s); break;
+        case AM_PLAIN: DR_TRY((launch_pick<AM_PLAIN, false, false>(gb, count, s))); break;
+        case AM_LNSILU: DR_TRY((launch_pick<AM_LNSILU, false, false>(gb, count, s))); break;
+        case AM_CONV: DR_TRY((launch_pick<AM_CONV, false, false>(gb, count, s))); break;
+        case AM_CONV_SRC: DR_TRY((launch_pick<AM_CONV_SRC, false, false>(gb, count, s))); break;
         case AM_LNBWD: {
           const bool r16 = gemm_bwd_rows16(probs, count);
           for (int i = 0; i < count; ++i) {
@@ -2987,7 +2955,7 @@ int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hip
               return DR_E_INVALID;
             }
           }
-          launch_pick<AM_LNBWD, false, false>(gb, count, s);
+          DR_TRY((launch_pick<AM_LNBWD, false, false>(gb, count, s)));
           break;
         }
         case AM_STEBWD: {
@@ -3004,14 +2972,14 @@ int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hip
               return DR_E_INVALID;
             }
           }
-          launch_pick<AM_STEBWD, false, false>(gb, count, s);
+          DR_TRY((launch_pick<AM_STEBWD, false, false>(gb, count, s)));
           break;
         }
         default: dr_set_error("gemm_launch: bad amode"); return DR_E_INVALID;
       }
       break;
-    case G_NN: launch_pick<AM_PLAIN, false, true>(gb, count, s); break;
-    case G_TN: launch_pick<AM_PLAIN, true, true>(gb, count, s); break;
+    case G_NN: DR_TRY((launch_pick<AM_PLAIN, false, true>(gb, count, s))); break;
+    case G_TN: DR_TRY((launch_pick<AM_PLAIN, true, true>(gb, count, s))); break;
   }
   return dr_check_launch("gemm");
 }

@@ -22,13 +22,7 @@ struct alignas(16) GruArgs {
   float* gh_ws;                // optional [B][3*Hd] scratch: enables the split path at B >= 128
   int gh_ready;                // split path: gh_ws already holds h W_hh^T + b_hh (computed by the
                                //   caller's grouped launch of the previous step), skip the GEMM
-  const float* wtb;            // optional W_ih^T in unit blocks [Hd/4][R*C + A][3][4] (op_wih_block):
-                               //   enables k_gru_gates_lds (contiguous 49 KB slice per workgroup)
-  unsigned short* hplanes;     // optional split3 planes of hout [3][B][hp_ld] (k_gru_gates, split path)
-  long long hp_ld;
 };
-// W_ih [3 Hd][L + A] -> wtb[j/4][r][gate][j%4] = W_ih[gate * Hd + j][r] (Hd % 4 == 0)
-int op_wih_block(int Hd, int LA, const float* w_ih, float* wtb, hipStream_t s);
 
 int op_gru_fused(const GruArgs& g, hipStream_t s);
 // out[m][n] = base[m][n] + sum over the R latent groups of zval[m][u] * wt[u*C + idx[m][u]][n]

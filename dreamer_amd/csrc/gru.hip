@@ -473,16 +473,6 @@ __global__ __launch_bounds__(GG_NT) void k_gru_gates(GruArgs ga) {
       no[e] = nn;
     }
     dr_st4(g.hout, (unsigned)(gm * (int)g.ldo + gj), make_float4(ho[0], ho[1], ho[2], ho[3]));
-    if (g.hplanes) {  // split3 planes of h' for the next grouped product (k_gemm_wks3's A)
-      unsigned h0, m0_, l0, h1, m1, l1;
-      split3_pair(ho[0], ho[1], h0, m0_, l0);
-      split3_pair(ho[2], ho[3], h1, m1, l1);
-      const long long ps = (long long)B * g.hp_ld, o = (long long)gm * g.hp_ld + gj;
-      typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
-      *reinterpret_cast<u32x2_t*>(g.hplanes + o) = (u32x2_t){h0, h1};
-      *reinterpret_cast<u32x2_t*>(g.hplanes + ps + o) = (u32x2_t){m0_, m1};
-      *reinterpret_cast<u32x2_t*>(g.hplanes + 2 * ps + o) = (u32x2_t){l0, l1};
-    }
     if (g.sr) {
       const unsigned o = (unsigned)(gm * Hd + gj);
       dr_st4(g.sr, o, make_float4(ro[0], ro[1], ro[2], ro[3]));
@@ -493,205 +483,6 @@ __global__ __launch_bounds__(GG_NT) void k_gru_gates(GruArgs ga) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// The same split-path gather + gates with the W_ih^T slice staged in LDS.  A
-// workgroup owns GL_UNITS hidden units (their 3 gate columns: (L + A) rows x
-// 3 GL_UNITS floats of W_ih^T, 49 KB at the reference's widths) for GL_ROWS
-// batch rows.  The slice is read ONCE from L2 with every load issued before the
-// first wait, together with the rows' indices, straight-through values,
-// actions, gh and h; each thread then gathers its row's R sampled rows (and the
-// A action rows) of the slice from LDS.  k_gru_gates' 8-row tiles re-read every
-// gathered row per batch row from L2 (about 65 MB per step at B = 256; here
-// 300 workgroups x 49 KB = 15 MB).  Thread = (row, 2 units) x 3 gates; gi keeps
-// k_gru_gates' summation order (groups ascending with fmaf, then actions, then
-// + b_ih), so the results are bitwise those of k_gru_gates.
-// ---------------------------------------------------------------------------
-#define GL_UNITS 4
-#define GL_ROWS 128
-#define GL_NT 256
-#define GL_WMAX 16  // W_ih^T slice float4s per thread: (L + A) * 3 <= 16 * 256
-static size_t gates_lds_bytes(int L, int A) { return (size_t)(L + A) * 3 * GL_UNITS * sizeof(float); }
-
-__global__ __launch_bounds__(GL_NT) void k_gru_gates_lds(GruArgs ga) {
-  __shared__ GruArgs g;
-  dr_stage_args(ga, g, threadIdx.x);
-  extern __shared__ __attribute__((aligned(16))) float sw[];  // [(L + A)][3][GL_UNITS]
-  const int Hd = dr_uni(g.Hd), B = dr_uni(g.B);
-  const int R = dr_uni(g.R), C = dr_uni(g.C), A = dr_uni(g.A), L = R * C;
-  const int tiles_j = Hd / GL_UNITS, tiles_m = (B + GL_ROWS - 1) / GL_ROWS;
-  const int lt = dr_xcd_tile(blockIdx.x, tiles_j * tiles_m);
-  if (lt < 0) return;
-  const int tj = lt / tiles_m, tm = lt - tj * tiles_m;  // row tiles of one unit slice are adjacent (one XCD)
-  const int j0 = tj * GL_UNITS, m0 = tm * GL_ROWS;
-  const int tid = threadIdx.x, ml = tid >> 1, hh = tid & 1;
-  const int m = m0 + ml, jj = j0 + 2 * hh;
-  const bool live = m < B;
-  // every global load of the workgroup, issued together: the W_ih^T slice (one
-  // contiguous 49 KB block of the unit-blocked copy: float4 x = (row x / 3, gate x % 3)) ...
-  const int nw4 = (L + A) * 3;
-  const float* wtb = dr_uni(g.wtb) + (long long)tj * nw4 * 4;
-  float4 wv[GL_WMAX];
-#pragma unroll
-  for (int i = 0; i < GL_WMAX; ++i) {
-    const int x = tid + GL_NT * i;
-    wv[i] = dr_ld4(wtb, x < nw4 ? 4u * (unsigned)x : 0u);
-  }
-  // ... and this thread's row: indices / values of the R groups, actions, gh, h, b_ih
-  int iv[GRU_MAXR];
-  float zv[GRU_MAXR];
-  const int* idx = dr_uni(g.idx);
-  const float* zval = dr_uni(g.zval);
-#pragma unroll
-  for (int u4 = 0; u4 < GRU_MAXR / 4; ++u4) {
-    const bool ok = live && 4 * u4 < R;
-    const unsigned e = ok ? (unsigned)(m * R + 4 * u4) : 0u;
-    typedef int i4v __attribute__((ext_vector_type(4)));
-    const i4v ix = *(const DR_GLOBAL i4v*)((const DR_GLOBAL char*)idx + (e << 2));
-    const float4 zx = dr_ld4(zval, e);
-    iv[4 * u4] = ix.x; iv[4 * u4 + 1] = ix.y; iv[4 * u4 + 2] = ix.z; iv[4 * u4 + 3] = ix.w;
-    zv[4 * u4] = zx.x; zv[4 * u4 + 1] = zx.y; zv[4 * u4 + 2] = zx.z; zv[4 * u4 + 3] = zx.w;
-  }
-  const float* act = dr_uni(g.a);
-  const int lda = dr_uni((int)g.lda);
-  float av[GRU_MAXA];
-#pragma unroll
-  for (int i = 0; i < GRU_MAXA; ++i) av[i] = dr_ld1(act, live && i < A ? (unsigned)(m * lda + i) : 0u);
-  const float* hp = dr_uni(g.h);
-  const float* gh = hp ? dr_uni(g.gh_ws) : nullptr;
-  float2 ghv[3], bi[3], hv = make_float2(0.f, 0.f);
-  typedef float f2v __attribute__((ext_vector_type(2)));
-  auto ld2 = [](const float* base, unsigned e) {
-    const f2v t = *(const DR_GLOBAL f2v*)((const DR_GLOBAL char*)base + (e << 2));
-    return make_float2(t.x, t.y);
-  };
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    ghv[t] = gh ? ld2(gh, live ? (unsigned)(m * 3 * Hd + t * Hd + jj) : 0u)
-                : ld2(dr_uni(g.b_hh), (unsigned)(t * Hd + jj));
-    bi[t] = ld2(dr_uni(g.b_ih), (unsigned)(t * Hd + jj));
-  }
-  if (hp) hv = ld2(hp, live ? (unsigned)(m * (int)g.ldh + jj) : 0u);
-#pragma unroll
-  for (int i = 0; i < GL_WMAX; ++i) {
-    const int x = tid + GL_NT * i;
-    if (x < nw4) *reinterpret_cast<float4*>(&sw[4 * x]) = wv[i];
-  }
-  __syncthreads();
-  // gi for the thread's 2 units x 3 gates: R gathered slice rows, in group order
-  float2 v[3] = {make_float2(0.f, 0.f), make_float2(0.f, 0.f), make_float2(0.f, 0.f)};
-  bool dense = false;
-#pragma unroll
-  for (int u = 0; u < GRU_MAXR; ++u) {
-    if (u < R) {
-      const int row = u * C + (iv[u] >= 0 ? iv[u] : 0);
-      dense = dense || iv[u] < 0;
-      const float* sr = &sw[row * 3 * GL_UNITS + 2 * hh];
-#pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const float2 w = *reinterpret_cast<const float2*>(sr + t * GL_UNITS);
-        v[t].x = fmaf(w.x, zv[u], v[t].x);
-        v[t].y = fmaf(w.y, zv[u], v[t].y);
-      }
-    }
-  }
-  if (dense && live) {  // groups with several non-zero classes: every class (as the fused kernel)
-    const float* zr = g.z + (long long)m * g.ldz;
-    for (int u = 0; u < R; ++u) {
-      if (iv[u] >= 0) continue;
-      for (int c = 0; c < C; ++c) {
-        const float zc = zr[u * C + c];
-        const float* sr = &sw[(u * C + c) * 3 * GL_UNITS + 2 * hh];
-        for (int t = 0; t < 3; ++t) {
-          const float2 w = *reinterpret_cast<const float2*>(sr + t * GL_UNITS);
-          v[t].x = fmaf(w.x, zc, v[t].x);
-          v[t].y = fmaf(w.y, zc, v[t].y);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < GRU_MAXA; ++i) {
-    if (i < A) {
-      const float* sr = &sw[(L + i) * 3 * GL_UNITS + 2 * hh];
-#pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const float2 w = *reinterpret_cast<const float2*>(sr + t * GL_UNITS);
-        v[t].x = fmaf(w.x, av[i], v[t].x);
-        v[t].y = fmaf(w.y, av[i], v[t].y);
-      }
-    }
-  }
-  if (!live) return;
-  // gates (torch gru_cell op order), as k_gru_gates
-  const float gi_r[2] = {v[0].x + bi[0].x, v[0].y + bi[0].y}, gi_u[2] = {v[1].x + bi[1].x, v[1].y + bi[1].y};
-  const float gi_n[2] = {v[2].x + bi[2].x, v[2].y + bi[2].y};
-  const float gh_r[2] = {ghv[0].x, ghv[0].y}, gh_u[2] = {ghv[1].x, ghv[1].y}, gh_n[2] = {ghv[2].x, ghv[2].y};
-  const float h2[2] = {hv.x, hv.y};
-  float ho[2], ro[2], uo[2], no[2];
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const float rr = 1.0f / (1.0f + expf(-(gh_r[e] + gi_r[e])));
-    const float uu = 1.0f / (1.0f + expf(-(gh_u[e] + gi_u[e])));
-    const float nn = tanhf(gi_n[e] + gh_n[e] * rr);
-    ho[e] = (h2[e] - nn) * uu + nn;
-    ro[e] = rr;
-    uo[e] = uu;
-    no[e] = nn;
-  }
-  auto st2 = [](float* base, unsigned e, float a, float b) {
-    *(DR_GLOBAL f2v*)((DR_GLOBAL char*)base + (e << 2)) = f2v{a, b};
-  };
-  st2(g.hout, (unsigned)(m * (int)g.ldo + jj), ho[0], ho[1]);
-  if (g.sr) {
-    const unsigned o = (unsigned)(m * Hd + jj);
-    st2(g.sr, o, ro[0], ro[1]);
-    st2(g.su, o, uo[0], uo[1]);
-    st2(g.sn, o, no[0], no[1]);
-    st2(g.sghn, o, gh_n[0], gh_n[1]);
-  }
-}
-
-static bool gates_lds_ok(const GruArgs& g) {
-  const int L = g.R * g.C;
-  return g.wtb && !g.hplanes && ((uintptr_t)g.wtb & 15) == 0 && g.Hd % GL_UNITS == 0 && g.R % 4 == 0 && (L + g.A) * 3 <= GL_WMAX * GL_NT && g.ldo % 2 == 0 &&
-         (!g.h || g.ldh % 2 == 0) && (g.lda >= g.A) && gates_lds_bytes(L, g.A) <= 64 * 1024 &&
-         (((uintptr_t)g.idx | (uintptr_t)g.zval) & 15) == 0 &&
-         (((uintptr_t)g.gh_ws | (uintptr_t)g.h | (uintptr_t)g.hout | (uintptr_t)g.b_ih | (uintptr_t)g.b_hh) & 7) == 0;
-}
-
-#ifndef DR_GATES_LDS
-#define DR_GATES_LDS 1  // A/B knob (tools/build_variant.py): 0 = k_gru_gates
-#endif
-
-__global__ void k_wih_block(int Hd, int LA, const float* __restrict__ w_ih, float* __restrict__ wtb) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // output element
-  const long long n = (long long)Hd * LA * 3;
-  if (i >= n) return;
-  const int u = (int)(i & 3);
-  const long long rest = i >> 2;  // (tj, r, gate)
-  const int t = (int)(rest % 3);
-  const long long rr = rest / 3;
-  const int r = (int)(rr % LA), tj = (int)(rr / LA);
-  wtb[i] = w_ih[(long long)(t * Hd + 4 * tj + u) * LA + r];
-}
-
-int op_wih_block(int Hd, int LA, const float* w_ih, float* wtb, hipStream_t s) {
-  if (Hd % 4 || LA <= 0) {
-    dr_set_error("wih_block: Hd %% 4 == 0 required");
-    return DR_E_INVALID;
-  }
-  const long long n = (long long)Hd * LA * 3;
-  hipLaunchKernelGGL(k_wih_block, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, Hd, LA, w_ih, wtb);
-  return dr_check_launch("wih_block");
-}
-
-#ifdef DR_PHASE_TIMING  // microbenchmark knob (tools/kbench), not in the product library
-static int g_gates_batch = 8;
-extern "C" void dr_debug_gates_batch(int v) { g_gates_batch = v; }
-static int gates_batch() { return g_gates_batch; }
-#else
-static int gates_batch() { return 8; }
-#endif
 
 // ---------------------------------------------------------------------------
 // Latent part of a Linear on cat(h, z) with a one-hot z (the actor's first
@@ -784,10 +575,6 @@ int op_gru_fused(const GruArgs& g, hipStream_t s) {
     dr_set_error("gru_fused: operands exceed 32-bit offsets");
     return DR_E_INVALID;
   }
-  if (g.hplanes && (g.hp_ld % 4 != 0 || g.hp_ld < g.Hd || ((uintptr_t)g.hplanes & 15))) {
-    dr_set_error("gru_fused: h planes need a 16-byte aligned buffer and a row stride >= Hd, % 4 == 0");
-    return DR_E_INVALID;
-  }
   if (g.gh_ws && g.B >= 128 && ((uintptr_t)g.gh_ws | (uintptr_t)g.hout | (uintptr_t)g.sr | (uintptr_t)g.su |
                                  (uintptr_t)g.sn | (uintptr_t)g.sghn) % 16 == 0 && g.ldo % 4 == 0) {
     // split path: hidden product on the tile GEMM, then gather + gates
@@ -800,23 +587,9 @@ int op_gru_fused(const GruArgs& g, hipStream_t s) {
       p.Y = g.gh_ws; p.ldy = 3 * g.Hd;
       DR_TRY(gemm_launch(G_NT, AM_PLAIN, &p, 1, s));
     }
-    if (DR_GATES_LDS && gates_lds_ok(g)) {
-      const int tl = (g.Hd / GL_UNITS) * ((g.B + GL_ROWS - 1) / GL_ROWS);
-      hipLaunchKernelGGL(k_gru_gates_lds, dim3(dr_xcd_grid(tl)), dim3(GL_NT), gates_lds_bytes(g.R * g.C, g.A), s, g);
-      return dr_check_launch("gru_gates_lds");
-    }
     const int tiles = ((g.Hd + GG_UNITS - 1) / GG_UNITS) * ((g.B + GG_ROWS - 1) / GG_ROWS);
-    switch (gates_batch()) {
-      case 4: hipLaunchKernelGGL(k_gru_gates<4>, dim3(dr_xcd_grid(tiles)), dim3(GG_NT), 0, s, g); break;
-      case 16: hipLaunchKernelGGL(k_gru_gates<16>, dim3(dr_xcd_grid(tiles)), dim3(GG_NT), 0, s, g); break;
-      case 32: hipLaunchKernelGGL(k_gru_gates<32>, dim3(dr_xcd_grid(tiles)), dim3(GG_NT), 0, s, g); break;
-      default: hipLaunchKernelGGL(k_gru_gates<8>, dim3(dr_xcd_grid(tiles)), dim3(GG_NT), 0, s, g); break;
-    }
+    hipLaunchKernelGGL(k_gru_gates<8>, dim3(dr_xcd_grid(tiles)), dim3(GG_NT), 0, s, g);
     return dr_check_launch("gru_gates");
-  }
-  if (g.hplanes) {
-    dr_set_error("gru_fused: h planes are written by the split path only (B >= 128 with gh scratch)");
-    return DR_E_INVALID;
   }
   const int tiles = ((g.Hd + 15) / 16) * ((g.B + 15) / 16);
   hipLaunchKernelGGL(k_gru_fused, dim3(dr_xcd_grid(tiles)), dim3(512), 0, s, g);

@@ -1,0 +1,670 @@
+// Persistent posterior scan: Dreamer.warm_start_generator (Dreamer.py:244-262)
+// as ONE launch instead of three launches per step.
+//
+//   t = 0:   pre_0 = feat_0                                  (h_0 = 0: latent_mapper.0 sees only features)
+//   t >= 1:  h_t   = GRUCell(cat(z_{t-1}, a_{t-1}), h_{t-1}) (SequenceModel.py:19-24)
+//            pre_t = feat_t + h_t W_m0h^T                    (latent_mapper.0 on cat(features, h), VAE.py:71-72)
+//   all t:   z_t   = sample(SiLU(LN(pre_t)) W_m3^T + b_m3)    (VAE.py:73-99: softmax, 1 % unimix, argmax(p/Exp(1)))
+//
+// feat_t (the conv encoder + latent_mapper.0's feature columns + bias of all
+// S/2 frames) is one time-batched launch before this one (dr_encoder_features).
+//
+// Why one launch.  The launch form spends ~41 us per step at B = 256 on three
+// dependent kernels that each re-read their weights from L2 / MALL (the GRU's
+// hidden product alone re-streams 7.9 MB of split weight planes per step, and
+// the one-hot gather of W_ih^T another ~60 MB of L2 traffic).  Here every
+// workgroup (one per CU) owns a FIXED tile of each of the three stages for the
+// whole scan, so its weights are loaded once per scan -- the W_hh / latent
+// mapper split3 planes into registers (228 VGPRs per wave in fp32 mode), the
+// tile's 30 columns of W_ih^T into LDS (123 KB) -- and per step only the
+// activations move between CUs:
+//
+//   S1 GRU      tile = MR batch rows x 10 hidden units (3 x 10 gate columns):
+//               gh = h_{t-1} W_hh^T on the bf16 MFMA (split3 6-product f32 scheme,
+//               K split over the 4 waves), gi by gather from the LDS W_ih^T slice
+//               (k_gru_gates' summation order: identical gi), gates.  Reads the
+//               MR rows of h_{t-1} (154 KB at MR = 64).
+//   S2 lm0      tile = 16 rows x 16 of the 200 latent_mapper.0 outputs, K = 600
+//   S3 sampler  tile = MS rows x one 32-class group: LN-SiLU of the MS pre rows,
+//               the group's 32 logits (split3, K = 200), the categorical sampler
+//               (k_ln_gemm_sample's arithmetic and noise keys).
+//
+// Hand-offs (MI355X_MICROARCH.md "Inter-workgroup visibility", valid-form table
+// row 1): every handed-off byte is stored write-through (sc1) and loaded sc1 by
+// its consumers; each storing wave drains (vmcnt 0), the workgroup barriers and
+// ONE lane adds to a per-row-block counter (agent-scope atomic); a consumer's
+// lane 0 polls the counters its rows need (relaxed sc1 loads + s_sleep), then
+// the workgroup barrier releases its loads.  Counters are monotonic within the
+// launch (zeroed by a fill kernel before it), so a stage waits for
+// "count >= producers x steps".  Each stage's outputs sit in a two-slot ring:
+// a producer can only be one step ahead of any reader of the slot it
+// overwrites (DESIGN.md section 5f walks the dependency chain).
+//
+// Deadlock freedom needs every workgroup resident: grid <= CUs of the stream
+// (CU-masked streams fall back to the launch form), 1 workgroup per CU by LDS.
+// Spins are bounded; a timeout sets the status word and the workgroup exits.
+#include "common.h"
+#include "scan.h"
+#include "ops.h"
+
+#include <string.h>
+#include <algorithm>
+
+namespace {
+constexpr int HD = 600, KSH = 19, EH = 200, KSE = 7, NR = 32, NCL = 32, LAT = NR * NCL;
+constexpr int UPT = 10, NUS = HD / UPT, NC2 = (EH + 15) / 16, WLD = 3 * UPT;
+constexpr int NTH = 256;
+constexpr int NPH = 1920;  // op_nt_split3_ws_bytes row padding of 3 HD
+constexpr int NPE = 256;   // ... of EH
+constexpr int NPL = 1024;  // ... of LAT
+constexpr int KSW = 5;     // 32-k steps per wave over K = HD (19 over 4 waves)
+constexpr int KSW3 = 2;    // 32-k steps per wave over K = EH (7 over 4 waves)
+constexpr int KP3 = 232;   // LDS row stride of the LN-SiLU rows (8 mod 16 dwords)
+constexpr int SCR_F = 8192;  // scratch floats (32 KB): idx/zval staging, K-split partials, LN rows
+constexpr int CNT_LD = 32;   // counters 128 B apart
+constexpr int CNT_H = 0, CNT_PRE = 16, CNT_Z = 32, CNT_STATUS = 48;
+}  // namespace
+
+typedef unsigned ps_u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 ps_bf16x8 __attribute__((ext_vector_type(8)));
+
+struct alignas(16) PScanArgs {
+  int B, T, A, step0;
+  const float* wt;  // W_ih^T [LAT + A][3 HD]
+  const float* b_ih;
+  const float* b_hh;
+  const unsigned short* whh;  // W_hh split3 planes [KSH][3][NPH][32]
+  const unsigned short* wm0;  // latent_mapper.0 h-columns [KSH][3][NPE][32]
+  const unsigned short* wm3;  // latent_mapper.3 [KSE][3][NPL][32]
+  const float* ln_g;
+  const float* ln_b;
+  const float* b3;
+  const float* feat;  // [T][B][EH]
+  const float* act;
+  long long act_sb, act_st;
+  dr_noise noise;
+  float unimix;
+  int spin_limit;
+  float* z_out;
+  float* h_out;
+  float* logits_out;
+  float* hb;      // [2][B][HD]
+  float* pre;     // [2][B][EH]
+  int* iz;        // [2][2][B][NR]: slot s: idx [B][NR] then zval [B][NR]
+  unsigned* cnt;  // counters, status
+};
+
+__device__ __forceinline__ f32x4 ps_mfma(ps_u32x4 w, ps_u32x4 a, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(ps_bf16x8, w), __builtin_bit_cast(ps_bf16x8, a),
+                                                  c, 0, 0, 0);
+}
+// NT = 3: the six products of order >= 2^-16, smallest first (k_gemm_wks3's
+// order); NT = 1: bf16 perf mode (plane 0 x RNE(a))
+template <int NT>
+__device__ __forceinline__ f32x4 ps_prod(const ps_u32x4 (&w)[NT], const ps_u32x4 (&a)[NT], f32x4 c) {
+  if constexpr (NT == 3) {
+    c = ps_mfma(w[0], a[2], c);
+    c = ps_mfma(w[1], a[1], c);
+    c = ps_mfma(w[2], a[0], c);
+    c = ps_mfma(w[0], a[1], c);
+    c = ps_mfma(w[1], a[0], c);
+  }
+  return ps_mfma(w[0], a[0], c);
+}
+__device__ __forceinline__ unsigned ps_rne2(float x0, float x1) {
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  const b2 v = {(__bf16)x0, (__bf16)x1};
+  return __builtin_bit_cast(unsigned, v);
+}
+// 8 consecutive k of one row -> the MFMA fragment(s)
+template <int NT>
+__device__ __forceinline__ void ps_split(f32x4 x0, f32x4 x1, ps_u32x4 (&a)[NT]) {
+  if constexpr (NT == 3) {
+    unsigned h[4], m[4], l[4];
+    split3_pair(x0[0], x0[1], h[0], m[0], l[0]);
+    split3_pair(x0[2], x0[3], h[1], m[1], l[1]);
+    split3_pair(x1[0], x1[1], h[2], m[2], l[2]);
+    split3_pair(x1[2], x1[3], h[3], m[3], l[3]);
+    a[0] = (ps_u32x4){h[0], h[1], h[2], h[3]};
+    a[1] = (ps_u32x4){m[0], m[1], m[2], m[3]};
+    a[2] = (ps_u32x4){l[0], l[1], l[2], l[3]};
+  } else {
+    a[0] = (ps_u32x4){ps_rne2(x0[0], x0[1]), ps_rne2(x0[2], x0[3]), ps_rne2(x1[0], x1[1]), ps_rne2(x1[2], x1[3])};
+  }
+}
+
+// write-through (sc1) buffer accesses of the handed-off rings
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ps_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 ps_ld4(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 16));
+}
+__device__ __forceinline__ float ps_ld1(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, 0, 16));
+}
+__device__ __forceinline__ void ps_st1(__amdgpu_buffer_rsrc_t r, unsigned byte_off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)byte_off, 0, 16);
+}
+__device__ __forceinline__ void ps_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// lane 0 of the workgroup: poll until *c >= target (relaxed sc1 loads + s_sleep)
+__device__ __forceinline__ bool ps_poll(const unsigned* c, unsigned target, int limit, unsigned* status) {
+  int spins = 0;
+  while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    __builtin_amdgcn_s_sleep(2);
+    if (++spins > limit) {
+      __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+  return true;
+}
+// every storing wave drained, then one lane signals for the workgroup
+__device__ __forceinline__ void ps_signal(unsigned* c) {
+  ps_drain();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int NT, int MR, int MS>
+__global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int s_ok;
+  const int B = g.B, T = g.T, A = g.A;
+  const int b = blockIdx.x, tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int n1 = (B / MR) * NUS, n2 = (B / 16) * NC2, n3 = (B / MS) * NR;
+  const bool do1 = b < n1, do2 = b < n2, do3 = b < n3;
+  float* wih = smem;                                  // [LAT + A][WLD]
+  float* scr = smem + (((LAT + A) * WLD + 3) & ~3);   // [SCR_F]
+  unsigned* cnt = g.cnt;
+  unsigned* status = cnt + CNT_LD * CNT_STATUS;
+  const int lim = g.spin_limit;
+  const __amdgpu_buffer_rsrc_t rh = ps_rsrc(g.hb, 2u * B * HD * 4u);
+  const __amdgpu_buffer_rsrc_t rp = ps_rsrc(g.pre, 2u * B * EH * 4u);
+  const __amdgpu_buffer_rsrc_t rz = ps_rsrc(g.iz, 4u * B * NR * 4u);
+
+  // ---- tiles and their resident weights -------------------------------------
+  const int rg = b / NUS, us = b - rg * NUS, r0 = rg * MR, u0 = us * UPT;  // S1
+  const int rt2 = b / NC2, ct2 = b - rt2 * NC2;                            // S2
+  const int rs = b / NR, gq = b - rs * NR, m3 = rs * MS;                   // S3
+  ps_u32x4 w1[KSW][NT][2], w2[KSW][NT], w3[KSW3][3][2];
+#pragma unroll
+  for (int s = 0; s < KSW; ++s) {
+    const int ks = KSW * wave + s;
+#pragma unroll
+    for (int p = 0; p < NT; ++p) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const int c = ct * 16 + r;
+        const bool ok = do1 && ks < KSH && c < WLD;
+        const int n = ok ? (c / UPT) * HD + u0 + (c % UPT) : 0;
+        const unsigned e = ok ? (unsigned)(((ks * 3 + p) * NPH + n) * 32 + 8 * q) : 0u;
+        w1[s][p][ct] = *(const DR_GLOBAL ps_u32x4*)((const DR_GLOBAL char*)g.whh + (e << 1));
+        if (!ok) w1[s][p][ct] = (ps_u32x4){0u, 0u, 0u, 0u};
+      }
+      const int c2 = ct2 * 16 + r;
+      const bool ok2 = do2 && ks < KSH && c2 < EH;
+      const unsigned e2 = ok2 ? (unsigned)(((ks * 3 + p) * NPE + c2) * 32 + 8 * q) : 0u;
+      w2[s][p] = *(const DR_GLOBAL ps_u32x4*)((const DR_GLOBAL char*)g.wm0 + (e2 << 1));
+      if (!ok2) w2[s][p] = (ps_u32x4){0u, 0u, 0u, 0u};
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < KSW3; ++s) {
+    const int ks = KSW3 * wave + s;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const bool ok = do3 && ks < KSE;
+        const int n = gq * NCL + ct * 16 + r;
+        const unsigned e = ok ? (unsigned)(((ks * 3 + p) * NPL + n) * 32 + 8 * q) : 0u;
+        w3[s][p][ct] = *(const DR_GLOBAL ps_u32x4*)((const DR_GLOBAL char*)g.wm3 + (e << 1));
+        if (!ok) w3[s][p][ct] = (ps_u32x4){0u, 0u, 0u, 0u};
+      }
+  }
+  // S3's LayerNorm parameters (one float4 per lane: K = 200 <= 256) and logit biases
+  const bool okk = lane < EH / 4;
+  const float4 lng = dr_ld4(g.ln_g, okk ? 4u * lane : 0u), lnb = dr_ld4(g.ln_b, okk ? 4u * lane : 0u);
+  // S1's W_ih^T slice: rows k of W_ih^T (latents, then actions), the tile's 30 gate columns
+  if (do1) {
+    const int nrow = LAT + A;
+    for (int x = tid; x < nrow * WLD; x += NTH) {
+      const int k = x / WLD, c = x - k * WLD;
+      wih[x] = dr_ld1(g.wt, (unsigned)(k * 3 * HD + (c / UPT) * HD + u0 + (c % UPT)));
+    }
+  }
+  __syncthreads();
+
+  // S3 sampler lanes: row ml3 = tid / 8 of the MS-row block, classes 4 sub .. 4 sub + 3
+  const int ml3 = tid >> 3, sub = tid & 7, c3 = 4 * sub;
+  const bool act3 = do3 && ml3 < MS;
+  const int m3r = m3 + (act3 ? ml3 : 0);
+  const float bc[4] = {dr_ld1(g.b3, (unsigned)(gq * NCL + c3)), dr_ld1(g.b3, (unsigned)(gq * NCL + c3 + 1)),
+                       dr_ld1(g.b3, (unsigned)(gq * NCL + c3 + 2)), dr_ld1(g.b3, (unsigned)(gq * NCL + c3 + 3))};
+  const unsigned long long* rngp = g.noise.rng;
+  const unsigned long long rng_seed = rngp ? rngp[0] : 0ull, rng_off = rngp ? rngp[1] : 0ull;
+
+  constexpr int NP1 = (MR * UPT + NTH - 1) / NTH;  // S1 (row, unit) pairs per thread
+
+  for (int t = 0; t < T; ++t) {
+    const int step = g.step0 + t;
+    // ======================= S1: GRU (t >= 1) ===============================
+    if (t >= 1 && do1) {
+      if (tid == 0) {
+        bool ok = true;
+        for (int i = 0; i < MR / MS && ok; ++i)
+          ok = ps_poll(cnt + CNT_LD * (CNT_Z + r0 / MS + i), (unsigned)(NR * t), lim, status);
+        if (ok && t >= 2) ok = ps_poll(cnt + CNT_LD * (CNT_H + rg), (unsigned)(NUS * (t - 1)), lim, status);
+        s_ok = ok;
+      }
+      __syncthreads();
+      if (!s_ok) return;
+      const unsigned hprev = (unsigned)(((t - 1) & 1) * B * HD);
+      // h_{t-1} fragments of this wave's k-steps, two steps ahead (h_0 = 0: t = 1 skips the product)
+      f32x4 ha[2][MR / 16][2];
+      auto load_h = [&](int s, int slot) {
+        const int ks = KSW * wave + s;
+        const int k = 32 * ks + 8 * q;
+        const bool ok = ks < KSH && k < HD;
+#pragma unroll
+        for (int rt = 0; rt < MR / 16; ++rt) {
+          const unsigned o = 4u * (hprev + (unsigned)((r0 + rt * 16 + r) * HD) + (ok ? (unsigned)k : 0u));
+          ha[slot][rt][0] = ps_ld4(rh, o);
+          ha[slot][rt][1] = ps_ld4(rh, o + 16u);
+          if (!ok) ha[slot][rt][0] = ha[slot][rt][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+      };
+      if (t >= 2) {
+        load_h(0, 0);
+        load_h(1, 1);
+      }
+      // this thread's (row, unit) pairs: h_{t-1} values for the gates
+      float hv[NP1];
+#pragma unroll
+      for (int i = 0; i < NP1; ++i) {
+        const int p = tid + NTH * i;
+        const int row = p / UPT, j = p - row * UPT;
+        const bool ok = t >= 2 && p < MR * UPT;
+        hv[i] = ps_ld1(rh, ok ? 4u * (hprev + (unsigned)((r0 + row) * HD + u0 + j)) : 0u);
+        if (!ok) hv[i] = 0.f;
+      }
+      // stage z_{t-1}'s indices / straight-through values of the MR rows
+      {
+        int* sidx = reinterpret_cast<int*>(scr);
+        float* szv = scr + MR * NR;
+        const unsigned zb = (unsigned)(((t - 1) & 1) * 2 * B * NR);
+        for (int x = tid; x < MR * NR / 4; x += NTH) {
+          const unsigned o = zb + (unsigned)(r0 * NR + 4 * x);
+          const f32x4 iv = ps_ld4(rz, 4u * o), zv = ps_ld4(rz, 4u * (o + (unsigned)(B * NR)));
+          *reinterpret_cast<f32x4*>(&sidx[4 * x]) = iv;
+          *reinterpret_cast<f32x4*>(&szv[4 * x]) = zv;
+        }
+      }
+      __syncthreads();
+      // gi by gather from the LDS slice: groups ascending (fmaf), actions, + b_ih (k_gru_gates' order)
+      float gi[NP1][3];
+      {
+        const int* sidx = reinterpret_cast<const int*>(scr);
+        const float* szv = scr + MR * NR;
+#pragma unroll
+        for (int i = 0; i < NP1; ++i) {
+          const int p = tid + NTH * i;
+          const bool live = p < MR * UPT;
+          const int row = live ? p / UPT : 0, j = live ? p - row * UPT : 0;
+          float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+#pragma unroll 8
+          for (int u = 0; u < NR; ++u) {
+            const int k = u * NCL + sidx[row * NR + u];
+            const float zv = szv[row * NR + u];
+            const float* wr = wih + k * WLD + j;
+            v0 = fmaf(wr[0], zv, v0);
+            v1 = fmaf(wr[UPT], zv, v1);
+            v2 = fmaf(wr[2 * UPT], zv, v2);
+          }
+          for (int ia = 0; ia < A; ++ia) {
+            const float av = dr_ld1(g.act, (unsigned)((r0 + row) * g.act_sb + (t - 1) * g.act_st + ia));
+            const float* wr = wih + (LAT + ia) * WLD + j;
+            v0 = fmaf(wr[0], av, v0);
+            v1 = fmaf(wr[UPT], av, v1);
+            v2 = fmaf(wr[2 * UPT], av, v2);
+          }
+          gi[i][0] = v0 + dr_ld1(g.b_ih, (unsigned)(u0 + j));
+          gi[i][1] = v1 + dr_ld1(g.b_ih, (unsigned)(HD + u0 + j));
+          gi[i][2] = v2 + dr_ld1(g.b_ih, (unsigned)(2 * HD + u0 + j));
+        }
+      }
+      // gh partial over this wave's k-steps
+      f32x4 acc[MR / 16][2];
+#pragma unroll
+      for (int rt = 0; rt < MR / 16; ++rt) acc[rt][0] = acc[rt][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (t >= 2) {
+#pragma unroll
+        for (int s = 0; s < KSW; ++s) {
+          const int slot = s & 1;
+          if (KSW * wave + s < KSH) {
+#pragma unroll
+            for (int rt = 0; rt < MR / 16; ++rt) {
+              ps_u32x4 a[NT];
+              ps_split<NT>(ha[slot][rt][0], ha[slot][rt][1], a);
+#pragma unroll
+              for (int ct = 0; ct < 2; ++ct) {
+                ps_u32x4 w[NT];
+#pragma unroll
+                for (int p = 0; p < NT; ++p) w[p] = w1[s][p][ct];
+                acc[rt][ct] = ps_prod<NT>(w, a, acc[rt][ct]);
+              }
+            }
+          }
+          if (s + 2 < KSW) load_h(s + 2, slot);
+        }
+      }
+      __syncthreads();  // every wave done with the staged indices: the scratch takes the partials
+      // partials: red[wave][(rt * 2 + ct) * 4 + e][lane]
+#pragma unroll
+      for (int rt = 0; rt < MR / 16; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) scr[((wave * (MR / 16) * 2 + rt * 2 + ct) * 4 + e) * 64 + lane] = acc[rt][ct][e];
+      __syncthreads();
+      // gates (torch gru_cell op order) for this thread's pairs
+      const unsigned hcur = (unsigned)((t & 1) * B * HD);
+#pragma unroll
+      for (int i = 0; i < NP1; ++i) {
+        const int p = tid + NTH * i;
+        if (p < MR * UPT) {
+          const int row = p / UPT, j = p - row * UPT, rt = row >> 4, rr16 = row & 15;
+          float gh[3];
+#pragma unroll
+          for (int gt = 0; gt < 3; ++gt) {
+            const int c = gt * UPT + j, ct = c >> 4, ql = (c & 15) >> 2, e = c & 3;
+            const int l = rr16 + 16 * ql;
+            float v = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) v += scr[((w * (MR / 16) * 2 + rt * 2 + ct) * 4 + e) * 64 + l];
+            gh[gt] = v + dr_ld1(g.b_hh, (unsigned)(gt * HD + u0 + j));
+          }
+          const float rr = 1.0f / (1.0f + expf(-(gh[0] + gi[i][0])));
+          const float uu = 1.0f / (1.0f + expf(-(gh[1] + gi[i][1])));
+          const float nn = tanhf(gi[i][2] + gh[2] * rr);
+          const float ho = (hv[i] - nn) * uu + nn;
+          const unsigned o = (unsigned)((r0 + row) * HD + u0 + j);
+          ps_st1(rh, 4u * (hcur + o), ho);
+          if (t == T - 1) g.h_out[o] = ho;
+        }
+      }
+      ps_signal(cnt + CNT_LD * (CNT_H + rg));
+    }
+    // ======================= S2: latent_mapper.0 h-part (t >= 1) ===========
+    if (t >= 1 && do2) {
+      const int m0 = rt2 * 16, n0 = ct2 * 16;
+      if (tid == 0) s_ok = ps_poll(cnt + CNT_LD * (CNT_H + m0 / MR), (unsigned)(NUS * t), lim, status);
+      __syncthreads();
+      if (!s_ok) return;
+      const unsigned hcur = (unsigned)((t & 1) * B * HD);
+      f32x4 ha[KSW][2];
+#pragma unroll
+      for (int s = 0; s < KSW; ++s) {
+        const int ks = KSW * wave + s, k = 32 * ks + 8 * q;
+        const bool ok = ks < KSH && k < HD;
+        const unsigned o = 4u * (hcur + (unsigned)((m0 + r) * HD) + (ok ? (unsigned)k : 0u));
+        ha[s][0] = ps_ld4(rh, o);
+        ha[s][1] = ps_ld4(rh, o + 16u);
+        if (!ok) ha[s][0] = ha[s][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+      // the feature part of this thread's output (plain: written before the launch)
+      const int e2 = tid >> 6, l2 = tid & 63, row2 = l2 & 15, col2 = 4 * (l2 >> 4) + e2;
+      const bool ok2 = n0 + col2 < EH;
+      const float fv = dr_ld1(g.feat, ok2 ? (unsigned)((t * B + m0 + row2) * EH + n0 + col2) : 0u);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KSW; ++s) {
+        if (KSW * wave + s < KSH) {
+          ps_u32x4 a[NT], w[NT];
+          ps_split<NT>(ha[s][0], ha[s][1], a);
+#pragma unroll
+          for (int p = 0; p < NT; ++p) w[p] = w2[s][p];
+          acc = ps_prod<NT>(w, a, acc);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) scr[(wave * 4 + e) * 64 + lane] = acc[e];
+      __syncthreads();
+      if (ok2) {
+        const float v = (((scr[(0 * 4 + e2) * 64 + l2] + scr[(1 * 4 + e2) * 64 + l2]) + scr[(2 * 4 + e2) * 64 + l2]) +
+                         scr[(3 * 4 + e2) * 64 + l2]);
+        ps_st1(rp, 4u * (unsigned)((t & 1) * B * EH + (m0 + row2) * EH + n0 + col2), v + fv);
+      }
+      ps_signal(cnt + CNT_LD * (CNT_PRE + rt2));
+    }
+    // ======================= S3: LN-SiLU -> logits -> sampler ===============
+    if (do3) {
+      // noise of this lane's 4 classes first (VALU only, before any wait)
+      float qn[4] = {1.f, 1.f, 1.f, 1.f};
+      if (act3) {
+        const int m = m3 + ml3;
+        if (g.noise.q) {
+          const float4 qx = dr_ld4(g.noise.q, (unsigned)((((long long)step * B + m) * NR + gq) * NCL + c3));
+          qn[0] = qx.x, qn[1] = qx.y, qn[2] = qx.z, qn[3] = qx.w;
+        } else {
+          const uint32_t st = (uint32_t)(g.noise.stream + step), row = (uint32_t)(g.noise.row0 + m);
+          const uint32_t e0 = (uint32_t)(gq * NCL + c3);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) qn[i] = dr_exp1_k(rng_seed, rng_off, st, row, e0 + i);
+        }
+      }
+      if (t >= 1) {
+        if (tid == 0) {
+          bool ok = true;
+          for (int i = 0; i < MS / 16 && ok; ++i)
+            ok = ps_poll(cnt + CNT_LD * (CNT_PRE + m3 / 16 + i), (unsigned)(NC2 * t), lim, status);
+          s_ok = ok;
+        }
+        __syncthreads();
+        if (!s_ok) return;
+      }
+      // LN-SiLU of the block's rows into LDS (a wave per row, DPP statistics;
+      // k_ln_gemm_sample's arithmetic), zero-padded to 224
+      float* sA = scr;
+#pragma unroll
+      for (int i = 0; i < MS / 4; ++i) {
+        const int ml = wave + 4 * i, m = m3 + ml;
+        f32x4 x = {0.f, 0.f, 0.f, 0.f};
+        if (t == 0) {
+          const float4 xf = dr_ld4(g.feat, okk ? (unsigned)(m * EH + 4 * lane) : 0u);
+          x = (f32x4){xf.x, xf.y, xf.z, xf.w};
+        } else {
+          x = ps_ld4(rp, 4u * ((unsigned)((t & 1) * B * EH + m * EH) + (okk ? 4u * lane : 0u)));
+        }
+        const float mean = wave_sum(okk ? (x[0] + x[1]) + (x[2] + x[3]) : 0.f) / (float)EH;
+        float sq = 0.f;
+        if (okk) {
+          const float dx = x[0] - mean, dy = x[1] - mean, dz = x[2] - mean, dw = x[3] - mean;
+          sq = (dx * dx + dy * dy) + (dz * dz + dw * dw);
+        }
+        const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)EH + 1e-5f);
+        float4 y;
+        y.x = dr_silu_fast((x[0] - mean) * rstd * lng.x + lnb.x);
+        y.y = dr_silu_fast((x[1] - mean) * rstd * lng.y + lnb.y);
+        y.z = dr_silu_fast((x[2] - mean) * rstd * lng.z + lnb.z);
+        y.w = dr_silu_fast((x[3] - mean) * rstd * lng.w + lnb.w);
+        if (!okk) y = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (lane < KSE * 8) *reinterpret_cast<float4*>(&sA[ml * KP3 + 4 * lane]) = y;
+      }
+      __syncthreads();
+      f32x4 acc[MS / 16][2];
+#pragma unroll
+      for (int rt = 0; rt < MS / 16; ++rt) acc[rt][0] = acc[rt][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KSW3; ++s) {
+        const int ks = KSW3 * wave + s;
+        if (ks < KSE) {
+#pragma unroll
+          for (int rt = 0; rt < MS / 16; ++rt) {
+            const float* pa = sA + (rt * 16 + r) * KP3 + 32 * ks + 8 * q;
+            const f32x4 x0 = *reinterpret_cast<const f32x4*>(pa), x1 = *reinterpret_cast<const f32x4*>(pa + 4);
+            ps_u32x4 a[3];
+            ps_split<3>(x0, x1, a);
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+              ps_u32x4 w[3] = {w3[s][0][ct], w3[s][1][ct], w3[s][2][ct]};
+              acc[rt][ct] = ps_prod<3>(w, a, acc[rt][ct]);
+            }
+          }
+        }
+      }
+      __syncthreads();  // sA consumed: the scratch takes the partials
+#pragma unroll
+      for (int rt = 0; rt < MS / 16; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) scr[((wave * (MS / 16) * 2 + rt * 2 + ct) * 4 + e) * 64 + lane] = acc[rt][ct][e];
+      __syncthreads();
+      if (act3) {
+        // logits of classes c3 .. c3 + 3 of row ml3: tile (rt, ct), lane r + 16 q, element e
+        float x[4];
+        const int rt = ml3 >> 4, rr16 = ml3 & 15;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = c3 + i, ct = c >> 4, ql = (c & 15) >> 2, e = c & 3, l = rr16 + 16 * ql;
+          float v = 0.f;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) v += scr[((w * (MS / 16) * 2 + rt * 2 + ct) * 4 + e) * 64 + l];
+          x[i] = v + bc[i];
+        }
+        // the sampler (softmax, 1 % unimix, argmax(p_hat / q), straight-through one-hot)
+        const float unimix = g.unimix;
+        float mx = fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3]));
+        mx = group_max(mx, 8);
+        float ex[4], pu[4], pp[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ex[i] = expf(x[i] - mx);
+        const float se = group_sum((ex[0] + ex[1]) + (ex[2] + ex[3]), 8);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pp[i] = ex[i] / se;
+          pu[i] = 0.99f * pp[i] + unimix;
+        }
+        const float sp = group_sum((pu[0] + pu[1]) + (pu[2] + pu[3]), 8);
+        float best = (pu[0] / sp) / qn[0];
+        int bi = c3;
+#pragma unroll
+        for (int i = 1; i < 4; ++i) {
+          const float v = (pu[i] / sp) / qn[i];
+          bi = v > best ? c3 + i : bi;  // ties keep the lower class
+          best = fmaxf(best, v);
+        }
+        group_argmax(best, bi, 8);
+        const int m = m3 + ml3;
+        const unsigned zb = (unsigned)((t & 1) * 2 * B * NR + m * NR + gq);
+        if (sub == 0) ps_st1(rz, 4u * zb, __int_as_float(bi));
+        if ((unsigned)(bi - c3) < 4u) {
+          const int i = bi - c3;
+          ps_st1(rz, 4u * (zb + (unsigned)(B * NR)), (1.0f + pu[i]) - pu[i]);
+        }
+        if (t == T - 1) {
+          float4 z;
+          z.x = (c3 + 0 == bi) ? ((1.0f + pu[0]) - pu[0]) : 0.0f;
+          z.y = (c3 + 1 == bi) ? ((1.0f + pu[1]) - pu[1]) : 0.0f;
+          z.z = (c3 + 2 == bi) ? ((1.0f + pu[2]) - pu[2]) : 0.0f;
+          z.w = (c3 + 3 == bi) ? ((1.0f + pu[3]) - pu[3]) : 0.0f;
+          const unsigned o = (unsigned)(m * LAT + gq * NCL + c3);
+          dr_st4(g.z_out, o, z);
+          if (g.logits_out) dr_st4(g.logits_out, o, make_float4(x[0], x[1], x[2], x[3]));
+        }
+      }
+      ps_signal(cnt + CNT_LD * (CNT_Z + rs));
+    }
+  }
+}
+
+static size_t pscan_lds_bytes(int A) { return sizeof(float) * ((((size_t)(LAT + A) * WLD + 3) & ~(size_t)3) + SCR_F); }
+
+size_t op_pscan_ring_bytes(int B) {
+  // hb [2][B][HD], pre [2][B][EH], iz [2][2][B][NR], counters
+  return sizeof(float) * ((size_t)2 * B * HD + (size_t)2 * B * EH + (size_t)4 * B * NR) + PSCAN_CNT_BYTES;
+}
+
+bool op_pscan_supported(const dr_dims* d, int B, int T, int A) {
+  return d->hidden == HD && d->enc_hidden == EH && d->rows == NR && d->cols == NCL && A >= 1 && A <= 8 && T >= 2 &&
+         B >= 16 && B <= 256 && B % 16 == 0 && (B <= 64 || B % 64 == 0);
+}
+
+template <int NT, int MR, int MS>
+static int launch_pscan(const PScanArgs& a, int grid, hipStream_t s) {
+  auto k = k_pscan<NT, MR, MS>;
+  const size_t lds = pscan_lds_bytes(a.A);
+  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, NTH, lds) != hipSuccess || per_cu < 1) {
+    dr_set_error("pscan: no residency");
+    return DR_E_UNSUPPORTED;
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(NTH), lds, s, a);
+  return dr_check_launch("pscan");
+}
+
+int op_pscan(const dr_dims* d, const dr_world_model* wm, int B, int T, int A, const float* feat, const float* actions,
+             long long act_sb, long long act_st, const float* wt, const void* whh_planes, const void* m0_planes,
+             const void* m3_planes, dr_noise noise, int step0, float* z_out, float* h_out, float* logits_out,
+             void* ring, hipStream_t s) {
+  if (!op_pscan_supported(d, B, T, A)) {
+    dr_set_error("pscan: unsupported shape (B=%d T=%d)", B, T);
+    return DR_E_UNSUPPORTED;
+  }
+  const int MR = B <= 64 ? 16 : (B <= 128 ? 32 : 64), MS = B <= 128 ? 16 : 32;
+  const int grid = std::max(std::max((B / MR) * NUS, (B / 16) * NC2), (B / MS) * NR);
+  // every workgroup must be resident: all CUs of an unmasked stream
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    dr_set_error("pscan: device query");
+    return DR_E_HIP;
+  }
+  unsigned mask[16] = {0};
+  int avail = cus;
+  if (hipExtStreamGetCUMask(s, 16, mask) == hipSuccess) {
+    int n = 0;
+    for (int i = 0; i < 16; ++i) n += __builtin_popcount(mask[i]);
+    if (n > 0) avail = std::min(avail, n);
+  }
+  if (grid > avail) {
+    dr_set_error("pscan: grid %d > %d CUs of the stream", grid, avail);
+    return DR_E_UNSUPPORTED;
+  }
+  char* base = reinterpret_cast<char*>(ring);
+  PScanArgs a;
+  memset(&a, 0, sizeof(a));
+  a.B = B; a.T = T; a.A = A; a.step0 = step0;
+  a.wt = wt; a.b_ih = wm->b_ih; a.b_hh = wm->b_hh;
+  a.whh = (const unsigned short*)whh_planes;
+  a.wm0 = (const unsigned short*)m0_planes;
+  a.wm3 = (const unsigned short*)m3_planes;
+  a.ln_g = wm->map1.w; a.ln_b = wm->map1.b; a.b3 = wm->map3.b;
+  a.feat = feat; a.act = actions; a.act_sb = act_sb; a.act_st = act_st;
+  a.noise = noise;
+  a.unimix = (float)(0.01 * (1.0 / d->cols));
+  a.spin_limit = 1 << 22;
+  a.z_out = z_out; a.h_out = h_out; a.logits_out = logits_out;
+  a.hb = reinterpret_cast<float*>(base);
+  a.pre = a.hb + (size_t)2 * B * HD;
+  a.iz = reinterpret_cast<int*>(a.pre + (size_t)2 * B * EH);
+  a.cnt = reinterpret_cast<unsigned*>(a.iz + (size_t)4 * B * NR);
+  // counters zeroed by a kernel (captured graphs replay it; a memset node was seen not to)
+  DR_TRY(op_fill(PSCAN_CNT_BYTES / 4, reinterpret_cast<float*>(a.cnt), 0.f, s));
+  const bool bf = d->precision == DR_PREC_BF16;
+#define PS_L(NT, MRv, MSv) \
+  if (MR == MRv && MS == MSv) return launch_pscan<NT, MRv, MSv>(a, grid, s);
+  if (bf) {
+    PS_L(1, 16, 16) PS_L(1, 32, 16) PS_L(1, 64, 32)
+  } else {
+    PS_L(3, 16, 16) PS_L(3, 32, 16) PS_L(3, 64, 32)
+  }
+#undef PS_L
+  dr_set_error("pscan: no instance");
+  return DR_E_INVALID;
+}

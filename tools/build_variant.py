@@ -12,7 +12,7 @@ from dreamer_amd import build as B  # noqa: E402
 
 def main():
     name, flags = sys.argv[1], sys.argv[2:]
-    obj = os.path.join(B.HERE, f"_build_{name}")
+    obj = os.path.join(os.path.dirname(os.path.abspath(__file__)), "variants", f"_build_{name}")
     os.makedirs(obj, exist_ok=True)
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "variants", f"libdreamer_hip_{name}.so")
 
