@@ -19,7 +19,10 @@ slice of the batch; the exchange is one all-gather of the lambda returns
 Each phase is captured once into a HIP graph and replayed; collectives run
 between the phase graphs.
 """
+import weakref
+
 import numpy as np
+
 import torch
 
 from . import _lib as L
@@ -56,23 +59,17 @@ class ImaginationEngine:
         self.use_graph = use_graph
         self.graph = None
         self.graph_key = None
-        # Optional second stream for branches that could overlap inside an
-        # epoch graph: the time-chunked conv encoder under the posterior scan
-        # and the critic backward beside the actor BPTT.  Measured on MI355X
-        # (profiles/r01_ab_overlap.txt) neither pays: the conv kernels fill
-        # every CU slot, so the scan's small kernels only queue behind them,
-        # and a forked branch slowed every later graph replay by ~6 %.  Both
-        # stay available behind DREAMER_WARM_CHUNK / DREAMER_FORK for
-        # re-measurement; the defaults run one stream, one encoder chunk.
-        # Round 4 re-tried the chunked encoder on a CU-masked stream beside a
-        # high-priority scan (the fence that pays for the pipelined epochs,
-        # warm_stream): 8-step chunks unfenced 7.56 ms per epoch against 6.92
-        # one-chunk, fenced to 7/8 of the CUs 17.9-18.9 ms -- every later phase
-        # of the epoch slowed 3-4x (profiles/r04l_overlap_phase_probe.txt).
+        # Second stream: the conv encoder of the warm start (one chunk, the
+        # scan waits on it) and the critic backward beside the actor BPTT in
+        # losses_and_grads(fork=True).  Measured and dropped:
+        # time-chunked encoding under the posterior scan (r01 and r04:
+        # slower, every later phase of the epoch 3-4x slower when fenced,
+        # profiles/r04l_overlap_phase_probe.txt) and a forked critic backward
+        # inside the epoch graph (~6 % slower replays, r01_ab_overlap.txt).
         self.side = torch.cuda.Stream(self.dev)
-        import os
-        self.chunks = self.warm_chunks(self.T, int(os.environ.get("DREAMER_WARM_CHUNK", str(self.T))))
-        self.fork = os.environ.get("DREAMER_FORK", "0") == "1"
+        self.chunks = [(0, self.T)]
+        self._masked_streams = []
+        weakref.finalize(self, ImaginationEngine._release_streams, self._masked_streams)
         self._alloc()
 
     # ------------------------------------------------------------------ setup
@@ -298,7 +295,7 @@ class ImaginationEngine:
         return a.elapsed_time(b) / reps
 
     def _ph_update(self):
-        self.losses_and_grads(fork=self.fork)
+        self.losses_and_grads(fork=False)
 
     def _ph_optim(self):
         self.optimise()
@@ -400,8 +397,20 @@ class ImaginationEngine:
             mask = (ctypes.c_uint * len(words))(*words)
             h = ctypes.c_void_p()
             L.call("dr_stream_create_cumask", len(words), mask, ctypes.byref(h))
-        self._masked_streams = getattr(self, "_masked_streams", []) + [h]
+        self._masked_streams.append(h.value)
         return torch.cuda.ExternalStream(h.value, device=self.dev)
+
+    @staticmethod
+    def _release_streams(handles):
+        """Destroy the CU-masked HIP streams of warm_stream (engine teardown):
+        synchronise each, then dr_stream_destroy."""
+        while handles:
+            h = handles.pop()
+            try:
+                torch.cuda.ExternalStream(h).synchronize()
+                L.call("dr_stream_destroy", h)
+            except Exception:  # interpreter shutdown: the runtime may be gone
+                pass
 
     def _pipe_capture(self, key):
         dev, B, H = self.dev, self.B, self.H

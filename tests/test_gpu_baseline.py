@@ -169,10 +169,12 @@ def test_baseline_b16_vs_reference(gpu):
     assert abs(pre["S"] - float(fx["S_after"])) <= 1e-6 * float(fx["S_after"])
 
 
-@pytest.mark.parametrize("B,data", [(64, "synthetic"), (256, "synthetic"), (16, "fixture")])
+@pytest.mark.parametrize("B,data", [(64, "synthetic"), (256, "synthetic"), (512, "synthetic"), (16, "fixture")])
 def test_epoch_vs_oracle_at_baseline_shape(B, data, gpu):
     """configs[1] (B=64) and the north-star batch (B=256), S=64 H=15, full
-    widths, reference default init, synthetic replay; and B=16 on the tests'
+    widths, reference default init, synthetic replay; B=512 (configs[2]'s
+    global batch in ONE process: the shape past 256 rows where the skinny
+    GEMMs widen their tiles) and B=16 on the tests'
     fixture replay (formula.replay_data: raw N(0,1) rewards, a terminal at
     index 37)."""
     import bench

@@ -14,12 +14,15 @@ that row's trajectory then diverges from the oracle's.  The test reports:
 * the fraction of batch rows whose trajectory diverged (any flipped index, or
   an h0 / hidden-state error above 1e-3 of the row's norm -- a flip inside the
   warm start that left z0 unchanged still shows in h0);
-* losses, S, and the clipped gradients (normwise) against the oracle.
+* losses, S, and the clipped gradients (normwise) against the oracle, with
+  a yardstick: the same oracle epoch with the noise of the diverged rows
+  re-drawn (what re-sampling those rows alone moves the gradients by).
 
 The mu head is given non-zero weights (the reference's default init zeroes it,
 Agent.py:188-189, which made every mus comparison vacuous).
 
-Bounds: fp32 -- at most 2 % of the rows diverge, losses within 1e-3
+Bounds: clipped gradients normwise <= 2 x yardstick + 1e-3 (fp32) / 2e-2
+(bf16); fp32 -- at most 2 % of the rows diverge, losses within 1e-3
 relative (first run, round 4: 0 flips, 0 rows diverged, mus 3.0e-7 and
 hiddens 1.6e-7 normwise); bf16 -- at most 50 % of the rows diverge, losses
 within 2e-2 relative (first run: flip fractions 5.2e-3 warm / 8.3e-3 dream,
@@ -104,14 +107,42 @@ def test_unguarded_flip_rate_B256(precision, gpu):
         got = torch.cat([f.grad[f.offsets[k.split(".", 1)[1]]:f.offsets[k.split(".", 1)[1]] + gr.numel()].cpu()
                          for k, gr in zip(keys, grads)])
         m[name] = _nw(got, want)
+    # Yardstick for the gradients: a diverged row is a different sample of the
+    # same policy / world model.  Re-draw the noise of exactly those rows and
+    # run the oracle again; the gradient distance between the two oracle
+    # epochs is what the divergence alone moves the gradients by.
+    yard = {"grad_actor": 0.0, "grad_critic": 0.0}
+    if bool(div.any()):
+        g2 = torch.Generator().manual_seed(977)
+        rows = torch.nonzero(div).reshape(-1)
+        q_warm2, eps2, q2 = q_warm.clone(), eps.clone(), q.clone()
+        for b in rows.tolist():
+            q_warm2[:, b * R:(b + 1) * R] = torch.empty(S // 2, R, C).exponential_(generator=g2)
+            q2[:, b * R:(b + 1) * R] = torch.empty(H, R, C).exponential_(generator=g2)
+            eps2[:, b] = torch.randn(H, 1, A, generator=g2)
+        ref2 = oracle_epoch(P, obs, act, S, H, R, C, q_warm2, eps2, q2, S0, guard=_NoGuard())
+        for grads, grads2, name in ((ref["ts"]["grad_actor_clipped"], ref2["ts"]["grad_actor_clipped"], "grad_actor"),
+                                    (ref["ts"]["grad_critic_clipped"], ref2["ts"]["grad_critic_clipped"],
+                                     "grad_critic")):
+            yard[name] = _nw(torch.cat([x.reshape(-1) for x in grads2]), torch.cat([x.reshape(-1) for x in grads]))
+    m["yardstick"] = yard
     print(f"{precision} epoch B=256 on NATURAL noise vs the fp32 oracle: {m}")
     assert float(mu.abs().max()) > 1e-3, "the mu head must be live for the mus comparison"
+    # clipped gradients, normwise: at most twice what re-sampling the diverged
+    # rows moves them by, plus the rounding floor of the mode
+    floor = 1e-3 if precision == "fp32" else 2e-2
+    for name in ("grad_actor", "grad_critic"):
+        assert m[name] <= 2.0 * yard[name] + floor, (name, m)
     if precision == "fp32":
         assert m["rows_diverged"] <= 0.02, m
         rel = 1e-3
         if bool(ok.any()):
             assert m["mus_ok_rows"] <= 1e-4 and m["hiddens_ok_rows"] <= 1e-4, m
     else:
+        # one flip anywhere in a row's 1,472 draws diverges the row; at the
+        # measured per-draw flip rates (5e-3 warm / 8e-3 dream, round 4) about
+        # a third of the rows diverge.  The bound is 50 % with the gradient
+        # yardstick above as the check that the divergence is benign.
         assert m["rows_diverged"] <= 0.5, m
         rel = 2e-2
     assert abs(pre["lc"] - lc_ref) <= rel * abs(lc_ref), m

@@ -204,19 +204,24 @@ def test_graph_replay_matches_eager(gpu):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("which,sched", [("small", None), ("full", None), ("full", "0.875:-1")])
+@pytest.mark.parametrize("which,sched", [("small", None), ("full", None), ("full", "1.0:0:1"), ("full", "0.875:0:1"),
+                                         ("full", "0.875:-1:0")])
 def test_pipelined_epochs_match_sequential(which, sched, gpu, monkeypatch):
     """run_many (warm start of epoch e+1 on a second stream beside epoch e's
     actor-critic chain) == the same epochs run one after another, bit for
     bit: losses of every epoch, actor / critic / target parameters, S.
-    sched "f:p": the warm stream restricted to a share f of the CUs
-    (dr_stream_create_cumask) and the chain on a stream of priority p."""
+    sched "f:p:w": the warm stream restricted to a share f of the CUs
+    (dr_stream_create_cumask; 1.0 = an unfenced plain stream), the chain on a
+    stream of priority p, w = DREAMER_WARM0_MAIN (1: a call's first warm start
+    on the chain's stream; 0: every warm start on the warm stream).  The
+    default (None) is "0.875:-1:1"."""
     from dreamer_amd.engine import ImaginationEngine
     from formula import replay_data
     if sched:
-        frac, prio = sched.split(":")
+        frac, prio, w0 = sched.split(":")
         monkeypatch.setenv("DREAMER_WARM_CUS", frac)
         monkeypatch.setenv("DREAMER_CHAIN_PRIORITY", prio)
+        monkeypatch.setenv("DREAMER_WARM0_MAIN", w0)
     fx = load_fixture("small_epoch")
     hw = (32, 32) if which == "small" else (64, 64)
     B, S, H, K = (8, 8, 5, 5) if which == "small" else (16, 16, 6, 4)
