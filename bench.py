@@ -349,26 +349,29 @@ def profile_encoder_ms(precision):
     (profiles/r*_kernel_stats*.txt; tools/prof_summary.py format): the sum of
     the average durations of every kernel launched as often as the fused conv1 +
     conv2 kernel (one launch per encode: the convs, their weight repacks, the
-    projection).  Returns (ms, kernels, source) or (None, None, None)."""
+    projection).  Returns (ms, kernels, source, source_hash or None) or Nones."""
     import glob
     import re
     tag = "_bf16" if precision == "bf16" else ""
     paths = [p for p in sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_kernel_stats{tag}.txt")))
              if precision == "bf16" or "_bf16" not in p]
     if not paths:
-        return None, None, None
+        return None, None, None, None
     path = paths[-1]
     rows = []
+    src = None
     for line in open(path):
+        if line.startswith("# source "):
+            src = line.split()[2]
         m = re.match(r"\s*([\d.]+)\s+(\d+)\s+([\d.]+)\s+(.*)", line)
         if m:
             rows.append((int(m.group(2)), float(m.group(3)), m.group(4)))
     enc = [r for r in rows if "k_enc12" in r[2]]
     if not enc:
-        return None, None, None
+        return None, None, None, None
     n = enc[0][0]
     grp = [r for r in rows if r[0] == n]
-    return sum(r[1] for r in grp) / 1e3, [r[2].split("(")[0][:60] for r in grp], os.path.relpath(path, REPO)
+    return sum(r[1] for r in grp) / 1e3, [r[2].split("(")[0][:60] for r in grp], os.path.relpath(path, REPO), src
 
 
 def make_dreamer(cfg, dev, B, S, H, res, ac_epochs, world, rank, group, precision, depth=4):
@@ -636,11 +639,16 @@ def main():
         out["roofline"]["frac_vs_bf16_pipe"] = round(6 * achieved / BF16_MFMA_PEAK_TFLOPS, 4)
     if (B, S, H, res) == (256, 64, 15, 64):
         # the same group from the committed kernel trace (per-kernel averages under the profiler)
-        pms, pk, psrc = profile_encoder_ms(args.precision)
+        pms, pk, psrc, phash = profile_encoder_ms(args.precision)
         if pms:
+            sys.path.insert(0, os.path.join(REPO, "tools"))
+            from prof_summary import source_hash
+            same = phash is not None and phash == source_hash()
             out["roofline"]["profile"] = {"encoder_ms": round(pms, 4), "frac": round(enc_flops / (pms / 1e3) / 1e12 / peak, 4),
                                           "live_over_profile": round(enc_s * 1e3 / pms, 4), "kernels": pk,
-                                          "source": psrc}
+                                          "source": psrc, "source_hash": phash, "matches_tree": same,
+                                          "note": ("committed kernel trace of this source tree" if same else
+                                                   "HISTORICAL: committed kernel trace of another source tree")}
     mf = PATH_MFLOP_PER_STEP.get((S, H, res))
     if mf is not None:
         tf = value * mf * 1e6 / 1e12

@@ -307,7 +307,38 @@ class ImaginationEngine:
               ("returns", self.returns, self._allgather_R if self.dp else None),
               ("update", self._ph_update, self._allreduce_grads if self.dp else None),
               ("optim", self._ph_optim, None)]
+        if self.dp:
+            # data-parallel: the update in two phase graphs, so that the
+            # critic's gradient all-reduce (issued async on RCCL's stream as
+            # soon as the critic backward is enqueued) runs under the actor's
+            # BPTT; the actor part is reduced after it (Agent.py:141-148)
+            ph[3:4] = [("critic", self._ph_critic, self._allreduce_critic_async),
+                       ("actor", self._ph_actor, self._allreduce_actor)]
         return ph
+
+    def _ph_critic(self):
+        """DP update, part 1: online critic forward, update_S, the actor loss
+        and its dL/dmu / dL/dsigma, the critic's CE backward, both loss slots
+        (the kernel order of losses_and_grads(fork=False) without the BPTT)."""
+        ag, d, st = self.dr.agent, self.d, hip.stream()
+        B, H = self.B, self.H
+        M = B * (H + 1)
+        scale = 1.0 / float(B * self.wsize * H)
+        L.call("dr_critic_fwd", d, ag.critic_struct(), M, L.ptr(self.hiddens), d.hidden, L.ptr(self.latents),
+               d.rows * d.cols, None, L.ptr(self.V_c), L.ptr(self.ctape), L.ptr(self.ws_cr), self.ws_cr.numel(), st)
+        self._actor_loss()
+        L.call("dr_critic_loss_bwd", d, ag.critic_struct(), B, H, L.ptr(self.hiddens), L.ptr(self.latents),
+               L.ptr(self.R), L.ptr(self.ctape), scale, L.ptr(ag.loss_slot(1)), ag.critic_struct(grad=True),
+               L.ptr(self.ws_cr), self.ws_cr.numel(), st)
+        ag.loss_slot(0).copy_(self.loss_a[0:1])
+
+    def _ph_actor(self):
+        """DP update, part 2: the actor's BPTT (dr_imagine_bwd)."""
+        ag, d = self.dr.agent, self.d
+        L.call("dr_imagine_bwd", d, self.dr.world_model.packed(), ag.actor_struct(), self.B, self.H,
+               L.ptr(self.latents), L.ptr(self.hiddens), L.ptr(self.actions), L.ptr(self.g_mu), L.ptr(self.g_sig),
+               None, None, None, L.ptr(self.tape), ag.actor_struct(grad=True), L.ptr(self.ws_im), self.ws_im.numel(),
+               hip.stream())
 
     def epoch_body(self):
         for _, body, coll in self.phases():
@@ -325,6 +356,24 @@ class ImaginationEngine:
         import torch.distributed as dist
         ag = self.dr.agent
         dist.all_reduce(ag.grad_buffer, op=dist.ReduceOp.SUM, group=self.world[2])
+        ag.loss_buffer.div_(self.wsize)
+
+    def _allreduce_critic_async(self):
+        """[critic grads | loss slots] of the flat buffer, async (RCCL's own
+        stream waits on the current one); waited for in _allreduce_actor."""
+        import torch.distributed as dist
+        ag = self.dr.agent
+        na = ag.fa.grad.numel()
+        self._critic_work = dist.all_reduce(ag.grad_buffer[na:], op=dist.ReduceOp.SUM, group=self.world[2],
+                                            async_op=True)
+
+    def _allreduce_actor(self):
+        import torch.distributed as dist
+        ag = self.dr.agent
+        na = ag.fa.grad.numel()
+        dist.all_reduce(ag.grad_buffer[:na], op=dist.ReduceOp.SUM, group=self.world[2])
+        self._critic_work.wait()
+        self._critic_work = None
         ag.loss_buffer.div_(self.wsize)
 
     # ----------------------------------------------------------------- driver
