@@ -217,11 +217,9 @@ struct ObsWs {
   float *gi, *gh, *pre1, *logits, *wt, *hb[2];
   int* idx;
   void *s3m0, *s3whh;  // bf16 planes of latent_mapper.0's h-columns and W_hh (k_gemm_wks3)
-  void* s3m3;          // split3 planes of latent_mapper.3 (persistent scan)
   void* ring;          // persistent scan: ring buffers + counters (scan.hip)
 };
 static void obs_carve(Carve& c, const dr_dims* d, int B, ObsWs& w) {
-  w.s3m3 = c.raw(op_nt_split3_ws_bytes(latent(d), d->enc_hidden));
   w.ring = c.raw(op_pscan_ring_bytes(B));
   w.s3m0 = c.raw(op_nt_split3_ws_bytes(d->enc_hidden, d->hidden));
   w.s3whh = c.raw(op_nt_split3_ws_bytes(3 * d->hidden, d->hidden));
@@ -266,10 +264,7 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
   }
   // the warm start (no z_init / h_init) as ONE persistent launch (scan.hip)
   if (DR_PSCAN && z_init == nullptr && h_init == nullptr && op_pscan_supported(d, B, T, d->action)) {
-    DR_TRY(op_nt_repack_split3(3 * Hd, Hd, wm->w_hh, Hd, w.s3whh, s));
-    DR_TRY(op_nt_repack_split3(eh, Hd, wm->map0.w + F, F + Hd, w.s3m0, s));
-    DR_TRY(op_nt_repack_split3(L, eh, wm->map3.w, eh, w.s3m3, s));
-    const int rc = op_pscan(d, wm, B, T, d->action, feat, actions, act_sb, act_st, w.wt, w.s3whh, w.s3m0, w.s3m3,
+    const int rc = op_pscan(d, wm, B, T, d->action, feat, actions, act_sb, act_st, w.wt, wm->map0.w + F, F + Hd,
                             noise, 0, z_out, h_out, logits_out, w.ring, s);
     if (rc != DR_E_UNSUPPORTED) return rc;
   }

@@ -9,11 +9,9 @@
 bool op_pscan_supported(const dr_dims* d, int B, int T, int A);
 // caller-owned ring buffers + counters of one launch
 size_t op_pscan_ring_bytes(int B);
-// z_init = h_init = NULL form of dr_observe_scan.  wt = W_ih^T [L + A][3 hidden];
-// *_planes = op_nt_repack_split3 planes of W_hh, latent_mapper.0's h-columns,
-// latent_mapper.3.  DR_E_UNSUPPORTED when the shape or the stream's CUs do not
+// z_init = h_init = NULL form of dr_observe_scan.  wt = W_ih^T [L + A][3 hidden]
+// (op_transpose); m0h = latent_mapper.0's h-columns (row stride ldm0).  DR_E_UNSUPPORTED when the shape or the stream's CUs do not
 // allow every workgroup to be resident (the caller then runs the launch form).
 int op_pscan(const dr_dims* d, const dr_world_model* wm, int B, int T, int A, const float* feat, const float* actions,
-             long long act_sb, long long act_st, const float* wt, const void* whh_planes, const void* m0_planes,
-             const void* m3_planes, dr_noise noise, int step0, float* z_out, float* h_out, float* logits_out,
+             long long act_sb, long long act_st, const float* wt, const float* m0h, long long ldm0, dr_noise noise, int step0, float* z_out, float* h_out, float* logits_out,
              void* ring, hipStream_t s);

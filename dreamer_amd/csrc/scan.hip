@@ -54,9 +54,6 @@ namespace {
 constexpr int HD = 600, KSH = 19, EH = 200, KSE = 7, NR = 32, NCL = 32, LAT = NR * NCL;
 constexpr int UPT = 10, NUS = HD / UPT, NC2 = (EH + 15) / 16, WLD = 3 * UPT;
 constexpr int NTH = 256;
-constexpr int NPH = 1920;  // op_nt_split3_ws_bytes row padding of 3 HD
-constexpr int NPE = 256;   // ... of EH
-constexpr int NPL = 1024;  // ... of LAT
 constexpr int KSW = 5;     // 32-k steps per wave over K = HD (19 over 4 waves)
 constexpr int KSW3 = 2;    // 32-k steps per wave over K = EH (7 over 4 waves)
 constexpr int KP3 = 232;   // LDS row stride of the LN-SiLU rows (8 mod 16 dwords)
@@ -73,9 +70,10 @@ struct alignas(16) PScanArgs {
   const float* wt;  // W_ih^T [LAT + A][3 HD]
   const float* b_ih;
   const float* b_hh;
-  const unsigned short* whh;  // W_hh split3 planes [KSH][3][NPH][32]
-  const unsigned short* wm0;  // latent_mapper.0 h-columns [KSH][3][NPE][32]
-  const unsigned short* wm3;  // latent_mapper.3 [KSE][3][NPL][32]
+  const float* whh;  // W_hh [3 HD][HD]
+  const float* wm0;  // latent_mapper.0 [EH][F + HD]: its h-columns start at column F
+  long long ldm0;
+  const float* wm3;  // latent_mapper.3 [LAT][EH]
   const float* ln_g;
   const float* ln_b;
   const float* b3;
@@ -130,6 +128,46 @@ __device__ __forceinline__ void ps_split(f32x4 x0, f32x4 x1, ps_u32x4 (&a)[NT]) 
     a[2] = (ps_u32x4){l[0], l[1], l[2], l[3]};
   } else {
     a[0] = (ps_u32x4){ps_rne2(x0[0], x0[1]), ps_rne2(x0[2], x0[3]), ps_rne2(x1[0], x1[1]), ps_rne2(x1[2], x1[3])};
+  }
+}
+
+// A resident weight fragment: the 8 consecutive k of one weight row a lane
+// feeds to the MFMA.  NT = 3 keeps them f32 (8 VGPRs) and splits them per use
+// (exact truncation split, 6 products); NT = 1 keeps their RNE bf16 (4 VGPRs).
+template <int NT>
+struct PsFrag {
+  f32x4 x0, x1;
+};
+template <>
+struct PsFrag<1> {
+  ps_u32x4 b;
+};
+template <int NT>
+__device__ __forceinline__ PsFrag<NT> ps_frag(const float* W, unsigned e, bool ok) {
+  const float4 a = dr_ld4(W, ok ? e : 0u), c = dr_ld4(W, ok ? e + 4u : 0u);
+  f32x4 x0 = {a.x, a.y, a.z, a.w}, x1 = {c.x, c.y, c.z, c.w};
+  if (!ok) x0 = x1 = (f32x4){0.f, 0.f, 0.f, 0.f};
+  PsFrag<NT> f;
+  if constexpr (NT == 3) {
+    f.x0 = x0;
+    f.x1 = x1;
+  } else {
+    ps_u32x4 b[1];
+    ps_split<1>(x0, x1, b);
+    f.b = b[0];
+  }
+  return f;
+}
+// the opaque copy keeps the compiler from hoisting the split of a resident
+// fragment out of the step loop (that would re-create the 12-VGPR planes)
+template <int NT>
+__device__ __forceinline__ void ps_wsplit(const PsFrag<NT>& f, ps_u32x4 (&w)[NT]) {
+  if constexpr (NT == 3) {
+    f32x4 x0 = f.x0, x1 = f.x1;
+    asm volatile("" : "+v"(x0), "+v"(x1));
+    ps_split<3>(x0, x1, w);
+  } else {
+    w[0] = f.b;
   }
 }
 
@@ -189,41 +227,32 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
   const int rg = b / NUS, us = b - rg * NUS, r0 = rg * MR, u0 = us * UPT;  // S1
   const int rt2 = b / NC2, ct2 = b - rt2 * NC2;                            // S2
   const int rs = b / NR, gq = b - rs * NR, m3 = rs * MS;                   // S3
-  ps_u32x4 w1[KSW][NT][2], w2[KSW][NT], w3[KSW3][3][2];
+  PsFrag<NT> w1[KSW][2], w2[KSW];
+  PsFrag<3> w3[KSW3][2];
 #pragma unroll
   for (int s = 0; s < KSW; ++s) {
-    const int ks = KSW * wave + s;
+    const int ks = KSW * wave + s, k = 32 * ks + 8 * q;
+    const bool kok = ks < KSH && k < HD;
 #pragma unroll
-    for (int p = 0; p < NT; ++p) {
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
-        const int c = ct * 16 + r;
-        const bool ok = do1 && ks < KSH && c < WLD;
-        const int n = ok ? (c / UPT) * HD + u0 + (c % UPT) : 0;
-        const unsigned e = ok ? (unsigned)(((ks * 3 + p) * NPH + n) * 32 + 8 * q) : 0u;
-        w1[s][p][ct] = *(const DR_GLOBAL ps_u32x4*)((const DR_GLOBAL char*)g.whh + (e << 1));
-        if (!ok) w1[s][p][ct] = (ps_u32x4){0u, 0u, 0u, 0u};
-      }
-      const int c2 = ct2 * 16 + r;
-      const bool ok2 = do2 && ks < KSH && c2 < EH;
-      const unsigned e2 = ok2 ? (unsigned)(((ks * 3 + p) * NPE + c2) * 32 + 8 * q) : 0u;
-      w2[s][p] = *(const DR_GLOBAL ps_u32x4*)((const DR_GLOBAL char*)g.wm0 + (e2 << 1));
-      if (!ok2) w2[s][p] = (ps_u32x4){0u, 0u, 0u, 0u};
+    for (int ct = 0; ct < 2; ++ct) {
+      const int c = ct * 16 + r;
+      const bool ok = do1 && kok && c < WLD;
+      const int n = ok ? (c / UPT) * HD + u0 + (c % UPT) : 0;
+      w1[s][ct] = ps_frag<NT>(g.whh, (unsigned)(n * HD + k), ok);
     }
+    const int c2 = ct2 * 16 + r;
+    const bool ok2 = do2 && kok && c2 < EH;
+    w2[s] = ps_frag<NT>(g.wm0, ok2 ? (unsigned)(c2 * g.ldm0 + k) : 0u, ok2);
   }
 #pragma unroll
   for (int s = 0; s < KSW3; ++s) {
-    const int ks = KSW3 * wave + s;
+    const int ks = KSW3 * wave + s, k = 32 * ks + 8 * q;
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
-        const bool ok = do3 && ks < KSE;
-        const int n = gq * NCL + ct * 16 + r;
-        const unsigned e = ok ? (unsigned)(((ks * 3 + p) * NPL + n) * 32 + 8 * q) : 0u;
-        w3[s][p][ct] = *(const DR_GLOBAL ps_u32x4*)((const DR_GLOBAL char*)g.wm3 + (e << 1));
-        if (!ok) w3[s][p][ct] = (ps_u32x4){0u, 0u, 0u, 0u};
-      }
+    for (int ct = 0; ct < 2; ++ct) {
+      const bool ok = do3 && ks < KSE && k < EH;
+      const int n = gq * NCL + ct * 16 + r;
+      w3[s][ct] = ps_frag<3>(g.wm3, (unsigned)(n * EH + k), ok);
+    }
   }
   // S3's LayerNorm parameters (one float4 per lane: K = 200 <= 256) and logit biases
   const bool okk = lane < EH / 4;
@@ -352,8 +381,7 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
 #pragma unroll
               for (int ct = 0; ct < 2; ++ct) {
                 ps_u32x4 w[NT];
-#pragma unroll
-                for (int p = 0; p < NT; ++p) w[p] = w1[s][p][ct];
+                ps_wsplit<NT>(w1[s][ct], w);
                 acc[rt][ct] = ps_prod<NT>(w, a, acc[rt][ct]);
               }
             }
@@ -425,8 +453,7 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
         if (KSW * wave + s < KSH) {
           ps_u32x4 a[NT], w[NT];
           ps_split<NT>(ha[s][0], ha[s][1], a);
-#pragma unroll
-          for (int p = 0; p < NT; ++p) w[p] = w2[s][p];
+          ps_wsplit<NT>(w2[s], w);
           acc = ps_prod<NT>(w, a, acc);
         }
       }
@@ -510,7 +537,8 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
             ps_split<3>(x0, x1, a);
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct) {
-              ps_u32x4 w[3] = {w3[s][0][ct], w3[s][1][ct], w3[s][2][ct]};
+              ps_u32x4 w[3];
+              ps_wsplit<3>(w3[s][ct], w);
               acc[rt][ct] = ps_prod<3>(w, a, acc[rt][ct]);
             }
           }
@@ -609,8 +637,7 @@ static int launch_pscan(const PScanArgs& a, int grid, hipStream_t s) {
 }
 
 int op_pscan(const dr_dims* d, const dr_world_model* wm, int B, int T, int A, const float* feat, const float* actions,
-             long long act_sb, long long act_st, const float* wt, const void* whh_planes, const void* m0_planes,
-             const void* m3_planes, dr_noise noise, int step0, float* z_out, float* h_out, float* logits_out,
+             long long act_sb, long long act_st, const float* wt, const float* m0h, long long ldm0, dr_noise noise, int step0, float* z_out, float* h_out, float* logits_out,
              void* ring, hipStream_t s) {
   if (!op_pscan_supported(d, B, T, A)) {
     dr_set_error("pscan: unsupported shape (B=%d T=%d)", B, T);
@@ -641,9 +668,10 @@ int op_pscan(const dr_dims* d, const dr_world_model* wm, int B, int T, int A, co
   memset(&a, 0, sizeof(a));
   a.B = B; a.T = T; a.A = A; a.step0 = step0;
   a.wt = wt; a.b_ih = wm->b_ih; a.b_hh = wm->b_hh;
-  a.whh = (const unsigned short*)whh_planes;
-  a.wm0 = (const unsigned short*)m0_planes;
-  a.wm3 = (const unsigned short*)m3_planes;
+  a.whh = wm->w_hh;
+  a.wm0 = m0h;
+  a.ldm0 = ldm0;
+  a.wm3 = wm->map3.w;
   a.ln_g = wm->map1.w; a.ln_b = wm->map1.b; a.b3 = wm->map3.b;
   a.feat = feat; a.act = actions; a.act_sb = act_sb; a.act_st = act_st;
   a.noise = noise;
