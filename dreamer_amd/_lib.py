@@ -31,7 +31,8 @@ class dr_dims(C.Structure):
     _fields_ = [(n, C.c_int) for n in (
         "hidden", "rows", "cols", "action", "img_h", "img_w", "enc_f1", "enc_f2", "enc_hidden",
         "prior_h1", "prior_h2", "rew_h1", "rew_h2", "cont_h1", "cont_h2",
-        "actor_h1", "actor_h2", "critic_h1", "critic_h2", "buckets", "dec_f1", "dec_f2", "dec_hidden", "precision", "obs_dim", "enc_depth")]
+        "actor_h1", "actor_h2", "critic_h1", "critic_h2", "buckets", "dec_f1", "dec_f2", "dec_hidden", "precision", "obs_dim", "enc_depth",
+        "launch_form")]
 
 DR_MAX_DEPTH = 5  # include/dreamer_hip.h: conv / convt slots (dr_dims.enc_depth <= 5)
 

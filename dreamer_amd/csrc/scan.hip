@@ -618,7 +618,7 @@ size_t op_pscan_ring_bytes(int B) {
 }
 
 bool op_pscan_supported(const dr_dims* d, int B, int T, int A) {
-  return d->hidden == HD && d->enc_hidden == EH && d->rows == NR && d->cols == NCL && A >= 1 && A <= 8 && T >= 2 &&
+  return !d->launch_form && d->hidden == HD && d->enc_hidden == EH && d->rows == NR && d->cols == NCL && A >= 1 && A <= 8 && T >= 2 &&
          B >= 16 && B <= 256 && B % 16 == 0 && (B <= 64 || B % 64 == 0);
 }
 

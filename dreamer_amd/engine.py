@@ -19,8 +19,6 @@ slice of the batch; the exchange is one all-gather of the lambda returns
 Each phase is captured once into a HIP graph and replayed; collectives run
 between the phase graphs.
 """
-import weakref
-
 import numpy as np
 
 import torch
@@ -30,6 +28,7 @@ from . import hip
 
 WARM_STREAM = 1 << 24
 DREAM_STREAM = 2 << 24
+_CU_STREAMS = {}  # (device index, CU mask words) -> HIP stream handle (warm_stream)
 
 
 def cu_mask_words(n_cus, fraction):
@@ -68,8 +67,6 @@ class ImaginationEngine:
         # inside the epoch graph (~6 % slower replays, r01_ab_overlap.txt).
         self.side = torch.cuda.Stream(self.dev)
         self.chunks = [(0, self.T)]
-        self._masked_streams = []
-        weakref.finalize(self, ImaginationEngine._release_streams, self._masked_streams)
         self._alloc()
 
     # ------------------------------------------------------------------ setup
@@ -443,23 +440,17 @@ class ImaginationEngine:
         with torch.cuda.device(self.dev):
             L.call("dr_device_cus", ctypes.byref(n))
             words = cu_mask_words(n.value, cu_fraction)
-            mask = (ctypes.c_uint * len(words))(*words)
-            h = ctypes.c_void_p()
-            L.call("dr_stream_create_cumask", len(words), mask, ctypes.byref(h))
-        self._masked_streams.append(h.value)
+            # one masked stream per (device, mask) for the process, shared by
+            # every engine: torch's allocator may still hold blocks used on it
+            # after an engine is gone, so it is never destroyed mid-run
+            ck = (torch.device(self.dev).index, tuple(words))
+            h = _CU_STREAMS.get(ck)
+            if h is None:
+                mask = (ctypes.c_uint * len(words))(*words)
+                h = ctypes.c_void_p()
+                L.call("dr_stream_create_cumask", len(words), mask, ctypes.byref(h))
+                _CU_STREAMS[ck] = h
         return torch.cuda.ExternalStream(h.value, device=self.dev)
-
-    @staticmethod
-    def _release_streams(handles):
-        """Destroy the CU-masked HIP streams of warm_stream (engine teardown):
-        synchronise each, then dr_stream_destroy."""
-        while handles:
-            h = handles.pop()
-            try:
-                torch.cuda.ExternalStream(h).synchronize()
-                L.call("dr_stream_destroy", h)
-            except Exception:  # interpreter shutdown: the runtime may be gone
-                pass
 
     def _pipe_capture(self, key):
         dev, B, H = self.dev, self.B, self.H
@@ -474,13 +465,18 @@ class ImaginationEngine:
         if P["key"] == key:
             return P
         d, A = self.d, self.d.action
+        # the warm graphs are captured here and replayed on the CU-masked warm
+        # stream: launch form (a persistent scan needs every workgroup
+        # resident, which the capture stream cannot vouch for)
+        dw = L.dr_dims.from_buffer_copy(d)
+        dw.launch_form = 1
 
         def warm(s):
             st = torch.cuda.current_stream(dev).cuda_stream
             self.dr.buffer.gather_actions(self.starts, self.act_win)
             self._encode_chunk(0, self.T, st)
             nz = L.dr_noise(None, None, P["rng"].data_ptr(), self.rank * B, WARM_STREAM)
-            L.call("dr_observe_scan", d, self.dr.world_model.packed(), B, self.T, L.ptr(self.feat),
+            L.call("dr_observe_scan", dw, self.dr.world_model.packed(), B, self.T, L.ptr(self.feat),
                    L.ptr(self.act_win), self.S * A, A, None, None, nz, L.ptr(P["z0"][s]), L.ptr(P["h0"][s]), None,
                    L.ptr(self.ws_obs), self.ws_obs.numel(), st)
             L.call("dr_rng_advance", P["rng"].data_ptr(), 1, st)

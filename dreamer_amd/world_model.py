@@ -3,6 +3,8 @@
 (loss, backward, clip_grad_norm_, AdamW: WorldModel.py:148-202) run on
 libdreamer_hip; unroll_model keeps a PyTorch-ROCm autograd version for
 callers that want the reference's intermediate tensors."""
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -64,6 +66,8 @@ class WorldModel(nn.Module):
         d.buckets = self.buckets
         self.decoder.fill_dims(d)
         d.precision = 1 if getattr(self, "precision", "fp32") == "bf16" else 0  # DR_PREC_BF16 / DR_PREC_FP32
+        # DREAMER_PERSISTENT=0: every entry point as its launch sequence (A/B of the persistent kernels)
+        d.launch_form = 1 if os.environ.get("DREAMER_PERSISTENT", "1") == "0" else 0
         if agent is not None:
             a, c = agent.actor.base_net, agent.critic.value_net
             d.actor_h1, d.actor_h2 = a[0].out_features, a[3].out_features

@@ -76,6 +76,10 @@ typedef struct {
                           stride-2 layer each way, so 128x128 frames reach the same 4x4 grid 64x64 frames reach
                           in the reference): encoder channels 3, f1, f2, 2 f2, 4 f2, 4 f2 (conv[0..4]); decoder
                           4 d2 (H/32 x W/32) -> 4 d2 -> 2 d2 -> d2 -> d1 -> 3 (convt[0..4]). */
+  int launch_form;     /* 0 (default): an entry point may run as ONE persistent launch where the shape and the
+                          stream's CUs allow it (the warm start's posterior scan, scan.hip); 1: always the
+                          launch sequence.  Set for work captured on one stream and replayed on a CU-masked
+                          one (the pipelined epochs' warm start), and by DREAMER_PERSISTENT=0. */
 } dr_dims;
 #define DR_MAX_DEPTH 5
 #define DR_PREC_FP32 0

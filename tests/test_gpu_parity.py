@@ -214,9 +214,13 @@ def test_pipelined_epochs_match_sequential(which, sched, gpu, monkeypatch):
     (dr_stream_create_cumask; 1.0 = an unfenced plain stream), the chain on a
     stream of priority p, w = DREAMER_WARM0_MAIN (1: a call's first warm start
     on the chain's stream; 0: every warm start on the warm stream).  The
-    default (None) is "0.875:-1:1"."""
+    default (None) is "0.875:-1:1".  The pipelined warm starts run the launch
+    form (dr_dims.launch_form: their graphs replay on a CU-masked stream), so
+    the sequential epochs here do too (DREAMER_PERSISTENT=0); the persistent
+    scan is pinned against the oracle by test_gpu_baseline.py."""
     from dreamer_amd.engine import ImaginationEngine
     from formula import replay_data
+    monkeypatch.setenv("DREAMER_PERSISTENT", "0")
     if sched:
         frac, prio, w0 = sched.split(":")
         monkeypatch.setenv("DREAMER_WARM_CUS", frac)
