@@ -4,6 +4,11 @@
 #include "common.h"
 
 #define PSCAN_CNT_BYTES 6400  // counter block (49 counters 128 B apart), a multiple of 16
+#ifdef DR_PSCAN_TS
+#define PSCAN_TS_BYTES (64 * 24 * 256 * 8)  // stage timestamps (tools/pscan_probe.py)
+#else
+#define PSCAN_TS_BYTES 0
+#endif
 
 // B rows, T >= 2 steps, the reference's widths (hidden 600, latent_mapper 200, 32 x 32 latents)
 bool op_pscan_supported(const dr_dims* d, int B, int T, int A);

@@ -90,7 +90,18 @@ struct alignas(16) PScanArgs {
   float* pre;     // [2][B][EH]
   int* iz;        // [2][2][B][NR]: slot s: idx [B][NR] then zval [B][NR]
   unsigned* cnt;  // counters, status
+  unsigned long long* zg;  // [B][NR] z granules {zval bits | step + 1 | class} (S3 -> S1)
+  unsigned long long* hg;  // [B][HD] h granules {step | h bits} (S1 -> S2)
+  long long* ts;  // DR_PSCAN_TS builds: [64 steps][3 stages][8 marks][grid] wall-clock stamps
 };
+#ifdef DR_PSCAN_TS
+#define PS_TS(st, mk) \
+  do { \
+    if (threadIdx.x == 0 && t < 64) g.ts[((t * 3 + (st)) * 8 + (mk)) * gridDim.x + blockIdx.x] = (long long)wall_clock64(); \
+  } while (0)
+#else
+#define PS_TS(st, mk) do {} while (0)
+#endif
 
 __device__ __forceinline__ f32x4 ps_mfma(ps_u32x4 w, ps_u32x4 a, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(ps_bf16x8, w), __builtin_bit_cast(ps_bf16x8, a),
@@ -142,6 +153,12 @@ template <>
 struct PsFrag<1> {
   ps_u32x4 b;
 };
+// an offset the compiler cannot see through: keeps per-step weight loads in
+// the step loop (hoisted, they would stay live in registers across the scan)
+__device__ __forceinline__ unsigned ps_opaque(unsigned x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
 template <int NT>
 __device__ __forceinline__ PsFrag<NT> ps_frag(const float* W, unsigned e, bool ok) {
   const float4 a = dr_ld4(W, ok ? e : 0u), c = dr_ld4(W, ok ? e + 4u : 0u);
@@ -185,6 +202,15 @@ __device__ __forceinline__ void ps_st1(__amdgpu_buffer_rsrc_t r, unsigned byte_o
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)byte_off, 0, 16);
 }
 __device__ __forceinline__ void ps_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// 8-byte {data, tag} granules (MI355X_MICROARCH.md: the data IS the flag): ONE
+// aligned 8-byte sc1 store per granule, sc1 loads re-read until the tag matches
+typedef unsigned long long ps_u64;
+__device__ __forceinline__ void ps_gst(ps_u64* p, ps_u64 v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ ps_u64 ps_gld(const ps_u64* p) {
+  return __hip_atomic_load(const_cast<ps_u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // lane 0 of the workgroup: poll until *c >= target (relaxed sc1 loads + s_sleep)
 __device__ __forceinline__ bool ps_poll(const unsigned* c, unsigned target, int limit, unsigned* status) {
@@ -216,6 +242,7 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
   const bool do1 = b < n1, do2 = b < n2, do3 = b < n3;
   float* wih = smem;                                  // [LAT + A][WLD]
   float* scr = smem + (((LAT + A) * WLD + 3) & ~3);   // [SCR_F]
+  float* sbias = scr + SCR_F;                         // [64]: S1's b_ih, b_hh of the tile's gate columns
   unsigned* cnt = g.cnt;
   unsigned* status = cnt + CNT_LD * CNT_STATUS;
   const int lim = g.spin_limit;
@@ -227,8 +254,7 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
   const int rg = b / NUS, us = b - rg * NUS, r0 = rg * MR, u0 = us * UPT;  // S1
   const int rt2 = b / NC2, ct2 = b - rt2 * NC2;                            // S2
   const int rs = b / NR, gq = b - rs * NR, m3 = rs * MS;                   // S3
-  PsFrag<NT> w1[KSW][2], w2[KSW];
-  PsFrag<3> w3[KSW3][2];
+  PsFrag<NT> w1[KSW][2];  // S1's W_hh fragments stay in registers for the scan
 #pragma unroll
   for (int s = 0; s < KSW; ++s) {
     const int ks = KSW * wave + s, k = 32 * ks + 8 * q;
@@ -240,19 +266,6 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
       const int n = ok ? (c / UPT) * HD + u0 + (c % UPT) : 0;
       w1[s][ct] = ps_frag<NT>(g.whh, (unsigned)(n * HD + k), ok);
     }
-    const int c2 = ct2 * 16 + r;
-    const bool ok2 = do2 && kok && c2 < EH;
-    w2[s] = ps_frag<NT>(g.wm0, ok2 ? (unsigned)(c2 * g.ldm0 + k) : 0u, ok2);
-  }
-#pragma unroll
-  for (int s = 0; s < KSW3; ++s) {
-    const int ks = KSW3 * wave + s, k = 32 * ks + 8 * q;
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-      const bool ok = do3 && ks < KSE && k < EH;
-      const int n = gq * NCL + ct * 16 + r;
-      w3[s][ct] = ps_frag<3>(g.wm3, (unsigned)(n * EH + k), ok);
-    }
   }
   // S3's LayerNorm parameters (one float4 per lane: K = 200 <= 256) and logit biases
   const bool okk = lane < EH / 4;
@@ -263,6 +276,11 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
     for (int x = tid; x < nrow * WLD; x += NTH) {
       const int k = x / WLD, c = x - k * WLD;
       wih[x] = dr_ld1(g.wt, (unsigned)(k * 3 * HD + (c / UPT) * HD + u0 + (c % UPT)));
+    }
+    if (tid < 64) {
+      const int c = tid & 31;
+      const unsigned col = (unsigned)((c / UPT) * HD + u0 + (c % UPT));
+      sbias[tid] = c < WLD ? dr_ld1(tid < 32 ? g.b_ih : g.b_hh, col) : 0.f;
     }
   }
   __syncthreads();
@@ -282,18 +300,16 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
     const int step = g.step0 + t;
     // ======================= S1: GRU (t >= 1) ===============================
     if (t >= 1 && do1) {
-      if (tid == 0) {
-        bool ok = true;
-        for (int i = 0; i < MR / MS && ok; ++i)
-          ok = ps_poll(cnt + CNT_LD * (CNT_Z + r0 / MS + i), (unsigned)(NR * t), lim, status);
-        if (ok && t >= 2) ok = ps_poll(cnt + CNT_LD * (CNT_H + rg), (unsigned)(NUS * (t - 1)), lim, status);
-        s_ok = ok;
-      }
+      PS_TS(0, 0);
+      // h_{t-1} is complete long before z_{t-1} (S1 of the previous step):
+      // wait for it first and issue its loads, then wait for the sampler
+      if (tid == 0) s_ok = t < 2 || ps_poll(cnt + CNT_LD * (CNT_H + rg), (unsigned)(NUS * (t - 1)), lim, status);
       __syncthreads();
       if (!s_ok) return;
       const unsigned hprev = (unsigned)(((t - 1) & 1) * B * HD);
-      // h_{t-1} fragments of this wave's k-steps, two steps ahead (h_0 = 0: t = 1 skips the product)
-      f32x4 ha[2][MR / 16][2];
+      // h_{t-1} fragments of this wave's k-steps, HR steps ahead (h_0 = 0: t = 1 skips the product)
+      constexpr int HR = 2;
+      f32x4 ha[HR][MR / 16][2];
       auto load_h = [&](int s, int slot) {
         const int ks = KSW * wave + s;
         const int k = 32 * ks + 8 * q;
@@ -307,10 +323,11 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
         }
       };
       if (t >= 2) {
-        load_h(0, 0);
-        load_h(1, 1);
+#pragma unroll
+        for (int s = 0; s < HR; ++s) load_h(s, s);
       }
-      // this thread's (row, unit) pairs: h_{t-1} values for the gates
+      PS_TS(0, 1);
+      // h_{t-1} for this thread's gate pairs
       float hv[NP1];
 #pragma unroll
       for (int i = 0; i < NP1; ++i) {
@@ -320,51 +337,76 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
         hv[i] = ps_ld1(rh, ok ? 4u * (hprev + (unsigned)((r0 + row) * HD + u0 + j)) : 0u);
         if (!ok) hv[i] = 0.f;
       }
-      // stage z_{t-1}'s indices / straight-through values of the MR rows
+      // z_{t-1} of the MR rows: sweep the sampler's granules until every tag is
+      // step t (no counter poll: the data carries its own flag); a_{t-1}
+      int2* siz = reinterpret_cast<int2*>(scr);  // [MR][NR] (class, straight-through value bits)
+      float* sact = scr + 2 * MR * NR;           // [MR][8]
+      float* sgi = sact + 8 * MR;                // [MR][32]: gi (+ b_ih) of the tile's 30 gate columns
       {
-        int* sidx = reinterpret_cast<int*>(scr);
-        float* szv = scr + MR * NR;
-        const unsigned zb = (unsigned)(((t - 1) & 1) * 2 * B * NR);
-        for (int x = tid; x < MR * NR / 4; x += NTH) {
-          const unsigned o = zb + (unsigned)(r0 * NR + 4 * x);
-          const f32x4 iv = ps_ld4(rz, 4u * o), zv = ps_ld4(rz, 4u * (o + (unsigned)(B * NR)));
-          *reinterpret_cast<f32x4*>(&sidx[4 * x]) = iv;
-          *reinterpret_cast<f32x4*>(&szv[4 * x]) = zv;
-        }
-      }
-      __syncthreads();
-      // gi by gather from the LDS slice: groups ascending (fmaf), actions, + b_ih (k_gru_gates' order)
-      float gi[NP1][3];
-      {
-        const int* sidx = reinterpret_cast<const int*>(scr);
-        const float* szv = scr + MR * NR;
+        constexpr int NZ = MR * NR / NTH;
+        const ps_u64* zsrc = g.zg + (size_t)r0 * NR;
+        unsigned pend = 0;
 #pragma unroll
-        for (int i = 0; i < NP1; ++i) {
-          const int p = tid + NTH * i;
-          const bool live = p < MR * UPT;
-          const int row = live ? p / UPT : 0, j = live ? p - row * UPT : 0;
-          float v0 = 0.f, v1 = 0.f, v2 = 0.f;
-#pragma unroll 8
-          for (int u = 0; u < NR; ++u) {
-            const int k = u * NCL + sidx[row * NR + u];
-            const float zv = szv[row * NR + u];
-            const float* wr = wih + k * WLD + j;
-            v0 = fmaf(wr[0], zv, v0);
-            v1 = fmaf(wr[UPT], zv, v1);
-            v2 = fmaf(wr[2 * UPT], zv, v2);
-          }
-          for (int ia = 0; ia < A; ++ia) {
-            const float av = dr_ld1(g.act, (unsigned)((r0 + row) * g.act_sb + (t - 1) * g.act_st + ia));
-            const float* wr = wih + (LAT + ia) * WLD + j;
-            v0 = fmaf(wr[0], av, v0);
-            v1 = fmaf(wr[UPT], av, v1);
-            v2 = fmaf(wr[2 * UPT], av, v2);
-          }
-          gi[i][0] = v0 + dr_ld1(g.b_ih, (unsigned)(u0 + j));
-          gi[i][1] = v1 + dr_ld1(g.b_ih, (unsigned)(HD + u0 + j));
-          gi[i][2] = v2 + dr_ld1(g.b_ih, (unsigned)(2 * HD + u0 + j));
+        for (int i = 0; i < NZ; ++i) {
+          const ps_u64 v = ps_gld(zsrc + tid + NTH * i);
+          siz[tid + NTH * i] = make_int2((int)(v & 0xFFFFu), (int)(v >> 32));
+          if ((unsigned)((v >> 16) & 0xFFFFu) != (unsigned)t) pend |= 1u << i;
         }
+        for (int x = tid; x < MR * A; x += NTH) {
+          const int row = x / A, ia = x - row * A;
+          sact[row * 8 + ia] = dr_ld1(g.act, (unsigned)((r0 + row) * g.act_sb + (t - 1) * g.act_st + ia));
+        }
+        int spins = 0;
+        while (pend && ++spins <= lim) {
+          __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+          for (int i = 0; i < NZ; ++i)
+            if (pend & (1u << i)) {
+              const ps_u64 v = ps_gld(zsrc + tid + NTH * i);
+              siz[tid + NTH * i] = make_int2((int)(v & 0xFFFFu), (int)(v >> 32));
+              if ((unsigned)((v >> 16) & 0xFFFFu) == (unsigned)t) pend &= ~(1u << i);
+            }
+        }
+        if (pend) __hip_atomic_store(status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!__syncthreads_and(pend == 0)) return;
       }
+      __syncthreads();  // a_{t-1}
+      PS_TS(0, 2);
+      // gi by gather from the LDS slice, thread = (row, 8 gate columns): the
+      // sampled W_ih^T row of every group read as four 8-byte pieces;
+      // groups ascending (fmaf), actions, + b_ih (k_gru_gates' summation order)
+      if (tid < 4 * MR) {
+        const int row = tid >> 2, c0 = 8 * (tid & 3);
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = 0.f;
+        const int2* iz = siz + row * NR;
+#pragma unroll 8
+        for (int u = 0; u < NR; ++u) {
+          const int2 p = iz[u];
+          const float zv = __int_as_float(p.y);
+          const float2* wr = reinterpret_cast<const float2*>(wih + (u * NCL + p.x) * WLD + c0);
+          const float2 w0 = wr[0], w1v = wr[1], w2v = wr[2], w3v = wr[3];
+          v[0] = fmaf(w0.x, zv, v[0]);
+          v[1] = fmaf(w0.y, zv, v[1]);
+          v[2] = fmaf(w1v.x, zv, v[2]);
+          v[3] = fmaf(w1v.y, zv, v[3]);
+          v[4] = fmaf(w2v.x, zv, v[4]);
+          v[5] = fmaf(w2v.y, zv, v[5]);
+          v[6] = fmaf(w3v.x, zv, v[6]);
+          v[7] = fmaf(w3v.y, zv, v[7]);
+        }
+        for (int ia = 0; ia < A; ++ia) {
+          const float av = sact[row * 8 + ia];
+          const float* wr = wih + (LAT + ia) * WLD + c0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaf(wr[e], av, v[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (c0 + e < WLD) sgi[row * 32 + c0 + e] = v[e] + sbias[c0 + e];
+      }
+      PS_TS(0, 3);
       // gh partial over this wave's k-steps
       f32x4 acc[MR / 16][2];
 #pragma unroll
@@ -372,77 +414,149 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
       if (t >= 2) {
 #pragma unroll
         for (int s = 0; s < KSW; ++s) {
-          const int slot = s & 1;
+          const int slot = s % HR;
           if (KSW * wave + s < KSH) {
+            ps_u32x4 w[2][NT];
+            ps_wsplit<NT>(w1[s][0], w[0]);
+            ps_wsplit<NT>(w1[s][1], w[1]);
 #pragma unroll
             for (int rt = 0; rt < MR / 16; ++rt) {
               ps_u32x4 a[NT];
               ps_split<NT>(ha[slot][rt][0], ha[slot][rt][1], a);
 #pragma unroll
-              for (int ct = 0; ct < 2; ++ct) {
-                ps_u32x4 w[NT];
-                ps_wsplit<NT>(w1[s][ct], w);
-                acc[rt][ct] = ps_prod<NT>(w, a, acc[rt][ct]);
-              }
+              for (int ct = 0; ct < 2; ++ct) acc[rt][ct] = ps_prod<NT>(w[ct], a, acc[rt][ct]);
             }
           }
-          if (s + 2 < KSW) load_h(s + 2, slot);
+          if (s + HR < KSW) load_h(s + HR, slot);
         }
       }
-      __syncthreads();  // every wave done with the staged indices: the scratch takes the partials
-      // partials: red[wave][(rt * 2 + ct) * 4 + e][lane]
-#pragma unroll
-      for (int rt = 0; rt < MR / 16; ++rt)
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) scr[((wave * (MR / 16) * 2 + rt * 2 + ct) * 4 + e) * 64 + lane] = acc[rt][ct][e];
+      PS_TS(0, 4);
+      // K-split partials meet in LDS in two rounds (waves 2, 3 -> 0, 1 -> 0):
+      // (w0 + w2) + (w1 + w3); the staged indices are dead (the gather is done)
+      constexpr int PF = (MR / 16) * 2 * 256;  // floats of one wave's partial tile set
       __syncthreads();
+      if (wave >= 2) {
+#pragma unroll
+        for (int rt = 0; rt < MR / 16; ++rt)
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) scr[(wave - 2) * PF + ((rt * 2 + ct) * 4 + e) * 64 + lane] = acc[rt][ct][e];
+      }
+      __syncthreads();
+      if (wave < 2) {
+#pragma unroll
+        for (int rt = 0; rt < MR / 16; ++rt)
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[rt][ct][e] += scr[wave * PF + ((rt * 2 + ct) * 4 + e) * 64 + lane];
+      }
+      __syncthreads();
+      if (wave == 1) {
+#pragma unroll
+        for (int rt = 0; rt < MR / 16; ++rt)
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) scr[((rt * 2 + ct) * 4 + e) * 64 + lane] = acc[rt][ct][e];
+      }
+      __syncthreads();
+      float* sgh = scr + PF;  // [MR][32]: gh (+ b_hh)
+      if (wave == 0) {
+#pragma unroll
+        for (int rt = 0; rt < MR / 16; ++rt)
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int c = ct * 16 + 4 * q + e;
+              const float v = acc[rt][ct][e] + scr[((rt * 2 + ct) * 4 + e) * 64 + lane];
+              if (c < WLD) sgh[(rt * 16 + r) * 32 + c] = v + sbias[32 + c];
+            }
+      }
+      __syncthreads();
+      PS_TS(0, 5);
       // gates (torch gru_cell op order) for this thread's pairs
       const unsigned hcur = (unsigned)((t & 1) * B * HD);
 #pragma unroll
       for (int i = 0; i < NP1; ++i) {
         const int p = tid + NTH * i;
         if (p < MR * UPT) {
-          const int row = p / UPT, j = p - row * UPT, rt = row >> 4, rr16 = row & 15;
-          float gh[3];
-#pragma unroll
-          for (int gt = 0; gt < 3; ++gt) {
-            const int c = gt * UPT + j, ct = c >> 4, ql = (c & 15) >> 2, e = c & 3;
-            const int l = rr16 + 16 * ql;
-            float v = 0.f;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) v += scr[((w * (MR / 16) * 2 + rt * 2 + ct) * 4 + e) * 64 + l];
-            gh[gt] = v + dr_ld1(g.b_hh, (unsigned)(gt * HD + u0 + j));
-          }
-          const float rr = 1.0f / (1.0f + expf(-(gh[0] + gi[i][0])));
-          const float uu = 1.0f / (1.0f + expf(-(gh[1] + gi[i][1])));
-          const float nn = tanhf(gi[i][2] + gh[2] * rr);
+          const int row = p / UPT, j = p - row * UPT;
+          const float* gh = sgh + row * 32 + j;
+          const float* gi = sgi + row * 32 + j;
+          const float rr = 1.0f / (1.0f + expf(-(gh[0] + gi[0])));
+          const float uu = 1.0f / (1.0f + expf(-(gh[UPT] + gi[UPT])));
+          const float nn = tanhf(gi[2 * UPT] + gh[2 * UPT] * rr);
           const float ho = (hv[i] - nn) * uu + nn;
           const unsigned o = (unsigned)((r0 + row) * HD + u0 + j);
           ps_st1(rh, 4u * (hcur + o), ho);
+          ps_gst(g.hg + o, ((ps_u64)(unsigned)t << 32) | __float_as_uint(ho));
           if (t == T - 1) g.h_out[o] = ho;
         }
       }
+      PS_TS(0, 6);
       ps_signal(cnt + CNT_LD * (CNT_H + rg));
+      PS_TS(0, 7);
     }
     // ======================= S2: latent_mapper.0 h-part (t >= 1) ===========
     if (t >= 1 && do2) {
       const int m0 = rt2 * 16, n0 = ct2 * 16;
-      if (tid == 0) s_ok = ps_poll(cnt + CNT_LD * (CNT_H + m0 / MR), (unsigned)(NUS * t), lim, status);
-      __syncthreads();
-      if (!s_ok) return;
-      const unsigned hcur = (unsigned)((t & 1) * B * HD);
-      f32x4 ha[KSW][2];
+      PS_TS(1, 0);
+      // latent_mapper.0's h-columns of the tile (40 KB, L2-resident across the
+      // steps), issued with the granule sweep
+      PsFrag<NT> w2[KSW];
 #pragma unroll
       for (int s = 0; s < KSW; ++s) {
-        const int ks = KSW * wave + s, k = 32 * ks + 8 * q;
-        const bool ok = ks < KSH && k < HD;
-        const unsigned o = 4u * (hcur + (unsigned)((m0 + r) * HD) + (ok ? (unsigned)k : 0u));
-        ha[s][0] = ps_ld4(rh, o);
-        ha[s][1] = ps_ld4(rh, o + 16u);
-        if (!ok) ha[s][0] = ha[s][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        const int ks = KSW * wave + s, k = 32 * ks + 8 * q, c2 = ct2 * 16 + r;
+        const bool ok2 = ks < KSH && k < HD && c2 < EH;
+        w2[s] = ps_frag<NT>(g.wm0, ps_opaque(ok2 ? (unsigned)(c2 * g.ldm0 + k) : 0u), ok2);
       }
+      // h_t of the tile's 16 rows: this lane's 8-k runs as granules, re-read
+      // until every tag is step t (a bit mask of the pending ones)
+      unsigned hval[KSW][8];
+      ps_u64 pend = 0;
+      const ps_u64* hrow = g.hg + (size_t)(m0 + r) * HD;
+#pragma unroll
+      for (int s = 0; s < KSW; ++s) {
+        const int k = 32 * (KSW * wave + s) + 8 * q;
+        const bool ok = KSW * wave + s < KSH && k < HD;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const ps_u64 v = ok ? ps_gld(hrow + k + e) : ((ps_u64)(unsigned)t << 32);
+          hval[s][e] = (unsigned)v;
+          if ((unsigned)(v >> 32) != (unsigned)t) pend |= 1ull << (8 * s + e);
+        }
+      }
+      {
+        int spins = 0;
+        while (pend && ++spins <= lim) {
+          __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+          for (int s = 0; s < KSW; ++s) {
+            const int k = 32 * (KSW * wave + s) + 8 * q;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (pend & (1ull << (8 * s + e))) {
+                const ps_u64 v = ps_gld(hrow + k + e);
+                hval[s][e] = (unsigned)v;
+                if ((unsigned)(v >> 32) == (unsigned)t) pend &= ~(1ull << (8 * s + e));
+              }
+          }
+        }
+        if (pend) __hip_atomic_store(status, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!__syncthreads_and(pend == 0)) return;
+      }
+      PS_TS(1, 1);
+      f32x4 ha[KSW][2];
+#pragma unroll
+      for (int s = 0; s < KSW; ++s)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ha[s][0][e] = __uint_as_float(hval[s][e]);
+          ha[s][1][e] = __uint_as_float(hval[s][4 + e]);
+        }
       // the feature part of this thread's output (plain: written before the launch)
       const int e2 = tid >> 6, l2 = tid & 63, row2 = l2 & 15, col2 = 4 * (l2 >> 4) + e2;
       const bool ok2 = n0 + col2 < EH;
@@ -457,6 +571,7 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
           acc = ps_prod<NT>(w, a, acc);
         }
       }
+      PS_TS(1, 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) scr[(wave * 4 + e) * 64 + lane] = acc[e];
       __syncthreads();
@@ -466,6 +581,7 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
         ps_st1(rp, 4u * (unsigned)((t & 1) * B * EH + (m0 + row2) * EH + n0 + col2), v + fv);
       }
       ps_signal(cnt + CNT_LD * (CNT_PRE + rt2));
+      PS_TS(1, 7);
     }
     // ======================= S3: LN-SiLU -> logits -> sampler ===============
     if (do3) {
@@ -483,6 +599,7 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
           for (int i = 0; i < 4; ++i) qn[i] = dr_exp1_k(rng_seed, rng_off, st, row, e0 + i);
         }
       }
+      PS_TS(2, 0);
       if (t >= 1) {
         if (tid == 0) {
           bool ok = true;
@@ -493,19 +610,36 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
         __syncthreads();
         if (!s_ok) return;
       }
+      PS_TS(2, 1);
       // LN-SiLU of the block's rows into LDS (a wave per row, DPP statistics;
       // k_ln_gemm_sample's arithmetic), zero-padded to 224
+      // latent_mapper.3's rows of the group (28 KB, L2-resident across the steps)
+      PsFrag<3> w3[KSW3][2];
+#pragma unroll
+      for (int s = 0; s < KSW3; ++s) {
+        const int ks = KSW3 * wave + s, k = 32 * ks + 8 * q;
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const bool ok = ks < KSE && k < EH;
+          w3[s][ct] = ps_frag<3>(g.wm3, ps_opaque((unsigned)((gq * NCL + ct * 16 + r) * EH + k)), ok);
+        }
+      }
       float* sA = scr;
+      f32x4 xr[MS / 4];  // every row of this wave issued before the first reduction
 #pragma unroll
       for (int i = 0; i < MS / 4; ++i) {
-        const int ml = wave + 4 * i, m = m3 + ml;
-        f32x4 x = {0.f, 0.f, 0.f, 0.f};
+        const int m = m3 + wave + 4 * i;
         if (t == 0) {
           const float4 xf = dr_ld4(g.feat, okk ? (unsigned)(m * EH + 4 * lane) : 0u);
-          x = (f32x4){xf.x, xf.y, xf.z, xf.w};
+          xr[i] = (f32x4){xf.x, xf.y, xf.z, xf.w};
         } else {
-          x = ps_ld4(rp, 4u * ((unsigned)((t & 1) * B * EH + m * EH) + (okk ? 4u * lane : 0u)));
+          xr[i] = ps_ld4(rp, 4u * ((unsigned)((t & 1) * B * EH + m * EH) + (okk ? 4u * lane : 0u)));
         }
+      }
+#pragma unroll
+      for (int i = 0; i < MS / 4; ++i) {
+        const int ml = wave + 4 * i;
+        const f32x4 x = xr[i];
         const float mean = wave_sum(okk ? (x[0] + x[1]) + (x[2] + x[3]) : 0.f) / (float)EH;
         float sq = 0.f;
         if (okk) {
@@ -522,6 +656,7 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
         if (lane < KSE * 8) *reinterpret_cast<float4*>(&sA[ml * KP3 + 4 * lane]) = y;
       }
       __syncthreads();
+      PS_TS(2, 2);
       f32x4 acc[MS / 16][2];
 #pragma unroll
       for (int rt = 0; rt < MS / 16; ++rt) acc[rt][0] = acc[rt][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -544,6 +679,7 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
           }
         }
       }
+      PS_TS(2, 4);
       __syncthreads();  // sA consumed: the scratch takes the partials
 #pragma unroll
       for (int rt = 0; rt < MS / 16; ++rt)
@@ -552,6 +688,7 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) scr[((wave * (MS / 16) * 2 + rt * 2 + ct) * 4 + e) * 64 + lane] = acc[rt][ct][e];
       __syncthreads();
+      PS_TS(2, 5);
       if (act3) {
         // logits of classes c3 .. c3 + 3 of row ml3: tile (rt, ct), lane r + 16 q, element e
         float x[4];
@@ -588,11 +725,11 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
         }
         group_argmax(best, bi, 8);
         const int m = m3 + ml3;
-        const unsigned zb = (unsigned)((t & 1) * 2 * B * NR + m * NR + gq);
-        if (sub == 0) ps_st1(rz, 4u * zb, __int_as_float(bi));
         if ((unsigned)(bi - c3) < 4u) {
           const int i = bi - c3;
-          ps_st1(rz, 4u * (zb + (unsigned)(B * NR)), (1.0f + pu[i]) - pu[i]);
+          const float zsv = (1.0f + pu[i]) - pu[i];
+          ps_gst(g.zg + (size_t)m * NR + gq,
+                 ((ps_u64)__float_as_uint(zsv) << 32) | ((ps_u64)(unsigned)(t + 1) << 16) | (unsigned)bi);
         }
         if (t == T - 1) {
           float4 z;
@@ -605,16 +742,19 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
           if (g.logits_out) dr_st4(g.logits_out, o, make_float4(x[0], x[1], x[2], x[3]));
         }
       }
-      ps_signal(cnt + CNT_LD * (CNT_Z + rs));
+      PS_TS(2, 7);
     }
   }
 }
 
-static size_t pscan_lds_bytes(int A) { return sizeof(float) * ((((size_t)(LAT + A) * WLD + 3) & ~(size_t)3) + SCR_F); }
+static size_t pscan_lds_bytes(int A) {
+  return sizeof(float) * ((((size_t)(LAT + A) * WLD + 3) & ~(size_t)3) + SCR_F + 64);
+}
 
 size_t op_pscan_ring_bytes(int B) {
   // hb [2][B][HD], pre [2][B][EH], iz [2][2][B][NR], counters
-  return sizeof(float) * ((size_t)2 * B * HD + (size_t)2 * B * EH + (size_t)4 * B * NR) + PSCAN_CNT_BYTES;
+  return sizeof(float) * ((size_t)2 * B * HD + (size_t)2 * B * EH + (size_t)4 * B * NR) + PSCAN_CNT_BYTES +
+         sizeof(unsigned long long) * (size_t)B * (NR + HD) + PSCAN_TS_BYTES;
 }
 
 bool op_pscan_supported(const dr_dims* d, int B, int T, int A) {
@@ -682,8 +822,14 @@ int op_pscan(const dr_dims* d, const dr_world_model* wm, int B, int T, int A, co
   a.pre = a.hb + (size_t)2 * B * HD;
   a.iz = reinterpret_cast<int*>(a.pre + (size_t)2 * B * EH);
   a.cnt = reinterpret_cast<unsigned*>(a.iz + (size_t)4 * B * NR);
+  a.zg = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(a.cnt) + PSCAN_CNT_BYTES);
+  a.hg = a.zg + (size_t)B * NR;
+  a.ts = reinterpret_cast<long long*>(a.hg + (size_t)B * HD);
   // counters zeroed by a kernel (captured graphs replay it; a memset node was seen not to)
-  DR_TRY(op_fill(PSCAN_CNT_BYTES / 4, reinterpret_cast<float*>(a.cnt), 0.f, s));
+  // counters and granule tags zeroed by a kernel (captured graphs replay it; a
+  // memset node was seen not to): no granule of an earlier launch carries a
+  // tag this launch waits for
+  DR_TRY(op_fill(PSCAN_CNT_BYTES / 4 + (long long)2 * B * (NR + HD), reinterpret_cast<float*>(a.cnt), 0.f, s));
   const bool bf = d->precision == DR_PREC_BF16;
 #define PS_L(NT, MRv, MSv) \
   if (MR == MRv && MS == MSv) return launch_pscan<NT, MRv, MSv>(a, grid, s);
