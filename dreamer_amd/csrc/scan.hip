@@ -91,7 +91,6 @@ struct alignas(16) PScanArgs {
   int* iz;        // [2][2][B][NR]: slot s: idx [B][NR] then zval [B][NR]
   unsigned* cnt;  // counters, status
   unsigned long long* zg;  // [B][NR] z granules {zval bits | step + 1 | class} (S3 -> S1)
-  unsigned long long* hg;  // [B][HD] h granules {step | h bits} (S1 -> S2)
   long long* ts;  // DR_PSCAN_TS builds: [64 steps][3 stages][8 marks][grid] wall-clock stamps
 };
 #ifdef DR_PSCAN_TS
@@ -301,14 +300,41 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
     // ======================= S1: GRU (t >= 1) ===============================
     if (t >= 1 && do1) {
       PS_TS(0, 0);
-      // h_{t-1} is complete long before z_{t-1} (S1 of the previous step):
-      // wait for it first and issue its loads, then wait for the sampler
+      // Loads in the order they are consumed (vmcnt retires in issue order): z
+      // granules, a_{t-1} and h_{t-1} for the gate pairs, then -- once the h
+      // counter says h_{t-1} is complete (long before z_{t-1}: it is S1 of the
+      // previous step) -- all of this wave's h fragments for the product
+      int2* siz = reinterpret_cast<int2*>(scr);  // [MR][NR] (class, straight-through value bits)
+      float* sact = scr + 2 * MR * NR;           // [MR][8]
+      float* sgi = sact + 8 * MR;                // [MR][32]: gi (+ b_ih) of the tile's 30 gate columns
+      constexpr int NZ = MR * NR / NTH;
+      constexpr int NA1 = (MR * 8 + NTH - 1) / NTH;
+      const ps_u64* zsrc = g.zg + (size_t)r0 * NR;
+      ps_u64 zv[NZ];
+#pragma unroll
+      for (int i = 0; i < NZ; ++i) zv[i] = ps_gld(zsrc + tid + NTH * i);
+      float av[NA1];
+#pragma unroll
+      for (int i = 0; i < NA1; ++i) {
+        const int x = tid + NTH * i, row = x >> 3, ia = x & 7;
+        const bool ok = row < MR && ia < A;
+        av[i] = dr_ld1(g.act, ok ? (unsigned)((r0 + row) * g.act_sb + (t - 1) * g.act_st + ia) : 0u);
+      }
+      const unsigned hprev = (unsigned)(((t - 1) & 1) * B * HD);
+      float hv[NP1];
+#pragma unroll
+      for (int i = 0; i < NP1; ++i) {
+        const int p = tid + NTH * i;
+        const int row = p / UPT, j = p - row * UPT;
+        const bool ok = t >= 2 && p < MR * UPT;
+        hv[i] = ps_ld1(rh, ok ? 4u * (hprev + (unsigned)((r0 + row) * HD + u0 + j)) : 0u);
+        if (!ok) hv[i] = 0.f;
+      }
       if (tid == 0) s_ok = t < 2 || ps_poll(cnt + CNT_LD * (CNT_H + rg), (unsigned)(NUS * (t - 1)), lim, status);
       __syncthreads();
       if (!s_ok) return;
-      const unsigned hprev = (unsigned)(((t - 1) & 1) * B * HD);
       // h_{t-1} fragments of this wave's k-steps, HR steps ahead (h_0 = 0: t = 1 skips the product)
-      constexpr int HR = 2;
+      constexpr int HR = 5;
       f32x4 ha[HR][MR / 16][2];
       auto load_h = [&](int s, int slot) {
         const int ks = KSW * wave + s;
@@ -327,50 +353,33 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
         for (int s = 0; s < HR; ++s) load_h(s, s);
       }
       PS_TS(0, 1);
-      // h_{t-1} for this thread's gate pairs
-      float hv[NP1];
-#pragma unroll
-      for (int i = 0; i < NP1; ++i) {
-        const int p = tid + NTH * i;
-        const int row = p / UPT, j = p - row * UPT;
-        const bool ok = t >= 2 && p < MR * UPT;
-        hv[i] = ps_ld1(rh, ok ? 4u * (hprev + (unsigned)((r0 + row) * HD + u0 + j)) : 0u);
-        if (!ok) hv[i] = 0.f;
-      }
-      // z_{t-1} of the MR rows: sweep the sampler's granules until every tag is
-      // step t (no counter poll: the data carries its own flag); a_{t-1}
-      int2* siz = reinterpret_cast<int2*>(scr);  // [MR][NR] (class, straight-through value bits)
-      float* sact = scr + 2 * MR * NR;           // [MR][8]
-      float* sgi = sact + 8 * MR;                // [MR][32]: gi (+ b_ih) of the tile's 30 gate columns
+      // z_{t-1} of the MR rows: the sampler's granules, re-read until every
+      // tag is step t (no counter: the data carries its own flag)
       {
-        constexpr int NZ = MR * NR / NTH;
-        const ps_u64* zsrc = g.zg + (size_t)r0 * NR;
-        unsigned pend = 0;
+        unsigned zpend = 0;
 #pragma unroll
-        for (int i = 0; i < NZ; ++i) {
-          const ps_u64 v = ps_gld(zsrc + tid + NTH * i);
-          siz[tid + NTH * i] = make_int2((int)(v & 0xFFFFu), (int)(v >> 32));
-          if ((unsigned)((v >> 16) & 0xFFFFu) != (unsigned)t) pend |= 1u << i;
-        }
-        for (int x = tid; x < MR * A; x += NTH) {
-          const int row = x / A, ia = x - row * A;
-          sact[row * 8 + ia] = dr_ld1(g.act, (unsigned)((r0 + row) * g.act_sb + (t - 1) * g.act_st + ia));
-        }
+        for (int i = 0; i < NZ; ++i)
+          if ((unsigned)((zv[i] >> 16) & 0xFFFFu) != (unsigned)t) zpend |= 1u << i;
         int spins = 0;
-        while (pend && ++spins <= lim) {
+        while (zpend && ++spins <= lim) {
           __builtin_amdgcn_s_sleep(1);
 #pragma unroll
           for (int i = 0; i < NZ; ++i)
-            if (pend & (1u << i)) {
-              const ps_u64 v = ps_gld(zsrc + tid + NTH * i);
-              siz[tid + NTH * i] = make_int2((int)(v & 0xFFFFu), (int)(v >> 32));
-              if ((unsigned)((v >> 16) & 0xFFFFu) == (unsigned)t) pend &= ~(1u << i);
+            if (zpend & (1u << i)) {
+              zv[i] = ps_gld(zsrc + tid + NTH * i);
+              if ((unsigned)((zv[i] >> 16) & 0xFFFFu) == (unsigned)t) zpend &= ~(1u << i);
             }
         }
-        if (pend) __hip_atomic_store(status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (!__syncthreads_and(pend == 0)) return;
+        if (zpend) __hip_atomic_store(status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int i = 0; i < NZ; ++i) siz[tid + NTH * i] = make_int2((int)(zv[i] & 0xFFFFu), (int)(zv[i] >> 32));
+#pragma unroll
+        for (int i = 0; i < NA1; ++i) {
+          const int x = tid + NTH * i;
+          if (x < MR * 8) sact[x] = av[i];
+        }
+        if (!__syncthreads_and(zpend == 0)) return;
       }
-      __syncthreads();  // a_{t-1}
       PS_TS(0, 2);
       // gi by gather from the LDS slice, thread = (row, 8 gate columns): the
       // sampled W_ih^T row of every group read as four 8-byte pieces;
@@ -492,7 +501,6 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
           const float ho = (hv[i] - nn) * uu + nn;
           const unsigned o = (unsigned)((r0 + row) * HD + u0 + j);
           ps_st1(rh, 4u * (hcur + o), ho);
-          ps_gst(g.hg + o, ((ps_u64)(unsigned)t << 32) | __float_as_uint(ho));
           if (t == T - 1) g.h_out[o] = ho;
         }
       }
@@ -513,50 +521,21 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
         const bool ok2 = ks < KSH && k < HD && c2 < EH;
         w2[s] = ps_frag<NT>(g.wm0, ps_opaque(ok2 ? (unsigned)(c2 * g.ldm0 + k) : 0u), ok2);
       }
-      // h_t of the tile's 16 rows: this lane's 8-k runs as granules, re-read
-      // until every tag is step t (a bit mask of the pending ones)
-      unsigned hval[KSW][8];
-      ps_u64 pend = 0;
-      const ps_u64* hrow = g.hg + (size_t)(m0 + r) * HD;
-#pragma unroll
-      for (int s = 0; s < KSW; ++s) {
-        const int k = 32 * (KSW * wave + s) + 8 * q;
-        const bool ok = KSW * wave + s < KSH && k < HD;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const ps_u64 v = ok ? ps_gld(hrow + k + e) : ((ps_u64)(unsigned)t << 32);
-          hval[s][e] = (unsigned)v;
-          if ((unsigned)(v >> 32) != (unsigned)t) pend |= 1ull << (8 * s + e);
-        }
-      }
-      {
-        int spins = 0;
-        while (pend && ++spins <= lim) {
-          __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-          for (int s = 0; s < KSW; ++s) {
-            const int k = 32 * (KSW * wave + s) + 8 * q;
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              if (pend & (1ull << (8 * s + e))) {
-                const ps_u64 v = ps_gld(hrow + k + e);
-                hval[s][e] = (unsigned)v;
-                if ((unsigned)(v >> 32) == (unsigned)t) pend &= ~(1ull << (8 * s + e));
-              }
-          }
-        }
-        if (pend) __hip_atomic_store(status, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (!__syncthreads_and(pend == 0)) return;
-      }
+      if (tid == 0) s_ok = ps_poll(cnt + CNT_LD * (CNT_H + m0 / MR), (unsigned)(NUS * t), lim, status);
+      __syncthreads();
+      if (!s_ok) return;
       PS_TS(1, 1);
+      const unsigned hcur = (unsigned)((t & 1) * B * HD);
       f32x4 ha[KSW][2];
 #pragma unroll
-      for (int s = 0; s < KSW; ++s)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          ha[s][0][e] = __uint_as_float(hval[s][e]);
-          ha[s][1][e] = __uint_as_float(hval[s][4 + e]);
-        }
+      for (int s = 0; s < KSW; ++s) {
+        const int ks = KSW * wave + s, k = 32 * ks + 8 * q;
+        const bool ok = ks < KSH && k < HD;
+        const unsigned o = 4u * (hcur + (unsigned)((m0 + r) * HD) + (ok ? (unsigned)k : 0u));
+        ha[s][0] = ps_ld4(rh, o);
+        ha[s][1] = ps_ld4(rh, o + 16u);
+        if (!ok) ha[s][0] = ha[s][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
       // the feature part of this thread's output (plain: written before the launch)
       const int e2 = tid >> 6, l2 = tid & 63, row2 = l2 & 15, col2 = 4 * (l2 >> 4) + e2;
       const bool ok2 = n0 + col2 < EH;
@@ -754,12 +733,15 @@ static size_t pscan_lds_bytes(int A) {
 size_t op_pscan_ring_bytes(int B) {
   // hb [2][B][HD], pre [2][B][EH], iz [2][2][B][NR], counters
   return sizeof(float) * ((size_t)2 * B * HD + (size_t)2 * B * EH + (size_t)4 * B * NR) + PSCAN_CNT_BYTES +
-         sizeof(unsigned long long) * (size_t)B * (NR + HD) + PSCAN_TS_BYTES;
+         sizeof(unsigned long long) * (size_t)B * NR + PSCAN_TS_BYTES;
 }
 
+// B <= 128 by measurement (profiles/r05j_ab_pscan.txt): configs[1]'s B = 64 gains 7-10 % per epoch; at
+// B = 256 the 64-row GRU tiles read 154 KB of h per step per CU, bound by the per-CU L2 / MALL rate
+// (~33 GB/s, 4.6 us of the 34 us step) and the launch form is 1 % faster there
 bool op_pscan_supported(const dr_dims* d, int B, int T, int A) {
-  return !d->launch_form && d->hidden == HD && d->enc_hidden == EH && d->rows == NR && d->cols == NCL && A >= 1 && A <= 8 && T >= 2 &&
-         B >= 16 && B <= 256 && B % 16 == 0 && (B <= 64 || B % 64 == 0);
+  return !d->launch_form && d->hidden == HD && d->enc_hidden == EH && d->rows == NR && d->cols == NCL && A >= 1 &&
+         A <= 8 && T >= 2 && B >= 16 && B <= 128 && B % 16 == 0 && (B <= 64 || B % 32 == 0);
 }
 
 template <int NT, int MR, int MS>
@@ -783,7 +765,7 @@ int op_pscan(const dr_dims* d, const dr_world_model* wm, int B, int T, int A, co
     dr_set_error("pscan: unsupported shape (B=%d T=%d)", B, T);
     return DR_E_UNSUPPORTED;
   }
-  const int MR = B <= 64 ? 16 : (B <= 128 ? 32 : 64), MS = B <= 128 ? 16 : 32;
+  const int MR = B <= 64 ? 16 : 32, MS = 16;
   const int grid = std::max(std::max((B / MR) * NUS, (B / 16) * NC2), (B / MS) * NR);
   // every workgroup must be resident: all CUs of an unmasked stream
   int dev = 0, cus = 0;
@@ -823,20 +805,19 @@ int op_pscan(const dr_dims* d, const dr_world_model* wm, int B, int T, int A, co
   a.iz = reinterpret_cast<int*>(a.pre + (size_t)2 * B * EH);
   a.cnt = reinterpret_cast<unsigned*>(a.iz + (size_t)4 * B * NR);
   a.zg = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(a.cnt) + PSCAN_CNT_BYTES);
-  a.hg = a.zg + (size_t)B * NR;
-  a.ts = reinterpret_cast<long long*>(a.hg + (size_t)B * HD);
+  a.ts = reinterpret_cast<long long*>(a.zg + (size_t)B * NR);
   // counters zeroed by a kernel (captured graphs replay it; a memset node was seen not to)
   // counters and granule tags zeroed by a kernel (captured graphs replay it; a
   // memset node was seen not to): no granule of an earlier launch carries a
   // tag this launch waits for
-  DR_TRY(op_fill(PSCAN_CNT_BYTES / 4 + (long long)2 * B * (NR + HD), reinterpret_cast<float*>(a.cnt), 0.f, s));
+  DR_TRY(op_fill(PSCAN_CNT_BYTES / 4 + (long long)2 * B * NR, reinterpret_cast<float*>(a.cnt), 0.f, s));
   const bool bf = d->precision == DR_PREC_BF16;
 #define PS_L(NT, MRv, MSv) \
   if (MR == MRv && MS == MSv) return launch_pscan<NT, MRv, MSv>(a, grid, s);
   if (bf) {
-    PS_L(1, 16, 16) PS_L(1, 32, 16) PS_L(1, 64, 32)
+    PS_L(1, 16, 16) PS_L(1, 32, 16)
   } else {
-    PS_L(3, 16, 16) PS_L(3, 32, 16) PS_L(3, 64, 32)
+    PS_L(3, 16, 16) PS_L(3, 32, 16)
   }
 #undef PS_L
   dr_set_error("pscan: no instance");

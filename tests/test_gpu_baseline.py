@@ -3,7 +3,7 @@ MI355X box: pytest -m gpu).
 
 * configs[0] shape (CarRacing widths, B=16 S=50 H=15, S0 = 5): against the
   reference's own outputs (tests/golden/baseline_b16.npz) and the oracle;
-* configs[1] (B=64 S=64 H=15) and the north-star batch (B=256 S=64 H=15):
+* configs[1] (B=64 S=64 H=15), B=128 and the north-star batch (B=256 S=64 H=15):
   against the CPU oracle run on the box's host cores on the same inputs and
   noise (default reference init under torch.manual_seed(0), SURVEY §8d
   synthetic replay, S0 = 3 so the max(S, 1) normaliser is > 1).
@@ -169,7 +169,16 @@ def test_baseline_b16_vs_reference(gpu):
     assert abs(pre["S"] - float(fx["S_after"])) <= 1e-6 * float(fx["S_after"])
 
 
-@pytest.mark.parametrize("B,data", [(64, "synthetic"), (256, "synthetic"), (512, "synthetic"), (16, "fixture")])
+def pscan_status(eng):
+    """Status word of the persistent posterior scan (scan.hip counter block in
+    the observe workspace's ring): 0 = every hand-off completed in time."""
+    B = eng.B
+    off = 4 * (2 * B * 600 + 2 * B * 200 + 4 * B * 32) + 48 * 128
+    return int(eng.ws_obs.view(torch.uint8)[off:off + 4].view(torch.int32).item())
+
+
+@pytest.mark.parametrize("B,data", [(64, "synthetic"), (128, "synthetic"), (256, "synthetic"), (512, "synthetic"),
+                                    (16, "fixture")])
 def test_epoch_vs_oracle_at_baseline_shape(B, data, gpu):
     """configs[1] (B=64) and the north-star batch (B=256), S=64 H=15, full
     widths, reference default init, synthetic replay; B=512 (configs[2]'s
@@ -206,4 +215,6 @@ def test_epoch_vs_oracle_at_baseline_shape(B, data, gpu):
     ref["P0"] = P
     eng, pre = run_gpu_epoch(d, frames, acts, rews, conts, n, 0, starts, q_warm, eps, q, S0)
     n_tiny = compare(d, eng, pre, ref, C, f"B{B}", S0)
+    if B <= 128:  # the warm start ran as the persistent scan (scan.hip)
+        assert pscan_status(eng) == 0
     print(f"B{B} {data}: actor grad norm {float(ref['ts']['norm_actor']):.4g}, guarded {ref['guarded']}/{ref['draws']} draws, {n_tiny} near-zero-gradient params")

@@ -34,7 +34,7 @@ def main():
     torch.cuda.synchronize()
     T = eng.T
     grid = {16: 60, 32: 120, 64: 240, 128: 256, 256: 256}[B]
-    off = 4 * (2 * B * 600 + 2 * B * 200 + 4 * B * 32) + 6400
+    off = 4 * (2 * B * 600 + 2 * B * 200 + 4 * B * 32) + 6400 + 8 * B * 32  # scan.hip ring layout
     n = 64 * 24 * grid
     st = eng.ws_obs.view(torch.uint8)[off:off + 8 * n].view(torch.int64).cpu().numpy().reshape(64, 3, 8, grid)
     st = st[:T].astype(np.float64) / 100.0  # us
