@@ -19,6 +19,9 @@ slice of the batch; the exchange is one all-gather of the lambda returns
 Each phase is captured once into a HIP graph and replayed; collectives run
 between the phase graphs.
 """
+import contextlib
+import gc
+
 import numpy as np
 
 import torch
@@ -29,6 +32,23 @@ from . import hip
 WARM_STREAM = 1 << 24
 DREAM_STREAM = 2 << 24
 _CU_STREAMS = {}  # (device index, CU mask words) -> HIP stream handle (warm_stream)
+
+
+@contextlib.contextmanager
+def _no_gc():
+    """Stream capture with Python's cyclic collector off: an engine of an
+    earlier Dreamer (they hold each other, so only the collector frees them)
+    must not destroy its captured graphs while this capture is open -- a graph
+    destroyed during a global-mode capture invalidates it and aborts in the
+    destructor.  torch.cuda.graph collects once before capture_begin."""
+    enabled = gc.isenabled()
+    gc.collect()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if enabled:
+            gc.enable()
 
 
 def cu_mask_words(n_cus, fraction):
@@ -484,7 +504,7 @@ class ImaginationEngine:
         cs = torch.cuda.Stream(dev)
         cs.wait_stream(torch.cuda.current_stream(dev))
         graphs = {}
-        with torch.cuda.stream(cs):
+        with _no_gc(), torch.cuda.stream(cs):
             for s in (0, 1):
                 for name, body in (("warm", lambda s=s: warm(s)),
                                    ("imagine", lambda s=s: self.imagine(z0=P["z0"][s], h0=P["h0"][s]))):
@@ -623,7 +643,7 @@ class ImaginationEngine:
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         graphs = []
-        with torch.cuda.stream(s):
+        with _no_gc(), torch.cuda.stream(s):
             for _, body, _ in self.phases():
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=s):
