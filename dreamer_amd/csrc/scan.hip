@@ -45,6 +45,7 @@
 // Spins are bounded; a timeout sets the status word and the workgroup exits.
 #include "common.h"
 #include "scan.h"
+#include "persist.h"
 #include "ops.h"
 
 #include <string.h>
@@ -62,8 +63,6 @@ constexpr int CNT_LD = 32;   // counters 128 B apart
 constexpr int CNT_H = 0, CNT_PRE = 16, CNT_Z = 32, CNT_STATUS = 48;
 }  // namespace
 
-typedef unsigned ps_u32x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 ps_bf16x8 __attribute__((ext_vector_type(8)));
 
 struct alignas(16) PScanArgs {
   int B, T, A, step0;
@@ -101,134 +100,6 @@ struct alignas(16) PScanArgs {
 #else
 #define PS_TS(st, mk) do {} while (0)
 #endif
-
-__device__ __forceinline__ f32x4 ps_mfma(ps_u32x4 w, ps_u32x4 a, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(ps_bf16x8, w), __builtin_bit_cast(ps_bf16x8, a),
-                                                  c, 0, 0, 0);
-}
-// NT = 3: the six products of order >= 2^-16, smallest first (k_gemm_wks3's
-// order); NT = 1: bf16 perf mode (plane 0 x RNE(a))
-template <int NT>
-__device__ __forceinline__ f32x4 ps_prod(const ps_u32x4 (&w)[NT], const ps_u32x4 (&a)[NT], f32x4 c) {
-  if constexpr (NT == 3) {
-    c = ps_mfma(w[0], a[2], c);
-    c = ps_mfma(w[1], a[1], c);
-    c = ps_mfma(w[2], a[0], c);
-    c = ps_mfma(w[0], a[1], c);
-    c = ps_mfma(w[1], a[0], c);
-  }
-  return ps_mfma(w[0], a[0], c);
-}
-__device__ __forceinline__ unsigned ps_rne2(float x0, float x1) {
-  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
-  const b2 v = {(__bf16)x0, (__bf16)x1};
-  return __builtin_bit_cast(unsigned, v);
-}
-// 8 consecutive k of one row -> the MFMA fragment(s)
-template <int NT>
-__device__ __forceinline__ void ps_split(f32x4 x0, f32x4 x1, ps_u32x4 (&a)[NT]) {
-  if constexpr (NT == 3) {
-    unsigned h[4], m[4], l[4];
-    split3_pair(x0[0], x0[1], h[0], m[0], l[0]);
-    split3_pair(x0[2], x0[3], h[1], m[1], l[1]);
-    split3_pair(x1[0], x1[1], h[2], m[2], l[2]);
-    split3_pair(x1[2], x1[3], h[3], m[3], l[3]);
-    a[0] = (ps_u32x4){h[0], h[1], h[2], h[3]};
-    a[1] = (ps_u32x4){m[0], m[1], m[2], m[3]};
-    a[2] = (ps_u32x4){l[0], l[1], l[2], l[3]};
-  } else {
-    a[0] = (ps_u32x4){ps_rne2(x0[0], x0[1]), ps_rne2(x0[2], x0[3]), ps_rne2(x1[0], x1[1]), ps_rne2(x1[2], x1[3])};
-  }
-}
-
-// A resident weight fragment: the 8 consecutive k of one weight row a lane
-// feeds to the MFMA.  NT = 3 keeps them f32 (8 VGPRs) and splits them per use
-// (exact truncation split, 6 products); NT = 1 keeps their RNE bf16 (4 VGPRs).
-template <int NT>
-struct PsFrag {
-  f32x4 x0, x1;
-};
-template <>
-struct PsFrag<1> {
-  ps_u32x4 b;
-};
-// an offset the compiler cannot see through: keeps per-step weight loads in
-// the step loop (hoisted, they would stay live in registers across the scan)
-__device__ __forceinline__ unsigned ps_opaque(unsigned x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
-template <int NT>
-__device__ __forceinline__ PsFrag<NT> ps_frag(const float* W, unsigned e, bool ok) {
-  const float4 a = dr_ld4(W, ok ? e : 0u), c = dr_ld4(W, ok ? e + 4u : 0u);
-  f32x4 x0 = {a.x, a.y, a.z, a.w}, x1 = {c.x, c.y, c.z, c.w};
-  if (!ok) x0 = x1 = (f32x4){0.f, 0.f, 0.f, 0.f};
-  PsFrag<NT> f;
-  if constexpr (NT == 3) {
-    f.x0 = x0;
-    f.x1 = x1;
-  } else {
-    ps_u32x4 b[1];
-    ps_split<1>(x0, x1, b);
-    f.b = b[0];
-  }
-  return f;
-}
-// the opaque copy keeps the compiler from hoisting the split of a resident
-// fragment out of the step loop (that would re-create the 12-VGPR planes)
-template <int NT>
-__device__ __forceinline__ void ps_wsplit(const PsFrag<NT>& f, ps_u32x4 (&w)[NT]) {
-  if constexpr (NT == 3) {
-    f32x4 x0 = f.x0, x1 = f.x1;
-    asm volatile("" : "+v"(x0), "+v"(x1));
-    ps_split<3>(x0, x1, w);
-  } else {
-    w[0] = f.b;
-  }
-}
-
-// write-through (sc1) buffer accesses of the handed-off rings
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t ps_rsrc(const void* p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ f32x4 ps_ld4(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, 16));
-}
-__device__ __forceinline__ float ps_ld1(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, 0, 16));
-}
-__device__ __forceinline__ void ps_st1(__amdgpu_buffer_rsrc_t r, unsigned byte_off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)byte_off, 0, 16);
-}
-__device__ __forceinline__ void ps_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// 8-byte {data, tag} granules (MI355X_MICROARCH.md: the data IS the flag): ONE
-// aligned 8-byte sc1 store per granule, sc1 loads re-read until the tag matches
-typedef unsigned long long ps_u64;
-__device__ __forceinline__ void ps_gst(ps_u64* p, ps_u64 v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ ps_u64 ps_gld(const ps_u64* p) {
-  return __hip_atomic_load(const_cast<ps_u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// lane 0 of the workgroup: poll until *c >= target (relaxed sc1 loads + s_sleep)
-__device__ __forceinline__ bool ps_poll(const unsigned* c, unsigned target, int limit, unsigned* status) {
-  int spins = 0;
-  while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    __builtin_amdgcn_s_sleep(2);
-    if (++spins > limit) {
-      __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-  }
-  return true;
-}
-// every storing wave drained, then one lane signals for the workgroup
-__device__ __forceinline__ void ps_signal(unsigned* c) {
-  ps_drain();
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 template <int NT, int MR, int MS>
 __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
