@@ -4,6 +4,7 @@
 // no allocation) so a whole train_Agent epoch can be captured in a hipGraph.
 #include "engine_util.h"
 #include "scan.h"
+#include "dream.h"
 
 #ifndef DR_B16_CHAIN_WKS
 #define DR_B16_CHAIN_WKS 1  // A/B knob: bf16 mode's per-step grouped products on bf16 weight planes
@@ -13,6 +14,9 @@
 #endif
 #ifndef DR_PSCAN
 #define DR_PSCAN 1  // A/B knob: 0 = the warm start's posterior scan as three launches per step
+#endif
+#ifndef DR_PDREAM
+#define DR_PDREAM 1  // A/B knob: 0 = the imagination unroll as seven launches per step
 #endif
 
 // fp32 mode, tall batches: the first Linear of a head over [h | z] on the
@@ -380,6 +384,7 @@ struct ImWs {
   float *tl6p, *tl3p, *tl0p, *twhh, *thead, *tl3a, *tl0a;
   void* tn;  // split3 TN scratch of the actor weight gradients (tn_launch)
   size_t tn_bytes;
+  void* pd;  // the persistent unroll's hand-off buffers and counters (dream.hip), carved last
 };
 static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   const long long Bl = B, BH = (long long)B * H, B1 = (long long)B * (H + 1);
@@ -447,6 +452,7 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
                                  op_gemm_tn_split3_ws_bytes(d->actor_h2, d->actor_h1, BHi)),
                         op_gemm_tn_split3_ws_bytes(A, d->actor_h2, BHi));
   w.tn = c.raw(w.tn_bytes);
+  w.pd = c.raw(op_pdream_ws_bytes(d, B, H));
 }
 
 extern "C" size_t dr_imagine_workspace_bytes(const dr_dims* d, int B, int H) {
@@ -456,41 +462,14 @@ extern "C" size_t dr_imagine_workspace_bytes(const dr_dims* d, int B, int H) {
   return c.off;
 }
 
-extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, int B, int H,
-                              const float* z0, const float* h0, dr_noise noise, int deterministic, float* latents,
-                              float* hiddens, float* actions, float* rewards, float* continues, float* mus,
-                              float* sigmas, void* tape, void* ws, size_t ws_bytes, hipStream_t s) {
-  DR_REQUIRE(d && wm && ac && z0 && h0 && latents && hiddens && actions && rewards && continues && mus && sigmas &&
-                 tape && B > 0 && H > 0,
-             "null argument or empty batch");
-  GemmBf16Scope bf16_scope(d->precision == DR_PREC_BF16);
-  Carve c(ws);
-  ImWs w;
-  imws_carve(c, d, B, H, w);
-  WS_CHECK(c, ws_bytes);
-  Carve ct(tape);
-  Tape tp;
-  tape_carve(ct, d, B, H, tp);
+// the unroll as seven launches per step (shapes outside dream.hip, launch_form)
+static int imagine_launch_form(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, int B, int H,
+                               const dr_noise& noise, const dr_noise& nq, int deterministic, float* latents,
+                               float* hiddens, float* actions, float* mus, float* sigmas, const Tape& tp, ImWs& w,
+                               bool split_gru, bool zg, hipStream_t s) {
   const int L = latent(d), Hd = d->hidden, A = d->action, a1 = d->actor_h1, a2 = d->actor_h2;
   const long long ldH = (long long)(H + 1) * Hd, ldL = (long long)(H + 1) * L, ldA = (long long)H * A;
   const long long lda1 = (long long)H * a1, lda2 = (long long)H * a2;
-  DR_TRY(copy2d(latents, ldL, z0, L, L, B, s));
-  DR_TRY(copy2d(hiddens, ldH, h0, Hd, Hd, B, s));
-  dr_noise nq = noise;  // Categorical draws: a Philox stream apart from the actor's
-  nq.stream += 65536;
-  // per-step structure (SURVEY a7-a10): the three products that read only
-  // h_{t+1} -- the prior's first Linear, the h-part of the next actor's first
-  // Linear and (B >= 128, split GRU) the next GRU step's hidden product --
-  // run as ONE grouped launch right after the GRU; the actor's latent part is
-  // then a gather of R rows of its transposed z-columns (z is one-hot)
-  const bool split_gru = B >= 128;
-  const bool zg = d->rows <= 32 && a1 % 4 == 0;
-  {
-    TransposeJob tj[2] = {{3 * Hd, L + A, 3 * Hd, wm->w_ih, w.wt}, {a1, Hd + L, a1, ac->l0.w, w.tl0f}};
-    DR_TRY(op_transpose_multi(tj, zg ? 2 : 1, s));
-  }
-  DR_TRY(op_onehot_index(B, d->rows, d->cols, latents, ldL, w.idx[0], onehot_vals(w.idx[0], B, d->rows), s));
-
   const bool planes = split_gru && H > 1 && Hd % 8 == 0;
   if (planes) {
     DR_TRY(split_planes(d->prior_h1, Hd, wm->prior.l0.w, Hd, w.s3p0, s));
@@ -574,6 +553,58 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
       DR_TRY(run(G_NT, AM_LNSILU, hd, s));
     }
   }
+  return DR_OK;
+}
+
+extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, int B, int H,
+                              const float* z0, const float* h0, dr_noise noise, int deterministic, float* latents,
+                              float* hiddens, float* actions, float* rewards, float* continues, float* mus,
+                              float* sigmas, void* tape, void* ws, size_t ws_bytes, hipStream_t s) {
+  DR_REQUIRE(d && wm && ac && z0 && h0 && latents && hiddens && actions && rewards && continues && mus && sigmas &&
+                 tape && B > 0 && H > 0,
+             "null argument or empty batch");
+  GemmBf16Scope bf16_scope(d->precision == DR_PREC_BF16);
+  Carve c(ws);
+  ImWs w;
+  imws_carve(c, d, B, H, w);
+  WS_CHECK(c, ws_bytes);
+  Carve ct(tape);
+  Tape tp;
+  tape_carve(ct, d, B, H, tp);
+  const int L = latent(d), Hd = d->hidden, A = d->action, a1 = d->actor_h1, a2 = d->actor_h2;
+  const long long ldH = (long long)(H + 1) * Hd, ldL = (long long)(H + 1) * L, ldA = (long long)H * A;
+  const long long lda1 = (long long)H * a1, lda2 = (long long)H * a2;
+  DR_TRY(copy2d(latents, ldL, z0, L, L, B, s));
+  DR_TRY(copy2d(hiddens, ldH, h0, Hd, Hd, B, s));
+  dr_noise nq = noise;  // Categorical draws: a Philox stream apart from the actor's
+  nq.stream += 65536;
+  // per-step structure (SURVEY a7-a10): the three products that read only
+  // h_{t+1} -- the prior's first Linear, the h-part of the next actor's first
+  // Linear and (B >= 128, split GRU) the next GRU step's hidden product --
+  // run as ONE grouped launch right after the GRU; the actor's latent part is
+  // then a gather of R rows of its transposed z-columns (z is one-hot)
+  const bool split_gru = B >= 128;
+  const bool zg = d->rows <= 32 && a1 % 4 == 0;
+  {
+    TransposeJob tj[2] = {{3 * Hd, L + A, 3 * Hd, wm->w_ih, w.wt}, {a1, Hd + L, a1, ac->l0.w, w.tl0f}};
+    DR_TRY(op_transpose_multi(tj, zg ? 2 : 1, s));
+  }
+  DR_TRY(op_onehot_index(B, d->rows, d->cols, latents, ldL, w.idx[0], onehot_vals(w.idx[0], B, d->rows), s));
+
+  // the whole unroll as one persistent launch where the shape and the stream's
+  // CUs allow it (dream.hip); the reward / continue heads below either way
+  bool unrolled = false;
+  if (DR_PDREAM && zg && op_pdream_supported(d, B, H, A)) {
+    const PDreamTape pt = {tp.eps, tp.ls_raw, tp.pre1a, tp.x1a, tp.pre2a, tp.x2a, tp.r, tp.u, tp.n, tp.ghn,
+                           tp.pre1p, tp.pre2p, tp.soft};
+    const int rc = op_pdream(d, wm, ac, B, H, w.wt, w.tl0f + (long long)Hd * a1, w.idx[0], noise, nq, deterministic,
+                             latents, hiddens, actions, mus, sigmas, pt, w.pd, s);
+    if (rc != DR_E_UNSUPPORTED && rc != DR_OK) return rc;
+    unrolled = rc == DR_OK;
+  }
+  if (!unrolled) DR_TRY(imagine_launch_form(d, wm, ac, B, H, noise, nq, deterministic, latents, hiddens, actions, mus,
+                                            sigmas, tp, w, split_gru, zg, s));
+
   // RewardPredictor / ContinuePredictor (DynamicsPredictors.py:64-74, 95-105)
   // on every imagined state (h_{t+1}, z_{t+1}) at once: rows m = b (H+1) + t'
   // of the contiguous [B][H+1] hiddens / latents (t' = 0 rides along unused);

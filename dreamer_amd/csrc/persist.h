@@ -66,6 +66,11 @@ __device__ __forceinline__ unsigned ps_opaque(unsigned x) {
   asm volatile("" : "+v"(x));
   return x;
 }
+// "these loaded values are needed here": one wait for a batch of loads issued
+// together (the scheduler would otherwise sink each load to its use and pay a
+// round trip per use under register pressure)
+__device__ __forceinline__ void ps_pin(f32x4& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void ps_pin(float& x) { asm volatile("" : "+v"(x)); }
 template <int NT>
 __device__ __forceinline__ PsFrag<NT> ps_frag(const float* W, unsigned e, bool ok) {
   const float4 a = dr_ld4(W, ok ? e : 0u), c = dr_ld4(W, ok ? e + 4u : 0u);

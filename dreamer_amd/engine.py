@@ -155,9 +155,10 @@ class ImaginationEngine:
         L.call("dr_observe_scan", d, wm, self.B, self.T, L.ptr(self.feat), L.ptr(self.act_win), self.S * A, A, None,
                None, nz, L.ptr(self.z0), L.ptr(self.h0), None, L.ptr(self.ws_obs), self.ws_obs.numel(), st)
 
-    def imagine(self, eps=None, q=None, deterministic=False, z0=None, h0=None):
-        """a7: unroll H steps from (self.z0, self.h0) (or the given slot)."""
-        d = self.d
+    def imagine(self, eps=None, q=None, deterministic=False, z0=None, h0=None, d=None):
+        """a7: unroll H steps from (self.z0, self.h0) (or the given slot);
+        d: dims override (the pipelined epochs pass launch_form = 1)."""
+        d = self.d if d is None else d
         z0 = self.z0 if z0 is None else z0
         h0 = self.h0 if h0 is None else h0
         if eps is not None or q is not None:
@@ -486,8 +487,10 @@ class ImaginationEngine:
             return P
         d, A = self.d, self.d.action
         # the warm graphs are captured here and replayed on the CU-masked warm
-        # stream: launch form (a persistent scan needs every workgroup
-        # resident, which the capture stream cannot vouch for)
+        # stream, the imagination beside them: both in launch form (a
+        # persistent kernel needs every workgroup resident, which neither the
+        # capture stream nor a chain sharing the CUs with the warm start can
+        # vouch for)
         dw = L.dr_dims.from_buffer_copy(d)
         dw.launch_form = 1
 
@@ -507,7 +510,7 @@ class ImaginationEngine:
         with _no_gc(), torch.cuda.stream(cs):
             for s in (0, 1):
                 for name, body in (("warm", lambda s=s: warm(s)),
-                                   ("imagine", lambda s=s: self.imagine(z0=P["z0"][s], h0=P["h0"][s]))):
+                                   ("imagine", lambda s=s: self.imagine(z0=P["z0"][s], h0=P["h0"][s], d=dw))):
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, stream=cs):
                         body()

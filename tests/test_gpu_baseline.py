@@ -177,6 +177,20 @@ def pscan_status(eng):
     return int(eng.ws_obs.view(torch.uint8)[off:off + 4].view(torch.int32).item())
 
 
+def pdream_status(eng):
+    """Status word of the persistent imagination unroll (dream.hip: its
+    counter block closes the imagination workspace): 0 = every hand-off
+    completed in time."""
+    from dreamer_amd import _lib as L
+    B, H = eng.B, eng.H
+    total = L.query("dr_imagine_workspace_bytes", eng.d, B, H)
+    pd = 4 * H * B * 200 + 8 * (H + 1) * B * 32
+    cnt = total - 7 * 16 * 32 * 4
+    word = lambda o: int(eng.ws_im.view(torch.uint8)[o:o + 4].view(torch.int32).item())
+    # (status, the GRU stage's counter of rows 0..15: 60 unit slices x H steps when it ran)
+    return word(cnt + 6 * 16 * 32 * 4), word(cnt + 2 * 16 * 32 * 4)
+
+
 @pytest.mark.parametrize("B,data", [(64, "synthetic"), (128, "synthetic"), (256, "synthetic"), (512, "synthetic"),
                                     (16, "fixture")])
 def test_epoch_vs_oracle_at_baseline_shape(B, data, gpu):
@@ -215,6 +229,7 @@ def test_epoch_vs_oracle_at_baseline_shape(B, data, gpu):
     ref["P0"] = P
     eng, pre = run_gpu_epoch(d, frames, acts, rews, conts, n, 0, starts, q_warm, eps, q, S0)
     n_tiny = compare(d, eng, pre, ref, C, f"B{B}", S0)
-    if B <= 128:  # the warm start ran as the persistent scan (scan.hip)
+    if B <= 128:  # the warm start and the unroll ran as the persistent kernels (scan.hip, dream.hip)
         assert pscan_status(eng) == 0
+        assert pdream_status(eng) == (0, 60 * H)
     print(f"B{B} {data}: actor grad norm {float(ref['ts']['norm_actor']):.4g}, guarded {ref['guarded']}/{ref['draws']} draws, {n_tiny} near-zero-gradient params")
