@@ -131,15 +131,6 @@ __device__ __forceinline__ f32x4 pd_tile_global(const PsFrag<NT> (&wf)[KS], __am
   return acc;
 }
 
-// the total over each 16-lane row, in every lane of the row (DPP only)
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dr_dpp<0xB1>(v);
-  v += dr_dpp<0x4E>(v);
-  v += dr_dpp<0x141>(v);
-  v += dr_dpp<0x140>(v);
-  return v;
-}
-
 // LN-SiLU (eps 1e-5, hardware exp2 SiLU: k_ln_gemm_sample's arithmetic) of 16
 // rows of MW floats from an sc1 buffer into LDS rows of stride KP3 (zero to
 // 224); optionally also the normalised rows to `out` (plain stores, stride

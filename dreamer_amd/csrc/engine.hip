@@ -5,6 +5,7 @@
 #include "engine_util.h"
 #include "scan.h"
 #include "dream.h"
+#include "bptt.h"
 
 #ifndef DR_B16_CHAIN_WKS
 #define DR_B16_CHAIN_WKS 1  // A/B knob: bf16 mode's per-step grouped products on bf16 weight planes
@@ -17,6 +18,9 @@
 #endif
 #ifndef DR_PDREAM
 #define DR_PDREAM 1  // A/B knob: 0 = the imagination unroll as seven launches per step
+#endif
+#ifndef DR_PBPTT
+#define DR_PBPTT 1  // A/B knob: 0 = the BPTT reverse loop as seven launches per step
 #endif
 
 // fp32 mode, tall batches: the first Linear of a head over [h | z] on the
@@ -385,6 +389,7 @@ struct ImWs {
   void* tn;  // split3 TN scratch of the actor weight gradients (tn_launch)
   size_t tn_bytes;
   void* pd;  // the persistent unroll's hand-off buffers and counters (dream.hip), carved last
+  void* pb;  // the persistent BPTT's (bptt.hip), after it
 };
 static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   const long long Bl = B, BH = (long long)B * H, B1 = (long long)B * (H + 1);
@@ -453,6 +458,7 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
                         op_gemm_tn_split3_ws_bytes(A, d->actor_h2, BHi));
   w.tn = c.raw(w.tn_bytes);
   w.pd = c.raw(op_pdream_ws_bytes(d, B, H));
+  w.pb = c.raw(op_pbptt_ws_bytes(d, B, H));
 }
 
 extern "C" size_t dr_imagine_workspace_bytes(const dr_dims* d, int B, int H) {
@@ -754,7 +760,19 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
   const bool planes = B >= 128 && (3 * Hd) % 8 == 0;
   if (!do_main) return DR_OK;
 
-  for (int t = H - 1; t >= 0; --t) {
+  // the reverse loop as one persistent launch where the shape and the stream's
+  // CUs allow it (bptt.hip); the weight gradients below either way
+  bool looped = false;
+  if (DR_PBPTT && op_pbptt_supported(d, B, H, A)) {
+    const PBpttIO io = {w.tl6p, w.tl3p, w.tl0p, w.wt, w.twhh, w.thead, w.tl3a, w.tl0a,
+                        tp.soft, tp.pre2p, tp.pre1p, tp.r, tp.u, tp.n, tp.ghn, tp.pre2a, tp.pre1a, tp.ls_raw, tp.eps,
+                        hiddens, actions, g_mus, g_sigmas, w.gH, w.gZ, w.gA,
+                        w.gheads, w.gpre2a, w.gy2a, w.xh2a, w.gpre1a, w.gy1a, w.xh1a};
+    const int rc = op_pbptt(d, wm, ac, B, H, io, w.pb, s);
+    if (rc != DR_E_UNSUPPORTED && rc != DR_OK) return rc;
+    looped = rc == DR_OK;
+  }
+  for (int t = H - 1; t >= 0 && !looped; --t) {
     const long long hb = (long long)Hd * B * t;
     float* gH_t = w.gH + (long long)t * Hd;
     float* gH_n = w.gH + (long long)(t + 1) * Hd;

@@ -143,3 +143,32 @@ __device__ __forceinline__ void ps_signal(unsigned* c) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+
+// the total over each 16-lane row, in every lane of the row (DPP only)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dr_dpp<0xB1>(v);
+  v += dr_dpp<0x4E>(v);
+  v += dr_dpp<0x141>(v);
+  v += dr_dpp<0x140>(v);
+  return v;
+}
+
+// lane 0 polls counters c0, c0 + ld, ... (n of them) >= target, then the
+// workgroup barrier; false on a timeout (the status word is set)
+__device__ __forceinline__ bool ps_wait(int* s_ok, const unsigned* c0, int ld, int n, unsigned target, int lim,
+                                        unsigned* status) {
+  if (threadIdx.x == 0) {
+    bool ok = true;
+    for (int i = 0; i < n && ok; ++i) ok = ps_poll(c0 + ld * i, target, lim, status);
+    *s_ok = ok;
+  }
+  __syncthreads();
+  return *s_ok != 0;
+}
+// every storing wave drained; lanes 0 .. n-1 add 1 to counters c0, c0 + ld, ...
+__device__ __forceinline__ void ps_signal_n(unsigned* c0, int ld, int n) {
+  ps_drain();
+  __syncthreads();
+  if ((int)threadIdx.x < n)
+    __hip_atomic_fetch_add(c0 + ld * threadIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}

@@ -243,8 +243,8 @@ class ImaginationEngine:
                L.ptr(self.R), L.ptr(self.ctape), scale, L.ptr(ag.loss_slot(1)), ag.critic_struct(grad=True),
                L.ptr(self.ws_cr2), self.ws_cr2.numel(), hip.stream())
 
-    def _bptt(self):
-        ag, d = self.dr.agent, self.d
+    def _bptt(self, d=None):
+        ag, d = self.dr.agent, (self.d if d is None else d)
         L.call("dr_imagine_bwd_main", d, self.dr.world_model.packed(), ag.actor_struct(), self.B, self.H,
                L.ptr(self.latents), L.ptr(self.hiddens), L.ptr(self.actions), L.ptr(self.g_mu), L.ptr(self.g_sig),
                0, L.ptr(self.tape), ag.actor_struct(grad=True), L.ptr(self.ws_im), self.ws_im.numel(), hip.stream())
@@ -487,7 +487,7 @@ class ImaginationEngine:
             return P
         d, A = self.d, self.d.action
         # the warm graphs are captured here and replayed on the CU-masked warm
-        # stream, the imagination beside them: both in launch form (a
+        # stream, the imagination and the BPTT beside them: all in launch form (a
         # persistent kernel needs every workgroup resident, which neither the
         # capture stream nor a chain sharing the CUs with the warm start can
         # vouch for)
@@ -517,7 +517,7 @@ class ImaginationEngine:
                     graphs[(name, s)] = g
             for name, body in (("returns", self.returns), ("xfwd", self._x_critic_fwd_and_prep),
                                ("actor_loss", self._actor_loss), ("xbwd", self._x_critic_bwd),
-                               ("bptt", self._bptt), ("optim", self._ph_optim)):
+                               ("bptt", lambda: self._bptt(d=dw)), ("optim", self._ph_optim)):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=cs):
                     body()

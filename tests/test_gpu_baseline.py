@@ -185,10 +185,16 @@ def pdream_status(eng):
     B, H = eng.B, eng.H
     total = L.query("dr_imagine_workspace_bytes", eng.d, B, H)
     pd = 4 * H * B * 200 + 8 * (H + 1) * B * 32
-    cnt = total - 7 * 16 * 32 * 4
+    pb = (4 * B * H * (4 * 200 + 200 + 2 * 1800 + 600 + 1664 + 2 * 200 + 1024 + 600) + 8 * 8 * 32 * 4) if B <= 64 else 0
+    cnt = (total - pb) - 7 * 16 * 32 * 4  # the unroll's block ends where the BPTT's starts (256-byte multiples)
     word = lambda o: int(eng.ws_im.view(torch.uint8)[o:o + 4].view(torch.int32).item())
-    # (status, the GRU stage's counter of rows 0..15: 60 unit slices x H steps when it ran)
-    return word(cnt + 6 * 16 * 32 * 4), word(cnt + 2 * 16 * 32 * 4)
+    # (status, the GRU stage's counter of rows 0..15: 60 unit slices x H steps when it ran), and, at
+    # B <= 64, the BPTT's (status, Q7's counter of rows 0..15: 51 column blocks x H steps)
+    st = (word(cnt + 6 * 16 * 32 * 4), word(cnt + 2 * 16 * 32 * 4))
+    if B <= 64:
+        pcnt = total - 8 * 8 * 32 * 4
+        st += (word(pcnt + 7 * 8 * 32 * 4), word(pcnt + 6 * 8 * 32 * 4))
+    return st
 
 
 @pytest.mark.parametrize("B,data", [(64, "synthetic"), (128, "synthetic"), (256, "synthetic"), (512, "synthetic"),
@@ -231,5 +237,8 @@ def test_epoch_vs_oracle_at_baseline_shape(B, data, gpu):
     n_tiny = compare(d, eng, pre, ref, C, f"B{B}", S0)
     if B <= 128:  # the warm start and the unroll ran as the persistent kernels (scan.hip, dream.hip)
         assert pscan_status(eng) == 0
-        assert pdream_status(eng) == (0, 60 * H)
+        st = pdream_status(eng)
+        assert st[:2] == (0, 60 * H)
+        if B <= 64:  # and the BPTT (bptt.hip)
+            assert st[2:] == (0, 51 * H)
     print(f"B{B} {data}: actor grad norm {float(ref['ts']['norm_actor']):.4g}, guarded {ref['guarded']}/{ref['draws']} draws, {n_tiny} near-zero-gradient params")
