@@ -860,7 +860,8 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
     float* sk = w.sk;
     long long skn = w.sk_n;
     for (int i = 0; i < 4; ++i) give_splitk(p[i], sk, skn);
-    DR_TRY(tn_launch(p, 4, w.tn, w.tn_bytes, s));
+    // bf16 perf mode: one-term bf16 operands, f32 accumulation (as the WM step's)
+    DR_TRY(tn_launch(p, 4, w.tn, w.tn_bytes, s, d->precision == DR_PREC_BF16 ? 1 : 3));
   }
   {
     ColsumJob cj[8] = {
@@ -1038,7 +1039,7 @@ extern "C" int dr_critic_loss_bwd(const dr_dims* d, const dr_critic* cr, int B, 
     float* sk = w.sk;
     long long skn = w.sk_n;
     for (int i = 0; i < 3; ++i) give_splitk(p[i], sk, skn);
-    DR_TRY(tn_launch(p, 3, w.tn, w.tn_bytes, s));
+    DR_TRY(tn_launch(p, 3, w.tn, w.tn_bytes, s, d->precision == DR_PREC_BF16 ? 1 : 3));
   }
   {
     ColsumJob cj[7] = {

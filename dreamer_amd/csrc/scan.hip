@@ -137,9 +137,6 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
       w1[s][ct] = ps_frag<NT>(g.whh, (unsigned)(n * HD + k), ok);
     }
   }
-  // S3's LayerNorm parameters (one float4 per lane: K = 200 <= 256) and logit biases
-  const bool okk = lane < EH / 4;
-  const float4 lng = dr_ld4(g.ln_g, okk ? 4u * lane : 0u), lnb = dr_ld4(g.ln_b, okk ? 4u * lane : 0u);
   // S1's W_ih^T slice: rows k of W_ih^T (latents, then actions), the tile's 30 gate columns
   if (do1) {
     const int nrow = LAT + A;
@@ -252,39 +249,31 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
         if (!__syncthreads_and(zpend == 0)) return;
       }
       PS_TS(0, 2);
-      // gi by gather from the LDS slice, thread = (row, 8 gate columns): the
-      // sampled W_ih^T row of every group read as four 8-byte pieces;
-      // groups ascending (fmaf), actions, + b_ih (k_gru_gates' summation order)
-      if (tid < 4 * MR) {
-        const int row = tid >> 2, c0 = 8 * (tid & 3);
-        float v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = 0.f;
-        const int2* iz = siz + row * NR;
+      // gi by gather from the LDS slice, thread = (row, column pair): the
+      // sampled W_ih^T row of every group read as one 8-byte piece; groups
+      // ascending (fmaf), actions, + b_ih (k_gru_gates' summation order)
+      for (int p = tid; p < MR * 16; p += NTH) {
+        const int row = p >> 4, c0 = 2 * (p & 15);
+        if (c0 < WLD) {
+          float v0 = 0.f, v1 = 0.f;
+          const int2* iz = siz + row * NR;
 #pragma unroll 8
-        for (int u = 0; u < NR; ++u) {
-          const int2 p = iz[u];
-          const float zv = __int_as_float(p.y);
-          const float2* wr = reinterpret_cast<const float2*>(wih + (u * NCL + p.x) * WLD + c0);
-          const float2 w0 = wr[0], w1v = wr[1], w2v = wr[2], w3v = wr[3];
-          v[0] = fmaf(w0.x, zv, v[0]);
-          v[1] = fmaf(w0.y, zv, v[1]);
-          v[2] = fmaf(w1v.x, zv, v[2]);
-          v[3] = fmaf(w1v.y, zv, v[3]);
-          v[4] = fmaf(w2v.x, zv, v[4]);
-          v[5] = fmaf(w2v.y, zv, v[5]);
-          v[6] = fmaf(w3v.x, zv, v[6]);
-          v[7] = fmaf(w3v.y, zv, v[7]);
+          for (int u = 0; u < NR; ++u) {
+            const int2 pz = iz[u];
+            const float zv = __int_as_float(pz.y);
+            const float2 w = *reinterpret_cast<const float2*>(wih + (u * NCL + pz.x) * WLD + c0);
+            v0 = fmaf(w.x, zv, v0);
+            v1 = fmaf(w.y, zv, v1);
+          }
+          for (int ia = 0; ia < A; ++ia) {
+            const float av = sact[row * 8 + ia];
+            const float2 w = *reinterpret_cast<const float2*>(wih + (LAT + ia) * WLD + c0);
+            v0 = fmaf(w.x, av, v0);
+            v1 = fmaf(w.y, av, v1);
+          }
+          sgi[row * 32 + c0] = v0 + sbias[c0];
+          sgi[row * 32 + c0 + 1] = v1 + sbias[c0 + 1];
         }
-        for (int ia = 0; ia < A; ++ia) {
-          const float av = sact[row * 8 + ia];
-          const float* wr = wih + (LAT + ia) * WLD + c0;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = fmaf(wr[e], av, v[e]);
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (c0 + e < WLD) sgi[row * 32 + c0 + e] = v[e] + sbias[c0 + e];
       }
       PS_TS(0, 3);
       // gh partial over this wave's k-steps
@@ -392,6 +381,10 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
         const bool ok2 = ks < KSH && k < HD && c2 < EH;
         w2[s] = ps_frag<NT>(g.wm0, ps_opaque(ok2 ? (unsigned)(c2 * g.ldm0 + k) : 0u), ok2);
       }
+      // the feature part of this thread's output (plain: written before the launch)
+      const int e2 = tid >> 6, l2 = tid & 63, row2 = l2 & 15, col2 = 4 * (l2 >> 4) + e2;
+      const bool ok2 = n0 + col2 < EH;
+      const float fv = dr_ld1(g.feat, ok2 ? (unsigned)((t * B + m0 + row2) * EH + n0 + col2) : 0u);
       if (tid == 0) s_ok = ps_poll(cnt + CNT_LD * (CNT_H + m0 / MR), (unsigned)(NUS * t), lim, status);
       __syncthreads();
       if (!s_ok) return;
@@ -407,10 +400,6 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
         ha[s][1] = ps_ld4(rh, o + 16u);
         if (!ok) ha[s][0] = ha[s][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
       }
-      // the feature part of this thread's output (plain: written before the launch)
-      const int e2 = tid >> 6, l2 = tid & 63, row2 = l2 & 15, col2 = 4 * (l2 >> 4) + e2;
-      const bool ok2 = n0 + col2 < EH;
-      const float fv = dr_ld1(g.feat, ok2 ? (unsigned)((t * B + m0 + row2) * EH + n0 + col2) : 0u);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KSW; ++s) {
@@ -449,6 +438,26 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
           for (int i = 0; i < 4; ++i) qn[i] = dr_exp1_k(rng_seed, rng_off, st, row, e0 + i);
         }
       }
+      // latent_mapper.3's rows of the group (28 KB, L2-resident across the
+      // steps) and this lane's LayerNorm chunks, issued before the poll
+      PsFrag<3> w3[KSW3][2];
+#pragma unroll
+      for (int s = 0; s < KSW3; ++s) {
+        const int ks = KSW3 * wave + s, k = 32 * ks + 8 * q;
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const bool ok = ks < KSE && k < EH;
+          w3[s][ct] = ps_frag<3>(g.wm3, ps_opaque((unsigned)((gq * NCL + ct * 16 + r) * EH + k)), ok);
+        }
+      }
+      const int sub16 = lane & 15;
+      float4 lg4[4], lb4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = sub16 + 16 * j;
+        lg4[j] = dr_ld4(g.ln_g, ps_opaque(c < EH / 4 ? 4u * c : 0u));
+        lb4[j] = dr_ld4(g.ln_b, ps_opaque(c < EH / 4 ? 4u * c : 0u));
+      }
       PS_TS(2, 0);
       if (t >= 1) {
         if (tid == 0) {
@@ -461,49 +470,52 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
         if (!s_ok) return;
       }
       PS_TS(2, 1);
-      // LN-SiLU of the block's rows into LDS (a wave per row, DPP statistics;
-      // k_ln_gemm_sample's arithmetic), zero-padded to 224
-      // latent_mapper.3's rows of the group (28 KB, L2-resident across the steps)
-      PsFrag<3> w3[KSW3][2];
-#pragma unroll
-      for (int s = 0; s < KSW3; ++s) {
-        const int ks = KSW3 * wave + s, k = 32 * ks + 8 * q;
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-          const bool ok = ks < KSE && k < EH;
-          w3[s][ct] = ps_frag<3>(g.wm3, ps_opaque((unsigned)((gq * NCL + ct * 16 + r) * EH + k)), ok);
-        }
-      }
+      // LN-SiLU of the block's rows into LDS (16 lanes per row, wave w takes
+      // rows 4 w .. 4 w + 3 of each 16-row pass, DPP-only sums; k_ln_gemm_sample's
+      // element arithmetic), zero-padded to 224
       float* sA = scr;
-      f32x4 xr[MS / 4];  // every row of this wave issued before the first reduction
 #pragma unroll
-      for (int i = 0; i < MS / 4; ++i) {
-        const int m = m3 + wave + 4 * i;
-        if (t == 0) {
-          const float4 xf = dr_ld4(g.feat, okk ? (unsigned)(m * EH + 4 * lane) : 0u);
-          xr[i] = (f32x4){xf.x, xf.y, xf.z, xf.w};
-        } else {
-          xr[i] = ps_ld4(rp, 4u * ((unsigned)((t & 1) * B * EH + m * EH) + (okk ? 4u * lane : 0u)));
+      for (int pass = 0; pass < MS / 16; ++pass) {
+        const int ml = pass * 16 + wave * 4 + (lane >> 4), m = m3 + ml;
+        f32x4 xr[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = sub16 + 16 * j;
+          const unsigned o = ps_opaque(c < EH / 4 ? 4u * c : 0u);
+          if (t == 0) {
+            const float4 xf = dr_ld4(g.feat, (unsigned)(m * EH) + o);
+            xr[j] = (f32x4){xf.x, xf.y, xf.z, xf.w};
+          } else {
+            xr[j] = ps_ld4(rp, 4u * ((unsigned)((t & 1) * B * EH + m * EH) + o));
+          }
         }
-      }
 #pragma unroll
-      for (int i = 0; i < MS / 4; ++i) {
-        const int ml = wave + 4 * i;
-        const f32x4 x = xr[i];
-        const float mean = wave_sum(okk ? (x[0] + x[1]) + (x[2] + x[3]) : 0.f) / (float)EH;
+        for (int j = 0; j < 4; ++j) ps_pin(xr[j]);
+        float sm = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (sub16 + 16 * j < EH / 4) sm += (xr[j][0] + xr[j][1]) + (xr[j][2] + xr[j][3]);
+        const float mean = row16_sum(sm) / (float)EH;
         float sq = 0.f;
-        if (okk) {
-          const float dx = x[0] - mean, dy = x[1] - mean, dz = x[2] - mean, dw = x[3] - mean;
-          sq = (dx * dx + dy * dy) + (dz * dz + dw * dw);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (sub16 + 16 * j < EH / 4) {
+            const float dx = xr[j][0] - mean, dy = xr[j][1] - mean, dz = xr[j][2] - mean, dw = xr[j][3] - mean;
+            sq += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+          }
+        const float rstd = 1.0f / sqrtf(row16_sum(sq) / (float)EH + 1e-5f);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = sub16 + 16 * j;
+          float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (c < EH / 4) {
+            y.x = dr_silu_fast((xr[j][0] - mean) * rstd * lg4[j].x + lb4[j].x);
+            y.y = dr_silu_fast((xr[j][1] - mean) * rstd * lg4[j].y + lb4[j].y);
+            y.z = dr_silu_fast((xr[j][2] - mean) * rstd * lg4[j].z + lb4[j].z);
+            y.w = dr_silu_fast((xr[j][3] - mean) * rstd * lg4[j].w + lb4[j].w);
+          }
+          if (c < KSE * 8) *reinterpret_cast<float4*>(&sA[ml * KP3 + 4 * c]) = y;
         }
-        const float rstd = 1.0f / sqrtf(wave_sum(sq) / (float)EH + 1e-5f);
-        float4 y;
-        y.x = dr_silu_fast((x[0] - mean) * rstd * lng.x + lnb.x);
-        y.y = dr_silu_fast((x[1] - mean) * rstd * lng.y + lnb.y);
-        y.z = dr_silu_fast((x[2] - mean) * rstd * lng.z + lnb.z);
-        y.w = dr_silu_fast((x[3] - mean) * rstd * lng.w + lnb.w);
-        if (!okk) y = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (lane < KSE * 8) *reinterpret_cast<float4*>(&sA[ml * KP3 + 4 * lane]) = y;
       }
       __syncthreads();
       PS_TS(2, 2);
@@ -607,12 +619,16 @@ size_t op_pscan_ring_bytes(int B) {
          sizeof(unsigned long long) * (size_t)B * NR + PSCAN_TS_BYTES;
 }
 
-// B <= 128 by measurement (profiles/r05j_ab_pscan.txt): configs[1]'s B = 64 gains 7-10 % per epoch; at
-// B = 256 the 64-row GRU tiles read 154 KB of h per step per CU, bound by the per-CU L2 / MALL rate
-// (~33 GB/s, 4.6 us of the 34 us step) and the launch form is 1 % faster there
+// B <= 128 by measurement (profiles/r05j_ab_pscan.txt, r05r_ab_scan_B256.txt): configs[1]'s B = 64 gains
+// 7-10 % per epoch; at B = 256 the 64-row GRU tiles read 154 KB of h per step per CU, bound by the per-CU
+// L2 / MALL rate, and the launch form stays 1 % faster (566.1 k vs 560.8 k fp32, 780.2 k vs 774.4 k bf16)
+#ifndef PSCAN_MAX_B
+#define PSCAN_MAX_B 128  // B = 256 (64-row GRU tiles, 32-row sampler tiles) builds: 560.8 k vs 566.1 k fp32 (r05r)
+#endif
 bool op_pscan_supported(const dr_dims* d, int B, int T, int A) {
   return !d->launch_form && d->hidden == HD && d->enc_hidden == EH && d->rows == NR && d->cols == NCL && A >= 1 &&
-         A <= 8 && T >= 2 && B >= 16 && B <= 128 && B % 16 == 0 && (B <= 64 || B % 32 == 0);
+         A <= 8 && T >= 2 && B >= 16 && B <= PSCAN_MAX_B && B % 16 == 0 && (B <= 64 || B % 32 == 0) &&
+         (B <= 128 || B % 64 == 0);
 }
 
 template <int NT, int MR, int MS>
@@ -636,7 +652,7 @@ int op_pscan(const dr_dims* d, const dr_world_model* wm, int B, int T, int A, co
     dr_set_error("pscan: unsupported shape (B=%d T=%d)", B, T);
     return DR_E_UNSUPPORTED;
   }
-  const int MR = B <= 64 ? 16 : 32, MS = 16;
+  const int MR = B <= 64 ? 16 : B <= 128 ? 32 : 64, MS = B <= 128 ? 16 : 32;
   const int grid = std::max(std::max((B / MR) * NUS, (B / 16) * NC2), (B / MS) * NR);
   // every workgroup must be resident: all CUs of an unmasked stream
   int dev = 0, cus = 0;
@@ -686,9 +702,9 @@ int op_pscan(const dr_dims* d, const dr_world_model* wm, int B, int T, int A, co
 #define PS_L(NT, MRv, MSv) \
   if (MR == MRv && MS == MSv) return launch_pscan<NT, MRv, MSv>(a, grid, s);
   if (bf) {
-    PS_L(1, 16, 16) PS_L(1, 32, 16)
+    PS_L(1, 16, 16) PS_L(1, 32, 16) PS_L(1, 64, 32)
   } else {
-    PS_L(3, 16, 16) PS_L(3, 32, 16)
+    PS_L(3, 16, 16) PS_L(3, 32, 16) PS_L(3, 64, 32)
   }
 #undef PS_L
   dr_set_error("pscan: no instance");
