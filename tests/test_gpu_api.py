@@ -137,9 +137,11 @@ def test_actor_act_batch1(widths, gpu):
     close(a2, torch.tanh(mu_ref + eps.view(1, 1, A) * sg_ref), 1e-4, 1e-6, "act sample")
 
 
-def test_dream_episodes_from_soft_latent(gpu):
-    """Dreamer.dream_episodes (Dreamer.py:143-175) from a non-one-hot z0."""
-    B, H = 4, 5
+@pytest.mark.parametrize("B", [4, 16])
+def test_dream_episodes_from_soft_latent(B, gpu):
+    """Dreamer.dream_episodes (Dreamer.py:143-175) from a non-one-hot z0 (B = 16:
+    the persistent unroll's dense-group path, dream.hip)."""
+    H = 5
     d, P = _dreamer(gpu, batch_size=B, horizon=H)
     g = torch.Generator().manual_seed(12)
     h0 = torch.randn(B, 1, HD, generator=g)
