@@ -1650,9 +1650,6 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tile_b16(GemmBatch gb, int spl
 // workgroups of a smaller problem idle in a blockIdx.z slice sized for the
 // largest: a grouped launch of the GRU hidden product (456 tiles) with a
 // 56-tile Linear ran 21.7 us against 12.3 for the product alone)
-#ifndef DR_WK_ACC2
-#define DR_WK_ACC2 0  // A/B knob: 1 = the two 16-k halves on separate accumulators (r04n: no gain)
-#endif
 template <int BM, int BN, int NW, int D, int KMAP = 0>
 __global__ __launch_bounds__(64 * NW) void k_gemm_wk(GemmBatch gb, int splits, int npack) {
   constexpr int NTH = 64 * NW, FM = BM / 16, FN = BN / 16, NT4 = FM * FN * 256;
@@ -1746,18 +1743,11 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wk(GemmBatch gb, int splits, i
       }
     }
   };
-  // NA = 2 (DR_WK_ACC2): the two 16-k halves of a block on separate
-  // accumulators, summed at the end -- twice the independent MFMA chains
-  // per wave (issue-stalled on MFMA read-after-write at four,
-  // profiles/r04a_pmc_sq_tcc_chain_kernels.txt)
-  constexpr int NA = DR_WK_ACC2 ? 2 : 1;
-  f32x4 acc[NA][FM][FN];
+  f32x4 acc[1][FM][FN];
 #pragma unroll
-  for (int a2 = 0; a2 < NA; ++a2)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[a2][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[0][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < D; ++u) load(min(b0 + u, blast), u);
   const int nbw = b1 - b0;
@@ -1777,29 +1767,16 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wk(GemmBatch gb, int splits, i
           for (int j = 0; j < FN; ++j) rb[u][j][h] = (f32x4){0.f, 0.f, 0.f, 0.f};
         }
       }
-      if constexpr (NA == 2) {  // the halves interleaved: 2 x FM x FN independent chains
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
-          for (int h = 0; h < 2; ++h)
+          for (int i = 0; i < FM; ++i)
 #pragma unroll
-            for (int i = 0; i < FM; ++i)
-#pragma unroll
-              for (int j = 0; j < FN; ++j)
-                acc[h][i][j] =
-                    __builtin_amdgcn_mfma_f32_16x16x4f32(ra[u][i][h][c], rb[u][j][h][c], acc[h][i][j], 0, 0, 0);
-      } else {
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-#pragma unroll
-            for (int i = 0; i < FM; ++i)
-#pragma unroll
-              for (int j = 0; j < FN; ++j)
-                acc[0][i][j] =
-                    __builtin_amdgcn_mfma_f32_16x16x4f32(ra[u][i][h][c], rb[u][j][h][c], acc[0][i][j], 0, 0, 0);
-      }
+            for (int j = 0; j < FN; ++j)
+              acc[0][i][j] =
+                  __builtin_amdgcn_mfma_f32_16x16x4f32(ra[u][i][h][c], rb[u][j][h][c], acc[0][i][j], 0, 0, 0);
       load(min(b + D, blast), u);  // unconditional: a load under a branch is waited for at once
     }
   }
@@ -1809,8 +1786,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wk(GemmBatch gb, int splits, i
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      f32x4 v = acc[0][i][j];
-      if constexpr (NA == 2) v = acc[0][i][j] + acc[1][i][j];
+      const f32x4 v = acc[0][i][j];
 #pragma unroll
       for (int e = 0; e < 4; ++e) red[wave][(i * FN + j) * 4 + e][lane] = v[e];
     }
@@ -1857,26 +1833,23 @@ __device__ __forceinline__ unsigned wk_pack_rne(float x0, float x1) {
   return __builtin_bit_cast(unsigned, v);
 }
 
-#ifndef DR_WKS3_ACC3
-#define DR_WKS3_ACC3 0  // A/B knob: 1 = per-order accumulators (r04n: 554.3k vs 558.2k off)
-#endif
 template <int NTP, int D, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) {
   constexpr bool FULL = false, APL = false;
-  constexpr int FM = 2, FN = 2, NTH = 64 * NW, NT4 = FM * FN * 256;
+  constexpr int FM = 2, FN = 2, BM = 16 * FM, NTH = 64 * NW, NT4 = FM * FN * 256;
   __shared__ GemmArgs s_args;
   __shared__ __attribute__((aligned(16))) float red[NW][FM * FN * 4][64];
   int z = 0;
-  const int plt = dr_pack_tile<32, 32>(gb, npack, z);
+  const int plt = dr_pack_tile<BM, 32>(gb, npack, z);
   if (plt == -1) return;
   dr_stage_args(gb.p[z], s_args, threadIdx.x);
   const GemmArgs& g = s_args;
   const int M = dr_uni(g.M), N = dr_uni(g.N), K = dr_uni(g.K);
-  const int tiles_m = (M + 31) / 32, tiles_n = (N + 31) / 32;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + 31) / 32;
   const int lt = plt >= 0 ? plt : dr_xcd_tile(blockIdx.x, tiles_m * tiles_n);
   if (lt < 0) return;
   const int tn = lt / tiles_m, tm = lt - tn * tiles_m;  // row tiles of one weight slice adjacent
-  const int m0 = tm * 32, n0 = tn * 32;
+  const int m0 = tm * BM, n0 = tn * 32;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
   const float* A = dr_uni(g.A);
   const int lda = dr_uni((int)g.lda);
@@ -1934,13 +1907,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) 
         rb[sl][p][j] = *(const DR_GLOBAL wk_u32x4*)((const DR_GLOBAL char*)wr + (e << 1));
       }
   };
-  // NA = 3 (DR_WKS3_ACC3, 3-term form): the products accumulate by order --
-  // acc[0] hi*hi, acc[1] the two 2^-8 cross terms, acc[2] the three 2^-16
-  // terms -- summed smallest first at the end: three independent MFMA chains
-  // per block instead of six dependent MFMAs in a row on one accumulator
-  // (the wave-K kernels were issue-stalled on MFMA read-after-write,
-  // profiles/r04a_pmc_sq_tcc_chain_kernels.txt)
-  constexpr int NA = (NTP == 3 && DR_WKS3_ACC3) ? 3 : 1;
+  constexpr int NA = 1;
   f32x4 acc[NA][FM][FN];
 #pragma unroll
   for (int a3 = 0; a3 < NA; ++a3)
@@ -1984,38 +1951,30 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) 
 #define DR_WK3(PA, PB, X)                        \
   _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[X][i][j] = \
       wk_mfma(rb[u][PB][j], a[PA][i], acc[X][i][j]);
-      if constexpr (NA == 3) {  // independent chains interleaved
-        DR_WK3(2 % NTP, 0, 2)
-        DR_WK3(1 % NTP, 0, 1)
-        DR_WK3(0, 0, 0)
-        DR_WK3(1 % NTP, 1 % NTP, 2)
-        DR_WK3(0, 1 % NTP, 1)
-        DR_WK3(0, 2 % NTP, 2)
-      } else {
-        if constexpr (NTP == 3) {
-          DR_WK3(2 % NTP, 0, 0)
-          DR_WK3(1 % NTP, 1 % NTP, 0)
-          DR_WK3(0, 2 % NTP, 0)
-          DR_WK3(1 % NTP, 0, 0)
-          DR_WK3(0, 1 % NTP, 0)
-        }
-        DR_WK3(0, 0, 0)
+      if constexpr (NTP == 3) {  // the six products of order >= 2^-16, smallest first
+        DR_WK3(2 % NTP, 0, 0)
+        DR_WK3(1 % NTP, 1 % NTP, 0)
+        DR_WK3(0, 2 % NTP, 0)
+        DR_WK3(1 % NTP, 0, 0)
+        DR_WK3(0, 1 % NTP, 0)
       }
+      DR_WK3(0, 0, 0)
 #undef DR_WK3
       // unconditional: a load under a branch is waited for at once
       if constexpr (!FULL) load(min(c + D, clast), u);
     }
   }
   // partial tiles meet in LDS; element (t, e, l) of tile t = (i, j): row 16 i + (l & 15), column 16 j + 4 (l >> 4) + e
+  {
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      f32x4 v = acc[0][i][j];
-      if constexpr (NA == 3) v = acc[2][i][j] + acc[1][i][j] + acc[0][i][j];
+      for (int j = 0; j < FN; ++j) {
+        const f32x4 v = acc[0][i][j];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) red[wave][(i * FN + j) * 4 + e][lane] = v[e];
-    }
+        for (int e = 0; e < 4; ++e) red[wave][(i * FN + j) * 4 + e][lane] = v[e];
+      }
+  }
   __syncthreads();
 #pragma unroll
   for (int ii = 0; ii < NEPI; ++ii) {
@@ -2579,6 +2538,8 @@ static bool wks3_ok(const GemmBatch& gb, int count) {
 // 4 waves per 32 x 32 tile, each over its own run of k-chunks, a 2-deep
 // register ring (r04g: 8 waves, whole-wave prefetch and A planes measured
 // slower, profiles/r04g_ab_wks3.txt, r04t_ab_aplanes.txt)
+// (r05w: 64-row tiles, each weight plane read by half as many row tiles,
+// measured slower -- 548 k vs 566 k fp32, 776 k vs 803 k bf16 at B = 256)
 static void launch_wks3(const GemmBatch& gb, int count, hipStream_t s, bool bf16) {
   int tot = 0, maxt = 0;
   for (int i = 0; i < count; ++i) {
