@@ -182,3 +182,21 @@ bool op_gemm_tn_split3_supported(int M, int N, int K);
 int op_gemm_tn_split3(int M, int N, int K, const float* G, long long ldg, const float* X, long long ldx,
                       const float* X2, long long ldx2, int nsplitB, float* Y, long long ldy, int accumulate, void* ws,
                       size_t ws_bytes, hipStream_t s, int terms = 3);  // terms = 1: RNE bf16 operands (bf16 WM step)
+// up to 4 such problems in one launch per pass (repack / products / finish),
+// each with its own scratch carved in order from `ws`; bitwise equal to
+// running them one after another
+struct TnProblem {
+  int M, N, K;
+  const float* G;
+  long long ldg;
+  const float* X;
+  long long ldx;
+  const float* X2;
+  long long ldx2;
+  int nsplitB;
+  float* Y;
+  long long ldy;
+  int accumulate;
+};
+size_t op_gemm_tn_split3_multi_ws_bytes(const TnProblem* p, int n);
+int op_gemm_tn_split3_multi(const TnProblem* p, int n, void* ws, size_t ws_bytes, hipStream_t s, int terms);

@@ -1709,6 +1709,7 @@ struct KnRepack {
   const float* X2;
   long long ldx, ldx2;
   u16* wr;
+  long long pad_;  // 16-byte multiple (staged in LDS)
 };
 
 template <int TERMS>
@@ -1765,31 +1766,50 @@ __device__ __forceinline__ void kn_repack_body(int K, int N, int P, const float*
   }
 }
 
-// both operands of a TN product in one launch (blockIdx.z): the world-model
-// step's ~15 weight-gradient products per step are small enough that the
-// second launch was a visible share of each
-template <int TERMS>
-__global__ __launch_bounds__(256) void k_kn_repack2_split3(KnRepack a, KnRepack b) {
-  // (field-wise selects: a select of the whole by-value struct can be
-  // materialised in scratch)
-  const bool z = blockIdx.z != 0;
-  const int P = z ? b.P : a.P;
-  if ((int)blockIdx.x * 256 >= P) return;
-  kn_repack_body<TERMS>(z ? b.K : a.K, z ? b.N : a.N, P, z ? b.X : a.X, z ? b.ldx : a.ldx, z ? b.X2 : a.X2,
-                        z ? b.ldx2 : a.ldx2, z ? b.nsplit : a.nsplit, z ? b.wr : a.wr);
-}
-
 struct GemmPP {
-  int M, N, K, Mp, Np, splits, accumulate;
+  int M, N, K, Mp, Np, splits, accumulate, tiles;  // tiles: output tiles of the launch's BM x BN shape
   long long ldy;
   const u16* wa;  // planes of the A side (rows m), [K/32][3][Mp][32]
   const u16* wb;  // planes of the B side (rows n), [K/32][3][Np][32]
   float* Y;
   float* part;    // splits > 1: [splits][M][N] partial sums
+  long long pad_;  // 16-byte multiple (staged in LDS)
 };
 
+// up to DR_TN_MAX weight-gradient problems of one backward stage in one
+// launch per pass (repack, products, split-K finish): the actor's four and
+// the critic's three were 12 / 9 dependent launches of a few us each.  Every
+// problem keeps its own planes, splits and summation order, so the grouped
+// launch is bitwise the one-at-a-time sequence.
+#define DR_TN_MAX 4
+struct TnBatch {
+  KnRepack r[2 * DR_TN_MAX];  // repack operands (G of problem i at 2 i, X at 2 i + 1)
+  GemmPP g[DR_TN_MAX];
+  int blk0[DR_TN_MAX + 1];    // first flat product block of problem i (tiles * splits each); [n..] = total
+  int fin0[DR_TN_MAX + 1];    // first finish block of problem i (0 blocks when splits == 1); [n..] = total
+  int n, nrep, pad_[2];
+};
+
+template <int TERMS>
+__global__ __launch_bounds__(256) void k_kn_repack_multi(TnBatch b) {
+  __shared__ __attribute__((aligned(16))) KnRepack s;
+  dr_stage_args(b.r[blockIdx.z], s, threadIdx.x);
+  const int P = dr_uni(s.P), K = dr_uni(s.K);
+  if ((int)blockIdx.x * 256 >= P || (int)blockIdx.y * 32 >= K) return;
+  kn_repack_body<TERMS>(K, dr_uni(s.N), P, dr_uni(s.X), s.ldx, dr_uni(s.X2), s.ldx2, dr_uni(s.nsplit), dr_uni(s.wr));
+}
+
+// the flat block list: problem z (uniform), then split and tile within it
+__device__ __forceinline__ int tn_find(const int* blk0, int flat) {
+  int z = 0;
+#pragma unroll
+  for (int i = 1; i < DR_TN_MAX; ++i)
+    if (flat >= blk0[i]) z = i;
+  return z;
+}
+
 template <int BM, int BN, int TERMS = 3>
-__global__ __launch_bounds__(BM * 2) void k_gemm_pp_split3(GemmPP g) {
+__global__ __launch_bounds__(BM * 2) void k_gemm_pp_multi(TnBatch b) {
   constexpr int NT = BM * 2;
   constexpr int WTN = BN / 2, FM = 4, FN = WTN / 16;
   constexpr int AU = TERMS * BM * 4, BU = TERMS * BN * 4;
@@ -1797,16 +1817,23 @@ __global__ __launch_bounds__(BM * 2) void k_gemm_pp_split3(GemmPP g) {
   static_assert(FN >= 1 && BM % 64 == 0 && (TERMS == 1 || TERMS == 3), "gemm_pp tile");
   __shared__ __attribute__((aligned(16))) u32x4 As[2][TERMS][BM][4];
   __shared__ __attribute__((aligned(16))) u32x4 Bs[2][TERMS][BN][4];
-  const int M = g.M, N = g.N, Mp = g.Mp, Np = g.Np;
+  __shared__ __attribute__((aligned(16))) GemmPP s_g;
+  const int flat = dr_xcd_tile(blockIdx.x, b.blk0[DR_TN_MAX]);
+  if (flat < 0) return;
+  const int z = tn_find(b.blk0, flat);
+  dr_stage_args(b.g[z], s_g, threadIdx.x);
+  const int M = dr_uni(s_g.M), N = dr_uni(s_g.N), Mp = dr_uni(s_g.Mp), Np = dr_uni(s_g.Np);
+  const int tiles = dr_uni(s_g.tiles), splits = dr_uni(s_g.splits);
+  const int local = flat - b.blk0[z];
+  const int split = local / tiles, lt = local - split * tiles;
   const int tiles_n = (N + BN - 1) / BN;
-  const int tiles = ((M + BM - 1) / BM) * tiles_n;
-  const int lt = dr_xcd_tile(blockIdx.x, tiles);
-  if (lt < 0) return;
   const int m0 = (lt / tiles_n) * BM, n0 = (lt % tiles_n) * BN;
+  const DR_GLOBAL u16* wa = dr_g(dr_uni(s_g.wa));
+  const DR_GLOBAL u16* wb = dr_g(dr_uni(s_g.wb));
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
-  const int NCH = (g.K + 31) / 32;
-  const int per = (NCH + g.splits - 1) / g.splits;
-  const int c0 = min(NCH, (int)blockIdx.y * per), c1 = min(NCH, c0 + per);
+  const int NCH = (dr_uni(s_g.K) + 31) / 32;
+  const int per = (NCH + splits - 1) / splits;
+  const int c0 = min(NCH, split * per), c1 = min(NCH, c0 + per);
   u32x4 ra0[APT], ra1[APT], rb0[BPT], rb1[BPT];
   auto load = [&](int c, auto slot) __attribute__((always_inline)) {
     u32x4* ra = decltype(slot)::value == 0 ? ra0 : ra1;
@@ -1816,7 +1843,7 @@ __global__ __launch_bounds__(BM * 2) void k_gemm_pp_split3(GemmPP g) {
       const int e = tid + NT * j;
       if (AU % NT == 0 || e < AU) {
         const int pl = e / (BM * 4), rm = e - pl * BM * 4, row = rm >> 2, u = rm & 3;
-        ra[j] = *reinterpret_cast<const u32x4*>(g.wa + (((long long)c * 3 + pl) * Mp + m0 + row) * 32 + 8 * u);
+        ra[j] = *reinterpret_cast<const DR_GLOBAL u32x4*>(wa + (((long long)c * 3 + pl) * Mp + m0 + row) * 32 + 8 * u);
       }
     }
 #pragma unroll
@@ -1824,7 +1851,7 @@ __global__ __launch_bounds__(BM * 2) void k_gemm_pp_split3(GemmPP g) {
       const int e = tid + NT * j;
       if (BU % NT == 0 || e < BU) {
         const int pl = e / (BN * 4), rm = e - pl * BN * 4, row = rm >> 2, u = rm & 3;
-        rb[j] = *reinterpret_cast<const u32x4*>(g.wb + (((long long)c * 3 + pl) * Np + n0 + row) * 32 + 8 * u);
+        rb[j] = *reinterpret_cast<const DR_GLOBAL u32x4*>(wb + (((long long)c * 3 + pl) * Np + n0 + row) * 32 + 8 * u);
       }
     }
   };
@@ -1898,6 +1925,10 @@ __global__ __launch_bounds__(BM * 2) void k_gemm_pp_split3(GemmPP g) {
     if (c < c1) step(c, S0{});
   }
   // lane (r, q) of acc[i][j]: row m0 + wm0 + 16 i + r, columns n0 + wn0 + 16 j + 4 q .. + 3
+  DR_GLOBAL float* part = dr_g(dr_uni(s_g.part));
+  DR_GLOBAL float* Y = dr_g(dr_uni(s_g.Y));
+  const long long ldy = s_g.ldy;
+  const bool accum = dr_uni(s_g.accumulate) != 0;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int m = m0 + wm0 + 16 * i + r;
@@ -1908,25 +1939,33 @@ __global__ __launch_bounds__(BM * 2) void k_gemm_pp_split3(GemmPP g) {
       for (int e = 0; e < 4; ++e) {
         const int n = n0 + wn0 + 16 * j + 4 * q + e;
         if (n >= N) continue;
-        if (g.splits > 1) {
-          g.part[((long long)blockIdx.y * M + m) * N + n] = acc[i][j][e];
+        if (splits > 1) {
+          part[((long long)split * M + m) * N + n] = acc[i][j][e];
         } else {
-          float* y = g.Y + (long long)m * g.ldy + n;
-          *y = g.accumulate ? *y + acc[i][j][e] : acc[i][j][e];
+          DR_GLOBAL float* y = Y + (long long)m * ldy + n;
+          *y = accum ? *y + acc[i][j][e] : acc[i][j][e];
         }
       }
     }
   }
 }
 
-__global__ void k_pp_finish(GemmPP g) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)g.M * g.N) return;
-  const int m = (int)(i / g.N), n = (int)(i - (long long)m * g.N);
+// Y (+)= the fixed-order sum of the split-K partials; block -> problem by fin0
+__global__ __launch_bounds__(256) void k_pp_finish_multi(TnBatch b) {
+  __shared__ __attribute__((aligned(16))) GemmPP s_g;
+  const int blk = blockIdx.x;
+  if (blk >= b.fin0[DR_TN_MAX]) return;
+  const int z = tn_find(b.fin0, blk);
+  dr_stage_args(b.g[z], s_g, threadIdx.x);
+  const int M = dr_uni(s_g.M), N = dr_uni(s_g.N), splits = dr_uni(s_g.splits);
+  const long long i = (long long)(blk - b.fin0[z]) * 256 + threadIdx.x;
+  if (i >= (long long)M * N) return;
+  const DR_GLOBAL float* part = dr_g(dr_uni(s_g.part));
+  const int m = (int)(i / N), n = (int)(i - (long long)m * N);
   float v = 0.f;
-  for (int sp = 0; sp < g.splits; ++sp) v += g.part[(long long)sp * g.M * g.N + i];
-  float* y = g.Y + (long long)m * g.ldy + n;
-  *y = g.accumulate ? *y + v : v;
+  for (int sp = 0; sp < splits; ++sp) v += part[(long long)sp * M * N + i];
+  DR_GLOBAL float* y = dr_g(dr_uni(s_g.Y)) + (long long)m * s_g.ldy + n;
+  *y = dr_uni(s_g.accumulate) ? *y + v : v;
 }
 
 #define DR_PP_SPLITS 8
@@ -1946,47 +1985,97 @@ bool op_gemm_tn_split3_supported(int M, int N, int K) {
 // host-side probe of the predicate (tests/test_host.py; not part of include/dreamer_hip.h)
 extern "C" int dr_internal_tn_split3_supported(int M, int N, int K) { return op_gemm_tn_split3_supported(M, N, K); }
 
+size_t op_gemm_tn_split3_multi_ws_bytes(const TnProblem* p, int n) {
+  size_t t = 0;
+  for (int i = 0; i < n; ++i) t += op_gemm_tn_split3_ws_bytes(p[i].M, p[i].N, p[i].K);
+  return t;
+}
+
+int op_gemm_tn_split3_multi(const TnProblem* p, int n, void* ws, size_t ws_bytes, hipStream_t s, int terms) {
+  if (n < 1 || n > DR_TN_MAX || (terms != 1 && terms != 3) || op_gemm_tn_split3_multi_ws_bytes(p, n) > ws_bytes) {
+    dr_set_error("gemm_tn_split3: %d problems, terms %d, or workspace too small", n, terms);
+    return DR_E_INVALID;
+  }
+  for (int i = 0; i < n; ++i) {
+    const TnProblem& q = p[i];
+    if (!op_gemm_tn_split3_supported(q.M, q.N, q.K) || !q.G || !q.X || !q.Y || (q.nsplitB < q.N && !q.X2)) {
+      dr_set_error("gemm_tn_split3: unsupported problem (M=%d N=%d K=%d)", q.M, q.N, q.K);
+      return DR_E_INVALID;
+    }
+  }
+  TnBatch b = {};
+  b.n = n;
+  b.nrep = 2 * n;
+  bool big[DR_TN_MAX];
+  int pmax = 0, kcmax = 0;
+  char* cur = reinterpret_cast<char*>(ws);
+  for (int i = 0; i < n; ++i) {
+    const TnProblem& q = p[i];
+    const int KC = (q.K + 31) / 32, Mp = s3_pad(q.M), Np = s3_pad(q.N);
+    u16* wa = reinterpret_cast<u16*>(cur);
+    u16* wb = wa + (size_t)KC * 32 * 3 * Mp;
+    float* part = reinterpret_cast<float*>(((uintptr_t)(wb + (size_t)KC * 32 * 3 * Np) + 255) & ~(uintptr_t)255);
+    cur += op_gemm_tn_split3_ws_bytes(q.M, q.N, q.K);
+    const int nsB = q.nsplitB < q.N ? q.nsplitB : q.N;
+    b.r[2 * i] = {q.K, q.M, Mp, q.M, q.G, q.G, q.ldg, q.ldg, wa, 0};
+    b.r[2 * i + 1] = {q.K, q.N, Np, nsB, q.X, q.X2 ? q.X2 : q.X, q.ldx, q.X2 ? q.ldx2 : q.ldx, wb, 0};
+    pmax = std::max(pmax, std::max(Mp, Np));
+    kcmax = std::max(kcmax, KC);
+    auto tl = [&](int bm, int bn) { return ((q.M + bm - 1) / bm) * ((q.N + bn - 1) / bn); };
+    big[i] = tl(128, 64) >= 512;
+    const int tiles = big[i] ? tl(128, 64) : tl(64, 64);
+    // split K while the grid is under two workgroups per CU, >= 8 chunks per split
+    int splits = 1;
+    while (splits < DR_PP_SPLITS && tiles * splits < 512 && KC / (2 * splits) >= 8) splits *= 2;
+    b.g[i] = {q.M, q.N, q.K, Mp, Np, splits, q.accumulate, tiles, q.ldy, wa, wb, q.Y, part, 0};
+  }
+  const dim3 rgrid((unsigned)((pmax + 255) / 256), (unsigned)kcmax, (unsigned)(2 * n));
+  if (terms == 1)
+    hipLaunchKernelGGL(k_kn_repack_multi<1>, rgrid, dim3(256), 0, s, b);
+  else
+    hipLaunchKernelGGL(k_kn_repack_multi<3>, rgrid, dim3(256), 0, s, b);
+  DR_TRY(dr_check_launch("kn_repack_multi"));
+  // products: one launch per tile shape present (problems of the other shape
+  // get no blocks: their blk0 run is empty)
+  for (int shape = 0; shape < 2; ++shape) {
+    const bool want_big = shape == 1;
+    TnBatch c = b;
+    int tot = 0, any = 0;
+    for (int i = 0; i < DR_TN_MAX; ++i) {
+      c.blk0[i] = tot;
+      if (i < n && big[i] == want_big) {
+        tot += b.g[i].tiles * b.g[i].splits;
+        any = 1;
+      }
+    }
+    c.blk0[DR_TN_MAX] = tot;
+    if (!any) continue;
+    const dim3 grid((unsigned)dr_xcd_grid(tot));
+    if (want_big) {
+      if (terms == 1) hipLaunchKernelGGL((k_gemm_pp_multi<128, 64, 1>), grid, dim3(256), 0, s, c);
+      else hipLaunchKernelGGL((k_gemm_pp_multi<128, 64, 3>), grid, dim3(256), 0, s, c);
+    } else {
+      if (terms == 1) hipLaunchKernelGGL((k_gemm_pp_multi<64, 64, 1>), grid, dim3(128), 0, s, c);
+      else hipLaunchKernelGGL((k_gemm_pp_multi<64, 64, 3>), grid, dim3(128), 0, s, c);
+    }
+    DR_TRY(dr_check_launch("gemm_pp_multi"));
+  }
+  int fb = 0;
+  for (int i = 0; i < DR_TN_MAX; ++i) {
+    b.fin0[i] = fb;
+    if (i < n && b.g[i].splits > 1) fb += (int)(((long long)b.g[i].M * b.g[i].N + 255) / 256);
+  }
+  b.fin0[DR_TN_MAX] = fb;
+  if (fb > 0) {
+    hipLaunchKernelGGL(k_pp_finish_multi, dim3((unsigned)fb), dim3(256), 0, s, b);
+    DR_TRY(dr_check_launch("pp_finish_multi"));
+  }
+  return DR_OK;
+}
+
 int op_gemm_tn_split3(int M, int N, int K, const float* G, long long ldg, const float* X, long long ldx,
                       const float* X2, long long ldx2, int nsplitB, float* Y, long long ldy, int accumulate, void* ws,
                       size_t ws_bytes, hipStream_t s, int terms) {
-  if (!op_gemm_tn_split3_supported(M, N, K) || !G || !X || !Y || (nsplitB < N && !X2) || (terms != 1 && terms != 3) ||
-      ws_bytes < op_gemm_tn_split3_ws_bytes(M, N, K)) {
-    dr_set_error("gemm_tn_split3: unsupported problem (M=%d N=%d K=%d) or workspace too small", M, N, K);
-    return DR_E_INVALID;
-  }
-  const int KC = (K + 31) / 32, Mp = s3_pad(M), Np = s3_pad(N);
-  u16* wa = reinterpret_cast<u16*>(ws);
-  u16* wb = wa + (size_t)KC * 32 * 3 * Mp;
-  float* part = reinterpret_cast<float*>(((uintptr_t)(wb + (size_t)KC * 32 * 3 * Np) + 255) & ~(uintptr_t)255);
-  const KnRepack ra = {K, M, Mp, M, G, G, ldg, ldg, wa};
-  const KnRepack rb = {K, N, Np, nsplitB < N ? nsplitB : N, X, X2 ? X2 : X, ldx, X2 ? ldx2 : ldx, wb};
-  const dim3 rgrid((unsigned)((std::max(Mp, Np) + 255) / 256), (unsigned)KC, 2);
-  if (terms == 1)
-    hipLaunchKernelGGL(k_kn_repack2_split3<1>, rgrid, dim3(256), 0, s, ra, rb);
-  else
-    hipLaunchKernelGGL(k_kn_repack2_split3<3>, rgrid, dim3(256), 0, s, ra, rb);
-  DR_TRY(dr_check_launch("kn_repack_split3"));
-  auto tl = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-  const bool big = tl(128, 64) >= 512;
-  const int tiles = big ? tl(128, 64) : tl(64, 64);
-  // split K while the grid is under two workgroups per CU, >= 8 chunks per split
-  int splits = 1;
-  while (splits < DR_PP_SPLITS && tiles * splits < 512 && KC / (2 * splits) >= 8) splits *= 2;
-  GemmPP g = {M, N, K, Mp, Np, splits, accumulate, ldy, wa, wb, Y, part};
-  if (terms == 1) {
-    if (big)
-      hipLaunchKernelGGL((k_gemm_pp_split3<128, 64, 1>), dim3(dr_xcd_grid(tiles), splits), dim3(256), 0, s, g);
-    else
-      hipLaunchKernelGGL((k_gemm_pp_split3<64, 64, 1>), dim3(dr_xcd_grid(tiles), splits), dim3(128), 0, s, g);
-  } else if (big) {
-    hipLaunchKernelGGL((k_gemm_pp_split3<128, 64>), dim3(dr_xcd_grid(tiles), splits), dim3(256), 0, s, g);
-  } else {
-    hipLaunchKernelGGL((k_gemm_pp_split3<64, 64>), dim3(dr_xcd_grid(tiles), splits), dim3(128), 0, s, g);
-  }
-  DR_TRY(dr_check_launch("gemm_pp_split3"));
-  if (splits > 1) {
-    hipLaunchKernelGGL(k_pp_finish, dim3((unsigned)(((long long)M * N + 255) / 256)), dim3(256), 0, s, g);
-    DR_TRY(dr_check_launch("pp_finish"));
-  }
-  return DR_OK;
+  const TnProblem q = {M, N, K, G, ldg, X, ldx, X2, ldx2, nsplitB, Y, ldy, accumulate};
+  return op_gemm_tn_split3_multi(&q, 1, ws, ws_bytes, s, terms);
 }

@@ -966,9 +966,8 @@ int op_pdream(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, in
   a.zg = reinterpret_cast<unsigned long long*>(a.hA + (size_t)H * B * MW);
   a.cnt = reinterpret_cast<unsigned*>(a.zg + (size_t)(H + 1) * B * NR);
   a.ts = reinterpret_cast<long long*>(reinterpret_cast<char*>(a.cnt) + PDREAM_CNT_BYTES);
-  // counters and granule tags zeroed by a kernel before every launch
-  DR_TRY(op_fill((long long)2 * (H + 1) * B * NR, reinterpret_cast<float*>(a.zg), 0.f, s));
-  DR_TRY(op_fill(PDREAM_CNT_BYTES / 4, reinterpret_cast<float*>(a.cnt), 0.f, s));
+  // granule tags and counters (adjacent) zeroed by one kernel before every launch
+  DR_TRY(op_fill((long long)2 * (H + 1) * B * NR + PDREAM_CNT_BYTES / 4, reinterpret_cast<float*>(a.zg), 0.f, s));
   const bool bf = d->precision == DR_PREC_BF16;
   if (MR == 16) return bf ? launch_pdream<1, 16>(a, grid, s) : launch_pdream<3, 16>(a, grid, s);
   return bf ? launch_pdream<1, 32>(a, grid, s) : launch_pdream<3, 32>(a, grid, s);

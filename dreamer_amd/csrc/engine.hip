@@ -428,7 +428,7 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.thead = c.f((long long)2 * A * d->actor_h2);
   w.tl3a = c.f((long long)d->actor_h2 * d->actor_h1);
   w.tl0a = c.f((long long)d->actor_h1 * (Hd + L));
-  w.gH = c.f(B1 * Hd);
+  w.gH = c.f(B1 * Hd);  // gH | gZ | gA back to back: zeroed by one fill
   w.gZ = c.f(B1 * L);
   w.gA = c.f(BH * A);
   w.glog = c.f(Bl * L);
@@ -453,9 +453,10 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
            2 * splitk_floats(A, d->actor_h2);
   w.sk = c.f(w.sk_n);
   const int BHi = (int)BH;
-  w.tn_bytes = std::max(std::max(op_gemm_tn_split3_ws_bytes(d->actor_h1, Hd + L, BHi),
-                                 op_gemm_tn_split3_ws_bytes(d->actor_h2, d->actor_h1, BHi)),
-                        op_gemm_tn_split3_ws_bytes(A, d->actor_h2, BHi));
+  // the four weight-gradient problems side by side (one grouped launch)
+  w.tn_bytes = op_gemm_tn_split3_ws_bytes(d->actor_h1, Hd + L, BHi) +
+               op_gemm_tn_split3_ws_bytes(d->actor_h2, d->actor_h1, BHi) +
+               2 * op_gemm_tn_split3_ws_bytes(A, d->actor_h2, BHi);
   w.tn = c.raw(w.tn_bytes);
   w.pd = c.raw(op_pdream_ws_bytes(d, B, H));
   w.pb = c.raw(op_pbptt_ws_bytes(d, B, H));
@@ -729,12 +730,17 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
   const bool upstream_state = g_latents || g_hiddens;
   if (do_prep) {
   // upstream gradients
-  if (g_hiddens) DR_TRY(copy2d(w.gH, Hd, g_hiddens, Hd, Hd, (long long)B * (H + 1), s));
-  else DR_TRY(zero(w.gH, (long long)B * (H + 1) * Hd, s));
-  if (g_latents) DR_TRY(copy2d(w.gZ, L, g_latents, L, L, (long long)B * (H + 1), s));
-  else DR_TRY(zero(w.gZ, (long long)B * (H + 1) * L, s));
-  if (g_actions) DR_TRY(copy2d(w.gA, A, g_actions, A, A, (long long)BH, s));
-  else DR_TRY(zero(w.gA, (long long)BH * A, s));
+  if (!g_hiddens && !g_latents && !g_actions) {
+    // gH | gZ | gA are carved back to back: one fill (train_Agent's case)
+    DR_TRY(zero(w.gH, (long long)((w.gA + (long long)BH * A) - w.gH), s));
+  } else {
+    if (g_hiddens) DR_TRY(copy2d(w.gH, Hd, g_hiddens, Hd, Hd, (long long)B * (H + 1), s));
+    else DR_TRY(zero(w.gH, (long long)B * (H + 1) * Hd, s));
+    if (g_latents) DR_TRY(copy2d(w.gZ, L, g_latents, L, L, (long long)B * (H + 1), s));
+    else DR_TRY(zero(w.gZ, (long long)B * (H + 1) * L, s));
+    if (g_actions) DR_TRY(copy2d(w.gA, A, g_actions, A, A, (long long)BH, s));
+    else DR_TRY(zero(w.gA, (long long)BH * A, s));
+  }
   {
     // weights are constant over the backward: transpose them once (one launch)
     // so every input-gradient GEMM below runs NT with 16-byte weight loads
@@ -976,9 +982,10 @@ struct CBws {
 };
 static void cbws_carve(Carve& c, const dr_dims* d, int B, int H, CBws& w) {
   const long long M = (long long)B * (H + 1);
-  w.tn_bytes = std::max(std::max(op_gemm_tn_split3_ws_bytes(d->buckets, d->critic_h2, (int)M),
-                                 op_gemm_tn_split3_ws_bytes(d->critic_h2, d->critic_h1, (int)M)),
-                        op_gemm_tn_split3_ws_bytes(d->critic_h1, d->hidden + latent(d), (int)M));
+  // the three weight-gradient problems side by side (one grouped launch)
+  w.tn_bytes = op_gemm_tn_split3_ws_bytes(d->buckets, d->critic_h2, (int)M) +
+               op_gemm_tn_split3_ws_bytes(d->critic_h2, d->critic_h1, (int)M) +
+               op_gemm_tn_split3_ws_bytes(d->critic_h1, d->hidden + latent(d), (int)M);
   w.tn = c.raw(w.tn_bytes);
   w.row_loss = c.f((long long)B * H);
   w.sk_n = splitk_floats(d->buckets, d->critic_h2) + splitk_floats(d->critic_h2, d->critic_h1) +

@@ -175,21 +175,34 @@ static inline GemmArgs bwd_w(int out, int in, int R, const float* G, long long l
   return g;
 }
 
-// weight-gradient (TN) problems built by bwd_w: on the split3 bf16 MFMA
-// (op_gemm_tn_split3, one problem after another through the same scratch)
-// when `ws` holds every problem's planes, else one grouped f32 tile launch
+// weight-gradient (TN) problems built by bwd_w: on the split3 bf16 MFMA,
+// up to 4 problems per grouped launch (op_gemm_tn_split3_multi) when `ws`
+// holds all their planes, else one problem after another through the same
+// scratch; the f32 tile GEMM when a problem does not fit the split3 path
 static inline bool tn_split3_ok(const GemmArgs& g) {
   return g.alpha == 1.0f && !g.act && !g.bias && !g.addend && g.ksplitB >= g.K && g.nsplitY >= g.N && !g.out_conv &&
          g.ksplitA >= g.K && g.epi == EPI_NONE && op_gemm_tn_split3_supported(g.M, g.N, g.K);
 }
+static inline TnProblem tn_problem(const GemmArgs& g) {
+  return {g.M, g.N, g.K, g.A, g.lda, g.W, g.ldb, g.W2, g.ldb2, g.nsplitB < g.N ? g.nsplitB : g.N, g.Y, g.ldy,
+          g.accumulate};
+}
+// scratch for n grouped problems of at most this size each
+static inline size_t tn_group_bytes(size_t one, int n) { return one * (size_t)(n < 4 ? n : 4); }
 static inline int tn_launch(const GemmArgs* p, int n, void* ws, size_t ws_bytes, hipStream_t s, int terms = 3) {
   bool ok = ws != nullptr;
   for (int i = 0; i < n && ok; ++i) ok = tn_split3_ok(p[i]) && op_gemm_tn_split3_ws_bytes(p[i].M, p[i].N, p[i].K) <= ws_bytes;
   if (!ok) return gemm_launch(G_TN, AM_PLAIN, p, n, s);
-  for (int i = 0; i < n; ++i) {
-    const GemmArgs& g = p[i];
-    DR_TRY(op_gemm_tn_split3(g.M, g.N, g.K, g.A, g.lda, g.W, g.ldb, g.W2, g.ldb2, g.nsplitB < g.N ? g.nsplitB : g.N,
-                             g.Y, g.ldy, g.accumulate, ws, ws_bytes, s, terms));
+  for (int i0 = 0; i0 < n;) {
+    TnProblem q[4];
+    int k = 0;
+    while (i0 + k < n && k < 4) {
+      q[k] = tn_problem(p[i0 + k]);
+      if (k > 0 && op_gemm_tn_split3_multi_ws_bytes(q, k + 1) > ws_bytes) break;
+      ++k;
+    }
+    DR_TRY(op_gemm_tn_split3_multi(q, k, ws, ws_bytes, s, terms));
+    i0 += k;
   }
   return DR_OK;
 }

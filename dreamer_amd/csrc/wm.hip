@@ -524,7 +524,8 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
     w.sk = c.f(w.sk_n);
   }
   {
-    // split3 TN scratch: the largest weight-gradient problem over K = M rows
+    // split3 TN scratch: room for four of the largest weight-gradient problem
+    // over K = M rows (tn_launch groups up to four per launch)
     const int hd = D.Hd, L = D.L, eh = D.eh;
     const int mn[][2] = {{D.nb, D.rh2}, {D.rh2, D.rh1}, {D.rh1, hd + L}, {1, D.ch2}, {D.ch2, D.ch1}, {D.ch1, hd + L},
                          {L, D.ph2}, {D.ph2, D.ph1}, {D.ph1, hd + L}, {D.Fd, D.dh}, {D.dh, hd + L}, {L, eh},
@@ -533,8 +534,8 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
     size_t mx = 0;
     for (const auto& q : mn)
       if (q[0] > 0 && q[1] > 0) mx = std::max(mx, op_gemm_tn_split3_ws_bytes(q[0], q[1], M));
-    w.tn_bytes = mx;
-    w.tn = c.raw(mx);
+    w.tn_bytes = tn_group_bytes(mx, 4);
+    w.tn = c.raw(w.tn_bytes);
   }
 }
 
