@@ -123,6 +123,9 @@ _SIGS = {
     "dr_clip_stats": (_i, [_ll, fp, _ll, fp, _i, fp, fp, fp, fp, fp]),
     "dr_adamw": (_i, [_ll, fp, fp, fp, fp, fp, _f, _d, _d, _d, _d, _d, fp, fp, fp, fp]),
     "dr_ema": (_i, [_ll, fp, fp, _f, _f, fp, fp]),
+    "dr_ac_optimiser_step": (_i, [_ll, fp, fp, fp, fp, fp, fp, _d, _d, _d, _d, _d,
+                                  _ll, fp, fp, fp, fp, fp, fp, _d, _d, _d, _d, _d,
+                                  _f, fp, _f, _f, _i, fp, fp, fp, fp, fp]),
     "dr_nonfinite": (_i, [_ll, fp, fp, fp]),
     "dr_replay_gather": (_i, [_ll, _i, _i, _i, _i, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp]),
     "dr_rng_advance": (_i, [fp, C.c_ulonglong, fp]),

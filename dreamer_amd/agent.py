@@ -289,11 +289,20 @@ class Agent(nn.Module):
         st = hip.stream()
         if getattr(self, "_clip_scratch", None) is None or self._clip_scratch.device != sq.device:
             self._clip_scratch = torch.zeros(1024, device=sq.device)  # DR_CLIP_SCRATCH_FLOATS
-        L.call("dr_clip_stats", self.fa.numel, self.fa.grad.data_ptr(), self.fc.numel, self.fc.grad.data_ptr(), 2,
-               self.loss_buffer.data_ptr(), sq.data_ptr(), skip.data_ptr(), self._clip_scratch.data_ptr(), st)
-        self.critic_optimiser.fused_step(sq[1:2], 100.0, skip)
-        self.actor_optimiser.fused_step(sq[0:1], 100.0, skip)
-        self.soft_update_target(skip=skip)
+        # critic / actor AdamW (clip by sq[1] / sq[0]) and the target EMA
+        # (tau = 0.02, Agent.py:90-94) in one more launch: dr_ac_optimiser_step
+        # = dr_clip_stats + dr_adamw x2 + dr_ema, the same bits
+        ca, oa, tau = self.critic_optimiser, self.actor_optimiser, 0.02
+        ga, gc = oa.param_groups[0], ca.param_groups[0]
+        L.call("dr_ac_optimiser_step",
+               self.fa.numel, self.fa.flat.data_ptr(), self.fa.grad.data_ptr(), oa.exp_avg.data_ptr(),
+               oa.exp_avg_sq.data_ptr(), oa.step_dev.data_ptr(), oa.hyper.data_ptr(), ga["lr"], ga["betas"][0],
+               ga["betas"][1], ga["eps"], ga["weight_decay"],
+               self.fc.numel, self.fc.flat.data_ptr(), self.fc.grad.data_ptr(), ca.exp_avg.data_ptr(),
+               ca.exp_avg_sq.data_ptr(), ca.step_dev.data_ptr(), ca.hyper.data_ptr(), gc["lr"], gc["betas"][0],
+               gc["betas"][1], gc["eps"], gc["weight_decay"],
+               100.0, self.ft.flat.data_ptr(), float(1.0 - tau), float(tau), 2, self.loss_buffer.data_ptr(),
+               sq.data_ptr(), skip.data_ptr(), self._clip_scratch.data_ptr(), st)
 
     def soft_update_target(self, tau=0.02, skip=None):  # Agent.py:90-94
         L.require_gpu(self.fc.flat)

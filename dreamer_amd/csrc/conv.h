@@ -35,7 +35,7 @@ bool op_conv_split3_supported(int n, int cin, int ih, int iw, int cout);
 // 32 -> 64 channels, u8 ring only; DR_E_INVALID, nothing launched, otherwise)
 int op_enc12_s1_bf16(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
                      const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, void* out,
-                     hipStream_t s);
+                     hipStream_t s, int prepacked = 0);
 int op_conv_s1_bf16(int n, int cin, int ih, int iw, int cout, const void* in, const void* wr, const float* bias,
                     void* out, int out_nchw, hipStream_t s);
 // k4 s2 p1 conv + bias + SiLU, f32 NHWC in -> f32 NHWC (or NCHW) out, as op_conv_nhwc
@@ -79,14 +79,33 @@ int op_conv1_bf16(int n, int nb, int h, int w, int cout, const dr_frames* src, c
 // conv1 + conv2 (32 -> 64 channels, 64 x 64 frames from the u8 ring), f32-accurate
 // (conv_split.hip); repacks both weights into wr1 (3 x cout1 x 64 bf16) and wr2
 // (op_conv_repack_split3); DR_E_INVALID (nothing launched) for other shapes/sources
+// prepacked = 1: wr1 / wr2 already hold the planes (op_repack_multi), no repack launched
+bool op_enc12_split3_ok(int n, int h, int w, int c1, int c2, const dr_frames* src);
 int op_enc12_split3(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
                     const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, float* out,
-                    hipStream_t s);
+                    hipStream_t s, int prepacked = 0);
 // the same with the world-model step's saves (NHWC f32, pre0 / a0 together or
 // neither): conv1's pre-activation and output, conv2's pre-activation
 int op_enc12_split3_ex(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
                        const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, float* out,
-                       float* pre0, float* a0, float* pre1, hipStream_t s, int terms = 3);
+                       float* pre0, float* a0, float* pre1, hipStream_t s, int terms = 3, int prepacked = 0);
+// several weight repacks in one launch: conv1 planes (op_enc12_split3's wr1),
+// conv planes (op_conv_repack_split3), NT planes (op_nt_repack_split3), bf16
+// copy (op_to_bf16_2d) -- the same element code as those ops
+enum { RJ_CONV1 = 0, RJ_CONV = 1, RJ_NT = 2, RJ_BF16 = 3 };
+struct RepackJob {
+  int kind, a, b, c;  // conv1: cout; conv: cout, cin; nt: N, K, Np; bf16: rows, cols
+  const float* w;
+  void* out;
+  long long ld;       // nt: ldw; bf16: row stride
+  long long total;    // elements of the job
+};
+#define DR_RJ_MAX 6
+RepackJob rj_conv1(int cout, const float* w, void* wr);
+RepackJob rj_conv(int cout, int cin, const float* w, void* wr);
+RepackJob rj_nt(int N, int K, const float* W, int ldw, void* wr);
+RepackJob rj_bf16(int rows, int cols, const float* x, long long ld, void* y);
+int op_repack_multi(const RepackJob* jobs, int n, hipStream_t s);
 int op_enc12_bf16(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const void* wr1, const float* b1,
                   const void* wr2, const float* b2, void* out, hipStream_t s);
 // k4 s2 p1 conv + bias + SiLU, bf16 NHWC in -> bf16 NHWC (or NCHW) out

@@ -340,9 +340,8 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
 // Conv2d weight [co][ci][4][4] f32 -> bf16 [K/32 chunks][3 planes][co][32]
 // (k = tap * cin + ci) with w = plane0 + plane1 + plane2 (split3): the BN rows
 // of one chunk and plane are one contiguous run of whole 128-byte lines
-__global__ void k_conv_repack_split3(int cout, int cin, const float* __restrict__ w, u16* __restrict__ wr) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cout * 16 * cin) return;
+__device__ __forceinline__ void conv_repack_split3_elem(int i, int cout, int cin, const float* __restrict__ w,
+                                                        u16* __restrict__ wr) {
   const int co = i / (16 * cin), k = i - co * 16 * cin;
   const int tap = k / cin, ci = k - tap * cin;
   unsigned h, m, l;
@@ -351,6 +350,11 @@ __global__ void k_conv_repack_split3(int cout, int cin, const float* __restrict_
   wr[base] = (u16)h;
   wr[base + plane] = (u16)m;
   wr[base + 2 * plane] = (u16)l;
+}
+__global__ void k_conv_repack_split3(int cout, int cin, const float* __restrict__ w, u16* __restrict__ wr) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cout * 16 * cin) return;
+  conv_repack_split3_elem(i, cout, cin, w, wr);
 }
 
 int op_conv_repack_split3(int cout, int cin, const float* w, void* wr, hipStream_t s) {
@@ -667,9 +671,8 @@ __global__ __launch_bounds__(64 * NW, NTM == 1 ? DR_E12S1_OCC : 1) void k_enc12_
 }
 
 // conv1 weight [cout][3][4][4] f32 -> three bf16 planes [3][cout][64], k = tap * 4 + c (c = 3: zero)
-__global__ void k_conv1_repack_split3(int cout, const float* __restrict__ w, u16* __restrict__ wr) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cout * 64) return;
+__device__ __forceinline__ void conv1_repack_split3_elem(int i, int cout, const float* __restrict__ w,
+                                                         u16* __restrict__ wr) {
   const int co = i >> 6, k = i & 63, tap = k >> 2, c = k & 3;
   unsigned h, m, l;
   split3(c < 3 ? w[((long long)co * 3 + c) * 16 + tap] : 0.f, h, m, l);
@@ -677,22 +680,31 @@ __global__ void k_conv1_repack_split3(int cout, const float* __restrict__ w, u16
   wr[cout * 64 + i] = (u16)m;
   wr[2 * cout * 64 + i] = (u16)l;
 }
+__global__ void k_conv1_repack_split3(int cout, const float* __restrict__ w, u16* __restrict__ wr) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cout * 64) return;
+  conv1_repack_split3_elem(i, cout, w, wr);
+}
+
+bool op_enc12_split3_ok(int n, int h, int w, int c1, int c2, const dr_frames* src) {
+  return c1 == 32 && c2 == 64 && h == 64 && w == 64 && src->ring && src->starts && src->ring_cap > 0 && n > 0 &&
+         (long long)n * 2 < (1LL << 31);
+}
 
 int op_enc12_split3(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
                     const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, float* out,
-                    hipStream_t s) {
-  return op_enc12_split3_ex(n, nb, h, w, c1, c2, src, w1, b1, w2, b2, wr1, wr2, out, nullptr, nullptr, nullptr, s);
+                    hipStream_t s, int prepacked) {
+  return op_enc12_split3_ex(n, nb, h, w, c1, c2, src, w1, b1, w2, b2, wr1, wr2, out, nullptr, nullptr, nullptr, s, 3,
+                            prepacked);
 }
 
 int op_enc12_split3_ex(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
                        const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, float* out,
-                       float* pre0, float* a0, float* pre1, hipStream_t s, int terms) {
+                       float* pre0, float* a0, float* pre1, hipStream_t s, int terms, int prepacked) {
   if ((pre0 != nullptr) != (a0 != nullptr) || ((uintptr_t)pre0 | (uintptr_t)a0 | (uintptr_t)pre1) & 15 ||
       (terms != 1 && terms != 3))
     return DR_E_INVALID;
-  if (c1 != 32 || c2 != 64 || h != 64 || w != 64 || !src->ring || !src->starts || src->ring_cap <= 0 || n <= 0 ||
-      (long long)n * 2 >= (1LL << 31))
-    return DR_E_INVALID;
+  if (!op_enc12_split3_ok(n, h, w, c1, c2, src)) return DR_E_INVALID;
   static const bool raised = [] {
     (void)hipFuncSetAttribute((const void*)k_enc12_split3<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)e12_lds_bytes());
@@ -701,9 +713,11 @@ int op_enc12_split3_ex(int n, int nb, int h, int w, int c1, int c2, const dr_fra
     return true;
   }();
   (void)raised;
-  hipLaunchKernelGGL(k_conv1_repack_split3, dim3((c1 * 64 + 255) / 256), dim3(256), 0, s, c1, w1, (u16*)wr1);
-  DR_TRY(dr_check_launch("conv1_repack_split3"));
-  DR_TRY(op_conv_repack_split3(c2, c1, w2, wr2, s));
+  if (!prepacked) {
+    hipLaunchKernelGGL(k_conv1_repack_split3, dim3((c1 * 64 + 255) / 256), dim3(256), 0, s, c1, w1, (u16*)wr1);
+    DR_TRY(dr_check_launch("conv1_repack_split3"));
+    DR_TRY(op_conv_repack_split3(c2, c1, w2, wr2, s));
+  }
   if (terms == 1) {  // one term, f32 out + saves: the one-term form's occupancy (op_enc12_s1_bf16)
     static int slots1[64];
     int dev = 0;
@@ -745,10 +759,8 @@ int op_enc12_split3_ex(int n, int nb, int h, int w, int c1, int c2, const dr_fra
 // bytes; plane 0 is read).  DR_E_INVALID (nothing launched) for other shapes.
 int op_enc12_s1_bf16(int n, int nb, int h, int w, int c1, int c2, const dr_frames* src, const float* w1,
                      const float* b1, const float* w2, const float* b2, void* wr1, void* wr2, void* out,
-                     hipStream_t s) {
-  if (c1 != 32 || c2 != 64 || h != 64 || w != 64 || !src->ring || !src->starts || src->ring_cap <= 0 || n <= 0 ||
-      (long long)n * 2 >= (1LL << 31) || ((uintptr_t)out & 15))
-    return DR_E_INVALID;
+                     hipStream_t s, int prepacked) {
+  if (!op_enc12_split3_ok(n, h, w, c1, c2, src) || ((uintptr_t)out & 15)) return DR_E_INVALID;
   // persistent: as many workgroups as are resident at once (occupancy x CUs)
   static int slots[64];
   int dev = 0;
@@ -763,9 +775,11 @@ int op_enc12_s1_bf16(int n, int nb, int h, int w, int c1, int c2, const dr_frame
                                                             64 * DR_E12S1_WAVES, e12_lds_bytes(1)));
     slots[dev] = std::max(1, per) * std::max(1, cus);
   }
-  hipLaunchKernelGGL(k_conv1_repack_split3, dim3((c1 * 64 + 255) / 256), dim3(256), 0, s, c1, w1, (u16*)wr1);
-  DR_TRY(dr_check_launch("conv1_repack_split3"));
-  DR_TRY(op_conv_repack_split3(c2, c1, w2, wr2, s));
+  if (!prepacked) {
+    hipLaunchKernelGGL(k_conv1_repack_split3, dim3((c1 * 64 + 255) / 256), dim3(256), 0, s, c1, w1, (u16*)wr1);
+    DR_TRY(dr_check_launch("conv1_repack_split3"));
+    DR_TRY(op_conv_repack_split3(c2, c1, w2, wr2, s));
+  }
   const int grid = std::min(n * 2, slots[dev]);
   hipLaunchKernelGGL((k_enc12_split3<DR_E12S1_WAVES, 1>), dim3((unsigned)grid), dim3(64 * DR_E12S1_WAVES),
                      e12_lds_bytes(1), s, n, nb, *src,
@@ -1593,10 +1607,9 @@ __global__ void k_s3_finish(GemmS3 g) {
 }
 
 // W [N][K] (row stride ldw) -> bf16 planes [K/32][3][Np][32], zero past N and K
-__global__ void k_nt_repack_split3(int N, int K, int Np, const float* __restrict__ W, int ldw, u16* __restrict__ wr) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void nt_repack_split3_elem(long long i, int N, int K, int Np, const float* __restrict__ W,
+                                                      long long ldw, u16* __restrict__ wr) {
   const int KC = (K + 31) / 32;
-  if (i >= (long long)KC * 32 * Np) return;
   const int n = (int)(i / (KC * 32)), k = (int)(i - (long long)n * KC * 32);
   unsigned hh = 0, mm = 0, ll = 0;
   if (n < N && k < K) split3(W[(long long)n * ldw + k], hh, mm, ll);
@@ -1605,6 +1618,74 @@ __global__ void k_nt_repack_split3(int N, int K, int Np, const float* __restrict
   wr[base] = (u16)hh;
   wr[base + plane] = (u16)mm;
   wr[base + 2 * plane] = (u16)ll;
+}
+__global__ void k_nt_repack_split3(int N, int K, int Np, const float* __restrict__ W, int ldw, u16* __restrict__ wr) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)((K + 31) / 32) * 32 * Np) return;
+  nt_repack_split3_elem(i, N, K, Np, W, ldw, wr);
+}
+
+// Several weight repacks in ONE launch (the encoder's per-call weight
+// preparation: conv1 / conv2..N planes, the projection's planes or bf16 copy),
+// blocks over the concatenated element ranges; the same element code as the
+// single-job kernels
+struct RepackBatch {
+  RepackJob j[DR_RJ_MAX];
+  int blk0[DR_RJ_MAX + 1];  // first block of job i; [n..] = total
+  int n;
+};
+__global__ __launch_bounds__(256) void k_repack_multi(RepackBatch b) {
+  __shared__ __attribute__((aligned(16))) RepackJob J;
+  int z = 0;
+#pragma unroll
+  for (int i = 1; i < DR_RJ_MAX; ++i)
+    if ((int)blockIdx.x >= b.blk0[i]) z = i;
+  dr_stage_args(b.j[z], J, threadIdx.x);
+  const long long i = (long long)(blockIdx.x - b.blk0[z]) * 256 + threadIdx.x;
+  if (i >= J.total) return;
+  u16* out = static_cast<u16*>(J.out);
+  switch (J.kind) {
+    case RJ_CONV1: conv1_repack_split3_elem((int)i, J.a, J.w, out); break;
+    case RJ_CONV: conv_repack_split3_elem((int)i, J.a, J.b, J.w, out); break;
+    case RJ_NT: nt_repack_split3_elem(i, J.a, J.b, J.c, J.w, J.ld, out); break;
+    default: {  // RJ_BF16: rows x cols (row stride ld) -> bf16 [rows][cols], RNE
+      const int rr = (int)(i / J.b), cc = (int)(i - (long long)rr * J.b);
+      out[i] = __builtin_bit_cast(u16, (__bf16)J.w[(long long)rr * J.ld + cc]);
+    }
+  }
+}
+
+RepackJob rj_conv1(int cout, const float* w, void* wr) { return {RJ_CONV1, cout, 0, 0, w, wr, 0, (long long)cout * 64}; }
+RepackJob rj_conv(int cout, int cin, const float* w, void* wr) {
+  return {RJ_CONV, cout, cin, 0, w, wr, 0, (long long)cout * 16 * cin};
+}
+RepackJob rj_nt(int N, int K, const float* W, int ldw, void* wr) {
+  const int Np = (N + 127) / 128 * 128;
+  return {RJ_NT, N, K, Np, W, wr, ldw, (long long)((K + 31) / 32) * 32 * Np};
+}
+RepackJob rj_bf16(int rows, int cols, const float* x, long long ld, void* y) {
+  return {RJ_BF16, rows, cols, 0, x, y, ld, (long long)rows * cols};
+}
+
+int op_repack_multi(const RepackJob* jobs, int n, hipStream_t s) {
+  if (n < 0 || n > DR_RJ_MAX) {
+    dr_set_error("repack_multi: %d jobs (at most %d)", n, DR_RJ_MAX);
+    return DR_E_INVALID;
+  }
+  if (n == 0) return DR_OK;
+  RepackBatch b = {};
+  int tot = 0;
+  for (int i = 0; i < DR_RJ_MAX; ++i) {
+    b.blk0[i] = tot;
+    if (i < n) {
+      b.j[i] = jobs[i];
+      tot += (int)((jobs[i].total + 255) / 256);
+    }
+  }
+  b.blk0[DR_RJ_MAX] = tot;
+  b.n = n;
+  hipLaunchKernelGGL(k_repack_multi, dim3((unsigned)tot), dim3(256), 0, s, b);
+  return dr_check_launch("repack_multi");
 }
 
 // weight planes hold N rounded up to 128 rows (either column tile reads whole tiles)

@@ -93,15 +93,29 @@ static int encoder_bf16(const dr_dims* d, const dr_world_model* wm, const dr_fra
   const int N = enc_chans(d, e);
   const int h0 = d->img_h, w0 = d->img_w;
   const int F = enc_feat_dim(d);
-  for (int k = 2; k < N; ++k)
-    if (!op_conv_split3_supported(n, e[k], h0 >> k, w0 >> k, e[k + 1]))
-      DR_TRY(op_conv_repack_bf16(e[k + 1], e[k], e[k], wm->conv[k].w, w.wr[k], s));
-  DR_TRY(op_to_bf16_2d(d->enc_hidden, F, wm->map0.w, F + d->hidden, w.wproj, s));
+  // the weight preparation of the fast path (conv1 + conv2 planes, conv3..N
+  // planes, the projection's bf16 copy) as ONE launch
+  const bool e12 = N >= 2 && op_enc12_split3_ok(n, h0, w0, e[1], e[2], src) && !((uintptr_t)w.a[1] & 15);
+  RepackJob rj[DR_RJ_MAX];
+  int nj = 0;
+  if (e12) {
+    rj[nj++] = rj_conv1(e[1], wm->conv[0].w, w.wr[0]);
+    rj[nj++] = rj_conv(e[2], e[1], wm->conv[1].w, w.wr[1]);
+  }
+  bool s3[DR_MAX_DEPTH + 1] = {};
+  for (int k = 2; k < N; ++k) {
+    s3[k] = op_conv_split3_supported(n, e[k], h0 >> k, w0 >> k, e[k + 1]) && nj < DR_RJ_MAX - 1;
+    if (s3[k]) rj[nj++] = rj_conv(e[k + 1], e[k], wm->conv[k].w, w.wr[k]);
+    else DR_TRY(op_conv_repack_bf16(e[k + 1], e[k], e[k], wm->conv[k].w, w.wr[k], s));
+  }
+  rj[nj++] = rj_bf16(d->enc_hidden, F, wm->map0.w, F + d->hidden, w.wproj);
+  DR_TRY(op_repack_multi(rj, nj, s));
   // conv1 + conv2: k_enc12_split3 with one term (64 x 64 from the u8 ring), else
   // k_enc12_bf16, else two launches
   // (DR_E_INVALID = shape / source not covered: next form; any other failure is returned)
-  const int rc_s1 = op_enc12_s1_bf16(n, B, h0, w0, e[1], e[2], src, wm->conv[0].w, wm->conv[0].b, wm->conv[1].w,
-                                     wm->conv[1].b, w.wr[0], w.wr[1], w.a[1], s);
+  const int rc_s1 = e12 ? op_enc12_s1_bf16(n, B, h0, w0, e[1], e[2], src, wm->conv[0].w, wm->conv[0].b, wm->conv[1].w,
+                                           wm->conv[1].b, w.wr[0], w.wr[1], w.a[1], s, 1)
+                        : DR_E_INVALID;
   if (rc_s1 != DR_OK) {
     if (rc_s1 != DR_E_INVALID) return rc_s1;
     DR_TRY(op_conv_repack_bf16(e[1], 3, 4, wm->conv[0].w, w.wr[0], s));
@@ -116,8 +130,7 @@ static int encoder_bf16(const dr_dims* d, const dr_world_model* wm, const dr_fra
   }
   for (int k = 2; k < N; ++k) {
     // the split-conv tiling with one bf16 term where the shape allows, else k_conv_bf16
-    if (op_conv_split3_supported(n, e[k], h0 >> k, w0 >> k, e[k + 1])) {
-      DR_TRY(op_conv_repack_split3(e[k + 1], e[k], wm->conv[k].w, w.wr[k], s));
+    if (s3[k]) {
       DR_TRY(op_conv_s1_bf16(n, e[k], h0 >> k, w0 >> k, e[k + 1], w.a[k - 1], w.wr[k], wm->conv[k].b, w.a[k],
                              k == N - 1 ? 1 : 0, s));
     } else {
@@ -167,13 +180,32 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
   WS_CHECK(c, ws_bytes);
   if (d->precision == DR_PREC_BF16) return encoder_bf16(d, wm, src, B, n, feat, w, s);
   const int h0 = d->img_h, w0 = d->img_w;
+  const int F = enc_feat_dim(d);
+  // the weight preparation of the fast path (conv1 + conv2 planes, conv3..N
+  // planes, the projection's planes) as ONE launch
+  const bool e12 = N >= 2 && op_enc12_split3_ok(n, h0, w0, e[1], e[2], src);
+  const bool s3p = w.s3proj && n >= 1024 &&
+                   op_gemm_nt_split3_supported(n, d->enc_hidden, F, w.a[N - 1], F, nullptr, 0, F, d->enc_hidden);
+  RepackJob rj[DR_RJ_MAX];
+  int nj = 0;
+  if (e12) {
+    rj[nj++] = rj_conv1(e[1], wm->conv[0].w, w.wr[0]);
+    rj[nj++] = rj_conv(e[2], e[1], wm->conv[1].w, w.wr[1]);
+  }
+  bool s3[DR_MAX_DEPTH + 1] = {};
+  for (int k = e12 ? 2 : 1; k < N; ++k) {
+    s3[k] = op_conv_split3_supported(n, e[k], h0 >> k, w0 >> k, e[k + 1]) && nj < DR_RJ_MAX - 1;
+    if (s3[k]) rj[nj++] = rj_conv(e[k + 1], e[k], wm->conv[k].w, w.wr[k]);
+  }
+  if (s3p) rj[nj++] = rj_nt(d->enc_hidden, F, wm->map0.w, F + d->hidden, w.s3proj);
+  DR_TRY(op_repack_multi(rj, nj, s));
   // conv1 + conv2 in one launch from the u8 ring (conv_split.hip) where the
   // shape allows; else the first conv straight from the frames (u8 ring or
   // f32), and shapes that does not tile through the normalised NHWC4 copy
   int k0 = 1;
-  const int rc12 = N >= 2 ? op_enc12_split3(n, B, h0, w0, e[1], e[2], src, wm->conv[0].w, wm->conv[0].b,
-                                            wm->conv[1].w, wm->conv[1].b, w.wr[0], w.wr[1], w.a[1], s)
-                          : DR_E_INVALID;
+  const int rc12 = e12 ? op_enc12_split3(n, B, h0, w0, e[1], e[2], src, wm->conv[0].w, wm->conv[0].b, wm->conv[1].w,
+                                         wm->conv[1].b, w.wr[0], w.wr[1], w.a[1], s, 1)
+                       : DR_E_INVALID;
   if (rc12 == DR_OK) {
     k0 = 2;
   } else {
@@ -191,19 +223,15 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
     const int cin = e[k], cout = e[k + 1], hin = h0 >> k, win = w0 >> k, last = k == N - 1;
     const float* cw = wm->conv[k].w;
     const float* cb = wm->conv[k].b;
-    if (op_conv_split3_supported(n, cin, hin, win, cout)) {
-      DR_TRY(op_conv_repack_split3(cout, cin, cw, w.wr[k], s));
+    if (s3[k]) {
       DR_TRY(op_conv_split3(n, cin, hin, win, cout, w.a[k - 1], w.wr[k], cb, w.a[k], last, s));
     } else {
       DR_TRY(op_conv_repack_pad(cout, cin, cin, cw, w.wr[k], s));
       DR_TRY(op_conv_nhwc(n, cin, hin, win, cout, w.a[k - 1], w.wr[k], cb, w.a[k], last, s));
     }
   }
-  const int F = enc_feat_dim(d);
-  if (w.s3proj && n >= 1024 &&
-      op_gemm_nt_split3_supported(n, d->enc_hidden, F, w.a[N - 1], F, nullptr, 0, F, d->enc_hidden)) {
+  if (s3p) {
     // latent_mapper.0's feature columns (VAE.py:57-75 -> WorldModel.py) on the split3 bf16 MFMA
-    DR_TRY(op_nt_repack_split3(d->enc_hidden, F, wm->map0.w, F + d->hidden, w.s3proj, s));
     // K split by K alone (32 chunks of 32 per split, at most 8): the frames
     // of a window step get the same sums whether the window is encoded whole
     // or in time chunks (engine.py's overlapped warm start)
@@ -581,8 +609,10 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
   const int L = latent(d), Hd = d->hidden, A = d->action, a1 = d->actor_h1, a2 = d->actor_h2;
   const long long ldH = (long long)(H + 1) * Hd, ldL = (long long)(H + 1) * L, ldA = (long long)H * A;
   const long long lda1 = (long long)H * a1, lda2 = (long long)H * a2;
-  DR_TRY(copy2d(latents, ldL, z0, L, L, B, s));
-  DR_TRY(copy2d(hiddens, ldH, h0, Hd, Hd, B, s));
+  {
+    const Copy2dJob cj[2] = {{latents, ldL, z0, L, L, B}, {hiddens, ldH, h0, Hd, Hd, B}};
+    DR_TRY(op_copy2d_multi(cj, 2, s));
+  }
   dr_noise nq = noise;  // Categorical draws: a Philox stream apart from the actor's
   nq.stream += 65536;
   // per-step structure: the three products that read only
@@ -665,8 +695,8 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
       DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, 2, s));
     }
     DR_TRY(op_bucket_value(M1, d->buckets, w.rlog, d->buckets, wm->buckets_rew, w.rval, 1, s));
-    DR_TRY(copy2d(rewards, H, w.rval + 1, H + 1, H, B, s));
-    DR_TRY(copy2d(continues, H, w.clog + 1, H + 1, H, B, s));
+    const Copy2dJob cj[2] = {{rewards, H, w.rval + 1, H + 1, H, B}, {continues, H, w.clog + 1, H + 1, H, B}};
+    DR_TRY(op_copy2d_multi(cj, 2, s));
   }
   return DR_OK;
 }
@@ -854,8 +884,11 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
     }
   }
   // ---- actor weight gradients over all B*H rows (rows r = b*H + t) ----
-  DR_TRY(copy2d(w.hcat, (long long)H * Hd, hiddens, ldH, (long long)H * Hd, B, s));
-  DR_TRY(copy2d(w.zcat, (long long)H * L, latents, ldL, (long long)H * L, B, s));
+  {
+    const Copy2dJob cj[2] = {{w.hcat, (long long)H * Hd, hiddens, ldH, (long long)H * Hd, B},
+                             {w.zcat, (long long)H * L, latents, ldL, (long long)H * L, B}};
+    DR_TRY(op_copy2d_multi(cj, 2, s));
+  }
   {
     GemmArgs p[4];
     p[0] = bwd_w(a1, Hd + L, BH, w.gpre1a, a1, w.hcat, Hd, gr->l0.w);

@@ -53,6 +53,16 @@ int op_conv_repack(int cout, int cin, const float* w, float* wr, hipStream_t s);
 int op_fill(long long n, float* x, float v, hipStream_t s);
 int op_copy2d(float* dst, long long dp, const float* src, long long sp, long long width, long long rows,
               hipStream_t s);
+// several strided copies (dst rows dp apart, src rows sp apart) in one launch
+struct Copy2dJob {
+  float* dst;
+  long long dp;
+  const float* src;
+  long long sp, width, rows;
+  int v4, pad_;
+};
+#define DR_COPY_MAX 4
+int op_copy2d_multi(const Copy2dJob* jobs, int n, hipStream_t s);
 int op_mean(int n, const float* x, float* out, hipStream_t s);
 
 // Vector observations (dr_dims.obs_dim = D > 0): frame f = t*nb + b of `src`

@@ -1108,10 +1108,27 @@ extern "C" int dr_sqnorm_multi(long long n, const float* g, float* acc, float* s
 // chunks of buffer a, the rest buffer b; each writes one partial, and the
 // last block to arrive (device-scope ticket) adds the partials in a fixed
 // order -- deterministic, no float atomics -- and re-arms the ticket.
+// Optional AdamW preludes (dr_ac_optimiser_step): the last block also runs
+// k_adamw_prelude's step / bias-correction update of both optimisers.
+struct AdamPre {
+  int* step[2];
+  float* hyper[2];
+  double lr[2], b1[2], b2[2];
+};
+__device__ __forceinline__ void adamw_prelude_body(int* step, float* hyper, double lr, double b1, double b2) {
+  const int st = *step + 1;
+  *step = st;
+  const double bc1 = 1.0 - pow(b1, (double)st);
+  const double bc2 = 1.0 - pow(b2, (double)st);
+  hyper[0] = (float)(lr / bc1);  // step_size
+  hyper[1] = (float)sqrt(bc2);   // bias_correction2_sqrt
+}
+
 __global__ __launch_bounds__(256) void k_clip_stats(long long na, const float* __restrict__ ga, long long nb,
                                                     const float* __restrict__ gb, int nba, long long cha,
                                                     long long chb, int nloss, const float* __restrict__ loss,
-                                                    float* part, unsigned* ticket, float* sq, int* skip) {
+                                                    float* part, unsigned* ticket, float* sq, int* skip,
+                                                    AdamPre pre) {
   __shared__ float red[256];
   __shared__ int last;
   const bool isa = (int)blockIdx.x < nba;
@@ -1163,6 +1180,9 @@ __global__ __launch_bounds__(256) void k_clip_stats(long long na, const float* _
     for (int i = 0; i < nloss; ++i) bad |= !isfinite(loss[i]);
     *skip = bad;
     *ticket = 0u;
+    if (!bad)
+      for (int w = 0; w < 2; ++w)
+        if (pre.step[w]) adamw_prelude_body(pre.step[w], pre.hyper[w], pre.lr[w], pre.b1[w], pre.b2[w]);
   }
 }
 
@@ -1175,8 +1195,9 @@ extern "C" int dr_clip_stats(long long na, const float* ga, long long nb, const 
   const long long cha = (na / 4 + nba - 1) / nba, chb = (nb / 4 + nbb - 1) / nbb;
   float* part = static_cast<float*>(scratch);
   unsigned* ticket = reinterpret_cast<unsigned*>(part + DR_CLIP_SCRATCH_FLOATS - 1);
+  AdamPre none = {};
   hipLaunchKernelGGL(k_clip_stats, dim3(nba + nbb), dim3(256), 0, stream, na, ga, nb, gb, nba, cha, chb, nloss,
-                     loss, part, ticket, sq, skip);
+                     loss, part, ticket, sq, skip, none);
   return dr_check_launch("clip_stats");
 }
 
@@ -1184,22 +1205,13 @@ extern "C" int dr_clip_stats(long long na, const float* ga, long long nb, const 
 // torch's python scalars (adam.py: bias_correction1 = 1 - beta1**step ...)
 __global__ void k_adamw_prelude(int* step, float* hyper, double lr, double b1, double b2, const int* skip) {
   if (skip && *skip) return;
-  const int st = *step + 1;
-  *step = st;
-  const double bc1 = 1.0 - pow(b1, (double)st);
-  const double bc2 = 1.0 - pow(b2, (double)st);
-  hyper[0] = (float)(lr / bc1);  // step_size
-  hyper[1] = (float)sqrt(bc2);   // bias_correction2_sqrt
+  adamw_prelude_body(step, hyper, lr, b1, b2);
 }
 
-__global__ void k_adamw(long long n, float* p, float* g, float* m, float* v, const float* sqnorm,
-                        float max_norm, float keep, float omb1, float b2, float omb2, const float* hyper, float eps,
-                        const int* skip) {
-  if (skip && *skip) return;
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  float clip = 1.0f;
-  if (sqnorm) clip = fminf(max_norm / (sqrtf(*sqnorm) + 1e-6f), 1.0f);
+// one AdamW element (clip scale applied to the gradient in place first);
+// returns the new parameter
+__device__ __forceinline__ float adamw_elem(long long i, float* p, float* g, float* m, float* v, float clip, float keep,
+                                            float omb1, float b2, float omb2, const float* hyper, float eps) {
   float gv = g[i];
   if (clip != 1.0f) {  // clip_grad_norm_ scales p.grad in place (Agent.py:147-148)
     gv = gv * clip;
@@ -1210,9 +1222,22 @@ __global__ void k_adamw(long long n, float* p, float* g, float* m, float* v, con
   const float mn = (omb1 < 0.5f) ? mv + omb1 * (gv - mv) : gv - (gv - mv) * (1.0f - omb1);
   const float vn = v[i] * b2 + (omb2 * gv) * gv;
   const float den = sqrtf(vn) / hyper[1] + eps;
-  p[i] = pv + ((-hyper[0]) * mn) / den;
+  const float pn = pv + ((-hyper[0]) * mn) / den;
+  p[i] = pn;
   m[i] = mn;
   v[i] = vn;
+  return pn;
+}
+
+__global__ void k_adamw(long long n, float* p, float* g, float* m, float* v, const float* sqnorm,
+                        float max_norm, float keep, float omb1, float b2, float omb2, const float* hyper, float eps,
+                        const int* skip) {
+  if (skip && *skip) return;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float clip = 1.0f;
+  if (sqnorm) clip = fminf(max_norm / (sqrtf(*sqnorm) + 1e-6f), 1.0f);
+  adamw_elem(i, p, g, m, v, clip, keep, omb1, b2, omb2, hyper, eps);
 }
 
 extern "C" int dr_adamw(long long n, float* p, float* g, float* m, float* v, const float* sqnorm,
@@ -1244,6 +1269,63 @@ extern "C" int dr_ema(long long n, float* target, const float* src, float keep, 
   if (n <= 0) return DR_OK;
   hipLaunchKernelGGL(k_ema, dim3(blocks_for(n, 256)), dim3(256), 0, stream, n, target, src, keep, tau, skip);
   return dr_check_launch("ema");
+}
+
+// The actor-critic optimiser step of one train_Agent epoch in two launches
+// (Agent.py:137-153): clip statistics + both AdamW preludes (k_clip_stats),
+// then both AdamW updates and the critic -> target EMA in one elementwise
+// pass (blocks [0, nbc) the critic, whose new parameters feed the EMA in
+// registers; the rest the actor).  Same per-element arithmetic as dr_clip_stats
+// + dr_adamw x2 + dr_ema, so the same bits.
+struct AdamNet {
+  long long n;
+  float *p, *g, *m, *v, *hyper;
+  const float* sq;
+  float max_norm, keep, omb1, b2, omb2, eps;
+};
+__global__ void k_adamw2_ema(AdamNet c, AdamNet a, int nbc, float* target, float ema_keep, float tau,
+                             const int* skip) {
+  if (*skip) return;
+  const bool isc = (int)blockIdx.x < nbc;
+  const long long i = (long long)(isc ? blockIdx.x : blockIdx.x - nbc) * blockDim.x + threadIdx.x;
+  const AdamNet& q = isc ? c : a;
+  if (i >= q.n) return;
+  const float clip = fminf(q.max_norm / (sqrtf(*q.sq) + 1e-6f), 1.0f);
+  const float pn = adamw_elem(i, q.p, q.g, q.m, q.v, clip, q.keep, q.omb1, q.b2, q.omb2, q.hyper, q.eps);
+  if (isc) {
+    const float t = target[i] * ema_keep;
+    target[i] = t + tau * pn;
+  }
+}
+
+extern "C" int dr_ac_optimiser_step(long long na, float* pa, float* ga, float* ma, float* va, int* step_a,
+                                    float* hyper_a, double lr_a, double b1_a, double b2_a, double eps_a, double wd_a,
+                                    long long nc, float* pc, float* gc, float* mc, float* vc, int* step_c,
+                                    float* hyper_c, double lr_c, double b1_c, double b2_c, double eps_c, double wd_c,
+                                    float max_norm, float* target, float ema_keep, float tau, int nloss,
+                                    const float* loss, float* sq, int* skip, void* scratch, hipStream_t stream) {
+  DR_REQUIRE(pa && ga && ma && va && step_a && hyper_a && pc && gc && mc && vc && step_c && hyper_c && target && sq &&
+                 skip && scratch && na > 0 && nc > 0,
+             "dr_ac_optimiser_step: bad arguments");
+  DR_REQUIRE(!(((uintptr_t)ga | (uintptr_t)gc) & 15), "dr_ac_optimiser_step: gradients must be 16-byte aligned");
+  auto blocks = [](long long n4) { long long b = (n4 + 2047) / 2048; return (int)(b < 1 ? 1 : (b > 256 ? 256 : b)); };
+  const int nba = blocks(na / 4), nbb = blocks(nc / 4);
+  const long long cha = (na / 4 + nba - 1) / nba, chb = (nc / 4 + nbb - 1) / nbb;
+  float* part = static_cast<float*>(scratch);
+  unsigned* ticket = reinterpret_cast<unsigned*>(part + DR_CLIP_SCRATCH_FLOATS - 1);
+  AdamPre pre = {{step_a, step_c}, {hyper_a, hyper_c}, {lr_a, lr_c}, {b1_a, b1_c}, {b2_a, b2_c}};
+  hipLaunchKernelGGL(k_clip_stats, dim3(nba + nbb), dim3(256), 0, stream, na, ga, nc, gc, nba, cha, chb, nloss,
+                     loss, part, ticket, sq, skip, pre);
+  DR_TRY(dr_check_launch("clip_stats"));
+  // torch's python-scalar math as dr_adamw
+  const AdamNet c = {nc, pc, gc, mc, vc, hyper_c, sq + 1, max_norm, (float)(1.0 - lr_c * wd_c), (float)(1.0 - b1_c),
+                     (float)b2_c, (float)(1.0 - b2_c), (float)eps_c};
+  const AdamNet a = {na, pa, ga, ma, va, hyper_a, sq, max_norm, (float)(1.0 - lr_a * wd_a), (float)(1.0 - b1_a),
+                     (float)b2_a, (float)(1.0 - b2_a), (float)eps_a};
+  const int nbc = (int)blocks_for(nc, 256);
+  hipLaunchKernelGGL(k_adamw2_ema, dim3(nbc + (unsigned)blocks_for(na, 256)), dim3(256), 0, stream, c, a, nbc, target,
+                     ema_keep, tau, skip);
+  return dr_check_launch("adamw2_ema");
 }
 
 __global__ void k_nonfinite(long long n, const float* x, int* flag) {
@@ -1285,6 +1367,47 @@ int op_fill(long long n, float* x, float v, hipStream_t s) {
     hipLaunchKernelGGL(k_fill, dim3(blocks_for(n, 256)), dim3(256), 0, s, n, x, v);
   }
   return dr_check_launch("fill");
+}
+
+// up to DR_COPY_MAX independent strided copies in one launch (blockIdx.y =
+// copy): the boundary copies around the unroll and the weight-gradient stage
+// were one launch each
+struct Copy2dBatch {
+  Copy2dJob j[DR_COPY_MAX];
+  int n;
+};
+__global__ void k_copy2d_multi(Copy2dBatch b) {
+  const Copy2dJob& c = b.j[blockIdx.y];
+  const bool v4 = c.v4 != 0;
+  const long long wv = v4 ? c.width / 4 : c.width;
+  const long long total = wv * c.rows;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / wv, k = i - r * wv;
+    if (v4) reinterpret_cast<float4*>(c.dst + r * c.dp)[k] = reinterpret_cast<const float4*>(c.src + r * c.sp)[k];
+    else c.dst[r * c.dp + k] = c.src[r * c.sp + k];
+  }
+}
+
+int op_copy2d_multi(const Copy2dJob* jobs, int n, hipStream_t s) {
+  if (n < 0 || n > DR_COPY_MAX) {
+    dr_set_error("copy2d_multi: %d copies (at most %d)", n, DR_COPY_MAX);
+    return DR_E_INVALID;
+  }
+  Copy2dBatch b = {};
+  long long most = 0;
+  int k = 0;
+  for (int i = 0; i < n; ++i) {
+    Copy2dJob c = jobs[i];
+    if (c.rows <= 0 || c.width <= 0) continue;
+    c.v4 = ((((uintptr_t)c.dst | (uintptr_t)c.src) & 15) == 0) && c.dp % 4 == 0 && c.sp % 4 == 0 && c.width % 4 == 0;
+    most = std::max(most, (c.v4 ? c.width / 4 : c.width) * c.rows);
+    b.j[k++] = c;
+  }
+  if (k == 0) return DR_OK;
+  b.n = k;
+  const unsigned blocks = (unsigned)std::min<long long>(blocks_for(most, 256), 2048);
+  hipLaunchKernelGGL(k_copy2d_multi, dim3(blocks, (unsigned)k), dim3(256), 0, s, b);
+  return dr_check_launch("copy2d_multi");
 }
 
 // rows x width floats, row pitches dp / sp (floats); float4 when everything is

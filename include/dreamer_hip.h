@@ -300,6 +300,18 @@ int dr_adamw(long long n, float* p, float* g, float* m, float* v, const float* s
              hipStream_t stream);
 int dr_ema(long long n, float* target, const float* src, float keep, float tau, const int* skip,
            hipStream_t stream);
+/* Agent.train_step's whole optimiser tail in two launches (Agent.py:137-153):
+ * dr_clip_stats over (actor, critic) grads with both AdamW preludes run by its
+ * last workgroup, then dr_adamw(actor, clip by sq[0]), dr_adamw(critic, clip by
+ * sq[1]) and dr_ema(target <- ema_keep * target + tau * critic) in one
+ * elementwise pass.  Same per-element arithmetic (same bits) as those five
+ * calls; scratch as dr_clip_stats. */
+int dr_ac_optimiser_step(long long na, float* pa, float* ga, float* ma, float* va, int* step_a, float* hyper_a,
+                         double lr_a, double b1_a, double b2_a, double eps_a, double wd_a, long long nc, float* pc,
+                         float* gc, float* mc, float* vc, int* step_c, float* hyper_c, double lr_c, double b1_c,
+                         double b2_c, double eps_c, double wd_c, float max_norm, float* target, float ema_keep,
+                         float tau, int nloss, const float* loss, float* sq, int* skip, void* scratch,
+                         hipStream_t stream);
 /* non-finite flag: *flag = any(!isfinite(x[0..n))) (OR-accumulate) */
 int dr_nonfinite(long long n, const float* x, int* flag, hipStream_t stream);
 

@@ -102,3 +102,58 @@ def test_ema_matches_reference_formula(gpu):
         L.call("dr_ema", tg.numel(), L.ptr(tg), L.ptr(s.to(gpu)), 1 - tau, tau, None, hip.stream())
     torch.cuda.synchronize()
     np.testing.assert_allclose(tg.cpu().numpy(), t.numpy(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("bad_loss", [False, True])
+def test_ac_optimiser_step_equals_five_calls(gpu, bad_loss):
+    """dr_ac_optimiser_step (the engine's optimiser tail: clip stats + both
+    AdamW preludes, then both AdamW updates and the target EMA in one pass)
+    is bitwise the sequence it replaces -- dr_clip_stats, dr_adamw(critic),
+    dr_adamw(actor), dr_ema -- over 3 steps with fresh gradients (clipping
+    active on one net), and a non-finite loss skips everything in both."""
+    from dreamer_amd import _lib as L
+    from dreamer_amd import hip
+    na, nc = 50_000, 30_004
+    hp = dict(lr_a=4e-5, lr_c=1e-4, b1=0.9, b2=0.999, eps=1e-5, wd=0.01)
+    gen = torch.Generator().manual_seed(5)
+
+    def state():
+        t = {k: torch.randn(n, generator=gen).to(gpu) for k, n in (("pa", na), ("pc", nc), ("tgt", nc))}
+        for k, n in (("ma", na), ("va", na), ("mc", nc), ("vc", nc)):
+            t[k] = torch.zeros(n, device=gpu)
+        t.update(sa=torch.zeros(1, dtype=torch.int32, device=gpu), sc=torch.zeros(1, dtype=torch.int32, device=gpu),
+                 ha=torch.zeros(2, device=gpu), hc=torch.zeros(2, device=gpu), sq=torch.zeros(2, device=gpu),
+                 skip=torch.zeros(1, dtype=torch.int32, device=gpu), scr=torch.zeros(1024, device=gpu))
+        return t
+
+    A, Bs = state(), None
+    Bs = {k: v.clone() for k, v in A.items()}
+    st = hip.stream()
+    for it in range(3):
+        ga = (torch.randn(na, generator=gen) * (30.0 if it == 1 else 0.01)).to(gpu)
+        gc = (torch.randn(nc, generator=gen) * 0.02).to(gpu)
+        loss = torch.tensor([0.5, float("nan") if (bad_loss and it == 2) else 1.5], device=gpu)
+        gA, gcA, gB, gcB = ga.clone(), gc.clone(), ga.clone(), gc.clone()
+        # the five calls
+        L.call("dr_clip_stats", na, L.ptr(gA), nc, L.ptr(gcA), 2, L.ptr(loss), L.ptr(A["sq"]), L.ptr(A["skip"]),
+               L.ptr(A["scr"]), st)
+        L.call("dr_adamw", nc, L.ptr(A["pc"]), L.ptr(gcA), L.ptr(A["mc"]), L.ptr(A["vc"]), L.ptr(A["sq"]) + 4, 100.0,
+               hp["lr_c"], hp["b1"], hp["b2"], hp["eps"], hp["wd"], L.ptr(A["sc"]), L.ptr(A["hc"]), L.ptr(A["skip"]),
+               st)
+        L.call("dr_adamw", na, L.ptr(A["pa"]), L.ptr(gA), L.ptr(A["ma"]), L.ptr(A["va"]), L.ptr(A["sq"]), 100.0,
+               hp["lr_a"], hp["b1"], hp["b2"], hp["eps"], hp["wd"], L.ptr(A["sa"]), L.ptr(A["ha"]), L.ptr(A["skip"]),
+               st)
+        L.call("dr_ema", nc, L.ptr(A["tgt"]), L.ptr(A["pc"]), float(1.0 - 0.02), 0.02, L.ptr(A["skip"]), st)
+        # the fused step
+        L.call("dr_ac_optimiser_step", na, L.ptr(Bs["pa"]), L.ptr(gB), L.ptr(Bs["ma"]), L.ptr(Bs["va"]),
+               L.ptr(Bs["sa"]), L.ptr(Bs["ha"]), hp["lr_a"], hp["b1"], hp["b2"], hp["eps"], hp["wd"],
+               nc, L.ptr(Bs["pc"]), L.ptr(gcB), L.ptr(Bs["mc"]), L.ptr(Bs["vc"]), L.ptr(Bs["sc"]), L.ptr(Bs["hc"]),
+               hp["lr_c"], hp["b1"], hp["b2"], hp["eps"], hp["wd"], 100.0, L.ptr(Bs["tgt"]), float(1.0 - 0.02),
+               0.02, 2, L.ptr(loss), L.ptr(Bs["sq"]), L.ptr(Bs["skip"]), L.ptr(Bs["scr"]), st)
+        torch.cuda.synchronize()
+        assert torch.equal(gA, gB) and torch.equal(gcA, gcB), f"step {it}: clipped gradients differ"
+        for k in A:
+            if k == "scr":
+                continue
+            assert torch.equal(A[k], Bs[k]), f"step {it}: {k} differs"
+    assert int(A["sa"].item()) == (2 if bad_loss else 3)
