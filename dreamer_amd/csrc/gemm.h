@@ -73,11 +73,6 @@ struct alignas(16) GemmArgs {
   // op_nt_repack_split3 of W): per-step chain products then run on the bf16
   // MFMA -- f32-accurate 3-term split (fp32 mode) or plane 0 alone (bf16 mode)
   const unsigned short* wsplit; int wsplit_np, pad2_;
-  // the A operand also given as split3 planes [3][M][asplit_ld] (asplit_ps
-  // elements apart; truncation split, split3_pair), written by its producer
-  // (the GRU gates kernel): k_gemm_wks3 then loads the planes instead of
-  // splitting A in registers -- bitwise the same products
-  const unsigned short* asplit; long long asplit_ps; int asplit_ld; int pad3_[3];
 };
 
 enum { EPI_NONE = 0, EPI_SAMPLE = 1, EPI_ACTOR = 2 };

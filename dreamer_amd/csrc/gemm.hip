@@ -1833,10 +1833,9 @@ __device__ __forceinline__ unsigned wk_pack_rne(float x0, float x1) {
   return __builtin_bit_cast(unsigned, v);
 }
 
-template <int NTP, int D, int NW = 4>
+template <int NTP, int D, int NW = 4, int FM = 2>
 __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) {
-  constexpr bool FULL = false, APL = false;
-  constexpr int FM = 2, FN = 2, BM = 16 * FM, NTH = 64 * NW, NT4 = FM * FN * 256;
+  constexpr int FN = 2, BM = 16 * FM, NTH = 64 * NW, NT4 = FM * FN * 256;
   __shared__ GemmArgs s_args;
   __shared__ __attribute__((aligned(16))) float red[NW][FM * FN * 4][64];
   int z = 0;
@@ -1872,32 +1871,20 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) 
   const int c0 = (nkc * wave) / NW, c1 = (nkc * (wave + 1)) / NW;
   const int clast = max(c1 - 1, 0);
   unsigned oa[FM];
-  const unsigned short* asp = APL ? dr_uni(g.asplit) : nullptr;
-  const unsigned aps = APL ? (unsigned)dr_uni((int)g.asplit_ps) : 0u;
-  const int ald = APL ? dr_uni(g.asplit_ld) : 0;
 #pragma unroll
-  for (int i = 0; i < FM; ++i) oa[i] = (unsigned)(min(m0 + 16 * i + r, M - 1) * (APL ? ald : lda));
+  for (int i = 0; i < FM; ++i) oa[i] = (unsigned)(min(m0 + 16 * i + r, M - 1) * lda);
   unsigned ob[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) ob[j] = (unsigned)(n0 + 16 * j + r) * 32u + 8u * q;  // within a plane (Np >= n rows)
-  f32x4 ra[APL ? 1 : D][FM][2];
-  wk_u32x4 rap[APL ? D : 1][3][FM];
+  f32x4 ra[D][FM][2];
   wk_u32x4 rb[D][NTP][FN];
   auto load = [&](int c, int sl) {
     const int k = 32 * c + 8 * q;
     const unsigned kk = k < K ? (unsigned)k : 0u;
-    if constexpr (APL) {
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-          rap[sl][p][i] = *(const DR_GLOBAL wk_u32x4*)((const DR_GLOBAL char*)asp + ((p * aps + oa[i] + kk) << 1));
-    } else {
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        ra[sl][i][0] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)A + ((oa[i] + kk) << 2));
-        ra[sl][i][1] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)A + ((oa[i] + kk + 4) << 2));
-      }
+    for (int i = 0; i < FM; ++i) {
+      ra[sl][i][0] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)A + ((oa[i] + kk) << 2));
+      ra[sl][i][1] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)A + ((oa[i] + kk + 4) << 2));
     }
 #pragma unroll
     for (int p = 0; p < NTP; ++p)
@@ -1927,12 +1914,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) 
       wk_u32x4 a[NTP][FM];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        if constexpr (APL) {
-#pragma unroll
-          for (int p = 0; p < 3; ++p) a[p % NTP][i] = kin ? rap[u][p][i] : (wk_u32x4){0u, 0u, 0u, 0u};
-          continue;
-        }
-        f32x4 x0 = ra[APL ? 0 : u][i][0], x1 = ra[APL ? 0 : u][i][1];
+        f32x4 x0 = ra[u][i][0], x1 = ra[u][i][1];
         if (!kin) x0 = x1 = (f32x4){0.f, 0.f, 0.f, 0.f};
         if constexpr (NTP == 3) {
           unsigned h[4], m[4], l[4];
@@ -1961,7 +1943,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) 
       DR_WK3(0, 0, 0)
 #undef DR_WK3
       // unconditional: a load under a branch is waited for at once
-      if constexpr (!FULL) load(min(c + D, clast), u);
+      load(min(c + D, clast), u);
     }
   }
   // partial tiles meet in LDS; element (t, e, l) of tile t = (i, j): row 16 i + (l & 15), column 16 j + 4 (l >> 4) + e
@@ -2535,23 +2517,38 @@ static bool wks3_ok(const GemmBatch& gb, int count) {
   }
   return true;
 }
-// 4 waves per 32 x 32 tile, each over its own run of k-chunks, a 2-deep
-// register ring (r04g: 8 waves, whole-wave prefetch and A planes measured
-// slower, profiles/r04g_ab_wks3.txt, r04t_ab_aplanes.txt)
+// 4 waves per 32 x 32 (bf16: 16 x 32) tile, each over its own run of
+// k-chunks through a register ring (r04g: 8 waves, whole-wave prefetch and A
+// planes measured slower, profiles/r04g_ab_wks3.txt, r04t_ab_aplanes.txt)
 // (r05w: 64-row tiles, each weight plane read by half as many row tiles,
 // measured slower -- 548 k vs 566 k fp32, 776 k vs 803 k bf16 at B = 256)
+#ifndef DR_WKS3_D
+// register-ring depth (K chunks in flight per wave).  1: the fp32 kernel at 83
+// VGPRs (4 waves per SIMD) instead of 140 (3), bf16 48 instead of 86 (7 / 4):
+// fp32 headline 581 -> 592 k, bf16 818 -> 828 k; depth 3 / 4 slower still
+// than 2 (profiles/r05zf_ab_wks3_depth.txt)
+#define DR_WKS3_D 1
+#endif
+// 16-row fragments per tile: 2 (32 x 32 tiles) for the fp32 products, 1 for
+// bf16 mode's (16 x 32 tiles: 828 -> 838 k bf16 headline; fp32 595 -> 587 k,
+// kept at 2; 8 or 2 waves per tile: +0.2 % / -6 %, profiles/r05zh_ab_wks3_shape.txt)
+#define DR_WKS3_NW 4  // waves per tile (each a 1/NW share of K)
+#define DR_WKS3_FM 2
+#define DR_WKS3_FM_B16 1
 static void launch_wks3(const GemmBatch& gb, int count, hipStream_t s, bool bf16) {
+  const int fm = bf16 ? DR_WKS3_FM_B16 : DR_WKS3_FM;
   int tot = 0, maxt = 0;
   for (int i = 0; i < count; ++i) {
     const GemmArgs& g = gb.p[i];
-    const int t = dr_cdiv(g.M, 32) * dr_cdiv(g.N, 32);
+    const int t = dr_cdiv(g.M, 16 * fm) * dr_cdiv(g.N, 32);
     tot += t;
     maxt = std::max(maxt, t);
   }
   const int npack = count > 1 ? count : 0;
   const dim3 grid(dr_xcd_grid(npack ? tot : maxt));
-  if (bf16) hipLaunchKernelGGL((k_gemm_wks3<1, 2>), grid, dim3(256), 0, s, gb, npack);
-  else hipLaunchKernelGGL((k_gemm_wks3<3, 2>), grid, dim3(256), 0, s, gb, npack);
+  const dim3 blk(64 * DR_WKS3_NW);
+  if (bf16) hipLaunchKernelGGL((k_gemm_wks3<1, DR_WKS3_D, DR_WKS3_NW, DR_WKS3_FM_B16>), grid, blk, 0, s, gb, npack);
+  else hipLaunchKernelGGL((k_gemm_wks3<3, DR_WKS3_D, DR_WKS3_NW, DR_WKS3_FM>), grid, blk, 0, s, gb, npack);
 }
 
 // split-K over workgroups only when the tile grid is under one workgroup per

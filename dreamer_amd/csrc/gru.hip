@@ -344,6 +344,7 @@ __global__ __launch_bounds__(512) void k_gru_fused(GruArgs ga) {
 #define GG_UNITS 32
 #define GG_NT (GG_ROWS * 3 * (GG_UNITS / 4))  // 192 threads
 
+#define DR_GATES_GB 8  // gathered W_ih^T rows issued per batch (4: the same, r05zh)
 template <int GB>  // gathered rows issued per batch (VGPRs vs round trips)
 __global__ __launch_bounds__(GG_NT) void k_gru_gates(GruArgs ga) {
   __shared__ GruArgs g;
@@ -588,7 +589,7 @@ int op_gru_fused(const GruArgs& g, hipStream_t s) {
       DR_TRY(gemm_launch(G_NT, AM_PLAIN, &p, 1, s));
     }
     const int tiles = ((g.Hd + GG_UNITS - 1) / GG_UNITS) * ((g.B + GG_ROWS - 1) / GG_ROWS);
-    hipLaunchKernelGGL(k_gru_gates<8>, dim3(dr_xcd_grid(tiles)), dim3(GG_NT), 0, s, g);
+    hipLaunchKernelGGL(k_gru_gates<DR_GATES_GB>, dim3(dr_xcd_grid(tiles)), dim3(GG_NT), 0, s, g);
     return dr_check_launch("gru_gates");
   }
   const int tiles = ((g.Hd + 15) / 16) * ((g.B + 15) / 16);
