@@ -2030,7 +2030,7 @@ static size_t min_lds() { return g_min_lds; }
 // floats of dynamic LDS a skinny launch needs (mirrors the kernel's layout)
 template <int MT, int NT, int AMODE, bool B_KN>
 static size_t skinny_lds_floats(const GemmBatch& gb, int count, bool vec) {
-  const size_t red = (size_t)8 * (MT / 16) * (NT / 16) * 4 * 64;
+  const size_t red = (size_t)DR_SKW * (MT / 16) * (NT / 16) * 4 * 64;  // the kernel's RED
   size_t need = red;
   if (!vec) return need;
   for (int i = 0; i < count; ++i) {
