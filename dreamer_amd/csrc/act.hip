@@ -416,9 +416,9 @@ __global__ __launch_bounds__(ACT_NT) void k_act_step(ActArgs ga) {
   ACT_TS(a, 7);
   // A barrier that timed out (a workgroup never arrived: the grid was not
   // co-resident) is reported, never silent: every workgroup that saw it raises
-  // the status word the host checks after the step, and workgroup 0 writes NaN
-  // to every output (action, mu, sigma, z', h') so nothing downstream can
-  // mistake them for a state.
+  // the status word the host checks after the step, and writes NaN to every
+  // output (action, mu, sigma, z', h') so nothing downstream can mistake them
+  // for a state.
   // Workgroup 0 also re-reads the shared fail flag after the last barrier: a
   // workgroup that timed out there raised it after arriving (its stage data is
   // complete), but the outputs are poisoned all the same.  `status` stays the
@@ -434,12 +434,15 @@ __global__ __launch_bounds__(ACT_NT) void k_act_step(ActArgs ga) {
       __hip_atomic_store(a.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (a.status) __hip_atomic_store(a.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    if (blockIdx.x == 0) {
-      const float qnan = __int_as_float(0x7fc00000);
-      for (int i = threadIdx.x; i < A; i += ACT_NT) a.a_out[i] = a.mu_out[i] = a.sig_out[i] = qnan;
-      for (int i = threadIdx.x; i < L; i += ACT_NT) a.z_out[i] = qnan;
-      for (int i = threadIdx.x; i < Hd; i += ACT_NT) a.h_out[i] = qnan;
-    }
+    // every failing workgroup poisons every output after its own writes: a
+    // workgroup that got past the barrier workgroup 0 gave up on still writes
+    // its h' / z' slice (a forced-timeout run caught workgroup 0's NaN being
+    // overwritten that way), but it cannot pass the next barrier (workgroup 0
+    // never arrives), so it fails too and poisons after its writes
+    const float qnan = __int_as_float(0x7fc00000);
+    for (int i = threadIdx.x; i < A; i += ACT_NT) a.a_out[i] = a.mu_out[i] = a.sig_out[i] = qnan;
+    for (int i = threadIdx.x; i < L; i += ACT_NT) a.z_out[i] = qnan;
+    for (int i = threadIdx.x; i < Hd; i += ACT_NT) a.h_out[i] = qnan;
     return;
   }
   // ---- stage 8 (workgroup 0): LN-SiLU, base_net.3, LN-SiLU, mu / log_sigma heads, tanh(mu + eps sigma) ----

@@ -19,6 +19,9 @@
 #ifndef DR_PDREAM
 #define DR_PDREAM 1  // A/B knob: 0 = the imagination unroll as seven launches per step
 #endif
+#ifndef DR_A0_PLANES
+#define DR_A0_PLANES 1  // A/B knob: 0 = the BPTT's actor input gradient on the staged skinny path
+#endif
 #ifndef DR_PBPTT
 #define DR_PBPTT 1  // A/B knob: 0 = the BPTT reverse loop as seven launches per step
 #endif
@@ -404,7 +407,7 @@ struct ImWs {
   float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog, *rval, *wt, *wst, *bst;  // forward scratch
   float *tl0f, *hpart;  // forward: actor Linear 0 transposed ([Hd+L][a1]), its h-part + bias [B][a1]
   void *s3r, *s3c;  // split3 weight planes of the reward / continue heads' first Linear
-  void *s3p0, *s3a0, *s3whh, *s3wt, *s3twhh;  // bf16 planes of the per-step chain weights (k_gemm_wks3)
+  void *s3p0, *s3a0, *s3whh, *s3wt, *s3twhh, *s3tl0a;  // bf16 planes of the per-step chain weights (k_gemm_wks3)
   float* s3part;    // their split-K partial sums
   size_t s3part_n;
   int* idx[2];
@@ -438,6 +441,7 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.s3whh = c.raw(op_nt_split3_ws_bytes(3 * Hd, Hd));
   w.s3wt = c.raw(op_nt_split3_ws_bytes(L + A, 3 * Hd));
   w.s3twhh = c.raw(op_nt_split3_ws_bytes(Hd, 3 * Hd));
+  w.s3tl0a = c.raw(op_nt_split3_ws_bytes(Hd + L, d->actor_h1));
   w.s3r = c.raw(op_nt_split3_ws_bytes(d->rew_h1, d->hidden + L));
   w.s3c = c.raw(op_nt_split3_ws_bytes(d->cont_h1, d->hidden + L));
   w.s3part_n = op_gemm_nt_split3_part_floats((int)B1, std::max(d->rew_h1, d->cont_h1));
@@ -790,6 +794,7 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
     if (B >= 128 && (3 * Hd) % 8 == 0) {
       DR_TRY(split_planes(L + A, 3 * Hd, w.wt, 3 * Hd, w.s3wt, s));
       DR_TRY(split_planes(Hd, 3 * Hd, w.twhh, 3 * Hd, w.s3twhh, s));
+      if (d->actor_h1 % 8 == 0) DR_TRY(split_planes(Hd + L, d->actor_h1, w.tl0a, d->actor_h1, w.s3tl0a, s));
     }
   }
   }  // do_prep
@@ -874,7 +879,17 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
     // prologue also writes g_pre and the LN-parameter saves for the weight grads
     DR_TRY(lnbwd_nt(B, a1, a2, w.gx2a, a2, tp.pre2a + o2, lda2, ac->n4, w.tl3a, w.gx1a, a1, 0, w.gpre2a + o2, lda2,
                     w.gy2a + o2, w.xh2a + o2, nullptr, 0, INT_MAX, s));
-    if (t > 0) {
+    if (t > 0 && planes && a1 % 8 == 0 && DR_A0_PLANES) {
+      // B >= 128: the LN-SiLU backward as its own pass, then the K = a1 input
+      // gradient [gH_t | gZ_t] on the wave-K split3 kernel (weight planes of
+      // the transposed base_net.0, split once per call)
+      DR_TRY(op_ln_silu_bwd(B, a1, w.gx1a, a1, tp.pre1a + o1, lda1, ac->n1.w, ac->n1.b, w.gpre1a + o1, lda1,
+                            w.gy1a + o1, w.xh1a + o1, s));
+      GemmArgs g = bwd_nt(B, Hd + L, a1, w.gpre1a + o1, lda1, w.tl0a, gH_t, ldH, 1);
+      g.Y2 = gZ_t; g.ldy2 = ldL; g.nsplitY = Hd;
+      wplanes(g, w.s3tl0a);
+      DR_TRY(run(G_NT, AM_PLAIN, g, s));
+    } else if (t > 0) {
       DR_TRY(lnbwd_nt(B, Hd + L, a1, w.gx1a, a1, tp.pre1a + o1, lda1, ac->n1, w.tl0a, gH_t, ldH, 1, w.gpre1a + o1,
                       lda1, w.gy1a + o1, w.xh1a + o1, gZ_t, ldL, Hd, s));
     } else {

@@ -2633,6 +2633,13 @@ static int launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
     // tiles, which re-read the weights per row tile and the activations per
     // 16 columns: 44 -> 32 us (BPTT, 2 problems), 23 -> 15 us (heads, 3
     // problems, split-K 4), profiles/r02h_kbench_tile_B256.txt
+    // shallow-K products the caller gave weight planes (the BPTT's actor
+    // input gradient, K = 200, N = 1624): the wave-K split3 kernel
+    if (DR_WKS3 && !A_KM && !B_KN && maxM >= 128 && maxM <= 512 && minK < 512 && g_tile_variant == 0 &&
+        wks3_ok(gb, count)) {
+      launch_wks3(gb, count, s, b16_ok(gb, count));
+      return DR_OK;
+    }
     if (!A_KM && !B_KN && maxM >= 128 && maxM <= 512 && g_tile_variant != 26) {
       int tiles32 = 0;
       for (int i = 0; i < count; ++i) tiles32 += dr_cdiv(gb.p[i].M, 32) * dr_cdiv(gb.p[i].N, 32);
