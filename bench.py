@@ -515,6 +515,31 @@ def main():
                 "value": round(world * 64 * 15 * args.steps / el64, 1), "unit": "imagined latent-steps/s",
                 "ms_per_epoch": round(el64 / args.steps * 1e3, 4),
                 "note": "BASELINE configs[1] shape (B=64/GPU S=64 H=15), Dreamer.train_Agent() AC_epochs=1"}
+            # the reference's default AC_epochs = 2 (car_racer_config.yaml:44) at configs[1]'s B = 64: the
+            # default train_Agent (sequential epochs on the persistent kernels) against the pipelined schedule
+            # (engine.run_many: warm start of epoch e+1 beside epoch e, everything in launch form)
+            k2 = max(2, args.steps // 2)
+            d64.AC_epochs, d64.pipeline_epochs = 2, True
+            el_seq, _ = time_train_agent(d64, k2, 2)
+
+            def pipelined_calls(dd, k, w):
+                e = dd._engine
+                for i in range(w + k):
+                    if i == w:
+                        barrier()
+                        t0 = time.perf_counter()
+                    e.run_many([dd.buffer.sample_start_indices(64) for _ in range(2)])
+                barrier()
+                return max_over_ranks(time.perf_counter() - t0)
+            el_pipe = pipelined_calls(d64, k2, 2)
+            secondary["configs1_B64_ac_epochs2"] = {
+                "value": round(world * 64 * 15 * 2 * k2 / el_seq, 1), "unit": "imagined latent-steps/s",
+                "ms_per_epoch": round(el_seq / (2 * k2) * 1e3, 4),
+                "pipelined_launch_form": {"value": round(world * 64 * 15 * 2 * k2 / el_pipe, 1),
+                                          "ms_per_epoch": round(el_pipe / (2 * k2) * 1e3, 4)},
+                "note": "configs[1] shape with the reference's AC_epochs=2: value = Dreamer.train_Agent() as shipped "
+                        "(B <= 128: sequential epochs on the persistent scan / unroll / BPTT); pipelined_launch_form "
+                        "= the same epochs through engine.run_many (DESIGN.md 5a)"}
             del d64
         if args.precision == "fp32":
             # bf16 perf mode (config key precision="bf16"; BASELINE configs[1] names bf16):
@@ -547,8 +572,11 @@ def main():
                                           "gpu_ms_per_step": round(wb_gpu_s * 1e3, 3), "loss": wb_loss, "T": H}
                 del db
             bf["note"] = ("Dreamer(config with precision='bf16'): conv1+conv2 fused from the u8 ring, conv3/conv4 "
-                          "and the projection as bf16 implicit GEMMs (f32 accumulate); the imagination / update "
-                          "chain stays f32 (tests/test_gpu_bf16.py states the tolerances)")
+                          "and the projection as bf16 implicit GEMMs (f32 accumulate); in the imagination / update "
+                          "chain the GEMM-shaped products (GRU hidden product, prior / actor / heads, BPTT input "
+                          "gradients, actor / critic weight gradients) take one-term bf16 operands with f32 "
+                          "accumulation, while the samplers, gates, LayerNorms, optimiser and losses stay f32 "
+                          "(INTEGRATION.md; tests/test_gpu_bf16.py states the tolerances)")
             secondary["bf16_perf_mode"] = bf
         # BASELINE configs[3]: 128x128 frames, the deeper VAE (encoder_depth = 5), H = 20, S = 64 at its
         # per-GPU share of the global batch 256 over 8 GPUs (B = 32) and at the whole batch on one GPU

@@ -32,7 +32,7 @@ class dr_dims(C.Structure):
         "hidden", "rows", "cols", "action", "img_h", "img_w", "enc_f1", "enc_f2", "enc_hidden",
         "prior_h1", "prior_h2", "rew_h1", "rew_h2", "cont_h1", "cont_h2",
         "actor_h1", "actor_h2", "critic_h1", "critic_h2", "buckets", "dec_f1", "dec_f2", "dec_hidden", "precision", "obs_dim", "enc_depth",
-        "launch_form")]
+        "launch_form")] + [("fault", fp)]
 
 DR_MAX_DEPTH = 5  # include/dreamer_hip.h: conv / convt slots (dr_dims.enc_depth <= 5)
 
@@ -129,6 +129,7 @@ _SIGS = {
     "dr_nonfinite": (_i, [_ll, fp, fp, fp]),
     "dr_replay_gather": (_i, [_ll, _i, _i, _i, _i, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp]),
     "dr_rng_advance": (_i, [fp, C.c_ulonglong, fp]),
+    "dr_persistent_kernels": (_i, [_P(dr_dims), _i, _i, _i]),
     "dr_stream_create_cumask": (_i, [_i, _P(C.c_uint), _P(fp)]),
     "dr_stream_destroy": (_i, [fp]),
     "dr_device_cus": (_i, [_P(_i)]),

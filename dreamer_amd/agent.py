@@ -223,6 +223,8 @@ class Agent(nn.Module):
         self.buckets = critic_buckets
         self.smoothing_factor = 0.99
         self.S_dev = torch.ones((), device=self.device)
+        # False after a persistent-kernel fault: every entry point then runs its launch form
+        self.persistent_ok = True
         self._A_hp = (A_lr, tuple(A_betas), A_eps)
         self._C_hp = (C_lr, tuple(C_betas), C_eps)
         self._flat = None
@@ -232,7 +234,11 @@ class Agent(nn.Module):
     def _bind(self):
         pad = lambda m: sum(-(-p.numel() // 64) * 64 for p in m.parameters())
         na, nc = pad(self.actor), pad(self.critic)
-        self.grad_buffer = torch.zeros(na + nc + 2, device=self.device)
+        # [actor grads | critic grads | actor loss, critic loss, fault]: the fault
+        # slot (dr_dims.fault) turns NaN when a persistent kernel timed out; it
+        # rides in the flat buffer's all-reduce (every rank sees it) and in the
+        # optimiser's non-finite check (the update is skipped, Agent.py:137-139)
+        self.grad_buffer = torch.zeros(na + nc + 3, device=self.device)
         self.loss_buffer = self.grad_buffer[na + nc:]
         self.fa = _Flat(self.actor, self.grad_buffer[:na])
         self.fc = _Flat(self.critic, self.grad_buffer[na:na + nc])
@@ -255,6 +261,11 @@ class Agent(nn.Module):
 
     def loss_slot(self, i):
         return self.loss_buffer[i:i + 1]
+
+    def fault_slot(self):
+        """Device float, NaN once a persistent kernel timed out (sticky until the
+        host acknowledges it, engine.ImaginationEngine.check_faults)."""
+        return self.loss_buffer[2:3]
 
     @property
     def S(self):
@@ -301,7 +312,7 @@ class Agent(nn.Module):
                self.fc.numel, self.fc.flat.data_ptr(), self.fc.grad.data_ptr(), ca.exp_avg.data_ptr(),
                ca.exp_avg_sq.data_ptr(), ca.step_dev.data_ptr(), ca.hyper.data_ptr(), gc["lr"], gc["betas"][0],
                gc["betas"][1], gc["eps"], gc["weight_decay"],
-               100.0, self.ft.flat.data_ptr(), float(1.0 - tau), float(tau), 2, self.loss_buffer.data_ptr(),
+               100.0, self.ft.flat.data_ptr(), float(1.0 - tau), float(tau), 3, self.loss_buffer.data_ptr(),
                sq.data_ptr(), skip.data_ptr(), self._clip_scratch.data_ptr(), st)
 
     def soft_update_target(self, tau=0.02, skip=None):  # Agent.py:90-94
@@ -376,6 +387,8 @@ class Agent(nn.Module):
             self.fa.sync_grads()
         sq = torch.zeros(2, device=dev)
         skip = torch.zeros(1, dtype=torch.int32, device=dev)
+        # a timed-out persistent BPTT left NaN gradients and the fault slot set
+        L.call("dr_nonfinite", 1, L.ptr(self.fault_slot()), skip.data_ptr(), st)
         L.call("dr_sqnorm", self.fa.numel, self.fa.grad.data_ptr(), sq.data_ptr(), st)
         L.call("dr_sqnorm", self.fc.numel, self.fc.grad.data_ptr(), sq.data_ptr() + 4, st)
         self.critic_optimiser.fused_step(sq[1:2], 100.0, skip)

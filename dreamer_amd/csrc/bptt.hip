@@ -66,6 +66,7 @@ struct alignas(16) PBpttArgs {
   float *ht;    // [H][B][HD]
   unsigned* cnt;
   long long* ts;  // DR_PBPTT_TS builds: [16 steps][7 stages][8 marks][grid] wall-clock stamps (first tile)
+  PsPoison pz;    // the actor weight gradients' saves NaN-filled on a timeout (persist.h ps_exit)
 };
 #ifdef DR_PBPTT_TS
 #define PB_TS(st, mk) \
@@ -269,7 +270,7 @@ __device__ __forceinline__ void pb_lnbwd16(__amdgpu_buffer_rsrc_t rg, unsigned g
     else
 
 template <int NT>
-__global__ __launch_bounds__(NTH, 1) void k_pbptt(PBpttArgs g) {
+__device__ __forceinline__ void pbptt_body(const PBpttArgs& g) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int s_ok;
   __shared__ float s_gh[16][16];
@@ -607,6 +608,15 @@ __global__ __launch_bounds__(NTH, 1) void k_pbptt(PBpttArgs g) {
   }
 }
 
+// every workgroup leaves through ps_exit (also after a timed-out wait): the
+// last one NaN-fills the saves the actor weight gradients are formed from and
+// the fault slot on a timeout
+template <int NT>
+__global__ __launch_bounds__(NTH, 1) void k_pbptt(PBpttArgs g) {
+  pbptt_body<NT>(g);
+  ps_exit(g.cnt + CNT_LD * (CNT_BLOCKS * C_STATUS + 1), g.cnt + CNT_LD * CNT_BLOCKS * C_STATUS, g.pz);
+}
+
 // ---------------------------------------------------------------------------
 // B <= 64: at B = 128 the K = 1800 stage has two tiles per workgroup and the
 // launch form measured faster (424.9 k against 439.1 k steps/s, profiles/r05q_ab_persistent.txt)
@@ -674,8 +684,17 @@ int op_pbptt(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, int
   }
   PBpttArgs a;
   memset(&a, 0, sizeof(a));
-  a.B = B; a.H = H; a.A = A; a.spin_limit = 1 << 22;
+  a.B = B; a.H = H; a.A = A; a.spin_limit = ps_spin_limit("bptt");
   a.io = io;
+  {
+    const unsigned long long BH = (unsigned long long)B * H;
+    float* const outs[7] = {io.gheads, io.gpre2a, io.gy2a, io.xh2a, io.gpre1a, io.gy1a, io.xh1a};
+    for (int i = 0; i < 7; ++i) {
+      a.pz.p[i] = outs[i];
+      a.pz.n[i] = i == 0 ? BH * 2 * A : BH * MW;
+    }
+    a.pz.fault = d->fault;
+  }
   a.pn4g = wm->prior.n4.w; a.pn4b = wm->prior.n4.b; a.pn1g = wm->prior.n1.w; a.pn1b = wm->prior.n1.b;
   a.an4g = ac->n4.w; a.an4b = ac->n4.b; a.an1g = ac->n1.w; a.an1b = ac->n1.b;
   float* f = reinterpret_cast<float*>(ws);

@@ -45,7 +45,7 @@ constexpr int SHW = 4352;  // scr offset of the actor heads' weights [2 A][MW] (
 constexpr int SLN4 = SHW + 16 * MW;  // base_net.4's gamma, beta [2][MW], then the heads' biases [16]
 constexpr int CNT_LD = 32;
 // counters per 16-row block: [stage][block]
-enum { C_A = 0, C_B = 1, C_G = 2, C_P0 = 3, C_P1 = 4, C_PRE = 5, C_STATUS = 6 };
+enum { C_A = 0, C_B = 1, C_G = 2, C_P0 = 3, C_P1 = 4, C_PRE = 5, C_STATUS = 6 };  // exit ticket: block 1 of C_STATUS
 constexpr int CNT_BLOCKS = 16;  // B <= 256
 }  // namespace
 
@@ -74,6 +74,7 @@ struct alignas(16) PDreamArgs {
   unsigned long long* zg;                              // [H + 1][B][NR]
   unsigned* cnt;
   long long* ts;  // DR_PDREAM_TS builds: [16 steps][6 stages][8 marks][grid] wall-clock stamps
+  PsPoison pz;    // outputs NaN-filled on a timeout (persist.h ps_exit)
 };
 #ifdef DR_PDREAM_TS
 #define PD_TS(st, mk) \
@@ -247,7 +248,7 @@ __device__ __forceinline__ void pd_signal(unsigned* c0, int n) {
 }
 
 template <int NT, int MR>
-__global__ __launch_bounds__(NTH, 1) void k_pdream(PDreamArgs g) {
+__device__ __forceinline__ void pdream_body(const PDreamArgs& g) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int s_ok;
   const int B = g.B, H = g.H, A = g.A;
@@ -880,6 +881,15 @@ __global__ __launch_bounds__(NTH, 1) void k_pdream(PDreamArgs g) {
   }
 }
 
+// every workgroup leaves through ps_exit (also after a timed-out wait): the
+// last one NaN-fills latents / hiddens / actions / mus / sigmas and the fault
+// slot on a timeout
+template <int NT, int MR>
+__global__ __launch_bounds__(NTH, 1) void k_pdream(PDreamArgs g) {
+  pdream_body<NT, MR>(g);
+  ps_exit(g.cnt + CNT_LD * (CNT_BLOCKS * C_STATUS + 1), g.cnt + CNT_LD * CNT_BLOCKS * C_STATUS, g.pz);
+}
+
 // ---------------------------------------------------------------------------
 static size_t pdream_lds_bytes(int A) {
   return sizeof(float) * ((((size_t)(LAT + A) * WLD + 3) & ~(size_t)3) + SCR_F + 64);
@@ -957,8 +967,19 @@ int op_pdream(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, in
   a.wmu = ac->mu.w; a.bmu = ac->mu.b; a.wls = ac->ls.w; a.bls = ac->ls.b;
   a.idx0 = idx0; a.noise = noise; a.nq = nq;
   a.unimix = (float)(0.01 * (1.0 / d->cols));
-  a.spin_limit = 1 << 22;
+  a.spin_limit = ps_spin_limit("dream");
   a.latents = latents; a.hiddens = hiddens; a.actions = actions; a.mus = mus; a.sigmas = sigmas;
+  {
+    const unsigned long long BH = (unsigned long long)B * H;
+    float* const outs[5] = {latents, hiddens, actions, mus, sigmas};
+    const unsigned long long ns[5] = {(unsigned long long)B * (H + 1) * LAT, (unsigned long long)B * (H + 1) * HD,
+                                      BH * A, BH * A, BH * A};
+    for (int i = 0; i < 5; ++i) {
+      a.pz.p[i] = outs[i];
+      a.pz.n[i] = ns[i];
+    }
+    a.pz.fault = d->fault;
+  }
   a.eps = tp.eps; a.ls_raw = tp.ls_raw; a.pre1a = tp.pre1a; a.x1a = tp.x1a; a.pre2a = tp.pre2a; a.x2a = tp.x2a;
   a.tr = tp.r; a.tu = tp.u; a.tn = tp.n; a.tghn = tp.ghn; a.pre1p = tp.pre1p; a.pre2p = tp.pre2p; a.soft = tp.soft;
   char* base = reinterpret_cast<char*>(ws);

@@ -1220,3 +1220,18 @@ extern "C" int dr_actor_act(const dr_dims* d, const dr_actor* ac, int B, const f
   return op_actor_head(B, A, mu_out, A, ls, A, &noise, 0, deterministic, a_out, A, nullptr, 0, sigma_out, A, nullptr,
                        s);
 }
+
+// which entry points of one train_Agent epoch run as their ONE persistent
+// launch for these dims and shapes (stream CU masks aside): bit 0 the warm
+// start's posterior scan (T = S / 2 steps), bit 1 the imagination unroll, bit 2
+// the BPTT.  The data-parallel schedule (dreamer_amd/engine.py) keeps
+// collective kernels away from a persistent BPTT with it.
+extern "C" int dr_persistent_kernels(const dr_dims* d, int B, int T, int H) {
+  if (!d || B <= 0 || T <= 0 || H <= 0) return 0;
+  const int A = d->action;
+  int m = 0;
+  if (op_pscan_supported(d, B, T, A)) m |= 1;
+  if (d->rows <= 32 && d->actor_h1 % 4 == 0 && op_pdream_supported(d, B, H, A)) m |= 2;
+  if (op_pbptt_supported(d, B, H, A)) m |= 4;
+  return m;
+}

@@ -124,8 +124,13 @@ __device__ __forceinline__ ps_u64 ps_gld(const ps_u64* p) {
   return __hip_atomic_load(const_cast<ps_u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// lane 0 of the workgroup: poll until *c >= target (relaxed sc1 loads + s_sleep)
+// lane 0 of the workgroup: poll until *c >= target (relaxed sc1 loads + s_sleep).
+// limit < 0 (DREAMER_PERSIST_FORCE, the failure-path test hook): every poll times out
 __device__ __forceinline__ bool ps_poll(const unsigned* c, unsigned target, int limit, unsigned* status) {
+  if (limit < 0) {
+    __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+  }
   int spins = 0;
   while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
     __builtin_amdgcn_s_sleep(2);
@@ -165,6 +170,46 @@ __device__ __forceinline__ bool ps_wait(int* s_ok, const unsigned* c0, int ld, i
   __syncthreads();
   return *s_ok != 0;
 }
+// The failure path of a persistent launch.  Every workgroup ends in ps_exit,
+// also after a timed-out wait; the LAST one to arrive (an exit ticket) reads
+// the status word and, if any wait timed out, writes NaN over the launch's
+// outputs and the caller's fault slot (dr_dims.fault).  A partly written result
+// therefore never passes for a valid one: NaN flows into the losses, the
+// agent's non-finite skip (Agent.py:137-139, dr_clip_stats over the loss slots,
+// which include the fault slot) rejects the update, and the host raises when it
+// reads the slot (engine.py check_faults).  The fault slot is sticky: the
+// library never clears it.
+struct PsPoison {
+  float* p[8];
+  unsigned long long n[8];  // floats at p[i]
+  float* fault;
+};
+__device__ __forceinline__ void ps_exit(unsigned* ticket, const unsigned* status, const PsPoison& pz) {
+  __shared__ int s_last;
+  ps_drain();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = t + 1u == gridDim.x &&
+             __hip_atomic_load(const_cast<unsigned*>(status), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const float nan = __builtin_nanf("");
+#pragma unroll 1
+  for (int i = 0; i < 8; ++i) {
+    float* p = pz.p[i];
+    if (!p) continue;
+    for (unsigned long long x = threadIdx.x; x < pz.n[i]; x += blockDim.x) p[x] = nan;
+  }
+  if (pz.fault && threadIdx.x == 0) *pz.fault = nan;
+}
+// the spin limit of a persistent launch: DREAMER_PERSIST_FORCE=timeout (or
+// the kernel's name: scan / dream / bptt) makes every wait of that kernel time
+// out at once (test hook of the failure path, read at each call like
+// DREAMER_ACT_FORCE; a captured graph keeps the value of its capture)
+int ps_spin_limit(const char* kernel);
+
 // every storing wave drained; lanes 0 .. n-1 add 1 to counters c0, c0 + ld, ...
 __device__ __forceinline__ void ps_signal_n(unsigned* c0, int ld, int n) {
   ps_drain();

@@ -48,6 +48,7 @@
 #include "persist.h"
 #include "ops.h"
 
+#include <stdlib.h>
 #include <string.h>
 #include <algorithm>
 
@@ -60,7 +61,7 @@ constexpr int KSW3 = 2;    // 32-k steps per wave over K = EH (7 over 4 waves)
 constexpr int KP3 = 232;   // LDS row stride of the LN-SiLU rows (8 mod 16 dwords)
 constexpr int SCR_F = 8192;  // scratch floats (32 KB): idx/zval staging, K-split partials, LN rows
 constexpr int CNT_LD = 32;   // counters 128 B apart
-constexpr int CNT_H = 0, CNT_PRE = 16, CNT_Z = 32, CNT_STATUS = 48;
+constexpr int CNT_H = 0, CNT_PRE = 16, CNT_Z = 32, CNT_STATUS = 48, CNT_EXIT = 49;
 }  // namespace
 
 
@@ -91,6 +92,7 @@ struct alignas(16) PScanArgs {
   unsigned* cnt;  // counters, status
   unsigned long long* zg;  // [B][NR] z granules {zval bits | step + 1 | class} (S3 -> S1)
   long long* ts;  // DR_PSCAN_TS builds: [64 steps][3 stages][8 marks][grid] wall-clock stamps
+  PsPoison pz;    // outputs NaN-filled on a timeout (persist.h ps_exit)
 };
 #ifdef DR_PSCAN_TS
 #define PS_TS(st, mk) \
@@ -102,7 +104,7 @@ struct alignas(16) PScanArgs {
 #endif
 
 template <int NT, int MR, int MS>
-__global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
+__device__ __forceinline__ void pscan_body(const PScanArgs& g) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int s_ok;
   const int B = g.B, T = g.T, A = g.A;
@@ -609,6 +611,20 @@ __global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
   }
 }
 
+// every workgroup leaves through ps_exit (also after a timed-out wait): the
+// last one NaN-fills z_out / h_out / logits_out and the fault slot on a timeout
+template <int NT, int MR, int MS>
+__global__ __launch_bounds__(NTH, 1) void k_pscan(PScanArgs g) {
+  pscan_body<NT, MR, MS>(g);
+  ps_exit(g.cnt + CNT_LD * CNT_EXIT, g.cnt + CNT_LD * CNT_STATUS, g.pz);
+}
+
+int ps_spin_limit(const char* kernel) {
+  const char* f = getenv("DREAMER_PERSIST_FORCE");
+  if (f && (strcmp(f, "timeout") == 0 || strcmp(f, kernel) == 0)) return -1;
+  return 1 << 22;
+}
+
 static size_t pscan_lds_bytes(int A) {
   return sizeof(float) * ((((size_t)(LAT + A) * WLD + 3) & ~(size_t)3) + SCR_F + 64);
 }
@@ -685,8 +701,12 @@ int op_pscan(const dr_dims* d, const dr_world_model* wm, int B, int T, int A, co
   a.feat = feat; a.act = actions; a.act_sb = act_sb; a.act_st = act_st;
   a.noise = noise;
   a.unimix = (float)(0.01 * (1.0 / d->cols));
-  a.spin_limit = 1 << 22;
+  a.spin_limit = ps_spin_limit("scan");
   a.z_out = z_out; a.h_out = h_out; a.logits_out = logits_out;
+  a.pz.p[0] = z_out; a.pz.n[0] = (unsigned long long)B * LAT;
+  a.pz.p[1] = h_out; a.pz.n[1] = (unsigned long long)B * HD;
+  a.pz.p[2] = logits_out; a.pz.n[2] = logits_out ? (unsigned long long)B * LAT : 0ull;
+  a.pz.fault = d->fault;
   a.hb = reinterpret_cast<float*>(base);
   a.pre = a.hb + (size_t)2 * B * HD;
   a.iz = reinterpret_cast<int*>(a.pre + (size_t)2 * B * EH);

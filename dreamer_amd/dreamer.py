@@ -180,13 +180,15 @@ class Dreamer(nn.Module):
 
     def train_Agent(self):
         """Dreamer.train_Agent (Dreamer.py:264-287): AC_epochs fused epochs."""
-        if self.AC_epochs > 1 and self.pipeline_epochs:
+        if self.AC_epochs > 1 and self.pipeline_epochs and not self.engine.persistent_chain():
             # config key pipeline_epochs (default on): the epochs' window
             # starts are drawn up front (same np.random order); the warm start
-            # of epoch e+1 then overlaps epoch e's update (engine.run_many).
-            # (Round 2 kept it off after epoch-2 mismatches inside the fake-env
-            # train_dreamer flow; the cause -- memset / memcpy2D nodes not
-            # re-executing on graph replay -- was fixed in round 3, DESIGN.md 5a)
+            # of epoch e+1 then overlaps epoch e's update (engine.run_many),
+            # bit for bit the sequential launch-form epochs.  Where the chain
+            # runs as the persistent kernels (B <= 128 per GPU) the sequential
+            # epochs below are faster (a persistent kernel needs every CU, so
+            # it cannot share the chip with an overlapped warm start; measured
+            # in bench.py's configs1_B64_ac_epochs2, DESIGN.md section 5a)
             B = self.batch_size if self.world is None else self.engine.B
             starts = [self.buffer.sample_start_indices(B) for _ in range(self.AC_epochs)]
             losses = self.engine.run_many(starts)

@@ -21,6 +21,7 @@ between the phase graphs.
 """
 import contextlib
 import gc
+import math
 
 import numpy as np
 
@@ -88,6 +89,15 @@ class ImaginationEngine:
         self.side = torch.cuda.Stream(self.dev)
         self.chunks = [(0, self.T)]
         self._alloc()
+        # persistent-kernel fault checks (dr_dims.fault): after every run / run_many
+        # the agent's fault slot is copied to pinned host memory on a stream of its
+        # own (nothing added to the epoch's stream); the copies are read when they
+        # are two calls old (check_faults), so the host never waits on the epoch it
+        # just queued
+        self._fs = torch.cuda.Stream(self.dev)
+        self._fault_pins = [torch.zeros(1).pin_memory() for _ in range(8)]
+        self._fault_i = 0
+        self._fault_pending = []
 
     # ------------------------------------------------------------------ setup
     @staticmethod
@@ -325,14 +335,69 @@ class ImaginationEngine:
               ("returns", self.returns, self._allgather_R if self.dp else None),
               ("update", self._ph_update, self._allreduce_grads if self.dp else None),
               ("optim", self._ph_optim, None)]
-        if self.dp:
-            # data-parallel: the update in two phase graphs, so that the
-            # critic's gradient all-reduce (issued async on RCCL's stream as
-            # soon as the critic backward is enqueued) runs under the actor's
-            # BPTT; the actor part is reduced after it (Agent.py:141-148)
+        if self.dp and not self.persistent_bptt():
+            # data-parallel, BPTT in launch form: the update in two phase graphs,
+            # so that the critic's gradient all-reduce (issued async on RCCL's
+            # stream as soon as the critic backward is enqueued) runs under the
+            # actor's BPTT; the actor part is reduced after it (Agent.py:141-148).
+            # With the persistent BPTT (B <= 64 per rank) the update stays one
+            # phase and the whole buffer is reduced after it: an RCCL kernel
+            # holding CUs beside k_pbptt (one workgroup on every CU) could push
+            # its waits past their bound
             ph[3:4] = [("critic", self._ph_critic, self._allreduce_critic_async),
                        ("actor", self._ph_actor, self._allreduce_actor)]
         return ph
+
+    def persistent_chain(self):
+        """True when the imagination unroll (and the warm start's scan) run as
+        the persistent kernels: train_Agent then keeps its epochs sequential."""
+        return bool(L.query("dr_persistent_kernels", self.d, self.B, self.T, self.H) & 2)
+
+    def persistent_bptt(self):
+        """True when dr_imagine_bwd runs as the one persistent k_pbptt launch."""
+        return bool(L.query("dr_persistent_kernels", self.d, self.B, self.T, self.H) & 4)
+
+    # ------------------------------------------------------- fault checks
+    def _fault_note(self):
+        """Queue the copy of the fault slot behind the work issued so far."""
+        main = torch.cuda.current_stream(self.dev)
+        self._fs.wait_stream(main)
+        pin = self._fault_pins[self._fault_i % len(self._fault_pins)]
+        self._fault_i += 1
+        with torch.cuda.stream(self._fs):
+            pin.copy_(self.dr.agent.fault_slot(), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._fs)
+        self._fault_pending.append((ev, pin))
+
+    def check_faults(self, keep=0):
+        """Read the queued fault-slot copies, all but the newest `keep` (waiting
+        for them).  A NaN slot means a persistent kernel (posterior scan,
+        imagination unroll or BPTT) timed out on a wait: its outputs were
+        written NaN and that epoch's update was skipped on every rank
+        (non-finite skip, Agent.py:137-139).  Then the slot is cleared, every
+        later epoch runs the launch form (new graphs), and RuntimeError is
+        raised."""
+        while len(self._fault_pending) > keep:
+            ev, pin = self._fault_pending.pop(0)
+            ev.synchronize()
+            if not math.isfinite(float(pin[0])):
+                self._on_fault()
+
+    def _on_fault(self):
+        for ev, _ in self._fault_pending:
+            ev.synchronize()
+        self._fault_pending = []
+        ag = self.dr.agent
+        torch.cuda.current_stream(self.dev).synchronize()
+        ag.fault_slot().zero_()
+        ag.persistent_ok = False
+        self.d = self.dims()
+        self.graph, self.graph_key, self._pipe = None, None, None
+        raise RuntimeError("dreamer_amd: a persistent kernel (posterior scan / imagination unroll / BPTT) timed out "
+                           "waiting on another workgroup (not every workgroup was resident, e.g. other work held "
+                           "CUs); its outputs were NaN and that epoch's actor-critic update was skipped. Every "
+                           "later epoch runs the launch form.")
 
     def _ph_critic(self):
         """DP update, part 1: online critic forward, update_S, the actor loss
@@ -399,6 +464,7 @@ class ImaginationEngine:
         """One train_Agent epoch from host window starts; returns the device
         loss slots (actor, critic).  With timing=True, HIP events bracket every
         phase (self.last_events)."""
+        self.check_faults(keep=1)
         i = self.epochs & 1
         if self.copy_ev[i] is not None:
             self.copy_ev[i].synchronize()
@@ -426,6 +492,7 @@ class ImaginationEngine:
                 e.record()
                 evs.append(e)
         self.last_events = evs
+        self._fault_note()
         return ag.loss_slot(0), ag.loss_slot(1)
 
     def phase_ms(self):
@@ -439,9 +506,15 @@ class ImaginationEngine:
     # ring, the window starts, its own noise) is untouched by the actor-critic
     # update, so the warm start of epoch e+1 (conv encoder + posterior scan)
     # can run on a second stream beside the imagination / update chain of
-    # epoch e.  The results are those of the sequential epochs bit for bit:
+    # epoch e.  The results are those of the sequential LAUNCH-FORM epochs bit
+    # for bit (test_pipelined_epochs_match_sequential, DREAMER_PERSISTENT=0):
     # the warm start keeps its own copy of the Philox state, advanced once per
-    # epoch like the main one, and (z0, h0) are double-buffered.
+    # epoch like the main one, and (z0, h0) are double-buffered.  Every graph
+    # here is captured in launch form (a persistent kernel needs every CU);
+    # the sequential run() at B <= 128 uses the persistent kernels, whose
+    # LayerNorm sums run in another order, so there the two agree to rounding
+    # -- and Dreamer.train_Agent does not pipeline where the chain is
+    # persistent (persistent_chain).
     def warm_stream(self, cu_fraction=None):
         """The stream of the pipelined warm start: a plain torch stream, or with
         cu_fraction in (0, 1) a HIP stream restricted to that share of the CUs
@@ -529,6 +602,7 @@ class ImaginationEngine:
     def run_many(self, starts_list):
         """len(starts_list) consecutive train_Agent epochs, pipelined (see
         above).  Returns a [K, 2] device tensor of (actor, critic) losses."""
+        self.check_faults(keep=1)
         ag = self.dr.agent
         key = (ag.params_key(), self.dr.world_model.params_key(), self.dr.buffer.device_key())
         P = self._pipe_capture(key)
@@ -551,8 +625,10 @@ class ImaginationEngine:
             with torch.cuda.stream(P["chain"]):
                 losses = self._run_many(P, G, starts_list, P["chain"])
             outer.wait_stream(P["chain"])
-            return losses
-        return self._run_many(P, G, starts_list, outer)
+        else:
+            losses = self._run_many(P, G, starts_list, outer)
+        self._fault_note()
+        return losses
 
     def _run_many(self, P, G, starts_list, main):
         import os

@@ -69,6 +69,10 @@ class WorldModel(nn.Module):
         # DREAMER_PERSISTENT=0: every entry point as its launch sequence (A/B of the persistent kernels)
         d.launch_form = 1 if os.environ.get("DREAMER_PERSISTENT", "1") == "0" else 0
         if agent is not None:
+            if not agent.persistent_ok:
+                d.launch_form = 1
+            if agent.grad_buffer.is_cuda:
+                d.fault = agent.fault_slot().data_ptr()
             a, c = agent.actor.base_net, agent.critic.value_net
             d.actor_h1, d.actor_h2 = a[0].out_features, a[3].out_features
             d.critic_h1, d.critic_h2 = c[0].out_features, c[3].out_features

@@ -80,6 +80,15 @@ typedef struct {
                           stream's CUs allow it (the warm start's posterior scan, scan.hip); 1: always the
                           launch sequence.  Set for work captured on one stream and replayed on a CU-masked
                           one (the pipelined epochs' warm start), and by DREAMER_PERSISTENT=0. */
+  float* fault;        /* device float, may be NULL: the fault slot of the persistent launches (posterior
+                          scan, imagination unroll, BPTT).  Their waits on other workgroups are bounded; if
+                          one times out (a workgroup was not resident, e.g. held off by other work on the
+                          CUs), the launch's outputs are written NaN and *fault = NaN.  Sticky: the library
+                          never clears it.  The engine keeps it among the agent's loss slots, so the
+                          non-finite skip (Agent.py:137-139) rejects that epoch's update on every rank, and
+                          the host raises when it reads it (dreamer_amd/engine.py check_faults).  Test hook:
+                          DREAMER_PERSIST_FORCE=timeout (or scan / dream / bptt) makes every wait of those
+                          launches time out, read at each call. */
 } dr_dims;
 #define DR_MAX_DEPTH 5
 #define DR_PREC_FP32 0
@@ -380,6 +389,13 @@ int dr_replay_gather(long long cap, int B, int S, int frame_elems, int A, const 
                      const float* actions, const float* rewards, const float* continues,
                      const long long* starts, float* obs_out, float* act_out, float* rew_out,
                      float* cont_out, hipStream_t stream);
+
+/* Which parts of a train_Agent epoch (Dreamer.py:264-287) run as ONE persistent
+ * launch for these dims and shapes (the stream's CU mask aside): bit 0 the warm
+ * start's posterior scan over T steps (Dreamer.py:255-261), bit 1 the
+ * imagination unroll (Dreamer.py:158-164), bit 2 its BPTT (Agent.py:141-145
+ * backward).  0 when dims->launch_form is set. */
+int dr_persistent_kernels(const dr_dims* d, int B, int T, int H);
 
 /* Philox offset bump (keeps graph replays drawing fresh noise) */
 int dr_rng_advance(unsigned long long* rng, unsigned long long delta, hipStream_t stream);

@@ -30,7 +30,7 @@ import torch
 
 from baseline_case import oracle_epoch, regen_fixture
 from conftest import load_fixture, state_layout
-from gpu_helpers import close, cpu
+from gpu_helpers import pdream_status, pscan_status, close, cpu
 from oracle import dreamer_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -167,34 +167,6 @@ def test_baseline_b16_vs_reference(gpu):
     assert np.array_equal(cpu(eng.z0).reshape(-1, C).argmax(-1).numpy(), fx["z0_idx"].astype(np.int64))
     assert abs(pre["la"] - float(fx["loss_actor"])) <= 1e-4 * abs(float(fx["loss_actor"]))
     assert abs(pre["S"] - float(fx["S_after"])) <= 1e-6 * float(fx["S_after"])
-
-
-def pscan_status(eng):
-    """Status word of the persistent posterior scan (scan.hip counter block in
-    the observe workspace's ring): 0 = every hand-off completed in time."""
-    B = eng.B
-    off = 4 * (2 * B * 600 + 2 * B * 200 + 4 * B * 32) + 48 * 128
-    return int(eng.ws_obs.view(torch.uint8)[off:off + 4].view(torch.int32).item())
-
-
-def pdream_status(eng):
-    """Status word of the persistent imagination unroll (dream.hip: its
-    counter block closes the imagination workspace): 0 = every hand-off
-    completed in time."""
-    from dreamer_amd import _lib as L
-    B, H = eng.B, eng.H
-    total = L.query("dr_imagine_workspace_bytes", eng.d, B, H)
-    pd = 4 * H * B * 200 + 8 * (H + 1) * B * 32
-    pb = (4 * B * H * (4 * 200 + 200 + 2 * 1800 + 600 + 1664 + 2 * 200 + 1024 + 600) + 8 * 8 * 32 * 4) if B <= 64 else 0
-    cnt = (total - pb) - 7 * 16 * 32 * 4  # the unroll's block ends where the BPTT's starts (256-byte multiples)
-    word = lambda o: int(eng.ws_im.view(torch.uint8)[o:o + 4].view(torch.int32).item())
-    # (status, the GRU stage's counter of rows 0..15: 60 unit slices x H steps when it ran), and, at
-    # B <= 64, the BPTT's (status, Q7's counter of rows 0..15: 51 column blocks x H steps)
-    st = (word(cnt + 6 * 16 * 32 * 4), word(cnt + 2 * 16 * 32 * 4))
-    if B <= 64:
-        pcnt = total - 8 * 8 * 32 * 4
-        st += (word(pcnt + 7 * 8 * 32 * 4), word(pcnt + 6 * 8 * 32 * 4))
-    return st
 
 
 @pytest.mark.parametrize("B,data", [(64, "synthetic"), (128, "synthetic"), (256, "synthetic"), (512, "synthetic"),

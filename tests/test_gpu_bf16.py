@@ -139,6 +139,8 @@ def test_train_agent_bf16_epoch_vs_oracle(B, gpu):
     torch.set_num_threads(16)
     ref = oracle_epoch(P, obs, act, S, H, R, C, q_warm, eps, q, S0, guard=TieGuard(BF16_TIE_REL, BF16_TIE_SCALE))
     eng, pre = run_gpu_epoch(d, frames, acts, rews, conts, n, 0, starts, q_warm, eps, q, S0)
+    from gpu_helpers import assert_persistent_ran
+    assert_persistent_ran(eng)  # B = 64: scan, unroll and BPTT ran persistent, status 0
     ag = d.agent
     m = {}
     zw = (eng.z0.cpu().reshape(-1, C).argmax(-1) != ref["z0"].reshape(-1, C).argmax(-1)).float().mean()

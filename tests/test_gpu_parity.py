@@ -281,3 +281,43 @@ def test_update_S_quantile_exact(n, gpu):
     L.call("dr_update_S", n, L.ptr(Rn.to(gpu)), L.ptr(Sd), None, None, 0, 0)
     torch.cuda.synchronize()
     assert float(Sd) == 2.0
+
+
+def test_pipelined_engine_dropped_then_new_capture(gpu):
+    """Regression test of the round-5 r05a abort: a
+    segfault in the first pipelined test after f76c296 made every engine
+    destroy its CU-masked warm stream when it was collected.  torch's caching
+    allocator still held blocks allocated on that stream (the window starts
+    and Philox copies run_many stages on it), and the next allocation that
+    reused them touched the destroyed stream.  Since b2e3f22 one masked stream
+    per (device, mask) lives for the process (engine._CU_STREAMS).  Here: an
+    engine with pipelined graphs is built, run and dropped, the collector runs
+    and the cache is emptied; a second engine then captures and runs both its
+    pipelined and its sequential graphs, finite, on the same masked stream."""
+    import gc
+    from dreamer_amd import engine as E
+    from formula import replay_data
+    fx = load_fixture("small_epoch")
+    B, S, H, K = 8, 8, 5, 3
+    handles = []
+    for rep in range(2):
+        d, P = build("small", gpu, fx, B=B, S=S, H=H)
+        fr, ac, rw, ct = replay_data(64, (32, 32), 3, seed=3)
+        d.buffer.load_arrays(fr, ac, O.symlog(torch.tensor(rw)).numpy(), ct)
+        eng = E.ImaginationEngine(d)
+        np.random.seed(5 + rep)
+        losses = eng.run_many([d.buffer.sample_start_indices(B) for _ in range(K)])
+        la, lc = eng.run(d.buffer.sample_start_indices(B))
+        torch.cuda.synchronize()
+        assert torch.isfinite(losses).all() and bool(torch.isfinite(la).all()) and bool(torch.isfinite(lc).all())
+        handles.append(eng._pipe["stream"].cuda_stream)
+        eng.check_faults()
+        del d, P, eng, losses, la, lc
+        gc.collect()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        # new allocations reuse the blocks the dropped engine used on the masked stream
+        junk = [torch.empty(1 << 20, device=gpu) for _ in range(8)]
+        del junk
+    assert handles[0] == handles[1], "the masked warm stream must be shared for the process"
+    assert handles[0] in [h.value for h in E._CU_STREAMS.values()]
