@@ -146,9 +146,7 @@ __global__ __launch_bounds__(256) void k_conv1_bf16(int n, int nb, int h, int w,
     }
 }
 
-#ifndef DR_E12B_WAVES
-#define DR_E12B_WAVES 4  // A/B knob (tools/build_variant.py): 8 waves measured slower (172 VGPRs, one workgroup per CU)
-#endif
+#define DR_E12B_WAVES 4  // 8 waves measured slower (172 VGPRs, one workgroup per CU)
 // ---------------------------------------------------------------------------
 // conv1 + conv2 fused (enc_f1 = 32 -> enc_f2 = 64): a workgroup owns R2 rows of
 // conv2 output (128 pixels); it stages the u8 input rows they depend on, runs

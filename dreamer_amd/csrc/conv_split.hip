@@ -68,12 +68,8 @@ __device__ __forceinline__ u32x2 pack_bf16x4(f32x4 v) {
 __device__ __forceinline__ unsigned pack_bf16x2(float x0, float x1) { return b16bits((__bf16)x0) | (b16bits((__bf16)x1) << 16); }
 }  // namespace
 
-// A/B knobs (MI355X guide T5): DR_CONV_PRIO 1 = s_setprio(1) around each
-// chunk's MFMA cluster; 2 = the static form, priority 1 for the younger half
-// of the workgroup's waves before the main loop
-#ifndef DR_CONV_PRIO
-#define DR_CONV_PRIO 0
-#endif
+// (s_setprio around each chunk's MFMA cluster, or for the younger half of the
+// waves, measured neutral to slower: profiles/r04zm_conv_prio_ab.txt)
 // EPI (conv.h): CONV_EPI_FWD: out = SiLU(acc + bias), optionally pre = acc + bias
 // (NHWC, for the world-model backward); CONV_EPI_DSILU (NHWC only, no bias):
 // out = acc * SiLU'(pre) -- the input gradient of a transposed conv followed by
@@ -263,7 +259,6 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
 #define DR_S3(PA, PB)                                                                                   \
   _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
       OUT_NCHW ? mfma_b16(a[PA][i], b[PB][j], acc[i][j]) : mfma_b16(b[PB][j], a[PA][i], acc[i][j]);
-    if (DR_CONV_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     if constexpr (NT3 == 3) {
       DR_S3(2, 0)
       DR_S3(1, 1)
@@ -272,13 +267,11 @@ __global__ __launch_bounds__(BM * 2) void k_conv_split3(int n_frames, int ih, in
       DR_S3(0, 1)
     }
     DR_S3(0, 0)
-    if (DR_CONV_PRIO == 1) __builtin_amdgcn_s_setprio(0);
 #undef DR_S3
     if (c + 1 < NCH) store(Next{}, buf ^ 1);
     dr_lds_barrier();
   };
   static_assert(PIPE == 2 && NCH % 2 == 0, "conv_split3 ring");
-  if (DR_CONV_PRIO == 2 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= NT / 2) __builtin_amdgcn_s_setprio(1);
   for (int c = 0; c < NCH; c += 2) {
     step(c, S0{});
     step(c + 1, S1{});
@@ -389,9 +382,6 @@ int op_conv_repack_split3(int cout, int cin, const float* w, void* wr, hipStream
 // distinct bank quads, as in k_enc12_bf16), 110.8 KB; input rows 20 KB;
 // weight ring 2 x 12 KB.  One workgroup per CU.
 // ---------------------------------------------------------------------------
-#ifndef DR_E12_WAVES
-#define DR_E12_WAVES 8  // A/B knob (tools/build_variant.py): 4 = one wave per SIMD
-#endif
 #define E12_R2 8
 #define E12_R1 (2 * E12_R2 + 2)
 #define E12_RI (2 * E12_R1 + 2)
@@ -415,12 +405,8 @@ static constexpr size_t e12_lds_bytes(int terms = 3) {
 // 4 waves, two workgroups per CU (57 KB of LDS each; 164 VGPRs, no spill):
 // encoder 0.936 ms; 8 waves at two workgroups per CU (128 VGPRs, 104 B spilled)
 // 1.01-1.02 ms; 8 waves at one (165 VGPRs) 0.962 ms
-#ifndef DR_E12S1_WAVES
-#define DR_E12S1_WAVES 4  // A/B knob: waves per workgroup of the one-term form
-#endif
-#ifndef DR_E12S1_OCC
-#define DR_E12S1_OCC 2  // A/B knob: min waves per SIMD of the one-term form
-#endif
+#define DR_E12S1_WAVES 4  // waves per workgroup of the one-term form
+#define DR_E12S1_OCC 2    // min waves per SIMD of the one-term form
 // O16 = false with NTM = 1: the bf16 world-model step's form -- one term, f32
 // output and the saves
 template <int NW, int NTM = 3, bool O16 = (NTM == 1)>
@@ -603,7 +589,6 @@ __global__ __launch_bounds__(64 * NW, NTM == 1 ? DR_E12S1_OCC : 1) void k_enc12_
 #define E12_S3(PW, PA)                       \
   _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int jj = 0; jj < 2; ++jj) acc[i][jj] = \
       mfma_b16(wf[PW][jj], pf[PA][i], acc[i][jj]);
-      if (DR_CONV_PRIO == 1) __builtin_amdgcn_s_setprio(1);
       if constexpr (NTM == 3) {
         E12_S3(2, 0)
         E12_S3(1, 1)
@@ -612,10 +597,8 @@ __global__ __launch_bounds__(64 * NW, NTM == 1 ? DR_E12S1_OCC : 1) void k_enc12_
         E12_S3(0, 1)
       }
       E12_S3(0, 0)
-      if (DR_CONV_PRIO == 1) __builtin_amdgcn_s_setprio(0);
 #undef E12_S3
     };
-    if (DR_CONV_PRIO == 2 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= NTH / 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll 1
     for (int tap = TAPS * kh; tap < TAPS * (kh + 1); ++tap) {
       tap_step(tap, wfa, wfb);
@@ -745,12 +728,9 @@ int op_enc12_split3_ex(int n, int nb, int h, int w, int c1, int c2, const dr_fra
   if (dev < 0 || dev >= 64) return DR_E_INVALID;
   if (cus[dev] == 0) DR_TRY_HIP(hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev));
   const int grid = std::min(n * 2, std::max(1, cus[dev]));
-  if (DR_E12_WAVES == 8)
-    hipLaunchKernelGGL(k_enc12_split3<8>, dim3((unsigned)grid), dim3(512), e12_lds_bytes(), s, n, nb, *src,
-                       (const u16*)wr1, b1, (const u16*)wr2, b2, out, pre0, a0, pre1);
-  else
-    hipLaunchKernelGGL(k_enc12_split3<4>, dim3((unsigned)grid), dim3(256), e12_lds_bytes(), s, n, nb, *src,
-                       (const u16*)wr1, b1, (const u16*)wr2, b2, out, pre0, a0, pre1);
+  // 8 waves (two per SIMD); one wave per SIMD measured 517.0 k against 532.9 k (r03o)
+  hipLaunchKernelGGL(k_enc12_split3<8>, dim3((unsigned)grid), dim3(512), e12_lds_bytes(), s, n, nb, *src,
+                     (const u16*)wr1, b1, (const u16*)wr2, b2, out, pre0, a0, pre1);
   return dr_check_launch("enc12_split3");
 }
 

@@ -7,24 +7,6 @@
 #include "dream.h"
 #include "bptt.h"
 
-#ifndef DR_B16_CHAIN_WKS
-#define DR_B16_CHAIN_WKS 1  // A/B knob: bf16 mode's per-step grouped products on bf16 weight planes
-#endif
-#ifndef DR_GRU_BWD_EPI
-#define DR_GRU_BWD_EPI 1  // A/B knob: 0 = the GRU backward as its own elementwise launch
-#endif
-#ifndef DR_PSCAN
-#define DR_PSCAN 1  // A/B knob: 0 = the warm start's posterior scan as three launches per step
-#endif
-#ifndef DR_PDREAM
-#define DR_PDREAM 1  // A/B knob: 0 = the imagination unroll as seven launches per step
-#endif
-#ifndef DR_A0_PLANES
-#define DR_A0_PLANES 1  // A/B knob: 0 = the BPTT's actor input gradient on the staged skinny path
-#endif
-#ifndef DR_PBPTT
-#define DR_PBPTT 1  // A/B knob: 0 = the BPTT reverse loop as seven launches per step
-#endif
 
 // fp32 mode, tall batches: the first Linear of a head over [h | z] on the
 // split3 bf16 MFMA (conv_split.hip) when the workspace holds its weight planes
@@ -302,7 +284,7 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
     DR_TRY(op_transpose(3 * Hd, L + d->action, wm->w_ih, w.wt, s));
   }
   // the warm start (no z_init / h_init) as ONE persistent launch (scan.hip)
-  if (DR_PSCAN && z_init == nullptr && h_init == nullptr && op_pscan_supported(d, B, T, d->action)) {
+  if (z_init == nullptr && h_init == nullptr && op_pscan_supported(d, B, T, d->action)) {
     const int rc = op_pscan(d, wm, B, T, d->action, feat, actions, act_sb, act_st, w.wt, wm->map0.w + F, F + Hd,
                             noise, 0, z_out, h_out, logits_out, w.ring, s);
     if (rc != DR_E_UNSUPPORTED) return rc;
@@ -327,7 +309,6 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
       // a time-chunked scan equals the whole-window scan bit for bit
       GemmArgs gh = lin(B, 3 * Hd, Hd, h_init, Hd, wm->w_hh, Hd, wm->b_hh, w.gh, 3 * Hd);
       wplanes(gh, w.s3whh);
-      if (!DR_B16_CHAIN_WKS) gh.bf16 = 0;
       DR_TRY(gemm_launch(G_NT, AM_PLAIN, &gh, 1, s));
       gh_pre = true;
     }
@@ -354,7 +335,6 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
         // bf16 mode: plane 0 times bf16-rounded h (k_gemm_wks3<1>); fp32 mode: the 3-term split
         wplanes(g[0], w.s3m0);
         wplanes(g[1], w.s3whh);
-        if (!DR_B16_CHAIN_WKS) g[0].bf16 = g[1].bf16 = 0;
       } else {
         g[0].bf16 = g[1].bf16 = 0;  // (bf16 mode: these products stay f32)
       }
@@ -561,7 +541,7 @@ static int imagine_launch_form(const dr_dims* d, const dr_world_model* wm, const
       // bf16 mode: on the weight planes the products run in bf16 (k_gemm_wks3<1>),
       // else they stay f32; fp32 mode: h_{t+1}'s split3 planes from the gates kernel
       for (int i = 0; i < np; ++i) {
-        if (!planes || !DR_B16_CHAIN_WKS) p[i].bf16 = 0;
+        if (!planes) p[i].bf16 = 0;
       }
       DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, np, s));
     }
@@ -635,7 +615,7 @@ extern "C" int dr_imagine_fwd(const dr_dims* d, const dr_world_model* wm, const 
   // the whole unroll as one persistent launch where the shape and the stream's
   // CUs allow it (dream.hip); the reward / continue heads below either way
   bool unrolled = false;
-  if (DR_PDREAM && zg && op_pdream_supported(d, B, H, A)) {
+  if (zg && op_pdream_supported(d, B, H, A)) {
     const PDreamTape pt = {tp.eps, tp.ls_raw, tp.pre1a, tp.x1a, tp.pre2a, tp.x2a, tp.r, tp.u, tp.n, tp.ghn,
                            tp.pre1p, tp.pre2p, tp.soft};
     const int rc = op_pdream(d, wm, ac, B, H, w.wt, w.tl0f + (long long)Hd * a1, w.idx[0], noise, nq, deterministic,
@@ -804,7 +784,7 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
   // the reverse loop as one persistent launch where the shape and the stream's
   // CUs allow it (bptt.hip); the weight gradients below either way
   bool looped = false;
-  if (DR_PBPTT && op_pbptt_supported(d, B, H, A)) {
+  if (op_pbptt_supported(d, B, H, A)) {
     const PBpttIO io = {w.tl6p, w.tl3p, w.tl0p, w.wt, w.twhh, w.thead, w.tl3a, w.tl0a,
                         tp.soft, tp.pre2p, tp.pre1p, tp.r, tp.u, tp.n, tp.ghn, tp.pre2a, tp.pre1a, tp.ls_raw, tp.eps,
                         hiddens, actions, g_mus, g_sigmas, w.gH, w.gZ, w.gA,
@@ -848,10 +828,7 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
       ge.r = tp.r + hb; ge.u = tp.u + hb; ge.n = tp.n + hb; ge.ghn = tp.ghn + hb;
       ge.gi = w.ggi; ge.gh = w.ggh; ge.ho = gH_t; ge.ldo = ldH; ge.Hd = Hd;
       DR_TRY(lnbwd_nt(B, Hd, h1, w.gx1, h1, tp.pre1p + (long long)t * B * h1, h1, wm->prior.n1, w.tl0p, gH_n, ldH, 1,
-                      w.gp1, h1, nullptr, nullptr, nullptr, 0, INT_MAX, s, DR_GRU_BWD_EPI ? &ge : nullptr));
-      if (!DR_GRU_BWD_EPI)
-        DR_TRY(op_gru_bwd(B, Hd, gH_n, ldH, hiddens + (long long)t * Hd, ldH, tp.r + hb, tp.u + hb, tp.n + hb,
-                          tp.ghn + hb, w.ggi, w.ggh, gH_t, ldH, 1, s));
+                      w.gp1, h1, nullptr, nullptr, nullptr, 0, INT_MAX, s, &ge));
       if (t > 0) {
         GemmArgs p[2];
         p[0] = bwd_nt(B, L + A, 3 * Hd, w.ggi, 3 * Hd, w.wt, gZ_t, ldL, 1);
@@ -879,7 +856,7 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
     // prologue also writes g_pre and the LN-parameter saves for the weight grads
     DR_TRY(lnbwd_nt(B, a1, a2, w.gx2a, a2, tp.pre2a + o2, lda2, ac->n4, w.tl3a, w.gx1a, a1, 0, w.gpre2a + o2, lda2,
                     w.gy2a + o2, w.xh2a + o2, nullptr, 0, INT_MAX, s));
-    if (t > 0 && planes && a1 % 8 == 0 && DR_A0_PLANES) {
+    if (t > 0 && planes && a1 % 8 == 0) {
       // B >= 128: the LN-SiLU backward as its own pass, then the K = a1 input
       // gradient [gH_t | gZ_t] on the wave-K split3 kernel (weight planes of
       // the transposed base_net.0, split once per call)

@@ -210,15 +210,12 @@ static inline int tn_launch(const GemmArgs* p, int n, void* ws, size_t ws_bytes,
 // per-step chain products on the bf16 MFMA (gemm.hip k_gemm_wks3): the weight
 // [N][K] (row stride ldw) split once per call into bf16 planes; wplanes() then
 // hands them to the problem
-#ifndef DR_WKS3_ENGINE
-#define DR_WKS3_ENGINE 1  // A/B knob: 0 = no weight planes (f32 wave-K kernel)
-#endif
 static inline int split_planes(int N, int K, const float* W, long long ldw, void* planes, hipStream_t s) {
-  if (!DR_WKS3_ENGINE || !planes) return DR_OK;
+  if (!planes) return DR_OK;
   return op_nt_repack_split3(N, K, W, (int)ldw, planes, s);
 }
 static inline void wplanes(GemmArgs& g, const void* planes) {
-  if (!DR_WKS3_ENGINE || !planes) return;
+  if (!planes) return;
   g.wsplit = reinterpret_cast<const unsigned short*>(planes);
   g.wsplit_np = (g.N + 127) / 128 * 128;  // op_nt_split3_ws_bytes' row padding
 }

@@ -89,12 +89,6 @@ struct GemmBf16Scope {
 };
 // Launch up to 4 problems sharing layout/A-mode in one dispatch.
 int gemm_launch(GemmLayout lay, int amode, const GemmArgs* probs, int count, hipStream_t s);
-#ifndef DR_BWD_WIDE
-#define DR_BWD_WIDE 1  // A/B knob: 0 = the staged backward prologues never on 32-column skinny tiles
-#endif
-#ifndef DR_BWD_ROWS16
-#define DR_BWD_ROWS16 1  // A/B knob: the staged backward prologues on 16-row tiles past 64 rows (+0.4 % at B = 256, r04d; the B = 512 mismatch of r04x was the 32-column tile, now excluded in try_skinny)
-#endif
 // true when AM_LNBWD / AM_STEBWD problems run on 16-row skinny tiles (K <= 1024)
 bool gemm_bwd_rows16(const GemmArgs* p, int count);
 

@@ -420,9 +420,7 @@ __device__ __forceinline__ void epilogue_store_b(const GemmArgs& g, int m, int n
   if (g.gb.Hd > 0 && n < g.gb.Hd) gru_bwd_elem(g.gb, m, n, fin);
 }
 
-#ifndef DR_SKW
-#define DR_SKW 8  // waves per skinny-GEMM workgroup (K split over them)
-#endif
+#define DR_SKW 8  // waves per skinny-GEMM workgroup (K split over them; 4 measured slower, r05)
 template <int MT, int NT, int AMODE, bool B_KN, bool VEC, int EPI>
 __global__ __launch_bounds__(64 * DR_SKW) void k_gemm_skinny(GemmBatch gb, int npack) {
   constexpr int NWAVE = DR_SKW, NTH = 64 * DR_SKW, FT = MT / 16, FN = NT / 16;
@@ -2084,7 +2082,7 @@ bool gemm_bwd_rows16(const GemmArgs* p, int count) {
     maxM = std::max(maxM, p[i].M);
     t16 += dr_cdiv(p[i].M, 16) * dr_cdiv(p[i].N, 16);
   }
-  return maxM <= 64 || (DR_BWD_ROWS16 && g_skinny_variant == 0 && maxM <= 4096 && t16 <= 640);
+  return maxM <= 64 || (g_skinny_variant == 0 && maxM <= 4096 && t16 <= 640);
 }
 
 template <int AMODE, bool B_KN>
@@ -2108,10 +2106,10 @@ static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
   // 16-row tiles past 64 rows while the grid stays within ~2.5 dispatch
   // rounds: a B = 256 per-step product (N = 200) then spreads over 208
   // workgroups instead of 52 (K = 1624: 19.3 -> 8.4 us, profiles/r02_kbench_B256.txt)
-  // (also the staged LayerNorm- and softmax-STE-backward prologues, DR_BWD_ROWS16:
+  // (also the staged LayerNorm- and softmax-STE-backward prologues:
   // at 64-row tiles a B = 256 LN-backward product ran on 52 workgroups, 16.5 us)
   if ((g_skinny_variant == 0 || g_skinny_variant == 5) && maxM > 64 &&
-      (AMODE == AM_PLAIN || AMODE == AM_LNSILU || (DR_BWD_ROWS16 && (AMODE == AM_LNBWD || AMODE == AM_STEBWD))) &&
+      (AMODE == AM_PLAIN || AMODE == AM_LNSILU || (AMODE == AM_LNBWD || AMODE == AM_STEBWD)) &&
       !(g_skinny_variant == 5 && epi == EPI_SAMPLE)) {
     int t16 = 0;
     for (int i = 0; i < count; ++i) t16 += dr_cdiv(gb.p[i].M, 16) * dr_cdiv(gb.p[i].N, epi == EPI_SAMPLE ? 32 : 16);
@@ -2129,7 +2127,6 @@ static bool try_skinny(const GemmBatch& gb, int count, hipStream_t s) {
   // would read the raw operand.  At K = 1024 (the STE backward of a 32 x 32
   // latent) the 32-column tile does not fit (48 x 1032 floats), so a B = 512
   // grid (416 16-column tiles) stays on 16 columns
-  if (!DR_BWD_WIDE && (AMODE == AM_LNBWD || AMODE == AM_STEBWD)) wide = false;
   if (AMODE == AM_LNBWD || AMODE == AM_STEBWD) {
     const int mt = maxM > 64 ? 64 : 16;
     for (int i = 0; i < count; ++i) {
@@ -2522,13 +2519,11 @@ static bool wks3_ok(const GemmBatch& gb, int count) {
 // planes measured slower, profiles/r04g_ab_wks3.txt, r04t_ab_aplanes.txt)
 // (r05w: 64-row tiles, each weight plane read by half as many row tiles,
 // measured slower -- 548 k vs 566 k fp32, 776 k vs 803 k bf16 at B = 256)
-#ifndef DR_WKS3_D
 // register-ring depth (K chunks in flight per wave).  1: the fp32 kernel at 83
 // VGPRs (4 waves per SIMD) instead of 140 (3), bf16 48 instead of 86 (7 / 4):
 // fp32 headline 581 -> 592 k, bf16 818 -> 828 k; depth 3 / 4 slower still
 // than 2 (profiles/r05zf_ab_wks3_depth.txt)
 #define DR_WKS3_D 1
-#endif
 // 16-row fragments per tile: 2 (32 x 32 tiles) for the fp32 products, 1 for
 // bf16 mode's (16 x 32 tiles: 828 -> 838 k bf16 headline; fp32 595 -> 587 k,
 // kept at 2; 8 or 2 waves per tile: +0.2 % / -6 %, profiles/r05zh_ab_wks3_shape.txt)
@@ -2607,14 +2602,9 @@ static bool tile_offsets_ok(const GemmBatch& gb, int count) {
   return true;
 }
 
-#ifndef DR_WKS3
-#define DR_WKS3 1  // A/B knob: 0 = chain products with weight planes keep the f32 wave-K / bf16 tile kernels
-#endif
-#ifndef DR_B16_CHAIN_TILE
-// bf16 mode's chain products on k_gemm_tile_b16 (0: the f32 wave-K kernel):
-// bf16 headline 730.5 k against 723.3 k (profiles/r03zf_ab_bf16_chain_route.txt)
-#define DR_B16_CHAIN_TILE 1  // A/B knob
-#endif
+// bf16 mode's chain products without weight planes on k_gemm_tile_b16 (the
+// f32 wave-K kernel measured 723.3 k against 730.5 k bf16 headline,
+// profiles/r03zf_ab_bf16_chain_route.txt)
 template <int AMODE, bool A_KM, bool B_KN>
 static int launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
   if (AMODE == AM_PLAIN && tile_offsets_ok(gb, count)) {
@@ -2635,7 +2625,7 @@ static int launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
     // problems, split-K 4), profiles/r02h_kbench_tile_B256.txt
     // shallow-K products the caller gave weight planes (the BPTT's actor
     // input gradient, K = 200, N = 1624): the wave-K split3 kernel
-    if (DR_WKS3 && !A_KM && !B_KN && maxM >= 128 && maxM <= 512 && minK < 512 && g_tile_variant == 0 &&
+    if (!A_KM && !B_KN && maxM >= 128 && maxM <= 512 && minK < 512 && g_tile_variant == 0 &&
         wks3_ok(gb, count)) {
       launch_wks3(gb, count, s, b16_ok(gb, count));
       return DR_OK;
@@ -2655,8 +2645,8 @@ static int launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
         // 15.8 -> 13.0 us, BPTT 32.2 -> 25.7, GRU hidden product 13.3 -> 12.3,
         // profiles/r03g_kbench_wk.txt); the LDS tile kernel stays for the
         // shapes the wave-K kernel does not take (and as kbench variant 25)
-        if (DR_WKS3 && wks3_ok(gb, count)) launch_wks3(gt, count, s, b16_ok(gb, count));
-        else if (DR_B16_CHAIN_TILE && b16_ok(gb, count)) launch_tile_b16<32, 32, 4>(gt, count, s);
+        if (wks3_ok(gb, count)) launch_wks3(gt, count, s, b16_ok(gb, count));
+        else if (b16_ok(gb, count)) launch_tile_b16<32, 32, 4>(gt, count, s);
         else if (g_tile_variant == 0 && wk_ok(gb, count)) launch_wk<32, 32, 4, 2, 1>(gt, count, s, 0);
         else if (g_tile_variant >= 12 && g_tile_variant < 25 && wk_ok(gb, count)) {
           GemmBatch gw = gb;  // (split-K scratch kept: launch_wk splits only under 256 tiles)

@@ -363,9 +363,6 @@ static inline int dec_cout_st(const WmDims& D, int k) { return k == D.N - 1 ? 4 
 // the convolutions that run f32-accurate on the bf16 MFMA (3-term split):
 // encoder conv k >= 1 (conv1's 4-channel input stays on the f32 MFMA) and the
 // data gradient of decoder convT k (a Conv2d from cout_t to cin_t channels)
-#ifndef DR_WM_BF16_GEMM
-#define DR_WM_BF16_GEMM 0  // A/B knob: 1 = the bf16 WM step's tile-routed Linears in bf16 (r04p: -0.1 ms, posterior flips 1.7e-4 -> 1.7e-3)
-#endif
 static inline bool enc_s3(const WmDims& D, int k) {
   return !D.Dv && k >= 1 && op_conv_split3_supported(D.M, D.e[k], D.IH >> k, D.IW >> k, D.e[k + 1]);
 }
@@ -594,9 +591,10 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   DR_REQUIRE(d->cols <= 64, "latent classes must be <= 64");
   DR_REQUIRE(d->obs_dim == 0 || d->obs_dim % 4 == 0, "vector observations: obs_dim % 4 == 0 required");
   const WmDims D = wm_dims(d, B, T);
-  // bf16 mode: the NT products that take the tile route run on the bf16 tile
-  // GEMM (operands rounded as staged, f32 accumulation), as in the epoch
-  GemmBf16Scope bf16_scope(DR_WM_BF16_GEMM && D.terms == 1);
+  // the NT products that take the tile route stay f32 in both modes (on the
+  // bf16 tile GEMM in bf16 mode they saved 0.1 ms but raised the posterior
+  // flips 1.7e-4 -> 1.7e-3, r04p)
+  GemmBf16Scope bf16_scope(false);
   const bool vec = D.Dv > 0;
   const int Dv = D.Dv;
   Carve c(ws);
