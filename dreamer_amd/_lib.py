@@ -32,7 +32,7 @@ class dr_dims(C.Structure):
         "hidden", "rows", "cols", "action", "img_h", "img_w", "enc_f1", "enc_f2", "enc_hidden",
         "prior_h1", "prior_h2", "rew_h1", "rew_h2", "cont_h1", "cont_h2",
         "actor_h1", "actor_h2", "critic_h1", "critic_h2", "buckets", "dec_f1", "dec_f2", "dec_hidden", "precision", "obs_dim", "enc_depth",
-        "launch_form")] + [("fault", fp)]
+        "launch_form")] + [("fault", fp), ("fault_host", fp)]
 
 DR_MAX_DEPTH = 5  # include/dreamer_hip.h: conv / convt slots (dr_dims.enc_depth <= 5)
 
@@ -133,6 +133,7 @@ _SIGS = {
     "dr_stream_create_cumask": (_i, [_i, _P(C.c_uint), _P(fp)]),
     "dr_stream_destroy": (_i, [fp]),
     "dr_device_cus": (_i, [_P(_i)]),
+    "dr_host_device_ptr": (_i, [fp, _P(fp)]),
     "dr_wm_train_workspace_bytes": (_sz, [_P(dr_dims), _i, _i]),
     "dr_decoder_workspace_bytes": (_sz, [_P(dr_dims), _i]),
     "dr_decoder_fwd": (_i, [_P(dr_dims), _P(dr_decoder), _i, fp, _ll, fp, _ll, fp, fp, _sz, fp]),

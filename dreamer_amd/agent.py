@@ -267,6 +267,17 @@ class Agent(nn.Module):
         host acknowledges it, engine.ImaginationEngine.check_faults)."""
         return self.loss_buffer[2:3]
 
+    def fault_host(self):
+        """(pinned host int32 [1], its device address): set to 1 by the kernel
+        that timed out, read by the host without a copy or a sync."""
+        if getattr(self, "_fault_host", None) is None:
+            import ctypes
+            h = torch.zeros(1, dtype=torch.int32).pin_memory()
+            p = ctypes.c_void_p()
+            L.call("dr_host_device_ptr", h.data_ptr(), ctypes.byref(p))
+            self._fault_host = (h, p.value)
+        return self._fault_host
+
     @property
     def S(self):
         return self.S_dev

@@ -694,6 +694,7 @@ int op_pbptt(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, int
       a.pz.n[i] = i == 0 ? BH * 2 * A : BH * MW;
     }
     a.pz.fault = d->fault;
+    a.pz.fault_host = d->fault_host;
   }
   a.pn4g = wm->prior.n4.w; a.pn4b = wm->prior.n4.b; a.pn1g = wm->prior.n1.w; a.pn1b = wm->prior.n1.b;
   a.an4g = ac->n4.w; a.an4b = ac->n4.b; a.an1g = ac->n1.w; a.an1b = ac->n1.b;

@@ -979,6 +979,7 @@ int op_pdream(const dr_dims* d, const dr_world_model* wm, const dr_actor* ac, in
       a.pz.n[i] = ns[i];
     }
     a.pz.fault = d->fault;
+    a.pz.fault_host = d->fault_host;
   }
   a.eps = tp.eps; a.ls_raw = tp.ls_raw; a.pre1a = tp.pre1a; a.x1a = tp.x1a; a.pre2a = tp.pre2a; a.x2a = tp.x2a;
   a.tr = tp.r; a.tu = tp.u; a.tn = tp.n; a.tghn = tp.ghn; a.pre1p = tp.pre1p; a.pre2p = tp.pre2p; a.soft = tp.soft;

@@ -1453,6 +1453,11 @@ extern "C" int dr_device_cus(int* out) {
   DR_TRY_HIP(hipDeviceGetAttribute(out, hipDeviceAttributeMultiprocessorCount, dev));
   return DR_OK;
 }
+extern "C" int dr_host_device_ptr(void* host, void** dev) {
+  DR_REQUIRE(host && dev, "null pointer");
+  DR_TRY_HIP(hipHostGetDevicePointer(dev, host, 0));
+  return DR_OK;
+}
 
 // ---------------------------------------------------------------------------
 // vector observations (BASELINE configs[4]): gather the window rows of the

@@ -177,12 +177,13 @@ __device__ __forceinline__ bool ps_wait(int* s_ok, const unsigned* c0, int ld, i
 // therefore never passes for a valid one: NaN flows into the losses, the
 // agent's non-finite skip (Agent.py:137-139, dr_clip_stats over the loss slots,
 // which include the fault slot) rejects the update, and the host raises when it
-// reads the slot (engine.py check_faults).  The fault slot is sticky: the
-// library never clears it.
+// sees the host-mapped fault word (engine.py check_faults).  Both are sticky:
+// the library never clears them.
 struct PsPoison {
   float* p[8];
   unsigned long long n[8];  // floats at p[i]
-  float* fault;
+  float* fault;             // dr_dims.fault (device)
+  unsigned* fault_host;     // dr_dims.fault_host (pinned host memory, device-mapped)
 };
 __device__ __forceinline__ void ps_exit(unsigned* ticket, const unsigned* status, const PsPoison& pz) {
   __shared__ int s_last;
@@ -202,7 +203,10 @@ __device__ __forceinline__ void ps_exit(unsigned* ticket, const unsigned* status
     if (!p) continue;
     for (unsigned long long x = threadIdx.x; x < pz.n[i]; x += blockDim.x) p[x] = nan;
   }
-  if (pz.fault && threadIdx.x == 0) *pz.fault = nan;
+  if (threadIdx.x == 0) {
+    if (pz.fault) *pz.fault = nan;
+    if (pz.fault_host) __hip_atomic_store(pz.fault_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 // the spin limit of a persistent launch: DREAMER_PERSIST_FORCE=timeout (or
 // the kernel's name: scan / dream / bptt) makes every wait of that kernel time

@@ -707,6 +707,7 @@ int op_pscan(const dr_dims* d, const dr_world_model* wm, int B, int T, int A, co
   a.pz.p[1] = h_out; a.pz.n[1] = (unsigned long long)B * HD;
   a.pz.p[2] = logits_out; a.pz.n[2] = logits_out ? (unsigned long long)B * LAT : 0ull;
   a.pz.fault = d->fault;
+  a.pz.fault_host = d->fault_host;
   a.hb = reinterpret_cast<float*>(base);
   a.pre = a.hb + (size_t)2 * B * HD;
   a.iz = reinterpret_cast<int*>(a.pre + (size_t)2 * B * EH);

@@ -21,7 +21,6 @@ between the phase graphs.
 """
 import contextlib
 import gc
-import math
 
 import numpy as np
 
@@ -89,16 +88,6 @@ class ImaginationEngine:
         self.side = torch.cuda.Stream(self.dev)
         self.chunks = [(0, self.T)]
         self._alloc()
-        # persistent-kernel fault checks (dr_dims.fault): after every run / run_many
-        # the agent's fault slot is copied to pinned host memory on a stream of its
-        # own (nothing added to the epoch's stream); the copies are read when they
-        # are two calls old (check_faults), so the host never waits on the epoch it
-        # just queued
-        self._fs = torch.cuda.Stream(self.dev)
-        self._fault_pins = [torch.zeros(1).pin_memory() for _ in range(8)]
-        self._fault_i = 0
-        self._fault_pending = []
-
     # ------------------------------------------------------------------ setup
     @staticmethod
     def warm_chunks(T, size=8):
@@ -358,39 +347,27 @@ class ImaginationEngine:
         return bool(L.query("dr_persistent_kernels", self.d, self.B, self.T, self.H) & 4)
 
     # ------------------------------------------------------- fault checks
-    def _fault_note(self):
-        """Queue the copy of the fault slot behind the work issued so far."""
-        main = torch.cuda.current_stream(self.dev)
-        self._fs.wait_stream(main)
-        pin = self._fault_pins[self._fault_i % len(self._fault_pins)]
-        self._fault_i += 1
-        with torch.cuda.stream(self._fs):
-            pin.copy_(self.dr.agent.fault_slot(), non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(self._fs)
-        self._fault_pending.append((ev, pin))
-
-    def check_faults(self, keep=0):
-        """Read the queued fault-slot copies, all but the newest `keep` (waiting
-        for them).  A NaN slot means a persistent kernel (posterior scan,
-        imagination unroll or BPTT) timed out on a wait: its outputs were
-        written NaN and that epoch's update was skipped on every rank
-        (non-finite skip, Agent.py:137-139).  Then the slot is cleared, every
-        later epoch runs the launch form (new graphs), and RuntimeError is
-        raised."""
-        while len(self._fault_pending) > keep:
-            ev, pin = self._fault_pending.pop(0)
-            ev.synchronize()
-            if not math.isfinite(float(pin[0])):
-                self._on_fault()
+    def check_faults(self, wait=True):
+        """Raise if a persistent kernel (posterior scan, imagination unroll or
+        BPTT) timed out on a wait.  Such a kernel wrote NaN over its outputs
+        and the agent's fault slot, so that epoch's update was skipped on every
+        rank (non-finite skip, Agent.py:137-139), and set the host-mapped fault
+        word (dr_dims.fault_host), which this reads without a copy.  wait=True
+        first waits for the queued work; run() / run_many() look without
+        waiting, so they see a fault of an epoch that has finished.  On a
+        fault: the flags are cleared, every later epoch runs the launch form
+        (new graphs), and RuntimeError is raised."""
+        h, _ = self.dr.agent.fault_host()
+        if wait:
+            torch.cuda.current_stream(self.dev).synchronize()
+        if int(h[0]) != 0:
+            self._on_fault()
 
     def _on_fault(self):
-        for ev, _ in self._fault_pending:
-            ev.synchronize()
-        self._fault_pending = []
         ag = self.dr.agent
-        torch.cuda.current_stream(self.dev).synchronize()
+        torch.cuda.synchronize(self.dev)
         ag.fault_slot().zero_()
+        ag.fault_host()[0][0] = 0
         ag.persistent_ok = False
         self.d = self.dims()
         self.graph, self.graph_key, self._pipe = None, None, None
@@ -464,7 +441,7 @@ class ImaginationEngine:
         """One train_Agent epoch from host window starts; returns the device
         loss slots (actor, critic).  With timing=True, HIP events bracket every
         phase (self.last_events)."""
-        self.check_faults(keep=1)
+        self.check_faults(wait=False)
         i = self.epochs & 1
         if self.copy_ev[i] is not None:
             self.copy_ev[i].synchronize()
@@ -492,7 +469,6 @@ class ImaginationEngine:
                 e.record()
                 evs.append(e)
         self.last_events = evs
-        self._fault_note()
         return ag.loss_slot(0), ag.loss_slot(1)
 
     def phase_ms(self):
@@ -602,7 +578,7 @@ class ImaginationEngine:
     def run_many(self, starts_list):
         """len(starts_list) consecutive train_Agent epochs, pipelined (see
         above).  Returns a [K, 2] device tensor of (actor, critic) losses."""
-        self.check_faults(keep=1)
+        self.check_faults(wait=False)
         ag = self.dr.agent
         key = (ag.params_key(), self.dr.world_model.params_key(), self.dr.buffer.device_key())
         P = self._pipe_capture(key)
@@ -627,7 +603,6 @@ class ImaginationEngine:
             outer.wait_stream(P["chain"])
         else:
             losses = self._run_many(P, G, starts_list, outer)
-        self._fault_note()
         return losses
 
     def _run_many(self, P, G, starts_list, main):

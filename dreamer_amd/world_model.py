@@ -73,6 +73,7 @@ class WorldModel(nn.Module):
                 d.launch_form = 1
             if agent.grad_buffer.is_cuda:
                 d.fault = agent.fault_slot().data_ptr()
+                d.fault_host = agent.fault_host()[1]
             a, c = agent.actor.base_net, agent.critic.value_net
             d.actor_h1, d.actor_h2 = a[0].out_features, a[3].out_features
             d.critic_h1, d.critic_h2 = c[0].out_features, c[3].out_features

@@ -85,10 +85,12 @@ typedef struct {
                           one times out (a workgroup was not resident, e.g. held off by other work on the
                           CUs), the launch's outputs are written NaN and *fault = NaN.  Sticky: the library
                           never clears it.  The engine keeps it among the agent's loss slots, so the
-                          non-finite skip (Agent.py:137-139) rejects that epoch's update on every rank, and
-                          the host raises when it reads it (dreamer_amd/engine.py check_faults).  Test hook:
-                          DREAMER_PERSIST_FORCE=timeout (or scan / dream / bptt) makes every wait of those
-                          launches time out, read at each call. */
+                          non-finite skip (Agent.py:137-139) rejects that epoch's update on every rank.  Test
+                          hook: DREAMER_PERSIST_FORCE=timeout (or scan / dream / bptt) makes every wait of
+                          those launches time out, read at each call. */
+  unsigned* fault_host; /* may be NULL: a word of pinned host memory (its device address,
+                          dr_host_device_ptr) set to 1 on the same timeouts, so the host notices a fault
+                          without a copy or a sync (dreamer_amd/engine.py check_faults raises).  Sticky. */
 } dr_dims;
 #define DR_MAX_DEPTH 5
 #define DR_PREC_FP32 0
@@ -154,6 +156,8 @@ int dr_stream_create_cumask(int n_words, const unsigned* mask, hipStream_t* out)
 int dr_stream_destroy(hipStream_t s);
 /* the device's CU count (hipDeviceAttributeMultiprocessorCount) */
 int dr_device_cus(int* out);
+/* the device address of pinned host memory (hipHostGetDevicePointer): dr_dims.fault_host */
+int dr_host_device_ptr(void* host, void** dev);
 
 /* ---- a3  Encoder conv stack + latent_mapper.0 feature columns ---------------
  * feat[f][enc_hidden] = flatten(SiLU(conv4(...SiLU(conv1(frame f)))))

@@ -190,8 +190,9 @@ def test_forced_timeout_skips_update_and_raises(which, gpu, monkeypatch):
     kernel (all three: "timeout") time out.  Then the kernel NaN-fills its
     outputs and the fault slot; the epoch's update is skipped like the
     reference's non-finite skip (Agent.py:137-139): actor, critic and target
-    parameters unchanged; train_Agent() raises within two more calls; after
-    that the engine runs the launch form and updates again."""
+    parameters unchanged; the host-mapped fault word is set and the next
+    train_Agent() raises; after that the engine runs the launch form and
+    updates again."""
     import numpy as np
     monkeypatch.setenv("DREAMER_PERSIST_FORCE", which)
     d = _fault_case(gpu)
@@ -204,11 +205,11 @@ def test_forced_timeout_skips_update_and_raises(which, gpu, monkeypatch):
     assert not torch.isfinite(ag.fault_slot()).all(), "fault slot not set"
     for a, b in zip(before, (ag.fa.flat, ag.fc.flat, ag.ft.flat)):
         assert torch.equal(a, b), "the faulted epoch's update was applied"
+    assert int(ag.fault_host()[0][0]) == 1, "host-mapped fault word not set"
     with pytest.raises(RuntimeError, match="persistent kernel"):
-        for _ in range(3):
-            d.train_Agent()
+        d.train_Agent()  # sees the fault of the finished epoch before queueing another
     assert not ag.persistent_ok and not d.engine.persistent_bptt()
-    assert float(ag.fault_slot()) == 0.0
+    assert float(ag.fault_slot()) == 0.0 and int(ag.fault_host()[0][0]) == 0
     la, lc = d.train_Agent()
     torch.cuda.synchronize()
     d.engine.check_faults()
