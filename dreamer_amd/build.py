@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libdreamer_hip.so")
-SOURCES = ["scan.hip", "dream.hip", "bptt.hip", "gemm.hip", "conv.hip", "conv_bf16.hip", "conv_split.hip", "wmconv.hip", "gru.hip", "ops.hip", "engine.hip", "wm.hip", "act.hip"]
+SOURCES = ["scan.hip", "dream.hip", "bptt.hip", "gemm.hip", "conv.hip", "conv_bf16.hip", "conv_split.hip", "conv_glds.hip", "wmconv.hip", "gru.hip", "ops.hip", "engine.hip", "wm.hip", "act.hip"]
 ARCH = os.environ.get("DREAMER_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 

@@ -38,6 +38,10 @@ int op_enc12_s1_bf16(int n, int nb, int h, int w, int c1, int c2, const dr_frame
                      hipStream_t s, int prepacked = 0);
 int op_conv_s1_bf16(int n, int cin, int ih, int iw, int cout, const void* in, const void* wr, const float* bias,
                     void* out, int out_nchw, hipStream_t s);
+// the same convolution with LDS-DMA staged operands, four stages deep (conv_glds.hip; cout % 128 == 0)
+bool op_conv_glds_bf16_supported(int n, int cin, int ih, int iw, int cout);
+int op_conv_glds_bf16(int n, int cin, int ih, int iw, int cout, const void* in, const void* wr, const float* bias,
+                      void* out, int out_nchw, hipStream_t s);
 // k4 s2 p1 conv + bias + SiLU, f32 NHWC in -> f32 NHWC (or NCHW) out, as op_conv_nhwc
 int op_conv_split3(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
                    float* out, int out_nchw, hipStream_t s);

@@ -1,0 +1,237 @@
+// bf16 perf mode's encoder convolutions conv3.. (VariationalAutoEncoder.py:33-42,
+// k4 s2 p1 + SiLU) as an implicit GEMM whose operands move global -> LDS by
+// LDS-DMA (global_load_lds_dwordx4), three stages deep, two workgroups per CU.
+//
+// Why a second kernel beside k_conv_split3<.., NT3 = 1>: that tiling was built
+// for the fp32 mode's six products per block.  With ONE bf16 product per block a
+// 32-deep K chunk is 16 MFMAs per wave, ~260 cycles, and its register ring
+// staged one chunk ahead: every chunk waited on its L2 / HBM loads (the counter
+// pass read 6.2 VALU per MFMA, 45 % of wave time waiting, 0.19 of the bf16 peak
+// for conv3, profiles/r05u_pmc_sq_tcc.txt).  Here the staging costs no VGPRs
+// and no VALU beyond the addresses, and two workgroups share each CU.
+//
+// Tile: 256 pixels x 128 output channels, K = tap x 32 channels per chunk
+// (conv_chunk's tap-parity order, the same chunk sequence as k_conv_split3, so
+// the sums are bitwise the old kernel's), 8 waves as 4 (pixels) x 2 (channels)
+// of 64 x 64, v_mfma_f32_16x16x32_bf16 with f32 accumulation.
+// LDS: one array of STAGES x (256 A rows + 128 B rows) x 64 bytes (72 KB).  An
+// LDS-DMA wave instruction writes 1 KiB contiguously (lane l at base + 16 l:
+// 16 rows x 4 units), so the bank-conflict swizzle of the fragment reads
+// (unit u of row r at u ^ swz(r)) is applied to the SOURCE address: lane
+// (row, slot) fetches unit slot ^ swz(row).  Out-of-frame taps fetch from a
+// 16-byte zero block (no branch, no select at the store).
+// Pipeline per chunk c (MI355X guide "Pipelining across barriers"):
+// s_waitcnt vmcnt(3 x chunks still in flight) -> raw s_barrier (every wave's
+// DMA of chunk c has landed; every wave has finished reading chunk c - 1) ->
+// issue chunk c + STAGES - 1 into chunk c - 1's stage -> fragment reads ->
+// 16 MFMAs.  No __syncthreads() in the loop (its fence would drain the DMA).
+#include "conv.h"
+
+#include <algorithm>
+
+namespace {
+typedef unsigned short u16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x4 g_mfma(u32x4 a, u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
+                                                  0);
+}
+__device__ __forceinline__ int g_swz(int row) { return (0x1320 >> (((row >> 2) & 3) * 4)) & 3; }
+__device__ __forceinline__ u32x2 g_pack4(f32x4 v) {
+  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+  const bf16x4_t b = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  return __builtin_bit_cast(u32x2, b);
+}
+// chunk c -> (tap, first channel, chunk index of the tap-major weight planes):
+// channel chunks outer, the 16 taps in four parity groups (conv_split.hip conv_chunk)
+template <int CIN>
+__device__ __forceinline__ void g_chunk(int c, int& tap, int& ci0, int& kc) {
+  constexpr int CPT = CIN / 32;
+  const int cc = c >> 4, t = c & 15;
+  const int g = t >> 2, j = t & 3;
+  const int ky = (g >> 1) + 2 * (j >> 1), kx = (g & 1) + 2 * (j & 1);
+  tap = ky * 4 + kx;
+  ci0 = 32 * cc;
+  kc = tap * CPT + cc;
+}
+// s_waitcnt vmcnt(3 n): the LDS-DMA of the n newest chunks may stay in flight
+__device__ __forceinline__ void g_vmcnt(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+  }
+}
+__device__ const u16 g_zero16[64] = {0};
+}  // namespace
+
+constexpr int GB_M = 256, GB_N = 128, GB_ROWS = GB_M + GB_N;
+
+template <int CIN, bool OUT_NCHW, int STAGES>
+__global__ __launch_bounds__(512, STAGES <= 3 ? 4 : 2) void k_conv_glds_bf16(int n_frames, int ih, int iw, int cout,
+                                                                               const u16* __restrict__ in,
+                                                                               const u16* __restrict__ wr,
+                                                                               const float* __restrict__ bias,
+                                                                               u16* __restrict__ out) {
+  constexpr int K = CIN * 16, NCH = K / 32;
+  static_assert(CIN % 32 == 0 && NCH >= STAGES, "conv_glds tile");
+  // every LDS byte in ONE array (a second __shared__ object can make hipcc
+  // drain the DMA before each fragment read, MI355X guide item 4(a))
+  __shared__ __attribute__((aligned(16))) u32x4 sm[STAGES * GB_ROWS * 4];
+  const int oh = ih / 2, ow = iw / 2, hw = oh * ow;
+  const long long M = (long long)n_frames * hw;
+  const int tiles_n = cout / GB_N;
+  const long long tiles = ((M + GB_M - 1) / GB_M) * tiles_n;
+  const int lt = dr_xcd_tile(blockIdx.x, (int)tiles);
+  if (lt < 0) return;
+  const long long m0 = (long long)(lt / tiles_n) * GB_M;
+  const int n0 = (lt % tiles_n) * GB_N;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int r = lane & 15, q = lane >> 4;
+
+  // DMA roles: A rows (2 wave instructions per wave), B rows (1)
+  const int lrow = lane >> 2, slot = lane & 3;
+  int pb[2];
+  unsigned vm[2];
+  int au[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 16 + lrow;
+    const long long m = m0 + row;
+    const int mm = (int)(m < M ? m : 0);
+    const int f = mm / hw, p = mm - f * hw, oy = p / ow, ox = p - oy * ow;
+    const int y0 = 2 * oy - 1, x0 = 2 * ox - 1;
+    pb[i] = ((f * ih + y0) * iw + x0) * CIN;
+    unsigned v = 0u;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      v |= (y0 + t >= 0 && y0 + t < ih) ? (1u << t) : 0u;
+      v |= (x0 + t >= 0 && x0 + t < iw) ? (16u << t) : 0u;
+    }
+    vm[i] = m < M ? v : 0u;
+    au[i] = 8 * (slot ^ g_swz(row));
+  }
+  const int brow = wave * 16 + lrow;
+  const long long bbase = (long long)(n0 + brow) * 32 + 8 * (slot ^ g_swz(brow));
+
+  auto issue = [&](int c) __attribute__((always_inline)) {
+    int tap, ci0, kc;
+    g_chunk<CIN>(c, tap, ci0, kc);
+    const int ky = tap >> 2, kx = tap & 3;
+    const int toff = (ky * iw + kx) * CIN + ci0;
+    u32x4* st = sm + (c % STAGES) * GB_ROWS * 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool ok = (vm[i] >> ky) & (vm[i] >> (4 + kx)) & 1u;
+      const u16* src = ok ? in + (pb[i] + toff + au[i]) : g_zero16;
+      __builtin_amdgcn_global_load_lds(src, st + (wave * 2 + i) * 16 * 4, 16, 0, 0);
+    }
+    __builtin_amdgcn_global_load_lds(wr + ((long long)kc * 3 * cout) * 32 + bbase, st + (GB_M + wave * 16) * 4, 16, 0,
+                                     0);
+  };
+
+  const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * 64;
+  const int fu = q ^ g_swz(r);
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int c = 0; c < STAGES - 1; ++c) issue(c);
+#pragma unroll 1
+  for (int c = 0; c < NCH; ++c) {
+    // chunks c .. min(c + STAGES - 2, NCH - 1) are in flight: retire chunk c
+    g_vmcnt(min(STAGES - 2, NCH - 1 - c));
+    __builtin_amdgcn_s_barrier();
+    if (c + STAGES - 1 < NCH) issue(c + STAGES - 1);
+    const u32x4* st = sm + (c % STAGES) * GB_ROWS * 4;
+    u32x4 a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = st[(wm0 + 16 * i + r) * 4 + fu];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = st[(GB_M + wn0 + 16 * j + r) * 4 + fu];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = OUT_NCHW ? g_mfma(a[i], b[j], acc[i][j]) : g_mfma(b[j], a[i], acc[i][j]);
+  }
+
+  // NHWC: lane (r, q) holds channels 4q..4q+3 of pixel r; NCHW: pixels 4q..4q+3 of channel r
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (OUT_NCHW) {
+        const long long m = m0 + wm0 + 16 * i + 4 * q;
+        const int co = n0 + wn0 + 16 * j + r;
+        if (m >= M) continue;
+        const float bv = bias[co];
+        f32x4 v = acc[i][j] + bv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(v[e]);
+        const long long f = m / hw;
+        *reinterpret_cast<u32x2*>(out + (f * cout + co) * hw + (m - f * hw)) = g_pack4(v);
+      } else {
+        const long long m = m0 + wm0 + 16 * i + r;
+        const int co = n0 + wn0 + 16 * j + 4 * q;
+        if (m >= M) continue;
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + co);
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(acc[i][j][e] + bv[e]);
+        *reinterpret_cast<u32x2*>(out + m * cout + co) = g_pack4(v);
+      }
+    }
+}
+
+bool op_conv_glds_bf16_supported(int n, int cin, int ih, int iw, int cout) {
+  return (cin == 32 || cin == 64 || cin == 128 || cin == 256) && cout % GB_N == 0 && ih % 2 == 0 && iw % 2 == 0 &&
+         ((ih / 2) * (iw / 2)) % 4 == 0 && (long long)n * ih * iw * cin < (1LL << 31) - (1LL << 20);
+}
+
+template <int C, bool NCHW>
+static int launch_glds(int n, int ih, int iw, int cout, const void* in, const void* wr, const float* bias, void* out,
+                       hipStream_t s) {
+  const long long M = (long long)n * (ih / 2) * (iw / 2);
+  const long long tiles = ((M + GB_M - 1) / GB_M) * (cout / GB_N);
+  if (tiles >= (1LL << 30)) {
+    dr_set_error("conv_glds_bf16: too many tiles");
+    return DR_E_INVALID;
+  }
+  // three stages, two workgroups per CU (72 KB of LDS, 100 VGPRs): B = 256 bf16
+  // encoder conv3 / conv4 181 / 138 us, against 219 / 180 (four stages, one
+  // workgroup per CU), 229 / 186 (six) and 288 / 173 on k_conv_split3<.., 1>
+  // (profiles/r06g_ab_conv_glds.txt)
+  hipLaunchKernelGGL((k_conv_glds_bf16<C, NCHW, 3>), dim3((unsigned)dr_xcd_grid((int)tiles)), dim3(512), 0, s, n, ih,
+                     iw, cout, (const u16*)in, (const u16*)wr, bias, (u16*)out);
+  return dr_check_launch("conv_glds_bf16");
+}
+
+// bf16 NHWC in, bf16 NHWC / NCHW out, weights as op_conv_repack_split3 planes
+// (plane 0 = their RNE bf16); DR_E_INVALID (nothing launched) for other shapes
+int op_conv_glds_bf16(int n, int cin, int ih, int iw, int cout, const void* in, const void* wr, const float* bias,
+                      void* out, int out_nchw, hipStream_t s) {
+  if (!op_conv_glds_bf16_supported(n, cin, ih, iw, cout) || (((uintptr_t)in | (uintptr_t)out | (uintptr_t)bias) & 15)) {
+    dr_set_error("conv_glds_bf16: unsupported shape (cin=%d ih=%d iw=%d cout=%d)", cin, ih, iw, cout);
+    return DR_E_INVALID;
+  }
+#define DR_GL(C)                                                                                  \
+  if (cin == C)                                                                                   \
+    return out_nchw ? launch_glds<C, true>(n, ih, iw, cout, in, wr, bias, out, s)                 \
+                    : launch_glds<C, false>(n, ih, iw, cout, in, wr, bias, out, s);
+  DR_GL(32)
+  DR_GL(64)
+  DR_GL(128)
+  DR_GL(256)
+#undef DR_GL
+  return DR_E_INVALID;
+}

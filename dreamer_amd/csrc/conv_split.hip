@@ -857,6 +857,8 @@ int op_conv_s1_bf16(int n, int cin, int ih, int iw, int cout, const void* in, co
     dr_set_error("conv_s1_bf16: unsupported shape (cin=%d ih=%d iw=%d cout=%d)", cin, ih, iw, cout);
     return DR_E_INVALID;
   }
+  if (op_conv_glds_bf16_supported(n, cin, ih, iw, cout))
+    return op_conv_glds_bf16(n, cin, ih, iw, cout, in, wr, bias, out, out_nchw, s);
 #define DR_S1L(C)                                                                              \
   if (cin == C) {                                                                              \
     if (cout % 128 == 0)                                                                       \

@@ -13,12 +13,13 @@ import bench  # noqa: E402
 
 
 def main():
+    prec = os.environ.get("PRECISION", "fp32")
     Bs = [int(x) for x in sys.argv[1:]] or [64, 128, 256]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     for B in Bs:
         np.random.seed(1)
-        _, d = bench.make_dreamer(bench.CAR_RACER, dev, B, 64, 15, 64, 1, 1, 0, None, "fp32")
+        _, d = bench.make_dreamer(bench.CAR_RACER, dev, B, 64, 15, 64, 1, 1, 0, None, prec)
         eng = d._engine
         for _ in range(3):
             eng.run(d.buffer.sample_start_indices(B))
@@ -30,7 +31,8 @@ def main():
             rows.append(eng.phase_ms())
         med = {k: float(np.median([r[k] for r in rows])) for k in rows[0]}
         tot = sum(med.values())
-        print(f"B={B:4d} epoch {tot:7.3f} ms | " + "  ".join(f"{k} {v:6.3f}" for k, v in med.items()), flush=True)
+        enc = eng.time_encoder(reps=5)
+        print(f"{prec} B={B:4d} encoder {enc:6.3f} ms, epoch {tot:7.3f} ms | " + "  ".join(f"{k} {v:6.3f}" for k, v in med.items()), flush=True)
         del d, eng
         torch.cuda.empty_cache()
 
