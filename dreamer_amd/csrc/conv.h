@@ -40,6 +40,11 @@ int op_conv_s1_bf16(int n, int cin, int ih, int iw, int cout, const void* in, co
                     void* out, int out_nchw, hipStream_t s);
 // the same convolution with LDS-DMA staged operands, four stages deep (conv_glds.hip; cout % 128 == 0)
 bool op_conv_glds_bf16_supported(int n, int cin, int ih, int iw, int cout);
+// bf16 NT GEMM Y = X W^T + bias (X [M][K], W [N][K] bf16; K % 32 == 0, N % 4 == 0) on the same
+// LDS-DMA pipeline with split-K; part: op_gemm_nt_glds_part_floats(M, N, K) floats (may be 0)
+size_t op_gemm_nt_glds_part_floats(int M, int N, int K);
+int op_gemm_nt_glds_bf16(int M, int N, int K, const void* X, int ldx, const void* W, int ldw, const float* bias,
+                         float* Y, int ldy, float* part, size_t part_floats, hipStream_t s);
 int op_conv_glds_bf16(int n, int cin, int ih, int iw, int cout, const void* in, const void* wr, const float* bias,
                       void* out, int out_nchw, hipStream_t s);
 // k4 s2 p1 conv + bias + SiLU, f32 NHWC in -> f32 NHWC (or NCHW) out, as op_conv_nhwc

@@ -235,3 +235,144 @@ int op_conv_glds_bf16(int n, int cin, int ih, int iw, int cout, const void* in, 
 #undef DR_GL
   return DR_E_INVALID;
 }
+
+// ---------------------------------------------------------------------------
+// bf16 perf mode's encoder feature projection (latent_mapper.0's feature
+// columns, VAE.py:71-72): Y[m][n] = X[m][:] . W[n][:] + bias[n] over the B S / 2
+// warm-start frames, X = the flattened conv4 output (bf16 [M][K], K = 4096), W
+// its bf16 copy [N][K] (N = 200).  The same LDS-DMA pipeline as the convolution
+// above on 128 x 64 tiles (4 waves as 2 x 2 of 64 x 32), four stages, split-K
+// over blockIdx so that ~512 workgroups run (k_conv_bf16's dense 128 x 128 tiles
+// gave 128 workgroups at B = 256 and 32 at B = 64: 72 / 61 us); the partial sums
+// meet in a fixed order in k_glds_finish (deterministic).
+// ---------------------------------------------------------------------------
+constexpr int GP_M = 128, GP_N = 64, GP_ROWS = GP_M + GP_N, GP_ST = 4;
+
+struct GemmGlds {
+  int M, N, K, ldx, ldw, ldy, splits, kper;  // kper: K per split (multiple of 32)
+  const u16* X;
+  const u16* W;
+  const float* bias;
+  float* Y;     // splits == 1
+  float* part;  // [splits][M][N]
+};
+
+__global__ __launch_bounds__(256) void k_gemm_glds_bf16(GemmGlds g) {
+  __shared__ __attribute__((aligned(16))) u32x4 sm[GP_ST * GP_ROWS * 4];
+  const int tiles_m = (g.M + GP_M - 1) / GP_M, tiles_n = (g.N + GP_N - 1) / GP_N;
+  const int tiles = tiles_m * tiles_n;
+  const int lb = dr_xcd_tile(blockIdx.x, tiles * g.splits);
+  if (lb < 0) return;
+  const int split = lb / tiles, lt = lb - split * tiles;
+  const int m0 = (lt / tiles_n) * GP_M, n0 = (lt % tiles_n) * GP_N;
+  const int k_begin = split * g.kper, nch = min(g.kper, g.K - k_begin) / 32;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int r = lane & 15, q = lane >> 4, lrow = lane >> 2, slot = lane & 3;
+  const u16* asrc[2];
+  bool aok[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 16 + lrow;
+    aok[i] = m0 + row < g.M;
+    asrc[i] = g.X + (long long)(aok[i] ? m0 + row : 0) * g.ldx + k_begin + 8 * (slot ^ g_swz(row));
+  }
+  const int brow = wave * 16 + lrow;
+  const bool bok = n0 + brow < g.N;
+  const u16* bsrc = g.W + (long long)(bok ? n0 + brow : 0) * g.ldw + k_begin + 8 * (slot ^ g_swz(brow));
+  auto issue = [&](int c) __attribute__((always_inline)) {
+    u32x4* st = sm + (c % GP_ST) * GP_ROWS * 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds(aok[i] ? asrc[i] + 32 * c : g_zero16, st + (wave * 2 + i) * 16 * 4, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(bok ? bsrc + 32 * c : g_zero16, st + (GP_M + wave * 16) * 4, 16, 0, 0);
+  };
+  const int wm0 = (wave >> 1) * 64, wn0 = (wave & 1) * 32;
+  const int fu = q ^ g_swz(r);
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < GP_ST - 1 && c < nch; ++c) issue(c);
+#pragma unroll 1
+  for (int c = 0; c < nch; ++c) {
+    g_vmcnt(min(GP_ST - 2, nch - 1 - c));
+    __builtin_amdgcn_s_barrier();
+    if (c + GP_ST - 1 < nch) issue(c + GP_ST - 1);
+    const u32x4* st = sm + (c % GP_ST) * GP_ROWS * 4;
+    u32x4 a[4], b[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = st[(wm0 + 16 * i + r) * 4 + fu];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b[j] = st[(GP_M + wn0 + 16 * j + r) * 4 + fu];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = g_mfma(b[j], a[i], acc[i][j]);
+  }
+  // lane (r, q): row m0 + wm0 + 16 i + r, columns n0 + wn0 + 16 j + 4 q .. + 3
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int m = m0 + wm0 + 16 * i + r, n = n0 + wn0 + 16 * j + 4 * q;
+      if (m >= g.M || n >= g.N) continue;
+      if (g.splits == 1) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(g.bias + n);
+        *reinterpret_cast<f32x4*>(g.Y + (long long)m * g.ldy + n) = acc[i][j] + bv;
+      } else {
+        *reinterpret_cast<f32x4*>(g.part + ((long long)split * g.M + m) * g.N + n) = acc[i][j];
+      }
+    }
+}
+
+// Y = sum over the splits (ascending) + bias, 4 columns per thread
+__global__ void k_glds_finish(GemmGlds g) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int n4 = g.N / 4;
+  if (i >= (long long)g.M * n4) return;
+  const int m = (int)(i / n4), n = 4 * (int)(i - (long long)m * n4);
+  f32x4 v = *reinterpret_cast<const f32x4*>(g.part + (long long)m * g.N + n);
+  for (int s = 1; s < g.splits; ++s) v += *reinterpret_cast<const f32x4*>(g.part + ((long long)s * g.M + m) * g.N + n);
+  *reinterpret_cast<f32x4*>(g.Y + (long long)m * g.ldy + n) = v + *reinterpret_cast<const f32x4*>(g.bias + n);
+}
+
+static int glds_splits(int M, int N, int K) {
+  const int tiles = ((M + GP_M - 1) / GP_M) * ((N + GP_N - 1) / GP_N);
+  int s = std::max(1, std::min(8, 512 / std::max(1, tiles)));
+  while (s > 1 && (K / 32) / s < GP_ST) --s;  // at least a full pipeline of chunks per split
+  return s;
+}
+
+size_t op_gemm_nt_glds_part_floats(int M, int N, int K) {
+  const int s = glds_splits(M, N, K);
+  return s > 1 ? (size_t)s * M * N : 0;
+}
+
+int op_gemm_nt_glds_bf16(int M, int N, int K, const void* X, int ldx, const void* W, int ldw, const float* bias,
+                         float* Y, int ldy, float* part, size_t part_floats, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K % 32 || N % 4 || ldx % 8 || ldw % 8 || ldy % 4 || !bias ||
+      (((uintptr_t)X | (uintptr_t)W | (uintptr_t)Y | (uintptr_t)bias) & 15)) {
+    dr_set_error("gemm_nt_glds_bf16: unsupported problem (M=%d N=%d K=%d)", M, N, K);
+    return DR_E_INVALID;
+  }
+  GemmGlds g;
+  g.M = M; g.N = N; g.K = K; g.ldx = ldx; g.ldw = ldw; g.ldy = ldy;
+  g.splits = glds_splits(M, N, K);
+  g.kper = ((K / 32 + g.splits - 1) / g.splits) * 32;
+  g.splits = (K + g.kper - 1) / g.kper;
+  g.X = (const u16*)X; g.W = (const u16*)W; g.bias = bias; g.Y = Y; g.part = part;
+  if (g.splits > 1 && (!part || (size_t)g.splits * M * N > part_floats || ((uintptr_t)part & 15))) {
+    dr_set_error("gemm_nt_glds_bf16: split-K scratch too small");
+    return DR_E_WORKSPACE;
+  }
+  const int tiles = ((M + GP_M - 1) / GP_M) * ((N + GP_N - 1) / GP_N);
+  hipLaunchKernelGGL(k_gemm_glds_bf16, dim3((unsigned)dr_xcd_grid(tiles * g.splits)), dim3(256), 0, s, g);
+  DR_TRY(dr_check_launch("gemm_glds_bf16"));
+  if (g.splits > 1) {
+    const long long work = (long long)M * (N / 4);
+    hipLaunchKernelGGL(k_glds_finish, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, g);
+    DR_TRY(dr_check_launch("glds_finish"));
+  }
+  return DR_OK;
+}

@@ -58,8 +58,9 @@ static void enc_carve(Carve& c, const dr_dims* d, int n, EncWs& w) {
   for (int k = 1; k < N; ++k) w.wr[k] = (float*)c.raw((long long)e[k + 1] * e[k] * 16 * 6);
   w.wproj = bf ? c.raw((size_t)d->enc_hidden * enc_feat_dim(d) * 2) : nullptr;
   w.s3proj = bf ? nullptr : c.raw(op_nt_split3_ws_bytes(d->enc_hidden, enc_feat_dim(d)));
-  w.s3part_n = bf ? 0 : op_gemm_nt_split3_part_floats(n, d->enc_hidden);
-  w.s3part = bf ? nullptr : c.f((long long)w.s3part_n);
+  w.s3part_n = bf ? op_gemm_nt_glds_part_floats(n, d->enc_hidden, enc_feat_dim(d))
+                  : op_gemm_nt_split3_part_floats(n, d->enc_hidden);
+  w.s3part = w.s3part_n ? c.f((long long)w.s3part_n) : nullptr;
 }
 
 extern "C" size_t dr_encoder_workspace_bytes(const dr_dims* d, int n_frames) {
@@ -123,6 +124,10 @@ static int encoder_bf16(const dr_dims* d, const dr_world_model* wm, const dr_fra
                           k == N - 1 ? 1 : 0, s));
     }
   }
+  // the projection on the LDS-DMA bf16 GEMM with split-K where it tiles (conv_glds.hip), else k_conv_bf16
+  const int rcp = op_gemm_nt_glds_bf16(n, d->enc_hidden, F, w.a[N - 1], F, w.wproj, F, wm->map0.b, feat, d->enc_hidden,
+                                       w.s3part, w.s3part_n, s);
+  if (rcp != DR_E_INVALID) return rcp;
   return op_gemm_nt_bf16(n, d->enc_hidden, F, w.a[N - 1], F, w.wproj, wm->map0.b, feat, d->enc_hidden, s);
 }
 

@@ -642,8 +642,9 @@ size_t op_pscan_ring_bytes(int B) {
 #define PSCAN_MAX_B 128  // B = 256 (64-row GRU tiles, 32-row sampler tiles) builds: 560.8 k vs 566.1 k fp32 (r05r)
 #endif
 bool op_pscan_supported(const dr_dims* d, int B, int T, int A) {
+  // T < 65535: the z granules carry step + 1 in a 16-bit tag (a tag of 0 would match the zeroed granules)
   return !d->launch_form && d->hidden == HD && d->enc_hidden == EH && d->rows == NR && d->cols == NCL && A >= 1 &&
-         A <= 8 && T >= 2 && B >= 16 && B <= PSCAN_MAX_B && B % 16 == 0 && (B <= 64 || B % 32 == 0) &&
+         A <= 8 && T >= 2 && T < 65535 && B >= 16 && B <= PSCAN_MAX_B && B % 16 == 0 && (B <= 64 || B % 32 == 0) &&
          (B <= 128 || B % 64 == 0);
 }
 
