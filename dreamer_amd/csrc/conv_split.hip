@@ -1162,6 +1162,8 @@ int op_convT_split3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s, 
 // 2 (a) x 4 (n), partial planes per pixel split reduced by k_wgrad_reduce.
 // Low-resolution sizes are powers of two (shift addressing).
 // ---------------------------------------------------------------------------
+// (Round 6: the six-product form runs on k_wgrad_split3_db below; this kernel
+// keeps the one-term form, whose single buffer is 55-83 KB.)
 // TERMS = 1: both operands RNE-rounded to one bf16 plane (bf16 world-model
 // step); that form also takes BN = 256 column tiles (the output-gradient rows
 // re-read half as often: 255 -> 209 us for the 128-channel layers, r04r) and
@@ -1175,7 +1177,8 @@ __global__ __launch_bounds__(512) void k_wgrad_split3(int n, int lh, int lw, int
                                                       float* __restrict__ part) {
   constexpr int KC = 64, RP = KC / 8 + 1;
   constexpr int FM = BM / 32, FN = BN / 64;  // wave tile (BM / 2) x (BN / 4)
-  static_assert((TERMS == 1 || TERMS == 3) && FM >= 1 && (BN == 128 || (BN == 256 && TERMS == 1)),
+  static_assert((TERMS == 1 || TERMS == 3) && FM >= 1 &&
+                    (BN == 128 || BN == 256 || (BN == 512 && TERMS == 1 && BM <= 64)),
                 "wgrad_split3 tile");
   __shared__ __attribute__((aligned(16))) u32x4 S[TERMS][BM + BN][RP];
   const int N = 16 * cb;
@@ -1319,6 +1322,154 @@ __global__ __launch_bounds__(512) void k_wgrad_split3(int n, int lh, int lw, int
       for (int e = 0; e < 4; ++e) P[(long long)(m0 + wm0 + 16 * i + 4 * q + e) * N + n0 + wn0 + 16 * j + r] = acc[i][j][e];
 }
 
+// Double-buffered form (the six-product tiles): the single LDS buffer above
+// makes every chunk two phases -- all waves split and store, barrier, all
+// waves run the MFMAs, barrier -- so the VALU split never overlaps the matrix
+// core.  Here the pixel chunks are 32 deep (KC = 32: a 128 x 128 six-product
+// tile's two buffers take 120 KB), a thread stages units of 4 pixels x 4
+// channels (4 float4 loads, 2 pixel pairs per channel, 8-byte LDS pieces), and
+// chunk c + 1 is loaded before and stored after chunk c's MFMAs into the other
+// buffer: one barrier per chunk, the split of one wave beside the MFMAs of its
+// SIMD partner.  Per split the products run over the same pixels in the same
+// order as the single-buffer kernel (its 64-pixel chunk = two 32-deep steps),
+// so the partial planes are bitwise the same.
+template <int BM, int TERMS, int BN, int KC>
+__global__ __launch_bounds__(512) void k_wgrad_split3_db(int n, int lh, int lw, int ca, int cb,
+                                                         const float* __restrict__ lo, int lda,
+                                                         const float* __restrict__ hi, int ldb, int chunk,
+                                                         float* __restrict__ part) {
+  constexpr int RP = KC / 8 + 1, NQ = KC / 4;  // 16-byte units per row (+1 pad), pixel quartets per chunk
+  constexpr int FM = BM / 32, FN = BN / 64;
+  static_assert((KC == 32 || KC == 64) && FM >= 1 && FN >= 1, "wgrad_split3_db tile");
+  __shared__ __attribute__((aligned(16))) u32x4 S[2][TERMS][BM + BN][RP];
+  const int N = 16 * cb;
+  const int tiles_n = N / BN, tiles = (ca / BM) * tiles_n;
+  const int h = 1 << lh, w = 1 << lw, H2 = 2 * h, W2 = 2 * w;
+  const long long K = (long long)n * h * w;
+  const int nsplit = (int)((K + chunk - 1) / chunk);
+  const int lb = dr_xcd_tile(blockIdx.x, tiles * nsplit);
+  if (lb < 0) return;
+  const int split = lb / tiles, lt = lb - split * tiles;
+  const int m0 = (lt / tiles_n) * BM, n0 = (lt % tiles_n) * BN;
+  const long long k_begin = (long long)split * chunk;
+  const long long k_end = k_begin + chunk < K ? k_begin + chunk : K;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
+
+  // staging units: channel quad cq, pixel quartet qt (A: channels m0 + 4 cq of
+  // lo; B: columns n0 + 4 cq, one tap, 4 channels of hi)
+  constexpr int AU = BM / 4 * NQ, BUn = BN / 4 * NQ, UPT = (AU + BUn + 511) / 512;
+  bool isA[UPT], active[UPT];
+  int qt[UPT], row0[UPT], bch[UPT], bky[UPT], bkx[UPT];
+  const float* src[UPT];
+#pragma unroll
+  for (int j = 0; j < UPT; ++j) {
+    const int id = tid + 512 * j;
+    isA[j] = id < AU;
+    active[j] = id < AU + BUn;
+    const int u = isA[j] ? id : id - AU, cq = u / NQ;
+    qt[j] = u - cq * NQ;
+    row0[j] = isA[j] ? 4 * cq : BM + 4 * cq;
+    const int bn = n0 + 4 * cq, btap = bn / cb;
+    bch[j] = bn - btap * cb;
+    bky[j] = btap >> 2;
+    bkx[j] = btap & 3;
+    src[j] = isA[j] ? lo + m0 + 4 * cq : hi;
+  }
+  f32x4 v[UPT][4];
+  auto load = [&](long long p0c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < UPT; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long long p = p0c + 4 * qt[j] + i;
+        bool ok = active[j] && p < k_end;
+        long long off;
+        if (isA[j]) {
+          off = p * lda;
+        } else {
+          const long long f = p >> (lw + lh);
+          const int y = (int)(p >> lw) & (h - 1), x = (int)p & (w - 1);
+          const int Y = 2 * y - 1 + bky[j], X = 2 * x - 1 + bkx[j];
+          ok = ok && Y >= 0 && Y < H2 && X >= 0 && X < W2;
+          off = ((f * H2 + Y) * W2 + X) * ldb + bch[j];
+        }
+        const f32x4 t = *reinterpret_cast<const f32x4*>(src[j] + (ok ? off : 0));
+        v[j][i] = ok ? t : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+  };
+  auto store = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+      if (!active[j]) continue;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if constexpr (TERMS == 1) {
+          const u32x2 ph = {pack_bf16x2(v[j][0][c], v[j][1][c]), pack_bf16x2(v[j][2][c], v[j][3][c])};
+          reinterpret_cast<u32x2*>(&S[buf][0][row0[j] + c][0])[qt[j]] = ph;
+        } else {
+          unsigned h0, m0w, l0, h1, m1, l1;
+          split3_pair(v[j][0][c], v[j][1][c], h0, m0w, l0);
+          split3_pair(v[j][2][c], v[j][3][c], h1, m1, l1);
+          reinterpret_cast<u32x2*>(&S[buf][0][row0[j] + c][0])[qt[j]] = (u32x2){h0, h1};
+          reinterpret_cast<u32x2*>(&S[buf][1][row0[j] + c][0])[qt[j]] = (u32x2){m0w, m1};
+          reinterpret_cast<u32x2*>(&S[buf][2][row0[j] + c][0])[qt[j]] = (u32x2){l0, l1};
+        }
+      }
+    }
+  };
+
+  const int wm0 = (wave >> 2) * (BM / 2), wn0 = (wave & 3) * (BN / 4);
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const long long nch = k_end > k_begin ? (k_end - k_begin + KC - 1) / KC : 0;
+  if (nch > 0) {
+    load(k_begin);
+    store(0);
+    __syncthreads();
+    for (long long c = 0; c < nch; ++c) {
+      const int buf = (int)(c & 1);
+      const bool more = c + 1 < nch;
+      if (more) load(k_begin + (c + 1) * KC);
+#pragma unroll
+      for (int ks = 0; ks < KC / 32; ++ks) {
+        u32x4 av[TERMS][FM], bv[TERMS][FN];
+#pragma unroll
+        for (int pl = 0; pl < TERMS; ++pl) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) av[pl][i] = S[buf][pl][wm0 + 16 * i + r][4 * ks + q];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) bv[pl][j] = S[buf][pl][BM + wn0 + 16 * j + r][4 * ks + q];
+        }
+#define DR_W3(PA, PB)                                                                                   \
+  _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
+      mfma_b16(av[PA][i], bv[PB][j], acc[i][j]);
+        if constexpr (TERMS == 3) {
+          DR_W3(2, 0)
+          DR_W3(1, 1)
+          DR_W3(0, 2)
+          DR_W3(1, 0)
+          DR_W3(0, 1)
+        }
+        DR_W3(0, 0)
+#undef DR_W3
+      }
+      if (more) store(buf ^ 1);
+      __syncthreads();
+    }
+  }
+  float* P = part + (long long)split * ca * N;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) P[(long long)(m0 + wm0 + 16 * i + 4 * q + e) * N + n0 + wn0 + 16 * j + r] = acc[i][j][e];
+}
+
+
 static int ilog2_exact(int v) {
   int l = 0;
   while ((1 << l) < v) ++l;
@@ -1332,10 +1483,18 @@ bool op_wgrad_split3_supported(int n, int h, int w, int ca, int cb, int terms) {
 }
 
 // tile of a problem: BM by the a-channels; the one-term form takes BN = 256
-// where N = 16 cb allows it
+// where N = 16 cb allows it.  The 64-channel layers (the encoder's conv2, the
+// decoder's 64 -> 32 transposed conv) re-read their staged bytes per output
+// more than the 128-channel ones at BN = 128 (64 x 128 tiles: 48 KB staged per
+// 64-pixel chunk for 1 MFLOP against 64 KB for 2), so BM = 64 takes wider
+// column tiles: 256 in the six-product form, 512 in the one-term form (WM step
+// B = 256 T = 15: fp32 14.16 -> 13.87 ms, bf16 9.30 -> 9.20 ms;
+// profiles/r06l_ab_gates_wgrad.txt)
 static void wgrad3_tile(int ca, int cb, int terms, int& bm, int& bn) {
   bm = ca >= 128 ? 128 : ca >= 64 ? 64 : 32;
-  bn = terms == 1 && (16 * cb) % 256 == 0 ? 256 : 128;
+  const int n = 16 * cb;
+  if (bm == 64) bn = terms == 1 && n % 512 == 0 ? 512 : n % 256 == 0 ? 256 : 128;
+  else bn = terms == 1 && n % 256 == 0 ? 256 : 128;
 }
 
 static void wgrad3_plan(int n, int h, int w, int ca, int cb, int bm, int bn, int& nsplit, int& chunk) {
@@ -1382,7 +1541,9 @@ int op_wgrad_split3(int n, int h, int w, int ca, int cb, const float* lo, int ld
   hipLaunchKernelGGL((k_wgrad_split3<BM, T, ##__VA_ARGS__>), dim3((unsigned)dr_xcd_grid(tiles * ns)), dim3(512), 0, s, n, lh, lw, \
                      ca, cb, lo, lda, hi, ldb, ch, ws)
   if (terms == 1) {
-    if (bn == 256) {
+    if (bn == 512) {
+      DR_W3L(64, 1, 512);
+    } else if (bn == 256) {
       if (bm == 128) DR_W3L(128, 1, 256);
       else if (bm == 64) DR_W3L(64, 1, 256);
       else DR_W3L(32, 1, 256);
@@ -1391,9 +1552,14 @@ int op_wgrad_split3(int n, int h, int w, int ca, int cb, const float* lo, int ld
       else if (bm == 64) DR_W3L(64, 1);
       else DR_W3L(32, 1);
     }
-  } else {
-    if (bm == 128) DR_W3L(128, 3);
-    else DR_W3L(64, 3);
+  } else {  // six products: the double-buffered kernel (WM step fp32 13.87 -> 13.82 ms, r06l)
+#define DR_W3D(BM, BN)                                                                                            \
+  hipLaunchKernelGGL((k_wgrad_split3_db<BM, 3, BN, 32>), dim3((unsigned)dr_xcd_grid(tiles * ns)), dim3(512), 0, s, n, \
+                     lh, lw, ca, cb, lo, lda, hi, ldb, ch, ws)
+    if (bm == 128) DR_W3D(128, 128);
+    else if (bn == 256) DR_W3D(64, 256);
+    else DR_W3D(64, 128);
+#undef DR_W3D
   }
 #undef DR_W3L
   DR_TRY(dr_check_launch("wgrad_split3"));

@@ -344,7 +344,9 @@ __global__ __launch_bounds__(512) void k_gru_fused(GruArgs ga) {
 #define GG_UNITS 32
 #define GG_NT (GG_ROWS * 3 * (GG_UNITS / 4))  // 192 threads
 
-#define DR_GATES_GB 8  // gathered W_ih^T rows issued per batch (4: the same, r05zh)
+// gathered W_ih^T rows issued per batch: 4 the same (r05zh); 16 / 32 slower
+// (fp32 headline 597 -> 584 / 582 k, bf16 888 -> 859 / 857 k, profiles/r06l_ab_gates_wgrad.txt)
+#define DR_GATES_GB 8
 template <int GB>  // gathered rows issued per batch (VGPRs vs round trips)
 __global__ __launch_bounds__(GG_NT) void k_gru_gates(GruArgs ga) {
   __shared__ GruArgs g;
