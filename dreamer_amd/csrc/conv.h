@@ -165,6 +165,8 @@ int op_convT_repack_split3(int cin, int cout, const float* wt, void* wr, hipStre
 // terms = 1: the bf16 world-model step's one-term form (as op_conv_split3_ex),
 // which also covers cout = 32
 bool op_convT_split3_supported(int n, int cin, int h, int w, int cout, int terms = 3);
+// the all-parity-class form op_convT_split3 takes for 64 -> 32 channels (8 x 16 anchor tiles)
+bool op_convT_cls_supported(int n, int cin, int h, int w, int cout);
 int op_convT_split3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s, int terms = 3);
 
 // Weight gradient of a k4 s2 p1 (transposed) convolution:

@@ -1101,11 +1101,178 @@ int op_convT_repack_split3(int cin, int cout, const float* wt, void* wr, hipStre
   return dr_check_launch("convT_repack_split3");
 }
 
+// ---------------------------------------------------------------------------
+// All four parity classes of a 64 -> 32-channel upsampling conv in one
+// workgroup (the decoder's ConvTranspose2d(64, 32) at 16x16 -> 32x32,
+// VAE.py:131-133, and the data gradient of the encoder's Conv2d(32, 64),
+// VAE.py:37-38).  The per-class kernels stage an im2col row per (class, tap):
+// every input element is fetched and split 16 times, and at 32 output channels
+// that staging outweighs the MFMAs (k_convT_nhwc: 790 / 950 us at B = 256
+// T = 15 on the f32 MFMA, 5.5 VALU per MFMA; k_convT_split3<.., 32, 64, ., 1>:
+// 365 / 450 us).  Here a workgroup owns 8 x 16 input anchors of one frame: it
+// stages their (8 + 2) x (16 + 2) x 64 input patch ONCE -- split3 (or RNE
+// bf16) into LDS planes, pixel rows of 144 bytes (64 bf16 + 16 bytes of pad:
+// the 16 pixels of a fragment read land on distinct bank quads) -- and wave w
+// computes parity class w (py, px) = (w >> 1, w & 1) for all 128 anchors and
+// 32 output channels: per tap (dy, dx) and 32-channel chunk, 8 anchor-row
+// fragments read straight from the patch at offset (py - dy, px - dx), the
+// weight fragments (op_convT_repack_split3 planes, class-major) from L2, one
+// tap-chunk ahead in registers.  Products per chunk in k_convT_split3's order
+// (six for TERMS = 3, f32-accurate; one for TERMS = 1).  WM step B = 256 T = 15:
+// fp32 13.67 -> 12.71 ms (the two layers 790 / 952 -> ~360 / 410 us), bf16
+// 9.18 -> 8.80 ms (365 / 450 -> ~240 / 267 us; the data-gradient form moves
+// 1.24 GB of input / pre-activation / output: HBM-bound), profiles/r06n_*.
+// ---------------------------------------------------------------------------
+constexpr int CC_TY = 8, CC_TX = 16, CC_PH = CC_TY + 2, CC_PW = CC_TX + 2, CC_PIX = CC_PH * CC_PW;
+constexpr int CC_ROWB = 144;  // bytes per staged pixel: 64 bf16 + 16 pad
+
+template <int EPI, int TERMS>
+__global__ __launch_bounds__(256) void k_convT_cls(ConvTArgs a, const u16* __restrict__ wr) {
+  constexpr int CIN = 64, COUT = 32, K = 4 * CIN, KCH = K / 32;
+  constexpr int PLANE = CC_PIX * CC_ROWB;
+  __shared__ __attribute__((aligned(16))) unsigned char sp[TERMS * PLANE];
+  const int h = a.h, w = a.w;
+  const int tiles_y = h / CC_TY, tiles_x = w / CC_TX;
+  const long long tiles = (long long)a.n * tiles_y * tiles_x;
+  const int lt = dr_xcd_tile(blockIdx.x, (int)tiles);
+  if (lt < 0) return;
+  const int f = lt / (tiles_y * tiles_x), rem = lt - f * tiles_y * tiles_x;
+  const int y0 = (rem / tiles_x) * CC_TY, x0 = (rem % tiles_x) * CC_TX;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
+
+  // ---- stage the input patch once: unit = (pixel, 8 channels) ----
+  constexpr int UNITS = CC_PIX * 8, UPT = (UNITS + 255) / 256;
+  const float* __restrict__ in = a.in + (long long)f * h * w * CIN;
+  f32x4 v[UPT][2];
+#pragma unroll
+  for (int j = 0; j < UPT; ++j) {
+    const int u = tid + 256 * j, pix = u >> 3, g = u & 7;
+    const int iy = y0 - 1 + pix / CC_PW, ix = x0 - 1 + pix % CC_PW;
+    const bool ok = u < UNITS && iy >= 0 && iy < h && ix >= 0 && ix < w;
+    const float* src = in + (ok ? ((long long)iy * w + ix) * CIN + 8 * g : 0);
+    const f32x4 t0 = *reinterpret_cast<const f32x4*>(src), t1 = *reinterpret_cast<const f32x4*>(src + 4);
+    v[j][0] = ok ? t0 : (f32x4){0.f, 0.f, 0.f, 0.f};
+    v[j][1] = ok ? t1 : (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int j = 0; j < UPT; ++j) {
+    const int u = tid + 256 * j, pix = u >> 3, g = u & 7;
+    if (u >= UNITS) continue;
+    unsigned char* dst = sp + pix * CC_ROWB + 16 * g;
+    if constexpr (TERMS == 1) {
+      const u32x4 hv = {pack_bf16x2(v[j][0][0], v[j][0][1]), pack_bf16x2(v[j][0][2], v[j][0][3]),
+                        pack_bf16x2(v[j][1][0], v[j][1][1]), pack_bf16x2(v[j][1][2], v[j][1][3])};
+      *reinterpret_cast<u32x4*>(dst) = hv;
+    } else {
+      unsigned hh[4], mm[4], ll[4];
+      split3_pair(v[j][0][0], v[j][0][1], hh[0], mm[0], ll[0]);
+      split3_pair(v[j][0][2], v[j][0][3], hh[1], mm[1], ll[1]);
+      split3_pair(v[j][1][0], v[j][1][1], hh[2], mm[2], ll[2]);
+      split3_pair(v[j][1][2], v[j][1][3], hh[3], mm[3], ll[3]);
+      *reinterpret_cast<u32x4*>(dst) = (u32x4){hh[0], hh[1], hh[2], hh[3]};
+      *reinterpret_cast<u32x4*>(dst + PLANE) = (u32x4){mm[0], mm[1], mm[2], mm[3]};
+      *reinterpret_cast<u32x4*>(dst + 2 * PLANE) = (u32x4){ll[0], ll[1], ll[2], ll[3]};
+    }
+  }
+  __syncthreads();
+
+  // ---- wave = parity class ----
+  const int cls = wave, py = cls >> 1, px = cls & 1;
+  const u16* __restrict__ wc = wr + (long long)cls * KCH * 3 * COUT * 32;
+  f32x4 acc[CC_TY][2];
+#pragma unroll
+  for (int i = 0; i < CC_TY; ++i) acc[i][0] = acc[i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  u32x4 bw[2][TERMS][2];
+  auto loadb = [&](int kc, int sl) __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = 0; p < TERMS; ++p)
+#pragma unroll
+      for (int jn = 0; jn < 2; ++jn)
+        bw[sl][p][jn] =
+            *reinterpret_cast<const u32x4*>(wc + ((long long)(kc * 3 + p) * COUT + 16 * jn + r) * 32 + 8 * q);
+  };
+  loadb(0, 0);
+#pragma unroll
+  for (int kc = 0; kc < KCH; ++kc) {  // k = 32 kc: tap = kc / 2, channels 32 (kc % 2) ..
+    const int sl = kc & 1;
+    if (kc + 1 < KCH) loadb(kc + 1, sl ^ 1);
+    const int tap = kc >> 1, dy = tap >> 1, dx = tap & 1, c0 = 32 * (kc & 1);
+    // anchor (y0 + i, x0 + r) reads input (y + py - dy, x + px - dx) = patch (i + 1 + py - dy, r + 1 + px - dx)
+    const unsigned char* pa = sp + ((1 + py - dy) * CC_PW + (r + 1 + px - dx)) * CC_ROWB + 2 * (c0 + 8 * q);
+#pragma unroll
+    for (int i = 0; i < CC_TY; ++i) {
+      u32x4 av[TERMS];
+#pragma unroll
+      for (int p = 0; p < TERMS; ++p)
+        av[p] = *reinterpret_cast<const u32x4*>(pa + p * PLANE + i * CC_PW * CC_ROWB);
+#define DR_CC(PA, PB)                                                                   \
+  _Pragma("unroll") for (int jn = 0; jn < 2; ++jn) acc[i][jn] = mfma_b16(bw[sl][PB][jn], av[PA], acc[i][jn]);
+      if constexpr (TERMS == 3) {
+        DR_CC(2, 0)
+        DR_CC(1, 1)
+        DR_CC(0, 2)
+        DR_CC(1, 0)
+        DR_CC(0, 1)
+      }
+      DR_CC(0, 0)
+#undef DR_CC
+    }
+  }
+
+  // ---- epilogue: lane (r, q) of acc[i][jn] = anchor (y0 + i, x0 + r), channels 16 jn + 4 q .. + 3 ----
+  const int OH = 2 * h, OW = 2 * w;
+#pragma unroll
+  for (int i = 0; i < CC_TY; ++i) {
+    const long long opix = ((long long)f * OH + 2 * (y0 + i) + py) * OW + 2 * (x0 + r) + px;
+#pragma unroll
+    for (int jn = 0; jn < 2; ++jn) {
+      const int co = 16 * jn + 4 * q;
+      f32x4 val = acc[i][jn];
+      if (EPI == CT_EPI_BIAS) {
+        val += *reinterpret_cast<const f32x4*>(a.bias + co);
+        f32x4 sv = val;
+        if (a.out2 || a.silu_out) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sv[e] = dr_silu_fast(val[e]);
+        }
+        *reinterpret_cast<f32x4*>(a.out + opix * COUT + co) = a.silu_out ? sv : val;
+        if (a.out2) *reinterpret_cast<f32x4*>(a.out2 + opix * COUT + co) = sv;
+      } else {
+        const f32x4 pv = *reinterpret_cast<const f32x4*>(a.pre + opix * COUT + co);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) val[e] = val[e] * dr_dsilu_fast(pv[e]);
+        *reinterpret_cast<f32x4*>(a.out + opix * COUT + co) = val;
+      }
+    }
+  }
+}
+
+bool op_convT_cls_supported(int n, int cin, int h, int w, int cout) {
+  return cin == 64 && cout == 32 && n > 0 && h % CC_TY == 0 && w % CC_TX == 0 &&
+         (long long)n * h * w * cin < (1LL << 31) - (1LL << 20) && (long long)n * (h / CC_TY) * (w / CC_TX) < (1LL << 30);
+}
+
+static int launch_convT_cls(int epi, const ConvTArgs& a, const void* wr, hipStream_t s, int terms) {
+  const long long tiles = (long long)a.n * (a.h / CC_TY) * (a.w / CC_TX);
+  const dim3 grid((unsigned)dr_xcd_grid((int)tiles));
+#define DR_CCL(E, T) hipLaunchKernelGGL((k_convT_cls<E, T>), grid, dim3(256), 0, s, a, (const u16*)wr)
+  if (epi == CT_EPI_DSILU) {
+    if (terms == 1) DR_CCL(CT_EPI_DSILU, 1);
+    else DR_CCL(CT_EPI_DSILU, 3);
+  } else {
+    if (terms == 1) DR_CCL(CT_EPI_BIAS, 1);
+    else DR_CCL(CT_EPI_BIAS, 3);
+  }
+#undef DR_CCL
+  return dr_check_launch("convT_cls");
+}
+
 // cout >= 64: at 32 output channels the 256 x 32 tile's split of the staged
 // activations outweighs its 24 MFMAs per wave and chunk (975 / 887 us against
 // 991 / 900 us on the f32 MFMA, WM step B = 256 T = 15, profiles/r03i_wm_step_kernels.txt)
 // (one term: the split's cost is gone, so cout = 32 takes the 256 x 32 tile)
 bool op_convT_split3_supported(int n, int cin, int h, int w, int cout, int terms) {
+  if ((terms == 1 || terms == 3) && op_convT_cls_supported(n, cin, h, w, cout)) return true;
   const bool cin_ok = cin == 32 || cin == 64 || cin == 128 || cin == 256;
   return cin_ok && (terms == 1 || terms == 3) && cout % (terms == 1 ? 32 : 64) == 0 && cout > 0 &&
          (long long)n * h * w * cin < (1LL << 31) - (1LL << 20) &&
@@ -1127,6 +1294,10 @@ int op_convT_split3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s, 
     dr_set_error("convT_split3: unsupported problem (cin=%d cout=%d h=%d w=%d epi=%d)", a.cin, a.cout, a.h, a.w, epi);
     return DR_E_INVALID;
   }
+  if (op_convT_cls_supported(a.n, a.cin, a.h, a.w, a.cout) && ((uintptr_t)a.in & 15) == 0 &&
+      ((uintptr_t)a.out & 15) == 0 && (!a.out2 || ((uintptr_t)a.out2 & 15) == 0) &&
+      (epi != CT_EPI_DSILU || ((uintptr_t)a.pre & 15) == 0) && (epi != CT_EPI_BIAS || ((uintptr_t)a.bias & 15) == 0))
+    return launch_convT_cls(epi, a, wr, s, terms);
 #define DR_T3E(BN, C, T) \
   (epi == CT_EPI_DSILU ? launch_t3<BN, C, CT_EPI_DSILU, T>(a, wr, s) : launch_t3<BN, C, CT_EPI_BIAS, T>(a, wr, s))
 #define DR_T3L(C)                                                                          \

@@ -241,6 +241,7 @@ extern "C" int dr_encoder_features(const dr_dims* d, const dr_world_model* wm, c
 // ===========================================================================
 struct ObsWs {
   float *gi, *gh, *pre1, *logits, *wt, *hb[2];
+  unsigned short* hb16[2];  // bf16 mode: hb[] rounded to bf16 by the gates kernel (k_gemm_wks3's A16)
   int* idx;
   void *s3m0, *s3whh;  // bf16 planes of latent_mapper.0's h-columns and W_hh (k_gemm_wks3)
   void* ring;          // persistent scan: ring buffers + counters (scan.hip)
@@ -256,6 +257,8 @@ static void obs_carve(Carve& c, const dr_dims* d, int B, ObsWs& w) {
   w.wt = c.f((long long)(latent(d) + d->action) * 3 * d->hidden);
   w.hb[0] = c.f((long long)B * d->hidden);
   w.hb[1] = c.f((long long)B * d->hidden);
+  w.hb16[0] = (unsigned short*)c.raw(sizeof(unsigned short) * B * d->hidden);
+  w.hb16[1] = (unsigned short*)c.raw(sizeof(unsigned short) * B * d->hidden);
   w.idx = c.i(2LL * B * d->rows);
 }
 
@@ -300,6 +303,10 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
     DR_TRY(split_planes(3 * Hd, Hd, wm->w_hh, Hd, w.s3whh, s));
   }
   const float* h = h_init;  // current hidden (NULL = zeros)
+  const unsigned short* h16 = nullptr;  // its bf16 copy when the gates kernel wrote one
+  // bf16 mode on the weight planes: the gates kernel also writes h rounded to
+  // bf16, which the grouped products read instead of rounding h themselves
+  const bool a16 = planes && d->precision == DR_PREC_BF16;
   int hb = 0;
   // B >= 128 (split GRU): the next step's hidden product h W_hh^T + b_hh rides
   // in the same grouped launch as latent_mapper.0 (both read only h)
@@ -323,10 +330,12 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
     if (do_gru) {
       const int ai = t - (z_init == nullptr ? 1 : 0);
       float* hn = w.hb[hb];
+      unsigned short* hn16 = a16 ? w.hb16[hb] : nullptr;
       hb ^= 1;
       DR_TRY(gru_onehot(d, wm, B, w.idx, actions + ai * act_st, act_sb, h, Hd, hn, Hd, w.wt, nullptr,
-                        nullptr, nullptr, nullptr, s, z_out, L, w.gh, gh_pre));
+                        nullptr, nullptr, nullptr, s, z_out, L, w.gh, gh_pre, hn16));
       h = hn;
+      h16 = hn16;
     }
     // latent_mapper.0 on cat(features, h): feature part precomputed in feat[t]
     GemmArgs g[2];
@@ -340,6 +349,7 @@ extern "C" int dr_observe_scan(const dr_dims* d, const dr_world_model* wm, int B
         // bf16 mode: plane 0 times bf16-rounded h (k_gemm_wks3<1>); fp32 mode: the 3-term split
         wplanes(g[0], w.s3m0);
         wplanes(g[1], w.s3whh);
+        g[0].A16 = g[1].A16 = h16;
       } else {
         g[0].bf16 = g[1].bf16 = 0;  // (bf16 mode: these products stay f32)
       }
@@ -390,6 +400,7 @@ extern "C" size_t dr_imagine_tape_bytes(const dr_dims* d, int B, int H) {
 
 struct ImWs {
   float *gi, *gh, *plog, *p1r, *p1c, *p2r, *p2c, *rlog, *clog, *rval, *wt, *wst, *bst;  // forward scratch
+  unsigned short* hid16;  // bf16 mode, launch form: hiddens rounded to bf16 by the gates kernel ([B][H+1][Hd])
   float *tl0f, *hpart;  // forward: actor Linear 0 transposed ([Hd+L][a1]), its h-part + bias [B][a1]
   void *s3r, *s3c;  // split3 weight planes of the reward / continue heads' first Linear
   void *s3p0, *s3a0, *s3whh, *s3wt, *s3twhh, *s3tl0a;  // bf16 planes of the per-step chain weights (k_gemm_wks3)
@@ -432,6 +443,7 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.s3part_n = op_gemm_nt_split3_part_floats((int)B1, std::max(d->rew_h1, d->cont_h1));
   w.s3part = c.f((long long)w.s3part_n);
   w.wt = c.f((long long)(L + A) * 3 * Hd);
+  w.hid16 = (unsigned short*)c.raw(sizeof(unsigned short) * Bl * (H + 1) * Hd);
   w.tl0f = c.f((long long)(Hd + L) * d->actor_h1);
   w.hpart = c.f(Bl * d->actor_h1);
   w.wst = c.f((long long)2 * A * d->actor_h2);
@@ -495,6 +507,7 @@ static int imagine_launch_form(const dr_dims* d, const dr_world_model* wm, const
   const long long ldH = (long long)(H + 1) * Hd, ldL = (long long)(H + 1) * L, ldA = (long long)H * A;
   const long long lda1 = (long long)H * a1, lda2 = (long long)H * a2;
   const bool planes = split_gru && H > 1 && Hd % 8 == 0;
+  const bool a16 = planes && d->precision == DR_PREC_BF16;
   if (planes) {
     DR_TRY(split_planes(d->prior_h1, Hd, wm->prior.l0.w, Hd, w.s3p0, s));
     if (zg) DR_TRY(split_planes(a1, Hd, ac->l0.w, Hd + L, w.s3a0, s));
@@ -522,8 +535,9 @@ static int imagine_launch_form(const dr_dims* d, const dr_world_model* wm, const
     float* z_t = latents + (long long)t * L;
     float* z_n = latents + (long long)(t + 1) * L;
     // WorldModel.imagine_step (WorldModel.py:72-77)
+    unsigned short* h_n16 = a16 ? w.hid16 + (long long)(t + 1) * Hd : nullptr;
     DR_TRY(gru_onehot(d, wm, B, w.idx[t & 1], actions + (long long)t * A, ldA, h_t, ldH, h_n, ldH, w.wt,
-                      tp.r + hb, tp.u + hb, tp.n + hb, tp.ghn + hb, s, z_t, ldL, w.gh, split_gru && t > 0));
+                      tp.r + hb, tp.u + hb, tp.n + hb, tp.ghn + hb, s, z_t, ldL, w.gh, split_gru && t > 0, h_n16));
     float* p1 = tp.pre1p + (long long)t * B * d->prior_h1;
     float* p2 = tp.pre2p + (long long)t * B * d->prior_h2;
     {
@@ -547,6 +561,7 @@ static int imagine_launch_form(const dr_dims* d, const dr_world_model* wm, const
       // else they stay f32; fp32 mode: h_{t+1}'s split3 planes from the gates kernel
       for (int i = 0; i < np; ++i) {
         if (!planes) p[i].bf16 = 0;
+        p[i].A16 = h_n16;  // bf16 mode: the gates kernel's bf16 copy of h_{t+1}
       }
       DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, np, s));
     }

@@ -281,7 +281,8 @@ static inline int stack_heads(const dr_actor* ac, int A, int in, float* w, float
 // where idx always comes from the sampler)
 static inline int gru_onehot(const dr_dims* d, const dr_world_model* wm, int B, int* idx, const float* a, long long lda, const float* h, long long ldh, float* hout,
                       long long ldo, const float* wt, float* sr, float* su, float* sn, float* sghn, hipStream_t s,
-                      const float* z = nullptr, long long ldz = 0, float* gh_ws = nullptr, int gh_ready = 0) {
+                      const float* z = nullptr, long long ldz = 0, float* gh_ws = nullptr, int gh_ready = 0,
+                      unsigned short* hout16 = nullptr) {
   GruArgs g;
   memset(&g, 0, sizeof(g));
   g.gh_ws = gh_ws;
@@ -290,7 +291,7 @@ static inline int gru_onehot(const dr_dims* d, const dr_world_model* wm, int B, 
   g.B = B; g.Hd = d->hidden; g.R = d->rows; g.C = d->cols; g.A = d->action;
   g.idx = idx; g.zval = onehot_vals(idx, B, d->rows); g.a = a; g.lda = lda; g.h = h; g.ldh = ldh;
   g.wt = wt; g.b_ih = wm->b_ih; g.w_hh = wm->w_hh; g.b_hh = wm->b_hh;
-  g.hout = hout; g.ldo = ldo; g.sr = sr; g.su = su; g.sn = sn; g.sghn = sghn;
+  g.hout = hout; g.hout16 = hout16; g.ldo = ldo; g.sr = sr; g.su = su; g.sn = sn; g.sghn = sghn;
   return op_gru_fused(g, s);
 }
 

@@ -73,6 +73,10 @@ struct alignas(16) GemmArgs {
   // op_nt_repack_split3 of W): per-step chain products then run on the bf16
   // MFMA -- f32-accurate 3-term split (fp32 mode) or plane 0 alone (bf16 mode)
   const unsigned short* wsplit; int wsplit_np, pad2_;
+  // bf16 mode: A also given rounded to bf16 (RNE, row stride lda) by its
+  // producer -- k_gemm_wks3<1> then loads 8 bf16 per lane instead of 8 f32 and
+  // skips the rounding (bitwise the same products)
+  const unsigned short* A16;
 };
 
 enum { EPI_NONE = 0, EPI_SAMPLE = 1, EPI_ACTOR = 2 };

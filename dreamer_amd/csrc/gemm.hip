@@ -1831,8 +1831,9 @@ __device__ __forceinline__ unsigned wk_pack_rne(float x0, float x1) {
   return __builtin_bit_cast(unsigned, v);
 }
 
-template <int NTP, int D, int NW = 4, int FM = 2>
+template <int NTP, int D, int NW = 4, int FM = 2, bool A16 = false>
 __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) {
+  static_assert(!A16 || NTP == 1, "bf16 A copies feed the one-term form only");
   constexpr int FN = 2, BM = 16 * FM, NTH = 64 * NW, NT4 = FM * FN * 256;
   __shared__ GemmArgs s_args;
   __shared__ __attribute__((aligned(16))) float red[NW][FM * FN * 4][64];
@@ -1849,6 +1850,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) 
   const int m0 = tm * BM, n0 = tn * 32;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 15, q = lane >> 4;
   const float* A = dr_uni(g.A);
+  const unsigned short* A16p = dr_uni(g.A16);
   const int lda = dr_uni((int)g.lda);
   const unsigned short* wr = dr_uni(g.wsplit);
   const int Np = dr_uni(g.wsplit_np);
@@ -1874,15 +1876,20 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) 
   unsigned ob[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) ob[j] = (unsigned)(n0 + 16 * j + r) * 32u + 8u * q;  // within a plane (Np >= n rows)
-  f32x4 ra[D][FM][2];
+  f32x4 ra[A16 ? 1 : D][FM][2];
+  wk_u32x4 ra16[A16 ? D : 1][FM];
   wk_u32x4 rb[D][NTP][FN];
   auto load = [&](int c, int sl) {
     const int k = 32 * c + 8 * q;
     const unsigned kk = k < K ? (unsigned)k : 0u;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      ra[sl][i][0] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)A + ((oa[i] + kk) << 2));
-      ra[sl][i][1] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)A + ((oa[i] + kk + 4) << 2));
+      if constexpr (A16) {
+        ra16[sl][i] = *(const DR_GLOBAL wk_u32x4*)((const DR_GLOBAL char*)A16p + ((oa[i] + kk) << 1));
+      } else {
+        ra[sl][i][0] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)A + ((oa[i] + kk) << 2));
+        ra[sl][i][1] = *(const DR_GLOBAL f32x4*)((const DR_GLOBAL char*)A + ((oa[i] + kk + 4) << 2));
+      }
     }
 #pragma unroll
     for (int p = 0; p < NTP; ++p)
@@ -1912,7 +1919,11 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_wks3(GemmBatch gb, int npack) 
       wk_u32x4 a[NTP][FM];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        f32x4 x0 = ra[u][i][0], x1 = ra[u][i][1];
+        if constexpr (A16) {
+          a[0][i] = kin ? ra16[u][i] : (wk_u32x4){0u, 0u, 0u, 0u};
+          continue;
+        }
+        f32x4 x0 = ra[A16 ? 0 : u][i][0], x1 = ra[A16 ? 0 : u][i][1];
         if (!kin) x0 = x1 = (f32x4){0.f, 0.f, 0.f, 0.f};
         if constexpr (NTP == 3) {
           unsigned h[4], m[4], l[4];
@@ -2542,7 +2553,16 @@ static void launch_wks3(const GemmBatch& gb, int count, hipStream_t s, bool bf16
   const int npack = count > 1 ? count : 0;
   const dim3 grid(dr_xcd_grid(npack ? tot : maxt));
   const dim3 blk(64 * DR_WKS3_NW);
-  if (bf16) hipLaunchKernelGGL((k_gemm_wks3<1, DR_WKS3_D, DR_WKS3_NW, DR_WKS3_FM_B16>), grid, blk, 0, s, gb, npack);
+  // bf16 A copies from the producers where every problem of the batch has one
+  // (bitwise the same epoch; bf16 headline B = 256 891 -> 909 k, profiles/r06n_ab_a16_convT_cls.txt)
+  bool a16 = bf16;
+  for (int i = 0; i < count && a16; ++i) {
+    const GemmArgs& g = gb.p[i];
+    a16 = g.A16 && ((uintptr_t)g.A16 & 15) == 0 && g.lda % 8 == 0;
+  }
+  if (a16)
+    hipLaunchKernelGGL((k_gemm_wks3<1, DR_WKS3_D, DR_WKS3_NW, DR_WKS3_FM_B16, true>), grid, blk, 0, s, gb, npack);
+  else if (bf16) hipLaunchKernelGGL((k_gemm_wks3<1, DR_WKS3_D, DR_WKS3_NW, DR_WKS3_FM_B16>), grid, blk, 0, s, gb, npack);
   else hipLaunchKernelGGL((k_gemm_wks3<3, DR_WKS3_D, DR_WKS3_NW, DR_WKS3_FM>), grid, blk, 0, s, gb, npack);
 }
 

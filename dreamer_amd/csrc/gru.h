@@ -17,6 +17,7 @@ struct alignas(16) GruArgs {
   const float* w_hh;    // [3*Hd][Hd]
   const float* b_hh;
   float* hout;          // row stride ldo; must NOT alias h (other workgroups still read h)
+  unsigned short* hout16;  // optional: h' also rounded to bf16 (RNE), row stride ldo (bf16 mode's GemmArgs.A16)
   long long ldo;
   float *sr, *su, *sn, *sghn;  // optional saves [B][Hd] for the backward
   float* gh_ws;                // optional [B][3*Hd] scratch: enables the split path at B >= 128

@@ -315,7 +315,9 @@ __global__ __launch_bounds__(512) void k_gru_fused(GruArgs ga) {
       const float hn = gh_s[ml][2][jl];
       const float nn = tanhf(gi_s[ml][2][jl] + hn * rr);
       const float hv = h ? dr_g(h)[(long long)m * g.ldh + j] : 0.0f;
-      dr_g(g.hout)[(long long)m * g.ldo + j] = (hv - nn) * uu + nn;
+      const float ho = (hv - nn) * uu + nn;
+      dr_g(g.hout)[(long long)m * g.ldo + j] = ho;
+      if (g.hout16) dr_g(g.hout16)[(long long)m * g.ldo + j] = __builtin_bit_cast(unsigned short, (__bf16)ho);
       if (g.sr) {
         const long long o = (long long)m * Hd + j;
         dr_g(g.sr)[o] = rr;
@@ -476,6 +478,12 @@ __global__ __launch_bounds__(GG_NT) void k_gru_gates(GruArgs ga) {
       no[e] = nn;
     }
     dr_st4(g.hout, (unsigned)(gm * (int)g.ldo + gj), make_float4(ho[0], ho[1], ho[2], ho[3]));
+    if (g.hout16) {
+      typedef __bf16 gg_b4 __attribute__((ext_vector_type(4)));
+      typedef unsigned gg_u2 __attribute__((ext_vector_type(2)));
+      const gg_b4 hb = {(__bf16)ho[0], (__bf16)ho[1], (__bf16)ho[2], (__bf16)ho[3]};
+      *(DR_GLOBAL gg_u2*)((DR_GLOBAL char*)g.hout16 + 2 * ((long long)gm * g.ldo + gj)) = __builtin_bit_cast(gg_u2, hb);
+    }
     if (g.sr) {
       const unsigned o = (unsigned)(gm * Hd + gj);
       dr_st4(g.sr, o, make_float4(ro[0], ro[1], ro[2], ro[3]));

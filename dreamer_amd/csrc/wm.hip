@@ -304,6 +304,9 @@ struct WmWs {
   // ... and of decoder convT k (forward) / encoder conv k's data gradient as upsampling convs
   void *t3d[DR_MAX_DEPTH], *t3e[DR_MAX_DEPTH];
   void* e12w1;  // conv1's split3 weight planes for k_enc12_split3
+  // the posterior scan's per-step products (latent_mapper.0's h-columns, W_hh)
+  // as split3 planes for k_gemm_wks3 (B >= 128), as in dr_observe_scan
+  void *s3m0, *s3whh;
   // loss
   float *coef_row, *coef_obs, *obs_part, *obs_bpart, *kl_grp, *rew_row, *cont_row, *scal, *stats;
   float* csp;  // per-tile channel sums of the last decoder layer's input gradient (k_conv_nhwc csum)
@@ -426,6 +429,8 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
   const int L = D.L, Hd = D.Hd, A = D.A, eh = D.eh, N = D.N;
   const long long Dv = D.Dv;
   w.x0 = c.f(Dv ? M * Dv : M * D.pix[0] * 4);
+  w.s3m0 = c.raw(op_nt_split3_ws_bytes(eh, Hd));
+  w.s3whh = c.raw(op_nt_split3_ws_bytes(3 * Hd, Hd));
   if (Dv) {  // MLP stand-in: layer 0 and the last layer of the conv slots, [M][F] each
     w.pre[0] = c.f(M * D.F); w.a[0] = c.f(M * D.F);
     w.pre[N - 1] = c.f(M * D.F); w.a[N - 1] = c.f(M * D.F);
@@ -718,6 +723,14 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   // B >= 128 (split GRU): the next step's hidden product h W_hh^T + b_hh rides
   // in the same grouped launch as latent_mapper.0 (both read only h_t)
   bool gh_pre = false;
+  // B >= 128: the grouped per-step products on the split3 wave-K kernel from
+  // weight planes split once per step (f32-accurate): 12.8 us per launch against
+  // the f32 k_gemm_wk's 23.5 (WM step bf16 9.22 -> 9.17 ms, fp32 unchanged, r06m)
+  const bool planes = B >= 128 && T > 1 && Hd % 8 == 0;
+  if (planes) {
+    DR_TRY(split_planes(eh, Hd, wm->map0.w + F, F + Hd, w.s3m0, s));
+    DR_TRY(split_planes(3 * Hd, Hd, wm->w_hh, Hd, w.s3whh, s));
+  }
   for (int t = 0; t < T; ++t) {
     const long long rb = (long long)t * B;
     float* h_t = w.h_all + rb * Hd;
@@ -736,6 +749,10 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     g[0].ld_add = eh;
     gh_pre = B >= 128 && t + 1 < T;
     if (gh_pre) g[1] = lin(B, 3 * Hd, Hd, h_t, Hd, wm->w_hh, Hd, wm->b_hh, w.gh, 3 * Hd);
+    if (planes) {
+      wplanes(g[0], w.s3m0);
+      if (gh_pre) wplanes(g[1], w.s3whh);
+    }
     DR_TRY(gemm_launch(G_NT, AM_PLAIN, g, gh_pre ? 2 : 1, s));
     GemmArgs gp = lin_ln(B, L, eh, w.pre_m + rb * eh, eh, wm->map1, wm->map3.w, wm->map3.b, w.plog + rb * L, L);
     gp.a_out = w.x_m + rb * eh;

@@ -11,7 +11,10 @@ import glob
 import sys
 
 KEYS = ("k_gemm_wks3", "k_gru_gates", "k_ln_gemm_sample", "k_gru_fused", "k_pscan", "k_pdream", "k_gemm_skinny",
-        "k_enc12", "k_conv_split3", "k_conv_bf16", "k_actor_head_bwd_x", "k_zgather_add", "k_mlp2_tail")
+        "k_enc12", "k_conv_split3", "k_conv_bf16", "k_actor_head_bwd_x", "k_zgather_add", "k_mlp2_tail",
+        # world-model step kernels
+        "k_convT", "k_wgrad", "k_conv_wgrad", "k_conv_nhwc", "k_gemm_tile", "k_gemm_pp_multi", "k_kn_repack",
+        "k_gemm_wk<", "k_conv_glds", "k_gemm_glds")
 
 
 def load(d):
