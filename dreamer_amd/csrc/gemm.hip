@@ -2528,6 +2528,13 @@ static bool wks3_ok(const GemmBatch& gb, int count) {
 // 4 waves per 32 x 32 (bf16: 16 x 32) tile, each over its own run of
 // k-chunks through a register ring (r04g: 8 waves, whole-wave prefetch and A
 // planes measured slower, profiles/r04g_ab_wks3.txt, r04t_ab_aplanes.txt)
+// (r06o / r06p: the K loop fully unrolled -- the rolled loop's back edge makes
+// the compiler wait for every outstanding load at each chunk, so the ring never
+// overlaps loads with MFMAs; unrolled, the waits are per slot -- bitwise the
+// same epoch, and no faster: B = 256 fp32 596 -> 596 k, bf16 909 -> 900 k (864 k
+// unrolled for short K too), B = 128 fp32 446 -> 454 k; not kept,
+// profiles/r06p_ab_wks3_unroll.txt.  The per-wave latency chain is not what
+// bounds these launches.)
 // (r05w: 64-row tiles, each weight plane read by half as many row tiles,
 // measured slower -- 548 k vs 566 k fp32, 776 k vs 803 k bf16 at B = 256)
 // register-ring depth (K chunks in flight per wave).  1: the fp32 kernel at 83
