@@ -76,6 +76,10 @@ size_t op_gemm_nt_split3_part_floats(int M, int N);
 int op_gemm_nt_split3_sk(int M, int N, int K, const float* A, int lda, const float* A2, int lda2, int ksA,
                          const void* wr, const float* bias, int act, float* Y, int ldy, float* part,
                          size_t part_floats, hipStream_t s, int splits_fixed = 0);
+// ... with Y += (accumulate) and columns n >= nsplitY stored to Y2 (the data-gradient products)
+int op_gemm_nt_split3_ex(int M, int N, int K, const float* A, int lda, const float* A2, int lda2, int ksA,
+                         const void* wr, const float* bias, int act, float* Y, int ldy, int accumulate, float* Y2,
+                         int ldy2, int nsplitY, float* part, size_t part_floats, hipStream_t s, int splits_fixed = 0);
 
 // ---- conv_bf16.hip (bf16 perf mode; activations bf16, accumulation f32) ----
 // weights: Conv2d [co][ci][4][4] f32 -> bf16 [co][tap][cin_pad]; matrix slice -> bf16 [rows][cols]

@@ -26,6 +26,7 @@
 #include "conv.h"
 
 #include <algorithm>
+#include <climits>
 #include <type_traits>
 
 namespace {
@@ -1756,7 +1757,17 @@ struct GemmS3 {
   float* Y;
   int splits;   // split-K over blockIdx.y (> 1: raw partial sums to part, k_s3_finish applies the epilogue)
   float* part;  // [splits][M][N]
+  // the world-model backward's data-gradient products: Y += (accumulate), and
+  // columns n >= nsplitY go to Y2[m][n - nsplitY] (nsplitY % 4 == 0)
+  int accumulate, ldy2, nsplitY, pad_;
+  float* Y2;
 };
+// the epilogue store of 4 consecutive columns n..n+3 (never straddling nsplitY)
+__device__ __forceinline__ void s3_store(const GemmS3& g, int m, int n, f32x4 v) {
+  float* dst = n < g.nsplitY ? g.Y + (long long)m * g.ldy + n : g.Y2 + (long long)m * g.ldy2 + (n - g.nsplitY);
+  if (g.accumulate) v += *reinterpret_cast<const f32x4*>(dst);
+  *reinterpret_cast<f32x4*>(dst) = v;
+}
 
 template <int BM, int BN>
 __global__ __launch_bounds__(BM * 2) void k_gemm_split3(GemmS3 g) {
@@ -1904,7 +1915,7 @@ __global__ __launch_bounds__(BM * 2) void k_gemm_split3(GemmS3 g) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = v[e] / (1.0f + expf(-v[e]));
       }
-      *reinterpret_cast<f32x4*>(g.Y + (long long)m * g.ldy + n) = v;
+      s3_store(g, m, n, v);
     }
   }
 }
@@ -1922,7 +1933,7 @@ __global__ void k_s3_finish(GemmS3 g) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = v[e] / (1.0f + expf(-v[e]));
   }
-  *reinterpret_cast<f32x4*>(g.Y + (long long)m * g.ldy + n) = v;
+  s3_store(g, m, n, v);
 }
 
 // W [N][K] (row stride ldw) -> bf16 planes [K/32][3][Np][32], zero past N and K
@@ -2036,13 +2047,23 @@ int op_gemm_nt_split3(int M, int N, int K, const float* A, int lda, const float*
 int op_gemm_nt_split3_sk(int M, int N, int K, const float* A, int lda, const float* A2, int lda2, int ksA,
                          const void* wr, const float* bias, int act, float* Y, int ldy, float* part,
                          size_t part_floats, hipStream_t s, int splits_fixed) {
+  return op_gemm_nt_split3_ex(M, N, K, A, lda, A2, lda2, ksA, wr, bias, act, Y, ldy, 0, nullptr, 0, INT_MAX, part,
+                              part_floats, s, splits_fixed);
+}
+
+int op_gemm_nt_split3_ex(int M, int N, int K, const float* A, int lda, const float* A2, int lda2, int ksA,
+                         const void* wr, const float* bias, int act, float* Y, int ldy, int accumulate, float* Y2,
+                         int ldy2, int nsplitY, float* part, size_t part_floats, hipStream_t s, int splits_fixed) {
+  const bool y2 = nsplitY < N;
   if (!op_gemm_nt_split3_supported(M, N, K, A, lda, A2, lda2, ksA, ldy) || ((uintptr_t)Y & 15) ||
       (bias && ((uintptr_t)bias & 15)) || ((uintptr_t)part & 15) || splits_fixed < 0 ||
-      splits_fixed > DR_S3_SPLITS || (splits_fixed > 1 && (!part || (size_t)splits_fixed * M * N > part_floats))) {
+      splits_fixed > DR_S3_SPLITS || (splits_fixed > 1 && (!part || (size_t)splits_fixed * M * N > part_floats)) ||
+      (y2 && (!Y2 || ((uintptr_t)Y2 & 15) || ldy2 % 4 || nsplitY % 4 || nsplitY < 0))) {
     dr_set_error("gemm_nt_split3: unsupported problem (M=%d N=%d K=%d)", M, N, K);
     return DR_E_INVALID;
   }
-  GemmS3 g = {M, N, K, ksA < K ? ksA : K, lda, lda2, ldy, act, s3_np(N), A, A2, (const u16*)wr, bias, Y, 1, part};
+  GemmS3 g = {M, N, K, ksA < K ? ksA : K, lda, lda2, ldy, act, s3_np(N), A, A2, (const u16*)wr, bias, Y, 1, part,
+              accumulate ? 1 : 0, ldy2, y2 ? nsplitY : INT_MAX, 0, Y2};
   auto tl = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   auto waves = [&](int bm, int bn) { return (long long)tl(bm, bn) * (bm / 32); };
   // the largest tile (256 x 128, 256 x 64, 128 x 128, 128 x 64, else 64 x 64)

@@ -140,7 +140,8 @@ static inline long long splitk_floats(long long M, long long N) { return DR_SPLI
 static inline int lnbwd_nt(int M, int N, int K, const float* gx, long long ldgx, const float* pre, long long ld_pre,
                     const dr_linear& ln, const float* WT, float* Y, long long ldy, int accumulate, float* gpre,
                     long long ld_gpre, float* gy, float* xh, float* Y2, long long ldy2, int nsplitY, hipStream_t s,
-                    const GruBwdEpi* gru_epi = nullptr) {
+                    const GruBwdEpi* gru_epi = nullptr, const void* planes = nullptr, float* sk = nullptr,
+                    long long sk_n = 0) {
   GemmArgs g = bwd_nt(M, N, K, gx, ldgx, WT, Y, ldy, accumulate);
   g.Y2 = Y2; g.ldy2 = ldy2; g.nsplitY = nsplitY;
   if (gru_epi) g.gb = *gru_epi;
@@ -162,6 +163,12 @@ static inline int lnbwd_nt(int M, int N, int K, const float* gx, long long ldgx,
   DR_REQUIRE(gpre != nullptr, "LN-backward fallback needs a g_pre buffer");
   DR_TRY(op_ln_silu_bwd(M, K, gx, ldgx, pre, ld_pre, ln.w, ln.b, gpre, ld_gpre, gy, xh, s));
   g.A = gpre; g.lda = ld_gpre;
+  if (planes) {  // tall products with weight planes: the split3 tall GEMM (gemm.hip s3_tall_ok; wplanes' layout)
+    g.wsplit = reinterpret_cast<const unsigned short*>(planes);
+    g.wsplit_np = (g.N + 127) / 128 * 128;
+    g.splitk_ws = sk;  // (its split-K partial sums, when given)
+    g.splitk_floats = sk ? sk_n : 0;
+  }
   return run(G_NT, AM_PLAIN, g, s);
 }
 

@@ -2629,11 +2629,53 @@ static bool tile_offsets_ok(const GemmBatch& gb, int count) {
   return true;
 }
 
+// tall NT products (>= 1024 rows) whose caller split the weights into planes,
+// f32 mode: the split3 tall GEMM of conv_split.hip (k_gemm_split3) with the
+// data-gradient epilogue (accumulate, split output).  The world-model
+// backward's K = 200 input gradients ran on the f32 tile kernel at ~21 TF/s.
+int op_gemm_nt_split3_ex(int M, int N, int K, const float* A, int lda, const float* A2, int lda2, int ksA,
+                         const void* wr, const float* bias, int act, float* Y, int ldy, int accumulate, float* Y2,
+                         int ldy2, int nsplitY, float* part, size_t part_floats, hipStream_t s, int splits_fixed);
+static bool s3_tall_ok(const GemmArgs& g) {
+  const bool seg = g.ksplitA < g.K;  // second A segment (A2 at k >= ksplitA)
+  return g.wsplit && !g.bf16 && g.M >= 1024 && g.epi == EPI_NONE && !g.out_conv && !g.W2 && !g.addend &&
+         g.alpha == 1.0f && (g.act == 0 || g.act == 1) &&
+         (!seg || (g.A2 && aligned16(g.A2) && g.ksplitA % 4 == 0 && g.lda2 % 4 == 0 &&
+                   (long long)g.M * g.lda2 < (1LL << 31))) &&
+         g.wsplit_np == (g.N + 127) / 128 * 128 &&
+         g.N % 4 == 0 && g.K % 4 == 0 && g.lda % 4 == 0 && g.ldy % 4 == 0 && aligned16(g.A) && aligned16(g.Y) &&
+         (!g.bias || aligned16(g.bias)) && (g.nsplitY >= g.N || (g.Y2 && aligned16(g.Y2) && g.ldy2 % 4 == 0 &&
+                                                                  g.nsplitY % 4 == 0)) &&
+         (long long)g.M * g.lda < (1LL << 31) && g.lda < INT_MAX && g.ldy < INT_MAX && g.ldy2 < INT_MAX;
+}
+
 // bf16 mode's chain products without weight planes on k_gemm_tile_b16 (the
 // f32 wave-K kernel measured 723.3 k against 730.5 k bf16 headline,
 // profiles/r03zf_ab_bf16_chain_route.txt)
 template <int AMODE, bool A_KM, bool B_KN>
 static int launch_pick(const GemmBatch& gb, int count, hipStream_t s) {
+  if (AMODE == AM_PLAIN && !A_KM && !B_KN) {
+    // problems of the batch that qualify run one after another on the split3
+    // tall GEMM, the rest as a (smaller) batch below
+    GemmBatch rest;
+    int nrest = 0;
+    for (int i = 0; i < count; ++i) {
+      const GemmArgs& g = gb.p[i];
+      if (!s3_tall_ok(g)) {
+        rest.p[nrest++] = g;
+        continue;
+      }
+      // (the 200-wide, K <= 1024 problems on the wave-K split3 kernel's 32 x 32
+      // tiles instead -- it fills the chip where 64 x 64 tiles leave ~450 waves
+      // -- measured the same WM step, r06t: not kept)
+      DR_TRY(op_gemm_nt_split3_ex(g.M, g.N, g.K, g.A, (int)g.lda, g.A2, (int)g.lda2, g.ksplitA < g.K ? g.ksplitA : g.K,
+                                  g.wsplit, g.bias, g.act, g.Y, (int)g.ldy, g.accumulate, g.Y2, (int)g.ldy2,
+                                  g.nsplitY < g.N ? g.nsplitY : INT_MAX, g.splitk_ws,
+                                  g.splitk_ws ? (size_t)g.splitk_floats : 0, s, 0));
+    }
+    if (nrest == 0) return DR_OK;
+    if (nrest < count) return launch_pick<AMODE, A_KM, B_KN>(rest, nrest, s);
+  }
   if (AMODE == AM_PLAIN && tile_offsets_ok(gb, count)) {
     int maxM = 0, minK = 1 << 30, tiles = 0;
     bool ws = true;

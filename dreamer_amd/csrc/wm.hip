@@ -307,6 +307,18 @@ struct WmWs {
   // the posterior scan's per-step products (latent_mapper.0's h-columns, W_hh)
   // as split3 planes for k_gemm_wks3 (B >= 128), as in dr_observe_scan
   void *s3m0, *s3whh;
+  // ... and of the scan backward's input-gradient products (W_ih^T's latent
+  // rows, W_hh^T; K = 3 Hd)
+  void *s3wtb, *s3twhh;
+  // split3 planes of the tall (B (T-1) / B T rows) NT products' weights: the
+  // heads' input-gradient Linears (.3 / .0 of each, the prior's .6), the
+  // decoder upscaler's .3 / .0, the encoder projection (forward, and its
+  // transposed input gradient) -- k_gemm_split3 instead of the f32 tile kernel
+  void *pl_h3[3], *pl_h0[3], *pl_h6, *pl_up3, *pl_up0, *pl_w0tp, *pl_map0f;
+  // ... and of the forward heads / upscaler over B (T - 1) rows: the first
+  // Linears (prior, reward, continue, upscaler.0), the .3 layers, the prior's
+  // .6, upscaler.3 (permuted rows)
+  void *pl_f0[4], *pl_f3[3], *pl_f6, *pl_fup3;
   // loss
   float *coef_row, *coef_obs, *obs_part, *obs_bpart, *kl_grp, *rew_row, *cont_row, *scal, *stats;
   float* csp;  // per-tile channel sums of the last decoder layer's input gradient (k_conv_nhwc csum)
@@ -431,6 +443,28 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
   w.x0 = c.f(Dv ? M * Dv : M * D.pix[0] * 4);
   w.s3m0 = c.raw(op_nt_split3_ws_bytes(eh, Hd));
   w.s3whh = c.raw(op_nt_split3_ws_bytes(3 * Hd, Hd));
+  w.s3wtb = c.raw(op_nt_split3_ws_bytes(L, 3 * Hd));
+  for (int i = 0; i < 3; ++i) {
+    w.pl_h3[i] = c.raw(op_nt_split3_ws_bytes(std::max(D.ph1, std::max(D.rh1, D.ch1)),
+                                             std::max(D.ph2, std::max(D.rh2, D.ch2))));
+    w.pl_h0[i] = c.raw(op_nt_split3_ws_bytes(Hd + L, std::max(D.ph1, std::max(D.rh1, D.ch1))));
+  }
+  w.pl_h6 = c.raw(op_nt_split3_ws_bytes(D.ph2, L));
+  if (!Dv) {
+    w.pl_up3 = c.raw(op_nt_split3_ws_bytes(D.dh, D.Fd));
+    w.pl_up0 = c.raw(op_nt_split3_ws_bytes(Hd + L, D.dh));
+  }
+  w.pl_w0tp = c.raw(op_nt_split3_ws_bytes(D.F, eh));
+  {
+    const int h1 = std::max(D.ph1, std::max(D.rh1, std::max(D.ch1, D.dh)));
+    const int h2 = std::max(D.ph2, std::max(D.rh2, D.ch2));
+    for (int i = 0; i < 4; ++i) w.pl_f0[i] = c.raw(op_nt_split3_ws_bytes(h1, Hd + L));
+    for (int i = 0; i < 3; ++i) w.pl_f3[i] = c.raw(op_nt_split3_ws_bytes(h2, h1));
+    w.pl_f6 = c.raw(op_nt_split3_ws_bytes(L, D.ph2));
+    if (!Dv) w.pl_fup3 = c.raw(op_nt_split3_ws_bytes(D.Fd, D.dh));
+  }
+  w.pl_map0f = c.raw(op_nt_split3_ws_bytes(eh, D.F));
+  w.s3twhh = c.raw(op_nt_split3_ws_bytes(Hd, 3 * Hd));
   if (Dv) {  // MLP stand-in: layer 0 and the last layer of the conv slots, [M][F] each
     w.pre[0] = c.f(M * D.F); w.a[0] = c.f(M * D.F);
     w.pre[N - 1] = c.f(M * D.F); w.a[N - 1] = c.f(M * D.F);
@@ -521,6 +555,9 @@ static void wm_carve(Carve& c, const dr_dims* d, const WmDims& D, WmWs& w) {
     long long mx = splitk_floats(1, L * eh + eh * (D.F + hd) + 3 * hd * (L + D.A) + 3 * hd * hd);
     mx = std::max(mx, splitk_floats(1, (long long)D.Fd * D.dh + (long long)D.dh * (hd + L)));
     mx = std::max(mx, splitk_floats(M, std::max(eh, (long long)D.dh)));
+    // the forward heads' four first Linears, each with its own slice (split-K
+    // of their K = Hd + L products on the split3 tall GEMM)
+    mx = std::max(mx, splitk_floats(D.M1, (long long)D.ph1 + D.rh1 + D.ch1 + D.dh));
     mx = std::max(mx, splitk_floats(1, (long long)D.nb * D.rh2 + (long long)D.rh2 * D.rh1 + D.rh1 * (hd + L)));
     w.sk_n = mx;
     w.sk = c.f(w.sk_n);
@@ -555,14 +592,28 @@ extern "C" size_t dr_wm_train_workspace_bytes(const dr_dims* d, int B, int T) {
 static int head_bwd(const WmDims& D, const dr_mlp3& m, const dr_mlp3& g, int w1, int w2, int nout, const float* glog,
                     const float* t6, const float* t3, const float* t0, const float* x1, const float* x2,
                     const float* pre1, const float* pre2, int in_z, const float* hB, const float* zB, float* gHB,
-                    float* gZB, MlpBwd& b, float* sk, long long sk_n, void* tn, size_t tn_bytes, hipStream_t s) {
+                    float* gZB, MlpBwd& b, float* sk, long long sk_n, void* tn, size_t tn_bytes, hipStream_t s,
+                    void* pl6 = nullptr, void* pl3 = nullptr, void* pl0 = nullptr) {
   const int terms = D.terms;
   const int M1 = D.M1, Hd = D.Hd, L = D.L;
-  DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M1, w2, nout, glog, nout, t6, b.gx2, w2, 0), s));
+  const int n0 = in_z ? Hd + L : Hd;
+  // tall (>= 1024 rows): the input-gradient products on split3 planes of the
+  // transposed weights, split here (the weights change every step)
+  const bool tall = M1 >= 1024;
+  if (!tall) pl6 = pl3 = pl0 = nullptr;
+  if (nout % 4) pl6 = nullptr;
+  if (pl6) DR_TRY(op_nt_repack_split3(w2, nout, t6, nout, pl6, s));
+  if (pl3) DR_TRY(op_nt_repack_split3(w1, w2, t3, w2, pl3, s));
+  if (pl0) DR_TRY(op_nt_repack_split3(n0, w1, t0, w1, pl0, s));
+  {
+    GemmArgs g6 = bwd_nt(M1, w2, nout, glog, nout, t6, b.gx2, w2, 0);
+    wplanes(g6, pl6);
+    DR_TRY(run(G_NT, AM_PLAIN, g6, s));
+  }
   DR_TRY(lnbwd_nt(M1, w1, w2, b.gx2, w2, pre2, w2, m.n4, t3, b.gx1, w1, 0, b.gp2, w2, b.gy2, b.xh2, nullptr, 0,
-                  INT_MAX, s));
-  DR_TRY(lnbwd_nt(M1, in_z ? Hd + L : Hd, w1, b.gx1, w1, pre1, w1, m.n1, t0, gHB, Hd, 1, b.gp1, w1, b.gy1, b.xh1,
-                  in_z ? gZB : nullptr, L, in_z ? Hd : INT_MAX, s));
+                  INT_MAX, s, nullptr, pl3, sk, sk_n));
+  DR_TRY(lnbwd_nt(M1, n0, w1, b.gx1, w1, pre1, w1, m.n1, t0, gHB, Hd, 1, b.gp1, w1, b.gy1, b.xh1,
+                  in_z ? gZB : nullptr, L, in_z ? Hd : INT_MAX, s, nullptr, pl0, sk, sk_n));
   GemmArgs p[3];
   p[0] = bwd_w(nout, w2, M1, glog, nout, x2, w2, g.l6.w);
   p[1] = bwd_w(w2, w1, M1, b.gp2, w2, x1, w1, g.l3.w);
@@ -715,6 +766,10 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   {
     GemmArgs g = lin(M, eh, F, aL, F, wm->map0.w, F + Hd, wm->map0.b, w.feat, eh);
     splitk_all(&g, 1, w.sk, w.sk_n);
+    if (M >= 1024) {  // the feature projection on split3 planes (as the epoch's warm-start encoder)
+      DR_TRY(op_nt_repack_split3(eh, F, wm->map0.w, F + Hd, w.pl_map0f, s));
+      wplanes(g, w.pl_map0f);
+    }
     DR_TRY(run(G_NT, AM_PLAIN, g, s));
   }
 
@@ -768,6 +823,14 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     p[1] = lin2(M1, D.rh1, hB, Hd, Hd, zB, L, L, wm->reward.l0.w, wm->reward.l0.b, w.rp1, D.rh1);
     p[2] = lin2(M1, D.ch1, hB, Hd, Hd, zB, L, L, wm->cont.l0.w, wm->cont.l0.b, w.cp1, D.ch1);
     p[3] = lin2(M1, D.dh, hB, Hd, Hd, zB, L, L, dec->up0.w, dec->up0.b, w.du1, D.dh);
+    if (M1 >= 1024) {  // tall: on split3 planes of the weights (gemm.hip s3_tall_ok), split per step
+      DR_TRY(op_nt_repack_split3(D.ph1, Hd, wm->prior.l0.w, Hd, w.pl_f0[0], s));
+      DR_TRY(op_nt_repack_split3(D.rh1, Hd + L, wm->reward.l0.w, Hd + L, w.pl_f0[1], s));
+      DR_TRY(op_nt_repack_split3(D.ch1, Hd + L, wm->cont.l0.w, Hd + L, w.pl_f0[2], s));
+      DR_TRY(op_nt_repack_split3(D.dh, Hd + L, dec->up0.w, Hd + L, w.pl_f0[3], s));
+      for (int i = 0; i < 4; ++i) wplanes(p[i], w.pl_f0[i]);
+      splitk_all(p, 4, w.sk, w.sk_n);
+    }
     DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, 4, s));
   }
   {
@@ -778,6 +841,12 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     p[1].a_out = w.rx1; p[1].ld_aout = D.rh1;
     p[2] = lin_ln(M1, D.ch2, D.ch1, w.cp1, D.ch1, wm->cont.n1, wm->cont.l3.w, wm->cont.l3.b, w.cp2, D.ch2);
     p[2].a_out = w.cx1; p[2].ld_aout = D.ch1;
+    if (M1 >= 1024) {
+      DR_TRY(op_nt_repack_split3(D.ph2, D.ph1, wm->prior.l3.w, D.ph1, w.pl_f3[0], s));
+      DR_TRY(op_nt_repack_split3(D.rh2, D.rh1, wm->reward.l3.w, D.rh1, w.pl_f3[1], s));
+      DR_TRY(op_nt_repack_split3(D.ch2, D.ch1, wm->cont.l3.w, D.ch1, w.pl_f3[2], s));
+      for (int i = 0; i < 3; ++i) wplanes(p[i], w.pl_f3[i]);
+    }
     DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, 3, s));
   }
   {
@@ -788,12 +857,20 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
     p[1].a_out = w.rx2; p[1].ld_aout = D.rh2;
     p[2] = lin_ln(M1, 1, D.ch2, w.cp2, D.ch2, wm->cont.n4, wm->cont.l6.w, wm->cont.l6.b, w.cont_lg, 1);
     p[2].a_out = w.cx2; p[2].ld_aout = D.ch2;
+    if (M1 >= 1024) {  // (the prior's 1024 outputs; the reward's 255 / continue's 1 stay on the tile kernel)
+      DR_TRY(op_nt_repack_split3(L, D.ph2, wm->prior.l6.w, D.ph2, w.pl_f6, s));
+      wplanes(p[0], w.pl_f6);
+    }
     DR_TRY(gemm_launch(G_NT, AM_LNSILU, p, 3, s));
   }
   // decoder (VAE.py:139-161): upscaler.3 pre-activation in NHWC, SiLU applied by the consumers
   {
     GemmArgs g = lin_ln(M1, D.Fd, D.dh, w.du1, D.dh, dec->up1, w.w3p, w.b3p, w.du2, D.Fd);
     g.a_out = w.dx1; g.ld_aout = D.dh;
+    if (M1 >= 1024 && !vec) {
+      DR_TRY(op_nt_repack_split3(D.Fd, D.dh, w.w3p, D.dh, w.pl_fup3, s));
+      wplanes(g, w.pl_fup3);
+    }
     DR_TRY(run(G_NT, AM_LNSILU, g, s));
   }
   if (vec) {
@@ -874,11 +951,14 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   DR_TRY(zero(w.gH, (long long)M * Hd, s));
   DR_TRY(zero(w.gZ, (long long)M * L, s));
   DR_TRY(head_bwd(D, wm->prior, gw->prior, D.ph1, D.ph2, L, w.g_prior, w.t_pl6, w.t_pl3, w.t_pl0, w.px1, w.px2, w.pp1,
-                  w.pp2, 0, hB, zB, gHB, gZB, w.bp, w.sk, w.sk_n, w.tn, w.tn_bytes, s));
+                  w.pp2, 0, hB, zB, gHB, gZB, w.bp, w.sk, w.sk_n, w.tn, w.tn_bytes, s, w.pl_h6, w.pl_h3[0],
+                  w.pl_h0[0]));
   DR_TRY(head_bwd(D, wm->reward, gw->reward, D.rh1, D.rh2, nb, w.g_rew, w.t_rl6, w.t_rl3, w.t_rl0, w.rx1, w.rx2, w.rp1,
-                  w.rp2, 1, hB, zB, gHB, gZB, w.br, w.sk, w.sk_n, w.tn, w.tn_bytes, s));
+                  w.rp2, 1, hB, zB, gHB, gZB, w.br, w.sk, w.sk_n, w.tn, w.tn_bytes, s, nullptr, w.pl_h3[1],
+                  w.pl_h0[1]));
   DR_TRY(head_bwd(D, wm->cont, gw->cont, D.ch1, D.ch2, 1, w.g_cont, w.t_cl6, w.t_cl3, w.t_cl0, w.cx1, w.cx2, w.cp1,
-                  w.cp2, 1, hB, zB, gHB, gZB, w.bc, w.sk, w.sk_n, w.tn, w.tn_bytes, s));
+                  w.cp2, 1, hB, zB, gHB, gZB, w.bc, w.sk, w.sk_n, w.tn, w.tn_bytes, s, nullptr, w.pl_h3[2],
+                  w.pl_h0[2]));
   // decoder: image_builder.6 .. .0 (data grads as strided convs, weight grads, bias sums)
   if (vec) {
     // image_builder stand-in backward: dgout = dL/dmu -> Wd2 / bd2 grads, dL/dq = (dgout Wd2) SiLU'(q)
@@ -941,10 +1021,15 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   {
     GemmArgs g = bwd_nt(M1, D.dh, D.Fd, w.dgu2, D.Fd, w.t_up3, w.gxu, D.dh, 0);
     splitk_all(&g, 1, w.sk, w.sk_n);
+    if (M1 >= 1024) {
+      DR_TRY(op_nt_repack_split3(D.dh, D.Fd, w.t_up3, D.Fd, w.pl_up3, s));
+      DR_TRY(op_nt_repack_split3(Hd + L, D.dh, w.t_up0, D.dh, w.pl_up0, s));
+      wplanes(g, w.pl_up3);
+    }
     DR_TRY(run(G_NT, AM_PLAIN, g, s));
   }
   DR_TRY(lnbwd_nt(M1, Hd + L, D.dh, w.gxu, D.dh, w.du1, D.dh, dec->up1, w.t_up0, gHB, Hd, 1, w.gpu, D.dh, w.gyu, w.xhu,
-                  gZB, L, Hd, s));
+                  gZB, L, Hd, s, nullptr, M1 >= 1024 ? w.pl_up0 : nullptr, w.sk, w.sk_n));
   {
     GemmArgs p[2];
     p[0] = bwd_w(D.Fd, D.dh, M1, w.dgu2, D.Fd, w.dx1, D.dh, w.dw3p);
@@ -967,6 +1052,14 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   if (bwd_scan) {
   // ---- backward through the posterior scan, t = T-1 .. 0 ----
   const int Wc = pow2_ge(d->cols);
+  // B >= 128: the per-step input-gradient products (K = 3 Hd) on the split3
+  // wave-K kernel from weight planes split once per step (the f32 wave-K
+  // kernel took 30.7 us per grouped launch at B = 256)
+  const bool bplanes = B >= 128 && T > 1 && (3 * Hd) % 8 == 0;
+  if (bplanes) {
+    DR_TRY(split_planes(L, 3 * Hd, w.wt, 3 * Hd, w.s3wtb, s));
+    DR_TRY(split_planes(Hd, 3 * Hd, w.t_whh, 3 * Hd, w.s3twhh, s));
+  }
   for (int t = T - 1; t >= 0; --t) {
     const long long rb = (long long)t * B;
     float* gH_t = w.gH + rb * Hd;
@@ -988,6 +1081,10 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
       GemmArgs p[2];
       p[0] = bwd_nt(B, L, 3 * Hd, w.ggi + rb * 3 * Hd, 3 * Hd, w.wt, w.gZ + (rb - B) * L, L, 1);
       p[1] = bwd_nt(B, Hd, 3 * Hd, w.ggh + rb * 3 * Hd, 3 * Hd, w.t_whh, gH_t - (long long)B * Hd, Hd, 1);
+      if (bplanes) {
+        wplanes(p[0], w.s3wtb);
+        wplanes(p[1], w.s3twhh);
+      }
       DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, 2, s));
     }
   }
@@ -1014,7 +1111,14 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   if (bwd_enc) {
   // ---- backward through the encoder convolutions (all M frames) ----
   float* gL = w.gp[N - 1];  // dL/d pre[N-1], NHWC (w0tp's rows are permuted to NHWC)
-  DR_TRY(run(G_NT, AM_PLAIN, bwd_nt(M, F, eh, w.gpre_m, eh, w.w0tp, gL, F, 0), s));
+  {
+    GemmArgs g = bwd_nt(M, F, eh, w.gpre_m, eh, w.w0tp, gL, F, 0);
+    if (M >= 1024) {
+      DR_TRY(op_nt_repack_split3(F, eh, w.w0tp, eh, w.pl_w0tp, s));
+      wplanes(g, w.pl_w0tp);
+    }
+    DR_TRY(run(G_NT, AM_PLAIN, g, s));
+  }
   hipLaunchKernelGGL(k_mul_dsilu, dim3(blocks((long long)M * F, 256)), dim3(256), 0, s, (long long)M * F, gL,
                      w.pre[N - 1]);
   DR_TRY(dr_check_launch("mul_dsilu"));
