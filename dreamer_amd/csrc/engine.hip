@@ -410,6 +410,7 @@ struct ImWs {
   // backward
   float *gH, *gZ, *gA, *glog, *gx2, *gp2, *gx1, *gp1, *ggi, *ggh, *gheads, *gx2a, *gpre2a, *gy2a, *xh2a, *gx1a,
       *gpre1a, *gy1a, *xh1a, *hcat, *zcat, *sk;
+  unsigned short *ggi16, *ggh16, *gpre1a16;  // bf16 mode: bf16 copies of ggi / ggh / gpre1a (GemmArgs.A16)
   long long sk_n;
   // transposed weights for the input-gradient GEMMs (NT with float4 loads)
   float *tl6p, *tl3p, *tl0p, *twhh, *thead, *tl3a, *tl0a;
@@ -467,6 +468,8 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.gp1 = c.f(Bl * d->prior_h1);
   w.ggi = c.f(Bl * 3 * Hd);
   w.ggh = c.f(Bl * 3 * Hd);
+  w.ggi16 = (unsigned short*)c.raw(sizeof(unsigned short) * Bl * 3 * Hd);
+  w.ggh16 = (unsigned short*)c.raw(sizeof(unsigned short) * Bl * 3 * Hd);
   w.gheads = c.f(BH * 2 * A);
   w.gx2a = c.f(Bl * d->actor_h2);
   w.gpre2a = c.f(BH * d->actor_h2);
@@ -474,6 +477,7 @@ static void imws_carve(Carve& c, const dr_dims* d, int B, int H, ImWs& w) {
   w.xh2a = c.f(BH * d->actor_h2);
   w.gx1a = c.f(Bl * d->actor_h1);
   w.gpre1a = c.f(BH * d->actor_h1);
+  w.gpre1a16 = (unsigned short*)c.raw(sizeof(unsigned short) * BH * d->actor_h1);
   w.gy1a = c.f(BH * d->actor_h1);
   w.xh1a = c.f(BH * d->actor_h1);
   w.hcat = c.f(BH * Hd);
@@ -847,6 +851,13 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
       ge.h = hiddens + (long long)t * Hd; ge.ldh = ldH;
       ge.r = tp.r + hb; ge.u = tp.u + hb; ge.n = tp.n + hb; ge.ghn = tp.ghn + hb;
       ge.gi = w.ggi; ge.gh = w.ggh; ge.ho = gH_t; ge.ldo = ldH; ge.Hd = Hd;
+      // bf16 mode on the weight planes: bf16 copies of the gates' gradients for
+      // the input-gradient products below (GemmArgs.A16; bitwise the same)
+      const bool a16 = planes && d->precision == DR_PREC_BF16;
+      if (a16) {
+        ge.gi16 = w.ggi16;
+        ge.gh16 = w.ggh16;
+      }
       DR_TRY(lnbwd_nt(B, Hd, h1, w.gx1, h1, tp.pre1p + (long long)t * B * h1, h1, wm->prior.n1, w.tl0p, gH_n, ldH, 1,
                       w.gp1, h1, nullptr, nullptr, nullptr, 0, INT_MAX, s, &ge));
       if (t > 0) {
@@ -857,6 +868,10 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
         if (planes) {
           wplanes(p[0], w.s3wt);
           wplanes(p[1], w.s3twhh);
+        }
+        if (a16) {
+          p[0].A16 = w.ggi16;
+          p[1].A16 = w.ggh16;
         }
         DR_TRY(gemm_launch(G_NT, AM_PLAIN, p, 2, s));
       } else {
@@ -880,9 +895,11 @@ static int imagine_bwd_impl(const dr_dims* d, const dr_world_model* wm, const dr
       // B >= 128: the LN-SiLU backward as its own pass, then the K = a1 input
       // gradient [gH_t | gZ_t] on the wave-K split3 kernel (weight planes of
       // the transposed base_net.0, split once per call)
+      const bool a16 = d->precision == DR_PREC_BF16 && lda1 % 8 == 0;
       DR_TRY(op_ln_silu_bwd(B, a1, w.gx1a, a1, tp.pre1a + o1, lda1, ac->n1.w, ac->n1.b, w.gpre1a + o1, lda1,
-                            w.gy1a + o1, w.xh1a + o1, s));
+                            w.gy1a + o1, w.xh1a + o1, s, a16 ? w.gpre1a16 + o1 : nullptr));
       GemmArgs g = bwd_nt(B, Hd + L, a1, w.gpre1a + o1, lda1, w.tl0a, gH_t, ldH, 1);
+      if (a16) g.A16 = w.gpre1a16 + o1;  // (bitwise the same one-term products)
       g.Y2 = gZ_t; g.ldy2 = ldL; g.nsplitY = Hd;
       wplanes(g, w.s3tl0a);
       DR_TRY(run(G_NT, AM_PLAIN, g, s));

@@ -28,6 +28,7 @@ struct GruBwdEpi {
   float *gi, *gh;                        // [M][3 Hd]
   float* ho; long long ldo;              // dL/dh (+=)
   int Hd, pad_;
+  unsigned short *gi16, *gh16;           // optional bf16 (RNE) copies of gi / gh (bf16 mode's GemmArgs.A16)
 };
 
 struct alignas(16) GemmArgs {

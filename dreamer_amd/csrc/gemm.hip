@@ -403,6 +403,16 @@ __device__ __noinline__ void gru_bwd_elem(const GruBwdEpi& e, int m, int j, floa
   ghb[j] = g_pr;
   ghb[Hd + j] = g_pu;
   ghb[2 * Hd + j] = g_hn;
+  if (e.gi16) {
+    DR_GLOBAL unsigned short* gi16 = dr_g(e.gi16) + (long long)m * 3 * Hd;
+    DR_GLOBAL unsigned short* gh16 = dr_g(e.gh16) + (long long)m * 3 * Hd;
+    gi16[j] = __builtin_bit_cast(unsigned short, (__bf16)g_pr);
+    gi16[Hd + j] = __builtin_bit_cast(unsigned short, (__bf16)g_pu);
+    gi16[2 * Hd + j] = __builtin_bit_cast(unsigned short, (__bf16)g_pn);
+    gh16[j] = __builtin_bit_cast(unsigned short, (__bf16)g_pr);
+    gh16[Hd + j] = __builtin_bit_cast(unsigned short, (__bf16)g_pu);
+    gh16[2 * Hd + j] = __builtin_bit_cast(unsigned short, (__bf16)g_hn);
+  }
   DR_GLOBAL float* o = dr_g(e.ho) + (long long)m * e.ldo + j;
   *o = *o + g_hmn;
 }

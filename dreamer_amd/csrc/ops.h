@@ -20,7 +20,7 @@ int op_softmax_ste_bwd(int M, int R, int C, const float* gz, long long ldg, cons
 // LayerNorm(eps 1e-5) + SiLU backward per row: gx = dL/d silu-out, pre = LN input
 int op_ln_silu_bwd(int M, int K, const float* gx, long long ldgx, const float* pre, long long ldp,
                    const float* gamma, const float* beta, float* g_pre, long long ldgp, float* gy, float* xhat,
-                   hipStream_t s);
+                   hipStream_t s, unsigned short* g_pre16 = nullptr);  // g_pre16: optional bf16 (RNE) copy of g_pre
 // out[n] (+)= sum_m X[m][n] * (Y ? Y[m][n] : 1)
 // several column sums in one launch (bias / LayerNorm parameter gradients)
 struct ColsumJob {

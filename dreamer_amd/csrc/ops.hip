@@ -210,7 +210,7 @@ template <bool REG>
 __global__ void k_ln_silu_bwd(int M, int K, const float* __restrict__ gx, long long ldgx,
                               const float* __restrict__ pre, long long ldp, const float* __restrict__ gamma,
                               const float* __restrict__ beta, float* __restrict__ g_pre, long long ldgp, float* gy_out,
-                              float* xhat_out) {
+                              float* xhat_out, unsigned short* __restrict__ g_pre16) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
   const float* p = pre + (long long)row * ldp;
@@ -261,7 +261,11 @@ __global__ void k_ln_silu_bwd(int M, int K, const float* __restrict__ gx, long l
 #pragma unroll
     for (int i = 0; i < LNB_NPL; ++i) {
       const int k = lane + 64 * i;
-      if (k < K) g_pre[(long long)row * ldgp + k] = rstd * (gv[i] - c1 - pv[i] * c2);
+      if (k < K) {
+        const float gp = rstd * (gv[i] - c1 - pv[i] * c2);
+        g_pre[(long long)row * ldgp + k] = gp;
+        if (g_pre16) g_pre16[(long long)row * ldgp + k] = __builtin_bit_cast(unsigned short, (__bf16)gp);
+      }
     }
     return;
   }
@@ -295,20 +299,22 @@ __global__ void k_ln_silu_bwd(int M, int K, const float* __restrict__ gx, long l
     const float y = xh * gamma[k] + beta[k];
     const float sg = 1.0f / (1.0f + expf(-y));
     const float gxh = g[k] * (sg * (1.0f + y * (1.0f - sg))) * gamma[k];
-    g_pre[(long long)row * ldgp + k] = rstd * (gxh - c1 - xh * c2);
+    const float gp = rstd * (gxh - c1 - xh * c2);
+    g_pre[(long long)row * ldgp + k] = gp;
+    if (g_pre16) g_pre16[(long long)row * ldgp + k] = __builtin_bit_cast(unsigned short, (__bf16)gp);
   }
 }
 
 int op_ln_silu_bwd(int M, int K, const float* gx, long long ldgx, const float* pre, long long ldp,
                    const float* gamma, const float* beta, float* g_pre, long long ldgp, float* gy, float* xhat,
-                   hipStream_t s) {
+                   hipStream_t s, unsigned short* g_pre16) {
   if (M == 0) return DR_OK;
   if (K <= 64 * LNB_NPL)
     hipLaunchKernelGGL(k_ln_silu_bwd<true>, dim3(dr_cdiv(M, 4)), dim3(256), 0, s, M, K, gx, ldgx, pre, ldp, gamma,
-                       beta, g_pre, ldgp, gy, xhat);
+                       beta, g_pre, ldgp, gy, xhat, g_pre16);
   else
     hipLaunchKernelGGL(k_ln_silu_bwd<false>, dim3(dr_cdiv(M, 4)), dim3(256), 0, s, M, K, gx, ldgx, pre, ldp, gamma,
-                       beta, g_pre, ldgp, gy, xhat);
+                       beta, g_pre, ldgp, gy, xhat, g_pre16);
   return dr_check_launch("ln_silu_bwd");
 }
 
