@@ -2555,6 +2555,8 @@ static bool wks3_ok(const GemmBatch& gb, int count) {
 // 16-row fragments per tile: 2 (32 x 32 tiles) for the fp32 products, 1 for
 // bf16 mode's (16 x 32 tiles: 828 -> 838 k bf16 headline; fp32 595 -> 587 k,
 // kept at 2; 8 or 2 waves per tile: +0.2 % / -6 %, profiles/r05zh_ab_wks3_shape.txt)
+// (64-column tiles, half the A re-reads: fp32 32 x 64 596 -> 567 k, 16 x 64
+// 567 k, bf16 16 x 64 917 -> 899 k; not kept, profiles/r06w_ab_wks3_columns.txt)
 #define DR_WKS3_NW 4  // waves per tile (each a 1/NW share of K)
 #define DR_WKS3_FM 2
 #define DR_WKS3_FM_B16 1
