@@ -1335,7 +1335,11 @@ int op_convT_split3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s, 
 // Low-resolution sizes are powers of two (shift addressing).
 // ---------------------------------------------------------------------------
 // (Round 6: the six-product form runs on k_wgrad_split3_db below; this kernel
-// keeps the one-term form, whose single buffer is 55-83 KB.)
+// keeps the one-term form, whose single buffer is 55-83 KB: on the
+// double-buffered kernel the one-term WM step measured 8.50 -> 8.64 ms with
+// 32-pixel chunks, 8.52 with 64 for the 128-channel layers,
+// profiles/r06x_ab_wgrad_db_one_term.txt -- without the split there is little
+// VALU for the second buffer to overlap.)
 // TERMS = 1: both operands RNE-rounded to one bf16 plane (bf16 world-model
 // step); that form also takes BN = 256 column tiles (the output-gradient rows
 // re-read half as often: 255 -> 209 us for the 128-channel layers, r04r) and
