@@ -336,6 +336,122 @@ __global__ __launch_bounds__(256) void k_conv1_direct(int n_frames, int ih, int 
 }
 
 
+// The SiLU-backward form of k_conv1_direct (CONV_EPI_DSILU, NHWC): the input
+// gradient of the decoder's last transposed conv (dL/d pre-tanh, 4 channels at
+// 64^2) into the 32-channel layer below, out = acc * SiLU'(pre).  The
+// LDS-tiled kernel ran it as three dependent round trips per workgroup (stage,
+// stage, then the epilogue's pre loads) at three workgroups per CU: 380 us for
+// 1.18 GB, 3.1 TB/s (WM step fp32 12.44 -> 12.35 ms, bf16 8.52 -> 8.44 ms with
+// this kernel, profiles/r06z1_ab_conv4_direct_dsilu.txt).  Here every wave issues its A / B fragments AND its pre
+// float4s up front, so one round trip covers the whole tile.  Same k
+// permutation and MFMA order: bitwise the same `out`.  csum (the tile's
+// per-channel sums, the next layer's bias-gradient partials): lanes of one
+// channel (xor over r, fragments i in order), then the 4 waves in LDS.
+__global__ __launch_bounds__(256) void k_conv4_direct_dsilu(int n_frames, int ih, int iw, int cout,
+                                                           const float* __restrict__ in, const float* __restrict__ wr,
+                                                           const float* __restrict__ pre, float* __restrict__ out,
+                                                           float* __restrict__ csum) {
+  constexpr int K = 64, WPX = 32;
+  __shared__ float s_cs[4][32];
+  const int oh = ih / 2, ow = iw / 2, hw = oh * ow;
+  const long long M = (long long)n_frames * hw;
+  const int tiles_n = cout / 32;
+  const long long tiles = ((M + 127) / 128) * tiles_n;
+  const int lt = dr_xcd_tile(blockIdx.x, (int)tiles);
+  if (lt < 0) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, q = lane >> 4;
+  const long long mt = (long long)(lt / tiles_n) * 128;
+  const long long m0 = mt + wave * WPX;
+  const int n0 = (lt % tiles_n) * 32;
+
+  float4 a[4][2], b[4][2];
+  f32x4 pv[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long long m = m0 + 16 * i + r;
+    const bool ok = m < M;
+    const long long mm = ok ? m : 0;
+    const long long f = mm / hw;
+    const int p = (int)(mm - f * hw), oy = p / ow, ox = p - oy * ow;
+    const float* base = in + f * ih * iw * 4;
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) {
+      const int tap = 4 * sl + q, y = 2 * oy - 1 + (tap >> 2), x = 2 * ox - 1 + (tap & 3);
+      const bool in_ok = ok && y >= 0 && y < ih && x >= 0 && x < iw;
+      const float4 t = *reinterpret_cast<const float4*>(base + (in_ok ? ((long long)y * iw + x) * 4 : 0));
+      a[sl][i] = in_ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) pv[i][j] = *reinterpret_cast<const f32x4*>(pre + mm * cout + n0 + 16 * j + 4 * q);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl)
+      b[sl][j] = *reinterpret_cast<const float4*>(wr + (long long)(n0 + 16 * j + r) * K + 16 * sl + 4 * q);
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int sl = 0; sl < 4; ++sl) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[sl][j].x, a[sl][i].x, acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[sl][j].y, a[sl][i].y, acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[sl][j].z, a[sl][i].z, acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[sl][j].w, a[sl][i].w, acc[i][j], 0, 0, 0);
+  }
+  float cs[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cs[j][e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const long long m = m0 + 16 * i + r;
+      if (m >= M) continue;
+      const int co = n0 + 16 * j + 4 * q;
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * dr_dsilu_fast(pv[i][j][e]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cs[j][e] += v[e];
+      *reinterpret_cast<f32x4*>(out + m * cout + co) = v;
+    }
+  if (csum) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = cs[j][e];
+        t += __shfl_xor(t, 1, 64);
+        t += __shfl_xor(t, 2, 64);
+        t += __shfl_xor(t, 4, 64);
+        t += __shfl_xor(t, 8, 64);
+        if (r == 0) s_cs[wave][16 * j + 4 * q + e] = t;
+      }
+    __syncthreads();
+    if (threadIdx.x < 32)
+      csum[(mt / 128) * cout + n0 + threadIdx.x] =
+          ((s_cs[0][threadIdx.x] + s_cs[1][threadIdx.x]) + s_cs[2][threadIdx.x]) + s_cs[3][threadIdx.x];
+  }
+}
+
 // k_conv1_direct fed from the frames themselves (with the hardware-exp2 SiLU,
 // so no longer bitwise equal to it: ~2 ulp, tests/test_gpu_bf16.py checks the
 // fp32 stack against torch at 1e-5).  A workgroup's 128 output
@@ -582,6 +698,17 @@ int op_conv_nhwc_ex(int n, int cin, int ih, int iw, int cout, const float* in, c
   if (epi == CONV_EPI_DSILU && (out_nchw || !pre)) {
     dr_set_error("conv: the SiLU-backward epilogue needs NHWC output and a pre-activation tensor");
     return DR_E_INVALID;
+  }
+  if (cin == 4 && epi == CONV_EPI_DSILU && cout % 32 == 0 &&
+      ((((uintptr_t)in | (uintptr_t)wr | (uintptr_t)pre | (uintptr_t)out) & 15) == 0)) {
+    const long long tiles = (((long long)n * (ih / 2) * (iw / 2) + 127) / 128) * (cout / 32);
+    if (tiles >= (1LL << 30)) {
+      dr_set_error("conv: too many tiles");
+      return DR_E_INVALID;
+    }
+    hipLaunchKernelGGL(k_conv4_direct_dsilu, dim3((unsigned)dr_xcd_grid((int)tiles)), dim3(256), 0, s, n, ih, iw, cout,
+                       in, wr, pre, out, csum);
+    return dr_check_launch("conv4_direct_dsilu");
   }
 #define DR_CONV_L(BM, BN, C, NCHW)                                                                \
   (epi == CONV_EPI_DSILU                                                                          \
