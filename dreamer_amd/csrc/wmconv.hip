@@ -522,6 +522,11 @@ int op_convT_nhwc(int epi, const ConvTArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
+// (Round 6: a row-staged form for the 4-channel layers -- contiguous loads of
+// whole low-resolution rows and the 4 hi rows they need, B fragments built by
+// offset from LDS, 4x finer splits -- measured the same WM step, 12.35 -> 12.36
+// ms fp32, 8.44 -> 8.48 ms bf16, profiles/r06z2_ab_conv4_wgrad.txt: this loop is
+// bound by its own LDS reads and barrier, not by the gathered loads.)
 // weight gradient: GEMM [ca] x [16*cb] over K = n*h*w low-res pixels, split-K
 // into deterministic partial planes (no atomics) and one ordered reduction.
 // Column n = tap * cb + b, so a float4 of the hi operand is 4 channels of one
