@@ -29,6 +29,7 @@
 
 #include <algorithm>
 
+
 namespace {
 typedef unsigned short u16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -228,6 +229,268 @@ int op_conv_glds_bf16(int n, int cin, int ih, int iw, int cout, const void* in, 
   if (cin == C)                                                                                   \
     return out_nchw ? launch_glds<C, true>(n, ih, iw, cout, in, wr, bias, out, s)                 \
                     : launch_glds<C, false>(n, ih, iw, cout, in, wr, bias, out, s);
+  DR_GL(32)
+  DR_GL(64)
+  DR_GL(128)
+  DR_GL(256)
+#undef DR_GL
+  return DR_E_INVALID;
+}
+
+// ---------------------------------------------------------------------------
+// fp32 mode's encoder convolutions conv3.. on the same LDS-DMA staging:
+// f32-accurate (the six split3 products of conv_split.hip's header) with the
+// f32 NHWC activations moved global -> LDS by LDS-DMA as they are, and split
+// per wave when the fragments are read.
+//
+// Why: k_conv_split3 (256 x 128 tiles, register-staged) splits each staged
+// float4 once per workgroup, but the staging sits between two barriers of the
+// chunk loop -- every wave loads, splits, stores to LDS, waits, then runs its
+// 96 MFMAs -- so the split and the LDS stores never overlap the MFMA pipe:
+// 0.45-0.47 of the split ceiling (conv3 718 us, conv4 692 us at 8192 frames,
+// profiles/r06z_epoch_kernel_table.txt).  Here the staging is LDS-DMA (8 or 6
+// instructions per wave and chunk); each wave owns 32 pixel rows x all 128
+// channels (8 waves x 1), so an A fragment is split by exactly one wave (no
+// duplicated split: 16 f32 per lane and chunk, ~1 VALU per MFMA), and the two
+// waves of a SIMD ping-pong between reading and multiplying (below): conv3 /
+// conv4 627 / 587 us, ~1.3-1.4 PFLOP/s of bf16 MFMA work under the chip's
+// load clock (profiles/r06z4_ab_conv_glds_s3.txt).  The per-accumulator order of
+// the six products and the chunk sequence are k_conv_split3's, so the output
+// is bitwise that kernel's.
+// LDS per stage: A 256 rows x 128 B (f32, 8 units a row, unit u of row r at
+// u ^ f[(r >> 1) & 7], f = {0,1,0,1,6,7,6,7}: the two ds_read_b128 of a lane
+// (units 2q, 2q + 1) are conflict-free in every 16-lane group of the b128
+// read) + B 3 planes x 128 rows x 64 B (g_swz); 56 KB, two stages, one
+// workgroup (8 waves, 2 per SIMD) per CU.
+// ---------------------------------------------------------------------------
+namespace {
+__device__ __forceinline__ int g_swz8(int row) { return (0x76761010 >> (((row >> 1) & 7) * 4)) & 7; }
+__device__ const float g_zero32[16] = {0.f};
+}  // namespace
+
+constexpr int GS_M = 256, GS_N = 128;
+constexpr int GS_AU = GS_M * 8, GS_BU = 3 * GS_N * 4, GS_STU = GS_AU + GS_BU;  // 16-byte units per stage
+
+template <int CIN, bool OUT_NCHW>
+__global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, int iw, int cout,
+                                                          const float* __restrict__ in, const u16* __restrict__ wr,
+                                                          const float* __restrict__ bias, float* __restrict__ out,
+                                                          float* __restrict__ pre) {
+  constexpr int K = CIN * 16, NCH = K / 32;
+  static_assert(CIN % 32 == 0 && NCH >= 2, "conv_glds_s3 tile");
+  __shared__ __attribute__((aligned(16))) u32x4 sm[2 * GS_STU];
+  const int oh = ih / 2, ow = iw / 2, hw = oh * ow;
+  const long long M = (long long)n_frames * hw;
+  const int tiles_n = cout / GS_N;
+  const long long tiles = ((M + GS_M - 1) / GS_M) * tiles_n;
+  const int lt = dr_xcd_tile(blockIdx.x, (int)tiles);
+  if (lt < 0) return;
+  const long long m0 = (long long)(lt / tiles_n) * GS_M;
+  const int n0 = (lt % tiles_n) * GS_N;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int r = lane & 15, q = lane >> 4;
+
+  // Ping-pong: waves 0-3 (X, one per SIMD) and 4-7 (Y) alternate between
+  // barrier-separated phases -- while X runs its 96 MFMAs on chunk c, Y reads and
+  // splits chunk c from LDS; then Y multiplies while X reads chunk c + 1 -- so each
+  // SIMD's MFMA pipe is fed by one wave while the other does its LDS / VALU work.
+  // DMA of chunk c + 1 (two stages: the stage it refills held chunk c - 1, read
+  // by X and Y in the two phases before): X issues the A rows in its read phase
+  // of chunk c, Y the B planes in its read phase of chunk c, each waiting for its
+  // own before the barrier that precedes X's read of chunk c + 1.  DMA issued
+  // inside an MFMA phase measured slower (conv3 631 -> 746 us), all of it by X
+  // in its read phase about the same (631 / 591 us against 628 / 587 us,
+  // profiles/r06z5_ab_conv_glds_dma.txt).
+  constexpr int NA = 8, NB = 2;  // DMA instructions per wave: A rows / 8 (X), B rows / 16 per plane (Y)
+  const bool X = wave < 4;
+  const int dw = wave & 3;
+  // A DMA: lane l of instruction i -> row dw * 8 NA + 8 i + l / 8, LDS unit l % 8 = source unit ^ swizzle
+  int pb[NA];
+  unsigned vm[NA];
+  int au[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int row = dw * 8 * NA + i * 8 + (lane >> 3);
+    const long long m = m0 + row;
+    const int mm = (int)(m < M ? m : 0);
+    const int f = mm / hw, p = mm - f * hw, oy = p / ow, ox = p - oy * ow;
+    const int y0 = 2 * oy - 1, x0 = 2 * ox - 1;
+    pb[i] = ((f * ih + y0) * iw + x0) * CIN;
+    unsigned v = 0u;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      v |= (y0 + t >= 0 && y0 + t < ih) ? (1u << t) : 0u;
+      v |= (x0 + t >= 0 && x0 + t < iw) ? (16u << t) : 0u;
+    }
+    vm[i] = m < M ? v : 0u;
+    au[i] = 4 * ((lane & 7) ^ g_swz8(row));
+  }
+  // B DMA: 16-row blocks dw * NB + h of each of the 3 planes
+  long long bbase[NB];
+#pragma unroll
+  for (int h = 0; h < NB; ++h) {
+    const int brow = (dw * NB + h) * 16 + (lane >> 2);
+    bbase[h] = (long long)(n0 + brow) * 32 + 8 * ((lane & 3) ^ g_swz(brow));
+  }
+
+  // parts: bit 0 = the A rows, bit 1 = the B planes
+  auto issue = [&](int c, int parts) __attribute__((always_inline)) {
+    int tap, ci0, kc;
+    g_chunk<CIN>(c, tap, ci0, kc);
+    const int ky = tap >> 2, kx = tap & 3;
+    const int toff = (ky * iw + kx) * CIN + ci0;
+    u32x4* st = sm + (c & 1) * GS_STU;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      if (!(parts & 1)) break;
+      const bool ok = (vm[i] >> ky) & (vm[i] >> (4 + kx)) & 1u;
+      const float* src = ok ? in + (pb[i] + toff + au[i]) : g_zero32;
+      __builtin_amdgcn_global_load_lds(src, st + (dw * NA + i) * 64, 16, 0, 0);
+    }
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int h = 0; h < NB; ++h) {
+        if (!(parts & 2)) break;
+        const u16* bs = wr + ((long long)kc * 3 + pl) * cout * 32 + bbase[h];
+        u32x4* bd = st + GS_AU + (pl * GS_N + (dw * NB + h) * 16) * 4;
+        __builtin_amdgcn_global_load_lds(bs, bd, 16, 0, 0);
+      }
+  };
+
+  const int wm0 = wave * 32;
+  const int fa0 = (2 * q) ^ g_swz8(r), fa1 = (2 * q + 1) ^ g_swz8(r);  // A rows are 16-aligned
+  const int fu = q ^ g_swz(r);
+  f32x4 acc[2][8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  u32x4 a[3][2], b[3][8];
+  auto fetch = [&](int c) __attribute__((always_inline)) {
+    const u32x4* st = sm + (c & 1) * GS_STU;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const f32x4 v0 = __builtin_bit_cast(f32x4, st[(wm0 + 16 * i + r) * 8 + fa0]);
+      const f32x4 v1 = __builtin_bit_cast(f32x4, st[(wm0 + 16 * i + r) * 8 + fa1]);
+      unsigned h[4], m[4], l[4];
+      split3_pair(v0[0], v0[1], h[0], m[0], l[0]);
+      split3_pair(v0[2], v0[3], h[1], m[1], l[1]);
+      split3_pair(v1[0], v1[1], h[2], m[2], l[2]);
+      split3_pair(v1[2], v1[3], h[3], m[3], l[3]);
+      a[0][i] = (u32x4){h[0], h[1], h[2], h[3]};
+      a[1][i] = (u32x4){m[0], m[1], m[2], m[3]};
+      a[2][i] = (u32x4){l[0], l[1], l[2], l[3]};
+    }
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[pl][j] = st[GS_AU + (pl * GS_N + 16 * j + r) * 4 + fu];
+  };
+  // k_conv_split3's order per accumulator: smallest terms first
+  auto multiply = [&]() __attribute__((always_inline)) {
+#define DR_GS3(PA, PB)                                                                                   \
+  _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int j = 0; j < 8; ++j) acc[i][j] = \
+      OUT_NCHW ? g_mfma(a[PA][i], b[PB][j], acc[i][j]) : g_mfma(b[PB][j], a[PA][i], acc[i][j]);
+    DR_GS3(2, 0)
+    DR_GS3(1, 1)
+    DR_GS3(0, 2)
+    DR_GS3(1, 0)
+    DR_GS3(0, 1)
+    DR_GS3(0, 0)
+#undef DR_GS3
+  };
+
+  if (X) {
+    issue(0, 3);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (!X) __builtin_amdgcn_s_barrier();  // Y runs one phase behind X
+#pragma unroll 1
+  for (int c = 0; c < NCH; ++c) {
+    // read phase: chunk c's fragments into registers, split; chunk c + 1's DMA
+    if (c + 1 < NCH) issue(c + 1, X ? 1 : 2);
+    fetch(c);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the stage may be refilled after the next barrier
+    if (!X) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // MFMA phase
+    multiply();
+    if (X) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk c + 1's A rows landed before X reads them
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (X) __builtin_amdgcn_s_barrier();
+
+  // k_conv_split3's CONV_EPI_FWD epilogue: out = SiLU(acc + bias), pre = acc + bias (NHWC) when given
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (OUT_NCHW) {
+        const long long m = m0 + wm0 + 16 * i + 4 * q;
+        const int co = n0 + 16 * j + r;
+        if (m >= M) continue;
+        f32x4 v = acc[i][j] + bias[co];
+        if (pre) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pre[(m + e) * cout + co] = v[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(v[e]);
+        const long long f = m / hw;
+        *reinterpret_cast<f32x4*>(out + (f * cout + co) * hw + (m - f * hw)) = v;
+      } else {
+        const long long m = m0 + wm0 + 16 * i + r;
+        const int co = n0 + 16 * j + 4 * q;
+        if (m >= M) continue;
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + co);
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + bv[e];
+        if (pre) *reinterpret_cast<f32x4*>(pre + m * cout + co) = v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = dr_silu_fast(v[e]);
+        *reinterpret_cast<f32x4*>(out + m * cout + co) = v;
+      }
+    }
+}
+
+bool op_conv_glds_s3_supported(int n, int cin, int ih, int iw, int cout) {
+  return op_conv_glds_bf16_supported(n, cin, ih, iw, cout);
+}
+
+template <int C, bool NCHW>
+static int launch_glds_s3(int n, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
+                          float* out, float* pre, hipStream_t s) {
+  const long long M = (long long)n * (ih / 2) * (iw / 2);
+  const long long tiles = ((M + GS_M - 1) / GS_M) * (cout / GS_N);
+  if (tiles >= (1LL << 30)) {
+    dr_set_error("conv_glds_s3: too many tiles");
+    return DR_E_INVALID;
+  }
+  hipLaunchKernelGGL((k_conv_glds_s3<C, NCHW>), dim3((unsigned)dr_xcd_grid((int)tiles)), dim3(512), 0, s, n, ih, iw,
+                     cout, in, (const u16*)wr, bias, out, pre);
+  return dr_check_launch("conv_glds_s3");
+}
+
+// f32 NHWC in, f32 NHWC / NCHW out (+ optional NHWC pre-activation), weights as
+// op_conv_repack_split3 planes; DR_E_INVALID (nothing launched) for other shapes
+int op_conv_glds_s3(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
+                    float* out, int out_nchw, float* pre, hipStream_t s) {
+  if (!op_conv_glds_s3_supported(n, cin, ih, iw, cout) ||
+      (((uintptr_t)in | (uintptr_t)wr | (uintptr_t)out | (uintptr_t)bias | (uintptr_t)pre) & 15)) {
+    dr_set_error("conv_glds_s3: unsupported shape (cin=%d ih=%d iw=%d cout=%d)", cin, ih, iw, cout);
+    return DR_E_INVALID;
+  }
+#define DR_GL(C)                                                                                  \
+  if (cin == C)                                                                                   \
+    return out_nchw ? launch_glds_s3<C, true>(n, ih, iw, cout, in, wr, bias, out, pre, s)         \
+                    : launch_glds_s3<C, false>(n, ih, iw, cout, in, wr, bias, out, pre, s);
   DR_GL(32)
   DR_GL(64)
   DR_GL(128)
