@@ -40,10 +40,10 @@ int op_conv_s1_bf16(int n, int cin, int ih, int iw, int cout, const void* in, co
                     void* out, int out_nchw, hipStream_t s);
 // the same convolution with LDS-DMA staged operands, four stages deep (conv_glds.hip; cout % 128 == 0)
 bool op_conv_glds_bf16_supported(int n, int cin, int ih, int iw, int cout);
-// fp32 (six split3 products) on the LDS-DMA staging: f32 NHWC in, CONV_EPI_FWD epilogue
+// fp32 (six split3 products) on the LDS-DMA staging: f32 NHWC in, CONV_EPI_FWD / CONV_EPI_DSILU epilogues
 bool op_conv_glds_s3_supported(int n, int cin, int ih, int iw, int cout);
 int op_conv_glds_s3(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
-                    float* out, int out_nchw, float* pre, hipStream_t s);
+                    float* out, int out_nchw, float* pre, int epi, hipStream_t s);
 // bf16 NT GEMM Y = X W^T + bias (X [M][K], W [N][K] bf16; K % 32 == 0, N % 4 == 0) on the same
 // LDS-DMA pipeline with split-K; part: op_gemm_nt_glds_part_floats(M, N, K) floats (may be 0)
 size_t op_gemm_nt_glds_part_floats(int M, int N, int K);

@@ -268,16 +268,18 @@ __device__ __forceinline__ int g_swz8(int row) { return (0x76761010 >> (((row >>
 __device__ const float g_zero32[16] = {0.f};
 }  // namespace
 
-constexpr int GS_M = 256, GS_N = 128;
-constexpr int GS_AU = GS_M * 8, GS_BU = 3 * GS_N * 4, GS_STU = GS_AU + GS_BU;  // 16-byte units per stage
+constexpr int GS_M = 256, GS_AU = GS_M * 8;  // A: 16-byte units per stage
 
-template <int CIN, bool OUT_NCHW>
+// BN = 128 or 64 output channels per tile; EPI = CONV_EPI_FWD or (NHWC) CONV_EPI_DSILU: out = acc * SiLU'(pre)
+template <int CIN, bool OUT_NCHW, int BN, int EPI>
 __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, int iw, int cout,
                                                           const float* __restrict__ in, const u16* __restrict__ wr,
                                                           const float* __restrict__ bias, float* __restrict__ out,
                                                           float* __restrict__ pre) {
   constexpr int K = CIN * 16, NCH = K / 32;
-  static_assert(CIN % 32 == 0 && NCH >= 2, "conv_glds_s3 tile");
+  constexpr int GS_N = BN, GS_STU = GS_AU + 3 * BN * 4, FN = BN / 16;  // 16-byte units per stage
+  static_assert(CIN % 32 == 0 && NCH >= 2 && (BN == 128 || BN == 64) && (EPI == CONV_EPI_FWD || !OUT_NCHW),
+                "conv_glds_s3 tile");
   __shared__ __attribute__((aligned(16))) u32x4 sm[2 * GS_STU];
   const int oh = ih / 2, ow = iw / 2, hw = oh * ow;
   const long long M = (long long)n_frames * hw;
@@ -301,7 +303,7 @@ __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, i
   // inside an MFMA phase measured slower (conv3 631 -> 746 us), all of it by X
   // in its read phase about the same (631 / 591 us against 628 / 587 us,
   // profiles/r06z5_ab_conv_glds_dma.txt).
-  constexpr int NA = 8, NB = 2;  // DMA instructions per wave: A rows / 8 (X), B rows / 16 per plane (Y)
+  constexpr int NA = 8, NB = BN / 64;  // DMA instructions per wave: A rows / 8 (X), B rows / 16 per plane (Y)
   const bool X = wave < 4;
   const int dw = wave & 3;
   // A DMA: lane l of instruction i -> row dw * 8 NA + 8 i + l / 8, LDS unit l % 8 = source unit ^ swizzle
@@ -361,12 +363,12 @@ __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, i
   const int wm0 = wave * 32;
   const int fa0 = (2 * q) ^ g_swz8(r), fa1 = (2 * q + 1) ^ g_swz8(r);  // A rows are 16-aligned
   const int fu = q ^ g_swz(r);
-  f32x4 acc[2][8];
+  f32x4 acc[2][FN];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  u32x4 a[3][2], b[3][8];
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  u32x4 a[3][2], b[3][FN];
   auto fetch = [&](int c) __attribute__((always_inline)) {
     const u32x4* st = sm + (c & 1) * GS_STU;
 #pragma unroll
@@ -385,12 +387,12 @@ __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, i
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) b[pl][j] = st[GS_AU + (pl * GS_N + 16 * j + r) * 4 + fu];
+      for (int j = 0; j < FN; ++j) b[pl][j] = st[GS_AU + (pl * GS_N + 16 * j + r) * 4 + fu];
   };
   // k_conv_split3's order per accumulator: smallest terms first
   auto multiply = [&]() __attribute__((always_inline)) {
 #define DR_GS3(PA, PB)                                                                                   \
-  _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int j = 0; j < 8; ++j) acc[i][j] = \
+  _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
       OUT_NCHW ? g_mfma(a[PA][i], b[PB][j], acc[i][j]) : g_mfma(b[PB][j], a[PA][i], acc[i][j]);
     DR_GS3(2, 0)
     DR_GS3(1, 1)
@@ -426,11 +428,12 @@ __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, i
   }
   if (X) __builtin_amdgcn_s_barrier();
 
-  // k_conv_split3's CONV_EPI_FWD epilogue: out = SiLU(acc + bias), pre = acc + bias (NHWC) when given
+  // k_conv_split3's epilogues: CONV_EPI_FWD out = SiLU(acc + bias), pre = acc + bias (NHWC) when given;
+  // CONV_EPI_DSILU out = acc * SiLU'(pre)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < FN; ++j) {
       if (OUT_NCHW) {
         const long long m = m0 + wm0 + 16 * i + 4 * q;
         const int co = n0 + 16 * j + r;
@@ -448,6 +451,14 @@ __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, i
         const long long m = m0 + wm0 + 16 * i + r;
         const int co = n0 + 16 * j + 4 * q;
         if (m >= M) continue;
+        if constexpr (EPI == CONV_EPI_DSILU) {
+          const f32x4 pv = *reinterpret_cast<const f32x4*>(pre + m * cout + co);
+          f32x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * dr_dsilu_fast(pv[e]);
+          *reinterpret_cast<f32x4*>(out + m * cout + co) = v;
+          continue;
+        }
         const f32x4 bv = *reinterpret_cast<const f32x4*>(bias + co);
         f32x4 v;
 #pragma unroll
@@ -461,40 +472,53 @@ __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, i
 }
 
 bool op_conv_glds_s3_supported(int n, int cin, int ih, int iw, int cout) {
-  return op_conv_glds_bf16_supported(n, cin, ih, iw, cout);
+  return (cin == 32 || cin == 64 || cin == 128 || cin == 256) && cout % 64 == 0 && ih % 2 == 0 && iw % 2 == 0 &&
+         ((ih / 2) * (iw / 2)) % 4 == 0 && (long long)n * ih * iw * cin < (1LL << 31) - (1LL << 20);
 }
 
-template <int C, bool NCHW>
+template <int C, bool NCHW, int BN, int EPI>
 static int launch_glds_s3(int n, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
                           float* out, float* pre, hipStream_t s) {
   const long long M = (long long)n * (ih / 2) * (iw / 2);
-  const long long tiles = ((M + GS_M - 1) / GS_M) * (cout / GS_N);
+  const long long tiles = ((M + GS_M - 1) / GS_M) * (cout / BN);
   if (tiles >= (1LL << 30)) {
     dr_set_error("conv_glds_s3: too many tiles");
     return DR_E_INVALID;
   }
-  hipLaunchKernelGGL((k_conv_glds_s3<C, NCHW>), dim3((unsigned)dr_xcd_grid((int)tiles)), dim3(512), 0, s, n, ih, iw,
+  hipLaunchKernelGGL((k_conv_glds_s3<C, NCHW, BN, EPI>), dim3((unsigned)dr_xcd_grid((int)tiles)), dim3(512), 0, s, n, ih, iw,
                      cout, in, (const u16*)wr, bias, out, pre);
   return dr_check_launch("conv_glds_s3");
 }
 
 // f32 NHWC in, f32 NHWC / NCHW out (+ optional NHWC pre-activation), weights as
-// op_conv_repack_split3 planes; DR_E_INVALID (nothing launched) for other shapes
+// op_conv_repack_split3 planes; epi CONV_EPI_FWD (bias given) or, NHWC out only,
+// CONV_EPI_DSILU (pre given, no bias); 128-channel tiles where cout allows, else
+// 64; DR_E_INVALID (nothing launched) for other shapes
 int op_conv_glds_s3(int n, int cin, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
-                    float* out, int out_nchw, float* pre, hipStream_t s) {
-  if (!op_conv_glds_s3_supported(n, cin, ih, iw, cout) ||
+                    float* out, int out_nchw, float* pre, int epi, hipStream_t s) {
+  const bool dsilu = epi == CONV_EPI_DSILU;
+  if (!op_conv_glds_s3_supported(n, cin, ih, iw, cout) || (epi != CONV_EPI_FWD && !dsilu) ||
+      (dsilu && (out_nchw || !pre)) || (!dsilu && !bias) ||
       (((uintptr_t)in | (uintptr_t)wr | (uintptr_t)out | (uintptr_t)bias | (uintptr_t)pre) & 15)) {
-    dr_set_error("conv_glds_s3: unsupported shape (cin=%d ih=%d iw=%d cout=%d)", cin, ih, iw, cout);
+    dr_set_error("conv_glds_s3: unsupported problem (cin=%d ih=%d iw=%d cout=%d epi=%d)", cin, ih, iw, cout, epi);
     return DR_E_INVALID;
   }
-#define DR_GL(C)                                                                                  \
-  if (cin == C)                                                                                   \
-    return out_nchw ? launch_glds_s3<C, true>(n, ih, iw, cout, in, wr, bias, out, pre, s)         \
-                    : launch_glds_s3<C, false>(n, ih, iw, cout, in, wr, bias, out, pre, s);
-  DR_GL(32)
-  DR_GL(64)
-  DR_GL(128)
-  DR_GL(256)
+#define DR_GL(C, BN)                                                                                             \
+  if (cin == C)                                                                                                  \
+    return dsilu ? launch_glds_s3<C, false, BN, CONV_EPI_DSILU>(n, ih, iw, cout, in, wr, bias, out, pre, s)      \
+                 : out_nchw ? launch_glds_s3<C, true, BN, CONV_EPI_FWD>(n, ih, iw, cout, in, wr, bias, out, pre, s) \
+                            : launch_glds_s3<C, false, BN, CONV_EPI_FWD>(n, ih, iw, cout, in, wr, bias, out, pre, s);
+  if (cout % 128 == 0) {
+    DR_GL(32, 128)
+    DR_GL(64, 128)
+    DR_GL(128, 128)
+    DR_GL(256, 128)
+  } else {
+    DR_GL(32, 64)
+    DR_GL(64, 64)
+    DR_GL(128, 64)
+    DR_GL(256, 64)
+  }
 #undef DR_GL
   return DR_E_INVALID;
 }

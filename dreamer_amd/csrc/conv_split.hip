@@ -798,9 +798,10 @@ int op_conv_split3_ex(int n, int cin, int ih, int iw, int cout, const float* in,
     dr_set_error("conv_split3: the SiLU-backward epilogue needs NHWC output and a pre-activation tensor");
     return DR_E_INVALID;
   }
-  if (terms == 3 && epi == CONV_EPI_FWD && op_conv_glds_s3_supported(n, cin, ih, iw, cout) &&
+  // six products: the LDS-DMA ping-pong kernel (conv_glds.hip) where it applies
+  if (terms == 3 && (epi == CONV_EPI_FWD ? bias != nullptr : pre != nullptr) && op_conv_glds_s3_supported(n, cin, ih, iw, cout) &&
       !(((uintptr_t)in | (uintptr_t)wr | (uintptr_t)out | (uintptr_t)bias | (uintptr_t)pre) & 15))
-    return op_conv_glds_s3(n, cin, ih, iw, cout, in, wr, bias, out, out_nchw, pre, s);
+    return op_conv_glds_s3(n, cin, ih, iw, cout, in, wr, bias, out, out_nchw, pre, epi, s);
   // measured at 8192 frames (tools/conv_ab.py): 256 x 64 tiles
   // for 64 output channels (980 us; 128 x 64 at two workgroups per CU: 1004),
   // 256 x 128 for 128 / 256 channels (709 / 658 us; 128 x 128: ~1.1 ms): the

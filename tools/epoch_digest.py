@@ -2,7 +2,9 @@
 setup, fixed seeds): sha256 of the actor / critic parameters and the last
 losses.  Two library variants whose kernels should be bitwise the same
 (DREAMER_LIB_VARIANT) must print the same digest.
-python tools/epoch_digest.py [B] [fp32|bf16] [epochs]   (GPU box)"""
+python tools/epoch_digest.py [B] [fp32|bf16] [epochs] [wm]   (GPU box)
+With `wm`: the same for WorldModel.training_step (bench.py's ring feed, fixed
+window starts): sha256 of the world-model parameters and the last loss."""
 import hashlib
 import os
 import sys
@@ -22,6 +24,16 @@ def main():
     torch.cuda.set_device(dev)
     np.random.seed(1000)
     _, d = bench.make_dreamer(bench.CAR_RACER, dev, B, 64, 15, 64, 1, 1, 0, None, prec)
+    if len(sys.argv) > 4 and sys.argv[4] == "wm":
+        wm = d.world_model
+        for _ in range(n):
+            wm.train_step_ring(d.buffer, d.buffer.sample_start_indices(B))
+        torch.cuda.synchronize()
+        h = hashlib.sha256()
+        for p in wm.parameters():
+            h.update(p.detach().float().cpu().numpy().tobytes())
+        print(f"wm digest {prec} B={B} steps={n}: {h.hexdigest()[:16]} loss {float(wm.last_losses[0]):.9g}", flush=True)
+        return
     for _ in range(n):
         la, lc = d.train_Agent()
     torch.cuda.synchronize()
