@@ -268,17 +268,19 @@ __device__ __forceinline__ int g_swz8(int row) { return (0x76761010 >> (((row >>
 __device__ const float g_zero32[16] = {0.f};
 }  // namespace
 
-constexpr int GS_M = 256, GS_AU = GS_M * 8;  // A: 16-byte units per stage
 
-// BN = 128 or 64 output channels per tile; EPI = CONV_EPI_FWD or (NHWC) CONV_EPI_DSILU: out = acc * SiLU'(pre)
-template <int CIN, bool OUT_NCHW, int BN, int EPI>
+// BN = 128 or 64 output channels per tile, RW = 32 or 64 pixel rows per wave (8 RW per tile); EPI =
+// CONV_EPI_FWD or (NHWC) CONV_EPI_DSILU: out = acc * SiLU'(pre)
+template <int CIN, bool OUT_NCHW, int BN, int EPI, int RW = 32>
 __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, int iw, int cout,
                                                           const float* __restrict__ in, const u16* __restrict__ wr,
                                                           const float* __restrict__ bias, float* __restrict__ out,
                                                           float* __restrict__ pre) {
   constexpr int K = CIN * 16, NCH = K / 32;
-  constexpr int GS_N = BN, GS_STU = GS_AU + 3 * BN * 4, FN = BN / 16;  // 16-byte units per stage
-  static_assert(CIN % 32 == 0 && NCH >= 2 && (BN == 128 || BN == 64) && (EPI == CONV_EPI_FWD || !OUT_NCHW),
+  constexpr int GS_M = 8 * RW, GS_N = BN, GS_AU = GS_M * 8, GS_STU = GS_AU + 3 * BN * 4;  // 16-byte units per stage
+  constexpr int FM = RW / 16, FN = BN / 16;
+  static_assert(CIN % 32 == 0 && NCH >= 2 && (BN == 128 || BN == 64) && (RW == 32 || RW == 64) &&
+                    (EPI == CONV_EPI_FWD || !OUT_NCHW),
                 "conv_glds_s3 tile");
   __shared__ __attribute__((aligned(16))) u32x4 sm[2 * GS_STU];
   const int oh = ih / 2, ow = iw / 2, hw = oh * ow;
@@ -303,7 +305,7 @@ __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, i
   // inside an MFMA phase measured slower (conv3 631 -> 746 us), all of it by X
   // in its read phase about the same (631 / 591 us against 628 / 587 us,
   // profiles/r06z5_ab_conv_glds_dma.txt).
-  constexpr int NA = 8, NB = BN / 64;  // DMA instructions per wave: A rows / 8 (X), B rows / 16 per plane (Y)
+  constexpr int NA = RW / 4, NB = BN / 64;  // DMA instructions per wave: A rows / 8 (X), B rows / 16 per plane (Y)
   const bool X = wave < 4;
   const int dw = wave & 3;
   // A DMA: lane l of instruction i -> row dw * 8 NA + 8 i + l / 8, LDS unit l % 8 = source unit ^ swizzle
@@ -360,19 +362,19 @@ __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, i
       }
   };
 
-  const int wm0 = wave * 32;
+  const int wm0 = wave * RW;
   const int fa0 = (2 * q) ^ g_swz8(r), fa1 = (2 * q + 1) ^ g_swz8(r);  // A rows are 16-aligned
   const int fu = q ^ g_swz(r);
-  f32x4 acc[2][FN];
+  f32x4 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  u32x4 a[3][2], b[3][FN];
+  u32x4 a[3][FM], b[3][FN];
   auto fetch = [&](int c) __attribute__((always_inline)) {
     const u32x4* st = sm + (c & 1) * GS_STU;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < FM; ++i) {
       const f32x4 v0 = __builtin_bit_cast(f32x4, st[(wm0 + 16 * i + r) * 8 + fa0]);
       const f32x4 v1 = __builtin_bit_cast(f32x4, st[(wm0 + 16 * i + r) * 8 + fa1]);
       unsigned h[4], m[4], l[4];
@@ -392,7 +394,7 @@ __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, i
   // k_conv_split3's order per accumulator: smallest terms first
   auto multiply = [&]() __attribute__((always_inline)) {
 #define DR_GS3(PA, PB)                                                                                   \
-  _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
+  _Pragma("unroll") for (int i = 0; i < FM; ++i) _Pragma("unroll") for (int j = 0; j < FN; ++j) acc[i][j] = \
       OUT_NCHW ? g_mfma(a[PA][i], b[PB][j], acc[i][j]) : g_mfma(b[PB][j], a[PA][i], acc[i][j]);
     DR_GS3(2, 0)
     DR_GS3(1, 1)
@@ -431,7 +433,7 @@ __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, i
   // k_conv_split3's epilogues: CONV_EPI_FWD out = SiLU(acc + bias), pre = acc + bias (NHWC) when given;
   // CONV_EPI_DSILU out = acc * SiLU'(pre)
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       if (OUT_NCHW) {
@@ -479,13 +481,16 @@ bool op_conv_glds_s3_supported(int n, int cin, int ih, int iw, int cout) {
 template <int C, bool NCHW, int BN, int EPI>
 static int launch_glds_s3(int n, int ih, int iw, int cout, const float* in, const void* wr, const float* bias,
                           float* out, float* pre, hipStream_t s) {
+  // 64-channel tiles take 64 pixel rows per wave (512-row tiles): 96 MFMAs per
+  // phase as on the 128-channel tiles
+  constexpr int RW = BN == 64 ? 64 : 32;
   const long long M = (long long)n * (ih / 2) * (iw / 2);
-  const long long tiles = ((M + GS_M - 1) / GS_M) * (cout / BN);
+  const long long tiles = ((M + 8 * RW - 1) / (8 * RW)) * (cout / BN);
   if (tiles >= (1LL << 30)) {
     dr_set_error("conv_glds_s3: too many tiles");
     return DR_E_INVALID;
   }
-  hipLaunchKernelGGL((k_conv_glds_s3<C, NCHW, BN, EPI>), dim3((unsigned)dr_xcd_grid((int)tiles)), dim3(512), 0, s, n, ih, iw,
+  hipLaunchKernelGGL((k_conv_glds_s3<C, NCHW, BN, EPI, RW>), dim3((unsigned)dr_xcd_grid((int)tiles)), dim3(512), 0, s, n, ih, iw,
                      cout, in, (const u16*)wr, bias, out, pre);
   return dr_check_launch("conv_glds_s3");
 }
