@@ -176,6 +176,9 @@ bool op_convT_split3_supported(int n, int cin, int h, int w, int cout, int terms
 // the all-parity-class form op_convT_split3 takes for 64 -> 32 channels (8 x 16 anchor tiles)
 bool op_convT_cls_supported(int n, int cin, int h, int w, int cout);
 int op_convT_split3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s, int terms = 3);
+// the six-product form on the LDS-DMA ping-pong kernel (conv_glds.hip), taken by op_convT_split3 where it applies
+bool op_convT_glds_s3_supported(const ConvTArgs& a, int epi);
+int op_convT_glds_s3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s);
 
 // Weight gradient of a k4 s2 p1 (transposed) convolution:
 //   dW[a][b][ky][kx] (+)= scale * sum_{f,y,x} lo[f][y][x][a] * hi[f][2y-1+ky][2x-1+kx][b]

@@ -271,26 +271,46 @@ __device__ const float g_zero32[16] = {0.f};
 
 // BN = 128 or 64 output channels per tile, RW = 32 or 64 pixel rows per wave (8 RW per tile); EPI =
 // CONV_EPI_FWD or (NHWC) CONV_EPI_DSILU: out = acc * SiLU'(pre)
-template <int CIN, bool OUT_NCHW, int BN, int EPI, int RW = 32>
-__global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, int iw, int cout,
-                                                          const float* __restrict__ in, const u16* __restrict__ wr,
-                                                          const float* __restrict__ bias, float* __restrict__ out,
-                                                          float* __restrict__ pre) {
-  constexpr int K = CIN * 16, NCH = K / 32;
+// TR: the upsampling k4 s2 p1 form of conv_split.hip's k_convT_split3 (per output
+// parity class a dense K = 4 taps x CIN over input-resolution pixels; weights
+// [class][K/32][3][cout][32]; its CT_EPI_BIAS / CT_EPI_DSILU epilogues), with the
+// same tile, chunk and product order: bitwise that kernel's sums.
+struct GS3Args {
+  int n, ih, iw, cout, silu_out;  // TR: ih, iw = the input resolution
+  const float* in;
+  const u16* wr;
+  const float* bias;
+  float* out;
+  float* out2;  // TR, CT_EPI_BIAS: optional SiLU(acc + bias)
+  float* pre;
+};
+
+template <int CIN, bool OUT_NCHW, int BN, int EPI, int RW = 32, bool TR = false>
+__global__ __launch_bounds__(512, 2) void k_conv_glds_s3(GS3Args g) {
+  const int ih = g.ih, iw = g.iw, cout = g.cout;
+  const float* __restrict__ in = g.in;
+  const float* __restrict__ bias = g.bias;
+  float* __restrict__ out = g.out;
+  float* __restrict__ pre = g.pre;
+  constexpr int K = TR ? CIN * 4 : CIN * 16, NCH = K / 32;
   constexpr int GS_M = 8 * RW, GS_N = BN, GS_AU = GS_M * 8, GS_STU = GS_AU + 3 * BN * 4;  // 16-byte units per stage
   constexpr int FM = RW / 16, FN = BN / 16;
   static_assert(CIN % 32 == 0 && NCH >= 2 && (BN == 128 || BN == 64) && (RW == 32 || RW == 64) &&
-                    (EPI == CONV_EPI_FWD || !OUT_NCHW),
+                    (EPI == CONV_EPI_FWD || !OUT_NCHW) && (!TR || !OUT_NCHW),
                 "conv_glds_s3 tile");
   __shared__ __attribute__((aligned(16))) u32x4 sm[2 * GS_STU];
-  const int oh = ih / 2, ow = iw / 2, hw = oh * ow;
-  const long long M = (long long)n_frames * hw;
+  const int oh = TR ? ih : ih / 2, ow = TR ? iw : iw / 2, hw = oh * ow;  // pixels of the GEMM rows
+  const long long M = (long long)g.n * hw;
   const int tiles_n = cout / GS_N;
-  const long long tiles = ((M + GS_M - 1) / GS_M) * tiles_n;
+  const long long tiles = ((M + GS_M - 1) / GS_M) * tiles_n * (TR ? 4 : 1);
   const int lt = dr_xcd_tile(blockIdx.x, (int)tiles);
   if (lt < 0) return;
-  const long long m0 = (long long)(lt / tiles_n) * GS_M;
-  const int n0 = (lt % tiles_n) * GS_N;
+  // TR: parity class fastest (the four classes of one pixel tile read the same input, k_convT_split3)
+  const int cls = TR ? (lt & 3) : 0, py = cls >> 1, px = cls & 1;
+  const int lr = TR ? (lt >> 2) : lt;
+  const long long m0 = (long long)(lr / tiles_n) * GS_M;
+  const int n0 = (lr % tiles_n) * GS_N;
+  const u16* __restrict__ wr = g.wr + (TR ? (long long)cls * NCH * 3 * cout * 32 : 0);
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int r = lane & 15, q = lane >> 4;
 
@@ -318,13 +338,23 @@ __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, i
     const long long m = m0 + row;
     const int mm = (int)(m < M ? m : 0);
     const int f = mm / hw, p = mm - f * hw, oy = p / ow, ox = p - oy * ow;
-    const int y0 = 2 * oy - 1, x0 = 2 * ox - 1;
-    pb[i] = ((f * ih + y0) * iw + x0) * CIN;
     unsigned v = 0u;
+    if constexpr (TR) {
+      // input pixel (oy, ox) of the class grid; tap t reads (oy + py - t / 2, ox + px - t % 2)
+      pb[i] = ((f * ih + oy) * iw + ox) * CIN;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      v |= (y0 + t >= 0 && y0 + t < ih) ? (1u << t) : 0u;
-      v |= (x0 + t >= 0 && x0 + t < iw) ? (16u << t) : 0u;
+      for (int t = 0; t < 4; ++t) {
+        const int yy = oy + py - (t >> 1), xx = ox + px - (t & 1);
+        v |= (yy >= 0 && yy < ih && xx >= 0 && xx < iw) ? (1u << t) : 0u;
+      }
+    } else {
+      const int y0 = 2 * oy - 1, x0 = 2 * ox - 1;
+      pb[i] = ((f * ih + y0) * iw + x0) * CIN;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        v |= (y0 + t >= 0 && y0 + t < ih) ? (1u << t) : 0u;
+        v |= (x0 + t >= 0 && x0 + t < iw) ? (16u << t) : 0u;
+      }
     }
     vm[i] = m < M ? v : 0u;
     au[i] = 4 * ((lane & 7) ^ g_swz8(row));
@@ -339,15 +369,21 @@ __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, i
 
   // parts: bit 0 = the A rows, bit 1 = the B planes
   auto issue = [&](int c, int parts) __attribute__((always_inline)) {
-    int tap, ci0, kc;
-    g_chunk<CIN>(c, tap, ci0, kc);
-    const int ky = tap >> 2, kx = tap & 3;
-    const int toff = (ky * iw + kx) * CIN + ci0;
+    int tap, ci0, kc, toff;
+    if constexpr (TR) {  // k_convT_split3's chunk order: tap-major, 32 channels per chunk
+      tap = (32 * c) / CIN;
+      ci0 = 32 * c - tap * CIN;
+      kc = c;
+      toff = ((py - (tap >> 1)) * iw + (px - (tap & 1))) * CIN + ci0;
+    } else {
+      g_chunk<CIN>(c, tap, ci0, kc);
+      toff = ((tap >> 2) * iw + (tap & 3)) * CIN + ci0;
+    }
     u32x4* st = sm + (c & 1) * GS_STU;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       if (!(parts & 1)) break;
-      const bool ok = (vm[i] >> ky) & (vm[i] >> (4 + kx)) & 1u;
+      const bool ok = TR ? ((vm[i] >> tap) & 1u) : ((vm[i] >> (tap >> 2)) & (vm[i] >> (4 + (tap & 3))) & 1u);
       const float* src = ok ? in + (pb[i] + toff + au[i]) : g_zero32;
       __builtin_amdgcn_global_load_lds(src, st + (dw * NA + i) * 64, 16, 0, 0);
     }
@@ -430,6 +466,39 @@ __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(int n_frames, int ih, i
   }
   if (X) __builtin_amdgcn_s_barrier();
 
+  if constexpr (TR) {
+    // k_convT_split3's epilogues at output pixel (2 y + py, 2 x + px): CT_EPI_BIAS out = acc + bias (or its
+    // SiLU, silu_out), out2 = SiLU(acc + bias); CT_EPI_DSILU out = acc * SiLU'(pre)
+    const int OW = 2 * iw, OH = 2 * ih;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const long long m = m0 + wm0 + 16 * i + r;
+      if (m >= M) continue;
+      const int f = (int)(m / hw), p = (int)(m - (long long)f * hw), y = p / iw, x = p - y * iw;
+      const long long opix = ((long long)f * OH + 2 * y + py) * OW + 2 * x + px;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int co = n0 + 16 * j + 4 * q;
+        f32x4 v = acc[i][j];
+        if constexpr (EPI == CT_EPI_BIAS) {
+          v += *reinterpret_cast<const f32x4*>(bias + co);
+          f32x4 sv = v;
+          if (g.out2 || g.silu_out) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sv[e] = dr_silu_fast(v[e]);
+          }
+          *reinterpret_cast<f32x4*>(out + opix * cout + co) = g.silu_out ? sv : v;
+          if (g.out2) *reinterpret_cast<f32x4*>(g.out2 + opix * cout + co) = sv;
+        } else {
+          const f32x4 pv = *reinterpret_cast<const f32x4*>(pre + opix * cout + co);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] * dr_dsilu_fast(pv[e]);
+          *reinterpret_cast<f32x4*>(out + opix * cout + co) = v;
+        }
+      }
+    }
+    return;
+  }
   // k_conv_split3's epilogues: CONV_EPI_FWD out = SiLU(acc + bias), pre = acc + bias (NHWC) when given;
   // CONV_EPI_DSILU out = acc * SiLU'(pre)
 #pragma unroll
@@ -490,8 +559,8 @@ static int launch_glds_s3(int n, int ih, int iw, int cout, const float* in, cons
     dr_set_error("conv_glds_s3: too many tiles");
     return DR_E_INVALID;
   }
-  hipLaunchKernelGGL((k_conv_glds_s3<C, NCHW, BN, EPI, RW>), dim3((unsigned)dr_xcd_grid((int)tiles)), dim3(512), 0, s, n, ih, iw,
-                     cout, in, (const u16*)wr, bias, out, pre);
+  GS3Args g = {n, ih, iw, cout, 0, in, (const u16*)wr, bias, out, nullptr, pre};
+  hipLaunchKernelGGL((k_conv_glds_s3<C, NCHW, BN, EPI, RW>), dim3((unsigned)dr_xcd_grid((int)tiles)), dim3(512), 0, s, g);
   return dr_check_launch("conv_glds_s3");
 }
 
@@ -525,6 +594,54 @@ int op_conv_glds_s3(int n, int cin, int ih, int iw, int cout, const float* in, c
     DR_GL(256, 64)
   }
 #undef DR_GL
+  return DR_E_INVALID;
+}
+
+template <int C, int BN, int EPI>
+static int launch_glds_t3(const ConvTArgs& a, const void* wr, hipStream_t s) {
+  constexpr int RW = BN == 64 ? 64 : 32;
+  const long long M = (long long)a.n * a.h * a.w;
+  const long long tiles = 4 * ((M + 8 * RW - 1) / (8 * RW)) * (a.cout / BN);
+  if (tiles >= (1LL << 30)) {
+    dr_set_error("convT_glds_s3: too many tiles");
+    return DR_E_INVALID;
+  }
+  GS3Args g = {a.n, a.h, a.w, a.cout, a.silu_out, a.in, (const u16*)wr, a.bias, a.out, a.out2, const_cast<float*>(a.pre)};
+  hipLaunchKernelGGL((k_conv_glds_s3<C, false, BN, EPI, RW, true>), dim3((unsigned)dr_xcd_grid((int)tiles)), dim3(512),
+                     0, s, g);
+  return dr_check_launch("convT_glds_s3");
+}
+
+bool op_convT_glds_s3_supported(const ConvTArgs& a, int epi) {
+  const bool cin_ok = a.cin == 32 || a.cin == 64 || a.cin == 128 || a.cin == 256;
+  const bool al = !(((uintptr_t)a.in | (uintptr_t)a.out | (uintptr_t)a.out2 | (uintptr_t)a.bias | (uintptr_t)a.pre) & 15);
+  return cin_ok && a.cout % 64 == 0 && a.cout > 0 && a.ldc == a.cout && !a.silu_in && al &&
+         (epi == CT_EPI_BIAS ? a.bias != nullptr : epi == CT_EPI_DSILU && a.pre != nullptr) &&
+         (long long)a.n * a.h * a.w * a.cin < (1LL << 31) - (1LL << 20);
+}
+
+// the six-product upsampling conv (k_convT_split3's problems, terms = 3) on the
+// LDS-DMA ping-pong kernel; DR_E_INVALID (nothing launched) where unsupported
+int op_convT_glds_s3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s) {
+  if (!op_convT_glds_s3_supported(a, epi) || ((uintptr_t)wr & 15)) {
+    dr_set_error("convT_glds_s3: unsupported problem (cin=%d cout=%d h=%d w=%d epi=%d)", a.cin, a.cout, a.h, a.w, epi);
+    return DR_E_INVALID;
+  }
+#define DR_GT(C, BN)                                                                                  \
+  if (a.cin == C)                                                                                     \
+    return epi == CT_EPI_DSILU ? launch_glds_t3<C, BN, CT_EPI_DSILU>(a, wr, s) : launch_glds_t3<C, BN, CT_EPI_BIAS>(a, wr, s);
+  if (a.cout % 128 == 0) {
+    DR_GT(32, 128)
+    DR_GT(64, 128)
+    DR_GT(128, 128)
+    DR_GT(256, 128)
+  } else {
+    DR_GT(32, 64)
+    DR_GT(64, 64)
+    DR_GT(128, 64)
+    DR_GT(256, 64)
+  }
+#undef DR_GT
   return DR_E_INVALID;
 }
 

@@ -1303,6 +1303,7 @@ int op_convT_split3(int epi, const ConvTArgs& a, const void* wr, hipStream_t s, 
       ((uintptr_t)a.out & 15) == 0 && (!a.out2 || ((uintptr_t)a.out2 & 15) == 0) &&
       (epi != CT_EPI_DSILU || ((uintptr_t)a.pre & 15) == 0) && (epi != CT_EPI_BIAS || ((uintptr_t)a.bias & 15) == 0))
     return launch_convT_cls(epi, a, wr, s, terms);
+  if (terms == 3 && op_convT_glds_s3_supported(a, epi) && !((uintptr_t)wr & 15)) return op_convT_glds_s3(epi, a, wr, s);
 #define DR_T3E(BN, C, T) \
   (epi == CT_EPI_DSILU ? launch_t3<BN, C, CT_EPI_DSILU, T>(a, wr, s) : launch_t3<BN, C, CT_EPI_BIAS, T>(a, wr, s))
 #define DR_T3L(C)                                                                          \
