@@ -12,7 +12,7 @@ import glob
 import json
 import sys
 
-ENCODER = ("k_enc12_split3", "k_conv_split3", "k_conv_nhwc", "k_frames_nhwc4", "k_conv1_direct", "k_conv1_frames", "k_enc12_bf16", "k_conv_bf16", "k_conv1_bf16")
+ENCODER = ("k_enc12_split3", "k_conv_split3", "k_conv_glds_s3", "k_conv_glds_bf16", "k_conv_nhwc", "k_frames_nhwc4", "k_conv1_direct", "k_conv1_frames", "k_enc12_bf16", "k_conv_bf16", "k_conv1_bf16")
 
 
 def load(d, counter):
