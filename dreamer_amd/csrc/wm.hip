@@ -781,6 +781,9 @@ static int wm_run(int phases, const dr_dims* d, const dr_world_model* wm, const 
   // B >= 128: the grouped per-step products on the split3 wave-K kernel from
   // weight planes split once per step (f32-accurate): 12.8 us per launch against
   // the f32 k_gemm_wk's 23.5 (WM step bf16 9.22 -> 9.17 ms, fp32 unchanged, r06m)
+  // (bf16 mode keeps the six products here: one-term scan products measured
+  // 8.46 -> 8.36 ms per bf16 WM step but took the posterior flip fraction against
+  // the fp32 oracle from ~2e-4 to 1.8e-3 of its 2e-3 bound, profiles/r06z9_ab_wm_scan_one_term.txt)
   const bool planes = B >= 128 && T > 1 && Hd % 8 == 0;
   if (planes) {
     DR_TRY(split_planes(eh, Hd, wm->map0.w + F, F + Hd, w.s3m0, s));
