@@ -324,7 +324,8 @@ __global__ __launch_bounds__(512, 2) void k_conv_glds_s3(GS3Args g) {
   // own before the barrier that precedes X's read of chunk c + 1.  DMA issued
   // inside an MFMA phase measured slower (conv3 631 -> 746 us), all of it by X
   // in its read phase about the same (631 / 591 us against 628 / 587 us,
-  // profiles/r06z5_ab_conv_glds_dma.txt).
+  // profiles/r06z5_ab_conv_glds_dma.txt).  s_setprio 1 around the MFMA phase:
+  // neutral (630 / 588 against 630 / 593 us, profiles/r06za_ab_glds_setprio.txt).
   constexpr int NA = RW / 4, NB = BN / 64;  // DMA instructions per wave: A rows / 8 (X), B rows / 16 per plane (Y)
   const bool X = wave < 4;
   const int dw = wave & 3;
