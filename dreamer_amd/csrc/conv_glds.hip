@@ -208,6 +208,10 @@ static int launch_glds(int n, int ih, int iw, int cout, const void* in, const vo
     dr_set_error("conv_glds_bf16: too many tiles");
     return DR_E_INVALID;
   }
+  // (the ping-pong form of k_conv_glds_s3 in one term -- 512 x 128 tiles, 32
+  // MFMAs per phase, one workgroup per CU -- measured slower: 235 / 188 us
+  // against 182 / 137, bf16 headline 921 -> 898 k; with no split there is
+  // little for the read phase to hide, profiles/r06zb_ab_b16_pingpong.txt)
   // three stages, two workgroups per CU (72 KB of LDS, 100 VGPRs): B = 256 bf16
   // encoder conv3 / conv4 181 / 138 us, against 219 / 180 (four stages, one
   // workgroup per CU), 229 / 186 (six) and 288 / 173 on k_conv_split3<.., 1>
